@@ -1,0 +1,541 @@
+/*
+ * eslam_detmath.h -- the deterministic arithmetic contract of the eslam MI355X core.
+ *
+ * Every transcendental, random-number and fixed-point operation that the particle-filter
+ * hot path performs is defined here, once, as a header that compiles both for the host
+ * (gcc / clang, x86-64 SSE2 + FMA3) and for the device (hipcc, gfx950).  Built with
+ * -ffp-contract=off on both sides, every function returns bit-identical results on the
+ * CPU and on the GPU, which is what lets the device path match the CPU oracle bit-for-bit
+ * (resample indices) and to the last ulp (weights).
+ *
+ * The reference delegates these operations to third-party code that is not vendored and
+ * whose version is not pinned: glibc exp/log/sin/cos/pow, boost.math
+ * normal pdf/cdf (src/ContactModel.cpp:104-115), boost.random minstd_rand + uniform_real
+ * (src/ParticleFilter.hpp:87-88,177; src/PoseEstimator.cpp:15-16) and an external odometry
+ * sampler (src/PoseEstimator.cpp:198).  Their results are reproduced here to ~1e-15
+ * relative (transcendentals) or exactly (minstd integers, boost's integral-engine
+ * uniform_real mapping), and tests/test_detmath.py checks them against mpmath / numpy.
+ *
+ * Only IEEE-exact primitives are used underneath: + - * / sqrt fma floor and integer ops.
+ */
+#ifndef ESLAM_DETMATH_H
+#define ESLAM_DETMATH_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define DM_FN __host__ __device__ static inline __attribute__((always_inline))
+#define DM_CONST static constexpr
+#define DM_UNROLL _Pragma("unroll")
+#else
+#define DM_FN static inline
+#define DM_CONST static const
+#define DM_UNROLL
+#endif
+
+/* ------------------------------------------------------------------------------------ */
+/* bit helpers                                                                           */
+/* ------------------------------------------------------------------------------------ */
+DM_FN uint64_t dm_bits(double x) { uint64_t u; __builtin_memcpy(&u, &x, 8); return u; }
+DM_FN double dm_from_bits(uint64_t u) { double x; __builtin_memcpy(&x, &u, 8); return x; }
+DM_FN uint32_t dm_fbits(float x) { uint32_t u; __builtin_memcpy(&u, &x, 4); return u; }
+DM_FN int dm_isnan(double x) { return x != x; }
+DM_FN int dm_isfinite(double x) { return (dm_bits(x) & 0x7ff0000000000000ull) != 0x7ff0000000000000ull; }
+DM_FN double dm_fabs(double x) { return dm_from_bits(dm_bits(x) & 0x7fffffffffffffffull); }
+DM_FN double dm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+DM_FN double dm_sqrt(double x) { return __builtin_sqrt(x); }
+DM_FN double dm_floor(double x) { return __builtin_floor(x); }
+
+/* 2^k for k in [-1022, 1023], exact */
+DM_FN double dm_pow2i(int k) { return dm_from_bits((uint64_t)(k + 1023) << 52); }
+
+/* x * 2^k rounded once (IEEE round-to-nearest), including gradual underflow and overflow. */
+DM_FN double dm_ldexp(double x, int k)
+{
+    if (x == 0.0 || !dm_isfinite(x)) return x;
+    uint64_t b = dm_bits(x);
+    int e = (int)((b >> 52) & 0x7ff);
+    if (e == 0) { x *= 18446744073709551616.0; /* 2^64, exact */ b = dm_bits(x); e = (int)((b >> 52) & 0x7ff); k -= 64; }
+    int t = e - 1023 + k;                                   /* target exponent */
+    double m = dm_from_bits((b & 0x800fffffffffffffull) | 0x3ff0000000000000ull); /* +-[1,2) */
+    if (t > 1023) return (m * dm_pow2i(1023)) * 2.0;        /* -> +-inf */
+    if (t >= -1022) return m * dm_pow2i(t);                 /* exact */
+    if (t < -1086) return m * 0.0;                          /* rounds to (signed) zero */
+    return (m * dm_pow2i(t + 64)) * dm_pow2i(-64);          /* exact, then one rounding */
+}
+
+/* round-to-nearest-even integer value of |x| < 2^51, as a double (magic-number trick) */
+DM_FN double dm_rint_small(double x)
+{
+    const double magic = 6755399441055744.0; /* 0x1.8p52 */
+    double t = x + magic;
+    return t - magic;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* exp                                                                                   */
+/* ------------------------------------------------------------------------------------ */
+#define DM_LN2_HI 6.93147180369123816490e-01  /* 0x3fe62e42fee00000: 32 significant bits */
+#define DM_LN2_LO 1.90821492927058770002e-10  /* ln2 - DM_LN2_HI                        */
+#define DM_INV_LN2 1.44269504088896338700e+00
+
+/* e^r on |r| <= 0.3466: Taylor series to r^13 (truncation < 6e-18 relative), fma Horner */
+DM_FN double dm_exp_kernel(double r)
+{
+    double p = 1.6059043836821613e-10;          /* 1/13! */
+    p = dm_fma(p, r, 2.08767569878681e-09);     /* 1/12! */
+    p = dm_fma(p, r, 2.505210838544172e-08);    /* 1/11! */
+    p = dm_fma(p, r, 2.755731922398589e-07);    /* 1/10! */
+    p = dm_fma(p, r, 2.7557319223985893e-06);   /* 1/9!  */
+    p = dm_fma(p, r, 2.48015873015873e-05);     /* 1/8!  */
+    p = dm_fma(p, r, 0.0001984126984126984);    /* 1/7!  */
+    p = dm_fma(p, r, 0.001388888888888889);     /* 1/6!  */
+    p = dm_fma(p, r, 0.008333333333333333);     /* 1/5!  */
+    p = dm_fma(p, r, 0.041666666666666664);     /* 1/4!  */
+    p = dm_fma(p, r, 0.16666666666666666);      /* 1/3!  */
+    p = dm_fma(p, r, 0.5);
+    p = dm_fma(p, r, 1.0);
+    return dm_fma(p, r, 1.0);
+}
+
+DM_FN double dm_exp(double x)
+{
+    if (x != x) return x;
+    if (x > 709.782712893384) return dm_from_bits(0x7ff0000000000000ull);
+    if (x < -745.1332191019412) return 0.0;
+    double kd = dm_rint_small(x * DM_INV_LN2);
+    double hi = x - kd * DM_LN2_HI;   /* exact: kd has <= 11 bits, LN2_HI 32 bits */
+    double r = hi - kd * DM_LN2_LO;
+    double p = dm_exp_kernel(r);
+    return dm_ldexp(p, (int)kd);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* log                                                                                   */
+/* ------------------------------------------------------------------------------------ */
+DM_FN double dm_log(double x)
+{
+    if (x != x) return x;
+    if (x <= 0.0) return x == 0.0 ? -dm_from_bits(0x7ff0000000000000ull) : dm_from_bits(0x7ff8000000000000ull);
+    if (!dm_isfinite(x)) return x;
+    int k = 0;
+    uint64_t b = dm_bits(x);
+    if ((b >> 52) == 0) { x *= 18014398509481984.0; /* 2^54 */ b = dm_bits(x); k = -54; }
+    k += (int)(b >> 52) - 1023;
+    double m = dm_from_bits((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull); /* [1,2) */
+    if (m > 1.4142135623730951) { m *= 0.5; k += 1; }
+    double f = m - 1.0;                 /* exact (Sterbenz) */
+    double s = f / (2.0 + f);           /* (m-1)/(m+1), |s| <= 0.1716 */
+    double z = s * s;
+    /* R = 2 z/3 + 2 z^2/5 + ... + 2 z^10/21  (atanh series; truncation < 3e-17 relative) */
+    double R = 0.09523809523809523;            /* 2/21 */
+    R = dm_fma(R, z, 0.10526315789473684);     /* 2/19 */
+    R = dm_fma(R, z, 0.11764705882352941);     /* 2/17 */
+    R = dm_fma(R, z, 0.13333333333333333);     /* 2/15 */
+    R = dm_fma(R, z, 0.15384615384615385);     /* 2/13 */
+    R = dm_fma(R, z, 0.18181818181818182);     /* 2/11 */
+    R = dm_fma(R, z, 0.2222222222222222);      /* 2/9  */
+    R = dm_fma(R, z, 0.2857142857142857);      /* 2/7  */
+    R = dm_fma(R, z, 0.4);                     /* 2/5  */
+    R = dm_fma(R, z, 0.6666666666666666);      /* 2/3  */
+    R = R * z;
+    /* log(1+f) = 2 atanh(s) = 2s + s R, and 2s = f - s f  ->  f - s (f - R) */
+    double l = f - s * (f - R);
+    double kd = (double)k;
+    return kd * DM_LN2_HI + (l + kd * DM_LN2_LO);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* sin / cos                                                                             */
+/* ------------------------------------------------------------------------------------ */
+#define DM_PIO2_1 1.57079632673412561417e+00   /* first 33 bits of pi/2 */
+#define DM_PIO2_2 6.07710050630396597660e-11   /* next 33 bits          */
+#define DM_PIO2_3 2.02226624871116645580e-21   /* next 33 bits          */
+#define DM_INV_PIO2 6.36619772367581382433e-01
+
+DM_FN double dm_sin_kernel(double r)   /* |r| <= pi/4, Taylor to r^19 */
+{
+    double z = r * r;
+    double p = 8.22063524662433e-18;            /* 1/19! */
+    p = dm_fma(p, z, -2.8114572543455206e-15);  /* -1/17! */
+    p = dm_fma(p, z, 7.647163731819816e-13);    /* 1/15! */
+    p = dm_fma(p, z, -1.6059043836821613e-10);  /* -1/13! */
+    p = dm_fma(p, z, 2.505210838544172e-08);    /* 1/11! */
+    p = dm_fma(p, z, -2.7557319223985893e-06);  /* -1/9! */
+    p = dm_fma(p, z, 0.0001984126984126984);    /* 1/7!  */
+    p = dm_fma(p, z, -0.008333333333333333);    /* -1/5! */
+    p = dm_fma(p, z, 0.16666666666666666);      /* 1/3! (subtracted below) */
+    return dm_fma(-r * z, p, r) ;
+}
+
+DM_FN double dm_cos_kernel(double r)   /* |r| <= pi/4, Taylor to r^20 */
+{
+    double z = r * r;
+    double p = 4.110317623312165e-19;           /* 1/20! */
+    p = dm_fma(p, z, -1.5619206968586225e-16);  /* -1/18! */
+    p = dm_fma(p, z, 4.779477332387385e-14);    /* 1/16! */
+    p = dm_fma(p, z, -1.1470745597729725e-11);  /* -1/14! */
+    p = dm_fma(p, z, 2.08767569878681e-09);     /* 1/12! */
+    p = dm_fma(p, z, -2.755731922398589e-07);   /* -1/10! */
+    p = dm_fma(p, z, 2.48015873015873e-05);     /* 1/8!  */
+    p = dm_fma(p, z, -0.001388888888888889);    /* -1/6! */
+    p = dm_fma(p, z, 0.041666666666666664);     /* 1/4!  */
+    p = dm_fma(p, z, -0.5);
+    return dm_fma(p, z, 1.0);
+}
+
+DM_FN void dm_sincos(double x, double* s, double* c)
+{
+    if (!dm_isfinite(x)) { *s = x - x; *c = x - x; return; }
+    double n = dm_rint_small(x * DM_INV_PIO2);
+    if (dm_fabs(n) > 1048576.0) n = dm_floor(x * DM_INV_PIO2 + 0.5); /* huge |x|: deterministic, inexact */
+    double r = ((x - n * DM_PIO2_1) - n * DM_PIO2_2) - n * DM_PIO2_3;
+    double sr = dm_sin_kernel(r), cr = dm_cos_kernel(r);
+    int64_t q = (int64_t)(n - 4.0 * dm_floor(n * 0.25));  /* n mod 4 in [0,3] */
+    if (q == 0) { *s = sr; *c = cr; }
+    else if (q == 1) { *s = cr; *c = -sr; }
+    else if (q == 2) { *s = -sr; *c = -cr; }
+    else { *s = -cr; *c = sr; }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* erfc                                                                                  */
+/* ------------------------------------------------------------------------------------ */
+/* Piecewise polynomial fits of erfcx(t) = exp(t^2) erfc(t), t >= 0, generated by
+ * tools/gen_erfcx_coeffs.py (mpmath, 60 digits; fit error < 1e-19 relative).           */
+DM_CONST double dm_erfcx_c0[19] = {9.283752145234023e-18, -1.1792469674650424e-16, 1.4147642917261418e-15, -1.6990873809451645e-14, 1.9815259170250877e-13, -2.237871975539458e-12, 2.443089253356378e-11, -2.5716880604565665e-10, 2.602534528787355e-09, -2.523338988527416e-08, 2.334361521750124e-07, -2.0502402237783523e-06, 1.699015396298168e-05, -0.00013180360649459388, 0.0009473309967177142, -0.006219475256501468, 0.03653406715146833, -0.18580147330750355, 0.7703465477309968};
+DM_CONST double dm_erfcx_c1[21] = {7.586363910623654e-16, -5.70498818820545e-15, 3.804139839023933e-14, -2.7298916881805636e-13, 1.923220700761848e-12, -1.316808218435804e-11, 8.78702258916541e-11, -5.707384863259472e-10, 3.6018496597373607e-09, -2.2042929675824138e-08, 1.3053024836981828e-07, -7.460049373598812e-07, 4.102614842889114e-06, -2.1633318561315704e-05, 0.00010890847460873127, -0.0005206834090754457, 0.002348268513455678, -0.009903371117665843, 0.03859289034297711, -0.13660600739194928, 0.427583576155807};
+DM_CONST double dm_erfcx_c2[21] = {5.057065718502677e-15, -3.068476570068241e-14, 1.5665515071079456e-13, -9.145569832047356e-13, 5.304280116094916e-12, -2.988095123391799e-11, 1.6501687267503609e-10, -8.932988395737626e-10, 4.733487001243104e-09, -2.452313531325191e-08, 1.2405991227876422e-07, -6.119614590410515e-07, 2.938639159152759e-06, -1.3711609161098606e-05, 6.20318170584252e-05, -0.0002714121303982754, 0.001145072748839861, -0.004641494381623146, 0.017995852918522272, -0.06636487710656187, 0.23108725873039188};
+DM_CONST double dm_erfcx_c3[21] = {1.3630546848219266e-15, -7.922495175389322e-15, 3.837381296081427e-14, -2.1703391711090554e-13, 1.228659481248371e-12, -6.783010963567072e-12, 3.694282205184398e-11, -1.9861768949727073e-10, 1.0530843369976437e-09, -5.5033698295504104e-09, 2.8331978822991838e-08, -1.4359644214436117e-07, 7.16045664615945e-07, -3.5103666499135004e-06, 1.6905649257776914e-05, -7.990888030554815e-05, 0.0003703524689955565, -0.001681182076746115, 0.007465433244975571, -0.032383506095021455, 0.13699945762506138};
+DM_CONST double dm_erfcx_tail[15] = {7.839577105055556e-16, -4.33825604370309e-15, 2.2414082272808668e-14, -1.4112442747221709e-13, 9.543596829961645e-13, -6.9177088797188345e-12, 5.462084473729142e-11, -4.76004525046868e-10, 4.6562063848232095e-09, -5.230561185110592e-08, 6.970116167625029e-07, -1.1575329006190274e-05, 0.0002604872169531935, -0.009441218224620304, 0.9902859647173192};
+
+DM_FN double dm_horner(const double* c, int n, double u)
+{
+    double p = c[0];
+    DM_UNROLL
+    for (int i = 1; i < n; ++i) p = dm_fma(p, u, c[i]);
+    return p;
+}
+
+/* erfcx(t) for t >= 0 (t finite) */
+DM_FN double dm_erfcx_pos(double t)
+{
+    if (t < 0.5) return dm_horner(dm_erfcx_c0, 19, (t - 0.25) * 4.0);
+    if (t < 1.5) return dm_horner(dm_erfcx_c1, 21, (t - 1.0) * 2.0);
+    if (t < 3.0) return dm_horner(dm_erfcx_c2, 21, (t - 2.25) / 0.75);
+    if (t < 5.0) return dm_horner(dm_erfcx_c3, 21, (t - 4.0));
+    double w = 1.0 / (t * t);
+    double q = dm_horner(dm_erfcx_tail, 15, w * 50.0 - 1.0);   /* u = 2 w / 0.04 - 1 */
+    return q / (t * 1.7724538509055159);                        /* sqrt(pi) */
+}
+
+/* exp(-x^2) with the square split exactly (hi + lo) so |x| up to 27 keeps ~1 ulp */
+DM_FN double dm_exp_negsq(double x)
+{
+    double hi = x * x;
+    double lo = dm_fma(x, x, -hi);
+    double e = dm_exp(-hi);
+    return e - e * lo;
+}
+
+DM_FN double dm_erfc(double x)
+{
+    if (x != x) return x;
+    double a = dm_fabs(x);
+    if (a > 27.3) return x > 0 ? 0.0 : 2.0;
+    double v = dm_exp_negsq(a) * dm_erfcx_pos(a);
+    return x >= 0 ? v : 2.0 - v;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* powers                                                                                */
+/* ------------------------------------------------------------------------------------ */
+/* x^k, k a non-negative integer <= 64, correctly rounded via double-double accumulation
+ * (matches glibc's correctly-rounded pow(x, (double)k) barring exact ties).             */
+DM_FN double dm_pow_ui(double x, uint32_t k)
+{
+    if (k == 0) return 1.0;
+    if (k == 1 || x != x || x == 0.0 || !dm_isfinite(x)) {
+        double r = x;
+        for (uint32_t i = 1; i < k; ++i) r = r * x;
+        return r;
+    }
+    double hi = x, lo = 0.0;
+    for (uint32_t i = 1; i < k; ++i) {
+        double p = hi * x;
+        double pe = dm_fma(hi, x, -p);
+        double l2 = dm_fma(lo, x, pe);
+        hi = p + l2;
+        lo = l2 - (hi - p);
+        if (!dm_isfinite(hi)) return hi;
+    }
+    return hi + lo;
+}
+
+/* std::pow(double x, (double)y) restricted to what the path needs:
+ *   y an exact non-negative integer <= 64 -> dm_pow_ui;
+ *   y >= 2^53 (the size_t wrap of `4 - cpoints.size()`, src/PoseEstimator.cpp:336) -> limits;
+ *   otherwise exp(y * log(x)) for x > 0.                                                  */
+DM_FN double dm_pow(double x, double y)
+{
+    if (y == 0.0) return 1.0;
+    if (y >= 0.0 && y <= 64.0 && dm_floor(y) == y) return dm_pow_ui(x, (uint32_t)y);
+    if (x != x || y != y) return x + y;
+    if (y == 0.5 && x >= 0.0) return dm_sqrt(x);      /* correctly rounded, like glibc */
+    if (y >= 9007199254740992.0) {           /* huge even integer exponent */
+        double a = dm_fabs(x);
+        if (a == 1.0) return 1.0;
+        return a < 1.0 ? 0.0 : dm_from_bits(0x7ff0000000000000ull);
+    }
+    if (x == 0.0) return y > 0 ? 0.0 : dm_from_bits(0x7ff0000000000000ull);
+    if (x < 0.0) return dm_from_bits(0x7ff8000000000000ull);
+    if (x == 1.0) return 1.0;
+    return dm_exp(y * dm_log(x));
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* boost::math::normal pdf / cdf ratio (src/ContactModel.cpp:104-115)                    */
+/* ------------------------------------------------------------------------------------ */
+/* ratio = pdf(N(0,s), z) / cdf(N(0,s), z), s = sigma * correction.  Evaluated as
+ *   y = z / (s sqrt 2);  E = exp(-y^2)   (= the pdf exponent -z^2 / (2 s^2))
+ *   pdf = E / (s sqrt(2 pi));   cdf = erfc(-y) / 2 with erfc sharing E.
+ * Identical in exact arithmetic to boost's two calls; one exp instead of three.         */
+DM_FN double dm_normal_pdf_cdf_ratio(double z, double s)
+{
+    double y = z / (s * 1.4142135623730951);
+    double t = -y;                              /* erfc argument */
+    double a = dm_fabs(t);
+    double E = dm_exp_negsq(a);
+    double pdf = E / (s * 2.5066282746310002);
+    double cx = a > 27.3 ? 0.0 : E * dm_erfcx_pos(a);
+    double erfc_t = t >= 0 ? cx : 2.0 - cx;
+    double cdf = erfc_t / 2.0;
+    return pdf / cdf;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Philox4x32-10 counter-based generator (Salmon et al., SC'11 / Random123)              */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { uint32_t v[4]; } dm_philox_ctr;
+
+DM_FN dm_philox_ctr dm_philox4x32_10(dm_philox_ctr c, uint32_t k0, uint32_t k1)
+{
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c.v[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c.v[2];
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        dm_philox_ctr o;
+        o.v[0] = hi1 ^ c.v[1] ^ k0;
+        o.v[1] = lo1;
+        o.v[2] = hi0 ^ c.v[3] ^ k1;
+        o.v[3] = lo0;
+        c = o;
+    }
+    return c;
+}
+
+/* 53-bit uniform in [0, 1) from two 32-bit words */
+DM_FN double dm_u53(uint32_t a, uint32_t b)
+{
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * 1.1102230246251565e-16;
+}
+
+/* Box-Muller: u1 in [0,1) mapped to (0,1] */
+DM_FN void dm_box_muller(double u1, double u2, double* z0, double* z1)
+{
+    double r = dm_sqrt(-2.0 * dm_log(1.0 - u1));
+    double s, c;
+    dm_sincos(6.283185307179586 * u2, &s, &c);
+    *z0 = r * c;
+    *z1 = r * s;
+}
+
+/* RNG stream identifiers (Philox counter word 3, bits 24..31) */
+#define DM_STREAM_PROJECT 1u
+#define DM_STREAM_INIT 2u
+#define DM_STREAM_HASH 3u
+
+/* Draw block `call` of particle `gidx` for event `ev` of stream `stream`. */
+DM_FN dm_philox_ctr dm_draw(uint64_t seed, uint32_t stream, uint64_t ev, uint64_t gidx, uint32_t call)
+{
+    dm_philox_ctr c;
+    c.v[0] = (uint32_t)gidx;
+    c.v[1] = (uint32_t)(gidx >> 32);
+    c.v[2] = (uint32_t)ev;
+    c.v[3] = (stream << 24) | ((call & 0xffu) << 16) | (uint32_t)((ev >> 32) & 0xffffu);
+    return dm_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x5EED5EEDu);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* minstd_rand (Park-Miller, a = 48271, m = 2^31 - 1) with jump-ahead                     */
+/* ------------------------------------------------------------------------------------ */
+#define DM_MINSTD_A 48271u
+#define DM_MINSTD_M 2147483647u
+
+DM_FN uint32_t dm_mulmod31(uint32_t a, uint32_t b)
+{
+    uint64_t p = (uint64_t)a * b;                  /* < 2^62 */
+    uint64_t r = (p & DM_MINSTD_M) + (p >> 31);    /* < 2^32 */
+    r = (r & DM_MINSTD_M) + (r >> 31);
+    if (r >= DM_MINSTD_M) r -= DM_MINSTD_M;
+    return (uint32_t)r;
+}
+
+/* boost::random::linear_congruential_engine::seed for minstd_rand */
+DM_FN uint32_t dm_minstd_seed(uint64_t s)
+{
+    uint32_t x = (uint32_t)(s % DM_MINSTD_M);
+    return x == 0 ? 1u : x;
+}
+
+DM_FN uint32_t dm_minstd_next(uint32_t x) { return dm_mulmod31(x, DM_MINSTD_A); }
+
+/* A^n mod m by square-and-multiply */
+DM_FN uint32_t dm_minstd_pow(uint64_t n)
+{
+    uint32_t r = 1, b = DM_MINSTD_A;
+    while (n) { if (n & 1) r = dm_mulmod31(r, b); b = dm_mulmod31(b, b); n >>= 1; }
+    return r;
+}
+
+/* boost::uniform_real<>(0,1) on an integral engine with min 1, max 2147483646:
+ * (x - min) / (max - min + 1) * (1 - 0) + 0                                            */
+DM_FN double dm_minstd_uniform(uint32_t x)
+{
+    return ((double)(x - 1u) / 2147483646.0) * 1.0 + 0.0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* exact fixed-point helpers (order-independent sums)                                    */
+/* ------------------------------------------------------------------------------------ */
+/* trunc(v * 2^shift) for the resample cumulative sum: v >= 0 finite; saturates at 2^62-1
+ * (values with v * 2^shift >= 2^62).  The update path uses shift 60 (normalised weights). */
+DM_FN uint64_t dm_fx_shift(double v, int shift)
+{
+    if (!(v > 0.0)) return 0;
+    uint64_t b = dm_bits(v);
+    int e = (int)(b >> 52);
+    if (e == 0x7ff) return 0x3fffffffffffffffull;
+    if (e == 0) return 0;
+    uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
+    int sh = e - 1075 + shift;     /* value = m * 2^(e-1075) */
+    if (sh >= 10) return 0x3fffffffffffffffull;
+    if (sh >= 0) return m << sh;
+    if (sh <= -64) return 0;
+    return m >> (-sh);
+}
+
+DM_FN uint64_t dm_fx61(double v) { return dm_fx_shift(v, 61); }
+
+/* trunc(v * 2^scale) as an unsigned 128-bit integer split in four 32-bit limbs.
+ * v >= 0 finite.  Returns 1 if saturated (v * 2^scale >= 2^127).                        */
+DM_FN int dm_fx128_limbs(double v, int scale, uint32_t limb[4])
+{
+    limb[0] = limb[1] = limb[2] = limb[3] = 0;
+    if (!(v > 0.0)) return 0;
+    uint64_t b = dm_bits(v);
+    int e = (int)(b >> 52);
+    uint64_t m;
+    int ex;
+    if (e == 0) { m = b & 0x000fffffffffffffull; ex = -1074; }
+    else { m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull; ex = e - 1075; }
+    int sh = ex + scale;
+    unsigned __int128 x;
+    if (sh >= 0) {
+        if (sh > 74) { limb[0] = limb[1] = limb[2] = 0xffffffffu; limb[3] = 0x7fffffffu; return 1; }
+        x = (unsigned __int128)m << sh;
+    } else {
+        if (sh <= -64) return 0;
+        x = (unsigned __int128)(m >> (-sh));
+    }
+    limb[0] = (uint32_t)x;
+    limb[1] = (uint32_t)(x >> 32);
+    limb[2] = (uint32_t)(x >> 64);
+    limb[3] = (uint32_t)(x >> 96);
+    return 0;
+}
+
+/* Convert an exact sum held as limb sums  S = sum_j L[j] * 2^(32 j)  (each L[j] < 2^64)
+ * into the nearest double (round-half-even), scaled by 2^(-scale).                      */
+DM_FN double dm_limbs_to_double(const uint64_t L[4], int scale)
+{
+    /* carry-propagate into 32-bit digits d[0..5] */
+    uint32_t d[6];
+    uint64_t carry = 0;
+    for (int j = 0; j < 4; ++j) {
+        uint64_t lo = (L[j] & 0xffffffffull) + carry;
+        d[j] = (uint32_t)lo;
+        carry = (L[j] >> 32) + (lo >> 32);
+    }
+    d[4] = (uint32_t)carry;
+    d[5] = (uint32_t)(carry >> 32);
+    int top = 5;
+    while (top >= 0 && d[top] == 0) --top;
+    if (top < 0) return 0.0;
+    int lz = __builtin_clz(d[top]);
+    int msb = top * 32 + (31 - lz);          /* index of the leading bit */
+    /* take 64 bits starting at msb downwards, sticky for the rest */
+    uint64_t mant = 0;
+    int sticky = 0;
+    for (int bit = 0; bit < 64; ++bit) {
+        int pos = msb - bit;
+        mant <<= 1;
+        if (pos >= 0) mant |= (d[pos >> 5] >> (pos & 31)) & 1u;
+    }
+    for (int pos = msb - 64; pos >= 0 && !sticky; --pos)
+        if ((d[pos >> 5] >> (pos & 31)) & 1u) sticky = 1;
+    /* mant holds bits [msb .. msb-63]; keep 53 */
+    uint64_t keep = mant >> 11;
+    uint64_t rest = mant & 0x7ffull;
+    if (rest > 0x400ull || (rest == 0x400ull && (sticky || (keep & 1ull)))) keep += 1;
+    int e2 = msb - 52;
+    if (keep == 0x0020000000000000ull) { keep >>= 1; e2 += 1; }
+    /* value = keep * 2^(e2 - scale) */
+    return dm_ldexp((double)keep, e2 - scale);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* canonical reduction order ("sum contract")                                 */
+/* ------------------------------------------------------------------------------------ */
+/* Per-particle doubles are summed in chunks of 64 sub-lanes x J rows of consecutive
+ * global particle indices: chunk c holds [c*64*J, (c+1)*64*J); sub-lane s sums rows
+ * j = 0..J-1 (index c*64*J + 64*j + s) sequentially from +0.0; the 64 sub-lane sums are
+ * then combined by the xor butterfly (offsets 32,16,8,4,2,1) and the chunk total is
+ * converted exactly to fixed point (dm_fx128_limbs) and summed as integers.  J depends
+ * only on the GLOBAL particle count, so any sharding over GPUs gives the same bits.     */
+#define DM_CHUNK_LANES 64
+#define DM_FX_SCALE 112          /* fixed-point scale of a chunk total bounded by 2^10 */
+#define DM_NBUCKETS 6            /* cpoints.size() buckets 0,1,2,3,4,>=5 (phase B)     */
+
+DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
+{
+    uint64_t q = n_global / 262144u;
+    uint32_t j = 1;
+    while (j < 16u && (uint64_t)(j * 2u) <= q) j *= 2u;
+    return j;
+}
+
+/* exponent e >= 1 with max_w < 2^e (weight scale of the A_n / B_n accumulators) */
+DM_FN int dm_weight_exp(double max_w)
+{
+    if (!(max_w > 0.0) || !dm_isfinite(max_w)) return 1;
+    int e = (int)((dm_bits(max_w) >> 52) & 0x7ff) - 1023 + 1;   /* 2^(e-1) <= max_w < 2^e */
+    return e < 1 ? 1 : e;
+}
+
+/* weightingFunction(x, alpha, beta, gamma)  src/PoseEstimator.cpp:114-128 */
+DM_FN double dm_weighting_function(double x, double alpha, double beta, double gamma)
+{
+    if (x < alpha) return 1.0;
+    if (x < beta) {
+        double a = (1.0 - gamma) / (alpha - beta);
+        double b = 1.0 - alpha * a;
+        return a * x + b;
+    }
+    if (x >= beta) return gamma;
+    return 0.0;
+}
+
+#endif /* ESLAM_DETMATH_H */

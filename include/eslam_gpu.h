@@ -1,0 +1,241 @@
+/*
+ * eslam_gpu.h -- C ABI of the MI355X-native eSLAM particle-filter core.
+ *
+ * Drop-in boundary for the per-step hot path of liyangSKD/slam-eslam:
+ *
+ *   EmbodiedSlamFilter::update(body2odometry, BodyContactState, ltc)   src/EmbodiedSlamFilter.cpp:353-369
+ *     -> PoseEstimator::project                                         src/PoseEstimator.cpp:184-242
+ *     -> PoseEstimator::update -> updateWeights                         src/PoseEstimator.cpp:244-352
+ *          -> ContactModel::setContactPoints/evaluatePose/evaluateWeight/updateZPositionEstimate
+ *                                                                       src/ContactModel.cpp:21-41,117-340
+ *          -> GridAccess::get -> MLSMap::getPatch(p, patch, 3.0)        src/PoseEstimator.hpp:97-105
+ *     -> ParticleFilter::normalizeWeights / resample_stratified         src/ParticleFilter.hpp:46-108
+ *
+ * Plain C: POD structs, pointers and sizes, no torch / HIP types in the signatures.  Every
+ * entry point returns ESLAM_OK (0) or a negative ESLAM_ERR_* code; eslam_gpu_last_error()
+ * gives the message (the reference's std::runtime_error texts where one exists).
+ *
+ * One context = one GPU (one process per GPU for multi-GPU; see eslam_gpu_shard_*).  A
+ * context is not thread-safe.  Device memory is owned by the context; host buffers passed
+ * in are owned by the caller and only read/written during the call.
+ */
+#ifndef ESLAM_GPU_H
+#define ESLAM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ESLAM_ABI_VERSION 1
+
+/* maximum number of contact points of one BodyContactState handled per step
+ * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
+#define ESLAM_MAX_CONTACTS 32
+
+/* ---- status codes -------------------------------------------------------------------- */
+#define ESLAM_OK 0
+#define ESLAM_ERR_INVALID_ARG -1
+#define ESLAM_ERR_NO_ENVIRONMENT -2      /* "No environment attached." src/PoseEstimator.cpp:259-260 */
+#define ESLAM_ERR_ZERO_MEAS_VAR -3       /* "using a zero measurement variance leads to singularities" src/ContactModel.cpp:122-123 */
+#define ESLAM_ERR_HASH_SAMPLE -4         /* "could not sample from pose hash." src/PoseEstimator.cpp:84 */
+#define ESLAM_ERR_NO_MLS_GRID -5         /* "The provided environment does not contain an mls grid." src/EmbodiedSlamFilter.cpp:104 */
+#define ESLAM_ERR_HIP -6                 /* HIP runtime failure (message has details) */
+#define ESLAM_ERR_NOT_INITIALISED -7     /* no particles yet */
+#define ESLAM_ERR_UNSUPPORTED -8
+#define ESLAM_ERR_OUT_OF_MEMORY -9
+
+/* ---- Configuration (src/Configuration.hpp:12-213, the fields consumed on the path) ---- */
+typedef struct eslam_config {
+    uint64_t seed;                         /* Configuration::seed (42)                     */
+    uint64_t particle_count;               /* Configuration::particleCount (250)           */
+    uint64_t min_effective;                /* Configuration::minEffective (50)             */
+    double initial_rotation_error[3];      /* (0, 0, 0.1)                                  */
+    double initial_translation_error[3];   /* (0.1, 0.1, 1.0)                              */
+    double measurement_error;              /* 0.1                                          */
+    double discount_factor;                /* 0.9                                          */
+    double spread_threshold;               /* 0.9                                          */
+    double spread_translation_factor;      /* 0.1                                          */
+    double spread_rotation_factor;         /* 0.05                                         */
+    double slip_factor;                    /* 0.05                                         */
+    double max_yaw_deviation;              /* 15 deg                                       */
+    double measurement_threshold_distance; /* UpdateThreshold(0.1, 10 deg).distance       */
+    double measurement_threshold_angle;    /*                             .angle           */
+    /* ContactModelConfiguration (src/Configuration.hpp:51-81) */
+    int32_t use_slip_update;               /* false                                        */
+    int32_t use_shape_update;              /* true                                         */
+    uint64_t min_contacts;                 /* 3                                            */
+    double contact_likelihood_correction;  /* 0.33                                         */
+    double contact_point_radius;           /* 0.01                                         */
+    /* SurfaceHashConfig (src/Configuration.hpp:32-49) */
+    int32_t hash_use;                      /* false                                        */
+    uint64_t hash_period;                  /* 10                                           */
+    double hash_percentage;                /* 0.05                                         */
+    double hash_avg_factor;                /* 0.1                                          */
+    uint64_t hash_slope_bins;              /* 20                                           */
+    uint64_t hash_angular_steps;           /* 16                                           */
+    int32_t log_debug;                     /* Configuration::logDebug (false)              */
+    /* build-specific knobs (not in the reference) */
+    uint32_t flags;                        /* ESLAM_FLAG_*                                 */
+} eslam_config;
+
+#define ESLAM_FLAG_RECORD_ANCESTORS 0x1u   /* keep the last resample's ancestor indices     */
+#define ESLAM_FLAG_NO_MAP_LDS 0x2u         /* disable the LDS map window (global lookups)   */
+#define ESLAM_FLAG_NO_AUX_GATHER 0x4u      /* do not carry mprob/floating through resample  */
+
+void eslam_config_default(eslam_config* cfg);
+
+/* ---- multi-level surface grid (envire::MLSGrid as consumed by GridAccess::get) ----------
+ * Cells are (m, n) with m along x; cell index = n * width + m.  Patches of cell c are
+ * patches[cell_start[c] .. cell_start[c+1]) in stored order.  getPatch(p, patch, 3.0)
+ * transforms p by global2local, finds the cell with
+ *   m = floor((x - offset_x) / scale_x), n = floor((y - offset_y) / scale_y),
+ * and returns the first patch whose distance to the query patch (mean = p.z,
+ * stdev = sqrt(measVar)) is below 3:  |mean_p - mean_q| / sqrt(stdev_p^2 + stdev_q^2)
+ * (vertical patches, height > 0, span [mean - height, mean]).                           */
+typedef struct eslam_mls_grid {
+    uint32_t width, height;
+    double scale_x, scale_y;
+    double offset_x, offset_y;
+    double global2local[12];               /* 3x4 row-major affine: GridAccess::C_global2local */
+    const uint32_t* cell_start;            /* width*height + 1 entries                       */
+    const float* patch_mean;               /* n_patches                                      */
+    const float* patch_stdev;              /* n_patches                                      */
+    const float* patch_height;             /* n_patches or NULL (all horizontal)             */
+    uint64_t n_patches;
+} eslam_mls_grid;
+
+/* ---- per-step input: EmbodiedSlamFilter::update(body2odometry, bs, ltc) ---------------- */
+typedef struct eslam_contact_point {       /* odometry::BodyContactPoint                    */
+    double position[3];                    /* body frame                                    */
+    float contact;                         /* contact probability, NaN = unknown (passes)   */
+    int32_t group_id;                      /* -1 = ungrouped                                */
+} eslam_contact_point;
+
+typedef struct eslam_step_input {
+    double body2odometry_rot[4];           /* quaternion (w, x, y, z) of body2odometry        */
+    double body2odometry_trans[3];
+    /* outputs of the external odometry::FootContact after odometry.update(bs, orientation):
+     * getPoseDelta().position, getPositionError()(2,2) and the Gaussian that
+     * getPoseDeltaSample2D() samples (mean dx, dy, dtheta; 3x3 covariance, row-major).     */
+    double pose_delta_trans[3];
+    double position_error_zz;
+    double sample_mean[3];
+    double sample_cov[9];
+    uint32_t n_contacts;
+    uint32_t ltc_count;                    /* terrain classifications given (gate only)      */
+    eslam_contact_point contacts[ESLAM_MAX_CONTACTS];
+} eslam_step_input;
+
+/* ---- particle state, structure of arrays (PoseParticle, src/PoseParticle.hpp:52-86) ----- */
+typedef struct eslam_particles {
+    double* x;                             /* position.x                                    */
+    double* y;                             /* position.y                                    */
+    double* orientation;
+    double* zpos;
+    double* zsigma;
+    double* weight;
+    double* mprob;
+    uint8_t* floating;
+    uint8_t* n_contact_points;             /* cpoints.size() of the last updateWeights       */
+} eslam_particles;
+
+/* result of one PoseEstimator::update (device-side values, read after eslam_gpu_sync) */
+typedef struct eslam_update_info {
+    double effective;                      /* normalizeWeights() return value                */
+    double weight_sum;                     /* sum of weights before normalisation            */
+    double floating_weight;                /* sum_data_weights / data_particles              */
+    double max_weight;                     /* PoseEstimator::max_weight after the update      */
+    uint64_t data_particles;
+    uint64_t total_points;
+    int32_t resampled;
+    int32_t uniform_reset;                 /* sumWeights <= 0 branch taken                   */
+    uint64_t resample_overruns;            /* draws beyond the cumulative sum (clamped, Q5)  */
+    uint64_t update_count;
+} eslam_update_info;
+
+/* ---- lifecycle ------------------------------------------------------------------------ */
+typedef struct eslam_ctx eslam_ctx;
+
+/* PoseEstimator(odometry, config) / EmbodiedSlamFilter(odoConfig, config): binds `device`. */
+int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx** out);
+void eslam_gpu_destroy(eslam_ctx* ctx);
+const char* eslam_gpu_last_error(const eslam_ctx* ctx);
+int eslam_gpu_abi_version(void);
+/* run on a caller-provided hipStream_t (NULL = the context's own stream) */
+int eslam_gpu_set_stream(eslam_ctx* ctx, void* hip_stream);
+
+/* ---- environment (PoseEstimator::setEnvironment / GridAccess::setMap, shared map) ------ */
+int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* grid);
+
+/* ---- initialisation -------------------------------------------------------------------
+ * PoseEstimator::init(N, mu, sigma, zpos, zsigma)  src/PoseEstimator.cpp:88-102
+ * mu/sigma = (x, y, theta).  weight = 0 (Q3), floating = true.                          */
+int eslam_gpu_init_gaussian(eslam_ctx* ctx, uint64_t n, const double mu[3], const double sigma[3],
+                            double zpos, double zsigma);
+/* EmbodiedSlamFilter::init(env, pose, useSharedMap=true)  src/EmbodiedSlamFilter.cpp:70-177
+ * pose = position[3] + quaternion (w,x,y,z); particle count / errors from the config.    */
+int eslam_gpu_init_pose(eslam_ctx* ctx, const double position[3], const double orientation[4]);
+/* replace the particle set (getParticles() is a mutable reference in the reference)       */
+int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const eslam_particles* p);
+int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p);
+int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n);
+
+/* ---- the hot path ----------------------------------------------------------------------- */
+/* EmbodiedSlamFilter::update(body2odometry, bs, ltc): project, then the measurement update
+ * when UpdateThreshold::test(udPose^-1 * body2odometry) (angle/distance swapped, Q6) or
+ * ltc_count > 0.  *updated receives the bool.  Asynchronous on the context stream.         */
+int eslam_gpu_step(eslam_ctx* ctx, const eslam_step_input* in, int* updated);
+/* PoseEstimator::project(state, orientation)                                              */
+int eslam_gpu_project(eslam_ctx* ctx, const eslam_step_input* in);
+/* PoseEstimator::update(state, orientation, ltc): updateWeights, normalizeWeights, resample
+ * if effective < minEffective.                                                             */
+int eslam_gpu_update(eslam_ctx* ctx, const eslam_step_input* in);
+/* wait for the stream; fetch the info of the last update (info may be NULL)               */
+int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info);
+
+/* ---- ParticleFilter<T> API (src/ParticleFilter.hpp:34-173) ------------------------------ */
+int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum);
+int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective);
+int eslam_gpu_resample(eslam_ctx* ctx);                       /* resample_stratified(N)   */
+int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index);
+/* PoseEstimator::getCentroid (normalises in place, Q15): position[3] + quaternion (w,x,y,z) */
+int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double orientation[4]);
+
+/* ---- resume state: RNG + the filter scalars (bit-exact resume with the particles) ------- */
+typedef struct eslam_rng_state {
+    uint32_t minstd_x;                     /* ParticleFilter::rand_gen state                */
+    uint32_t pad;
+    uint64_t project_count;                /* Philox event counter of project()              */
+    uint64_t init_count;
+    uint64_t hash_count;
+    double max_weight;                     /* PoseEstimator::max_weight                      */
+    double ud_pose[12];                    /* EmbodiedSlamFilter::udPose, 3x4 row-major      */
+} eslam_rng_state;
+int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st);
+int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st);
+
+/* ---- diagnostics ------------------------------------------------------------------------- */
+/* ancestor index of every particle of the last resample (needs ESLAM_FLAG_RECORD_ANCESTORS) */
+int eslam_gpu_get_ancestors(eslam_ctx* ctx, uint32_t* out, uint64_t n);
+/* per-kernel timing of the last step, milliseconds (HIP events on the context stream)     */
+typedef struct eslam_kernel_times {
+    float project_weight_ms;
+    float finalize_ms;
+    float normalize_scan_ms;
+    float resample_ms;
+    float total_ms;
+} eslam_kernel_times;
+int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable);
+int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t);
+/* evaluate the deterministic math on the device for n inputs (tests/test_gpu_math.py):
+ * fn: 0 exp, 1 log, 2 sin, 3 cos, 4 erfc, 5 sqrt, 6 div(x, y), 7 pdf/cdf ratio(x, y),
+ *     8 pow(x, y), 9 fx61(x) as bits                                                        */
+int eslam_gpu_selftest_math(int device, int fn, const double* x, const double* y, double* out, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESLAM_GPU_H */

@@ -1,0 +1,1134 @@
+/*
+ * eslam_oracle.c -- CPU oracle (TEST INFRASTRUCTURE, see eslam_oracle.h).
+ *
+ * Plain-C restatement of the reference per-step particle-filter path.  Citations are
+ * path:line into the reference (liyangSKD/slam-eslam).  Third-party arithmetic the
+ * reference calls (Eigen, base-types, boost.math, boost.random, envire, odometry) is
+ * restated from its published algorithm; see DESIGN.md "oracle" for what is pinned.
+ *
+ * Build: oracle/Makefile  (gcc -O2 -mfma -ffp-contract=off -fPIC -shared).
+ */
+#include "eslam_oracle.h"
+#include "../include/eslam_detmath.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ========================================================================================
+ * small Eigen / base-types restatements (host only)
+ * ====================================================================================== */
+
+/* Eigen::QuaternionBase::toRotationMatrix */
+static void q_to_mat(const double q[4], double R[9])
+{
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+    R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+/* Eigen quaternion product (generic quat_product) */
+static void q_mul(const double a[4], const double b[4], double r[4])
+{
+    double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
+    double z = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
+    r[0] = w; r[1] = x; r[2] = y; r[3] = z;
+}
+
+/* Quaternion(AngleAxis(angle, UnitZ)) */
+static void q_from_yaw(double angle, double q[4])
+{
+    double ha = 0.5 * angle;
+    q[0] = cos(ha);
+    double s = sin(ha);
+    q[1] = s * 0.0; q[2] = s * 0.0; q[3] = s * 1.0;
+}
+
+/* QuaternionBase::_transformVector:  uv = vec x v; uv += uv; v + w*uv + vec x uv */
+static void q_rotate(const double q[4], const double v[3], double out[3])
+{
+    const double qx = q[1], qy = q[2], qz = q[3], w = q[0];
+    double uv[3] = {qy * v[2] - qz * v[1], qz * v[0] - qx * v[2], qx * v[1] - qy * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    double c[3] = {qy * uv[2] - qz * uv[1], qz * uv[0] - qx * uv[2], qx * uv[1] - qy * uv[0]};
+    out[0] = (v[0] + w * uv[0]) + c[0];
+    out[1] = (v[1] + w * uv[1]) + c[1];
+    out[2] = (v[2] + w * uv[2]) + c[2];
+}
+
+/* base::getYaw = getEuler(q)[0]: atan2(m10, m00) unless gimbal-locked (base/Pose.hpp) */
+static double get_yaw(const double q[4])
+{
+    double R[9];
+    q_to_mat(q, R);
+    double x = sqrt(R[8] * R[8] + R[7] * R[7]);
+    if (x > 1e-12) return atan2(R[3], R[0]);
+    return 0.0;
+}
+
+/* base::removeYaw(q) = AngleAxis(-getYaw(q), UnitZ) * q */
+static void remove_yaw(const double q[4], double out[4])
+{
+    double a[4];
+    q_from_yaw(-get_yaw(q), a);
+    q_mul(a, q, out);
+}
+
+/* Eigen: Quaternion from a rotation matrix (quaternionbase_assign_impl, 3x3) */
+static void q_from_mat(const double m[9], double q[4])
+{
+    double t = m[0] + m[4] + m[8];
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[0] = 0.5 * t;
+        t = 0.5 / t;
+        q[1] = (m[7] - m[5]) * t;
+        q[2] = (m[2] - m[6]) * t;
+        q[3] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+        double v[3];
+        v[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        v[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        v[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+        q[1] = v[0]; q[2] = v[1]; q[3] = v[2];
+    }
+}
+
+/* AngleAxisd(Quaternion).angle() */
+static double q_angle(const double q[4])
+{
+    double n = sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    if (n != 0.0) return 2.0 * atan2(n, fabs(q[0]));
+    return 0.0;
+}
+
+/* UpdateThreshold::test(const Affine3d& delta)  src/Configuration.hpp:18-26 (args swapped, Q6)
+ * with delta = udPose.inverse() * body2odometry                                              */
+static int update_threshold_test(double thr_distance, double thr_angle, const double ud[12],
+                                 const double q_b[4], const double t_b[3])
+{
+    double Rb[9];
+    q_to_mat(q_b, Rb);
+    /* Transform::inverse (Affine): linear = R^T, translation = -(R^T t) */
+    double Ri[9] = {ud[0], ud[4], ud[8], ud[1], ud[5], ud[9], ud[2], ud[6], ud[10]};
+    double ti[3];
+    for (int r = 0; r < 3; ++r) ti[r] = -((Ri[r * 3 + 0] * ud[3] + Ri[r * 3 + 1] * ud[7]) + Ri[r * 3 + 2] * ud[11]);
+    double L[9], t[3];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c)
+            L[r * 3 + c] = (Ri[r * 3 + 0] * Rb[0 * 3 + c] + Ri[r * 3 + 1] * Rb[1 * 3 + c]) + Ri[r * 3 + 2] * Rb[2 * 3 + c];
+        t[r] = ((Ri[r * 3 + 0] * t_b[0] + Ri[r * 3 + 1] * t_b[1]) + Ri[r * 3 + 2] * t_b[2]) + ti[r];
+    }
+    double q[4];
+    q_from_mat(L, q);
+    double angle = q_angle(q);
+    double dist = sqrt((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]);
+    /* test(distance := angle, angle := translation norm) */
+    return angle > thr_distance || dist > thr_angle;
+}
+
+static void set_translation_pose(double ud[12], double x, double y, double z)
+{
+    memset(ud, 0, 12 * sizeof(double));
+    ud[0] = ud[5] = ud[10] = 1.0;
+    ud[3] = x; ud[7] = y; ud[11] = z;
+}
+
+/* ========================================================================================
+ * MLS grid: envire::MLSGrid::getPatch(p, patch, sigma_threshold = 3.0)
+ * ====================================================================================== */
+/* The query patch (src/ContactModel.cpp:151) has mean = point z; it is compared in the
+ * grid frame, i.e. against the local z of the transformed point.                        */
+int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_world, double q_stdev,
+                     double* mean, double* stdev)
+{
+    const double* A = g->global2local;
+    double lx = ((A[0] * p[0] + A[1] * p[1]) + A[2] * p[2]) + A[3];
+    double ly = ((A[4] * p[0] + A[5] * p[1]) + A[6] * p[2]) + A[7];
+    double lz = ((A[8] * p[0] + A[9] * p[1]) + A[10] * p[2]) + A[11];
+    const double q_mean = lz;
+    (void)q_mean_world;
+    double fm = floor((lx - g->offset_x) / g->scale_x);
+    double fn = floor((ly - g->offset_y) / g->scale_y);
+    if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) return 0;
+    uint64_t cell = (uint64_t)fn * g->width + (uint64_t)fm;
+    uint32_t b = g->cell_start[cell], e = g->cell_start[cell + 1];
+    double qv = q_stdev * q_stdev;
+    for (uint32_t k = b; k < e; ++k) {
+        double pm = (double)g->patch_mean[k];
+        double ps = (double)g->patch_stdev[k];
+        double ph = g->patch_height ? (double)g->patch_height[k] : 0.0;
+        double diff;
+        if (ph > 0.0) {                   /* vertical patch spans [mean - height, mean] */
+            if (q_mean > pm) diff = q_mean - pm;
+            else if (q_mean < pm - ph) diff = (pm - ph) - q_mean;
+            else diff = 0.0;
+        } else {
+            diff = fabs(pm - q_mean);
+        }
+        double d = diff / sqrt(ps * ps + qv);
+        if (d < 3.0) { *mean = pm; *stdev = ps; return 1; }
+    }
+    return 0;
+}
+
+static int grid_map_fn(void* user, const double p[3], double q_mean, double q_stdev, double* mean, double* stdev)
+{
+    return or_mls_get_patch((const eslam_mls_grid*)user, p, q_mean, q_stdev, mean, stdev);
+}
+
+/* ========================================================================================
+ * ContactModel
+ * ====================================================================================== */
+void or_cm_init(or_contact_model* cm, const eslam_config* cfg)
+{
+    memset(cm, 0, sizeof(*cm));
+    cm->use_slip_update = cfg->use_slip_update;
+    cm->use_shape_update = cfg->use_shape_update;
+    cm->min_contacts = cfg->min_contacts;
+    cm->correction = cfg->contact_likelihood_correction;
+    cm->radius = cfg->contact_point_radius;
+}
+
+/* src/ContactModel.cpp:21-41 */
+void or_cm_set_contact_points(or_contact_model* cm, uint32_t n, const eslam_contact_point* pts, const double q[4])
+{
+    double yc[4];
+    remove_yaw(q, yc);
+    cm->m = n;
+    cm->nlow = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        q_rotate(yc, pts[i].position, cm->pos[i]);
+        cm->contact[i] = pts[i].contact;
+        cm->group[i] = pts[i].group_id;
+    }
+}
+
+/* ContactModel::contactLikelihoodRatio  src/ContactModel.cpp:104-115 */
+static double contact_likelihood_ratio(const or_contact_model* cm, double z, double sigma)
+{
+    return dm_normal_pdf_cdf_ratio(z, sigma * cm->correction);
+}
+
+/* ContactModel::evaluateWeight  src/ContactModel.cpp:262-317 */
+static void evaluate_weight(or_contact_model* cm)
+{
+    double d1 = 0, d2 = 0;
+    for (uint32_t i = 0; i < cm->ncp; ++i) {
+        d1 += cm->cp[i].zdiff / cm->cp[i].zvar;
+        d2 += 1.0 / cm->cp[i].zvar;
+    }
+    const double delta = d1 / d2;
+    double pz = 1.0;
+    for (uint32_t i = 0; i < cm->ncp; ++i) {
+        const double odiff = (cm->cp[i].zdiff - delta) / sqrt(cm->cp[i].zvar);
+        const double zk = dm_exp(-(odiff * odiff) / (2.0));
+        if (cm->use_shape_update) pz *= zk;
+        if (cm->use_slip_update) pz *= cm->cp[i].prob;
+    }
+    cm->weight = pz;
+    cm->zdelta = -delta;
+    cm->zvar = 1.0 / d2;
+}
+
+/* ContactModel::evaluatePose  src/ContactModel.cpp:117-224 (group quirk Q7 kept) */
+int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_var, or_map_fn map, void* user)
+{
+    if (meas_var == 0) return -1;
+    cm->ncp = 0;
+    or_cpoint p = {{0, 0, 0}, INFINITY, INFINITY, 1.0};
+    int valid = 0, group_valid = 1;
+    const double contact_threshold = 0.2;
+    double contact_ratio = 0, pose_var_avg = 0;
+    cm->posevar = 0;
+    const double q_stdev = sqrt(meas_var);
+    for (uint32_t i = 0; i < cm->m; ++i) {
+        const int32_t gid = cm->group[i];
+        const double* c = cm->pos[i];
+        double w[3];
+        w[0] = ((T[0] * c[0] + T[1] * c[1]) + T[2] * c[2]) + T[3];
+        w[1] = ((T[4] * c[0] + T[5] * c[1]) + T[6] * c[2]) + T[7];
+        w[2] = ((T[8] * c[0] + T[9] * c[1]) + T[10] * c[2]) + T[11];
+        w[0] = w[0] - 0.0;
+        w[1] = w[1] - 0.0;
+        w[2] = w[2] - cm->radius;
+        const float cp = cm->contact[i];
+        if (group_valid && !((double)cp < contact_threshold)) {
+            double mean, stdev;
+            if (map(user, w, w[2], q_stdev, &mean, &stdev)) {
+                const double zdiff = w[2] - mean;
+                const double pose_var = stdev * stdev;
+                const double zvar = stdev * stdev + meas_var;
+                const double ratio = contact_likelihood_ratio(cm, zdiff, sqrt(zvar));
+                if (!valid) {
+                    p.point[0] = w[0]; p.point[1] = w[1]; p.point[2] = mean;
+                    p.zdiff = zdiff * ratio;
+                    p.zvar = zvar * ratio;
+                    p.prob = 1.0;
+                    contact_ratio = ratio;
+                    pose_var_avg = pose_var * ratio;
+                } else {
+                    p.zdiff += zdiff * ratio;
+                    p.zvar += zvar * ratio;
+                    contact_ratio += ratio;
+                    pose_var_avg += pose_var * ratio;
+                }
+                valid = 1;
+            } else {
+                group_valid = 0;
+            }
+        }
+        if (valid && (gid == -1 || i + 1 == cm->m || gid != cm->group[i + 1])) {
+            if (group_valid && contact_ratio > 1e-9) {
+                p.zdiff /= contact_ratio;
+                p.zvar /= contact_ratio;
+                cm->posevar += pose_var_avg / contact_ratio;
+                cm->cp[cm->ncp++] = p;
+                /* useSlipUpdate: p.prob *= matchTerrain(...) happens after the push (Q8) */
+            }
+            group_valid = 1;
+            valid = 0;
+            pose_var_avg = 0;
+            contact_ratio = 0;
+        }
+    }
+    if ((uint64_t)cm->ncp >= cm->min_contacts) {
+        evaluate_weight(cm);
+        return 1;
+    }
+    return 0;
+}
+
+/* src/ContactModel.cpp:319-340 (1-sigma gate, Q9) */
+int or_cm_update_z(const or_contact_model* cm, double* z_pos, double* z_var)
+{
+    const double pose_var = cm->posevar / (double)cm->ncp;
+    double a = *z_var - pose_var;
+    double delta_var = (a < 1e-9) ? 1e-9 : a;         /* std::max(a, 1e-9) */
+    const double z_delta = cm->zdelta;
+    if (fabs(z_delta / sqrt(delta_var)) > 1.0) return 0;
+    double gain = *z_var / (*z_var + cm->zvar);
+    *z_pos += gain * z_delta;
+    double var_gain = delta_var / (delta_var + cm->zvar);
+    delta_var = (1.0 - var_gain) * delta_var;
+    *z_var = pose_var + delta_var;
+    return 1;
+}
+
+/* ContactModel::lowestPointHeuristic  src/ContactModel.cpp:48-79 */
+static void lowest_point_heuristic(or_contact_model* cm, int update_probabilities)
+{
+    cm->nlow = 0;
+    int gidx[ESLAM_MAX_CONTACTS];
+    int ng = 0;
+    for (uint32_t i = 0; i < cm->m; ++i) {
+        if (cm->group[i] >= 0) {
+            gidx[ng++] = (int)i;
+            if (update_probabilities) cm->contact[i] = 0;
+        }
+        if (ng == 0) {
+            memcpy(cm->low[cm->nlow++], cm->pos[i], sizeof(double) * 3);
+        } else if (i + 1 == cm->m || cm->group[i + 1] != cm->group[i]) {
+            /* std::sort of (z, index) pairs: lowest z, ties by index */
+            int best = gidx[0];
+            for (int k = 1; k < ng; ++k) {
+                int c = gidx[k];
+                if (cm->pos[c][2] < cm->pos[best][2] || (cm->pos[c][2] == cm->pos[best][2] && c < best)) best = c;
+            }
+            memcpy(cm->low[cm->nlow++], cm->pos[best], sizeof(double) * 3);
+            if (update_probabilities) cm->contact[best] = 1;
+            ng = 0;
+        }
+    }
+}
+
+uint32_t or_cm_lowest_points(or_contact_model* cm, double* out)
+{
+    if (cm->nlow == 0) lowest_point_heuristic(cm, 0);
+    if (out) memcpy(out, cm->low, sizeof(double) * 3 * cm->nlow);
+    return cm->nlow;
+}
+
+void or_cm_update_contact_state_lph(or_contact_model* cm) { lowest_point_heuristic(cm, 1); }
+
+/* ========================================================================================
+ * SurfaceHash pieces
+ * ====================================================================================== */
+/* Buckets<T>::bucketIndex  src/SurfaceHash.hpp:25-29 */
+int or_bucket_index(int count, double min_val, double max_val, double value)
+{
+    int idx = (int)((value - min_val) / (max_val - min_val) * count);
+    int lo = idx > 0 ? idx : 0;
+    return (count - 1) < lo ? (count - 1) : lo;
+}
+
+/* SurfaceParam::fromPoints  src/SurfaceHash.hpp:60-110: normal equations solved by a
+ * pivoted LDL^T (Eigen::LDLT: largest remaining diagonal as pivot)                       */
+void or_surface_param_from_points(const double* P, uint32_t n, double* slope_x, double* slope_y)
+{
+    double x = 0, y = 0, z = 0, xx = 0, yy = 0, xy = 0, xz = 0, yz = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const double* p = P + 3 * i;
+        x += p[0]; y += p[1]; z += p[2];
+        xx += p[0] * p[0]; yy += p[1] * p[1]; xy += p[0] * p[1];
+        xz += p[0] * p[2]; yz += p[1] * p[2];
+    }
+    double A[3][3] = {{xx, xy, x}, {xy, yy, y}, {x, y, (double)n}};
+    double b[3] = {xz, yz, z};
+    int perm[3] = {0, 1, 2};
+    /* in-place pivoted LDL^T */
+    for (int k = 0; k < 3; ++k) {
+        int piv = k;
+        for (int i = k + 1; i < 3; ++i) if (fabs(A[i][i]) > fabs(A[piv][piv])) piv = i;
+        if (piv != k) {
+            int t = perm[k]; perm[k] = perm[piv]; perm[piv] = t;
+            for (int c = 0; c < 3; ++c) { double tmp = A[k][c]; A[k][c] = A[piv][c]; A[piv][c] = tmp; }
+            for (int r = 0; r < 3; ++r) { double tmp = A[r][k]; A[r][k] = A[r][piv]; A[r][piv] = tmp; }
+        }
+        for (int j = 0; j < k; ++j) A[k][k] -= A[k][j] * A[k][j] * A[j][j];
+        for (int i = k + 1; i < 3; ++i) {
+            double s = A[i][k];
+            for (int j = 0; j < k; ++j) s -= A[i][j] * A[k][j] * A[j][j];
+            A[i][k] = A[k][k] != 0.0 ? s / A[k][k] : 0.0;
+        }
+    }
+    double r[3] = {b[perm[0]], b[perm[1]], b[perm[2]]};
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < i; ++j) r[i] -= A[i][j] * r[j];
+    for (int i = 0; i < 3; ++i) r[i] = A[i][i] != 0.0 ? r[i] / A[i][i] : 0.0;
+    for (int i = 2; i >= 0; --i) for (int j = i + 1; j < 3; ++j) r[i] -= A[j][i] * r[j];
+    double res[3];
+    for (int i = 0; i < 3; ++i) res[perm[i]] = r[i];
+    *slope_x = res[0];
+    *slope_y = res[1];
+}
+
+/* ========================================================================================
+ * the filter
+ * ====================================================================================== */
+struct or_filter {
+    eslam_config cfg;
+    int sum_mode;
+    uint64_t n;
+    double *x, *y, *th, *z, *zs, *w, *mprob;
+    uint8_t *floating, *ncp;
+    /* debug of the last updateWeights */
+    uint32_t* dbg_ncp;
+    or_cpoint* dbg_cp;
+    double *dbg_zdelta, *dbg_zvar;
+    /* environment */
+    int has_map;
+    eslam_mls_grid map;
+    uint32_t* map_cells;
+    float *map_mean, *map_stdev, *map_height;
+    /* random state */
+    uint32_t minstd;
+    uint64_t project_count, init_count, hash_count;
+    /* PoseEstimator members */
+    double max_weight;
+    double zcomp[4];
+    int wexp;
+    /* EmbodiedSlamFilter members */
+    double ud_pose[12];
+    /* last update */
+    eslam_update_info info;
+    uint32_t* anc;
+    int has_anc;
+};
+
+static void or_free_particles(or_filter* f)
+{
+    free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob);
+    free(f->floating); free(f->ncp); free(f->anc);
+    free(f->dbg_ncp); free(f->dbg_cp); free(f->dbg_zdelta); free(f->dbg_zvar);
+    f->x = f->y = f->th = f->z = f->zs = f->w = f->mprob = NULL;
+    f->floating = f->ncp = NULL;
+    f->anc = NULL;
+    f->dbg_ncp = NULL; f->dbg_cp = NULL; f->dbg_zdelta = f->dbg_zvar = NULL;
+    f->n = 0;
+}
+
+static int or_alloc_particles(or_filter* f, uint64_t n)
+{
+    or_free_particles(f);
+    f->n = n;
+    size_t b = (size_t)(n ? n : 1);
+    f->x = calloc(b, 8); f->y = calloc(b, 8); f->th = calloc(b, 8); f->z = calloc(b, 8);
+    f->zs = calloc(b, 8); f->w = calloc(b, 8); f->mprob = calloc(b, 8);
+    f->floating = calloc(b, 1); f->ncp = calloc(b, 1); f->anc = calloc(b, 4);
+    f->dbg_ncp = calloc(b, 4);
+    f->dbg_cp = calloc(b * ESLAM_MAX_CONTACTS, sizeof(or_cpoint));
+    f->dbg_zdelta = calloc(b, 8); f->dbg_zvar = calloc(b, 8);
+    f->has_anc = 0;
+    return (f->x && f->dbg_cp) ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
+}
+
+or_filter* or_create(const eslam_config* cfg, int sum_mode)
+{
+    or_filter* f = calloc(1, sizeof(or_filter));
+    f->cfg = *cfg;
+    f->sum_mode = sum_mode;
+    f->minstd = dm_minstd_seed(cfg->seed);      /* ParticleFilter(seed) src/ParticleFilter.hpp:24-27 */
+    f->max_weight = 0;                          /* src/PoseEstimator.cpp:13-25 */
+    f->zcomp[0] = 1.0;
+    f->wexp = 1;
+    set_translation_pose(f->ud_pose, 1000, 0, 0);
+    return f;
+}
+
+void or_destroy(or_filter* f)
+{
+    if (!f) return;
+    or_free_particles(f);
+    free(f->map_cells); free(f->map_mean); free(f->map_stdev); free(f->map_height);
+    free(f);
+}
+
+int or_set_map(or_filter* f, const eslam_mls_grid* g)
+{
+    uint64_t ncell = (uint64_t)g->width * g->height;
+    free(f->map_cells); free(f->map_mean); free(f->map_stdev); free(f->map_height);
+    f->map = *g;
+    f->map_cells = malloc((ncell + 1) * 4);
+    memcpy(f->map_cells, g->cell_start, (ncell + 1) * 4);
+    size_t np = (size_t)(g->n_patches ? g->n_patches : 1);
+    f->map_mean = malloc(np * 4); f->map_stdev = malloc(np * 4);
+    memcpy(f->map_mean, g->patch_mean, g->n_patches * 4);
+    memcpy(f->map_stdev, g->patch_stdev, g->n_patches * 4);
+    f->map_height = NULL;
+    if (g->patch_height) { f->map_height = malloc(np * 4); memcpy(f->map_height, g->patch_height, g->n_patches * 4); }
+    f->map.cell_start = f->map_cells;
+    f->map.patch_mean = f->map_mean;
+    f->map.patch_stdev = f->map_stdev;
+    f->map.patch_height = f->map_height;
+    f->has_map = 1;
+    return 0;
+}
+
+uint64_t or_count(const or_filter* f) { return f->n; }
+
+/* PoseEstimator::init(N, mu, sigma, zpos, zsigma)  src/PoseEstimator.cpp:88-102, with
+ * samplePose2D (src/PoseEstimator.cpp:64-73) drawing its 3 normals from the INIT stream. */
+int or_init_gaussian(or_filter* f, uint64_t n, const double mu[3], const double sigma[3], double zpos, double zsigma)
+{
+    int rc = or_alloc_particles(f, n);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i) {
+        dm_philox_ctr d0 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, i, 0);
+        dm_philox_ctr d1 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, i, 1);
+        double n0, n1, n2, n3;
+        dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &n0, &n1);
+        dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &n2, &n3);
+        f->x[i] = n0 * sigma[0] + mu[0];
+        f->y[i] = n1 * sigma[1] + mu[1];
+        f->th[i] = n2 * sigma[2] + mu[2];
+        f->z[i] = zpos;
+        f->zs[i] = zsigma;
+        f->w[i] = 0;            /* PoseParticle ctor: weight(0), Q3 */
+        f->mprob[i] = 0;
+        f->floating[i] = 1;
+        f->ncp[i] = 0;
+    }
+    f->init_count++;
+    f->wexp = 1;
+    return 0;
+}
+
+/* EmbodiedSlamFilter::init(env, pose) non-hash branch  src/EmbodiedSlamFilter.cpp:109-128:
+ * angle = eulerAngles(2,1,0)[0] (Eigen >= 3.3 folds it into [0, pi]), sigma from config,
+ * zsigma = initialTranslationError.z + 1e-3, udPose = Translation(1000,0,0).            */
+int or_init_pose(or_filter* f, const double pos[3], const double q[4])
+{
+    double R[9];
+    q_to_mat(q, R);
+    double angle = atan2(R[3], R[0]);
+    if (angle < 0.0) angle += M_PI;
+    double mu[3] = {pos[0], pos[1], angle};
+    double sg[3] = {f->cfg.initial_translation_error[0], f->cfg.initial_translation_error[1],
+                    f->cfg.initial_rotation_error[2]};
+    int rc = or_init_gaussian(f, f->cfg.particle_count, mu, sg, pos[2], f->cfg.initial_translation_error[2] + 1e-3);
+    set_translation_pose(f->ud_pose, 1000, 0, 0);
+    return rc;
+}
+
+int or_upload(or_filter* f, uint64_t n, const eslam_particles* p)
+{
+    int rc = or_alloc_particles(f, n);
+    if (rc) return rc;
+    memcpy(f->x, p->x, n * 8); memcpy(f->y, p->y, n * 8); memcpy(f->th, p->orientation, n * 8);
+    memcpy(f->z, p->zpos, n * 8); memcpy(f->zs, p->zsigma, n * 8); memcpy(f->w, p->weight, n * 8);
+    if (p->mprob) memcpy(f->mprob, p->mprob, n * 8);
+    if (p->floating) memcpy(f->floating, p->floating, n);
+    if (p->n_contact_points) memcpy(f->ncp, p->n_contact_points, n);
+    double mx = 0;
+    for (uint64_t i = 0; i < n; ++i) if (f->w[i] > mx) mx = f->w[i];
+    f->wexp = dm_weight_exp(mx);
+    return 0;
+}
+
+int or_download(or_filter* f, eslam_particles* p)
+{
+    uint64_t n = f->n;
+    if (p->x) memcpy(p->x, f->x, n * 8);
+    if (p->y) memcpy(p->y, f->y, n * 8);
+    if (p->orientation) memcpy(p->orientation, f->th, n * 8);
+    if (p->zpos) memcpy(p->zpos, f->z, n * 8);
+    if (p->zsigma) memcpy(p->zsigma, f->zs, n * 8);
+    if (p->weight) memcpy(p->weight, f->w, n * 8);
+    if (p->mprob) memcpy(p->mprob, f->mprob, n * 8);
+    if (p->floating) memcpy(p->floating, f->floating, n);
+    if (p->n_contact_points) memcpy(p->n_contact_points, f->ncp, n);
+    return 0;
+}
+
+/* ---- per-step host preparation ------------------------------------------------------------ */
+typedef struct {
+    double yaw, zcomp[4], z_delta, z_var;
+    double mu[3], L[9];
+} or_prep;
+
+static void lower_cholesky(const double S[9], double L[9])
+{
+    memset(L, 0, 9 * sizeof(double));
+    for (int j = 0; j < 3; ++j) {
+        double d = S[j * 3 + j];
+        for (int k = 0; k < j; ++k) d -= L[j * 3 + k] * L[j * 3 + k];
+        double ljj = d > 0.0 ? sqrt(d) : 0.0;
+        L[j * 3 + j] = ljj;
+        for (int i = j + 1; i < 3; ++i) {
+            double s = S[i * 3 + j];
+            for (int k = 0; k < j; ++k) s -= L[i * 3 + k] * L[j * 3 + k];
+            L[i * 3 + j] = ljj > 0.0 ? s / ljj : 0.0;
+        }
+    }
+}
+
+/* src/PoseEstimator.cpp:186-192 */
+static void or_prepare(const eslam_step_input* in, or_prep* p)
+{
+    const double* q = in->body2odometry_rot;
+    p->yaw = get_yaw(q);
+    remove_yaw(q, p->zcomp);
+    double R[9];
+    q_to_mat(q, R);
+    const double* t = in->pose_delta_trans;
+    p->z_delta = (R[6] * t[0] + R[7] * t[1]) + R[8] * t[2];
+    p->z_var = in->position_error_zz * 2.0;
+    for (int i = 0; i < 3; ++i) p->mu[i] = in->sample_mean[i];
+    lower_cholesky(in->sample_cov, p->L);
+}
+
+/* ---- project  src/PoseEstimator.cpp:184-242 --------------------------------------------- */
+int or_project(or_filter* f, const eslam_step_input* in)
+{
+    if (!f->n) return ESLAM_ERR_NOT_INITIALISED;
+    or_prep pp;
+    or_prepare(in, &pp);
+    memcpy(f->zcomp, pp.zcomp, sizeof(pp.zcomp));
+    const eslam_config* c = &f->cfg;
+    double spread = dm_weighting_function(f->max_weight, 0.0, c->spread_threshold, 0.0);
+    int do_spread = spread > 0 && !c->hash_use;
+    const double tf = c->spread_translation_factor * spread;
+    const double rf = c->spread_rotation_factor * spread;
+    const double* L = pp.L;
+    for (uint64_t i = 0; i < f->n; ++i) {
+        double z0, z1, z2, sn0, sn1 = 0, sn2 = 0;
+        dm_philox_ctr d0 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 0);
+        dm_philox_ctr d1 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 1);
+        dm_philox_ctr d2 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 2);
+        dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &z0, &z1);
+        dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &z2, &sn0);
+        /* odometry.getPoseDeltaSample2D(): mu + L z */
+        double dx = pp.mu[0] + L[0] * z0;
+        double dy = pp.mu[1] + (L[3] * z0 + L[4] * z1);
+        double dth = pp.mu[2] + ((L[6] * z0 + L[7] * z1) + L[8] * z2);
+        const double u_slip = dm_u53(d2.v[0], d2.v[1]);
+        if (u_slip < c->slip_factor) dy *= dm_u53(d2.v[2], d2.v[3]);
+        double s, co;
+        dm_sincos(f->th[i], &s, &co);
+        f->x[i] += co * dx - s * dy;
+        f->y[i] += s * dx + co * dy;
+        f->th[i] += dth;
+        if (c->max_yaw_deviation > 0.0) {
+            if (fabs(f->th[i] - pp.yaw) > c->max_yaw_deviation) f->w[i] *= 0.7;
+        }
+        f->z[i] += pp.z_delta;
+        f->zs[i] = sqrt(f->zs[i] * f->zs[i] + pp.z_var);
+        if (do_spread) {
+            dm_philox_ctr d3 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 3);
+            dm_box_muller(dm_u53(d3.v[0], d3.v[1]), dm_u53(d3.v[2], d3.v[3]), &sn1, &sn2);
+            f->x[i] += sn0 * tf + 0.0;
+            f->y[i] += sn1 * tf + 0.0;
+            f->th[i] += sn2 * rf + 0.0;
+        }
+    }
+    f->project_count++;
+    /* hash respawn (useHash) is not modelled here yet (next) */
+    return 0;
+}
+
+/* ---- canonical chunk reduction ------------------------------------------------------------ */
+typedef struct { uint64_t L[4]; uint32_t nan, inf; } or_acc;
+
+static void acc_add_chunk(or_acc* a, double v, int scale)
+{
+    if (v != v) { a->nan = 1; return; }
+    if (!dm_isfinite(v)) { a->inf = 1; return; }
+    uint32_t l[4];
+    dm_fx128_limbs(v, scale, l);
+    for (int j = 0; j < 4; ++j) a->L[j] += l[j];
+}
+
+static double acc_value(const or_acc* a, int scale)
+{
+    if (a->nan) return NAN;
+    if (a->inf) return INFINITY;
+    return dm_limbs_to_double(a->L, scale);
+}
+
+/* the 64-lane xor butterfly of the device, lane 0's result */
+static double butterfly64(double* v)
+{
+    double t[64];
+    for (int o = 32; o >= 1; o >>= 1) {
+        for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ o];
+        memcpy(v, t, sizeof(t));
+    }
+    return v[0];
+}
+
+/* chunk sums of vals[i] restricted to sel(i) (bucket match), accumulated into acc */
+static void chunk_reduce(const double* vals, const uint8_t* bucket, int want_bucket, uint64_t n, uint32_t J,
+                         or_acc* acc, int scale)
+{
+    const uint64_t csz = 64ull * J;
+    for (uint64_t c0 = 0; c0 < n; c0 += csz) {
+        double lane[64];
+        for (int s = 0; s < 64; ++s) {
+            double a = 0.0;
+            for (uint32_t j = 0; j < J; ++j) {
+                uint64_t i = c0 + 64ull * j + (uint64_t)s;
+                if (i >= n) continue;
+                double v = (bucket == NULL || (int)bucket[i] == want_bucket) ? vals[i] : 0.0;
+                a = a + v;
+            }
+            lane[s] = a;
+        }
+        acc_add_chunk(acc, butterfly64(lane), scale);
+    }
+}
+
+/* ---- updateWeights  src/PoseEstimator.cpp:257-352 ----------------------------------------- */
+typedef struct {
+    double fw, f[DM_NBUCKETS];
+    double S, Q;          /* contract: sum of final weights and of their squares */
+} or_phase;
+
+static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase* ph)
+{
+    if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
+    const eslam_config* c = &f->cfg;
+    or_contact_model cm;
+    or_cm_init(&cm, c);
+    or_cm_set_contact_points(&cm, in->n_contacts, in->contacts, in->body2odometry_rot);
+
+    uint64_t total_points = 0, data_particles = 0;
+    double sum_data_weights = 0.0;      /* reference mode */
+    const double last_max_weight = f->max_weight;
+    double maxw = 0;
+    const double me2 = c->measurement_error * c->measurement_error;
+    double* a_val = malloc(f->n * 8);   /* w_A * mprob, contract mode */
+    double* sw_val = malloc(f->n * 8);
+    uint8_t* bucket = malloc(f->n);
+    int err = 0;
+
+    for (uint64_t i = 0; i < f->n; ++i) {
+        double s, co;
+        dm_sincos(f->th[i], &s, &co);
+        const double r22 = (1.0 - co) + co;
+        /* Translation3d(x, y, zPos) * AngleAxisd(theta, UnitZ) */
+        double T[12] = {co, -s, 0.0, f->x[i], s, co, 0.0, f->y[i], 0.0, 0.0, r22, f->z[i]};
+        const double meas_var = f->zs[i] * f->zs[i] + me2;
+        int acc = or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
+        if (acc < 0) { err = ESLAM_ERR_ZERO_MEAS_VAR; break; }
+        sw_val[i] = 0.0;
+        if (acc) {
+            double zvar = f->zs[i] * f->zs[i];
+            or_cm_update_z(&cm, &f->z[i], &zvar);
+            f->zs[i] = sqrt(zvar);
+            const double weight = cm.weight;
+            f->w[i] *= weight;
+            f->mprob[i] = weight;
+            f->floating[i] = 0;
+            maxw = (maxw < weight) ? weight : maxw;
+            data_particles++;
+            const uint64_t found = cm.ncp;
+            sw_val[i] = dm_pow(weight, 1.0 / (double)found);
+            sum_data_weights += sw_val[i];
+            total_points += found;
+        } else {
+            f->floating[i] = 1;
+            f->mprob[i] = 1.0;
+        }
+        f->ncp[i] = (uint8_t)cm.ncp;
+        bucket[i] = (uint8_t)(cm.ncp < DM_NBUCKETS - 1 ? cm.ncp : DM_NBUCKETS - 1);
+        a_val[i] = f->w[i] * f->mprob[i];
+        f->dbg_ncp[i] = cm.ncp;
+        memcpy(&f->dbg_cp[i * ESLAM_MAX_CONTACTS], cm.cp, cm.ncp * sizeof(or_cpoint));
+        f->dbg_zdelta[i] = acc ? cm.zdelta : 0.0;
+        f->dbg_zvar[i] = acc ? cm.zvar : 0.0;
+    }
+    if (err) { free(a_val); free(sw_val); free(bucket); return err; }
+
+    const uint32_t J = dm_chunk_rows(f->n);
+    if (f->sum_mode == OR_SUM_CONTRACT) {
+        or_acc sw = {{0}};
+        chunk_reduce(sw_val, NULL, 0, f->n, J, &sw, DM_FX_SCALE);
+        sum_data_weights = acc_value(&sw, DM_FX_SCALE);
+    }
+    const double floating_weight = data_particles > 0 ? sum_data_weights / (double)data_particles : 1.0;
+    ph->fw = floating_weight;
+    const double base = c->discount_factor * floating_weight;
+    for (int b = 0; b < DM_NBUCKETS; ++b) {
+        uint64_t ncp = (uint64_t)b;                      /* bucket 5 = every n >= 5 */
+        double expo = (double)(uint64_t)(4ull - ncp);    /* size_t arithmetic (Q2) */
+        ph->f[b] = dm_pow(base, expo);
+    }
+    /* phase B  src/PoseEstimator.cpp:332-345 */
+    for (uint64_t i = 0; i < f->n; ++i) {
+        double factor = f->mprob[i] * ph->f[bucket[i]];
+        f->w[i] *= factor;
+    }
+    if (f->sum_mode == OR_SUM_CONTRACT) {
+        double S = 0.0, Q = 0.0;
+        const int sa = DM_FX_SCALE - f->wexp, sb = DM_FX_SCALE - 2 * f->wexp;
+        double* a2 = malloc(f->n * 8);
+        for (uint64_t i = 0; i < f->n; ++i) a2[i] = a_val[i] * a_val[i];
+        for (int b = 0; b < DM_NBUCKETS; ++b) {
+            or_acc A = {{0}}, B = {{0}};
+            chunk_reduce(a_val, bucket, b, f->n, J, &A, sa);
+            chunk_reduce(a2, bucket, b, f->n, J, &B, sb);
+            S = S + ph->f[b] * acc_value(&A, sa);
+            Q = Q + (ph->f[b] * ph->f[b]) * acc_value(&B, sb);
+        }
+        free(a2);
+        ph->S = S;
+        ph->Q = Q;
+    }
+    f->max_weight = maxw;
+    if (total_points == 0) f->max_weight = last_max_weight * c->discount_factor;
+    f->info.data_particles = data_particles;
+    f->info.total_points = total_points;
+    f->info.floating_weight = floating_weight;
+    f->info.max_weight = f->max_weight;
+    free(a_val); free(sw_val); free(bucket);
+    return 0;
+}
+
+/* ---- normalizeWeights  src/ParticleFilter.hpp:46-70 ----------------------------------------- */
+static double normalize_with(or_filter* f, double S, double Q, int have_sums)
+{
+    const uint64_t n = f->n;
+    double effective = 0;
+    if (f->sum_mode == OR_SUM_REFERENCE || !have_sums) {
+        if (f->sum_mode == OR_SUM_REFERENCE) {
+            S = 0;
+            for (uint64_t i = 0; i < n; ++i) S += f->w[i];
+        } else {
+            const uint32_t J = dm_chunk_rows(n);
+            int e = f->wexp;
+            double* w2 = malloc(n * 8);
+            for (uint64_t i = 0; i < n; ++i) w2[i] = f->w[i] * f->w[i];
+            or_acc A = {{0}}, B = {{0}};
+            chunk_reduce(f->w, NULL, 0, n, J, &A, DM_FX_SCALE - e);
+            chunk_reduce(w2, NULL, 0, n, J, &B, DM_FX_SCALE - 2 * e);
+            free(w2);
+            S = acc_value(&A, DM_FX_SCALE - e);
+            Q = acc_value(&B, DM_FX_SCALE - 2 * e);
+        }
+    }
+    f->info.weight_sum = S;
+    f->info.uniform_reset = 0;
+    if (S <= 0.0) {
+        f->info.uniform_reset = 1;
+        for (uint64_t i = 0; i < n; ++i) {
+            double* w = &f->w[i];
+            *w = 1.0 / (double)n;
+            effective += *w * *w;
+        }
+        if (f->sum_mode == OR_SUM_CONTRACT) effective = 1.0 / (double)n;   /* eff := N */
+    } else {
+        for (uint64_t i = 0; i < n; ++i) {
+            f->w[i] /= S;
+            effective += f->w[i] * f->w[i];
+        }
+        if (f->sum_mode == OR_SUM_CONTRACT) effective = Q / (S * S);
+    }
+    f->wexp = 1;
+    return 1.0 / effective;
+}
+
+double or_normalize_weights(or_filter* f) { return normalize_with(f, 0, 0, 0); }
+
+double or_get_weights_sum(or_filter* f)
+{
+    if (f->sum_mode == OR_SUM_REFERENCE) {
+        double s = 0;
+        for (uint64_t i = 0; i < f->n; ++i) s += f->w[i];
+        return s;
+    }
+    or_acc A = {{0}};
+    chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(f->n), &A, DM_FX_SCALE - f->wexp);
+    return acc_value(&A, DM_FX_SCALE - f->wexp);
+}
+
+/* ---- resample_stratified  src/ParticleFilter.hpp:85-108 ------------------------------------ */
+static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
+{
+    double *nx = malloc(samples * 8), *ny = malloc(samples * 8), *nt = malloc(samples * 8), *nz = malloc(samples * 8),
+           *ns = malloc(samples * 8), *nw = malloc(samples * 8), *nm = malloc(samples * 8);
+    uint8_t *nf = malloc(samples), *nc = malloc(samples);
+    for (uint64_t k = 0; k < samples; ++k) {
+        uint32_t i = anc[k];
+        nx[k] = f->x[i]; ny[k] = f->y[i]; nt[k] = f->th[i]; nz[k] = f->z[i]; ns[k] = f->zs[i];
+        nw[k] = f->w[i]; nm[k] = f->mprob[i]; nf[k] = f->floating[i]; nc[k] = f->ncp[i];
+    }
+    free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob); free(f->floating); free(f->ncp);
+    f->x = nx; f->y = ny; f->th = nt; f->z = nz; f->zs = ns; f->w = nw; f->mprob = nm; f->floating = nf; f->ncp = nc;
+}
+
+/* shift: fixed-point shift of the contract-mode cumulative sum (device ctl->scan_shift) */
+static void resample_stratified(or_filter* f, uint64_t samples, int shift)
+{
+    const uint64_t n = f->n;
+    uint32_t* anc = f->anc;
+    uint64_t overruns = 0;
+    uint64_t idx = 0;
+    if (f->sum_mode == OR_SUM_REFERENCE) {
+        double sum_w = f->w[idx];
+        for (uint64_t k = 0; k < samples; ++k) {
+            f->minstd = dm_minstd_next(f->minstd);
+            double sum_r = ((double)k + dm_minstd_uniform(f->minstd)) / (double)samples;
+            while (sum_w < sum_r) {
+                if (idx + 1 >= n) { overruns++; break; }   /* Q5: clamp instead of UB */
+                ++idx;
+                sum_w += f->w[idx];
+            }
+            anc[k] = (uint32_t)idx;
+        }
+    } else {
+        uint64_t sum_w = dm_fx_shift(f->w[idx], shift);
+        for (uint64_t k = 0; k < samples; ++k) {
+            f->minstd = dm_minstd_next(f->minstd);
+            double sum_r = ((double)k + dm_minstd_uniform(f->minstd)) / (double)samples;
+            uint64_t t = dm_fx_shift(sum_r, shift);
+            while (sum_w < t) {
+                if (idx + 1 >= n) { overruns++; break; }
+                ++idx;
+                sum_w += dm_fx_shift(f->w[idx], shift);
+            }
+            anc[k] = (uint32_t)idx;
+        }
+    }
+    f->info.resample_overruns = overruns;
+    gather(f, anc, samples);
+    f->has_anc = 1;
+}
+
+/* standalone ParticleFilter::resample() on the weights as they are: the contract scales
+ * the cumulative sum by the exact weight sum's exponent (device FIN_RESAMPLE)          */
+void or_resample(or_filter* f)
+{
+    int shift = 60;
+    if (f->sum_mode == OR_SUM_CONTRACT) {
+        or_acc A = {{0}};
+        chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(f->n), &A, DM_FX_SCALE - f->wexp);
+        shift = 61 - (dm_weight_exp(acc_value(&A, DM_FX_SCALE - f->wexp)) + 1);
+    }
+    resample_stratified(f, f->n, shift);
+}
+
+/* src/ParticleFilter.hpp:120-148 (not used by PoseEstimator; weights reset to 1/N) */
+void or_resample_multinomial(or_filter* f, uint64_t samples)
+{
+    uint32_t* anc = malloc(samples * 4);
+    uint64_t m = 0;
+    for (uint64_t k = 0; k < samples; ++k) {
+        f->minstd = dm_minstd_next(f->minstd);
+        double r = dm_minstd_uniform(f->minstd);
+        double sum = 0;
+        for (uint64_t i = 0; i < f->n; ++i) {
+            sum += f->w[i];
+            if (r <= sum) { anc[m++] = (uint32_t)i; break; }
+        }
+    }
+    gather(f, anc, m);
+    f->n = m;
+    for (uint64_t i = 0; i < m; ++i) f->w[i] = 1.0 / (double)m;
+    free(anc);
+}
+
+/* ---- PoseEstimator::update  src/PoseEstimator.cpp:244-255 ---------------------------------- */
+int or_update(or_filter* f, const eslam_step_input* in)
+{
+    if (!f->n) return ESLAM_ERR_NOT_INITIALISED;
+    or_phase ph;
+    memset(&ph, 0, sizeof(ph));
+    int rc = or_update_weights(f, in, &ph);
+    if (rc) return rc;
+    double eff = normalize_with(f, ph.S, ph.Q, 1);
+    f->info.effective = eff;
+    f->info.resampled = 0;
+    f->info.resample_overruns = 0;
+    if (eff < (double)f->cfg.min_effective) {
+        resample_stratified(f, f->n, 60);
+        f->info.resampled = 1;
+    }
+    f->info.update_count++;
+    return 0;
+}
+
+/* ---- EmbodiedSlamFilter::update(body2odometry, bs, ltc)  src/EmbodiedSlamFilter.cpp:353-369 */
+int or_step(or_filter* f, const eslam_step_input* in, int* updated)
+{
+    int rc = or_project(f, in);
+    if (rc) return rc;
+    int gate = update_threshold_test(f->cfg.measurement_threshold_distance, f->cfg.measurement_threshold_angle,
+                                     f->ud_pose, in->body2odometry_rot, in->body2odometry_trans);
+    if (gate || in->ltc_count > 0) {
+        rc = or_update(f, in);
+        if (rc) return rc;
+        double R[9];
+        q_to_mat(in->body2odometry_rot, R);
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) f->ud_pose[r * 4 + c] = R[r * 3 + c];
+            f->ud_pose[r * 4 + 3] = in->body2odometry_trans[r];
+        }
+        if (updated) *updated = 1;
+    } else if (updated) {
+        *updated = 0;
+    }
+    return 0;
+}
+
+int or_last_info(or_filter* f, eslam_update_info* info) { *info = f->info; return 0; }
+
+/* src/ParticleFilter.hpp:160-173 (first maximum, strict >) */
+uint64_t or_best_index(or_filter* f)
+{
+    uint64_t index = 0;
+    double weight = -INFINITY;
+    for (uint64_t i = 0; i < f->n; ++i)
+        if (f->w[i] > weight) { index = i; weight = f->w[i]; }
+    return index;
+}
+
+/* PoseEstimator::getCentroid  src/PoseEstimator.cpp:354-383 (reference arithmetic) */
+void or_get_centroid(or_filter* f, double position[3], double q[4])
+{
+    or_normalize_weights(f);
+    double mx = 0, my = 0, mo = 0, zm = 0, sw = 0;
+    for (uint64_t i = 0; i < f->n; ++i) {
+        mx += f->x[i] * f->w[i];
+        my += f->y[i] * f->w[i];
+        mo += f->th[i] * f->w[i];
+        zm += f->z[i] * f->w[i];
+        sw += f->w[i];
+    }
+    mx /= sw; my /= sw; mo /= sw; zm /= sw;
+    position[0] = mx; position[1] = my; position[2] = zm;
+    double a[4];
+    q_from_yaw(mo, a);
+    q_mul(a, f->zcomp, q);
+}
+
+int or_get_ancestors(or_filter* f, uint32_t* out, uint64_t n)
+{
+    if (!f->has_anc) return ESLAM_ERR_INVALID_ARG;
+    memcpy(out, f->anc, (n < f->n ? n : f->n) * 4);
+    return 0;
+}
+
+void or_get_rng_state(or_filter* f, eslam_rng_state* st)
+{
+    memset(st, 0, sizeof(*st));
+    st->minstd_x = f->minstd;
+    st->project_count = f->project_count;
+    st->init_count = f->init_count;
+    st->hash_count = f->hash_count;
+    st->max_weight = f->max_weight;
+    memcpy(st->ud_pose, f->ud_pose, sizeof(f->ud_pose));
+}
+
+void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
+{
+    f->minstd = st->minstd_x;
+    f->project_count = st->project_count;
+    f->init_count = st->init_count;
+    f->hash_count = st->hash_count;
+    f->max_weight = st->max_weight;
+    memcpy(f->ud_pose, st->ud_pose, sizeof(f->ud_pose));
+}
+
+int or_get_debug(or_filter* f, uint32_t* ncp, or_cpoint* cp, double* zdelta, double* zvar)
+{
+    uint64_t n = f->n;
+    if (ncp) memcpy(ncp, f->dbg_ncp, n * 4);
+    if (cp) memcpy(cp, f->dbg_cp, n * ESLAM_MAX_CONTACTS * sizeof(or_cpoint));
+    if (zdelta) memcpy(zdelta, f->dbg_zdelta, n * 8);
+    if (zvar) memcpy(zvar, f->dbg_zvar, n * 8);
+    return 0;
+}
+
+/* ---- detmath wrappers --------------------------------------------------------------------- */
+double or_dm(int fn, double x, double y)
+{
+    double s, c;
+    switch (fn) {
+    case 0: return dm_exp(x);
+    case 1: return dm_log(x);
+    case 2: dm_sincos(x, &s, &c); return s;
+    case 3: dm_sincos(x, &s, &c); return c;
+    case 4: return dm_erfc(x);
+    case 5: return dm_sqrt(x);
+    case 6: return x / y;
+    case 7: return dm_normal_pdf_cdf_ratio(x, y);
+    case 8: return dm_pow(x, y);
+    case 9: { uint64_t v = dm_fx61(x); return dm_from_bits(v); }
+    case 10: return dm_erfcx_pos(x);
+    case 11: return dm_ldexp(x, (int)y);
+    case 12: return dm_weighting_function(x, 0.0, y, 0.0);
+    default: return NAN;
+    }
+}
+
+void or_dm_philox(uint64_t seed, uint32_t stream, uint64_t ev, uint64_t gidx, uint32_t call, uint32_t out[4])
+{
+    dm_philox_ctr c = dm_draw(seed, stream, ev, gidx, call);
+    memcpy(out, c.v, 16);
+}
+
+void or_dm_philox_raw(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4])
+{
+    dm_philox_ctr c;
+    memcpy(c.v, ctr, 16);
+    c = dm_philox4x32_10(c, k0, k1);
+    memcpy(out, c.v, 16);
+}
+
+uint32_t or_dm_minstd_jump(uint32_t x, uint64_t n) { return dm_mulmod31(dm_minstd_pow(n), x); }
+double or_dm_limbs_to_double(const uint64_t L[4], int scale) { return dm_limbs_to_double(L, scale); }
+void or_dm_fx128(double v, int scale, uint32_t limbs[4]) { dm_fx128_limbs(v, scale, limbs); }

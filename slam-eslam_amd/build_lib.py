@@ -1,0 +1,59 @@
+"""Build libeslam_gpu.so (gfx950) in-tree with hipcc -- no cmake, no JIT cache.
+
+    python slam-eslam_amd/build_lib.py            # incremental
+    python slam-eslam_amd/build_lib.py --force
+
+The library is the product: HIP kernels + the C ABI of include/eslam_gpu.h.
+-ffp-contract=off keeps device and host arithmetic bit-identical to the CPU oracle;
+Machine-LICM is disabled because it hoists the ~150 fp64 polynomial constants of the
+contact model out of the particle loop and drives the kernel to 256 VGPRs / occupancy 1.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "lib")
+LIB = os.path.join(OUT_DIR, "libeslam_gpu.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("ESLAM_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["eslam_kernels.hip", "eslam_ctx.hip"]
+HEADERS = [os.path.join(CSRC, "eslam_internal.h"), os.path.join(ROOT, "include", "eslam_gpu.h"),
+           os.path.join(ROOT, "include", "eslam_detmath.h")]
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+         "-mfma", "-mllvm", "-disable-machine-licm", "-Wall", "-Wno-unused-result", "-Wno-unused-function",
+         f"-I{os.path.join(ROOT, 'include')}"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OUT_DIR, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OUT_DIR, src + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [path] + HEADERS):
+            cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+    if force or _stale(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

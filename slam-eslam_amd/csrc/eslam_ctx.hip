@@ -1,0 +1,874 @@
+// eslam_ctx.hip -- host side of libeslam_gpu: the C ABI of include/eslam_gpu.h.
+//
+// Per-step host work is O(1): the reference's per-step scalar preparation
+// (src/PoseEstimator.cpp:186-194: yaw, removeYaw, the odometry z delta and variance,
+// the sampler's Cholesky factor; src/ContactModel.cpp:21-41: the yaw-compensated feet) and
+// the EmbodiedSlamFilter update gate (src/EmbodiedSlamFilter.cpp:360).  Everything that
+// touches particles runs on the GPU; the resample decision is taken on the device, so a
+// step is four asynchronous launches with no host round trip.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "eslam_internal.h"
+
+using namespace eslam_dev;
+
+extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
+                                                  const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
+                                                  hipStream_t stream);
+extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
+                                                hipStream_t stream);
+extern "C" hipError_t eslam_launch_finalize(Shard* shards, Ctl* ctl, const FinParams* fp, hipStream_t stream);
+extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
+                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream);
+extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint32_t* marks,
+                                                   const uint32_t* tile_first, uint64_t* status, uint32_t* anc,
+                                                   uint32_t record, uint32_t aux, hipStream_t stream);
+extern "C" hipError_t eslam_launch_init_gaussian(DevState s0, uint64_t n, uint64_t gbase, uint64_t seed, uint64_t ev,
+                                                 const double mu[3], const double sigma[3], double zpos, double zsigma,
+                                                 hipStream_t stream);
+extern "C" hipError_t eslam_launch_selftest_math(int fn, const double* x, const double* y, double* out, uint64_t n,
+                                                 hipStream_t stream);
+extern "C" hipError_t eslam_launch_best_index(DevState s0, DevState s1, uint64_t n, Ctl* ctl, uint64_t* out2,
+                                              hipStream_t stream);
+extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, double* out,
+                                            hipStream_t stream);
+
+// ---------------------------------------------------------------------------------------
+// small Eigen / base-types restatements (host, per step)
+// ---------------------------------------------------------------------------------------
+namespace {
+
+void q_to_mat(const double q[4], double R[9])          // QuaternionBase::toRotationMatrix
+{
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+    R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+void q_mul(const double a[4], const double b[4], double r[4])
+{
+    const double w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    const double x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    const double y = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
+    const double z = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
+    r[0] = w; r[1] = x; r[2] = y; r[3] = z;
+}
+
+void q_from_yaw(double angle, double q[4])              // Quaternion(AngleAxis(angle, UnitZ))
+{
+    const double ha = 0.5 * angle;
+    q[0] = cos(ha);
+    const double s = sin(ha);
+    q[1] = s * 0.0; q[2] = s * 0.0; q[3] = s * 1.0;
+}
+
+void q_rotate(const double q[4], const double v[3], double out[3])   // _transformVector
+{
+    const double qx = q[1], qy = q[2], qz = q[3], w = q[0];
+    double uv[3] = {qy * v[2] - qz * v[1], qz * v[0] - qx * v[2], qx * v[1] - qy * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const double c[3] = {qy * uv[2] - qz * uv[1], qz * uv[0] - qx * uv[2], qx * uv[1] - qy * uv[0]};
+    out[0] = (v[0] + w * uv[0]) + c[0];
+    out[1] = (v[1] + w * uv[1]) + c[1];
+    out[2] = (v[2] + w * uv[2]) + c[2];
+}
+
+double get_yaw(const double q[4])                        // base::getYaw (getEuler()[0])
+{
+    double R[9];
+    q_to_mat(q, R);
+    const double x = sqrt(R[8] * R[8] + R[7] * R[7]);
+    return x > 1e-12 ? atan2(R[3], R[0]) : 0.0;
+}
+
+void remove_yaw(const double q[4], double out[4])       // base::removeYaw
+{
+    double a[4];
+    q_from_yaw(-get_yaw(q), a);
+    q_mul(a, q, out);
+}
+
+void q_from_mat(const double m[9], double q[4])          // Eigen quaternion from 3x3
+{
+    double t = m[0] + m[4] + m[8];
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[0] = 0.5 * t;
+        t = 0.5 / t;
+        q[1] = (m[7] - m[5]) * t;
+        q[2] = (m[2] - m[6]) * t;
+        q[3] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+        double v[3];
+        v[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        v[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        v[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+        q[1] = v[0]; q[2] = v[1]; q[3] = v[2];
+    }
+}
+
+// UpdateThreshold::test(udPose.inverse() * body2odometry)  src/Configuration.hpp:18-26 (Q6)
+bool update_gate(double thr_distance, double thr_angle, const double ud[12], const double q_b[4], const double t_b[3])
+{
+    double Rb[9];
+    q_to_mat(q_b, Rb);
+    const double Ri[9] = {ud[0], ud[4], ud[8], ud[1], ud[5], ud[9], ud[2], ud[6], ud[10]};
+    double ti[3], L[9], t[3];
+    for (int r = 0; r < 3; ++r) ti[r] = -((Ri[r * 3 + 0] * ud[3] + Ri[r * 3 + 1] * ud[7]) + Ri[r * 3 + 2] * ud[11]);
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c)
+            L[r * 3 + c] = (Ri[r * 3 + 0] * Rb[0 * 3 + c] + Ri[r * 3 + 1] * Rb[1 * 3 + c]) + Ri[r * 3 + 2] * Rb[2 * 3 + c];
+        t[r] = ((Ri[r * 3 + 0] * t_b[0] + Ri[r * 3 + 1] * t_b[1]) + Ri[r * 3 + 2] * t_b[2]) + ti[r];
+    }
+    double q[4];
+    q_from_mat(L, q);
+    const double n = sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double angle = n != 0.0 ? 2.0 * atan2(n, fabs(q[0])) : 0.0;
+    const double dist = sqrt((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]);
+    return angle > thr_distance || dist > thr_angle;
+}
+
+void lower_cholesky(const double S[9], double L[9])
+{
+    memset(L, 0, 9 * sizeof(double));
+    for (int j = 0; j < 3; ++j) {
+        double d = S[j * 3 + j];
+        for (int k = 0; k < j; ++k) d -= L[j * 3 + k] * L[j * 3 + k];
+        const double ljj = d > 0.0 ? sqrt(d) : 0.0;
+        L[j * 3 + j] = ljj;
+        for (int i = j + 1; i < 3; ++i) {
+            double s = S[i * 3 + j];
+            for (int k = 0; k < j; ++k) s -= L[i * 3 + k] * L[j * 3 + k];
+            L[i * 3 + j] = ljj > 0.0 ? s / ljj : 0.0;
+        }
+    }
+}
+
+void set_translation_pose(double ud[12], double x, double y, double z)
+{
+    memset(ud, 0, 12 * sizeof(double));
+    ud[0] = ud[5] = ud[10] = 1.0;
+    ud[3] = x; ud[7] = y; ud[11] = z;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------
+struct eslam_ctx {
+    eslam_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // particles
+    uint64_t n = 0, cap = 0;
+    uint64_t gbase = 0, n_global = 0;
+    DevState st[2] = {};
+    void* state_mem = nullptr;
+    uint32_t* marks = nullptr;
+    uint32_t* tile_first = nullptr;
+    uint64_t* status = nullptr;
+    uint32_t* anc = nullptr;
+    bool has_anc = false;
+    // statistics and control
+    Shard* shards = nullptr;
+    Ctl* ctl = nullptr;
+    Ctl* ctl_host = nullptr;    // pinned
+    uint32_t* jump = nullptr;
+    double* scratch = nullptr;  // small device scratch (centroid, best index)
+    double* scratch_host = nullptr;
+    // map
+    bool has_map = false;
+    MapView map = {};
+    uint32_t* d_cells = nullptr;
+    float2* d_patch = nullptr;
+    float* d_height = nullptr;
+    uint32_t maxp = 4;
+    // host-side filter state
+    uint64_t proj_event = 0, init_event = 0, hash_event = 0;
+    double ud_pose[12];
+    double zcomp[4] = {1, 0, 0, 0};
+    // diagnostics
+    std::string err;
+    bool timing = false;
+    hipEvent_t ev[5] = {};
+    eslam_kernel_times times = {};
+};
+
+#define HIPCHK(ctx, expr)                                                                    \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                  \
+            return ESLAM_ERR_HIP;                                                            \
+        }                                                                                    \
+    } while (0)
+
+static int fail(eslam_ctx* ctx, int code, const char* msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+extern "C" int eslam_gpu_abi_version(void) { return ESLAM_ABI_VERSION; }
+
+extern "C" void eslam_config_default(eslam_config* c)
+{
+    memset(c, 0, sizeof(*c));
+    c->seed = 42;
+    c->particle_count = 250;
+    c->min_effective = 50;
+    c->initial_rotation_error[2] = 0.1;
+    c->initial_translation_error[0] = 0.1;
+    c->initial_translation_error[1] = 0.1;
+    c->initial_translation_error[2] = 1.0;
+    c->measurement_error = 0.1;
+    c->discount_factor = 0.9;
+    c->spread_threshold = 0.9;
+    c->spread_translation_factor = 0.1;
+    c->spread_rotation_factor = 0.05;
+    c->slip_factor = 0.05;
+    c->max_yaw_deviation = 15 * M_PI / 180.0;
+    c->measurement_threshold_distance = 0.1;
+    c->measurement_threshold_angle = 10 * M_PI / 180.0;
+    c->use_slip_update = 0;
+    c->use_shape_update = 1;
+    c->min_contacts = 3;
+    c->contact_likelihood_correction = 0.33;
+    c->contact_point_radius = 0.01;
+    c->hash_use = 0;
+    c->hash_period = 10;
+    c->hash_percentage = 0.05;
+    c->hash_avg_factor = 0.1;
+    c->hash_slope_bins = 20;
+    c->hash_angular_steps = 16;
+    c->log_debug = 0;
+    c->flags = 0;
+}
+
+extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+static int read_ctl(eslam_ctx* ctx)
+{
+    HIPCHK(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return ESLAM_OK;
+}
+
+static int write_ctl(eslam_ctx* ctx)
+{
+    HIPCHK(ctx, hipMemcpyAsync(ctx->ctl, ctx->ctl_host, sizeof(Ctl), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx** out)
+{
+    if (!cfg || !out) return ESLAM_ERR_INVALID_ARG;
+    *out = nullptr;
+    eslam_ctx* ctx = new eslam_ctx();
+    ctx->cfg = *cfg;
+    ctx->device = device;
+    set_translation_pose(ctx->ud_pose, 1000, 0, 0);
+    int rc = ESLAM_OK;
+    do {
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) { ctx->err = std::string("hipSetDevice: ") + hipGetErrorString(e); rc = ESLAM_ERR_HIP; break; }
+        if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { rc = fail(ctx, ESLAM_ERR_HIP, "stream"); break; }
+        ctx->own_stream = true;
+        if (hipMalloc(&ctx->shards, sizeof(Shard) * kNShard) != hipSuccess ||
+            hipMalloc(&ctx->ctl, sizeof(Ctl)) != hipSuccess ||
+            hipHostMalloc(&ctx->ctl_host, sizeof(Ctl)) != hipSuccess ||
+            hipMalloc(&ctx->jump, sizeof(uint32_t) * (2048 + 2048 + 1024)) != hipSuccess ||
+            hipMalloc(&ctx->scratch, 4096) != hipSuccess ||
+            hipHostMalloc(&ctx->scratch_host, 4096) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "device allocation failed");
+            break;
+        }
+        hipMemset(ctx->shards, 0, sizeof(Shard) * kNShard);
+        memset(ctx->ctl_host, 0, sizeof(Ctl));
+        ctx->ctl_host->minstd = dm_minstd_seed(cfg->seed);     // ParticleFilter(seed)
+        ctx->ctl_host->max_weight = 0.0;                         // PoseEstimator ctor
+        ctx->ctl_host->wexp = 1;
+        ctx->ctl_host->scan_shift = 60;
+        hipMemcpy(ctx->ctl, ctx->ctl_host, sizeof(Ctl), hipMemcpyHostToDevice);
+        // minstd jump tables
+        std::vector<uint32_t> jt(2048 + 2048 + 1024);
+        uint32_t a = 1;
+        for (int i = 0; i < 2048; ++i) { jt[i] = a; a = dm_mulmod31(a, DM_MINSTD_A); }
+        const uint32_t a11 = dm_minstd_pow(1ull << 11);
+        a = 1;
+        for (int i = 0; i < 2048; ++i) { jt[2048 + i] = a; a = dm_mulmod31(a, a11); }
+        const uint32_t a22 = dm_minstd_pow(1ull << 22);
+        a = 1;
+        for (int i = 0; i < 1024; ++i) { jt[4096 + i] = a; a = dm_mulmod31(a, a22); }
+        hipMemcpy(ctx->jump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice);
+        for (auto& e2 : ctx->ev) hipEventCreate(&e2);
+        if (hipDeviceSynchronize() != hipSuccess) { rc = fail(ctx, ESLAM_ERR_HIP, "device synchronize"); break; }
+    } while (0);
+    if (rc != ESLAM_OK) {
+        fprintf(stderr, "eslam_gpu_create: %s\n", ctx->err.c_str());
+        eslam_gpu_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return ESLAM_OK;
+}
+
+static void free_particles(eslam_ctx* ctx)
+{
+    hipFree(ctx->state_mem); ctx->state_mem = nullptr;
+    hipFree(ctx->marks); ctx->marks = nullptr;
+    hipFree(ctx->tile_first); ctx->tile_first = nullptr;
+    hipFree(ctx->status); ctx->status = nullptr;
+    hipFree(ctx->anc); ctx->anc = nullptr;
+    ctx->n = ctx->cap = 0;
+    ctx->has_anc = false;
+}
+
+static void free_map(eslam_ctx* ctx)
+{
+    hipFree(ctx->d_cells); hipFree(ctx->d_patch); hipFree(ctx->d_height);
+    ctx->d_cells = nullptr; ctx->d_patch = nullptr; ctx->d_height = nullptr;
+    ctx->has_map = false;
+}
+
+extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
+{
+    if (!ctx) return;
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    free_particles(ctx);
+    free_map(ctx);
+    hipFree(ctx->shards); hipFree(ctx->ctl); hipHostFree(ctx->ctl_host); hipFree(ctx->jump);
+    hipFree(ctx->scratch); hipHostFree(ctx->scratch_host);
+    for (auto& e : ctx->ev) if (e) hipEventDestroy(e);
+    if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" int eslam_gpu_set_stream(eslam_ctx* ctx, void* s)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (s) {
+        if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+        ctx->stream = (hipStream_t)s;
+        ctx->own_stream = false;
+    }
+    return ESLAM_OK;
+}
+
+// 256-byte aligned SoA carve-out: 7 fp64 arrays + 1 byte array, two copies
+static int alloc_particles(eslam_ctx* ctx, uint64_t n)
+{
+    if (n >= (1ull << 32) - 1) return fail(ctx, ESLAM_ERR_INVALID_ARG, "particle count must be < 2^32 - 1");
+    free_particles(ctx);
+    const uint64_t cap = n ? n : 1;
+    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+    const uint64_t per = 7 * al(cap * 8) + al(cap);
+    HIPCHK(ctx, hipMalloc(&ctx->state_mem, 2 * per));
+    for (int k = 0; k < 2; ++k) {
+        char* p = (char*)ctx->state_mem + k * per;
+        DevState& s = ctx->st[k];
+        double** f[7] = {&s.x, &s.y, &s.th, &s.z, &s.zs, &s.w, &s.mprob};
+        for (int j = 0; j < 7; ++j) { *f[j] = (double*)p; p += al(cap * 8); }
+        s.flags = (uint8_t*)p;
+    }
+    const uint64_t ntiles = (cap + kScanTile - 1) / kScanTile;
+    HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->tile_first, ntiles * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->status, ntiles * 8));
+    HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
+    HIPCHK(ctx, hipMemset(ctx->status, 0, ntiles * 8));
+    if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
+    ctx->n = n;
+    ctx->cap = cap;
+    ctx->n_global = n;
+    ctx->gbase = 0;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
+{
+    if (!ctx || !g || !g->cell_start || !g->patch_mean || !g->patch_stdev) return ESLAM_ERR_INVALID_ARG;
+    if (g->width == 0 || g->height == 0) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
+    const uint64_t ncell = (uint64_t)g->width * g->height;
+    if ((uint64_t)g->cell_start[ncell] != g->n_patches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "cell_start[width*height] != n_patches");
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    free_map(ctx);
+    const uint64_t np = g->n_patches ? g->n_patches : 1;
+    std::vector<float2> patch(np);
+    for (uint64_t k = 0; k < g->n_patches; ++k) patch[k] = make_float2(g->patch_mean[k], g->patch_stdev[k]);
+    HIPCHK(ctx, hipMalloc(&ctx->d_cells, (ncell + 1) * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->d_patch, np * sizeof(float2)));
+    HIPCHK(ctx, hipMemcpy(ctx->d_cells, g->cell_start, (ncell + 1) * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->d_patch, patch.data(), np * sizeof(float2), hipMemcpyHostToDevice));
+    if (g->patch_height) {
+        HIPCHK(ctx, hipMalloc(&ctx->d_height, np * 4));
+        HIPCHK(ctx, hipMemcpy(ctx->d_height, g->patch_height, g->n_patches * 4, hipMemcpyHostToDevice));
+    }
+    MapView& m = ctx->map;
+    m.cell_start = ctx->d_cells;
+    m.patch = ctx->d_patch;
+    m.height = ctx->d_height;
+    m.width = g->width;
+    m.height_cells = g->height;
+    m.scale_x = g->scale_x;
+    m.scale_y = g->scale_y;
+    m.offset_x = g->offset_x;
+    m.offset_y = g->offset_y;
+    memcpy(m.g2l, g->global2local, sizeof(m.g2l));
+    ctx->has_map = true;
+    return ESLAM_OK;
+}
+
+static int reset_ctl_for_new_particles(eslam_ctx* ctx, int wexp)
+{
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    ctx->ctl_host->base = 0;
+    ctx->ctl_host->flip = 0;
+    ctx->ctl_host->wexp = wexp;
+    ctx->has_anc = false;
+    return write_ctl(ctx);
+}
+
+extern "C" int eslam_gpu_init_gaussian(eslam_ctx* ctx, uint64_t n, const double mu[3], const double sigma[3], double zpos,
+                                       double zsigma)
+{
+    if (!ctx || !mu || !sigma) return ESLAM_ERR_INVALID_ARG;
+    int rc = alloc_particles(ctx, n);
+    if (rc) return rc;
+    rc = reset_ctl_for_new_particles(ctx, 1);
+    if (rc) return rc;
+    HIPCHK(ctx, eslam_launch_init_gaussian(ctx->st[0], n, ctx->gbase, ctx->cfg.seed, ctx->init_event, mu, sigma, zpos, zsigma,
+                                           ctx->stream));
+    ctx->init_event++;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_init_pose(eslam_ctx* ctx, const double pos[3], const double q[4])
+{
+    if (!ctx || !pos || !q) return ESLAM_ERR_INVALID_ARG;
+    if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
+    double R[9];
+    q_to_mat(q, R);
+    double angle = atan2(R[3], R[0]);          // eulerAngles(2,1,0)[0], folded into [0, pi]
+    if (angle < 0.0) angle += M_PI;
+    const double mu[3] = {pos[0], pos[1], angle};
+    const double sg[3] = {ctx->cfg.initial_translation_error[0], ctx->cfg.initial_translation_error[1],
+                          ctx->cfg.initial_rotation_error[2]};
+    const int rc = eslam_gpu_init_gaussian(ctx, ctx->cfg.particle_count, mu, sg, pos[2], ctx->cfg.initial_translation_error[2] + 1e-3);
+    set_translation_pose(ctx->ud_pose, 1000, 0, 0);
+    return rc;
+}
+
+extern "C" int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n)
+{
+    if (!ctx || !n) return ESLAM_ERR_INVALID_ARG;
+    *n = ctx->n;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const eslam_particles* p)
+{
+    if (!ctx || !p || !p->x || !p->y || !p->orientation || !p->zpos || !p->zsigma || !p->weight) return ESLAM_ERR_INVALID_ARG;
+    int rc = alloc_particles(ctx, n);
+    if (rc) return rc;
+    const DevState& s = ctx->st[0];
+    const uint64_t b = n * 8;
+    if (n) {
+        HIPCHK(ctx, hipMemcpy(s.x, p->x, b, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(s.y, p->y, b, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(s.th, p->orientation, b, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(s.z, p->zpos, b, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(s.zs, p->zsigma, b, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(s.w, p->weight, b, hipMemcpyHostToDevice));
+        if (p->mprob) HIPCHK(ctx, hipMemcpy(s.mprob, p->mprob, b, hipMemcpyHostToDevice));
+        else HIPCHK(ctx, hipMemset(s.mprob, 0, b));
+        std::vector<uint8_t> fl(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint8_t f = p->floating ? (p->floating[i] ? 1 : 0) : 1;
+            const uint8_t c = p->n_contact_points ? (p->n_contact_points[i] & 0x7f) : 0;
+            fl[i] = (uint8_t)(c | (f << 7));
+        }
+        HIPCHK(ctx, hipMemcpy(s.flags, fl.data(), n, hipMemcpyHostToDevice));
+    }
+    double mx = 0;
+    for (uint64_t i = 0; i < n; ++i) if (p->weight[i] > mx) mx = p->weight[i];
+    return reset_ctl_for_new_particles(ctx, dm_weight_exp(mx));
+}
+
+extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
+{
+    if (!ctx || !p) return ESLAM_ERR_INVALID_ARG;
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    const DevState& s = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip];
+    const uint64_t n = ctx->n, b = n * 8;
+    if (!n) return ESLAM_OK;
+    if (p->x) HIPCHK(ctx, hipMemcpy(p->x, s.x, b, hipMemcpyDeviceToHost));
+    if (p->y) HIPCHK(ctx, hipMemcpy(p->y, s.y, b, hipMemcpyDeviceToHost));
+    if (p->orientation) HIPCHK(ctx, hipMemcpy(p->orientation, s.th, b, hipMemcpyDeviceToHost));
+    if (p->zpos) HIPCHK(ctx, hipMemcpy(p->zpos, s.z, b, hipMemcpyDeviceToHost));
+    if (p->zsigma) HIPCHK(ctx, hipMemcpy(p->zsigma, s.zs, b, hipMemcpyDeviceToHost));
+    if (p->weight) HIPCHK(ctx, hipMemcpy(p->weight, s.w, b, hipMemcpyDeviceToHost));
+    if (p->mprob) HIPCHK(ctx, hipMemcpy(p->mprob, s.mprob, b, hipMemcpyDeviceToHost));
+    if (p->floating || p->n_contact_points) {
+        std::vector<uint8_t> fl(n);
+        HIPCHK(ctx, hipMemcpy(fl.data(), s.flags, n, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < n; ++i) {
+            if (p->floating) p->floating[i] = fl[i] >> 7;
+            if (p->n_contact_points) p->n_contact_points[i] = fl[i] & 0x7f;
+        }
+    }
+    return ESLAM_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// the hot path
+// ---------------------------------------------------------------------------------------
+static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepParams& p)
+{
+    memset(&p, 0, sizeof(p));
+    const eslam_config& c = ctx->cfg;
+    const double* q = in->body2odometry_rot;
+    // PoseEstimator::project preamble  src/PoseEstimator.cpp:186-194
+    p.yaw = get_yaw(q);
+    double R[9];
+    q_to_mat(q, R);
+    const double* t = in->pose_delta_trans;
+    p.z_delta = (R[6] * t[0] + R[7] * t[1]) + R[8] * t[2];
+    p.z_var = in->position_error_zz * 2.0;
+    for (int i = 0; i < 3; ++i) p.mu[i] = in->sample_mean[i];
+    double L[9];
+    lower_cholesky(in->sample_cov, L);
+    p.L00 = L[0]; p.L10 = L[3]; p.L11 = L[4]; p.L20 = L[6]; p.L21 = L[7]; p.L22 = L[8];
+    p.slip_factor = c.slip_factor;
+    p.max_yaw_dev = c.max_yaw_deviation;
+    p.spread_threshold = c.spread_threshold;
+    p.spread_trans = c.spread_translation_factor;
+    p.spread_rot = c.spread_rotation_factor;
+    p.hash_use = c.hash_use ? 1u : 0u;
+    p.seed = c.seed;
+    // ContactModel::setContactPoints  src/ContactModel.cpp:21-41
+    double yc[4];
+    remove_yaw(q, yc);
+    memcpy(ctx->zcomp, yc, sizeof(yc));
+    const uint32_t m = in->n_contacts < ESLAM_MAX_CONTACTS ? in->n_contacts : ESLAM_MAX_CONTACTS;
+    p.m = m;
+    uint32_t ends = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+        double pos[3];
+        q_rotate(yc, in->contacts[i].position, pos);
+        p.c[i].px = pos[0]; p.c[i].py = pos[1]; p.c[i].pz = pos[2];
+        p.c[i].eval = !((double)in->contacts[i].contact < 0.2) ? 1u : 0u;
+        const int32_t g = in->contacts[i].group_id;
+        p.c[i].end = (g == -1 || i + 1 == m || g != in->contacts[i + 1].group_id) ? 1u : 0u;
+        ends += p.c[i].end;
+    }
+    ctx->maxp = ends;
+    p.me2 = c.measurement_error * c.measurement_error;
+    p.radius = c.contact_point_radius;
+    p.corr = c.contact_likelihood_correction;
+    p.min_contacts = c.min_contacts;
+    p.use_shape = c.use_shape_update ? 1u : 0u;
+    p.use_slip = c.use_slip_update ? 1u : 0u;
+    p.n = ctx->n;
+    p.gbase = ctx->gbase;
+    p.n_global = ctx->n_global;
+    p.J = dm_chunk_rows(ctx->n_global);
+}
+
+static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normalize)
+{
+    ScanParams sp;
+    memset(&sp, 0, sizeof(sp));
+    sp.n = ctx->n;
+    sp.gbase = ctx->gbase;
+    sp.n_global = ctx->n_global;
+    sp.phase_b = phase_b;
+    sp.normalize = normalize;
+    sp.ntiles = (uint32_t)((ctx->n + kScanTile - 1) / kScanTile);
+    return sp;
+}
+
+static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
+{
+    FinParams fp;
+    memset(&fp, 0, sizeof(fp));
+    fp.n_global = ctx->n_global;
+    fp.min_effective = ctx->cfg.min_effective;
+    fp.discount = ctx->cfg.discount_factor;
+    fp.spread_threshold = ctx->cfg.spread_threshold;
+    fp.mode = mode;
+    return fp;
+}
+
+static int run_update_tail(eslam_ctx* ctx, uint32_t mode)
+{
+    const FinParams fp = fin_params(ctx, mode);
+    HIPCHK(ctx, eslam_launch_finalize(ctx->shards, ctx->ctl, &fp, ctx->stream));
+    if (ctx->timing) hipEventRecord(ctx->ev[2], ctx->stream);
+    const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
+    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
+                                            ctx->jump, ctx->stream));
+    if (ctx->timing) hipEventRecord(ctx->ev[3], ctx->stream);
+    const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
+    const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
+    HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->marks, ctx->tile_first, ctx->status,
+                                             ctx->anc, record, aux, ctx->stream));
+    if (ctx->timing) hipEventRecord(ctx->ev[4], ctx->stream);
+    if (record) ctx->has_anc = true;
+    return ESLAM_OK;
+}
+
+static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project, bool weight)
+{
+    if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    if (weight && !ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
+    StepParams p;
+    fill_step_params(ctx, in, p);
+    p.proj_event = ctx->proj_event;
+    if (ctx->timing) hipEventRecord(ctx->ev[0], ctx->stream);
+    HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
+                                            ctx->shards, ctx->stream));
+    if (ctx->timing) hipEventRecord(ctx->ev[1], ctx->stream);
+    if (project) ctx->proj_event++;
+    if (weight) return run_update_tail(ctx, FIN_UPDATE);
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_project(eslam_ctx* ctx, const eslam_step_input* in)
+{
+    if (!ctx || !in) return ESLAM_ERR_INVALID_ARG;
+    return launch_step(ctx, in, true, false);
+}
+
+extern "C" int eslam_gpu_update(eslam_ctx* ctx, const eslam_step_input* in)
+{
+    if (!ctx || !in) return ESLAM_ERR_INVALID_ARG;
+    return launch_step(ctx, in, false, true);
+}
+
+extern "C" int eslam_gpu_step(eslam_ctx* ctx, const eslam_step_input* in, int* updated)
+{
+    if (!ctx || !in) return ESLAM_ERR_INVALID_ARG;
+    const bool gate = update_gate(ctx->cfg.measurement_threshold_distance, ctx->cfg.measurement_threshold_angle, ctx->ud_pose,
+                                  in->body2odometry_rot, in->body2odometry_trans) ||
+                      in->ltc_count > 0;
+    const int rc = launch_step(ctx, in, true, gate);
+    if (rc) return rc;
+    if (gate) {
+        double R[9];
+        q_to_mat(in->body2odometry_rot, R);
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) ctx->ud_pose[r * 4 + c] = R[r * 3 + c];
+            ctx->ud_pose[r * 4 + 3] = in->body2odometry_trans[r];
+        }
+    }
+    if (updated) *updated = gate ? 1 : 0;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    const Ctl& c = *ctx->ctl_host;
+    if (info) {
+        info->effective = c.eff;
+        info->weight_sum = c.S;
+        info->floating_weight = c.fw;
+        info->max_weight = c.max_weight;
+        info->data_particles = c.data_particles;
+        info->total_points = c.total_points;
+        info->resampled = (int32_t)c.resample;
+        info->uniform_reset = (int32_t)c.uniform;
+        info->resample_overruns = c.overruns;
+        info->update_count = c.update_count;
+    }
+    if (ctx->timing) {
+        eslam_kernel_times& t = ctx->times;
+        hipEventElapsedTime(&t.project_weight_ms, ctx->ev[0], ctx->ev[1]);
+        hipEventElapsedTime(&t.finalize_ms, ctx->ev[1], ctx->ev[2]);
+        hipEventElapsedTime(&t.normalize_scan_ms, ctx->ev[2], ctx->ev[3]);
+        hipEventElapsedTime(&t.resample_ms, ctx->ev[3], ctx->ev[4]);
+        hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[4]);
+    }
+    if (c.err & 1ull) {
+        ctx->ctl_host->err = 0;
+        write_ctl(ctx);
+        return fail(ctx, ESLAM_ERR_ZERO_MEAS_VAR, "using a zero measurement variance leads to singularities");
+    }
+    if (c.err & 2ull) return fail(ctx, ESLAM_ERR_HIP, "prefix-sum look-back timed out");
+    return ESLAM_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// ParticleFilter<T> API
+// ---------------------------------------------------------------------------------------
+static int standalone(eslam_ctx* ctx, uint32_t mode)
+{
+    if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    const uint32_t J = dm_chunk_rows(ctx->n_global);
+    HIPCHK(ctx, eslam_launch_weight_stats(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->shards, ctx->stream));
+    if (mode == FIN_SUM) {
+        const FinParams fp = fin_params(ctx, mode);
+        HIPCHK(ctx, eslam_launch_finalize(ctx->shards, ctx->ctl, &fp, ctx->stream));
+        return ESLAM_OK;
+    }
+    return run_update_tail(ctx, mode);
+}
+
+extern "C" int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum)
+{
+    if (!ctx || !sum) return ESLAM_ERR_INVALID_ARG;
+    int rc = standalone(ctx, FIN_SUM);
+    if (rc) return rc;
+    rc = read_ctl(ctx);
+    if (rc) return rc;
+    *sum = ctx->ctl_host->S;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    int rc = standalone(ctx, FIN_NORMALIZE);
+    if (rc) return rc;
+    rc = read_ctl(ctx);
+    if (rc) return rc;
+    if (effective) *effective = ctx->ctl_host->eff;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_resample(eslam_ctx* ctx)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    return standalone(ctx, FIN_RESAMPLE);
+}
+
+extern "C" int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index)
+{
+    if (!ctx || !index) return ESLAM_ERR_INVALID_ARG;
+    if (!ctx->n) { *index = 0; return ESLAM_OK; }
+    uint64_t* out = reinterpret_cast<uint64_t*>(ctx->scratch);
+    HIPCHK(ctx, eslam_launch_best_index(ctx->st[0], ctx->st[1], ctx->n, ctx->ctl, out, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->scratch_host, ctx->scratch, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t* h = reinterpret_cast<const uint64_t*>(ctx->scratch_host);
+    *index = h[1] == ~0ull ? 0 : h[1];
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double orientation[4])
+{
+    if (!ctx || !position || !orientation) return ESLAM_ERR_INVALID_ARG;
+    int rc = eslam_gpu_normalize_weights(ctx, nullptr);     // side effect, Q15
+    if (rc) return rc;
+    const uint32_t J = dm_chunk_rows(ctx->n_global);
+    HIPCHK(ctx, eslam_launch_centroid(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->scratch, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->scratch_host, ctx->scratch, 5 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const double* h = ctx->scratch_host;       // sum x w, y w, theta w, z w, w
+    const double sw = h[4];
+    position[0] = h[0] / sw;
+    position[1] = h[1] / sw;
+    position[2] = h[3] / sw;
+    const double mo = h[2] / sw;
+    double a[4];
+    q_from_yaw(mo, a);
+    q_mul(a, ctx->zcomp, orientation);
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st)
+{
+    if (!ctx || !st) return ESLAM_ERR_INVALID_ARG;
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    memset(st, 0, sizeof(*st));
+    st->minstd_x = ctx->ctl_host->minstd;
+    st->project_count = ctx->proj_event;
+    st->init_count = ctx->init_event;
+    st->hash_count = ctx->hash_event;
+    st->max_weight = ctx->ctl_host->max_weight;
+    memcpy(st->ud_pose, ctx->ud_pose, sizeof(ctx->ud_pose));
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st)
+{
+    if (!ctx || !st) return ESLAM_ERR_INVALID_ARG;
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    ctx->ctl_host->minstd = st->minstd_x;
+    ctx->proj_event = st->project_count;
+    ctx->init_event = st->init_count;
+    ctx->hash_event = st->hash_count;
+    ctx->ctl_host->max_weight = st->max_weight;
+    memcpy(ctx->ud_pose, st->ud_pose, sizeof(ctx->ud_pose));
+    return write_ctl(ctx);
+}
+
+extern "C" int eslam_gpu_get_ancestors(eslam_ctx* ctx, uint32_t* out, uint64_t n)
+{
+    if (!ctx || !out) return ESLAM_ERR_INVALID_ARG;
+    if (!ctx->has_anc || !ctx->anc) return fail(ctx, ESLAM_ERR_INVALID_ARG, "no ancestors recorded (ESLAM_FLAG_RECORD_ANCESTORS)");
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(out, ctx->anc, (n < ctx->n ? n : ctx->n) * 4, hipMemcpyDeviceToHost));
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    ctx->timing = enable != 0;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t)
+{
+    if (!ctx || !t) return ESLAM_ERR_INVALID_ARG;
+    *t = ctx->times;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_selftest_math(int device, int fn, const double* x, const double* y, double* out, uint64_t n)
+{
+    if (hipSetDevice(device) != hipSuccess) return ESLAM_ERR_HIP;
+    double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    const uint64_t b = (n ? n : 1) * 8;
+    if (hipMalloc(&dx, b) != hipSuccess || hipMalloc(&dy, b) != hipSuccess || hipMalloc(&dout, b) != hipSuccess)
+        return ESLAM_ERR_OUT_OF_MEMORY;
+    hipMemcpy(dx, x, n * 8, hipMemcpyHostToDevice);
+    if (y) hipMemcpy(dy, y, n * 8, hipMemcpyHostToDevice);
+    else hipMemset(dy, 0, b);
+    hipError_t e = eslam_launch_selftest_math(fn, dx, dy, dout, n, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
+    hipFree(dx); hipFree(dy); hipFree(dout);
+    return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
+}

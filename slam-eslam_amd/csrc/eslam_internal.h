@@ -1,0 +1,130 @@
+// eslam_internal.h -- shared between the HIP kernels and the host side of libeslam_gpu.
+//
+// Device memory layout (per context, one GPU):
+//   state[2]   SoA fp64 x, y, theta, zpos, zsigma, weight, mprob + uint8 flags
+//              (flags = n_contact_points | floating << 7); double-buffered for resample
+//   marks      uint32 per particle: resample segment starts (particle index + 1)
+//   tile_first uint32 per resample tile: particle covering the tile's first output
+//   status     uint64 per scan tile: decoupled look-back words (2-bit tag | 62-bit value)
+//   shards     NSHARD x Shard: exact fixed-point statistics of the weighting kernel
+//   ctl        Ctl: per-step scalars decided on the device (no host round trip per step)
+//   jump       minstd jump-ahead tables A^(i), A^(i*2^11), A^(i*2^22)
+#pragma once
+#include <stdint.h>
+#include "../../include/eslam_gpu.h"
+#include "../../include/eslam_detmath.h"
+
+namespace eslam_dev {
+
+constexpr int kBlock = 256;              // threads per block (4 waves of 64)
+constexpr int kWaves = kBlock / 64;
+constexpr int kScanItems = 8;            // particles per thread in the scan kernel
+constexpr int kScanTile = kBlock * kScanItems;   // 2048 particles per scan tile
+constexpr int kGatherTile = kScanTile;           // outputs per resample-gather block
+constexpr int kNShard = 16;              // statistics shards (blockIdx % kNShard)
+constexpr int kJumpBits = 11;
+
+// one statistics shard: exact sums as 4 limbs of 32-bit columns (uint64 each)
+struct alignas(128) Shard {
+    uint64_t A[DM_NBUCKETS][4];          // sum over chunks of  w_A * mprob        (per bucket)
+    uint64_t B[DM_NBUCKETS][4];          // sum over chunks of (w_A * mprob)^2     (per bucket)
+    uint64_t SW[4];                      // sum of m^(1/n) over accepted particles
+    uint64_t D, TP;                      // data_particles, total_points
+    uint64_t maxm;                       // bits of max accepted m (non-negative double)
+    uint64_t flags;                      // bit b: A[b] non-finite, bit 8+b: B[b], bit 16: SW; nan in bits 24+
+    uint64_t err;                        // bit 0: zero measurement variance
+    uint64_t pad[7];
+};
+static_assert(sizeof(Shard) % 128 == 0, "shard alignment");
+
+// per-step device-side control block
+struct alignas(128) Ctl {
+    // committed buffer index and pending flip (latest state = base ^ flip)
+    uint32_t base, flip;
+    uint32_t resample;                   // decided by finalize for this update
+    uint32_t uniform;                    // sumWeights <= 0 branch
+    uint32_t mode;                       // finalize mode (see FinMode)
+    uint32_t special;                    // 1: S NaN, 2: S inf
+    int32_t scan_shift;                  // fixed-point shift of the resample cumulative sum
+    int32_t wexp;                        // weight exponent bound for the next weighting
+    double S, Q, eff, fw, max_weight;
+    double f[DM_NBUCKETS];
+    double inv_n;
+    uint32_t minstd;                     // ParticleFilter::rand_gen state
+    uint32_t minstd_start;               // state at the start of the current resample
+    uint64_t tile_counter;               // dynamic tile id of the scan kernel
+    uint64_t overruns;
+    uint64_t data_particles, total_points;
+    uint64_t update_count;
+    uint64_t err;
+    uint64_t pad[4];
+};
+
+enum FinMode : uint32_t {
+    FIN_UPDATE = 0,       // updateWeights statistics -> phase B factors, normalise, maybe resample
+    FIN_NORMALIZE = 1,    // standalone normalizeWeights (weights as they are)
+    FIN_RESAMPLE = 2,     // standalone resample (no normalisation)
+    FIN_SUM = 3,          // getWeightsSum only
+};
+
+struct DevState {
+    double* x; double* y; double* th; double* z; double* zs; double* w; double* mprob;
+    uint8_t* flags;
+};
+
+struct MapView {
+    const uint32_t* cell_start;
+    const float2* patch;                 // (mean, stdev) per patch
+    const float* height;                 // nullable: all horizontal
+    uint32_t width, height_cells;
+    double scale_x, scale_y, offset_x, offset_y;
+    double g2l[12];
+};
+
+struct ContactC {
+    double px, py, pz;                   // yaw-compensated body-frame position
+    uint32_t eval;                       // !(contact < 0.2)
+    uint32_t end;                        // group ends after this contact
+};
+
+struct StepParams {
+    // ---- project (PoseEstimator::project)
+    double yaw, z_delta, z_var;
+    double mu[3];
+    double L00, L10, L11, L20, L21, L22;
+    double slip_factor, max_yaw_dev;
+    double spread_threshold, spread_trans, spread_rot;
+    uint32_t hash_use;
+    uint32_t m;                          // number of contacts
+    uint64_t seed, proj_event;
+    // ---- weighting (updateWeights)
+    double me2, radius, corr;
+    uint64_t min_contacts;
+    uint32_t use_shape, use_slip;
+    // ---- sizes
+    uint64_t n, gbase, n_global;
+    uint32_t J;                          // canonical chunk rows
+    uint32_t pad;
+    ContactC c[ESLAM_MAX_CONTACTS];
+};
+
+struct FinParams {
+    uint64_t n_global;
+    uint64_t min_effective;
+    double discount;
+    double spread_threshold;
+    uint32_t mode;
+    int32_t wexp;                        // scale exponent used by the statistics kernel
+    uint32_t record;                     // 1: write update info
+    uint32_t pad;
+};
+
+struct ScanParams {
+    uint64_t n, gbase, n_global;
+    uint32_t phase_b;                    // apply phase-B factors
+    uint32_t normalize;                  // divide by S
+    uint32_t ntiles;
+    uint32_t pad;
+};
+
+}  // namespace eslam_dev

@@ -1,0 +1,1045 @@
+// eslam_kernels.hip -- gfx950 kernels of the eSLAM per-step particle-filter update.
+//
+// One update of the reference (EmbodiedSlamFilter::update -> PoseEstimator::project +
+// PoseEstimator::update, src/EmbodiedSlamFilter.cpp:353-369) runs as four launches with no
+// host round trip:
+//
+//   k_project_weight  predict (src/PoseEstimator.cpp:196-237) fused with updateWeights
+//                     phase A (src/PoseEstimator.cpp:276-327: ContactModel::evaluatePose,
+//                     evaluateWeight, updateZPositionEstimate + the MLS lookup of
+//                     GridAccess::get) and the exact per-bucket statistics
+//   k_finalize        one block: floating weight, phase-B factors, normalisation sum,
+//                     effective count and the resample decision (src/PoseEstimator.cpp:329,
+//                     src/ParticleFilter.hpp:46-70, src/PoseEstimator.cpp:250)
+//   k_normalize_scan  phase B + normalisation + decoupled look-back prefix sum of the
+//                     fixed-point weights + the stratified-draw segment boundaries
+//                     (src/PoseEstimator.cpp:332-345, src/ParticleFilter.hpp:85-108)
+//   k_resample_gather expand the segments (max-scan) and gather the particle state
+//
+// Everything is wave64: 256-thread blocks, butterfly reductions with __shfl_xor over 64
+// lanes, ballots as 64-bit masks.  All arithmetic goes through include/eslam_detmath.h and
+// the file is compiled with -ffp-contract=off, so results equal the CPU oracle bit for bit.
+#include <hip/hip_runtime.h>
+
+#include "eslam_internal.h"
+
+namespace eslam_dev {
+
+// ---------------------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum_butterfly(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_max_butterfly(double v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        double t = __shfl_xor(v, o, 64);
+        v = (v < t) ? t : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t atomic_load_agent(const uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void atomic_store_agent(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t jump_pow(const uint32_t* __restrict__ jt, uint64_t e)
+{
+    // A^e for e < 2^32 from three tables: A^(i), A^(i*2^11), A^(i*2^22)
+    uint32_t a = jt[e & 2047u];
+    uint32_t b = jt[2048u + ((e >> 11) & 2047u)];
+    uint32_t c = jt[4096u + ((e >> 22) & 1023u)];
+    return dm_mulmod31(dm_mulmod31(a, b), c);
+}
+
+// ---------------------------------------------------------------------------------------
+// GridAccess::get -> MLSMap::getPatch(C_global2local * p, patch, 3.0)  (src/PoseEstimator.hpp:97-105)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool get_patch(const MapView& m, double px, double py, double pz, double qv,
+                                          double& mean, double& stdev)
+{
+    const double* A = m.g2l;
+    double lx = ((A[0] * px + A[1] * py) + A[2] * pz) + A[3];
+    double ly = ((A[4] * px + A[5] * py) + A[6] * pz) + A[7];
+    double lz = ((A[8] * px + A[9] * py) + A[10] * pz) + A[11];
+    double fm = floor((lx - m.offset_x) / m.scale_x);
+    double fn = floor((ly - m.offset_y) / m.scale_y);
+    if (!(fm >= 0.0 && fm < (double)m.width && fn >= 0.0 && fn < (double)m.height_cells)) return false;
+    uint64_t cell = (uint64_t)fn * m.width + (uint64_t)fm;
+    uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
+    for (uint32_t k = b; k < e; ++k) {
+        float2 pf = m.patch[k];
+        double pm = (double)pf.x, ps = (double)pf.y;
+        double ph = m.height ? (double)m.height[k] : 0.0;
+        double diff;
+        if (ph > 0.0) {
+            if (lz > pm) diff = lz - pm;
+            else if (lz < pm - ph) diff = (pm - ph) - lz;
+            else diff = 0.0;
+        } else {
+            diff = dm_fabs(pm - lz);
+        }
+        double d = diff / dm_sqrt(ps * ps + qv);
+        if (d < 3.0) { mean = pm; stdev = ps; return true; }
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------------------
+// ContactModel::evaluatePose + evaluateWeight  (src/ContactModel.cpp:117-224, 262-317)
+// ---------------------------------------------------------------------------------------
+struct CMResult {
+    uint32_t ncp;
+    bool accepted;
+    double weight, zdelta, zvar, posevar;
+};
+
+template <int MAXP>
+__device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const MapView& map, double co, double s,
+                                                  double r22, double x, double y, double z, double meas_var)
+{
+    CMResult r;
+    double cz[MAXP], cv[MAXP];
+    uint32_t ncp = 0;
+    bool valid = false, group_valid = true;
+    double contact_ratio = 0, pose_var_avg = 0, posevar = 0;
+    double pzd = 0, pzv = 0;
+    const double q_stdev = dm_sqrt(meas_var);
+    const double qv = q_stdev * q_stdev;
+    for (uint32_t i = 0; i < p.m; ++i) {
+        const ContactC c = p.c[i];
+        double wx = ((co * c.px + (-s) * c.py) + 0.0 * c.pz) + x;
+        double wy = ((s * c.px + co * c.py) + 0.0 * c.pz) + y;
+        double wz = ((0.0 * c.px + 0.0 * c.py) + r22 * c.pz) + z;
+        wx = wx - 0.0;
+        wy = wy - 0.0;
+        wz = wz - p.radius;
+        if (group_valid && c.eval) {
+            double mean, stdev;
+            if (get_patch(map, wx, wy, wz, qv, mean, stdev)) {
+                const double zdiff = wz - mean;
+                const double pose_var = stdev * stdev;
+                const double zvar = stdev * stdev + meas_var;
+                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * p.corr);
+                if (!valid) {
+                    pzd = zdiff * ratio;
+                    pzv = zvar * ratio;
+                    contact_ratio = ratio;
+                    pose_var_avg = pose_var * ratio;
+                } else {
+                    pzd += zdiff * ratio;
+                    pzv += zvar * ratio;
+                    contact_ratio += ratio;
+                    pose_var_avg += pose_var * ratio;
+                }
+                valid = true;
+            } else {
+                group_valid = false;
+            }
+        }
+        if (valid && c.end) {
+            if (group_valid && contact_ratio > 1e-9) {
+                pzd /= contact_ratio;
+                pzv /= contact_ratio;
+                posevar += pose_var_avg / contact_ratio;
+#pragma unroll
+                for (int k = 0; k < MAXP; ++k)
+                    if ((uint32_t)k == ncp) { cz[k] = pzd; cv[k] = pzv; }
+                ++ncp;
+            }
+            group_valid = true;
+            valid = false;
+            pose_var_avg = 0;
+            contact_ratio = 0;
+        }
+    }
+    r.ncp = ncp;
+    r.posevar = posevar;
+    r.accepted = (uint64_t)ncp >= p.min_contacts;
+    r.weight = r.zdelta = r.zvar = 0.0;
+    if (r.accepted) {
+        double d1 = 0, d2 = 0;
+#pragma unroll
+        for (int k = 0; k < MAXP; ++k) {
+            if ((uint32_t)k < ncp) {
+                d1 += cz[k] / cv[k];
+                d2 += 1.0 / cv[k];
+            }
+        }
+        const double delta = d1 / d2;
+        double pz = 1.0;
+#pragma unroll
+        for (int k = 0; k < MAXP; ++k) {
+            if ((uint32_t)k < ncp) {
+                const double odiff = (cz[k] - delta) / dm_sqrt(cv[k]);
+                const double zk = dm_exp(-(odiff * odiff) / (2.0));
+                if (p.use_shape) pz *= zk;
+            }
+        }
+        r.weight = pz;
+        r.zdelta = -delta;
+        r.zvar = 1.0 / d2;
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_project_weight: PoseEstimator::project and/or updateWeights phase A, one particle per
+// lane, one canonical chunk (64 lanes x J rows) per wave.
+// ---------------------------------------------------------------------------------------
+template <bool PROJECT, bool WEIGHT, int MAXP>
+__global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState s1, MapView map, StepParams p,
+                                                           Ctl* __restrict__ ctl, Shard* __restrict__ shards)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
+    const uint64_t lbase = chunk * 64ull * p.J;
+    const uint32_t cur = ctl->base ^ ctl->flip;
+    const DevState st = cur ? s1 : s0;
+    const int wexp = ctl->wexp;
+
+    double spread = 0.0;
+    bool do_spread = false;
+    double tf = 0.0, rf = 0.0;
+    if (PROJECT) {
+        spread = dm_weighting_function(ctl->max_weight, 0.0, p.spread_threshold, 0.0);
+        do_spread = spread > 0 && !p.hash_use;
+        tf = p.spread_trans * spread;
+        rf = p.spread_rot * spread;
+    }
+
+    double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
+#pragma unroll
+    for (int b = 0; b < DM_NBUCKETS; ++b) { accA[b] = 0.0; accB[b] = 0.0; }
+    double accSW = 0.0, maxm = 0.0;
+    uint32_t nD = 0, nTP = 0, err = 0;
+
+    for (uint32_t j = 0; j < p.J; ++j) {
+        const uint64_t i = lbase + 64ull * j + lane;
+        if (i >= p.n) continue;
+        double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i], w = st.w[i];
+        const double w_in = w;
+        if (PROJECT) {
+            const uint64_t gi = p.gbase + i;
+            dm_philox_ctr d0 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 0);
+            dm_philox_ctr d1 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 1);
+            dm_philox_ctr d2 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 2);
+            double z0, z1, z2, sn0;
+            dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &z0, &z1);
+            dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &z2, &sn0);
+            // odometry.getPoseDeltaSample2D() = mu + L z
+            const double dx = p.mu[0] + p.L00 * z0;
+            double dy = p.mu[1] + (p.L10 * z0 + p.L11 * z1);
+            const double dth = p.mu[2] + ((p.L20 * z0 + p.L21 * z1) + p.L22 * z2);
+            if (dm_u53(d2.v[0], d2.v[1]) < p.slip_factor) dy *= dm_u53(d2.v[2], d2.v[3]);
+            double s, co;
+            dm_sincos(th, &s, &co);
+            x += co * dx - s * dy;
+            y += s * dx + co * dy;
+            th += dth;
+            if (p.max_yaw_dev > 0.0) {
+                if (dm_fabs(th - p.yaw) > p.max_yaw_dev) w *= 0.7;
+            }
+            z += p.z_delta;
+            zs = dm_sqrt(zs * zs + p.z_var);
+            if (do_spread) {
+                dm_philox_ctr d3 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 3);
+                double sn1, sn2;
+                dm_box_muller(dm_u53(d3.v[0], d3.v[1]), dm_u53(d3.v[2], d3.v[3]), &sn1, &sn2);
+                x += sn0 * tf + 0.0;
+                y += sn1 * tf + 0.0;
+                th += sn2 * rf + 0.0;
+            }
+            st.x[i] = x;
+            st.y[i] = y;
+            st.th[i] = th;
+        }
+        if (WEIGHT) {
+            double s, co;
+            dm_sincos(th, &s, &co);
+            const double r22 = (1.0 - co) + co;
+            const double meas_var = zs * zs + p.me2;
+            if (meas_var == 0) err = 1;
+            const CMResult r = evaluate_pose<MAXP>(p, map, co, s, r22, x, y, z, meas_var);
+            double mprob;
+            uint32_t floating;
+            double sw = 0.0;
+            if (r.accepted) {
+                // ContactModel::updateZPositionEstimate  src/ContactModel.cpp:319-340
+                double zvar = zs * zs;
+                const double pose_var = r.posevar / (double)r.ncp;
+                const double a = zvar - pose_var;
+                double delta_var = (a < 1e-9) ? 1e-9 : a;
+                if (!(dm_fabs(r.zdelta / dm_sqrt(delta_var)) > 1.0)) {
+                    const double gain = zvar / (zvar + r.zvar);
+                    z += gain * r.zdelta;
+                    const double var_gain = delta_var / (delta_var + r.zvar);
+                    delta_var = (1.0 - var_gain) * delta_var;
+                    zvar = pose_var + delta_var;
+                }
+                zs = dm_sqrt(zvar);
+                w *= r.weight;
+                mprob = r.weight;
+                floating = 0;
+                maxm = (maxm < r.weight) ? r.weight : maxm;
+                nD += 1;
+                sw = dm_pow(r.weight, 1.0 / (double)r.ncp);
+                nTP += r.ncp;
+            } else {
+                floating = 1;
+                mprob = 1.0;
+            }
+            const uint32_t bucket = r.ncp < DM_NBUCKETS - 1 ? r.ncp : DM_NBUCKETS - 1;
+            const double a = w * mprob;
+            const double a2 = a * a;
+#pragma unroll
+            for (int b = 0; b < DM_NBUCKETS; ++b) {
+                accA[b] = accA[b] + (bucket == (uint32_t)b ? a : 0.0);
+                accB[b] = accB[b] + (bucket == (uint32_t)b ? a2 : 0.0);
+            }
+            accSW = accSW + sw;
+            st.mprob[i] = mprob;
+            st.flags[i] = (uint8_t)((r.ncp & 0x7fu) | (floating << 7));
+        }
+        if (PROJECT || WEIGHT) {
+            st.z[i] = z;
+            st.zs[i] = zs;
+            if (w != w_in || w != w) st.w[i] = w;
+        }
+    }
+
+    if (!WEIGHT) return;
+
+    // ---- exact statistics: chunk totals -> fixed point -> block -> sharded atomics ----
+    __shared__ uint32_t s_limb[kWaves][2 * DM_NBUCKETS + 1][4];
+    __shared__ uint32_t s_flag[kWaves];
+    __shared__ uint32_t s_cnt[kWaves][2];
+    __shared__ double s_max[kWaves];
+    uint32_t flag = 0;
+    const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
+#pragma unroll
+    for (int q = 0; q < 2 * DM_NBUCKETS + 1; ++q) {
+        double v = q < DM_NBUCKETS ? accA[q] : (q < 2 * DM_NBUCKETS ? accB[q - DM_NBUCKETS] : accSW);
+        const int scale = q < DM_NBUCKETS ? sa : (q < 2 * DM_NBUCKETS ? sb : DM_FX_SCALE);
+        uint32_t l[4] = {0, 0, 0, 0};
+        if (__ballot(v != 0.0) != 0ull) {
+            v = wave_sum_butterfly(v);
+            if (v != v) flag |= 1u << q;
+            else if (!dm_isfinite(v)) flag |= 1u << (q + 16);
+            else dm_fx128_limbs(v, scale, l);
+        }
+        if (lane == 0) {
+            s_limb[wave][q][0] = l[0];
+            s_limb[wave][q][1] = l[1];
+            s_limb[wave][q][2] = l[2];
+            s_limb[wave][q][3] = l[3];
+        }
+    }
+    const double wmax = wave_max_butterfly(maxm);
+    const uint32_t wD = wave_sum_u32(nD), wTP = wave_sum_u32(nTP);
+    const uint32_t werr = __ballot(err != 0) != 0ull ? 1u : 0u;
+    if (lane == 0) {
+        s_flag[wave] = flag | (werr << 31);
+        s_cnt[wave][0] = wD;
+        s_cnt[wave][1] = wTP;
+        s_max[wave] = wmax;
+    }
+    __syncthreads();
+    Shard* sh = shards + (blockIdx.x % kNShard);
+    const int t = threadIdx.x;
+    if (t < (2 * DM_NBUCKETS + 1) * 4) {
+        const int q = t >> 2, j = t & 3;
+        uint64_t v = 0;
+#pragma unroll
+        for (int wv = 0; wv < kWaves; ++wv) v += s_limb[wv][q][j];
+        if (v) {
+            uint64_t* dst = q < DM_NBUCKETS ? &sh->A[q][j] : (q < 2 * DM_NBUCKETS ? &sh->B[q - DM_NBUCKETS][j] : &sh->SW[j]);
+            atomicAdd((unsigned long long*)dst, (unsigned long long)v);
+        }
+    } else if (t == 64) {
+        uint64_t d = 0, tp = 0;
+        uint32_t f = 0;
+        double mx = 0.0;
+        for (int wv = 0; wv < kWaves; ++wv) {
+            d += s_cnt[wv][0];
+            tp += s_cnt[wv][1];
+            f |= s_flag[wv];
+            mx = (mx < s_max[wv]) ? s_max[wv] : mx;
+        }
+        if (d) atomicAdd((unsigned long long*)&sh->D, (unsigned long long)d);
+        if (tp) atomicAdd((unsigned long long*)&sh->TP, (unsigned long long)tp);
+        if (mx > 0.0) atomicMax((unsigned long long*)&sh->maxm, (unsigned long long)dm_bits(mx));
+        if (f & 0x7fffffffu) atomicOr((unsigned long long*)&sh->flags, (unsigned long long)(f & 0x7fffffffu));
+        if (f >> 31) atomicOr((unsigned long long*)&sh->err, 1ull);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_weight_stats: exact sum of the weights and of their squares (standalone
+// getWeightsSum / normalizeWeights / resample, src/ParticleFilter.hpp:34-70)
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J,
+                                                         Ctl* __restrict__ ctl, Shard* __restrict__ shards)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t lbase = ((uint64_t)blockIdx.x * kWaves + wave) * 64ull * J;
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    const int wexp = ctl->wexp;
+    double a = 0.0, b = 0.0;
+    for (uint32_t j = 0; j < J; ++j) {
+        const uint64_t i = lbase + 64ull * j + lane;
+        if (i >= n) continue;
+        const double w = st.w[i];
+        a = a + w;
+        b = b + w * w;
+    }
+    __shared__ uint32_t s_limb[kWaves][2][4];
+    __shared__ uint32_t s_flag[kWaves];
+    uint32_t flag = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        double v = q == 0 ? a : b;
+        uint32_t l[4] = {0, 0, 0, 0};
+        if (__ballot(v != 0.0) != 0ull) {
+            v = wave_sum_butterfly(v);
+            if (v != v) flag |= 1u << (q * DM_NBUCKETS);
+            else if (!dm_isfinite(v)) flag |= 1u << (q * DM_NBUCKETS + 16);
+            else dm_fx128_limbs(v, q == 0 ? DM_FX_SCALE - wexp : DM_FX_SCALE - 2 * wexp, l);
+        }
+        if (lane == 0) for (int j = 0; j < 4; ++j) s_limb[wave][q][j] = l[j];
+    }
+    if (lane == 0) s_flag[wave] = flag;
+    __syncthreads();
+    Shard* sh = shards + (blockIdx.x % kNShard);
+    const int t = threadIdx.x;
+    if (t < 8) {
+        const int q = t >> 2, j = t & 3;
+        uint64_t v = 0;
+        for (int wv = 0; wv < kWaves; ++wv) v += s_limb[wv][q][j];
+        if (v) atomicAdd((unsigned long long*)(q == 0 ? &sh->A[0][j] : &sh->B[0][j]), (unsigned long long)v);
+    } else if (t == 64) {
+        uint32_t f = 0;
+        for (int wv = 0; wv < kWaves; ++wv) f |= s_flag[wv];
+        if (f) atomicOr((unsigned long long*)&sh->flags, (unsigned long long)f);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_finalize: one block.  Sums the shards exactly, then the scalar part of the update.
+// ---------------------------------------------------------------------------------------
+constexpr int kShardFields = 2 * DM_NBUCKETS * 4 + 4 + 5;   // A, B, SW, D, TP, maxm, flags, err
+
+__device__ __forceinline__ double acc_value(const uint64_t* L, uint64_t flags, int qbit, int scale)
+{
+    if (flags & (1ull << qbit)) return __builtin_nan("");
+    if (flags & (1ull << (qbit + 16))) return __builtin_inf();
+    return dm_limbs_to_double(L, scale);
+}
+
+__global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ shards, Ctl* __restrict__ ctl, FinParams fp)
+{
+    __shared__ uint64_t s[kShardFields];
+    const int t = threadIdx.x;
+    if (t < kShardFields) {
+        uint64_t acc = 0;
+        for (int k = 0; k < kNShard; ++k) {
+            uint64_t* f = reinterpret_cast<uint64_t*>(shards + k) + t;
+            const uint64_t v = *f;
+            if (t == kShardFields - 3) acc = acc > v ? acc : v;                 // maxm
+            else if (t >= kShardFields - 2) acc |= v;                            // flags, err
+            else acc += v;
+            *f = 0;
+        }
+        s[t] = acc;
+    }
+    __syncthreads();
+    if (t != 0) return;
+
+    const uint64_t* sA = s;
+    const uint64_t* sB = s + DM_NBUCKETS * 4;
+    const uint64_t* sSW = s + 2 * DM_NBUCKETS * 4;
+    const uint64_t D = s[2 * DM_NBUCKETS * 4 + 4];
+    const uint64_t TP = s[2 * DM_NBUCKETS * 4 + 5];
+    const double maxm = dm_from_bits(s[2 * DM_NBUCKETS * 4 + 6]);
+    const uint64_t flags = s[2 * DM_NBUCKETS * 4 + 7];
+    const uint64_t err = s[2 * DM_NBUCKETS * 4 + 8];
+    const int wexp = ctl->wexp;      // the exponent the statistics kernel used
+    const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
+
+    // commit the previous resample's buffer flip
+    ctl->base ^= ctl->flip;
+    ctl->flip = 0;
+    ctl->err |= err;
+    ctl->tile_counter = 0;
+    ctl->overruns = 0;
+    const double N = (double)fp.n_global;
+
+    double S = 0.0, Q = 0.0;
+    if (fp.mode == FIN_UPDATE) {
+        const double SW = acc_value(sSW, flags, 2 * DM_NBUCKETS, DM_FX_SCALE);
+        const double fw = D > 0 ? SW / (double)D : 1.0;
+        const double base = fp.discount * fw;
+        for (int b = 0; b < DM_NBUCKETS; ++b) {
+            const uint64_t ncp = (uint64_t)b;
+            ctl->f[b] = dm_pow(base, (double)(uint64_t)(4ull - ncp));
+        }
+        for (int b = 0; b < DM_NBUCKETS; ++b) {
+            const double Ab = acc_value(sA + 4 * b, flags, b, sa);
+            const double Bb = acc_value(sB + 4 * b, flags, DM_NBUCKETS + b, sb);
+            S = S + ctl->f[b] * Ab;
+            Q = Q + (ctl->f[b] * ctl->f[b]) * Bb;
+        }
+        ctl->fw = fw;
+        const double last = ctl->max_weight;
+        double mw = maxm;
+        if (TP == 0) mw = last * fp.discount;
+        ctl->max_weight = mw;
+        ctl->data_particles = D;
+        ctl->total_points = TP;
+        ctl->update_count += 1;
+    } else {
+        S = acc_value(sA, flags, 0, sa);
+        Q = acc_value(sB, flags, DM_NBUCKETS, sb);
+        for (int b = 0; b < DM_NBUCKETS; ++b) ctl->f[b] = 1.0;
+    }
+    ctl->S = S;
+    ctl->Q = Q;
+    ctl->inv_n = 1.0 / N;
+
+    if (fp.mode == FIN_UPDATE || fp.mode == FIN_NORMALIZE) {
+        double eff;
+        ctl->uniform = 0;
+        if (S <= 0.0) {
+            ctl->uniform = 1;
+            eff = 1.0 / (1.0 / N);
+        } else {
+            eff = 1.0 / (Q / (S * S));
+        }
+        ctl->eff = eff;
+        ctl->wexp = 1;
+        ctl->scan_shift = 60;
+        ctl->resample = (fp.mode == FIN_UPDATE && eff < (double)fp.min_effective) ? 1u : 0u;
+    } else if (fp.mode == FIN_RESAMPLE) {
+        ctl->resample = 1;
+        ctl->scan_shift = 61 - (dm_weight_exp(S) + 1);
+    } else {
+        ctl->resample = 0;
+    }
+    if (ctl->resample) {
+        ctl->minstd_start = ctl->minstd;
+        ctl->minstd = dm_mulmod31(dm_minstd_pow(fp.n_global), ctl->minstd);
+        ctl->flip = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// count of stratified draws T_k = fx(((k + U_k) / N), shift) that are <= c
+// (U_k = boost uniform_real of the (k+1)-th minstd draw after x_start)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t fx_shift(double v, int shift) { return dm_fx_shift(v, shift); }
+
+__device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint32_t xs, int shift,
+                                                   const uint32_t* __restrict__ jt)
+{
+    const unsigned __int128 prod = (unsigned __int128)c * N;
+    const uint64_t kstar = (uint64_t)(prod >> shift);
+    const uint64_t k0 = kstar >= 1 ? kstar - 1 : 0;
+    if (k0 >= N) return N;
+    uint64_t cnt = k0;
+    uint32_t x = dm_mulmod31(jump_pow(jt, k0 + 1), xs);
+    const double dN = (double)N;
+    for (uint64_t k = k0; k <= kstar + 1 && k < N; ++k) {
+        const double u = dm_minstd_uniform(x);
+        const uint64_t T = fx_shift(((double)k + u) / dN, shift);
+        if (T <= c) cnt = k + 1;
+        else break;
+        x = dm_minstd_next(x);
+    }
+    return cnt;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_normalize_scan: phase B + normalisation, then (when resampling) the decoupled
+// look-back prefix sum of the fixed-point weights and the segment boundaries.
+// ---------------------------------------------------------------------------------------
+constexpr uint64_t kTagAgg = 1ull << 62, kTagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+                                                           uint64_t* __restrict__ status, uint32_t* __restrict__ marks,
+                                                           uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt)
+{
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_wtot[kWaves];
+    __shared__ uint64_t s_excl;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const bool resample = ctl->resample != 0;
+    uint32_t tile = blockIdx.x;
+    if (resample) {
+        if (tid == 0) s_tile = (uint32_t)atomicAdd((unsigned long long*)&ctl->tile_counter, 1ull);
+        __syncthreads();
+        tile = s_tile;
+    }
+    const DevState st = ctl->base ? s1 : s0;
+    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+    const double S = ctl->S;
+    const bool uniform = ctl->uniform != 0;
+    const double inv_n = ctl->inv_n;
+    double f[DM_NBUCKETS];
+#pragma unroll
+    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
+
+    double w[kScanItems];
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        w[r] = 0.0;
+        if (i < sp.n) {
+            double v = st.w[i];
+            if (sp.phase_b) {
+                const uint32_t fl = st.flags[i];
+                const uint32_t ncp = fl & 0x7fu;
+                const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
+                double fb = f[0];
+#pragma unroll
+                for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
+                const double factor = st.mprob[i] * fb;
+                v *= factor;
+            }
+            if (sp.normalize) v = uniform ? inv_n : v / S;
+            if (sp.phase_b || sp.normalize) st.w[i] = v;
+            w[r] = v;
+        }
+    }
+    if (!resample) return;
+
+    // ---- fixed-point inclusive scan: thread -> wave -> block ----
+    const int shift = ctl->scan_shift;
+    uint64_t c[kScanItems];
+    uint64_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        run += fx_shift(w[r], shift);
+        c[r] = run;
+    }
+    uint64_t tincl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_up(tincl, o, 64);
+        if ((int)lane >= o) tincl += t;
+    }
+    if (lane == 63) s_wtot[wave] = tincl;
+    __syncthreads();
+    uint64_t wexcl = 0, agg = 0;
+#pragma unroll
+    for (int wv = 0; wv < kWaves; ++wv) {
+        if ((uint32_t)wv < wave) wexcl += s_wtot[wv];
+        agg += s_wtot[wv];
+    }
+    const uint64_t texcl = wexcl + (tincl - run);
+
+    // ---- decoupled look-back (wave 0): 8-byte {tag, value} granules, relaxed agent scope ----
+    if (wave == 0) {
+        uint64_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) atomic_store_agent(&status[0], kTagInc | agg);
+        } else {
+            if (lane == 0) atomic_store_agent(&status[tile], kTagAgg | agg);
+            int64_t pred = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            bool timeout = false;
+            while (true) {
+                const int64_t idx = pred - (int64_t)lane;
+                uint64_t v = kTagInc;   // before tile 0: an inclusive zero
+                if (idx >= 0) {
+                    v = atomic_load_agent(&status[idx]);
+                    while ((v >> 62) == 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        v = atomic_load_agent(&status[idx]);
+                        if (++spins > (1u << 22)) { timeout = true; v = kTagInc; break; }
+                    }
+                }
+                const uint64_t incl_mask = __ballot((v >> 62) == 2);
+                uint64_t val = v & kValMask;
+                if (incl_mask) {
+                    const int first = __builtin_ctzll(incl_mask);
+                    if ((int)lane > first) val = 0;
+                    uint64_t tot = val;
+                    for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
+                    excl += tot;
+                    break;
+                }
+                uint64_t tot = val;
+                for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
+                excl += tot;
+                pred -= 64;
+            }
+            if (__ballot(timeout) != 0ull && lane == 0) atomicOr((unsigned long long*)&ctl->err, 2ull);
+            if (lane == 0) atomic_store_agent(&status[tile], kTagInc | ((excl + agg) & kValMask));
+        }
+        if (lane == 0) s_excl = excl;
+    }
+    __syncthreads();
+    const uint64_t excl = s_excl;
+
+    // ---- segment boundaries: particle i covers draws [lo_i, hi_i) ----
+    const uint64_t N = sp.n_global;
+    const uint32_t xs = ctl->minstd_start;
+    uint64_t lo = count_draws_le(excl + texcl, N, xs, shift, jt);
+    if (i0 == 0 && sp.gbase == 0) lo = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        if (i >= sp.n) break;
+        const uint64_t gi = sp.gbase + i;
+        const uint64_t cc = excl + texcl + c[r];
+        uint64_t hi = count_draws_le(cc, N, xs, shift, jt);
+        if (gi == N - 1) {
+            if (hi < N) atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
+            hi = N;
+        }
+        if (hi > lo) {
+            marks[lo] = (uint32_t)(i + 1);
+            for (uint64_t t = (lo + kGatherTile - 1) / kGatherTile; t * kGatherTile < hi; ++t)
+                tile_first[t] = (uint32_t)i;
+        }
+        lo = hi;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_resample_gather: expand the segments (inclusive max-scan of the marks) and gather
+// the particle state into the other buffer (xi_k.swap(xi_kp), src/ParticleFilter.hpp:107).
+// Weights are carried, not reset (Q4).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+                                                            uint32_t* __restrict__ marks, const uint32_t* __restrict__ tile_first,
+                                                            uint64_t* __restrict__ status, uint32_t* __restrict__ anc,
+                                                            uint32_t record, uint32_t aux)
+{
+    if (!ctl->resample) return;
+    __shared__ uint32_t s_wmax[kWaves];
+    __shared__ uint32_t s_idx[kGatherTile];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t t = blockIdx.x;
+    if (tid == 0 && t < sp.ntiles) status[t] = 0;       // reset the look-back words for next time
+    const DevState in = ctl->base ? s1 : s0;
+    const DevState out = ctl->base ? s0 : s1;
+    const uint64_t k0 = (uint64_t)t * kGatherTile + (uint64_t)tid * kScanItems;
+    uint32_t mk[kScanItems];
+    uint32_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t k = k0 + r;
+        uint32_t v = 0;
+        if (k < sp.n) { v = marks[k]; if (v) marks[k] = 0; }
+        run = run > v ? run : v;
+        mk[r] = run;
+    }
+    uint32_t tincl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(tincl, o, 64);
+        if ((int)lane >= o) tincl = tincl > x ? tincl : x;
+    }
+    if (lane == 63) s_wmax[wave] = tincl;
+    __syncthreads();
+    uint32_t carry = tile_first[t] + 1u;
+    for (uint32_t wv = 0; wv < wave; ++wv) carry = carry > s_wmax[wv] ? carry : s_wmax[wv];
+    uint32_t texcl = __shfl_up(tincl, 1, 64);
+    if (lane == 0) texcl = 0;
+    carry = carry > texcl ? carry : texcl;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint32_t v = mk[r] > carry ? mk[r] : carry;
+        s_idx[tid * kScanItems + r] = v - 1u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint32_t slot = (uint32_t)r * kBlock + tid;
+        const uint64_t k = (uint64_t)t * kGatherTile + slot;
+        if (k >= sp.n) continue;
+        const uint32_t i = s_idx[slot];
+        out.x[k] = in.x[i];
+        out.y[k] = in.y[i];
+        out.th[k] = in.th[i];
+        out.z[k] = in.z[i];
+        out.zs[k] = in.zs[i];
+        out.w[k] = in.w[i];
+        if (aux) {
+            out.mprob[k] = in.mprob[i];
+            out.flags[k] = in.flags[i];
+        }
+        if (record) anc[k] = i;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// PoseEstimator::init(N, mu, sigma, zpos, zsigma): samplePose2D per particle
+// (src/PoseEstimator.cpp:64-73, 88-102) from the INIT Philox stream.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_init_gaussian(DevState s0, uint64_t n, uint64_t gbase, uint64_t seed, uint64_t ev,
+                                                          double mx, double my, double mt, double sx, double sy, double stt,
+                                                          double zpos, double zsigma)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t gi = gbase + i;
+    dm_philox_ctr d0 = dm_draw(seed, DM_STREAM_INIT, ev, gi, 0);
+    dm_philox_ctr d1 = dm_draw(seed, DM_STREAM_INIT, ev, gi, 1);
+    double n0, n1, n2, n3;
+    dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &n0, &n1);
+    dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &n2, &n3);
+    s0.x[i] = n0 * sx + mx;
+    s0.y[i] = n1 * sy + my;
+    s0.th[i] = n2 * stt + mt;
+    s0.z[i] = zpos;
+    s0.zs[i] = zsigma;
+    s0.w[i] = 0.0;
+    s0.mprob[i] = 0.0;
+    s0.flags[i] = 0x80u;   // floating = true, no contact points
+}
+
+// ---------------------------------------------------------------------------------------
+// ParticleFilter::getBestParticleIndex (src/ParticleFilter.hpp:160-173): first index of the
+// maximum weight; NaN never compares greater.  out[0] = max ordered key, out[1] = index.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t order_key(double w)
+{
+    const uint64_t b = dm_bits(w);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__global__ void __launch_bounds__(kBlock) k_best_max(DevState s0, DevState s1, uint64_t n, const Ctl* __restrict__ ctl,
+                                                     uint64_t* out)
+{
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    uint64_t best = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const double w = st.w[i];
+        if (w == w) { const uint64_t k = order_key(w); best = best > k ? best : k; }
+    }
+    for (int o = 32; o >= 1; o >>= 1) { const uint64_t t = __shfl_xor(best, o, 64); best = best > t ? best : t; }
+    if ((threadIdx.x & 63u) == 0 && best) atomicMax((unsigned long long*)&out[0], (unsigned long long)best);
+}
+
+__global__ void __launch_bounds__(kBlock) k_best_index(DevState s0, DevState s1, uint64_t n, const Ctl* __restrict__ ctl,
+                                                       uint64_t* out)
+{
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    const uint64_t key = out[0];
+    uint64_t idx = ~0ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const double w = st.w[i];
+        if (w == w && order_key(w) == key) { idx = i < idx ? i : idx; break; }
+    }
+    for (int o = 32; o >= 1; o >>= 1) { const uint64_t t = __shfl_xor(idx, o, 64); idx = idx < t ? idx : t; }
+    if ((threadIdx.x & 63u) == 0 && idx != ~0ull) atomicMin((unsigned long long*)&out[1], (unsigned long long)idx);
+}
+
+// ---------------------------------------------------------------------------------------
+// PoseEstimator::getCentroid sums (src/PoseEstimator.cpp:354-383): x w, y w, theta w, z w, w
+// in the canonical chunk order, then a fixed pairwise tree over the chunk totals.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_centroid_chunks(DevState s0, DevState s1, uint64_t n, uint32_t J,
+                                                            const Ctl* __restrict__ ctl, double* __restrict__ chunk_out)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
+    const uint64_t lbase = chunk * 64ull * J;
+    if (lbase >= n) return;
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    for (uint32_t j = 0; j < J; ++j) {
+        const uint64_t i = lbase + 64ull * j + lane;
+        if (i >= n) continue;
+        const double w = st.w[i];
+        a[0] = a[0] + st.x[i] * w;
+        a[1] = a[1] + st.y[i] * w;
+        a[2] = a[2] + st.th[i] * w;
+        a[3] = a[3] + st.z[i] * w;
+        a[4] = a[4] + w;
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const double v = wave_sum_butterfly(a[q]);
+        if (lane == 0) chunk_out[chunk * 5 + q] = v;
+    }
+}
+
+// one level of the fixed pairwise tree: dst[i] = src[2i] + src[2i+1]; odd tail moves up
+__global__ void __launch_bounds__(kBlock) k_tree_level(const double* __restrict__ src, double* __restrict__ dst, uint64_t m)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t h = m / 2;
+    if (i > h || (i == h && !(m & 1))) return;
+    for (int q = 0; q < 5; ++q)
+        dst[i * 5 + q] = i < h ? src[(2 * i) * 5 + q] + src[(2 * i + 1) * 5 + q] : src[(m - 1) * 5 + q];
+}
+
+// device self-test of the deterministic math (tests/test_gpu_math.py)
+__global__ void k_selftest_math(int fn, const double* x, const double* y, double* out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s, c, r = 0;
+    switch (fn) {
+    case 0: r = dm_exp(x[i]); break;
+    case 1: r = dm_log(x[i]); break;
+    case 2: dm_sincos(x[i], &s, &c); r = s; break;
+    case 3: dm_sincos(x[i], &s, &c); r = c; break;
+    case 4: r = dm_erfc(x[i]); break;
+    case 5: r = dm_sqrt(x[i]); break;
+    case 6: r = x[i] / y[i]; break;
+    case 7: r = dm_normal_pdf_cdf_ratio(x[i], y[i]); break;
+    case 8: r = dm_pow(x[i], y[i]); break;
+    case 9: r = dm_from_bits(dm_fx61(x[i])); break;
+    default: r = __builtin_nan("");
+    }
+    out[i] = r;
+}
+
+}  // namespace eslam_dev
+
+// ---------------------------------------------------------------------------------------
+// launchers (called by eslam_ctx.hip)
+// ---------------------------------------------------------------------------------------
+using namespace eslam_dev;
+
+extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
+                                                  const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
+                                                  hipStream_t stream)
+{
+    const uint64_t csz = 64ull * p->J;
+    const uint64_t chunks = (p->n + csz - 1) / csz;
+    const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
+    if (blocks == 0) return hipSuccess;
+    dim3 g(blocks), b(kBlock);
+#define ESLAM_LAUNCH(P, W, M) hipLaunchKernelGGL((k_project_weight<P, W, M>), g, b, 0, stream, s0, s1, *map, *p, ctl, shards)
+    if (project && !weight) ESLAM_LAUNCH(true, false, 4);
+    else if (!project && weight) {
+        if (maxp <= 4) ESLAM_LAUNCH(false, true, 4);
+        else if (maxp <= 8) ESLAM_LAUNCH(false, true, 8);
+        else ESLAM_LAUNCH(false, true, ESLAM_MAX_CONTACTS);
+    } else {
+        if (maxp <= 4) ESLAM_LAUNCH(true, true, 4);
+        else if (maxp <= 8) ESLAM_LAUNCH(true, true, 8);
+        else ESLAM_LAUNCH(true, true, ESLAM_MAX_CONTACTS);
+    }
+#undef ESLAM_LAUNCH
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
+                                                hipStream_t stream)
+{
+    const uint64_t csz = 64ull * J;
+    const uint64_t chunks = (n + csz - 1) / csz;
+    const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_weight_stats, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, J, ctl, shards);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_finalize(Shard* shards, Ctl* ctl, const FinParams* fp, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, stream, shards, ctl, *fp);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
+                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream)
+{
+    if (sp->ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_normalize_scan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, status, marks,
+                       tile_first, jt);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint32_t* marks,
+                                                   const uint32_t* tile_first, uint64_t* status, uint32_t* anc,
+                                                   uint32_t record, uint32_t aux, hipStream_t stream)
+{
+    if (sp->ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_resample_gather, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, marks, tile_first,
+                       status, anc, record, aux);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_init_gaussian(DevState s0, uint64_t n, uint64_t gbase, uint64_t seed, uint64_t ev,
+                                                 const double mu[3], const double sigma[3], double zpos, double zsigma,
+                                                 hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((n + kBlock - 1) / kBlock);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_init_gaussian, dim3(blocks), dim3(kBlock), 0, stream, s0, n, gbase, seed, ev, mu[0], mu[1], mu[2],
+                       sigma[0], sigma[1], sigma[2], zpos, zsigma);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_selftest_math(int fn, const double* x, const double* y, double* out, uint64_t n,
+                                                 hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_selftest_math, dim3(blocks), dim3(kBlock), 0, stream, fn, x, y, out, n);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_best_index(DevState s0, DevState s1, uint64_t n, Ctl* ctl, uint64_t* out2,
+                                              hipStream_t stream)
+{
+    const uint64_t init[2] = {0ull, ~0ull};
+    hipError_t e = hipMemcpyAsync(out2, init, 16, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    uint32_t blocks = (uint32_t)((n + kBlock - 1) / kBlock);
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(k_best_max, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, ctl, out2);
+    hipLaunchKernelGGL(k_best_index, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, ctl, out2);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, double* out,
+                                            hipStream_t stream)
+{
+    const uint64_t csz = 64ull * J;
+    const uint64_t chunks = (n + csz - 1) / csz;
+    const uint64_t cap = chunks ? chunks : 1;
+    double* tmp = nullptr;
+    hipError_t e = hipMallocAsync((void**)&tmp, 2 * cap * 5 * sizeof(double), stream);
+    if (e != hipSuccess) return e;
+    double* a = tmp;
+    double* b = tmp + cap * 5;
+    hipMemsetAsync(a, 0, 5 * sizeof(double), stream);
+    const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
+    if (blocks) hipLaunchKernelGGL(k_centroid_chunks, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, J, ctl, a);
+    uint64_t m = chunks;
+    while (m > 1) {
+        const uint64_t m2 = (m + 1) / 2;
+        hipLaunchKernelGGL(k_tree_level, dim3((uint32_t)((m2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, a, b, m);
+        double* t = a; a = b; b = t;
+        m = m2;
+    }
+    hipMemcpyAsync(out, a, 5 * sizeof(double), hipMemcpyDeviceToDevice, stream);
+    e = hipGetLastError();
+    hipFreeAsync(tmp, stream);
+    return e;
+}

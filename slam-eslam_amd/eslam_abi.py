@@ -1,0 +1,250 @@
+"""ctypes mirror of include/eslam_gpu.h (the C ABI of the MI355X eSLAM core).
+
+Shared by the product wrapper (eslam_amd.py), the tests and bench.py.  Field order and
+types must match the header exactly; tests/test_abi.py checks sizes against the C compiler.
+"""
+import ctypes as C
+
+MAX_CONTACTS = 32
+
+OK = 0
+ERR_INVALID_ARG = -1
+ERR_NO_ENVIRONMENT = -2
+ERR_ZERO_MEAS_VAR = -3
+ERR_HASH_SAMPLE = -4
+ERR_NO_MLS_GRID = -5
+ERR_HIP = -6
+ERR_NOT_INITIALISED = -7
+ERR_UNSUPPORTED = -8
+ERR_OUT_OF_MEMORY = -9
+
+FLAG_RECORD_ANCESTORS = 0x1
+FLAG_NO_MAP_LDS = 0x2
+FLAG_NO_AUX_GATHER = 0x4
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("particle_count", C.c_uint64),
+        ("min_effective", C.c_uint64),
+        ("initial_rotation_error", C.c_double * 3),
+        ("initial_translation_error", C.c_double * 3),
+        ("measurement_error", C.c_double),
+        ("discount_factor", C.c_double),
+        ("spread_threshold", C.c_double),
+        ("spread_translation_factor", C.c_double),
+        ("spread_rotation_factor", C.c_double),
+        ("slip_factor", C.c_double),
+        ("max_yaw_deviation", C.c_double),
+        ("measurement_threshold_distance", C.c_double),
+        ("measurement_threshold_angle", C.c_double),
+        ("use_slip_update", C.c_int32),
+        ("use_shape_update", C.c_int32),
+        ("min_contacts", C.c_uint64),
+        ("contact_likelihood_correction", C.c_double),
+        ("contact_point_radius", C.c_double),
+        ("hash_use", C.c_int32),
+        ("hash_period", C.c_uint64),
+        ("hash_percentage", C.c_double),
+        ("hash_avg_factor", C.c_double),
+        ("hash_slope_bins", C.c_uint64),
+        ("hash_angular_steps", C.c_uint64),
+        ("log_debug", C.c_int32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class MlsGrid(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("scale_x", C.c_double),
+        ("scale_y", C.c_double),
+        ("offset_x", C.c_double),
+        ("offset_y", C.c_double),
+        ("global2local", C.c_double * 12),
+        ("cell_start", C.POINTER(C.c_uint32)),
+        ("patch_mean", C.POINTER(C.c_float)),
+        ("patch_stdev", C.POINTER(C.c_float)),
+        ("patch_height", C.POINTER(C.c_float)),
+        ("n_patches", C.c_uint64),
+    ]
+
+
+class ContactPoint(C.Structure):
+    _fields_ = [
+        ("position", C.c_double * 3),
+        ("contact", C.c_float),
+        ("group_id", C.c_int32),
+    ]
+
+
+class StepInput(C.Structure):
+    _fields_ = [
+        ("body2odometry_rot", C.c_double * 4),
+        ("body2odometry_trans", C.c_double * 3),
+        ("pose_delta_trans", C.c_double * 3),
+        ("position_error_zz", C.c_double),
+        ("sample_mean", C.c_double * 3),
+        ("sample_cov", C.c_double * 9),
+        ("n_contacts", C.c_uint32),
+        ("ltc_count", C.c_uint32),
+        ("contacts", ContactPoint * MAX_CONTACTS),
+    ]
+
+
+class Particles(C.Structure):
+    _fields_ = [
+        ("x", C.POINTER(C.c_double)),
+        ("y", C.POINTER(C.c_double)),
+        ("orientation", C.POINTER(C.c_double)),
+        ("zpos", C.POINTER(C.c_double)),
+        ("zsigma", C.POINTER(C.c_double)),
+        ("weight", C.POINTER(C.c_double)),
+        ("mprob", C.POINTER(C.c_double)),
+        ("floating", C.POINTER(C.c_uint8)),
+        ("n_contact_points", C.POINTER(C.c_uint8)),
+    ]
+
+
+class UpdateInfo(C.Structure):
+    _fields_ = [
+        ("effective", C.c_double),
+        ("weight_sum", C.c_double),
+        ("floating_weight", C.c_double),
+        ("max_weight", C.c_double),
+        ("data_particles", C.c_uint64),
+        ("total_points", C.c_uint64),
+        ("resampled", C.c_int32),
+        ("uniform_reset", C.c_int32),
+        ("resample_overruns", C.c_uint64),
+        ("update_count", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class RngState(C.Structure):
+    _fields_ = [
+        ("minstd_x", C.c_uint32),
+        ("pad", C.c_uint32),
+        ("project_count", C.c_uint64),
+        ("init_count", C.c_uint64),
+        ("hash_count", C.c_uint64),
+        ("max_weight", C.c_double),
+        ("ud_pose", C.c_double * 12),
+    ]
+
+
+class KernelTimes(C.Structure):
+    _fields_ = [
+        ("project_weight_ms", C.c_float),
+        ("finalize_ms", C.c_float),
+        ("normalize_scan_ms", C.c_float),
+        ("resample_ms", C.c_float),
+        ("total_ms", C.c_float),
+    ]
+
+
+def default_config(lib=None):
+    """eslam_config_default() restated (src/Configuration.hpp:85-111 defaults)."""
+    import math
+    c = Config()
+    c.seed = 42
+    c.particle_count = 250
+    c.min_effective = 50
+    c.initial_rotation_error[:] = [0.0, 0.0, 0.1]
+    c.initial_translation_error[:] = [0.1, 0.1, 1.0]
+    c.measurement_error = 0.1
+    c.discount_factor = 0.9
+    c.spread_threshold = 0.9
+    c.spread_translation_factor = 0.1
+    c.spread_rotation_factor = 0.05
+    c.slip_factor = 0.05
+    c.max_yaw_deviation = 15 * math.pi / 180.0
+    c.measurement_threshold_distance = 0.1
+    c.measurement_threshold_angle = 10 * math.pi / 180.0
+    c.use_slip_update = 0
+    c.use_shape_update = 1
+    c.min_contacts = 3
+    c.contact_likelihood_correction = 0.33
+    c.contact_point_radius = 0.01
+    c.hash_use = 0
+    c.hash_period = 10
+    c.hash_percentage = 0.05
+    c.hash_avg_factor = 0.1
+    c.hash_slope_bins = 20
+    c.hash_angular_steps = 16
+    c.log_debug = 0
+    c.flags = 0
+    return c
+
+
+# ---------------------------------------------------------------------------------------
+# numpy helpers
+# ---------------------------------------------------------------------------------------
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class ParticleArrays:
+    """Host SoA buffers + the eslam_particles view onto them."""
+
+    def __init__(self, n):
+        import numpy as np
+        self.n = n
+        self.x = np.zeros(n)
+        self.y = np.zeros(n)
+        self.orientation = np.zeros(n)
+        self.zpos = np.zeros(n)
+        self.zsigma = np.zeros(n)
+        self.weight = np.zeros(n)
+        self.mprob = np.zeros(n)
+        self.floating = np.zeros(n, dtype=np.uint8)
+        self.n_contact_points = np.zeros(n, dtype=np.uint8)
+
+    def view(self):
+        p = Particles()
+        for f in ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob"):
+            setattr(p, f, _ptr(getattr(self, f), C.c_double))
+        p.floating = _ptr(self.floating, C.c_uint8)
+        p.n_contact_points = _ptr(self.n_contact_points, C.c_uint8)
+        return p
+
+    FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f in self.FIELDS}
+
+
+class GridArrays:
+    """An MLS grid held in numpy arrays + the eslam_mls_grid view onto them."""
+
+    def __init__(self, width, height, scale, offset, cell_start, mean, stdev, height_arr=None,
+                 global2local=None):
+        import numpy as np
+        self.width, self.height = int(width), int(height)
+        self.scale = (float(scale[0]), float(scale[1]))
+        self.offset = (float(offset[0]), float(offset[1]))
+        self.cell_start = np.ascontiguousarray(cell_start, dtype=np.uint32)
+        self.mean = np.ascontiguousarray(mean, dtype=np.float32)
+        self.stdev = np.ascontiguousarray(stdev, dtype=np.float32)
+        self.patch_height = None if height_arr is None else np.ascontiguousarray(height_arr, dtype=np.float32)
+        self.g2l = [1.0, 0, 0, 0, 0, 1.0, 0, 0, 0, 0, 1.0, 0] if global2local is None else list(global2local)
+        assert self.cell_start.shape[0] == self.width * self.height + 1
+        assert int(self.cell_start[-1]) == self.mean.shape[0] == self.stdev.shape[0]
+
+    def view(self):
+        g = MlsGrid()
+        g.width, g.height = self.width, self.height
+        g.scale_x, g.scale_y = self.scale
+        g.offset_x, g.offset_y = self.offset
+        g.global2local[:] = self.g2l
+        g.cell_start = _ptr(self.cell_start, C.c_uint32)
+        g.patch_mean = _ptr(self.mean, C.c_float)
+        g.patch_stdev = _ptr(self.stdev, C.c_float)
+        g.patch_height = None if self.patch_height is None else _ptr(self.patch_height, C.c_float)
+        g.n_patches = int(self.mean.shape[0])
+        return g

@@ -1,0 +1,207 @@
+"""Python binding of libeslam_gpu.so (the MI355X eSLAM core) through its C ABI.
+
+This is the host-side mirror of the reference's API for tests and benchmarks:
+``EmbodiedSlamFilter`` (src/EmbodiedSlamFilter.hpp:58-74) and the ``PoseEstimator`` /
+``ParticleFilter<T>`` calls it forwards (src/PoseEstimator.hpp:123-134,
+src/ParticleFilter.hpp:34-173).  Every call goes to the GPU; there is no CPU fallback --
+a missing library or GPU raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+import eslam_abi as A
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libeslam_gpu.so")
+
+_lib = None
+
+
+class EslamError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+def load_library(path=LIB_PATH):
+    """Load libeslam_gpu.so and declare every entry point of include/eslam_gpu.h."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libeslam_gpu.so not built ({path}); run __graft_entry__.build()")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    dp = C.POINTER(C.c_double)
+    L.eslam_config_default.argtypes = [C.POINTER(A.Config)]
+    L.eslam_config_default.restype = None
+    L.eslam_gpu_abi_version.restype = C.c_int
+    L.eslam_gpu_create.argtypes = [C.POINTER(A.Config), C.c_int, C.POINTER(vp)]
+    L.eslam_gpu_destroy.argtypes = [vp]
+    L.eslam_gpu_destroy.restype = None
+    L.eslam_gpu_last_error.argtypes = [vp]
+    L.eslam_gpu_last_error.restype = C.c_char_p
+    L.eslam_gpu_set_stream.argtypes = [vp, vp]
+    L.eslam_gpu_set_map.argtypes = [vp, C.POINTER(A.MlsGrid)]
+    L.eslam_gpu_init_gaussian.argtypes = [vp, C.c_uint64, dp, dp, C.c_double, C.c_double]
+    L.eslam_gpu_init_pose.argtypes = [vp, dp, dp]
+    L.eslam_gpu_upload_particles.argtypes = [vp, C.c_uint64, C.POINTER(A.Particles)]
+    L.eslam_gpu_download_particles.argtypes = [vp, C.POINTER(A.Particles)]
+    L.eslam_gpu_particle_count.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.eslam_gpu_step.argtypes = [vp, C.POINTER(A.StepInput), C.POINTER(C.c_int)]
+    L.eslam_gpu_project.argtypes = [vp, C.POINTER(A.StepInput)]
+    L.eslam_gpu_update.argtypes = [vp, C.POINTER(A.StepInput)]
+    L.eslam_gpu_sync.argtypes = [vp, C.POINTER(A.UpdateInfo)]
+    L.eslam_gpu_get_weights_sum.argtypes = [vp, dp]
+    L.eslam_gpu_normalize_weights.argtypes = [vp, dp]
+    L.eslam_gpu_resample.argtypes = [vp]
+    L.eslam_gpu_get_best_particle_index.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.eslam_gpu_get_centroid.argtypes = [vp, dp, dp]
+    L.eslam_gpu_get_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
+    L.eslam_gpu_set_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
+    L.eslam_gpu_get_ancestors.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
+    L.eslam_gpu_enable_timing.argtypes = [vp, C.c_int]
+    L.eslam_gpu_get_kernel_times.argtypes = [vp, C.POINTER(A.KernelTimes)]
+    L.eslam_gpu_selftest_math.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_uint64]
+    _lib = L
+    return L
+
+
+def _dv(v):
+    return (C.c_double * len(v))(*v)
+
+
+class GpuFilter:
+    """One eslam_ctx: the PoseEstimator / EmbodiedSlamFilter of one GPU."""
+
+    def __init__(self, cfg=None, device=0):
+        self.L = load_library()
+        self.cfg = cfg if cfg is not None else A.default_config()
+        h = C.c_void_p()
+        rc = self.L.eslam_gpu_create(C.byref(self.cfg), device, C.byref(h))
+        if rc != 0:
+            raise EslamError(rc, f"eslam_gpu_create failed ({rc}) -- is an MI355X visible?")
+        self.h = h
+        self._grid = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.eslam_gpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise EslamError(rc, self.L.eslam_gpu_last_error(self.h).decode())
+        return rc
+
+    # -- environment / init -------------------------------------------------------------
+    def set_map(self, grid):
+        self._grid = grid
+        g = grid.view()
+        self._check(self.L.eslam_gpu_set_map(self.h, C.byref(g)))
+
+    def init_gaussian(self, n, mu, sigma, zpos, zsigma):
+        self._check(self.L.eslam_gpu_init_gaussian(self.h, n, _dv(mu), _dv(sigma), zpos, zsigma))
+
+    def init_pose(self, position, orientation):
+        self._check(self.L.eslam_gpu_init_pose(self.h, _dv(position), _dv(orientation)))
+
+    def upload(self, pa):
+        v = pa.view()
+        self._check(self.L.eslam_gpu_upload_particles(self.h, pa.n, C.byref(v)))
+
+    def download(self):
+        n = self.count()
+        pa = A.ParticleArrays(n)
+        v = pa.view()
+        self._check(self.L.eslam_gpu_download_particles(self.h, C.byref(v)))
+        return pa
+
+    def count(self):
+        n = C.c_uint64()
+        self._check(self.L.eslam_gpu_particle_count(self.h, C.byref(n)))
+        return n.value
+
+    # -- hot path -------------------------------------------------------------------------
+    def step(self, st):
+        u = C.c_int(0)
+        self._check(self.L.eslam_gpu_step(self.h, C.byref(st), C.byref(u)))
+        return bool(u.value)
+
+    def project(self, st):
+        self._check(self.L.eslam_gpu_project(self.h, C.byref(st)))
+
+    def update(self, st):
+        self._check(self.L.eslam_gpu_update(self.h, C.byref(st)))
+
+    def sync(self):
+        info = A.UpdateInfo()
+        self._check(self.L.eslam_gpu_sync(self.h, C.byref(info)))
+        return info
+
+    # -- ParticleFilter API ----------------------------------------------------------------
+    def weights_sum(self):
+        s = C.c_double()
+        self._check(self.L.eslam_gpu_get_weights_sum(self.h, C.byref(s)))
+        return s.value
+
+    def normalize(self):
+        e = C.c_double()
+        self._check(self.L.eslam_gpu_normalize_weights(self.h, C.byref(e)))
+        return e.value
+
+    def resample(self):
+        self._check(self.L.eslam_gpu_resample(self.h))
+
+    def best_index(self):
+        i = C.c_uint64()
+        self._check(self.L.eslam_gpu_get_best_particle_index(self.h, C.byref(i)))
+        return i.value
+
+    def centroid(self):
+        p = (C.c_double * 3)()
+        q = (C.c_double * 4)()
+        self._check(self.L.eslam_gpu_get_centroid(self.h, p, q))
+        return list(p), list(q)
+
+    def ancestors(self):
+        n = self.count()
+        out = np.zeros(n, dtype=np.uint32)
+        self._check(self.L.eslam_gpu_get_ancestors(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n))
+        return out
+
+    def rng_state(self):
+        s = A.RngState()
+        self._check(self.L.eslam_gpu_get_rng_state(self.h, C.byref(s)))
+        return s
+
+    def set_rng_state(self, s):
+        self._check(self.L.eslam_gpu_set_rng_state(self.h, C.byref(s)))
+
+    def enable_timing(self, on=True):
+        self._check(self.L.eslam_gpu_enable_timing(self.h, 1 if on else 0))
+
+    def kernel_times(self):
+        t = A.KernelTimes()
+        self._check(self.L.eslam_gpu_get_kernel_times(self.h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in t._fields_}
+
+
+def selftest_math(fn, x, y=None, device=0):
+    L = load_library()
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros_like(x)
+    yp = None
+    if y is not None:
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        yp = y.ctypes.data_as(C.POINTER(C.c_double))
+    rc = L.eslam_gpu_selftest_math(device, fn, x.ctypes.data_as(C.POINTER(C.c_double)), yp,
+                                   out.ctypes.data_as(C.POINTER(C.c_double)), x.shape[0])
+    if rc != 0:
+        raise EslamError(rc, "selftest_math failed")
+    return out

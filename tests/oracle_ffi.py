@@ -1,0 +1,214 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so) -- test infrastructure."""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "slam-eslam_amd"))
+import eslam_abi as A  # noqa: E402
+
+LIB_PATH = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+
+SUM_CONTRACT = 0
+SUM_REFERENCE = 1
+
+
+class CPoint(C.Structure):
+    _fields_ = [("point", C.c_double * 3), ("zdiff", C.c_double), ("zvar", C.c_double), ("prob", C.c_double)]
+
+
+class ContactModelS(C.Structure):
+    _fields_ = [
+        ("use_slip_update", C.c_int32), ("use_shape_update", C.c_int32),
+        ("min_contacts", C.c_uint64), ("correction", C.c_double), ("radius", C.c_double),
+        ("m", C.c_uint32),
+        ("pos", (C.c_double * 3) * A.MAX_CONTACTS),
+        ("contact", C.c_float * A.MAX_CONTACTS),
+        ("group", C.c_int32 * A.MAX_CONTACTS),
+        ("ncp", C.c_uint32),
+        ("cp", CPoint * A.MAX_CONTACTS),
+        ("zdelta", C.c_double), ("zvar", C.c_double), ("weight", C.c_double), ("posevar", C.c_double),
+        ("nlow", C.c_uint32),
+        ("low", (C.c_double * 3) * A.MAX_CONTACTS),
+    ]
+
+
+MAPFN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_double, C.c_double,
+                    C.POINTER(C.c_double), C.POINTER(C.c_double))
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.or_create.restype = vp
+    L.or_create.argtypes = [C.POINTER(A.Config), C.c_int]
+    L.or_destroy.argtypes = [vp]
+    L.or_set_map.argtypes = [vp, C.POINTER(A.MlsGrid)]
+    L.or_init_gaussian.argtypes = [vp, C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double, C.c_double]
+    L.or_init_pose.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_upload.argtypes = [vp, C.c_uint64, C.POINTER(A.Particles)]
+    L.or_download.argtypes = [vp, C.POINTER(A.Particles)]
+    L.or_count.restype = C.c_uint64
+    L.or_count.argtypes = [vp]
+    for fn in ("or_project", "or_update"):
+        getattr(L, fn).argtypes = [vp, C.POINTER(A.StepInput)]
+    L.or_step.argtypes = [vp, C.POINTER(A.StepInput), C.POINTER(C.c_int)]
+    L.or_last_info.argtypes = [vp, C.POINTER(A.UpdateInfo)]
+    L.or_get_weights_sum.restype = C.c_double
+    L.or_get_weights_sum.argtypes = [vp]
+    L.or_normalize_weights.restype = C.c_double
+    L.or_normalize_weights.argtypes = [vp]
+    L.or_resample.argtypes = [vp]
+    L.or_resample_multinomial.argtypes = [vp, C.c_uint64]
+    L.or_best_index.restype = C.c_uint64
+    L.or_best_index.argtypes = [vp]
+    L.or_get_centroid.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_get_ancestors.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
+    L.or_get_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
+    L.or_set_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
+    L.or_get_debug.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(CPoint), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_cm_init.argtypes = [C.POINTER(ContactModelS), C.POINTER(A.Config)]
+    L.or_cm_set_contact_points.argtypes = [C.POINTER(ContactModelS), C.c_uint32, C.POINTER(A.ContactPoint), C.POINTER(C.c_double)]
+    L.or_cm_evaluate_pose.argtypes = [C.POINTER(ContactModelS), C.POINTER(C.c_double), C.c_double, MAPFN, C.c_void_p]
+    L.or_cm_update_z.argtypes = [C.POINTER(ContactModelS), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_cm_lowest_points.restype = C.c_uint32
+    L.or_cm_lowest_points.argtypes = [C.POINTER(ContactModelS), C.POINTER(C.c_double)]
+    L.or_cm_update_contact_state_lph.argtypes = [C.POINTER(ContactModelS)]
+    L.or_surface_param_from_points.argtypes = [C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_bucket_index.restype = C.c_int
+    L.or_bucket_index.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double]
+    L.or_mls_get_patch.argtypes = [C.POINTER(A.MlsGrid), C.POINTER(C.c_double), C.c_double, C.c_double,
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_dm.restype = C.c_double
+    L.or_dm.argtypes = [C.c_int, C.c_double, C.c_double]
+    L.or_dm_philox.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.or_dm_philox_raw.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.or_dm_minstd_jump.restype = C.c_uint32
+    L.or_dm_minstd_jump.argtypes = [C.c_uint32, C.c_uint64]
+    L.or_dm_limbs_to_double.restype = C.c_double
+    L.or_dm_limbs_to_double.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    L.or_dm_fx128.argtypes = [C.c_double, C.c_int, C.POINTER(C.c_uint32)]
+    _lib = L
+    return L
+
+
+def dvec(v):
+    return (C.c_double * len(v))(*v)
+
+
+class OracleFilter:
+    """The oracle PoseEstimator / EmbodiedSlamFilter."""
+
+    def __init__(self, cfg, sum_mode=SUM_CONTRACT):
+        self.L = lib()
+        self.cfg = cfg
+        self.h = self.L.or_create(C.byref(cfg), sum_mode)
+        self._map = None
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.or_destroy(self.h)
+            self.h = None
+
+    def set_map(self, grid):
+        self._map = grid
+        g = grid.view()
+        assert self.L.or_set_map(self.h, C.byref(g)) == 0
+
+    def init_gaussian(self, n, mu, sigma, z, zs):
+        assert self.L.or_init_gaussian(self.h, n, dvec(mu), dvec(sigma), z, zs) == 0
+
+    def init_pose(self, pos, q):
+        assert self.L.or_init_pose(self.h, dvec(pos), dvec(q)) == 0
+
+    def upload(self, pa):
+        v = pa.view()
+        assert self.L.or_upload(self.h, pa.n, C.byref(v)) == 0
+
+    def download(self):
+        n = self.L.or_count(self.h)
+        pa = A.ParticleArrays(n)
+        v = pa.view()
+        assert self.L.or_download(self.h, C.byref(v)) == 0
+        return pa
+
+    def count(self):
+        return self.L.or_count(self.h)
+
+    def project(self, st):
+        return self.L.or_project(self.h, C.byref(st))
+
+    def update(self, st):
+        return self.L.or_update(self.h, C.byref(st))
+
+    def step(self, st):
+        u = C.c_int(0)
+        rc = self.L.or_step(self.h, C.byref(st), C.byref(u))
+        assert rc == 0, rc
+        return bool(u.value)
+
+    def info(self):
+        i = A.UpdateInfo()
+        self.L.or_last_info(self.h, C.byref(i))
+        return i
+
+    def weights_sum(self):
+        return self.L.or_get_weights_sum(self.h)
+
+    def normalize(self):
+        return self.L.or_normalize_weights(self.h)
+
+    def resample(self):
+        self.L.or_resample(self.h)
+
+    def best_index(self):
+        return self.L.or_best_index(self.h)
+
+    def centroid(self):
+        p = (C.c_double * 3)()
+        q = (C.c_double * 4)()
+        self.L.or_get_centroid(self.h, p, q)
+        return list(p), list(q)
+
+    def ancestors(self):
+        n = self.count()
+        out = np.zeros(n, dtype=np.uint32)
+        rc = self.L.or_get_ancestors(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n)
+        return out if rc == 0 else None
+
+    def rng_state(self):
+        s = A.RngState()
+        self.L.or_get_rng_state(self.h, C.byref(s))
+        return s
+
+    def set_rng_state(self, s):
+        self.L.or_set_rng_state(self.h, C.byref(s))
+
+    def debug(self):
+        n = self.count()
+        ncp = np.zeros(n, dtype=np.uint32)
+        cp = (CPoint * (n * A.MAX_CONTACTS))()
+        zd = np.zeros(n)
+        zv = np.zeros(n)
+        self.L.or_get_debug(self.h, ncp.ctypes.data_as(C.POINTER(C.c_uint32)), cp,
+                            zd.ctypes.data_as(C.POINTER(C.c_double)), zv.ctypes.data_as(C.POINTER(C.c_double)))
+        return ncp, cp, zd, zv
+
+
+def dm(fn, x, y=0.0):
+    return lib().or_dm(fn, x, y)

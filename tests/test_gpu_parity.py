@@ -1,0 +1,188 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the same seeded
+inputs.  Bit-exact on every particle field, the update info and the resample ancestors."""
+import math
+
+import numpy as np
+import pytest
+
+import eslam_abi as A
+import oracle_ffi as O
+import synthetic as S
+from parity_util import assert_bit_identical, info_tuple, run_pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu_mod():
+    import eslam_amd
+    eslam_amd.load_library()
+    return eslam_amd
+
+
+@pytest.fixture(scope="module")
+def flat_grid():
+    return S.flat_map(cells=200)
+
+
+@pytest.fixture(scope="module")
+def rough_grid():
+    return S.rough_map(cells=200)
+
+
+def factory(gpu_mod):
+    return lambda cfg: gpu_mod.GpuFilter(cfg)
+
+
+@pytest.mark.parametrize("fn,lo,hi", [(0, -740, 700), (1, 1e-300, 1e300), (2, -50, 50), (3, -50, 50), (4, -8, 27),
+                                      (5, 0, 1e10), (8, 0, 1.5), (9, 0, 1.9)])
+def test_gpu_math_bit_identical(gpu_mod, oracle, fn, lo, hi):
+    rng = np.random.default_rng(fn)
+    x = rng.uniform(lo, hi, 20000) if fn != 1 else np.exp(rng.uniform(-690, 690, 20000))
+    y = rng.uniform(0, 4, 20000)
+    if fn == 8:
+        y = np.where(rng.random(20000) < 0.5, np.floor(y), 1.0 / rng.integers(1, 9, 20000))
+    got = gpu_mod.selftest_math(fn, x, y)
+    want = np.array([oracle.dm(fn, float(a), float(b)) for a, b in zip(x, y)])
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), f"fn {fn}: {np.count_nonzero(got != want)} differ"
+
+
+def test_gpu_div_and_ratio(gpu_mod, oracle):
+    rng = np.random.default_rng(7)
+    x = rng.normal(size=20000) * 10.0 ** rng.uniform(-5, 5, 20000)
+    y = 10.0 ** rng.uniform(-3, 3, 20000)
+    for fn in (6, 7):
+        got = gpu_mod.selftest_math(fn, x, y)
+        want = np.array([oracle.dm(fn, float(a), float(b)) for a, b in zip(x, y)])
+        assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_flat_forced_resample(gpu_mod, flat_grid):
+    cfg = S.bench_config(A.default_config(), 1000)
+    run_pair(cfg, flat_grid, S.step_stream(8), 1000, gpu_factory=factory(gpu_mod), label="flat")
+
+
+def test_rough_tilted_natural_gate(gpu_mod, rough_grid):
+    cfg = A.default_config()
+    cfg.particle_count = 3000
+    run_pair(cfg, rough_grid, S.step_stream(25, tilt=True), 3000, gpu_factory=factory(gpu_mod), label="rough")
+
+
+def test_rough_forced_every_step_ragged(gpu_mod, rough_grid):
+    n = 4097                       # not a multiple of 64 or of the 2048-particle scan tile
+    cfg = S.bench_config(A.default_config(), n)
+    run_pair(cfg, rough_grid, S.step_stream(6, tilt=True), n, gpu_factory=factory(gpu_mod), label="ragged")
+
+
+def test_grouped_nan_contacts_and_misses(gpu_mod, rough_grid):
+    # 8 contacts in 4 groups of 2 (asguard-like wheels), NaN = unknown contact probability
+    feet = [(0.3, 0.1, -0.18), (0.3, -0.1, -0.2), (-0.3, 0.1, -0.18), (-0.3, -0.1, -0.22),
+            (0.3, -0.5, -0.18), (0.3, -0.7, -0.19), (-0.3, -0.5, -0.18), (-0.3, -0.7, -0.25)]
+    groups = [0, 0, 1, 1, 2, 2, 3, 3]
+    contact = lambda s, i: float("nan") if (s + i) % 3 == 0 else (0.1 if (s * 7 + i) % 5 == 0 else 0.9)
+    stream = S.step_stream(10, tilt=True, feet=feet, groups=groups, contact=contact, ltc=1)
+    cfg = A.default_config()
+    cfg.particle_count = 2000
+    cfg.min_contacts = 2
+    run_pair(cfg, rough_grid, stream, 2000, init=dict(mu=[0, 0, 0], sigma=[3.0, 3.0, 1.0], z=0.18, zs=0.3),
+             gpu_factory=factory(gpu_mod), label="grouped")
+
+
+def test_particles_leaving_the_map(gpu_mod):
+    grid = S.flat_map(cells=20)    # 2 x 2 m map: most feet miss (GridAccess::get false)
+    cfg = S.bench_config(A.default_config(), 1500)
+    run_pair(cfg, grid, S.step_stream(6), 1500, init=dict(mu=[0.5, 0.5, 0], sigma=[1.5, 1.5, 0.5], z=0.18, zs=0.5),
+             gpu_factory=factory(gpu_mod), label="offmap")
+
+
+def test_all_floating_uniform_reset(gpu_mod):
+    grid = S.flat_map(cells=20)
+    cfg = A.default_config()
+    cfg.particle_count = 700
+    # every particle far away from the map: no contact points, data_particles == 0;
+    # initial weights are 0 (Q3) so normalizeWeights takes the uniform branch
+    run_pair(cfg, grid, S.step_stream(4, ltc=1), 700, init=dict(mu=[40, 40, 0], sigma=[0.1, 0.1, 0.1], z=0.18, zs=1.0),
+             gpu_factory=factory(gpu_mod), label="uniform")
+
+
+def test_uploaded_large_weights(gpu_mod, rough_grid):
+    n = 2500
+    rng = np.random.default_rng(5)
+    pa = A.ParticleArrays(n)
+    pa.x[:] = rng.normal(0, 0.2, n)
+    pa.y[:] = rng.normal(0, 0.2, n)
+    pa.orientation[:] = rng.normal(0, 0.1, n)
+    pa.zpos[:] = 0.18
+    pa.zsigma[:] = 0.2
+    pa.weight[:] = rng.uniform(0, 37.5, n)      # unnormalised, > 1: exercises the weight exponent
+    pa.floating[:] = 1
+    cfg = S.bench_config(A.default_config(), n)
+    run_pair(cfg, rough_grid, S.step_stream(5, tilt=True), n, init=pa, gpu_factory=factory(gpu_mod), label="upload")
+
+
+def test_project_then_update_separately(gpu_mod, flat_grid):
+    cfg = S.bench_config(A.default_config(), 1200)
+    stream = S.step_stream(4)
+    gpu, orc = run_pair(cfg, flat_grid, stream, 1200, gpu_factory=factory(gpu_mod), mode="project", label="project")
+    for k, st in enumerate(stream):
+        orc.update(st)
+        gpu.update(st)
+        gpu.sync()
+        assert_bit_identical(gpu.download(), orc.download(), f"update {k}")
+        assert info_tuple(gpu.sync()) == info_tuple(orc.info())
+
+
+def test_particle_filter_api(gpu_mod, rough_grid):
+    """getWeightsSum, normalizeWeights, resample (unnormalised weights), getBestParticleIndex,
+    getCentroid (src/ParticleFilter.hpp:34-173, src/PoseEstimator.cpp:354-383)."""
+    n = 3333
+    rng = np.random.default_rng(11)
+    pa = A.ParticleArrays(n)
+    pa.x[:] = rng.normal(0, 1, n)
+    pa.y[:] = rng.normal(0, 1, n)
+    pa.orientation[:] = rng.normal(0, 0.3, n)
+    pa.zpos[:] = rng.normal(0.2, 0.01, n)
+    pa.zsigma[:] = 0.1
+    pa.weight[:] = np.exp(-0.5 * (pa.x ** 2 + pa.y ** 2)) / math.sqrt(2 * math.pi)   # like UnitTest.cpp's tracker
+    pa.weight[17] = pa.weight.max()                                                   # tie: first max wins
+    cfg = A.default_config()
+    cfg.flags |= A.FLAG_RECORD_ANCESTORS
+    orc = O.OracleFilter(cfg)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc.upload(pa)
+    gpu.upload(pa)
+    assert gpu.weights_sum() == orc.weights_sum()
+    assert gpu.best_index() == orc.best_index()
+    gpu.resample()
+    orc.resample()
+    gpu.sync()
+    assert np.array_equal(gpu.ancestors(), orc.ancestors())
+    assert_bit_identical(gpu.download(), orc.download(), "resample")
+    assert gpu.normalize() == orc.normalize()
+    assert_bit_identical(gpu.download(), orc.download(), "normalize")
+    assert gpu.count() == n
+
+
+def test_rng_state_resume(gpu_mod, flat_grid):
+    cfg = S.bench_config(A.default_config(), 1000)
+    stream = S.step_stream(6)
+    a = gpu_mod.GpuFilter(cfg)
+    a.set_map(flat_grid)
+    a.init_gaussian(1000, [0, 0, 0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    for st in stream[:3]:
+        a.step(st)
+    a.sync()
+    snap = a.download()
+    rs = a.rng_state()
+    for st in stream[3:]:
+        a.step(st)
+    a.sync()
+    b = gpu_mod.GpuFilter(cfg)
+    b.set_map(flat_grid)
+    b.upload(snap)
+    b.set_rng_state(rs)
+    # upload re-derives the weight exponent; the snapshot weights are normalised (exp 1)
+    for st in stream[3:]:
+        b.step(st)
+    b.sync()
+    assert_bit_identical(b.download(), a.download(), "resume")
