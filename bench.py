@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Benchmark of the eSLAM per-step particle-filter hot path on MI355X.
+
+Metric (BASELINE.json): M particle-updates/s (predict+weight+resample) @ 1/2/4/8 MI355X.
+One step = EmbodiedSlamFilter::update on one batch of synthetic odometry + 4 foot contacts:
+project (predict) -> updateWeights (contact model against the MLS map) -> normalizeWeights ->
+stratified resample, forced every step (minEffective = N + 1, measurement gate forced).
+Workload at N=1: BASELINE configs[2] -- 4M particles, 100 x 100 m MLS map @ 0.1 m.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--particles P]
+
+For N > 1 launch with torch.distributed.run (one process per GPU); each rank holds
+P particles of one global filter (weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "slam-eslam_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+# algorithmic bytes per particle-update (DESIGN.md "roofline")
+BYTES_PREDICT_WEIGHT = 96     # read 6 x f64 state, write 6 x f64
+BYTES_NORMALIZE = 8
+BYTES_RESAMPLE = 104          # scan read 8 + gather 48 + write 48
+BYTES_TOTAL = BYTES_PREDICT_WEIGHT + BYTES_NORMALIZE + BYTES_RESAMPLE
+HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--particles", type=int, default=4 * 1024 * 1024, help="particles per GPU")
+    ap.add_argument("--map-cells", type=int, default=1000)
+    ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=131072, help="particles in the CPU baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=4)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, grid, stream):
+    """The CPU oracle (a restatement of the reference path, reference-order double sums),
+    single-threaded on this host, on a bounded sample of the same workload."""
+    import eslam_abi as A
+    import oracle_ffi as O
+    import synthetic as S
+    n = args.cpu_sample
+    cfg = S.bench_config(A.default_config(), n)
+    f = O.OracleFilter(cfg, O.SUM_REFERENCE)
+    f.set_map(grid)
+    f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    f.step(stream[0])                     # first step (uniform reset) untimed
+    t0 = time.perf_counter()
+    k = 0
+    for st in stream[1:1 + args.cpu_steps]:
+        f.step(st)
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": 1, "kind": "port",
+            "sample": f"{n} particles x {k} steps of the same workload (flat map, forced update+resample), "
+                      f"oracle/eslam_oracle.c in reference-sum mode, 1 thread, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    import numpy as np
+    import eslam_abi as A
+    import eslam_amd
+    import synthetic as S
+
+    n = args.particles
+    grid = S.rough_map(cells=args.map_cells) if args.rough else S.flat_map(cells=args.map_cells)
+    stream = S.step_stream(args.warmup + args.steps + 1)
+    cfg = S.bench_config(A.default_config(), n * world)
+    f = eslam_amd.GpuFilter(cfg, device=local_rank if world > 1 else 0)
+    f.set_map(grid)
+    f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+
+    def barrier():
+        f.sync()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for st in stream[:args.warmup]:
+        f.step(st)
+    barrier()
+    f.enable_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for st in stream[args.warmup:args.warmup + args.steps]:
+        f.step(st)
+    info = f.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    kt = f.kernel_times()
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    total_updates = n * world * args.steps
+    value = total_updates / dt / 1e6
+    ms_step = dt / args.steps * 1e3
+
+    # roofline of the dominant kernel (HIP events around every launch of the timed region)
+    per_kernel = {"k_project_weight": (kt["project_weight_ms"], BYTES_PREDICT_WEIGHT),
+                  "k_normalize_scan": (kt["normalize_scan_ms"], BYTES_NORMALIZE + 8),
+                  "k_resample_gather": (kt["resample_ms"], BYTES_RESAMPLE - 8)}
+    dom = max(per_kernel, key=lambda k: per_kernel[k][0])
+    dom_ms, dom_bytes = per_kernel[dom]
+    achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    result = {
+        "metric": "M particle-updates/s (predict+weight+resample) @ 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "M particle-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (flat 100x100 m MLS map @0.1 m; odometry + 4 foot contacts per step)",
+        "config": {"workload": "configs[2]: %d particles/GPU, 1 MI355X per rank, MLS %dx%d @0.1 m, 4 contacts, "
+                               "resample forced every step" % (n, args.map_cells, args.map_cells),
+                   "particles_per_gpu": n, "global_particles": n * world,
+                   "parallelism": "dp%d (particle shards)" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_particle": dom_bytes,
+                     "avg_launch_ms": round(dom_ms, 5)},
+        "kernel_ms": {k: round(v, 5) for k, v in kt.items()},
+        "step_roofline_frac": round(BYTES_TOTAL * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "last_update": {"effective": info.effective, "resampled": info.resampled},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, grid, stream)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    f.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -211,7 +211,9 @@ struct eslam_ctx {
     // diagnostics
     std::string err;
     bool timing = false;
-    hipEvent_t ev[5] = {};
+    hipEvent_t ev[5] = {};                  // events of the step being recorded
+    std::vector<hipEvent_t> ring;           // 5 events per recorded step (timing mode)
+    uint32_t ring_steps = 0;
     eslam_kernel_times times = {};
 };
 
@@ -223,6 +225,22 @@ struct eslam_ctx {
             return ESLAM_ERR_HIP;                                                            \
         }                                                                                    \
     } while (0)
+
+static constexpr uint32_t kRingSteps = 2048;
+
+// timing mode: event k (0..4) of the current step, kept in a ring so a whole timed region
+// of back-to-back steps is measured without synchronising between steps
+static void rec(eslam_ctx* ctx, int k)
+{
+    if (!ctx->timing) return;
+    if (ctx->ring.empty()) {
+        ctx->ring.resize(5 * kRingSteps);
+        for (auto& e : ctx->ring) hipEventCreate(&e);
+    }
+    if (ctx->ring_steps >= kRingSteps) return;
+    hipEventRecord(ctx->ring[5 * ctx->ring_steps + k], ctx->stream);
+    if (k == 4) ctx->ring_steps++;
+}
 
 static int fail(eslam_ctx* ctx, int code, const char* msg)
 {
@@ -362,6 +380,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     hipFree(ctx->shards); hipFree(ctx->ctl); hipHostFree(ctx->ctl_host); hipFree(ctx->jump);
     hipFree(ctx->scratch); hipHostFree(ctx->scratch_host);
     for (auto& e : ctx->ev) if (e) hipEventDestroy(e);
+    for (auto& e : ctx->ring) if (e) hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -625,20 +644,20 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
     return fp;
 }
 
-static int run_update_tail(eslam_ctx* ctx, uint32_t mode)
+static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const FinParams fp = fin_params(ctx, mode);
     HIPCHK(ctx, eslam_launch_finalize(ctx->shards, ctx->ctl, &fp, ctx->stream));
-    if (ctx->timing) hipEventRecord(ctx->ev[2], ctx->stream);
+    if (timed) rec(ctx, 2);
     const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
                                             ctx->jump, ctx->stream));
-    if (ctx->timing) hipEventRecord(ctx->ev[3], ctx->stream);
+    if (timed) rec(ctx, 3);
     const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
     const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
     HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->marks, ctx->tile_first, ctx->status,
                                              ctx->anc, record, aux, ctx->stream));
-    if (ctx->timing) hipEventRecord(ctx->ev[4], ctx->stream);
+    if (timed) rec(ctx, 4);
     if (record) ctx->has_anc = true;
     return ESLAM_OK;
 }
@@ -650,12 +669,13 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     StepParams p;
     fill_step_params(ctx, in, p);
     p.proj_event = ctx->proj_event;
-    if (ctx->timing) hipEventRecord(ctx->ev[0], ctx->stream);
+    rec(ctx, 0);
     HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
                                             ctx->shards, ctx->stream));
-    if (ctx->timing) hipEventRecord(ctx->ev[1], ctx->stream);
+    rec(ctx, 1);
     if (project) ctx->proj_event++;
-    if (weight) return run_update_tail(ctx, FIN_UPDATE);
+    if (weight) return run_update_tail(ctx, FIN_UPDATE, true);
+    rec(ctx, 2); rec(ctx, 3); rec(ctx, 4);
     return ESLAM_OK;
 }
 
@@ -709,13 +729,22 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         info->resample_overruns = c.overruns;
         info->update_count = c.update_count;
     }
-    if (ctx->timing) {
+    if (ctx->timing && ctx->ring_steps) {
+        double acc[5] = {0, 0, 0, 0, 0};
+        for (uint32_t k = 0; k < ctx->ring_steps; ++k) {
+            hipEvent_t* e = &ctx->ring[5 * k];
+            float ms;
+            for (int j = 0; j < 4; ++j) { ms = 0; hipEventElapsedTime(&ms, e[j], e[j + 1]); acc[j] += ms; }
+            ms = 0; hipEventElapsedTime(&ms, e[0], e[4]); acc[4] += ms;
+        }
         eslam_kernel_times& t = ctx->times;
-        hipEventElapsedTime(&t.project_weight_ms, ctx->ev[0], ctx->ev[1]);
-        hipEventElapsedTime(&t.finalize_ms, ctx->ev[1], ctx->ev[2]);
-        hipEventElapsedTime(&t.normalize_scan_ms, ctx->ev[2], ctx->ev[3]);
-        hipEventElapsedTime(&t.resample_ms, ctx->ev[3], ctx->ev[4]);
-        hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[4]);
+        const double inv = 1.0 / ctx->ring_steps;
+        t.project_weight_ms = (float)(acc[0] * inv);
+        t.finalize_ms = (float)(acc[1] * inv);
+        t.normalize_scan_ms = (float)(acc[2] * inv);
+        t.resample_ms = (float)(acc[3] * inv);
+        t.total_ms = (float)(acc[4] * inv);
+        ctx->ring_steps = 0;
     }
     if (c.err & 1ull) {
         ctx->ctl_host->err = 0;
@@ -739,7 +768,7 @@ static int standalone(eslam_ctx* ctx, uint32_t mode)
         HIPCHK(ctx, eslam_launch_finalize(ctx->shards, ctx->ctl, &fp, ctx->stream));
         return ESLAM_OK;
     }
-    return run_update_tail(ctx, mode);
+    return run_update_tail(ctx, mode, false);
 }
 
 extern "C" int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum)
@@ -845,7 +874,9 @@ extern "C" int eslam_gpu_get_ancestors(eslam_ctx* ctx, uint32_t* out, uint64_t n
 extern "C" int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->timing = enable != 0;
+    ctx->ring_steps = 0;
     return ESLAM_OK;
 }
 
