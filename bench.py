@@ -39,18 +39,19 @@ def parse():
     ap.add_argument("--map-cells", type=int, default=1000)
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=131072, help="particles in the CPU baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--cpu-sample", type=int, default=1048576, help="particles in the CPU baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=48)
     return ap.parse_args()
 
 
-def cpu_baseline(args, grid, stream):
+def cpu_baseline(args, grid):
     """The CPU oracle (a restatement of the reference path, reference-order double sums),
     single-threaded on this host, on a bounded sample of the same workload."""
     import eslam_abi as A
     import oracle_ffi as O
     import synthetic as S
     n = args.cpu_sample
+    stream = S.step_stream(args.cpu_steps + 1)
     cfg = S.bench_config(A.default_config(), n)
     f = O.OracleFilter(cfg, O.SUM_REFERENCE)
     f.set_map(grid)
@@ -154,7 +155,7 @@ def main():
         "last_update": {"effective": info.effective, "resampled": info.resampled},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, grid, stream)
+        result["cpu_baseline"] = cpu_baseline(args, grid)
     if rank == 0:
         print(json.dumps(result), flush=True)
     f.close()

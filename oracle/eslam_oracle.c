@@ -151,9 +151,11 @@ static void set_translation_pose(double ud[12], double x, double y, double z)
 /* ========================================================================================
  * MLS grid: envire::MLSGrid::getPatch(p, patch, sigma_threshold = 3.0)
  * ====================================================================================== */
-/* The query patch (src/ContactModel.cpp:151) has mean = point z; it is compared in the
- * grid frame, i.e. against the local z of the transformed point.                        */
-int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_world, double q_stdev,
+/* The query patch (src/ContactModel.cpp:151) has mean = point z and variance measVar; it
+ * is compared in the grid frame, i.e. against the local z of the transformed point.  The
+ * 3-sigma test is |mean_p - mean_q| < 3 sqrt(stdev_p^2 + measVar), evaluated squared.
+ * Cell index (toGrid): floor((x - offset) * (1 / scale)).                               */
+int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_world, double q_var,
                      double* mean, double* stdev)
 {
     const double* A = g->global2local;
@@ -162,12 +164,12 @@ int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_w
     double lz = ((A[8] * p[0] + A[9] * p[1]) + A[10] * p[2]) + A[11];
     const double q_mean = lz;
     (void)q_mean_world;
-    double fm = floor((lx - g->offset_x) / g->scale_x);
-    double fn = floor((ly - g->offset_y) / g->scale_y);
+    const double inv_x = 1.0 / g->scale_x, inv_y = 1.0 / g->scale_y;
+    double fm = floor((lx - g->offset_x) * inv_x);
+    double fn = floor((ly - g->offset_y) * inv_y);
     if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) return 0;
     uint64_t cell = (uint64_t)fn * g->width + (uint64_t)fm;
     uint32_t b = g->cell_start[cell], e = g->cell_start[cell + 1];
-    double qv = q_stdev * q_stdev;
     for (uint32_t k = b; k < e; ++k) {
         double pm = (double)g->patch_mean[k];
         double ps = (double)g->patch_stdev[k];
@@ -180,15 +182,14 @@ int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_w
         } else {
             diff = fabs(pm - q_mean);
         }
-        double d = diff / sqrt(ps * ps + qv);
-        if (d < 3.0) { *mean = pm; *stdev = ps; return 1; }
+        if (diff * diff < 9.0 * (ps * ps + q_var)) { *mean = pm; *stdev = ps; return 1; }
     }
     return 0;
 }
 
-static int grid_map_fn(void* user, const double p[3], double q_mean, double q_stdev, double* mean, double* stdev)
+static int grid_map_fn(void* user, const double p[3], double q_mean, double q_var, double* mean, double* stdev)
 {
-    return or_mls_get_patch((const eslam_mls_grid*)user, p, q_mean, q_stdev, mean, stdev);
+    return or_mls_get_patch((const eslam_mls_grid*)user, p, q_mean, q_var, mean, stdev);
 }
 
 /* ========================================================================================
@@ -224,25 +225,39 @@ static double contact_likelihood_ratio(const or_contact_model* cm, double z, dou
     return dm_normal_pdf_cdf_ratio(z, sigma * cm->correction);
 }
 
-/* ContactModel::evaluateWeight  src/ContactModel.cpp:262-317 */
+/* ContactModel::evaluateWeight  src/ContactModel.cpp:262-317, restated at the rounding
+ * level: 1/zvar is formed once per point (d1 += zdiff * (1/zvar); odiff = (zdiff - delta) *
+ * sqrt(1/zvar)) and the product of exp(-odiff^2 / 2) is one exp of the summed squares.
+ * The sum is kept (shape_s2) so that m^(1/n) = exp(-s2 / (2 n)) needs no log.           */
 static void evaluate_weight(or_contact_model* cm)
 {
     double d1 = 0, d2 = 0;
+    double iv[ESLAM_MAX_CONTACTS];
     for (uint32_t i = 0; i < cm->ncp; ++i) {
-        d1 += cm->cp[i].zdiff / cm->cp[i].zvar;
-        d2 += 1.0 / cm->cp[i].zvar;
+        iv[i] = 1.0 / cm->cp[i].zvar;
+        d1 += cm->cp[i].zdiff * iv[i];
+        d2 += iv[i];
     }
     const double delta = d1 / d2;
-    double pz = 1.0;
+    double s2 = 0.0;
     for (uint32_t i = 0; i < cm->ncp; ++i) {
-        const double odiff = (cm->cp[i].zdiff - delta) / sqrt(cm->cp[i].zvar);
-        const double zk = dm_exp(-(odiff * odiff) / (2.0));
-        if (cm->use_shape_update) pz *= zk;
-        if (cm->use_slip_update) pz *= cm->cp[i].prob;
+        const double odiff = (cm->cp[i].zdiff - delta) * sqrt(iv[i]);
+        s2 += odiff * odiff;
     }
-    cm->weight = pz;
+    /* useSlipUpdate multiplies by p.prob, which is always 1 at push time (Q8) */
+    cm->shape_s2 = s2;
+    cm->weight = cm->use_shape_update ? dm_exp(-0.5 * s2) : 1.0;
     cm->zdelta = -delta;
     cm->zvar = 1.0 / d2;
+}
+
+/* contactLikelihoodRatio(z, sigma) > 1e-9 guaranteed (exact-arithmetic bounds with a wide
+ * margin): for a group of ONE evaluated point the ratio cancels,
+ * (zdiff*r)/r = zdiff, and is not evaluated (rounding-level restatement)                */
+static int ratio_surely_significant(double z, double s)
+{
+    if (z <= 0.0) return s < 1e8;                  /* ratio >= sqrt(2/pi)/s            */
+    return s < 40.0 && z < 5.6 * s;                /* ratio >= 0.399 exp(-16) / s      */
 }
 
 /* ContactModel::evaluatePose  src/ContactModel.cpp:117-224 (group quirk Q7 kept) */
@@ -255,7 +270,6 @@ int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_va
     const double contact_threshold = 0.2;
     double contact_ratio = 0, pose_var_avg = 0;
     cm->posevar = 0;
-    const double q_stdev = sqrt(meas_var);
     for (uint32_t i = 0; i < cm->m; ++i) {
         const int32_t gid = cm->group[i];
         const double* c = cm->pos[i];
@@ -269,11 +283,27 @@ int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_va
         const float cp = cm->contact[i];
         if (group_valid && !((double)cp < contact_threshold)) {
             double mean, stdev;
-            if (map(user, w, w[2], q_stdev, &mean, &stdev)) {
+            if (map(user, w, w[2], meas_var, &mean, &stdev)) {
                 const double zdiff = w[2] - mean;
                 const double pose_var = stdev * stdev;
                 const double zvar = stdev * stdev + meas_var;
-                const double ratio = contact_likelihood_ratio(cm, zdiff, sqrt(zvar));
+                const double sq = sqrt(zvar);
+                const int ends = (gid == -1 || i + 1 == cm->m || gid != cm->group[i + 1]);
+                if (!valid && ends && ratio_surely_significant(zdiff, sq * cm->correction)) {
+                    /* single-point group: push (zdiff, zvar) directly */
+                    p.point[0] = w[0]; p.point[1] = w[1]; p.point[2] = mean;
+                    p.zdiff = zdiff;
+                    p.zvar = zvar;
+                    p.prob = 1.0;
+                    cm->posevar += pose_var;
+                    cm->cp[cm->ncp++] = p;
+                    group_valid = 1;
+                    valid = 0;
+                    pose_var_avg = 0;
+                    contact_ratio = 0;
+                    continue;
+                }
+                const double ratio = contact_likelihood_ratio(cm, zdiff, sq);
                 if (!valid) {
                     p.point[0] = w[0]; p.point[1] = w[1]; p.point[2] = mean;
                     p.zdiff = zdiff * ratio;
@@ -294,9 +324,10 @@ int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_va
         }
         if (valid && (gid == -1 || i + 1 == cm->m || gid != cm->group[i + 1])) {
             if (group_valid && contact_ratio > 1e-9) {
-                p.zdiff /= contact_ratio;
-                p.zvar /= contact_ratio;
-                cm->posevar += pose_var_avg / contact_ratio;
+                const double inv = 1.0 / contact_ratio;
+                p.zdiff *= inv;
+                p.zvar *= inv;
+                cm->posevar += pose_var_avg * inv;
                 cm->cp[cm->ncp++] = p;
                 /* useSlipUpdate: p.prob *= matchTerrain(...) happens after the push (Q8) */
             }
@@ -320,7 +351,8 @@ int or_cm_update_z(const or_contact_model* cm, double* z_pos, double* z_var)
     double a = *z_var - pose_var;
     double delta_var = (a < 1e-9) ? 1e-9 : a;         /* std::max(a, 1e-9) */
     const double z_delta = cm->zdelta;
-    if (fabs(z_delta / sqrt(delta_var)) > 1.0) return 0;
+    /* |z_delta / sqrt(delta_var)| > 1 (the "3-sigma" gate is 1 sigma, Q9), squared */
+    if (z_delta * z_delta > delta_var) return 0;
     double gain = *z_var / (*z_var + cm->zvar);
     *z_pos += gain * z_delta;
     double var_gain = delta_var / (delta_var + cm->zvar);
@@ -776,7 +808,9 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
             maxw = (maxw < weight) ? weight : maxw;
             data_particles++;
             const uint64_t found = cm.ncp;
-            sw_val[i] = dm_pow(weight, 1.0 / (double)found);
+            /* pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found)) */
+            if (!cm.use_shape_update || found == 0) sw_val[i] = dm_pow(weight, 1.0 / (double)found);
+            else sw_val[i] = weight == 0.0 ? 0.0 : dm_exp((-0.5 * cm.shape_s2) * (1.0 / (double)found));
             sum_data_weights += sw_val[i];
             total_points += found;
         } else {

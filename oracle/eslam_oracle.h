@@ -27,9 +27,9 @@ extern "C" {
 #define OR_SUM_REFERENCE 1
 
 /* ---- ContactModel (src/ContactModel.hpp:32-166) on an arbitrary map callback ---------- */
-/* bool map(const Vector3d& p, SurfacePatch& patch): q_mean/q_stdev describe the query patch
- * the reference constructs at src/ContactModel.cpp:151.                                    */
-typedef int (*or_map_fn)(void* user, const double p[3], double q_mean, double q_stdev,
+/* bool map(const Vector3d& p, SurfacePatch& patch): q_mean/q_var describe the query patch
+ * the reference constructs at src/ContactModel.cpp:151 (mean = p.z, stdev^2 = measVar).    */
+typedef int (*or_map_fn)(void* user, const double p[3], double q_mean, double q_var,
                          double* mean, double* stdev);
 
 typedef struct or_cpoint {                 /* eslam::ContactPoint src/PoseParticle.hpp:20-43 */
@@ -51,6 +51,7 @@ typedef struct or_contact_model {
     uint32_t ncp;
     or_cpoint cp[ESLAM_MAX_CONTACTS];
     double zdelta, zvar, weight, posevar;
+    double shape_s2;                       /* sum of squared normalised deviations       */
     /* lowest points per group */
     uint32_t nlow;
     double low[ESLAM_MAX_CONTACTS][3];
@@ -75,7 +76,7 @@ void or_surface_param_from_points(const double* xyz, uint32_t n, double* slope_x
 int or_bucket_index(int count, double min_val, double max_val, double value);
 
 /* ---- MLS grid (envire::MLSGrid::getPatch semantics, see eslam_gpu.h) --------------------- */
-int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean, double q_stdev,
+int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean, double q_var,
                      double* mean, double* stdev);
 
 /* ---- the filter (PoseEstimator + EmbodiedSlamFilter) -------------------------------------- */

@@ -35,25 +35,30 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, defines=(), lib=None, tag=""):
+    """defines: extra -D macros (ablation builds only); lib/tag: alternative output names."""
     os.makedirs(OUT_DIR, exist_ok=True)
+    lib = lib or LIB
     objs = []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(OUT_DIR, src + ".o")
+        obj = os.path.join(OUT_DIR, src + tag + ".o")
         objs.append(obj)
         if force or _stale(obj, [path] + HEADERS):
-            cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+            cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-c", path, "-o", obj]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
-    if force or _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    if force or _stale(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
+    tag = "_" + "_".join(d.lower() for d in defs) if defs else ""
+    build(force="--force" in sys.argv, defines=defs, tag=tag,
+          lib=os.path.join(OUT_DIR, f"libeslam_gpu{tag}.so") if defs else None)

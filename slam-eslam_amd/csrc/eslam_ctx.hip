@@ -452,8 +452,8 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
     m.height = ctx->d_height;
     m.width = g->width;
     m.height_cells = g->height;
-    m.scale_x = g->scale_x;
-    m.scale_y = g->scale_y;
+    m.inv_scale_x = 1.0 / g->scale_x;
+    m.inv_scale_y = 1.0 / g->scale_y;
     m.offset_x = g->offset_x;
     m.offset_y = g->offset_y;
     memcpy(m.g2l, g->global2local, sizeof(m.g2l));
@@ -607,6 +607,16 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
         ends += p.c[i].end;
     }
     ctx->maxp = ends;
+    // LDS window margin: foot reach + mean motion + 6 sigma of the sampled motion + 2 cells
+    double reach = 0.0;
+    for (uint32_t i = 0; i < m; ++i) {
+        const double r = sqrt(p.c[i].px * p.c[i].px + p.c[i].py * p.c[i].py);
+        reach = r > reach ? r : reach;
+    }
+    const double motion = sqrt(p.mu[0] * p.mu[0] + p.mu[1] * p.mu[1]) +
+                          6.0 * sqrt(in->sample_cov[0] + in->sample_cov[4]);
+    p.win_margin = reach + motion + 0.05;
+    p.use_window = (c.flags & ESLAM_FLAG_NO_MAP_LDS) ? 0u : 1u;
     p.me2 = c.measurement_error * c.measurement_error;
     p.radius = c.contact_point_radius;
     p.corr = c.contact_likelihood_correction;

@@ -23,6 +23,8 @@ constexpr int kScanTile = kBlock * kScanItems;   // 2048 particles per scan tile
 constexpr int kGatherTile = kScanTile;           // outputs per resample-gather block
 constexpr int kNShard = 16;              // statistics shards (blockIdx % kNShard)
 constexpr int kJumpBits = 11;
+constexpr int kStatsLds = 1024;          // bytes of the statistics scratch at the LDS base
+constexpr int kWindowLds = 40 * 1024;    // bytes of the MLS window after it
 
 // one statistics shard: exact sums as 4 limbs of 32-bit columns (uint64 each)
 struct alignas(128) Shard {
@@ -31,9 +33,10 @@ struct alignas(128) Shard {
     uint64_t SW[4];                      // sum of m^(1/n) over accepted particles
     uint64_t D, TP;                      // data_particles, total_points
     uint64_t maxm;                       // bits of max accepted m (non-negative double)
-    uint64_t flags;                      // bit b: A[b] non-finite, bit 8+b: B[b], bit 16: SW; nan in bits 24+
+    uint64_t flags;                      // bit q: accumulator q NaN, bit 16+q: infinite
     uint64_t err;                        // bit 0: zero measurement variance
-    uint64_t pad[7];
+    uint64_t bbox[4];                    // max of ~key(min x), key(max x), ~key(min y), key(max y)
+    uint64_t pad[3];
 };
 static_assert(sizeof(Shard) % 128 == 0, "shard alignment");
 
@@ -57,7 +60,7 @@ struct alignas(128) Ctl {
     uint64_t data_particles, total_points;
     uint64_t update_count;
     uint64_t err;
-    uint64_t pad[4];
+    uint64_t bbox[4];                    // particle bounding box of the last weighting (keys)
 };
 
 enum FinMode : uint32_t {
@@ -77,7 +80,7 @@ struct MapView {
     const float2* patch;                 // (mean, stdev) per patch
     const float* height;                 // nullable: all horizontal
     uint32_t width, height_cells;
-    double scale_x, scale_y, offset_x, offset_y;
+    double inv_scale_x, inv_scale_y, offset_x, offset_y;
     double g2l[12];
 };
 
@@ -104,7 +107,8 @@ struct StepParams {
     // ---- sizes
     uint64_t n, gbase, n_global;
     uint32_t J;                          // canonical chunk rows
-    uint32_t pad;
+    uint32_t use_window;                 // stage the MLS window under the cloud in LDS
+    double win_margin;                   // world-frame margin around the last bounding box
     ContactC c[ESLAM_MAX_CONTACTS];
 };
 

@@ -73,35 +73,153 @@ __device__ __forceinline__ uint32_t jump_pow(const uint32_t* __restrict__ jt, ui
 
 // ---------------------------------------------------------------------------------------
 // GridAccess::get -> MLSMap::getPatch(C_global2local * p, patch, 3.0)  (src/PoseEstimator.hpp:97-105)
+// qv: the query patch variance (measVar).  Cell: floor((x - offset) * (1/scale)); the
+// 3-sigma gate |mean_p - z| < 3 sqrt(stdev_p^2 + measVar) is evaluated squared.
+// The window part of the grid under the particle cloud may be staged in LDS: identical
+// values, so the result never depends on whether a cell came from LDS or global memory.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool get_patch(const MapView& m, double px, double py, double pz, double qv,
-                                          double& mean, double& stdev)
+struct Window {
+    int on;
+    int m0, m1, n0, n1, cols1;           // cell range [m0,m1) x [n0,n1); cols1 = m1 - m0 + 1
+    const uint32_t* cs;                  // rows x cols1 cell_start values (LDS)
+    const int32_t* rowoff;               // LDS patch offset minus the row's first global index
+    const float2* pt;                    // staged patches (LDS)
+};
+
+__device__ __forceinline__ bool patch_gate(const MapView& m, uint32_t k, float2 pf, double lz, double qv,
+                                           double& mean, double& stdev)
+{
+    const double pm = (double)pf.x, ps = (double)pf.y;
+    const double ph = m.height ? (double)m.height[k] : 0.0;
+    double diff;
+    if (ph > 0.0) {
+        if (lz > pm) diff = lz - pm;
+        else if (lz < pm - ph) diff = (pm - ph) - lz;
+        else diff = 0.0;
+    } else {
+        diff = dm_fabs(pm - lz);
+    }
+    if (diff * diff < 9.0 * (ps * ps + qv)) { mean = pm; stdev = ps; return true; }
+    return false;
+}
+
+__device__ __forceinline__ bool get_patch(const MapView& m, const Window& win, double px, double py, double pz,
+                                          double qv, double& mean, double& stdev)
 {
     const double* A = m.g2l;
     double lx = ((A[0] * px + A[1] * py) + A[2] * pz) + A[3];
     double ly = ((A[4] * px + A[5] * py) + A[6] * pz) + A[7];
     double lz = ((A[8] * px + A[9] * py) + A[10] * pz) + A[11];
-    double fm = floor((lx - m.offset_x) / m.scale_x);
-    double fn = floor((ly - m.offset_y) / m.scale_y);
+    double fm = floor((lx - m.offset_x) * m.inv_scale_x);
+    double fn = floor((ly - m.offset_y) * m.inv_scale_y);
     if (!(fm >= 0.0 && fm < (double)m.width && fn >= 0.0 && fn < (double)m.height_cells)) return false;
-    uint64_t cell = (uint64_t)fn * m.width + (uint64_t)fm;
-    uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
-    for (uint32_t k = b; k < e; ++k) {
-        float2 pf = m.patch[k];
-        double pm = (double)pf.x, ps = (double)pf.y;
-        double ph = m.height ? (double)m.height[k] : 0.0;
-        double diff;
-        if (ph > 0.0) {
-            if (lz > pm) diff = lz - pm;
-            else if (lz < pm - ph) diff = (pm - ph) - lz;
-            else diff = 0.0;
-        } else {
-            diff = dm_fabs(pm - lz);
-        }
-        double d = diff / dm_sqrt(ps * ps + qv);
-        if (d < 3.0) { mean = pm; stdev = ps; return true; }
+    const int im = (int)fm, in = (int)fn;
+    if (win.on && im >= win.m0 && im < win.m1 && in >= win.n0 && in < win.n1) {
+        const int r = in - win.n0;
+        const uint32_t* row = win.cs + r * win.cols1 + (im - win.m0);
+        const uint32_t b = row[0], e = row[1];
+        const int32_t off = win.rowoff[r];
+        for (uint32_t k = b; k < e; ++k)
+            if (patch_gate(m, k, win.pt[(int32_t)k + off], lz, qv, mean, stdev)) return true;
+        return false;
     }
+    const uint64_t cell = (uint64_t)in * m.width + (uint64_t)im;
+    const uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
+    for (uint32_t k = b; k < e; ++k)
+        if (patch_gate(m, k, m.patch[k], lz, qv, mean, stdev)) return true;
     return false;
+}
+
+__device__ __forceinline__ uint64_t order_key(double w)
+{
+    const uint64_t b = dm_bits(w);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double key_value(uint64_t k)
+{
+    return dm_from_bits((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k);
+}
+
+// Stage the grid cells under last step's particle cloud (+ margin) into LDS.  Every block
+// computes the same window from ctl; a window that does not fit is simply not used.
+__device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl* ctl, double extra_margin,
+                               unsigned char* lds)
+{
+    __shared__ int s_w[8];
+    Window w;
+    w.on = 0;
+    uint32_t* cs = reinterpret_cast<uint32_t*>(lds);
+    if (threadIdx.x == 0) {
+        int on = 0;
+        const uint64_t k0 = ctl->bbox[0], k1 = ctl->bbox[1], k2 = ctl->bbox[2], k3 = ctl->bbox[3];
+        if (p.use_window && k0 && k1 && k2 && k3 && !m.height) {
+            const double mg = p.win_margin + extra_margin;
+            const double x0 = key_value(~k0) - mg, x1 = key_value(k1) + mg;
+            const double y0 = key_value(~k2) - mg, y1 = key_value(k3) + mg;
+            const double* A = m.g2l;
+            double lx0 = 1e300, lx1 = -1e300, ly0 = 1e300, ly1 = -1e300;
+            for (int c = 0; c < 4; ++c) {
+                const double wx = (c & 1) ? x1 : x0, wy = (c & 2) ? y1 : y0;
+                const double lx = (A[0] * wx + A[1] * wy) + A[3], ly = (A[4] * wx + A[5] * wy) + A[7];
+                lx0 = lx < lx0 ? lx : lx0; lx1 = lx > lx1 ? lx : lx1;
+                ly0 = ly < ly0 ? ly : ly0; ly1 = ly > ly1 ? ly : ly1;
+            }
+            const double fm0 = floor((lx0 - m.offset_x) * m.inv_scale_x) - 1.0;
+            const double fm1 = floor((lx1 - m.offset_x) * m.inv_scale_x) + 2.0;
+            const double fn0 = floor((ly0 - m.offset_y) * m.inv_scale_y) - 1.0;
+            const double fn1 = floor((ly1 - m.offset_y) * m.inv_scale_y) + 2.0;
+            if (dm_isfinite(fm0) && dm_isfinite(fm1) && dm_isfinite(fn0) && dm_isfinite(fn1)) {
+                const double W = (double)m.width, H = (double)m.height_cells;
+                const int m0 = (int)(fm0 < 0 ? 0 : (fm0 > W ? W : fm0));
+                const int m1 = (int)(fm1 < 0 ? 0 : (fm1 > W ? W : fm1));
+                const int n0 = (int)(fn0 < 0 ? 0 : (fn0 > H ? H : fn0));
+                const int n1 = (int)(fn1 < 0 ? 0 : (fn1 > H ? H : fn1));
+                const int rows = n1 - n0, cols1 = m1 - m0 + 1;
+                if (rows > 0 && cols1 > 1 && (int64_t)rows * cols1 * 4 + rows * 4 + 64 <= kWindowLds) {
+                    on = 1;
+                    s_w[1] = m0; s_w[2] = m1; s_w[3] = n0; s_w[4] = n1; s_w[5] = cols1;
+                }
+            }
+        }
+        s_w[0] = on;
+    }
+    __syncthreads();
+    if (!s_w[0]) return w;
+    w.m0 = s_w[1]; w.m1 = s_w[2]; w.n0 = s_w[3]; w.n1 = s_w[4]; w.cols1 = s_w[5];
+    const int rows = w.n1 - w.n0;
+    const int ncs = rows * w.cols1;
+    for (int t = threadIdx.x; t < ncs; t += kBlock) {
+        const int r = t / w.cols1, c = t - r * w.cols1;
+        cs[t] = m.cell_start[(uint64_t)(w.n0 + r) * m.width + (uint64_t)(w.m0 + c)];
+    }
+    int32_t* rowoff = reinterpret_cast<int32_t*>(cs + ((ncs + 3) & ~3));
+    float2* pt = reinterpret_cast<float2*>(rowoff + ((rows + 3) & ~3));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int64_t cap = (kWindowLds - (int64_t)((unsigned char*)pt - (unsigned char*)cs)) / 8;
+        int64_t tot = 0;
+        for (int r = 0; r < rows; ++r) {
+            const uint32_t b = cs[r * w.cols1], e = cs[r * w.cols1 + w.cols1 - 1];
+            rowoff[r] = (int32_t)(tot - (int64_t)b);
+            tot += (int64_t)(e - b);
+        }
+        s_w[6] = tot <= cap ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_w[6]) return w;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int r = wave; r < rows; r += kWaves) {
+        const uint32_t b = cs[r * w.cols1], e = cs[r * w.cols1 + w.cols1 - 1];
+        const int32_t off = rowoff[r];
+        for (uint32_t k = b + lane; k < e; k += 64) pt[(int32_t)k + off] = m.patch[k];
+    }
+    __syncthreads();
+    w.on = 1;
+    w.cs = cs;
+    w.rowoff = rowoff;
+    w.pt = pt;
+    return w;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -110,12 +228,20 @@ __device__ __forceinline__ bool get_patch(const MapView& m, double px, double py
 struct CMResult {
     uint32_t ncp;
     bool accepted;
-    double weight, zdelta, zvar, posevar;
+    double weight, zdelta, zvar, posevar, s2;
 };
 
+// contactLikelihoodRatio(z, sigma) > 1e-9 guaranteed (exact-arithmetic bounds, wide margin):
+// a one-point group's ratio cancels ((zdiff*r)/r = zdiff) and is not evaluated
+__device__ __forceinline__ bool ratio_surely_significant(double z, double s)
+{
+    if (z <= 0.0) return s < 1e8;
+    return s < 40.0 && z < 5.6 * s;
+}
+
 template <int MAXP>
-__device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const MapView& map, double co, double s,
-                                                  double r22, double x, double y, double z, double meas_var)
+__device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const MapView& map, const Window& win, double co,
+                                                  double s, double r22, double x, double y, double z, double meas_var)
 {
     CMResult r;
     double cz[MAXP], cv[MAXP];
@@ -123,8 +249,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
     bool valid = false, group_valid = true;
     double contact_ratio = 0, pose_var_avg = 0, posevar = 0;
     double pzd = 0, pzv = 0;
-    const double q_stdev = dm_sqrt(meas_var);
-    const double qv = q_stdev * q_stdev;
+    const double qv = meas_var;
     for (uint32_t i = 0; i < p.m; ++i) {
         const ContactC c = p.c[i];
         double wx = ((co * c.px + (-s) * c.py) + 0.0 * c.pz) + x;
@@ -135,11 +260,29 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
         wz = wz - p.radius;
         if (group_valid && c.eval) {
             double mean, stdev;
-            if (get_patch(map, wx, wy, wz, qv, mean, stdev)) {
+            if (get_patch(map, win, wx, wy, wz, qv, mean, stdev)) {
                 const double zdiff = wz - mean;
                 const double pose_var = stdev * stdev;
                 const double zvar = stdev * stdev + meas_var;
-                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * p.corr);
+                const double sq = dm_sqrt(zvar);
+                if (!valid && c.end && ratio_surely_significant(zdiff, sq * p.corr)) {
+                    // single-point group: (zdiff, zvar) pushed directly
+                    posevar += pose_var;
+#pragma unroll
+                    for (int k = 0; k < MAXP; ++k)
+                        if ((uint32_t)k == ncp) { cz[k] = zdiff; cv[k] = zvar; }
+                    ++ncp;
+                    group_valid = true;
+                    valid = false;
+                    pose_var_avg = 0;
+                    contact_ratio = 0;
+                    continue;
+                }
+#ifdef ESLAM_ABL_NO_RATIO
+                const double ratio = 1.0 + zdiff * 1e-3;
+#else
+                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, sq * p.corr);
+#endif
                 if (!valid) {
                     pzd = zdiff * ratio;
                     pzv = zvar * ratio;
@@ -158,9 +301,10 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
         }
         if (valid && c.end) {
             if (group_valid && contact_ratio > 1e-9) {
-                pzd /= contact_ratio;
-                pzv /= contact_ratio;
-                posevar += pose_var_avg / contact_ratio;
+                const double inv = 1.0 / contact_ratio;
+                pzd *= inv;
+                pzv *= inv;
+                posevar += pose_var_avg * inv;
 #pragma unroll
                 for (int k = 0; k < MAXP; ++k)
                     if ((uint32_t)k == ncp) { cz[k] = pzd; cv[k] = pzv; }
@@ -175,26 +319,32 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
     r.ncp = ncp;
     r.posevar = posevar;
     r.accepted = (uint64_t)ncp >= p.min_contacts;
-    r.weight = r.zdelta = r.zvar = 0.0;
+    r.weight = r.zdelta = r.zvar = r.s2 = 0.0;
     if (r.accepted) {
         double d1 = 0, d2 = 0;
 #pragma unroll
         for (int k = 0; k < MAXP; ++k) {
             if ((uint32_t)k < ncp) {
-                d1 += cz[k] / cv[k];
-                d2 += 1.0 / cv[k];
+                cv[k] = 1.0 / cv[k];            // cv now holds 1/zvar
+                d1 += cz[k] * cv[k];
+                d2 += cv[k];
             }
         }
         const double delta = d1 / d2;
-        double pz = 1.0;
+        double s2 = 0.0;
 #pragma unroll
         for (int k = 0; k < MAXP; ++k) {
             if ((uint32_t)k < ncp) {
-                const double odiff = (cz[k] - delta) / dm_sqrt(cv[k]);
-                const double zk = dm_exp(-(odiff * odiff) / (2.0));
-                if (p.use_shape) pz *= zk;
+                const double odiff = (cz[k] - delta) * dm_sqrt(cv[k]);
+                s2 += odiff * odiff;
             }
         }
+        r.s2 = s2;
+#ifdef ESLAM_ABL_NO_EW
+        const double pz = p.use_shape ? 1.0 - 0.5 * s2 : 1.0;
+#else
+        const double pz = p.use_shape ? dm_exp(-0.5 * s2) : 1.0;
+#endif
         r.weight = pz;
         r.zdelta = -delta;
         r.zvar = 1.0 / d2;
@@ -227,11 +377,17 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
         rf = p.spread_rot * spread;
     }
 
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Window win;
+    win.on = 0;
+    if (WEIGHT) win = stage_window(map, p, ctl, 6.0 * tf, smem + kStatsLds);
+
     double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
 #pragma unroll
     for (int b = 0; b < DM_NBUCKETS; ++b) { accA[b] = 0.0; accB[b] = 0.0; }
     double accSW = 0.0, maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0;
+    uint64_t bb[4] = {0, 0, 0, 0};      // ~key(min x), key(max x), ~key(min y), key(max y)
 
     for (uint32_t j = 0; j < p.J; ++j) {
         const uint64_t i = lbase + 64ull * j + lane;
@@ -240,12 +396,17 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
         const double w_in = w;
         if (PROJECT) {
             const uint64_t gi = p.gbase + i;
+#ifdef ESLAM_ABL_NO_RNG
+            dm_philox_ctr d2; d2.v[0] = (uint32_t)gi * 2654435761u; d2.v[1] = d2.v[0] ^ 0x9e3779b9u; d2.v[2] = d2.v[1] * 3u; d2.v[3] = d2.v[2] + 7u;
+            double z0 = dm_u53(d2.v[0], d2.v[1]) - 0.5, z1 = dm_u53(d2.v[2], d2.v[3]) - 0.5, z2 = z0 * z1, sn0 = z1 - z0;
+#else
             dm_philox_ctr d0 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 0);
             dm_philox_ctr d1 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 1);
             dm_philox_ctr d2 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 2);
             double z0, z1, z2, sn0;
             dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &z0, &z1);
             dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &z2, &sn0);
+#endif
             // odometry.getPoseDeltaSample2D() = mu + L z
             const double dx = p.mu[0] + p.L00 * z0;
             double dy = p.mu[1] + (p.L10 * z0 + p.L11 * z1);
@@ -279,7 +440,7 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
             const double r22 = (1.0 - co) + co;
             const double meas_var = zs * zs + p.me2;
             if (meas_var == 0) err = 1;
-            const CMResult r = evaluate_pose<MAXP>(p, map, co, s, r22, x, y, z, meas_var);
+            const CMResult r = evaluate_pose<MAXP>(p, map, win, co, s, r22, x, y, z, meas_var);
             double mprob;
             uint32_t floating;
             double sw = 0.0;
@@ -289,7 +450,7 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
                 const double pose_var = r.posevar / (double)r.ncp;
                 const double a = zvar - pose_var;
                 double delta_var = (a < 1e-9) ? 1e-9 : a;
-                if (!(dm_fabs(r.zdelta / dm_sqrt(delta_var)) > 1.0)) {
+                if (!(r.zdelta * r.zdelta > delta_var)) {
                     const double gain = zvar / (zvar + r.zvar);
                     z += gain * r.zdelta;
                     const double var_gain = delta_var / (delta_var + r.zvar);
@@ -302,7 +463,9 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
                 floating = 0;
                 maxm = (maxm < r.weight) ? r.weight : maxm;
                 nD += 1;
-                sw = dm_pow(r.weight, 1.0 / (double)r.ncp);
+                // pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found))
+                if (!p.use_shape || r.ncp == 0) sw = dm_pow(r.weight, 1.0 / (double)r.ncp);
+                else sw = r.weight == 0.0 ? 0.0 : dm_exp((-0.5 * r.s2) * (1.0 / (double)r.ncp));
                 nTP += r.ncp;
             } else {
                 floating = 1;
@@ -325,15 +488,44 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
             st.zs[i] = zs;
             if (w != w_in || w != w) st.w[i] = w;
         }
+        if (x == x && y == y) {
+            const uint64_t kx = order_key(x), ky = order_key(y);
+            bb[0] = bb[0] > ~kx ? bb[0] : ~kx;
+            bb[1] = bb[1] > kx ? bb[1] : kx;
+            bb[2] = bb[2] > ~ky ? bb[2] : ~ky;
+            bb[3] = bb[3] > ky ? bb[3] : ky;
+        }
+    }
+
+    // bounding box of the cloud for the next step's LDS window (exact maxima, any order)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint64_t v = bb[q];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) { const uint64_t t = __shfl_xor(v, o, 64); v = v > t ? v : t; }
+        bb[q] = v;
+    }
+    Shard* shb = shards + (blockIdx.x % kNShard);
+    if (lane == 0 && bb[1]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) atomicMax((unsigned long long*)&shb->bbox[q], (unsigned long long)bb[q]);
     }
 
     if (!WEIGHT) return;
 
     // ---- exact statistics: chunk totals -> fixed point -> block -> sharded atomics ----
-    __shared__ uint32_t s_limb[kWaves][2 * DM_NBUCKETS + 1][4];
-    __shared__ uint32_t s_flag[kWaves];
-    __shared__ uint32_t s_cnt[kWaves][2];
-    __shared__ double s_max[kWaves];
+    struct StatsLds {
+        uint32_t limb[kWaves][2 * DM_NBUCKETS + 1][4];
+        uint32_t flag[kWaves];
+        uint32_t cnt[kWaves][2];
+        double mx[kWaves];
+    };
+    static_assert(sizeof(StatsLds) <= kStatsLds, "stats scratch");
+    StatsLds& sl = *reinterpret_cast<StatsLds*>(smem);
+    auto& s_limb = sl.limb;
+    auto& s_flag = sl.flag;
+    auto& s_cnt = sl.cnt;
+    auto& s_max = sl.mx;
     uint32_t flag = 0;
     const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
 #pragma unroll
@@ -364,7 +556,7 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
         s_max[wave] = wmax;
     }
     __syncthreads();
-    Shard* sh = shards + (blockIdx.x % kNShard);
+    Shard* sh = shb;
     const int t = threadIdx.x;
     if (t < (2 * DM_NBUCKETS + 1) * 4) {
         const int q = t >> 2, j = t & 3;
@@ -446,7 +638,7 @@ __global__ void __launch_bounds__(kBlock) k_weight_stats(DevState s0, DevState s
 // ---------------------------------------------------------------------------------------
 // k_finalize: one block.  Sums the shards exactly, then the scalar part of the update.
 // ---------------------------------------------------------------------------------------
-constexpr int kShardFields = 2 * DM_NBUCKETS * 4 + 4 + 5;   // A, B, SW, D, TP, maxm, flags, err
+constexpr int kShardFields = 2 * DM_NBUCKETS * 4 + 4 + 5 + 4;   // A, B, SW, D, TP, maxm, flags, err, bbox
 
 __device__ __forceinline__ double acc_value(const uint64_t* L, uint64_t flags, int qbit, int scale)
 {
@@ -464,8 +656,9 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ shards,
         for (int k = 0; k < kNShard; ++k) {
             uint64_t* f = reinterpret_cast<uint64_t*>(shards + k) + t;
             const uint64_t v = *f;
-            if (t == kShardFields - 3) acc = acc > v ? acc : v;                 // maxm
-            else if (t >= kShardFields - 2) acc |= v;                            // flags, err
+            const int base = 2 * DM_NBUCKETS * 4 + 4;                         // D
+            if (t == base + 2 || t >= base + 5) acc = acc > v ? acc : v;       // maxm, bbox
+            else if (t == base + 3 || t == base + 4) acc |= v;                 // flags, err
             else acc += v;
             *f = 0;
         }
@@ -482,6 +675,9 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ shards,
     const double maxm = dm_from_bits(s[2 * DM_NBUCKETS * 4 + 6]);
     const uint64_t flags = s[2 * DM_NBUCKETS * 4 + 7];
     const uint64_t err = s[2 * DM_NBUCKETS * 4 + 8];
+    if (s[2 * DM_NBUCKETS * 4 + 10]) {                 // a weighting kernel saw particles
+        for (int q = 0; q < 4; ++q) ctl->bbox[q] = s[2 * DM_NBUCKETS * 4 + 9 + q];
+    }
     const int wexp = ctl->wexp;      // the exponent the statistics kernel used
     const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
 
@@ -823,12 +1019,6 @@ __global__ void __launch_bounds__(kBlock) k_init_gaussian(DevState s0, uint64_t 
 // ParticleFilter::getBestParticleIndex (src/ParticleFilter.hpp:160-173): first index of the
 // maximum weight; NaN never compares greater.  out[0] = max ordered key, out[1] = index.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t order_key(double w)
-{
-    const uint64_t b = dm_bits(w);
-    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-
 __global__ void __launch_bounds__(kBlock) k_best_max(DevState s0, DevState s1, uint64_t n, const Ctl* __restrict__ ctl,
                                                      uint64_t* out)
 {
@@ -934,7 +1124,8 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
     if (blocks == 0) return hipSuccess;
     dim3 g(blocks), b(kBlock);
-#define ESLAM_LAUNCH(P, W, M) hipLaunchKernelGGL((k_project_weight<P, W, M>), g, b, 0, stream, s0, s1, *map, *p, ctl, shards)
+    const size_t lds = kStatsLds + (weight ? kWindowLds : 0);
+#define ESLAM_LAUNCH(P, W, M) hipLaunchKernelGGL((k_project_weight<P, W, M>), g, b, lds, stream, s0, s1, *map, *p, ctl, shards)
     if (project && !weight) ESLAM_LAUNCH(true, false, 4);
     else if (!project && weight) {
         if (maxp <= 4) ESLAM_LAUNCH(false, true, 4);

@@ -14,7 +14,7 @@ import numpy as np
 import eslam_abi as A
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libeslam_gpu.so")
+LIB_PATH = os.environ.get("ESLAM_GPU_LIB", os.path.join(HERE, "lib", "libeslam_gpu.so"))
 
 _lib = None
 

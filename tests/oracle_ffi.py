@@ -31,6 +31,7 @@ class ContactModelS(C.Structure):
         ("ncp", C.c_uint32),
         ("cp", CPoint * A.MAX_CONTACTS),
         ("zdelta", C.c_double), ("zvar", C.c_double), ("weight", C.c_double), ("posevar", C.c_double),
+        ("shape_s2", C.c_double),
         ("nlow", C.c_uint32),
         ("low", (C.c_double * 3) * A.MAX_CONTACTS),
     ]
