@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--map-cells", type=int, default=1000)
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU (sharded, RCCL) path even on one rank (measures its overhead)")
     ap.add_argument("--cpu-sample", type=int, default=1048576, help="particles in the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=48)
     return ap.parse_args()
@@ -74,9 +76,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
         import torch
         import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl")
         dist = tdist
@@ -90,7 +97,15 @@ def main():
     grid = S.rough_map(cells=args.map_cells) if args.rough else S.flat_map(cells=args.map_cells)
     stream = S.step_stream(args.warmup + args.steps + 1)
     cfg = S.bench_config(A.default_config(), n * world)
-    f = eslam_amd.GpuFilter(cfg, device=local_rank if world > 1 else 0)
+    if sharded:
+        # one global filter of n * world particles, sharded over the ranks: RCCL all_gathers
+        # of the statistics / totals / counts and an all_to_all_v of the migrating particles
+        import eslam_dist
+        comm = eslam_dist.TorchComm(device_memory=True, device=local_rank)
+        f = eslam_dist.ShardedGpuFilter(cfg, n * world, comm, device=local_rank)
+        assert f.n_local == n, (f.n_local, n)
+    else:
+        f = eslam_amd.GpuFilter(cfg, device=0)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
 
@@ -145,7 +160,7 @@ def main():
         "config": {"workload": "configs[2]: %d particles/GPU, 1 MI355X per rank, MLS %dx%d @0.1 m, 4 contacts, "
                                "resample forced every step" % (n, args.map_cells, args.map_cells),
                    "particles_per_gpu": n, "global_particles": n * world,
-                   "parallelism": "dp%d (particle shards)" % world},
+                   "parallelism": "dp%d (particle shards%s)" % (world, ", sharded path" if sharded else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "algorithmic_bytes_per_particle": dom_bytes,

@@ -46,6 +46,7 @@ extern "C" {
 #define ESLAM_ERR_NOT_INITIALISED -7     /* no particles yet */
 #define ESLAM_ERR_UNSUPPORTED -8
 #define ESLAM_ERR_OUT_OF_MEMORY -9
+#define ESLAM_ERR_COMM -10               /* a collective callback failed */
 
 /* ---- Configuration (src/Configuration.hpp:12-213, the fields consumed on the path) ---- */
 typedef struct eslam_config {
@@ -216,6 +217,41 @@ typedef struct eslam_rng_state {
 } eslam_rng_state;
 int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st);
 int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st);
+
+/* ---- multi-GPU: one context per GPU holds a contiguous shard of ONE global filter -------
+ * The library is transport-agnostic: it calls the collectives below at the three exchange
+ * points of an update.  In production they are torch.distributed over RCCL
+ * (xGMI) on device buffers (slam-eslam_amd/eslam_dist.py); tests use gloo on host buffers.
+ *   1. all_gather of the exact per-rank weighting statistics (~0.5 KB per rank)
+ *      -> every rank finalises the same global floating weight, weight sum, effective N
+ *   2. all_gather of the per-rank fixed-point weight totals (8 B per rank)
+ *      -> global cumulative-sum offsets for the stratified draws
+ *   3. all_gather of the per-destination send counts + all_to_all_v of the particles
+ *      whose stratified draws land on another rank (72-byte records)
+ * Results are bit-identical to the single-GPU run of the same global filter.          */
+typedef struct eslam_comm {
+    void* user;
+    int32_t rank, nranks;
+    int32_t device_memory;                 /* 1: callbacks take device pointers (RCCL)     */
+    int32_t pad;
+    /* recv[r * bytes .. (r+1) * bytes) <- send of rank r.  stream: the context's HIP
+     * stream when device_memory (the collective is ordered after the work already on it
+     * and work queued after the call returns must see its result), NULL otherwise.        */
+    int (*allgather)(void* user, const void* send, void* recv, uint64_t bytes, void* stream);
+    /* send_bytes[r] bytes to rank r (packed in rank order), recv_bytes[r] from rank r    */
+    int (*alltoallv)(void* user, const void* send, const uint64_t* send_bytes, void* recv,
+                     const uint64_t* recv_bytes, void* stream);
+} eslam_comm;
+
+/* Make this context shard [gbase, gbase + n_local) of an n_global-particle filter; call
+ * before init.  shard_gbase lists the first global index of every rank (nranks + 1
+ * entries, strictly increasing, last = n_global < 2^32); every entry must be a multiple
+ * of 64 * dm_chunk_rows(n_global) (the canonical summation chunk) except the last.
+ * The context's config particle_count is the global count.  Sharded contexts support
+ * the hot path (step/project/update/sync), init, upload/download of the local shard,
+ * weights sum / normalise / resample and the best particle (global index); the centroid
+ * returns ESLAM_ERR_UNSUPPORTED.  comm == NULL returns the context to one GPU.        */
+int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase);
 
 /* ---- diagnostics ------------------------------------------------------------------------- */
 /* ancestor index of every particle of the last resample (needs ESLAM_FLAG_RECORD_ANCESTORS) */

@@ -479,7 +479,20 @@ struct or_filter {
     eslam_update_info info;
     uint32_t* anc;
     int has_anc;
+    /* sharded mode (or_set_comm): this filter is shard [gbase, gbase + n) of n_global */
+    int sharded;
+    eslam_comm comm;
+    uint64_t n_global, gbase;
+    uint64_t gall[ESLAM_ORACLE_MAX_RANKS + 1];
 };
+
+/* global particle count: the N of every formula of the reference */
+static uint64_t NG(const or_filter* f) { return f->sharded ? f->n_global : f->n; }
+
+static int comm_allgather(or_filter* f, const void* send, void* recv, uint64_t bytes)
+{
+    return f->comm.allgather(f->comm.user, send, recv, bytes, NULL);
+}
 
 static void or_free_particles(or_filter* f)
 {
@@ -495,6 +508,7 @@ static void or_free_particles(or_filter* f)
 
 static int or_alloc_particles(or_filter* f, uint64_t n)
 {
+    if (f->sharded && n != f->gall[f->comm.rank + 1] - f->gall[f->comm.rank]) return ESLAM_ERR_INVALID_ARG;
     or_free_particles(f);
     f->n = n;
     size_t b = (size_t)(n ? n : 1);
@@ -559,8 +573,8 @@ int or_init_gaussian(or_filter* f, uint64_t n, const double mu[3], const double 
     int rc = or_alloc_particles(f, n);
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i) {
-        dm_philox_ctr d0 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, i, 0);
-        dm_philox_ctr d1 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, i, 1);
+        dm_philox_ctr d0 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, f->gbase + i, 0);
+        dm_philox_ctr d1 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, f->gbase + i, 1);
         double n0, n1, n2, n3;
         dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &n0, &n1);
         dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &n2, &n3);
@@ -591,7 +605,9 @@ int or_init_pose(or_filter* f, const double pos[3], const double q[4])
     double mu[3] = {pos[0], pos[1], angle};
     double sg[3] = {f->cfg.initial_translation_error[0], f->cfg.initial_translation_error[1],
                     f->cfg.initial_rotation_error[2]};
-    int rc = or_init_gaussian(f, f->cfg.particle_count, mu, sg, pos[2], f->cfg.initial_translation_error[2] + 1e-3);
+    uint64_t n = f->cfg.particle_count;
+    if (f->sharded) n = f->gall[f->comm.rank + 1] - f->gall[f->comm.rank];
+    int rc = or_init_gaussian(f, n, mu, sg, pos[2], f->cfg.initial_translation_error[2] + 1e-3);
     set_translation_pose(f->ud_pose, 1000, 0, 0);
     return rc;
 }
@@ -607,6 +623,11 @@ int or_upload(or_filter* f, uint64_t n, const eslam_particles* p)
     if (p->n_contact_points) memcpy(f->ncp, p->n_contact_points, n);
     double mx = 0;
     for (uint64_t i = 0; i < n; ++i) if (f->w[i] > mx) mx = f->w[i];
+    if (f->sharded) {
+        double all[ESLAM_ORACLE_MAX_RANKS];
+        if (comm_allgather(f, &mx, all, 8)) return ESLAM_ERR_COMM;
+        for (int r = 0; r < f->comm.nranks; ++r) if (all[r] > mx) mx = all[r];
+    }
     f->wexp = dm_weight_exp(mx);
     return 0;
 }
@@ -678,9 +699,10 @@ int or_project(or_filter* f, const eslam_step_input* in)
     const double* L = pp.L;
     for (uint64_t i = 0; i < f->n; ++i) {
         double z0, z1, z2, sn0, sn1 = 0, sn2 = 0;
-        dm_philox_ctr d0 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 0);
-        dm_philox_ctr d1 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 1);
-        dm_philox_ctr d2 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 2);
+        const uint64_t gi = f->gbase + i;
+        dm_philox_ctr d0 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 0);
+        dm_philox_ctr d1 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 1);
+        dm_philox_ctr d2 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 2);
         dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &z0, &z1);
         dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &z2, &sn0);
         /* odometry.getPoseDeltaSample2D(): mu + L z */
@@ -700,7 +722,7 @@ int or_project(or_filter* f, const eslam_step_input* in)
         f->z[i] += pp.z_delta;
         f->zs[i] = sqrt(f->zs[i] * f->zs[i] + pp.z_var);
         if (do_spread) {
-            dm_philox_ctr d3 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, i, 3);
+            dm_philox_ctr d3 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 3);
             dm_box_muller(dm_u53(d3.v[0], d3.v[1]), dm_u53(d3.v[2], d3.v[3]), &sn1, &sn2);
             f->x[i] += sn0 * tf + 0.0;
             f->y[i] += sn1 * tf + 0.0;
@@ -713,7 +735,26 @@ int or_project(or_filter* f, const eslam_step_input* in)
 }
 
 /* ---- canonical chunk reduction ------------------------------------------------------------ */
-typedef struct { uint64_t L[4]; uint32_t nan, inf; } or_acc;
+typedef struct or_acc_s { uint64_t L[4]; uint32_t nan, inf; } or_acc;
+
+/* exact cross-rank sum of k accumulators (limb sums, NaN/inf flags) */
+static int combine_accs(or_filter* f, or_acc* a, int k)
+{
+    if (!f->sharded) return 0;
+    const int G = f->comm.nranks;
+    or_acc* all = malloc(sizeof(or_acc) * (size_t)k * (size_t)G);
+    if (comm_allgather(f, a, all, sizeof(or_acc) * (uint64_t)k)) { free(all); return ESLAM_ERR_COMM; }
+    memset(a, 0, sizeof(or_acc) * (size_t)k);
+    for (int r = 0; r < G; ++r)
+        for (int q = 0; q < k; ++q) {
+            const or_acc* s = &all[r * k + q];
+            for (int j = 0; j < 4; ++j) a[q].L[j] += s->L[j];
+            a[q].nan |= s->nan;
+            a[q].inf |= s->inf;
+        }
+    free(all);
+    return 0;
+}
 
 static void acc_add_chunk(or_acc* a, double v, int scale)
 {
@@ -827,11 +868,36 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     }
     if (err) { free(a_val); free(sw_val); free(bucket); return err; }
 
-    const uint32_t J = dm_chunk_rows(f->n);
+    const uint32_t J = dm_chunk_rows(NG(f));
+    /* contract mode: every exact partial sum of the update; sharded filters combine them
+     * across ranks in one exchange (the device's per-rank statistics record) */
+    or_acc accs[2 * DM_NBUCKETS + 1];
+    memset(accs, 0, sizeof(accs));
+    const int sa = DM_FX_SCALE - f->wexp, sb = DM_FX_SCALE - 2 * f->wexp;
     if (f->sum_mode == OR_SUM_CONTRACT) {
-        or_acc sw = {{0}};
-        chunk_reduce(sw_val, NULL, 0, f->n, J, &sw, DM_FX_SCALE);
-        sum_data_weights = acc_value(&sw, DM_FX_SCALE);
+        chunk_reduce(sw_val, NULL, 0, f->n, J, &accs[2 * DM_NBUCKETS], DM_FX_SCALE);
+        double* a2 = malloc(f->n * 8 + 8);
+        for (uint64_t i = 0; i < f->n; ++i) a2[i] = a_val[i] * a_val[i];
+        for (int b = 0; b < DM_NBUCKETS; ++b) {
+            chunk_reduce(a_val, bucket, b, f->n, J, &accs[b], sa);
+            chunk_reduce(a2, bucket, b, f->n, J, &accs[DM_NBUCKETS + b], sb);
+        }
+        free(a2);
+        if (combine_accs(f, accs, 2 * DM_NBUCKETS + 1)) { free(a_val); free(sw_val); free(bucket); return ESLAM_ERR_COMM; }
+        sum_data_weights = acc_value(&accs[2 * DM_NBUCKETS], DM_FX_SCALE);
+    }
+    if (f->sharded) {
+        uint64_t mine[3], all[3 * ESLAM_ORACLE_MAX_RANKS];
+        mine[0] = data_particles; mine[1] = total_points; memcpy(&mine[2], &maxw, 8);
+        if (comm_allgather(f, mine, all, sizeof(mine))) { free(a_val); free(sw_val); free(bucket); return ESLAM_ERR_COMM; }
+        data_particles = 0; total_points = 0;
+        for (int r = 0; r < f->comm.nranks; ++r) {
+            double m;
+            data_particles += all[3 * r];
+            total_points += all[3 * r + 1];
+            memcpy(&m, &all[3 * r + 2], 8);
+            maxw = (maxw < m) ? m : maxw;
+        }
     }
     const double floating_weight = data_particles > 0 ? sum_data_weights / (double)data_particles : 1.0;
     ph->fw = floating_weight;
@@ -848,17 +914,10 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     }
     if (f->sum_mode == OR_SUM_CONTRACT) {
         double S = 0.0, Q = 0.0;
-        const int sa = DM_FX_SCALE - f->wexp, sb = DM_FX_SCALE - 2 * f->wexp;
-        double* a2 = malloc(f->n * 8);
-        for (uint64_t i = 0; i < f->n; ++i) a2[i] = a_val[i] * a_val[i];
         for (int b = 0; b < DM_NBUCKETS; ++b) {
-            or_acc A = {{0}}, B = {{0}};
-            chunk_reduce(a_val, bucket, b, f->n, J, &A, sa);
-            chunk_reduce(a2, bucket, b, f->n, J, &B, sb);
-            S = S + ph->f[b] * acc_value(&A, sa);
-            Q = Q + (ph->f[b] * ph->f[b]) * acc_value(&B, sb);
+            S = S + ph->f[b] * acc_value(&accs[b], sa);
+            Q = Q + (ph->f[b] * ph->f[b]) * acc_value(&accs[DM_NBUCKETS + b], sb);
         }
-        free(a2);
         ph->S = S;
         ph->Q = Q;
     }
@@ -876,22 +935,25 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
 static double normalize_with(or_filter* f, double S, double Q, int have_sums)
 {
     const uint64_t n = f->n;
+    const uint64_t N = NG(f);
     double effective = 0;
     if (f->sum_mode == OR_SUM_REFERENCE || !have_sums) {
         if (f->sum_mode == OR_SUM_REFERENCE) {
             S = 0;
             for (uint64_t i = 0; i < n; ++i) S += f->w[i];
         } else {
-            const uint32_t J = dm_chunk_rows(n);
+            const uint32_t J = dm_chunk_rows(N);
             int e = f->wexp;
-            double* w2 = malloc(n * 8);
+            double* w2 = malloc(n * 8 + 8);
             for (uint64_t i = 0; i < n; ++i) w2[i] = f->w[i] * f->w[i];
-            or_acc A = {{0}}, B = {{0}};
-            chunk_reduce(f->w, NULL, 0, n, J, &A, DM_FX_SCALE - e);
-            chunk_reduce(w2, NULL, 0, n, J, &B, DM_FX_SCALE - 2 * e);
+            or_acc AB[2];
+            memset(AB, 0, sizeof(AB));
+            chunk_reduce(f->w, NULL, 0, n, J, &AB[0], DM_FX_SCALE - e);
+            chunk_reduce(w2, NULL, 0, n, J, &AB[1], DM_FX_SCALE - 2 * e);
             free(w2);
-            S = acc_value(&A, DM_FX_SCALE - e);
-            Q = acc_value(&B, DM_FX_SCALE - 2 * e);
+            combine_accs(f, AB, 2);
+            S = acc_value(&AB[0], DM_FX_SCALE - e);
+            Q = acc_value(&AB[1], DM_FX_SCALE - 2 * e);
         }
     }
     f->info.weight_sum = S;
@@ -900,10 +962,10 @@ static double normalize_with(or_filter* f, double S, double Q, int have_sums)
         f->info.uniform_reset = 1;
         for (uint64_t i = 0; i < n; ++i) {
             double* w = &f->w[i];
-            *w = 1.0 / (double)n;
+            *w = 1.0 / (double)N;
             effective += *w * *w;
         }
-        if (f->sum_mode == OR_SUM_CONTRACT) effective = 1.0 / (double)n;   /* eff := N */
+        if (f->sum_mode == OR_SUM_CONTRACT) effective = 1.0 / (double)N;   /* eff := N */
     } else {
         for (uint64_t i = 0; i < n; ++i) {
             f->w[i] /= S;
@@ -925,7 +987,8 @@ double or_get_weights_sum(or_filter* f)
         return s;
     }
     or_acc A = {{0}};
-    chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(f->n), &A, DM_FX_SCALE - f->wexp);
+    chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
+    combine_accs(f, &A, 1);
     return acc_value(&A, DM_FX_SCALE - f->wexp);
 }
 
@@ -982,6 +1045,119 @@ static void resample_stratified(or_filter* f, uint64_t samples, int shift)
     f->has_anc = 1;
 }
 
+
+/* ---- sharded resample: the multi-GPU decomposition restated on the CPU -----------------
+ * Particle i (global index g) with inclusive fixed-point cumulative sum C_g fills the
+ * outputs [lo, hi) with lo = #{k : T_k <= C_(g-1)} (0 for g = 0) and hi = #{k : T_k <= C_g}
+ * (N for the last particle: the Q5 clamp), T_k = fx((k + U_k) / N) -- the same ancestors
+ * as resample_stratified.  Each rank sends every particle whose range meets another
+ * rank's output slice there (all_to_all_v) and fills its own slice from what it gets.  */
+typedef struct {
+    double x, y, th, z, zs, w, mprob;
+    uint64_t lo, hi, src;          /* global output range, global source index */
+    uint8_t floating, ncp, pad[6];
+} or_mig;
+
+static void resample_sharded(or_filter* f, int shift)
+{
+    const int G = f->comm.nranks, me = f->comm.rank;
+    const uint64_t N = f->n_global, n = f->n;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += dm_fx_shift(f->w[i], shift);
+    uint64_t totals[ESLAM_ORACLE_MAX_RANKS];
+    comm_allgather(f, &total, totals, 8);
+    uint64_t off = 0;
+    for (int r = 0; r < me; ++r) off += totals[r];
+    /* the N stratified draws (every rank walks the whole minstd stream) */
+    uint64_t* T = malloc(N * 8);
+    for (uint64_t k = 0; k < N; ++k) {
+        f->minstd = dm_minstd_next(f->minstd);
+        T[k] = dm_fx_shift(((double)k + dm_minstd_uniform(f->minstd)) / (double)N, shift);
+    }
+    uint64_t* lo = malloc(n * 8 + 8);
+    uint64_t* hi = malloc(n * 8 + 8);
+    uint64_t c = off, k = 0, overruns = 0;
+    while (k < N && T[k] <= c) ++k;
+    for (uint64_t i = 0; i < n; ++i) {
+        lo[i] = (f->gbase + i == 0) ? 0 : k;
+        c += dm_fx_shift(f->w[i], shift);
+        while (k < N && T[k] <= c) ++k;
+        hi[i] = k;
+        if (f->gbase + i == N - 1) { overruns = N - k; hi[i] = N; }
+    }
+    free(T);
+    /* per-destination records */
+    uint64_t cnt[ESLAM_ORACLE_MAX_RANKS] = {0};
+    for (int d = 0; d < G; ++d)
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t a = lo[i] > f->gall[d] ? lo[i] : f->gall[d];
+            const uint64_t b = hi[i] < f->gall[d + 1] ? hi[i] : f->gall[d + 1];
+            if (a < b) cnt[d]++;
+        }
+    uint64_t nsend = 0;
+    for (int d = 0; d < G; ++d) nsend += cnt[d];
+    or_mig* send = malloc(sizeof(or_mig) * (nsend ? nsend : 1));
+    uint64_t j = 0;
+    for (int d = 0; d < G; ++d)
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t a = lo[i] > f->gall[d] ? lo[i] : f->gall[d];
+            const uint64_t b = hi[i] < f->gall[d + 1] ? hi[i] : f->gall[d + 1];
+            if (a >= b) continue;
+            or_mig* m = &send[j++];
+            memset(m, 0, sizeof(*m));
+            m->x = f->x[i]; m->y = f->y[i]; m->th = f->th[i]; m->z = f->z[i]; m->zs = f->zs[i];
+            m->w = f->w[i]; m->mprob = f->mprob[i];
+            m->floating = f->floating[i]; m->ncp = f->ncp[i];
+            m->lo = a; m->hi = b; m->src = f->gbase + i;
+        }
+    free(lo); free(hi);
+    uint64_t all[ESLAM_ORACLE_MAX_RANKS * ESLAM_ORACLE_MAX_RANKS];
+    comm_allgather(f, cnt, all, 8ull * G);
+    uint64_t sb[ESLAM_ORACLE_MAX_RANKS], rb[ESLAM_ORACLE_MAX_RANKS], nrecv = 0;
+    for (int r = 0; r < G; ++r) {
+        sb[r] = cnt[r] * sizeof(or_mig);
+        rb[r] = all[r * G + me] * sizeof(or_mig);
+        nrecv += all[r * G + me];
+    }
+    or_mig* recv = malloc(sizeof(or_mig) * (nrecv ? nrecv : 1));
+    f->comm.alltoallv(f->comm.user, send, sb, recv, rb, NULL);
+    free(send);
+    uint32_t* anc = calloc(n + 1, 4);
+    or_mig* src = calloc(n ? n : 1, sizeof(or_mig));
+    for (uint64_t q = 0; q < nrecv; ++q)
+        for (uint64_t o = recv[q].lo; o < recv[q].hi; ++o) {
+            src[o - f->gbase] = recv[q];
+            anc[o - f->gbase] = (uint32_t)recv[q].src;
+        }
+    free(recv);
+    for (uint64_t o = 0; o < n; ++o) {
+        const or_mig* m = &src[o];
+        f->x[o] = m->x; f->y[o] = m->y; f->th[o] = m->th; f->z[o] = m->z; f->zs[o] = m->zs;
+        f->w[o] = m->w; f->mprob[o] = m->mprob; f->floating[o] = m->floating; f->ncp[o] = m->ncp;
+        f->anc[o] = anc[o];
+    }
+    free(src); free(anc);
+    f->info.resample_overruns = overruns;
+    f->has_anc = 1;
+}
+
+int or_set_comm(or_filter* f, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase)
+{
+    or_free_particles(f);
+    if (!comm) { f->sharded = 0; f->n_global = 0; f->gbase = 0; return 0; }
+    if (comm->device_memory || comm->nranks < 1 || comm->nranks > ESLAM_ORACLE_MAX_RANKS) return ESLAM_ERR_INVALID_ARG;
+    const uint64_t csz = 64ull * dm_chunk_rows(n_global);
+    if (shard_gbase[0] != 0 || shard_gbase[comm->nranks] != n_global) return ESLAM_ERR_INVALID_ARG;
+    for (int r = 0; r < comm->nranks; ++r)
+        if (shard_gbase[r + 1] <= shard_gbase[r] || shard_gbase[r] % csz) return ESLAM_ERR_INVALID_ARG;
+    f->sharded = 1;
+    f->comm = *comm;
+    f->n_global = n_global;
+    memcpy(f->gall, shard_gbase, sizeof(uint64_t) * (size_t)(comm->nranks + 1));
+    f->gbase = shard_gbase[comm->rank];
+    return 0;
+}
+
 /* standalone ParticleFilter::resample() on the weights as they are: the contract scales
  * the cumulative sum by the exact weight sum's exponent (device FIN_RESAMPLE)          */
 void or_resample(or_filter* f)
@@ -989,16 +1165,18 @@ void or_resample(or_filter* f)
     int shift = 60;
     if (f->sum_mode == OR_SUM_CONTRACT) {
         or_acc A = {{0}};
-        chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(f->n), &A, DM_FX_SCALE - f->wexp);
+        chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
+        combine_accs(f, &A, 1);
         shift = 61 - (dm_weight_exp(acc_value(&A, DM_FX_SCALE - f->wexp)) + 1);
     }
-    resample_stratified(f, f->n, shift);
+    if (f->sharded) resample_sharded(f, shift);
+    else resample_stratified(f, f->n, shift);
 }
 
 /* src/ParticleFilter.hpp:120-148 (not used by PoseEstimator; weights reset to 1/N) */
 void or_resample_multinomial(or_filter* f, uint64_t samples)
 {
-    uint32_t* anc = malloc(samples * 4);
+    uint32_t* anc = calloc(samples + 1, 4);
     uint64_t m = 0;
     for (uint64_t k = 0; k < samples; ++k) {
         f->minstd = dm_minstd_next(f->minstd);
@@ -1028,7 +1206,8 @@ int or_update(or_filter* f, const eslam_step_input* in)
     f->info.resampled = 0;
     f->info.resample_overruns = 0;
     if (eff < (double)f->cfg.min_effective) {
-        resample_stratified(f, f->n, 60);
+        if (f->sharded) resample_sharded(f, 60);
+        else resample_stratified(f, f->n, 60);
         f->info.resampled = 1;
     }
     f->info.update_count++;
@@ -1067,12 +1246,25 @@ uint64_t or_best_index(or_filter* f)
     double weight = -INFINITY;
     for (uint64_t i = 0; i < f->n; ++i)
         if (f->w[i] > weight) { index = i; weight = f->w[i]; }
+    if (f->sharded) {          /* the same scan over the ranks' results in rank order */
+        double mine[2] = {weight, (double)(f->gbase + index)}, all[2 * ESLAM_ORACLE_MAX_RANKS];
+        comm_allgather(f, mine, all, sizeof(mine));
+        index = 0;
+        weight = -INFINITY;
+        for (int r = 0; r < f->comm.nranks; ++r)
+            if (all[2 * r] > weight) { index = (uint64_t)all[2 * r + 1]; weight = all[2 * r]; }
+    }
     return index;
 }
 
 /* PoseEstimator::getCentroid  src/PoseEstimator.cpp:354-383 (reference arithmetic) */
 void or_get_centroid(or_filter* f, double position[3], double q[4])
 {
+    if (f->sharded) {          /* not defined for a sharded filter (device: ERR_UNSUPPORTED) */
+        position[0] = position[1] = position[2] = NAN;
+        q[0] = q[1] = q[2] = q[3] = NAN;
+        return;
+    }
     or_normalize_weights(f);
     double mx = 0, my = 0, mo = 0, zm = 0, sw = 0;
     for (uint64_t i = 0; i < f->n; ++i) {

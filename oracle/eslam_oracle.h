@@ -23,6 +23,7 @@
 extern "C" {
 #endif
 
+#define ESLAM_ORACLE_MAX_RANKS 16
 #define OR_SUM_CONTRACT 0
 #define OR_SUM_REFERENCE 1
 
@@ -104,6 +105,9 @@ void or_get_centroid(or_filter* f, double position[3], double q_wxyz[4]);
 int or_get_ancestors(or_filter* f, uint32_t* out, uint64_t n);
 void or_get_rng_state(or_filter* f, eslam_rng_state* st);
 void or_set_rng_state(or_filter* f, const eslam_rng_state* st);
+/* sharded mode (host-memory eslam_comm only, contract sums): shard [gbase, gbase + n) of an
+ * n_global filter -- the CPU statement of the multi-GPU decomposition (eslam_gpu_set_comm) */
+int or_set_comm(or_filter* f, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase);
 /* per-particle debug of the last updateWeights: found contact points (cp: n*MAX entries) */
 int or_get_debug(or_filter* f, uint32_t* ncp, or_cpoint* cp, double* zdelta, double* zvar);
 

@@ -24,9 +24,23 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
                                                   hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
                                                 hipStream_t stream);
-extern "C" hipError_t eslam_launch_finalize(Shard* shards, Ctl* ctl, const FinParams* fp, hipStream_t stream);
+extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream);
+extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
-                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream);
+                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt,
+                                                  uint64_t* tile_excl, uint64_t* total, hipStream_t stream);
+extern "C" hipError_t eslam_launch_plan(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
+                                        const uint64_t* tile_excl, const uint64_t* totals, const uint32_t* jt, uint2* range,
+                                        uint64_t* first_last, uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off,
+                                        hipStream_t stream);
+extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
+                                        const uint64_t* first_last, const uint64_t* sd_ed, const uint64_t* send_off,
+                                        uint64_t nsend, void* send, hipStream_t stream);
+extern "C" hipError_t eslam_launch_expand_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const void* recv,
+                                                 uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* tile_first,
+                                                 uint64_t* status, uint32_t* anc, uint32_t record, uint32_t aux,
+                                                 hipStream_t stream);
+extern "C" uint64_t eslam_record_bytes(void);
 extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint32_t* marks,
                                                    const uint32_t* tile_first, uint64_t* status, uint32_t* anc,
                                                    uint32_t record, uint32_t aux, hipStream_t stream);
@@ -208,6 +222,19 @@ struct eslam_ctx {
     uint64_t proj_event = 0, init_event = 0, hash_event = 0;
     double ud_pose[12];
     double zcomp[4] = {1, 0, 0, 0};
+    // multi-GPU (eslam_gpu_set_comm): this context is shard [gbase, gbase + n) of n_global
+    bool sharded = false;
+    eslam_comm comm = {};
+    std::vector<uint64_t> gall;             // first global index of every rank (+ n_global)
+    Shard* rec_local = nullptr;             // this rank's statistics record
+    Shard* recs = nullptr;                  // gathered records of all ranks
+    uint64_t* mg = nullptr;                 // MgBlock (device)
+    uint64_t* mg_host = nullptr;            // pinned
+    uint64_t* tile_excl = nullptr;          // per scan tile: exclusive fixed-point prefix
+    uint2* range = nullptr;                 // per particle: [lo, hi) of its global outputs
+    void* sendbuf = nullptr; uint64_t send_cap = 0;
+    void* recvbuf = nullptr; uint64_t recv_cap = 0;
+    void* stage = nullptr; uint64_t stage_cap = 0;   // pinned staging (host-memory comm)
     // diagnostics
     std::string err;
     bool timing = false;
@@ -227,6 +254,22 @@ struct eslam_ctx {
     } while (0)
 
 static constexpr uint32_t kRingSteps = 2048;
+
+// multi-GPU scratch block (uint64 words, device + pinned host mirror)
+namespace mg {
+constexpr int kTotal = 0;                                   // this rank's fixed-point weight total
+constexpr int kTotals = kTotal + 1;                         // [kMaxRanks] gathered totals
+constexpr int kCounts = kTotals + kMaxRanks;                // [kMaxRanks] records sent to each rank
+constexpr int kCountsAll = kCounts + kMaxRanks;             // [kMaxRanks^2] gathered counts
+constexpr int kSendOff = kCountsAll + kMaxRanks * kMaxRanks;   // [kMaxRanks + 1]
+constexpr int kSdEd = kSendOff + kMaxRanks + 1;             // [2 kMaxRanks]
+constexpr int kFirstLast = kSdEd + 2 * kMaxRanks;           // [2 kMaxRanks]
+constexpr int kBest = kFirstLast + 2 * kMaxRanks;           // [2] local best (key, global index)
+constexpr int kBestAll = kBest + 2;                         // [2 kMaxRanks]
+constexpr int kMaxW = kBestAll + 2 * kMaxRanks;             // local max weight (bits)
+constexpr int kMaxWAll = kMaxW + 1;                         // [kMaxRanks]
+constexpr int kWords = kMaxWAll + kMaxRanks;
+}  // namespace mg
 
 // timing mode: event k (0..4) of the current step, kept in a ring so a whole timed region
 // of back-to-back steps is measured without synchronising between steps
@@ -360,6 +403,8 @@ static void free_particles(eslam_ctx* ctx)
     hipFree(ctx->tile_first); ctx->tile_first = nullptr;
     hipFree(ctx->status); ctx->status = nullptr;
     hipFree(ctx->anc); ctx->anc = nullptr;
+    hipFree(ctx->tile_excl); ctx->tile_excl = nullptr;
+    hipFree(ctx->range); ctx->range = nullptr;
     ctx->n = ctx->cap = 0;
     ctx->has_anc = false;
 }
@@ -379,6 +424,8 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     free_map(ctx);
     hipFree(ctx->shards); hipFree(ctx->ctl); hipHostFree(ctx->ctl_host); hipFree(ctx->jump);
     hipFree(ctx->scratch); hipHostFree(ctx->scratch_host);
+    hipFree(ctx->rec_local); hipFree(ctx->recs); hipFree(ctx->mg); hipHostFree(ctx->mg_host);
+    hipFree(ctx->sendbuf); hipFree(ctx->recvbuf); hipHostFree(ctx->stage);
     for (auto& e : ctx->ev) if (e) hipEventDestroy(e);
     for (auto& e : ctx->ring) if (e) hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
@@ -401,6 +448,8 @@ extern "C" int eslam_gpu_set_stream(eslam_ctx* ctx, void* s)
 static int alloc_particles(eslam_ctx* ctx, uint64_t n)
 {
     if (n >= (1ull << 32) - 1) return fail(ctx, ESLAM_ERR_INVALID_ARG, "particle count must be < 2^32 - 1");
+    if (ctx->sharded && n != ctx->gall[ctx->comm.rank + 1] - ctx->gall[ctx->comm.rank])
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "sharded context: particle count must equal this rank's shard size");
     free_particles(ctx);
     const uint64_t cap = n ? n : 1;
     auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
@@ -422,8 +471,130 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     ctx->n = n;
     ctx->cap = cap;
-    ctx->n_global = n;
-    ctx->gbase = 0;
+    if (ctx->sharded) {
+        HIPCHK(ctx, hipMalloc(&ctx->tile_excl, ntiles * 8));
+        HIPCHK(ctx, hipMalloc(&ctx->range, cap * sizeof(uint2)));
+    } else {
+        ctx->n_global = n;
+        ctx->gbase = 0;
+    }
+    return ESLAM_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// multi-GPU plumbing: the three exchanges of an update go through the user's collectives
+// ---------------------------------------------------------------------------------------
+static int grow(eslam_ctx* ctx, void** buf, uint64_t* cap, uint64_t bytes, bool pinned)
+{
+    if (bytes <= *cap) return ESLAM_OK;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t want = bytes + bytes / 4 + 4096;
+    if (pinned) {
+        hipHostFree(*buf);
+        *buf = nullptr; *cap = 0;
+        HIPCHK(ctx, hipHostMalloc(buf, want));
+    } else {
+        hipFree(*buf);
+        *buf = nullptr; *cap = 0;
+        HIPCHK(ctx, hipMalloc(buf, want));
+    }
+    *cap = want;
+    return ESLAM_OK;
+}
+
+// all_gather of `bytes` per rank from device memory into device memory
+static int comm_allgather(eslam_ctx* ctx, const void* dsend, void* drecv, uint64_t bytes)
+{
+    const eslam_comm& c = ctx->comm;
+    if (c.device_memory) {
+        if (c.allgather(c.user, dsend, drecv, bytes, (void*)ctx->stream) != 0)
+            return fail(ctx, ESLAM_ERR_COMM, "allgather callback failed");
+        return ESLAM_OK;
+    }
+    int rc = grow(ctx, &ctx->stage, &ctx->stage_cap, bytes * (c.nranks + 1), true);
+    if (rc) return rc;
+    char* h = (char*)ctx->stage;
+    HIPCHK(ctx, hipMemcpyAsync(h, dsend, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (c.allgather(c.user, h, h + bytes, bytes, nullptr) != 0) return fail(ctx, ESLAM_ERR_COMM, "allgather callback failed");
+    HIPCHK(ctx, hipMemcpyAsync(drecv, h + bytes, bytes * c.nranks, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));     // the staging buffer is reused
+    return ESLAM_OK;
+}
+
+static int comm_alltoallv(eslam_ctx* ctx, const void* dsend, const uint64_t* sb, void* drecv, const uint64_t* rb)
+{
+    const eslam_comm& c = ctx->comm;
+    if (c.device_memory) {
+        if (c.alltoallv(c.user, dsend, sb, drecv, rb, (void*)ctx->stream) != 0)
+            return fail(ctx, ESLAM_ERR_COMM, "alltoallv callback failed");
+        return ESLAM_OK;
+    }
+    uint64_t ts = 0, tr = 0;
+    for (int r = 0; r < c.nranks; ++r) { ts += sb[r]; tr += rb[r]; }
+    int rc = grow(ctx, &ctx->stage, &ctx->stage_cap, ts + tr + 64, true);
+    if (rc) return rc;
+    char* h = (char*)ctx->stage;
+    char* hr = h + ((ts + 63) & ~63ull);
+    if (ts) HIPCHK(ctx, hipMemcpyAsync(h, dsend, ts, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (c.alltoallv(c.user, h, sb, hr, rb, nullptr) != 0) return fail(ctx, ESLAM_ERR_COMM, "alltoallv callback failed");
+    if (tr) HIPCHK(ctx, hipMemcpyAsync(drecv, hr, tr, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return ESLAM_OK;
+}
+
+static PlanParams plan_params(eslam_ctx* ctx)
+{
+    PlanParams pp;
+    memset(&pp, 0, sizeof(pp));
+    pp.n_global = ctx->n_global;
+    pp.rank = ctx->comm.rank;
+    pp.nranks = ctx->comm.nranks;
+    for (int r = 0; r <= ctx->comm.nranks; ++r) pp.gbase[r] = ctx->gall[r];
+    return pp;
+}
+
+extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    free_particles(ctx);
+    if (!comm) {
+        ctx->sharded = false;
+        ctx->gall.clear();
+        ctx->gbase = 0;
+        ctx->n_global = 0;
+        return ESLAM_OK;
+    }
+    if (!shard_gbase || !comm->allgather || !comm->alltoallv || comm->nranks < 1 || comm->nranks > kMaxRanks ||
+        comm->rank < 0 || comm->rank >= comm->nranks)
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: bad communicator (1 <= nranks <= 16)");
+    if (n_global == 0 || n_global >= (1ull << 32) - 1)
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: n_global must be in [1, 2^32 - 1)");
+    const uint64_t csz = 64ull * dm_chunk_rows(n_global);
+    if (shard_gbase[0] != 0 || shard_gbase[comm->nranks] != n_global)
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: shard_gbase must run from 0 to n_global");
+    for (int r = 0; r < comm->nranks; ++r) {
+        if (shard_gbase[r + 1] <= shard_gbase[r])
+            return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: every shard needs at least one particle");
+        if (shard_gbase[r] % csz)
+            return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: shard starts must be multiples of the summation chunk");
+    }
+    if (!ctx->mg) {
+        HIPCHK(ctx, hipMalloc(&ctx->rec_local, sizeof(Shard)));
+        HIPCHK(ctx, hipMalloc(&ctx->recs, sizeof(Shard) * kMaxRanks));
+        HIPCHK(ctx, hipMalloc(&ctx->mg, mg::kWords * 8));
+        HIPCHK(ctx, hipHostMalloc(&ctx->mg_host, mg::kWords * 8));
+        HIPCHK(ctx, hipMemset(ctx->rec_local, 0, sizeof(Shard)));
+        HIPCHK(ctx, hipMemset(ctx->recs, 0, sizeof(Shard) * kMaxRanks));
+        HIPCHK(ctx, hipMemset(ctx->mg, 0, mg::kWords * 8));
+    }
+    ctx->comm = *comm;
+    ctx->sharded = true;
+    ctx->gall.assign(shard_gbase, shard_gbase + comm->nranks + 1);
+    ctx->n_global = n_global;
+    ctx->gbase = shard_gbase[comm->rank];
     return ESLAM_OK;
 }
 
@@ -497,7 +668,12 @@ extern "C" int eslam_gpu_init_pose(eslam_ctx* ctx, const double pos[3], const do
     const double mu[3] = {pos[0], pos[1], angle};
     const double sg[3] = {ctx->cfg.initial_translation_error[0], ctx->cfg.initial_translation_error[1],
                           ctx->cfg.initial_rotation_error[2]};
-    const int rc = eslam_gpu_init_gaussian(ctx, ctx->cfg.particle_count, mu, sg, pos[2], ctx->cfg.initial_translation_error[2] + 1e-3);
+    uint64_t n = ctx->cfg.particle_count;
+    if (ctx->sharded) {
+        if (n != ctx->n_global) return fail(ctx, ESLAM_ERR_INVALID_ARG, "sharded context: particle_count must be n_global");
+        n = ctx->gall[ctx->comm.rank + 1] - ctx->gall[ctx->comm.rank];
+    }
+    const int rc = eslam_gpu_init_gaussian(ctx, n, mu, sg, pos[2], ctx->cfg.initial_translation_error[2] + 1e-3);
     set_translation_pose(ctx->ud_pose, 1000, 0, 0);
     return rc;
 }
@@ -535,6 +711,19 @@ extern "C" int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const esla
     }
     double mx = 0;
     for (uint64_t i = 0; i < n; ++i) if (p->weight[i] > mx) mx = p->weight[i];
+    if (ctx->sharded) {                      // the statistics scale must agree on every rank
+        uint64_t* h = ctx->mg_host;
+        memcpy(&h[mg::kMaxW], &mx, 8);
+        HIPCHK(ctx, hipMemcpy(ctx->mg + mg::kMaxW, &h[mg::kMaxW], 8, hipMemcpyHostToDevice));
+        rc = comm_allgather(ctx, ctx->mg + mg::kMaxW, ctx->mg + mg::kMaxWAll, 8);
+        if (rc) return rc;
+        HIPCHK(ctx, hipMemcpy(&h[mg::kMaxWAll], ctx->mg + mg::kMaxWAll, 8 * ctx->comm.nranks, hipMemcpyDeviceToHost));
+        for (int r = 0; r < ctx->comm.nranks; ++r) {
+            double v;
+            memcpy(&v, &h[mg::kMaxWAll + r], 8);
+            if (v > mx) mx = v;
+        }
+    }
     return reset_ctl_for_new_particles(ctx, dm_weight_exp(mx));
 }
 
@@ -654,14 +843,75 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
     return fp;
 }
 
+// multi-GPU update tail:
+//   shards -> rank record -> all_gather -> every rank finalises the same global scalars
+//   -> normalise + local fixed-point scan -> all_gather of rank totals -> plan of the
+//   global stratified segments -> all_gather of the send counts (one host sync)
+//   -> pack the migrating particles -> all_to_all_v -> expand + gather
+static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
+{
+    const int G = ctx->comm.nranks, me = ctx->comm.rank;
+    HIPCHK(ctx, eslam_launch_shard_reduce(ctx->shards, ctx->rec_local, ctx->stream));
+    int rc = comm_allgather(ctx, ctx->rec_local, ctx->recs, sizeof(Shard));
+    if (rc) return rc;
+    const FinParams fp = fin_params(ctx, mode);
+    HIPCHK(ctx, eslam_launch_finalize(ctx->recs, G, ctx->ctl, &fp, ctx->stream));
+    if (timed) rec(ctx, 2);
+    if (mode == FIN_SUM) return ESLAM_OK;
+    ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
+    sp.multi = 1;
+    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
+                                            ctx->jump, ctx->tile_excl, ctx->mg + mg::kTotal, ctx->stream));
+    rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
+    if (rc) return rc;
+    const PlanParams pp = plan_params(ctx);
+    HIPCHK(ctx, eslam_launch_plan(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->tile_excl, ctx->mg + mg::kTotals, ctx->jump,
+                                  ctx->range, ctx->mg + mg::kFirstLast, ctx->mg + mg::kCounts, ctx->mg + mg::kSdEd,
+                                  ctx->mg + mg::kSendOff, ctx->stream));
+    if (timed) rec(ctx, 3);
+    rc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
+    if (rc) return rc;
+    uint64_t* h = ctx->mg_host;
+    HIPCHK(ctx, hipMemcpyAsync(h + mg::kCountsAll, ctx->mg + mg::kCountsAll, 8ull * G * G, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t R = eslam_record_bytes();
+    uint64_t sb[kMaxRanks], rb[kMaxRanks], nsend = 0, nrecv = 0, any = 0;
+    for (int r = 0; r < G; ++r) {
+        sb[r] = h[mg::kCountsAll + me * G + r] * R;
+        rb[r] = h[mg::kCountsAll + r * G + me] * R;
+        nsend += h[mg::kCountsAll + me * G + r];
+        nrecv += h[mg::kCountsAll + r * G + me];
+        for (int d = 0; d < G; ++d) any |= h[mg::kCountsAll + r * G + d];
+    }
+    if (!any) {                              // no resample this update
+        if (timed) rec(ctx, 4);
+        return ESLAM_OK;
+    }
+    rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
+    if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
+    if (rc) return rc;
+    HIPCHK(ctx, eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
+                                  ctx->mg + mg::kSdEd, ctx->mg + mg::kSendOff, nsend, ctx->sendbuf, ctx->stream));
+    rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
+    if (rc) return rc;
+    const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
+    const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
+    HIPCHK(ctx, eslam_launch_expand_gather(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->recvbuf, nrecv, ctx->gbase, ctx->marks,
+                                           ctx->tile_first, ctx->status, ctx->anc, record, aux, ctx->stream));
+    if (timed) rec(ctx, 4);
+    if (record) ctx->has_anc = true;
+    return ESLAM_OK;
+}
+
 static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
+    if (ctx->sharded) return run_update_tail_multi(ctx, mode, timed);
     const FinParams fp = fin_params(ctx, mode);
-    HIPCHK(ctx, eslam_launch_finalize(ctx->shards, ctx->ctl, &fp, ctx->stream));
+    HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
-                                            ctx->jump, ctx->stream));
+                                            ctx->jump, nullptr, nullptr, ctx->stream));
     if (timed) rec(ctx, 3);
     const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
     const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
@@ -773,9 +1023,9 @@ static int standalone(eslam_ctx* ctx, uint32_t mode)
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
     const uint32_t J = dm_chunk_rows(ctx->n_global);
     HIPCHK(ctx, eslam_launch_weight_stats(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->shards, ctx->stream));
-    if (mode == FIN_SUM) {
+    if (mode == FIN_SUM && !ctx->sharded) {
         const FinParams fp = fin_params(ctx, mode);
-        HIPCHK(ctx, eslam_launch_finalize(ctx->shards, ctx->ctl, &fp, ctx->stream));
+        HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
         return ESLAM_OK;
     }
     return run_update_tail(ctx, mode, false);
@@ -818,13 +1068,32 @@ extern "C" int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index
     HIPCHK(ctx, hipMemcpyAsync(ctx->scratch_host, ctx->scratch, 16, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t* h = reinterpret_cast<const uint64_t*>(ctx->scratch_host);
-    *index = h[1] == ~0ull ? 0 : h[1];
+    if (!ctx->sharded) {
+        *index = h[1] == ~0ull ? 0 : h[1];
+        return ESLAM_OK;
+    }
+    // sharded: the first global maximum = the lowest rank holding the largest key
+    uint64_t* m = ctx->mg_host;
+    m[mg::kBest] = h[0];
+    m[mg::kBest + 1] = h[1] == ~0ull ? ~0ull : ctx->gbase + h[1];
+    HIPCHK(ctx, hipMemcpy(ctx->mg + mg::kBest, &m[mg::kBest], 16, hipMemcpyHostToDevice));
+    const int rc = comm_allgather(ctx, ctx->mg + mg::kBest, ctx->mg + mg::kBestAll, 16);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpy(&m[mg::kBestAll], ctx->mg + mg::kBestAll, 16ull * ctx->comm.nranks, hipMemcpyDeviceToHost));
+    uint64_t best = 0, idx = ~0ull;
+    for (int r = 0; r < ctx->comm.nranks; ++r) {
+        const uint64_t k = m[mg::kBestAll + 2 * r], i = m[mg::kBestAll + 2 * r + 1];
+        if (i == ~0ull) continue;
+        if (idx == ~0ull || k > best) { best = k; idx = i; }
+    }
+    *index = idx == ~0ull ? 0 : idx;
     return ESLAM_OK;
 }
 
 extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double orientation[4])
 {
     if (!ctx || !position || !orientation) return ESLAM_ERR_INVALID_ARG;
+    if (ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "getCentroid is not implemented for a sharded filter");
     int rc = eslam_gpu_normalize_weights(ctx, nullptr);     // side effect, Q15
     if (rc) return rc;
     const uint32_t J = dm_chunk_rows(ctx->n_global);

@@ -128,7 +128,15 @@ struct ScanParams {
     uint32_t phase_b;                    // apply phase-B factors
     uint32_t normalize;                  // divide by S
     uint32_t ntiles;
-    uint32_t pad;
+    uint32_t multi;                      // multi-GPU: tile prefixes + rank total, no marks
+};
+
+constexpr int kMaxRanks = 16;
+
+struct PlanParams {
+    uint64_t n_global;
+    int32_t rank, nranks;
+    uint64_t gbase[kMaxRanks + 1];       // first global index of every rank (+ n_global)
 };
 
 }  // namespace eslam_dev

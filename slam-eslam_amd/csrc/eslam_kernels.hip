@@ -647,23 +647,35 @@ __device__ __forceinline__ double acc_value(const uint64_t* L, uint64_t flags, i
     return dm_limbs_to_double(L, scale);
 }
 
-__global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ shards, Ctl* __restrict__ ctl, FinParams fp)
+// combine field t of nrec statistics records exactly (sum / max / or by field) and zero them
+__device__ __forceinline__ uint64_t reduce_field(Shard* recs, int nrec, int t)
+{
+    uint64_t acc = 0;
+    const int base = 2 * DM_NBUCKETS * 4 + 4;                                  // D
+    for (int k = 0; k < nrec; ++k) {
+        uint64_t* f = reinterpret_cast<uint64_t*>(recs + k) + t;
+        const uint64_t v = *f;
+        if (t == base + 2 || t >= base + 5) acc = acc > v ? acc : v;            // maxm, bbox
+        else if (t == base + 3 || t == base + 4) acc |= v;                      // flags, err
+        else acc += v;
+        *f = 0;
+    }
+    return acc;
+}
+
+// multi-GPU phase 1: this rank's shards -> one record (sent to every rank)
+__global__ void __launch_bounds__(kBlock) k_shard_reduce(Shard* __restrict__ shards, Shard* __restrict__ out)
+{
+    const int t = threadIdx.x;
+    if (t < kShardFields) reinterpret_cast<uint64_t*>(out)[t] = reduce_field(shards, kNShard, t);
+}
+
+// recs: kNShard local shards (one GPU) or the gathered per-rank records (multi-GPU)
+__global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, int nrec, Ctl* __restrict__ ctl, FinParams fp)
 {
     __shared__ uint64_t s[kShardFields];
     const int t = threadIdx.x;
-    if (t < kShardFields) {
-        uint64_t acc = 0;
-        for (int k = 0; k < kNShard; ++k) {
-            uint64_t* f = reinterpret_cast<uint64_t*>(shards + k) + t;
-            const uint64_t v = *f;
-            const int base = 2 * DM_NBUCKETS * 4 + 4;                         // D
-            if (t == base + 2 || t >= base + 5) acc = acc > v ? acc : v;       // maxm, bbox
-            else if (t == base + 3 || t == base + 4) acc |= v;                 // flags, err
-            else acc += v;
-            *f = 0;
-        }
-        s[t] = acc;
-    }
+    if (t < kShardFields) s[t] = reduce_field(recs, nrec, t);
     __syncthreads();
     if (t != 0) return;
 
@@ -781,7 +793,8 @@ constexpr uint64_t kTagAgg = 1ull << 62, kTagInc = 2ull << 62, kValMask = (1ull 
 
 __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                            uint64_t* __restrict__ status, uint32_t* __restrict__ marks,
-                                                           uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt)
+                                                           uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt,
+                                                           uint64_t* __restrict__ tile_excl, uint64_t* __restrict__ total)
 {
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_wtot[kWaves];
@@ -895,6 +908,15 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     }
     __syncthreads();
     const uint64_t excl = s_excl;
+    if (sp.multi) {
+        // multi-GPU: keep the tile's exclusive prefix and the rank total; the segment
+        // boundaries need the other ranks' totals (k_plan)
+        if (tid == 0) {
+            tile_excl[tile] = excl;
+            if (tile == sp.ntiles - 1) *total = excl + agg;
+        }
+        return;
+    }
 
     // ---- segment boundaries: particle i covers draws [lo_i, hi_i) ----
     const uint64_t N = sp.n_global;
@@ -926,10 +948,18 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
 // the particle state into the other buffer (xi_k.swap(xi_kp), src/ParticleFilter.hpp:107).
 // Weights are carried, not reset (Q4).
 // ---------------------------------------------------------------------------------------
+struct alignas(8) Rec {                  // one migrating particle (72 bytes)
+    double x, y, th, z, zs, w, mprob;
+    uint64_t lohi;                       // [lo, hi) of the outputs it fills (global, clipped)
+    uint64_t src;                        // flags | global source index << 8
+};
+static_assert(sizeof(Rec) == 72, "record size");
+
+template <bool RECS>
 __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                             uint32_t* __restrict__ marks, const uint32_t* __restrict__ tile_first,
                                                             uint64_t* __restrict__ status, uint32_t* __restrict__ anc,
-                                                            uint32_t record, uint32_t aux)
+                                                            uint32_t record, uint32_t aux, const Rec* __restrict__ recs)
 {
     if (!ctl->resample) return;
     __shared__ uint32_t s_wmax[kWaves];
@@ -975,6 +1005,13 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
         const uint64_t k = (uint64_t)t * kGatherTile + slot;
         if (k >= sp.n) continue;
         const uint32_t i = s_idx[slot];
+        if (RECS) {
+            const Rec& r = recs[i];
+            out.x[k] = r.x; out.y[k] = r.y; out.th[k] = r.th; out.z[k] = r.z; out.zs[k] = r.zs; out.w[k] = r.w;
+            if (aux) { out.mprob[k] = r.mprob; out.flags[k] = (uint8_t)r.src; }
+            if (record) anc[k] = (uint32_t)(r.src >> 8);
+            continue;
+        }
         out.x[k] = in.x[i];
         out.y[k] = in.y[i];
         out.th[k] = in.th[i];
@@ -986,6 +1023,142 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
             out.flags[k] = in.flags[i];
         }
         if (record) anc[k] = i;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// multi-GPU resample: plan (global segment boundaries + per-destination send ranges),
+// pack, expand, gather.  Output k of the global filter lives on the rank whose shard
+// holds global index k; particle i of rank r fills outputs [lo_i, hi_i).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void plan_bounds(const PlanParams& pp, const Ctl* ctl, const uint64_t* totals,
+                                            const uint32_t* jt, uint64_t& off, uint64_t& O0, uint64_t& O1)
+{
+    off = 0;
+    for (int r = 0; r < pp.rank; ++r) off += totals[r];
+    const uint64_t N = pp.n_global;
+    const uint32_t xs = ctl->minstd_start;
+    const int shift = ctl->scan_shift;
+    O0 = pp.rank == 0 ? 0 : count_draws_le(off, N, xs, shift, jt);
+    O1 = pp.rank == pp.nranks - 1 ? N : count_draws_le(off + totals[pp.rank], N, xs, shift, jt);
+}
+
+__global__ void __launch_bounds__(kBlock) k_plan(DevState s0, DevState s1, ScanParams sp, PlanParams pp, Ctl* __restrict__ ctl,
+                                                 const uint64_t* __restrict__ tile_excl, const uint64_t* __restrict__ totals,
+                                                 const uint32_t* __restrict__ jt, uint2* __restrict__ range,
+                                                 uint64_t* __restrict__ first_last)
+{
+    __shared__ uint64_t s_wtot[kWaves];
+    if (!ctl->resample) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tile = blockIdx.x;
+    const DevState st = ctl->base ? s1 : s0;
+    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+    const int shift = ctl->scan_shift;
+    uint64_t c[kScanItems];
+    uint64_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        if (i < sp.n) run += fx_shift(st.w[i], shift);
+        c[r] = run;
+    }
+    uint64_t tincl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_up(tincl, o, 64);
+        if ((int)lane >= o) tincl += t;
+    }
+    if (lane == 63) s_wtot[wave] = tincl;
+    __syncthreads();
+    uint64_t wexcl = 0;
+    for (uint32_t wv = 0; wv < wave; ++wv) wexcl += s_wtot[wv];
+    uint64_t off, O0, O1;
+    plan_bounds(pp, ctl, totals, jt, off, O0, O1);
+    const uint64_t base = off + tile_excl[tile] + wexcl + (tincl - run);
+    const uint64_t N = pp.n_global;
+    const uint32_t xs = ctl->minstd_start;
+    uint64_t lo = count_draws_le(base, N, xs, shift, jt);
+    if (i0 == 0) lo = O0;
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        if (i >= sp.n) break;
+        uint64_t hi = count_draws_le(base + c[r], N, xs, shift, jt);
+        if (i + 1 == sp.n) {
+            if (pp.rank == pp.nranks - 1 && hi < N)
+                atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
+            hi = O1;
+        }
+        range[i] = make_uint2((uint32_t)lo, (uint32_t)hi);
+        if (hi > lo) {
+            for (int d = 0; d < pp.nranks; ++d) {
+                const uint64_t W0 = pp.gbase[d], W1 = pp.gbase[d + 1];
+                const uint64_t Sd = O0 > W0 ? O0 : W0, Ed = O1 < W1 ? O1 : W1;
+                if (Sd >= Ed) continue;
+                if (lo <= Sd && Sd < hi) first_last[2 * d] = i;
+                if (lo <= Ed - 1 && Ed - 1 < hi) first_last[2 * d + 1] = i;
+            }
+        }
+        lo = hi;
+    }
+}
+
+// counts[d] = particles this rank sends to rank d (0 when not resampling), their clipped
+// output ranges [S_d, E_d) and the packing offsets send_off[0..nranks]
+__global__ void k_plan_counts(const Ctl* __restrict__ ctl, PlanParams pp, const uint64_t* __restrict__ totals,
+                              const uint32_t* __restrict__ jt, const uint64_t* __restrict__ first_last,
+                              uint64_t* __restrict__ counts, uint64_t* __restrict__ sd_ed, uint64_t* __restrict__ send_off)
+{
+    if (threadIdx.x != 0) return;
+    uint64_t off, O0 = 0, O1 = 0;
+    if (ctl->resample) plan_bounds(pp, ctl, totals, jt, off, O0, O1);
+    uint64_t acc = 0;
+    send_off[0] = 0;
+    for (int d = 0; d < pp.nranks; ++d) {
+        const uint64_t W0 = pp.gbase[d], W1 = pp.gbase[d + 1];
+        const uint64_t Sd = O0 > W0 ? O0 : W0, Ed = O1 < W1 ? O1 : W1;
+        uint64_t cnt = 0;
+        if (ctl->resample && Sd < Ed) cnt = first_last[2 * d + 1] - first_last[2 * d] + 1;
+        counts[d] = cnt;
+        sd_ed[2 * d] = Sd;
+        sd_ed[2 * d + 1] = Ed;
+        acc += cnt;
+        send_off[d + 1] = acc;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
+                                                 const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
+                                                 const uint64_t* __restrict__ sd_ed, const uint64_t* __restrict__ send_off,
+                                                 Rec* __restrict__ send)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= send_off[pp.nranks]) return;
+    int d = 0;
+    while (j >= send_off[d + 1]) ++d;
+    const uint64_t i = first_last[2 * d] + (j - send_off[d]);
+    const DevState st = ctl->base ? s1 : s0;
+    const uint2 rg = range[i];
+    const uint64_t Sd = sd_ed[2 * d], Ed = sd_ed[2 * d + 1];
+    const uint64_t lo = rg.x > Sd ? rg.x : Sd, hi = rg.y < Ed ? rg.y : Ed;
+    Rec r;
+    r.x = st.x[i]; r.y = st.y[i]; r.th = st.th[i]; r.z = st.z[i]; r.zs = st.zs[i]; r.w = st.w[i]; r.mprob = st.mprob[i];
+    r.lohi = lo | (hi << 32);
+    r.src = (uint64_t)st.flags[i] | ((pp.gbase[pp.rank] + i) << 8);
+    send[j] = r;
+}
+
+__global__ void __launch_bounds__(kBlock) k_expand(const Rec* __restrict__ recv, uint64_t nrecv, uint64_t W0,
+                                                   uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= nrecv) return;
+    const uint64_t lh = recv[j].lohi;
+    const uint64_t glo = lh & 0xffffffffull, ghi = lh >> 32;
+    if (ghi > glo) {
+        const uint64_t lo = glo - W0, hi = ghi - W0;
+        marks[lo] = (uint32_t)(j + 1);
+        for (uint64_t t = (lo + kGatherTile - 1) / kGatherTile; t * kGatherTile < hi; ++t) tile_first[t] = (uint32_t)j;
     }
 }
 
@@ -1151,18 +1324,25 @@ extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_finalize(Shard* shards, Ctl* ctl, const FinParams* fp, hipStream_t stream)
+extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, stream, shards, ctl, *fp);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, stream, recs, nrec, ctl, *fp);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_shard_reduce, dim3(1), dim3(kBlock), 0, stream, shards, out);
     return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
-                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream)
+                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt,
+                                                  uint64_t* tile_excl, uint64_t* total, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
     hipLaunchKernelGGL(k_normalize_scan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, status, marks,
-                       tile_first, jt);
+                       tile_first, jt, tile_excl, total);
     return hipGetLastError();
 }
 
@@ -1171,10 +1351,45 @@ extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, con
                                                    uint32_t record, uint32_t aux, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_resample_gather, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, marks, tile_first,
-                       status, anc, record, aux);
+    hipLaunchKernelGGL(k_resample_gather<false>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, marks, tile_first,
+                       status, anc, record, aux, (const Rec*)nullptr);
     return hipGetLastError();
 }
+
+extern "C" hipError_t eslam_launch_plan(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
+                                        const uint64_t* tile_excl, const uint64_t* totals, const uint32_t* jt, uint2* range,
+                                        uint64_t* first_last, uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off,
+                                        hipStream_t stream)
+{
+    if (sp->ntiles) hipLaunchKernelGGL(k_plan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl, tile_excl,
+                                       totals, jt, range, first_last);
+    hipLaunchKernelGGL(k_plan_counts, dim3(1), dim3(64), 0, stream, ctl, *pp, totals, jt, first_last, counts, sd_ed, send_off);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
+                                        const uint64_t* first_last, const uint64_t* sd_ed, const uint64_t* send_off,
+                                        uint64_t nsend, void* send, hipStream_t stream)
+{
+    if (!nsend) return hipSuccess;
+    hipLaunchKernelGGL(k_pack, dim3((uint32_t)((nsend + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, s0, s1, ctl, *pp,
+                       range, first_last, sd_ed, send_off, (Rec*)send);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_expand_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const void* recv,
+                                                 uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* tile_first,
+                                                 uint64_t* status, uint32_t* anc, uint32_t record, uint32_t aux,
+                                                 hipStream_t stream)
+{
+    if (nrecv) hipLaunchKernelGGL(k_expand, dim3((uint32_t)((nrecv + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                                  (const Rec*)recv, nrecv, W0, marks, tile_first);
+    if (sp->ntiles) hipLaunchKernelGGL(k_resample_gather<true>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl,
+                                       marks, tile_first, status, anc, record, aux, (const Rec*)recv);
+    return hipGetLastError();
+}
+
+extern "C" uint64_t eslam_record_bytes(void) { return sizeof(Rec); }
 
 extern "C" hipError_t eslam_launch_init_gaussian(DevState s0, uint64_t n, uint64_t gbase, uint64_t seed, uint64_t ev,
                                                  const double mu[3], const double sigma[3], double zpos, double zsigma,

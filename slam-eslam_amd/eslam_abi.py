@@ -148,6 +148,47 @@ class KernelTimes(C.Structure):
     ]
 
 
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p,
+                           C.POINTER(C.c_uint64), C.c_void_p)
+
+
+class Comm(C.Structure):
+    """eslam_comm (include/eslam_gpu.h)."""
+    _fields_ = [
+        ("user", C.c_void_p),
+        ("rank", C.c_int32), ("nranks", C.c_int32),
+        ("device_memory", C.c_int32), ("pad", C.c_int32),
+        ("allgather", ALLGATHER_FN),
+        ("alltoallv", ALLTOALLV_FN),
+    ]
+
+
+MAX_RANKS = 16
+
+
+def chunk_rows(n_global):
+    """dm_chunk_rows (include/eslam_detmath.h): rows of 64 lanes per canonical summation chunk."""
+    q = n_global // 262144
+    j = 1
+    while j < 16 and j * 2 <= q:
+        j *= 2
+    return j
+
+
+def shard_bounds(n_global, nranks):
+    """First global index of every rank (+ n_global): near-equal shards whose starts are
+    multiples of the summation chunk (64 * chunk_rows), as eslam_gpu_set_comm requires."""
+    csz = 64 * chunk_rows(n_global)
+    chunks = -(-n_global // csz)
+    if chunks < nranks:
+        raise ValueError(f"{n_global} particles cannot be split into {nranks} chunk-aligned shards")
+    g = [min(n_global, (chunks * r // nranks) * csz) for r in range(nranks)] + [n_global]
+    if any(g[r + 1] <= g[r] for r in range(nranks)):
+        raise ValueError("empty shard")
+    return g
+
+
 def default_config(lib=None):
     """eslam_config_default() restated (src/Configuration.hpp:85-111 defaults)."""
     import math

@@ -1,0 +1,95 @@
+"""Scenarios shared by the multi-rank tests (test infrastructure).
+
+``run_scenario`` drives one filter -- the whole filter (lo=0, hi=n_global) or one rank's
+shard [lo, hi) of it -- through a fixed sequence of inputs and records everything the
+rank holds after every call.  A sharded run concatenated over the ranks must equal the
+single run bit for bit (include/eslam_gpu.h, eslam_gpu_set_comm)."""
+import numpy as np
+
+import eslam_abi as A
+import synthetic as S
+
+FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
+SCENARIOS = ("forced", "natural", "upload")
+
+
+def scenario_config(name, n_global):
+    cfg = A.default_config()
+    cfg.seed = 1234
+    cfg.flags |= A.FLAG_RECORD_ANCESTORS
+    if name == "forced":
+        S.bench_config(cfg, n_global)
+    else:
+        cfg.particle_count = n_global
+        cfg.min_effective = (n_global * 9) // 10
+        cfg.measurement_threshold_distance = -1.0
+        cfg.measurement_threshold_angle = -1.0
+    return cfg
+
+
+def scenario_grid(name):
+    return S.rough_map(cells=120) if name != "forced" else S.rough_map(cells=120, multi=False)
+
+
+def upload_arrays(n_global, lo, hi):
+    rng = np.random.default_rng(99)
+    pa = A.ParticleArrays(n_global)
+    pa.x[:] = rng.normal(0, 0.2, n_global)
+    pa.y[:] = rng.normal(0, 0.2, n_global)
+    pa.orientation[:] = rng.normal(0, 0.1, n_global)
+    pa.zpos[:] = 0.18 + rng.normal(0, 0.01, n_global)
+    pa.zsigma[:] = 0.5
+    w = rng.exponential(1.0, n_global) ** 3
+    w[rng.random(n_global) < 0.2] = 0.0
+    pa.weight[:] = w
+    pa.mprob[:] = 1.0
+    pa.floating[:] = 1
+    pa.n_contact_points[:] = 0
+    out = A.ParticleArrays(hi - lo)
+    for f in FIELDS:
+        getattr(out, f)[:] = getattr(pa, f)[lo:hi]
+    return out
+
+
+def _snap(rec, key, f, with_anc):
+    pa = f.download()
+    for fld in FIELDS:
+        rec[f"{key}/{fld}"] = np.array(getattr(pa, fld))
+    if with_anc:
+        a = f.ancestors()
+        if a is not None:
+            rec[f"{key}/anc"] = a
+
+
+def _info(rec, key, i):
+    rec[f"{key}/info"] = np.array([i.effective, i.weight_sum, i.floating_weight, i.max_weight,
+                                   float(i.data_particles), float(i.total_points), float(i.resampled),
+                                   float(i.uniform_reset)])
+
+
+def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
+    """f: OracleFilter or GpuFilter-like (set_map/init_gaussian/upload/step/...).
+    info_fn(f) returns the eslam_update_info of the last update."""
+    rec = {}
+    grid = scenario_grid(name)
+    f.set_map(grid)
+    if name == "upload":
+        f.upload(upload_arrays(n_global, lo, hi))
+        rec["sum0"] = np.array([f.weights_sum()])
+        rec["best0"] = np.array([f.best_index()])
+        rec["eff0"] = np.array([f.normalize()])
+        _snap(rec, "norm", f, False)
+        f.resample()
+        _snap(rec, "res", f, True)
+    else:
+        sigma = [0.1, 0.1, 0.1] if name == "forced" else [0.6, 0.6, 0.3]
+        f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], sigma, 0.18, 1.001)
+    _snap(rec, "init", f, False)
+    stream = S.step_stream(steps, tilt=(name == "natural"))
+    for k, st in enumerate(stream):
+        f.step(st)
+        _info(rec, f"s{k}", info_fn(f))
+        _snap(rec, f"s{k}", f, True)
+    rec["best"] = np.array([f.best_index()])
+    rec["rng"] = np.array([f.rng_state().minstd_x])
+    return rec

@@ -1,0 +1,55 @@
+"""One rank of a multi-rank test: runs a scenario on its shard and saves what it holds.
+
+    RANK=r WORLD_SIZE=w MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
+        python tests/dist_worker.py {oracle|gpu} SCENARIO N_GLOBAL OUT.npz [host|device]
+
+oracle: the CPU oracle's sharded mode over gloo (host-memory callbacks);
+gpu:    libeslam_gpu sharded over gloo (host staging) or, with 'device', RCCL on device
+        buffers (one rank per GPU).
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "slam-eslam_amd"))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    kind, name, n_global, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    mem = sys.argv[5] if len(sys.argv) > 5 else "host"
+    import torch
+    import torch.distributed as dist
+    import eslam_abi as A
+    import eslam_dist
+    from dist_scenarios import run_scenario, scenario_config
+    rank = int(os.environ["RANK"])
+    if kind == "gpu" and mem == "device":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl")
+    else:
+        dist.init_process_group("gloo")
+    comm = eslam_dist.TorchComm(device_memory=(mem == "device"))
+    cfg = scenario_config(name, n_global)
+    bounds = A.shard_bounds(n_global, comm.nranks)
+    lo, hi = bounds[rank], bounds[rank + 1]
+    if kind == "oracle":
+        import oracle_ffi as O
+        f = O.OracleFilter(cfg, O.SUM_CONTRACT)
+        f.set_comm(comm, n_global)
+        rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.info())
+    else:
+        f = eslam_dist.ShardedGpuFilter(cfg, n_global, comm, device=int(os.environ.get("LOCAL_RANK", "0")))
+        rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.sync())
+        f.close()
+    if comm.error is not None:
+        raise comm.error
+    np.savez(out, **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

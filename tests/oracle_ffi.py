@@ -95,6 +95,7 @@ def lib():
     L.or_bucket_index.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double]
     L.or_mls_get_patch.argtypes = [C.POINTER(A.MlsGrid), C.POINTER(C.c_double), C.c_double, C.c_double,
                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.or_set_comm.argtypes = [vp, C.POINTER(A.Comm), C.c_uint64, C.POINTER(C.c_uint64)]
     L.or_dm.restype = C.c_double
     L.or_dm.argtypes = [C.c_int, C.c_double, C.c_double]
     L.or_dm_philox.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32)]
@@ -125,6 +126,14 @@ class OracleFilter:
         if getattr(self, "h", None):
             self.L.or_destroy(self.h)
             self.h = None
+
+    def set_comm(self, comm, n_global):
+        """Sharded mode over a host-memory eslam_comm (slam-eslam_amd/eslam_dist.TorchComm)."""
+        self._comm = comm
+        self.bounds = A.shard_bounds(n_global, comm.nranks)
+        self._gb = (C.c_uint64 * len(self.bounds))(*self.bounds)
+        rc = self.L.or_set_comm(self.h, C.byref(comm.struct), n_global, self._gb)
+        assert rc == 0, rc
 
     def set_map(self, grid):
         self._map = grid

@@ -19,6 +19,7 @@ for step in "$@"; do
     testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    benchsharded) run bench_sharded 600 python bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchshort) run bench 600 python bench.py --steps 20 --warmup 5 --cpu-steps 2 ;;
   esac
 done
