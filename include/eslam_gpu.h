@@ -245,7 +245,7 @@ typedef struct eslam_comm {
 
 /* Make this context shard [gbase, gbase + n_local) of an n_global-particle filter; call
  * before init.  shard_gbase lists the first global index of every rank (nranks + 1
- * entries, strictly increasing, last = n_global < 2^32); every entry must be a multiple
+ * entries, strictly increasing, last = n_global <= 2^30 - 64); every entry must be a multiple
  * of 64 * dm_chunk_rows(n_global) (the canonical summation chunk) except the last.
  * The context's config particle_count is the global count.  Sharded contexts support
  * the hot path (step/project/update/sync), init, upload/download of the local shard,

@@ -27,12 +27,12 @@ extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64
 extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
-                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt,
-                                                  uint64_t* tile_excl, uint64_t* total, hipStream_t stream);
-extern "C" hipError_t eslam_launch_plan(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
-                                        const uint64_t* tile_excl, const uint64_t* totals, const uint32_t* jt, uint2* range,
-                                        uint64_t* first_last, uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off,
-                                        hipStream_t stream);
+                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, uint64_t* total,
+                                                  hipStream_t stream);
+extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
+                                                  uint64_t* status, uint32_t* marks, uint32_t* tile_first,
+                                                  const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
+                                                  uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
                                         const uint64_t* first_last, const uint64_t* sd_ed, const uint64_t* send_off,
                                         uint64_t nsend, void* send, hipStream_t stream);
@@ -230,7 +230,6 @@ struct eslam_ctx {
     Shard* recs = nullptr;                  // gathered records of all ranks
     uint64_t* mg = nullptr;                 // MgBlock (device)
     uint64_t* mg_host = nullptr;            // pinned
-    uint64_t* tile_excl = nullptr;          // per scan tile: exclusive fixed-point prefix
     uint2* range = nullptr;                 // per particle: [lo, hi) of its global outputs
     void* sendbuf = nullptr; uint64_t send_cap = 0;
     void* recvbuf = nullptr; uint64_t recv_cap = 0;
@@ -403,7 +402,6 @@ static void free_particles(eslam_ctx* ctx)
     hipFree(ctx->tile_first); ctx->tile_first = nullptr;
     hipFree(ctx->status); ctx->status = nullptr;
     hipFree(ctx->anc); ctx->anc = nullptr;
-    hipFree(ctx->tile_excl); ctx->tile_excl = nullptr;
     hipFree(ctx->range); ctx->range = nullptr;
     ctx->n = ctx->cap = 0;
     ctx->has_anc = false;
@@ -472,7 +470,6 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     ctx->n = n;
     ctx->cap = cap;
     if (ctx->sharded) {
-        HIPCHK(ctx, hipMalloc(&ctx->tile_excl, ntiles * 8));
         HIPCHK(ctx, hipMalloc(&ctx->range, cap * sizeof(uint2)));
     } else {
         ctx->n_global = n;
@@ -570,8 +567,8 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
     if (!shard_gbase || !comm->allgather || !comm->alltoallv || comm->nranks < 1 || comm->nranks > kMaxRanks ||
         comm->rank < 0 || comm->rank >= comm->nranks)
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: bad communicator (1 <= nranks <= 16)");
-    if (n_global == 0 || n_global >= (1ull << 32) - 1)
-        return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: n_global must be in [1, 2^32 - 1)");
+    if (n_global == 0 || n_global > (1ull << 30) - 64)     // resample mark encoding (kMarkOwn)
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: n_global must be in [1, 2^30 - 64]");
     const uint64_t csz = 64ull * dm_chunk_rows(n_global);
     if (shard_gbase[0] != 0 || shard_gbase[comm->nranks] != n_global)
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: shard_gbase must run from 0 to n_global");
@@ -845,9 +842,10 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
 
 // multi-GPU update tail:
 //   shards -> rank record -> all_gather -> every rank finalises the same global scalars
-//   -> normalise + local fixed-point scan -> all_gather of rank totals -> plan of the
-//   global stratified segments -> all_gather of the send counts (one host sync)
-//   -> pack the migrating particles -> all_to_all_v -> expand + gather
+//   -> normalise + this rank's fixed-point weight total -> all_gather of the totals
+//   -> global stratified segments (outputs in this rank's slice are marked directly)
+//   -> all_gather of the send counts (one host sync) -> pack the particles whose outputs
+//   lie in other slices -> all_to_all_v -> expand + gather
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const int G = ctx->comm.nranks, me = ctx->comm.rank;
@@ -860,42 +858,47 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     if (mode == FIN_SUM) return ESLAM_OK;
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
     sp.multi = 1;
+    HIPCHK(ctx, hipMemsetAsync(ctx->mg + mg::kTotal, 0, 8, ctx->stream));
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
-                                            ctx->jump, ctx->tile_excl, ctx->mg + mg::kTotal, ctx->stream));
+                                            ctx->jump, ctx->mg + mg::kTotal, ctx->stream));
     rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
     if (rc) return rc;
     const PlanParams pp = plan_params(ctx);
-    HIPCHK(ctx, eslam_launch_plan(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->tile_excl, ctx->mg + mg::kTotals, ctx->jump,
-                                  ctx->range, ctx->mg + mg::kFirstLast, ctx->mg + mg::kCounts, ctx->mg + mg::kSdEd,
-                                  ctx->mg + mg::kSendOff, ctx->stream));
+    HIPCHK(ctx, eslam_launch_segments_multi(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->status, ctx->marks,
+                                            ctx->tile_first, ctx->mg + mg::kTotals, ctx->jump, ctx->range,
+                                            ctx->mg + mg::kFirstLast, ctx->mg + mg::kCounts, ctx->mg + mg::kSdEd,
+                                            ctx->mg + mg::kSendOff, ctx->stream));
     if (timed) rec(ctx, 3);
-    rc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
-    if (rc) return rc;
-    uint64_t* h = ctx->mg_host;
-    HIPCHK(ctx, hipMemcpyAsync(h + mg::kCountsAll, ctx->mg + mg::kCountsAll, 8ull * G * G, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    const uint64_t R = eslam_record_bytes();
-    uint64_t sb[kMaxRanks], rb[kMaxRanks], nsend = 0, nrecv = 0, any = 0;
-    for (int r = 0; r < G; ++r) {
-        sb[r] = h[mg::kCountsAll + me * G + r] * R;
-        rb[r] = h[mg::kCountsAll + r * G + me] * R;
-        nsend += h[mg::kCountsAll + me * G + r];
-        nrecv += h[mg::kCountsAll + r * G + me];
-        for (int d = 0; d < G; ++d) any |= h[mg::kCountsAll + r * G + d];
-    }
-    if (!any) {                              // no resample this update
-        if (timed) rec(ctx, 4);
-        return ESLAM_OK;
-    }
-    rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
-    if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
-    if (rc) return rc;
-    HIPCHK(ctx, eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
-                                  ctx->mg + mg::kSdEd, ctx->mg + mg::kSendOff, nsend, ctx->sendbuf, ctx->stream));
-    rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
-    if (rc) return rc;
     const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
     const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
+    uint64_t nrecv = 0;
+    if (G > 1) {                             // particle migration between slices
+        rc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
+        if (rc) return rc;
+        uint64_t* h = ctx->mg_host;
+        HIPCHK(ctx, hipMemcpyAsync(h + mg::kCountsAll, ctx->mg + mg::kCountsAll, 8ull * G * G, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        const uint64_t R = eslam_record_bytes();
+        uint64_t sb[kMaxRanks], rb[kMaxRanks], nsend = 0, any = 0;
+        for (int r = 0; r < G; ++r) {
+            sb[r] = h[mg::kCountsAll + me * G + r] * R;
+            rb[r] = h[mg::kCountsAll + r * G + me] * R;
+            nsend += h[mg::kCountsAll + me * G + r];
+            nrecv += h[mg::kCountsAll + r * G + me];
+            for (int d = 0; d < G; ++d) any |= h[mg::kCountsAll + r * G + d];
+        }
+        if (any) {
+            rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
+            if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
+            if (rc) return rc;
+            HIPCHK(ctx, eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
+                                          ctx->mg + mg::kSdEd, ctx->mg + mg::kSendOff, nsend, ctx->sendbuf, ctx->stream));
+            rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
+            if (rc) return rc;
+        }
+    }
+    // the gather runs on the device's resample decision (no-op without a resample)
     HIPCHK(ctx, eslam_launch_expand_gather(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->recvbuf, nrecv, ctx->gbase, ctx->marks,
                                            ctx->tile_first, ctx->status, ctx->anc, record, aux, ctx->stream));
     if (timed) rec(ctx, 4);
@@ -911,7 +914,7 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     if (timed) rec(ctx, 2);
     const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
-                                            ctx->jump, nullptr, nullptr, ctx->stream));
+                                            ctx->jump, nullptr, ctx->stream));
     if (timed) rec(ctx, 3);
     const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
     const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;

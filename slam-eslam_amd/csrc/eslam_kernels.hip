@@ -791,64 +791,17 @@ __device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint3
 // ---------------------------------------------------------------------------------------
 constexpr uint64_t kTagAgg = 1ull << 62, kTagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
 
-__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
-                                                           uint64_t* __restrict__ status, uint32_t* __restrict__ marks,
-                                                           uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt,
-                                                           uint64_t* __restrict__ tile_excl, uint64_t* __restrict__ total)
+// multi-GPU mark encoding (monotone in output order): records from lower ranks,
+// then this rank's own particles, then records from higher ranks
+constexpr uint32_t kMarkOwn = 1u << 30, kMarkHigh = 1u << 31;
+
+// Inclusive scan of one 2048-particle tile (thread -> wave -> block) chained to the
+// previous tiles by the decoupled look-back.  In: run = this thread's total.  Returns the
+// exclusive prefix of the thread's first item (tile prefix + in-tile prefix).
+__device__ __forceinline__ uint64_t tile_scan(uint64_t run, uint32_t tile, uint64_t* __restrict__ status,
+                                              Ctl* __restrict__ ctl, uint64_t* s_wtot, uint64_t* s_excl)
 {
-    __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_wtot[kWaves];
-    __shared__ uint64_t s_excl;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const bool resample = ctl->resample != 0;
-    uint32_t tile = blockIdx.x;
-    if (resample) {
-        if (tid == 0) s_tile = (uint32_t)atomicAdd((unsigned long long*)&ctl->tile_counter, 1ull);
-        __syncthreads();
-        tile = s_tile;
-    }
-    const DevState st = ctl->base ? s1 : s0;
-    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
-    const double S = ctl->S;
-    const bool uniform = ctl->uniform != 0;
-    const double inv_n = ctl->inv_n;
-    double f[DM_NBUCKETS];
-#pragma unroll
-    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
-
-    double w[kScanItems];
-#pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        const uint64_t i = i0 + r;
-        w[r] = 0.0;
-        if (i < sp.n) {
-            double v = st.w[i];
-            if (sp.phase_b) {
-                const uint32_t fl = st.flags[i];
-                const uint32_t ncp = fl & 0x7fu;
-                const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
-                double fb = f[0];
-#pragma unroll
-                for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
-                const double factor = st.mprob[i] * fb;
-                v *= factor;
-            }
-            if (sp.normalize) v = uniform ? inv_n : v / S;
-            if (sp.phase_b || sp.normalize) st.w[i] = v;
-            w[r] = v;
-        }
-    }
-    if (!resample) return;
-
-    // ---- fixed-point inclusive scan: thread -> wave -> block ----
-    const int shift = ctl->scan_shift;
-    uint64_t c[kScanItems];
-    uint64_t run = 0;
-#pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        run += fx_shift(w[r], shift);
-        c[r] = run;
-    }
     uint64_t tincl = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -865,7 +818,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     }
     const uint64_t texcl = wexcl + (tincl - run);
 
-    // ---- decoupled look-back (wave 0): 8-byte {tag, value} granules, relaxed agent scope ----
+    // decoupled look-back (wave 0): 8-byte {tag, value} granules, relaxed agent scope
     if (wave == 0) {
         uint64_t excl = 0;
         if (tile == 0) {
@@ -904,50 +857,210 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
             if (__ballot(timeout) != 0ull && lane == 0) atomicOr((unsigned long long*)&ctl->err, 2ull);
             if (lane == 0) atomic_store_agent(&status[tile], kTagInc | ((excl + agg) & kValMask));
         }
-        if (lane == 0) s_excl = excl;
+        if (lane == 0) *s_excl = excl;
     }
     __syncthreads();
-    const uint64_t excl = s_excl;
-    if (sp.multi) {
-        // multi-GPU: keep the tile's exclusive prefix and the rank total; the segment
-        // boundaries need the other ranks' totals (k_plan)
-        if (tid == 0) {
-            tile_excl[tile] = excl;
-            if (tile == sp.ntiles - 1) *total = excl + agg;
+    return *s_excl + texcl;
+}
+
+// mark the segment [lo, hi) (outputs relative to this rank's slice) with value v
+__device__ __forceinline__ void mark_segment(uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
+                                             uint64_t lo, uint64_t hi, uint32_t v)
+{
+    marks[lo] = v;
+    for (uint64_t t = (lo + kGatherTile - 1) / kGatherTile; t * kGatherTile < hi; ++t) tile_first[t] = v - 1u;
+}
+
+__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+                                                           uint64_t* __restrict__ status, uint32_t* __restrict__ marks,
+                                                           uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt,
+                                                           uint64_t* __restrict__ total)
+{
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_wtot[kWaves];
+    __shared__ uint64_t s_excl;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const bool resample = ctl->resample != 0;
+    uint32_t tile = blockIdx.x;
+    if (resample && !sp.multi) {
+        if (tid == 0) s_tile = (uint32_t)atomicAdd((unsigned long long*)&ctl->tile_counter, 1ull);
+        __syncthreads();
+        tile = s_tile;
+    }
+    const DevState st = ctl->base ? s1 : s0;
+    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+    const double S = ctl->S;
+    const bool uniform = ctl->uniform != 0;
+    const double inv_n = ctl->inv_n;
+    double f[DM_NBUCKETS];
+#pragma unroll
+    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
+
+    double w[kScanItems];
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        w[r] = 0.0;
+        if (i < sp.n) {
+            double v = st.w[i];
+            if (sp.phase_b) {
+                const uint32_t fl = st.flags[i];
+                const uint32_t ncp = fl & 0x7fu;
+                const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
+                double fb = f[0];
+#pragma unroll
+                for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
+                const double factor = st.mprob[i] * fb;
+                v *= factor;
+            }
+            if (sp.normalize) v = uniform ? inv_n : v / S;
+            if (sp.phase_b || sp.normalize) st.w[i] = v;
+            w[r] = v;
         }
+    }
+    if (!resample) return;
+
+    const int shift = ctl->scan_shift;
+    uint64_t c[kScanItems];
+    uint64_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        run += fx_shift(w[r], shift);
+        c[r] = run;
+    }
+    if (sp.multi) {
+        // multi-GPU: only this rank's fixed-point total (exact, any order); the segments
+        // need every rank's total (k_segments_multi)
+        uint64_t t = run;
+        for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+        if (lane == 0 && t) atomicAdd((unsigned long long*)total, (unsigned long long)t);
         return;
     }
+    const uint64_t base = tile_scan(run, tile, status, ctl, s_wtot, &s_excl);
 
     // ---- segment boundaries: particle i covers draws [lo_i, hi_i) ----
     const uint64_t N = sp.n_global;
     const uint32_t xs = ctl->minstd_start;
-    uint64_t lo = count_draws_le(excl + texcl, N, xs, shift, jt);
-    if (i0 == 0 && sp.gbase == 0) lo = 0;
+    uint64_t lo = count_draws_le(base, N, xs, shift, jt);
+    if (i0 == 0) lo = 0;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const uint64_t i = i0 + r;
         if (i >= sp.n) break;
-        const uint64_t gi = sp.gbase + i;
-        const uint64_t cc = excl + texcl + c[r];
-        uint64_t hi = count_draws_le(cc, N, xs, shift, jt);
-        if (gi == N - 1) {
+        uint64_t hi = count_draws_le(base + c[r], N, xs, shift, jt);
+        if (i == N - 1) {
             if (hi < N) atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
             hi = N;
         }
-        if (hi > lo) {
-            marks[lo] = (uint32_t)(i + 1);
-            for (uint64_t t = (lo + kGatherTile - 1) / kGatherTile; t * kGatherTile < hi; ++t)
-                tile_first[t] = (uint32_t)i;
-        }
+        if (hi > lo) mark_segment(marks, tile_first, lo, hi, (uint32_t)(i + 1));
         lo = hi;
     }
 }
 
 // ---------------------------------------------------------------------------------------
-// k_resample_gather: expand the segments (inclusive max-scan of the marks) and gather
-// the particle state into the other buffer (xi_k.swap(xi_kp), src/ParticleFilter.hpp:107).
-// Weights are carried, not reset (Q4).
+// multi-GPU segments: the same scan, offset by the lower ranks' totals.  Outputs that land
+// in this rank's slice [W0, W1) are marked directly (own particles never move); particles
+// whose outputs reach another rank's slice record their range for k_pack.
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void plan_bounds(const PlanParams& pp, const Ctl* ctl, const uint64_t* totals,
+                                            const uint32_t* jt, uint64_t& off, uint64_t& O0, uint64_t& O1)
+{
+    off = 0;
+    for (int r = 0; r < pp.rank; ++r) off += totals[r];
+    const uint64_t N = pp.n_global;
+    const uint32_t xs = ctl->minstd_start;
+    const int shift = ctl->scan_shift;
+    O0 = pp.rank == 0 ? 0 : count_draws_le(off, N, xs, shift, jt);
+    O1 = pp.rank == pp.nranks - 1 ? N : count_draws_le(off + totals[pp.rank], N, xs, shift, jt);
+}
+
+__global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState s1, ScanParams sp, PlanParams pp,
+                                                           Ctl* __restrict__ ctl, uint64_t* __restrict__ status,
+                                                           uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
+                                                           const uint64_t* __restrict__ totals, const uint32_t* __restrict__ jt,
+                                                           uint2* __restrict__ range, uint64_t* __restrict__ first_last)
+{
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_wtot[kWaves];
+    __shared__ uint64_t s_excl;
+    if (!ctl->resample) return;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) s_tile = (uint32_t)atomicAdd((unsigned long long*)&ctl->tile_counter, 1ull);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const DevState st = ctl->base ? s1 : s0;
+    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+    const int shift = ctl->scan_shift;
+    uint64_t c[kScanItems];
+    uint64_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        if (i < sp.n) run += fx_shift(st.w[i], shift);
+        c[r] = run;
+    }
+    const uint64_t tbase = tile_scan(run, tile, status, ctl, s_wtot, &s_excl);
+    uint64_t off, O0, O1;
+    plan_bounds(pp, ctl, totals, jt, off, O0, O1);
+    const uint64_t base = off + tbase;
+    const uint64_t N = pp.n_global;
+    const uint64_t W0 = pp.gbase[pp.rank], W1 = pp.gbase[pp.rank + 1];
+    const uint32_t xs = ctl->minstd_start;
+    uint64_t lo = i0 == 0 ? O0 : count_draws_le(base, N, xs, shift, jt);
+    for (int r = 0; r < kScanItems; ++r) {
+        const uint64_t i = i0 + r;
+        if (i >= sp.n) break;
+        uint64_t hi = count_draws_le(base + c[r], N, xs, shift, jt);
+        if (i + 1 == sp.n) {
+            if (pp.rank == pp.nranks - 1 && hi < N)
+                atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
+            hi = O1;
+        }
+        const uint64_t a = lo > W0 ? lo : W0, b = hi < W1 ? hi : W1;
+        if (a < b) mark_segment(marks, tile_first, a - W0, b - W0, kMarkOwn + 1u + (uint32_t)i);
+        // every particle a foreign destination's [first, last] run can include (empty
+        // ranges too) has lo < W0 or hi > W1: record its range for k_pack
+        if (lo < W0 || hi > W1) {
+            range[i] = make_uint2((uint32_t)lo, (uint32_t)hi);
+            if (hi > lo) {
+                for (int d = 0; d < pp.nranks; ++d) {
+                    if (d == pp.rank) continue;
+                    const uint64_t Wd0 = pp.gbase[d], Wd1 = pp.gbase[d + 1];
+                    const uint64_t Sd = O0 > Wd0 ? O0 : Wd0, Ed = O1 < Wd1 ? O1 : Wd1;
+                    if (Sd >= Ed) continue;
+                    if (lo <= Sd && Sd < hi) first_last[2 * d] = i;
+                    if (lo <= Ed - 1 && Ed - 1 < hi) first_last[2 * d + 1] = i;
+                }
+            }
+        }
+        lo = hi;
+    }
+}
+
+// counts[d] = particles this rank sends to rank d != rank (0 when not resampling), their
+// clipped output ranges [S_d, E_d) and the packing offsets send_off[0..nranks]
+__global__ void k_plan_counts(const Ctl* __restrict__ ctl, PlanParams pp, const uint64_t* __restrict__ totals,
+                              const uint32_t* __restrict__ jt, const uint64_t* __restrict__ first_last,
+                              uint64_t* __restrict__ counts, uint64_t* __restrict__ sd_ed, uint64_t* __restrict__ send_off)
+{
+    if (threadIdx.x != 0) return;
+    uint64_t off, O0 = 0, O1 = 0;
+    if (ctl->resample) plan_bounds(pp, ctl, totals, jt, off, O0, O1);
+    uint64_t acc = 0;
+    send_off[0] = 0;
+    for (int d = 0; d < pp.nranks; ++d) {
+        const uint64_t W0 = pp.gbase[d], W1 = pp.gbase[d + 1];
+        const uint64_t Sd = O0 > W0 ? O0 : W0, Ed = O1 < W1 ? O1 : W1;
+        uint64_t cnt = 0;
+        if (ctl->resample && d != pp.rank && Sd < Ed) cnt = first_last[2 * d + 1] - first_last[2 * d] + 1;
+        counts[d] = cnt;
+        sd_ed[2 * d] = Sd;
+        sd_ed[2 * d + 1] = Ed;
+        acc += cnt;
+        send_off[d + 1] = acc;
+    }
+}
+
 struct alignas(8) Rec {                  // one migrating particle (72 bytes)
     double x, y, th, z, zs, w, mprob;
     uint64_t lohi;                       // [lo, hi) of the outputs it fills (global, clipped)
@@ -955,11 +1068,52 @@ struct alignas(8) Rec {                  // one migrating particle (72 bytes)
 };
 static_assert(sizeof(Rec) == 72, "record size");
 
-template <bool RECS>
+__global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
+                                                 const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
+                                                 const uint64_t* __restrict__ sd_ed, const uint64_t* __restrict__ send_off,
+                                                 Rec* __restrict__ send)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= send_off[pp.nranks]) return;
+    int d = 0;
+    while (j >= send_off[d + 1]) ++d;
+    const uint64_t i = first_last[2 * d] + (j - send_off[d]);
+    const DevState st = ctl->base ? s1 : s0;
+    const uint64_t Sd = sd_ed[2 * d], Ed = sd_ed[2 * d + 1];
+    const uint2 rg = range[i];
+    const uint64_t lo = rg.x > Sd ? rg.x : Sd, hi = rg.y < Ed ? rg.y : Ed;
+    Rec r;
+    r.x = st.x[i]; r.y = st.y[i]; r.th = st.th[i]; r.z = st.z[i]; r.zs = st.zs[i]; r.w = st.w[i]; r.mprob = st.mprob[i];
+    r.lohi = lo | (hi << 32);
+    r.src = (uint64_t)st.flags[i] | ((pp.gbase[pp.rank] + i) << 8);
+    send[j] = r;
+}
+
+// records -> marks (lower ranks: 1 + j, higher ranks: kMarkHigh + 1 + j)
+__global__ void __launch_bounds__(kBlock) k_expand(const Rec* __restrict__ recv, uint64_t nrecv, uint64_t W0,
+                                                   uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= nrecv) return;
+    const Rec& r = recv[j];
+    const uint64_t glo = r.lohi & 0xffffffffull, ghi = r.lohi >> 32;
+    if (ghi > glo) {
+        const uint32_t v = ((r.src >> 8) < W0 ? 1u : kMarkHigh + 1u) + (uint32_t)j;
+        mark_segment(marks, tile_first, glo - W0, ghi - W0, v);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_resample_gather: expand the segments (inclusive max-scan of the marks) and gather
+// the particle state into the other buffer (xi_k.swap(xi_kp), src/ParticleFilter.hpp:107).
+// Weights are carried, not reset (Q4).  MULTI: marks carry the source encoding above.
+// ---------------------------------------------------------------------------------------
+template <bool MULTI>
 __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                             uint32_t* __restrict__ marks, const uint32_t* __restrict__ tile_first,
                                                             uint64_t* __restrict__ status, uint32_t* __restrict__ anc,
-                                                            uint32_t record, uint32_t aux, const Rec* __restrict__ recs)
+                                                            uint32_t record, uint32_t aux, const Rec* __restrict__ recs,
+                                                            uint64_t gbase)
 {
     if (!ctl->resample) return;
     __shared__ uint32_t s_wmax[kWaves];
@@ -1004,13 +1158,17 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
         const uint32_t slot = (uint32_t)r * kBlock + tid;
         const uint64_t k = (uint64_t)t * kGatherTile + slot;
         if (k >= sp.n) continue;
-        const uint32_t i = s_idx[slot];
-        if (RECS) {
-            const Rec& r = recs[i];
-            out.x[k] = r.x; out.y[k] = r.y; out.th[k] = r.th; out.z[k] = r.z; out.zs[k] = r.zs; out.w[k] = r.w;
-            if (aux) { out.mprob[k] = r.mprob; out.flags[k] = (uint8_t)r.src; }
-            if (record) anc[k] = (uint32_t)(r.src >> 8);
-            continue;
+        uint32_t i = s_idx[slot];
+        if (MULTI) {
+            if (i >= kMarkOwn && i < kMarkHigh) {
+                i -= kMarkOwn;                   // own particle
+            } else {
+                const Rec& rc = recs[i >= kMarkHigh ? i - kMarkHigh : i];
+                out.x[k] = rc.x; out.y[k] = rc.y; out.th[k] = rc.th; out.z[k] = rc.z; out.zs[k] = rc.zs; out.w[k] = rc.w;
+                if (aux) { out.mprob[k] = rc.mprob; out.flags[k] = (uint8_t)rc.src; }
+                if (record) anc[k] = (uint32_t)(rc.src >> 8);
+                continue;
+            }
         }
         out.x[k] = in.x[i];
         out.y[k] = in.y[i];
@@ -1022,143 +1180,7 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
             out.mprob[k] = in.mprob[i];
             out.flags[k] = in.flags[i];
         }
-        if (record) anc[k] = i;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// multi-GPU resample: plan (global segment boundaries + per-destination send ranges),
-// pack, expand, gather.  Output k of the global filter lives on the rank whose shard
-// holds global index k; particle i of rank r fills outputs [lo_i, hi_i).
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void plan_bounds(const PlanParams& pp, const Ctl* ctl, const uint64_t* totals,
-                                            const uint32_t* jt, uint64_t& off, uint64_t& O0, uint64_t& O1)
-{
-    off = 0;
-    for (int r = 0; r < pp.rank; ++r) off += totals[r];
-    const uint64_t N = pp.n_global;
-    const uint32_t xs = ctl->minstd_start;
-    const int shift = ctl->scan_shift;
-    O0 = pp.rank == 0 ? 0 : count_draws_le(off, N, xs, shift, jt);
-    O1 = pp.rank == pp.nranks - 1 ? N : count_draws_le(off + totals[pp.rank], N, xs, shift, jt);
-}
-
-__global__ void __launch_bounds__(kBlock) k_plan(DevState s0, DevState s1, ScanParams sp, PlanParams pp, Ctl* __restrict__ ctl,
-                                                 const uint64_t* __restrict__ tile_excl, const uint64_t* __restrict__ totals,
-                                                 const uint32_t* __restrict__ jt, uint2* __restrict__ range,
-                                                 uint64_t* __restrict__ first_last)
-{
-    __shared__ uint64_t s_wtot[kWaves];
-    if (!ctl->resample) return;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t tile = blockIdx.x;
-    const DevState st = ctl->base ? s1 : s0;
-    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
-    const int shift = ctl->scan_shift;
-    uint64_t c[kScanItems];
-    uint64_t run = 0;
-#pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        const uint64_t i = i0 + r;
-        if (i < sp.n) run += fx_shift(st.w[i], shift);
-        c[r] = run;
-    }
-    uint64_t tincl = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t t = __shfl_up(tincl, o, 64);
-        if ((int)lane >= o) tincl += t;
-    }
-    if (lane == 63) s_wtot[wave] = tincl;
-    __syncthreads();
-    uint64_t wexcl = 0;
-    for (uint32_t wv = 0; wv < wave; ++wv) wexcl += s_wtot[wv];
-    uint64_t off, O0, O1;
-    plan_bounds(pp, ctl, totals, jt, off, O0, O1);
-    const uint64_t base = off + tile_excl[tile] + wexcl + (tincl - run);
-    const uint64_t N = pp.n_global;
-    const uint32_t xs = ctl->minstd_start;
-    uint64_t lo = count_draws_le(base, N, xs, shift, jt);
-    if (i0 == 0) lo = O0;
-    for (int r = 0; r < kScanItems; ++r) {
-        const uint64_t i = i0 + r;
-        if (i >= sp.n) break;
-        uint64_t hi = count_draws_le(base + c[r], N, xs, shift, jt);
-        if (i + 1 == sp.n) {
-            if (pp.rank == pp.nranks - 1 && hi < N)
-                atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
-            hi = O1;
-        }
-        range[i] = make_uint2((uint32_t)lo, (uint32_t)hi);
-        if (hi > lo) {
-            for (int d = 0; d < pp.nranks; ++d) {
-                const uint64_t W0 = pp.gbase[d], W1 = pp.gbase[d + 1];
-                const uint64_t Sd = O0 > W0 ? O0 : W0, Ed = O1 < W1 ? O1 : W1;
-                if (Sd >= Ed) continue;
-                if (lo <= Sd && Sd < hi) first_last[2 * d] = i;
-                if (lo <= Ed - 1 && Ed - 1 < hi) first_last[2 * d + 1] = i;
-            }
-        }
-        lo = hi;
-    }
-}
-
-// counts[d] = particles this rank sends to rank d (0 when not resampling), their clipped
-// output ranges [S_d, E_d) and the packing offsets send_off[0..nranks]
-__global__ void k_plan_counts(const Ctl* __restrict__ ctl, PlanParams pp, const uint64_t* __restrict__ totals,
-                              const uint32_t* __restrict__ jt, const uint64_t* __restrict__ first_last,
-                              uint64_t* __restrict__ counts, uint64_t* __restrict__ sd_ed, uint64_t* __restrict__ send_off)
-{
-    if (threadIdx.x != 0) return;
-    uint64_t off, O0 = 0, O1 = 0;
-    if (ctl->resample) plan_bounds(pp, ctl, totals, jt, off, O0, O1);
-    uint64_t acc = 0;
-    send_off[0] = 0;
-    for (int d = 0; d < pp.nranks; ++d) {
-        const uint64_t W0 = pp.gbase[d], W1 = pp.gbase[d + 1];
-        const uint64_t Sd = O0 > W0 ? O0 : W0, Ed = O1 < W1 ? O1 : W1;
-        uint64_t cnt = 0;
-        if (ctl->resample && Sd < Ed) cnt = first_last[2 * d + 1] - first_last[2 * d] + 1;
-        counts[d] = cnt;
-        sd_ed[2 * d] = Sd;
-        sd_ed[2 * d + 1] = Ed;
-        acc += cnt;
-        send_off[d + 1] = acc;
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
-                                                 const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
-                                                 const uint64_t* __restrict__ sd_ed, const uint64_t* __restrict__ send_off,
-                                                 Rec* __restrict__ send)
-{
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= send_off[pp.nranks]) return;
-    int d = 0;
-    while (j >= send_off[d + 1]) ++d;
-    const uint64_t i = first_last[2 * d] + (j - send_off[d]);
-    const DevState st = ctl->base ? s1 : s0;
-    const uint2 rg = range[i];
-    const uint64_t Sd = sd_ed[2 * d], Ed = sd_ed[2 * d + 1];
-    const uint64_t lo = rg.x > Sd ? rg.x : Sd, hi = rg.y < Ed ? rg.y : Ed;
-    Rec r;
-    r.x = st.x[i]; r.y = st.y[i]; r.th = st.th[i]; r.z = st.z[i]; r.zs = st.zs[i]; r.w = st.w[i]; r.mprob = st.mprob[i];
-    r.lohi = lo | (hi << 32);
-    r.src = (uint64_t)st.flags[i] | ((pp.gbase[pp.rank] + i) << 8);
-    send[j] = r;
-}
-
-__global__ void __launch_bounds__(kBlock) k_expand(const Rec* __restrict__ recv, uint64_t nrecv, uint64_t W0,
-                                                   uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first)
-{
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= nrecv) return;
-    const uint64_t lh = recv[j].lohi;
-    const uint64_t glo = lh & 0xffffffffull, ghi = lh >> 32;
-    if (ghi > glo) {
-        const uint64_t lo = glo - W0, hi = ghi - W0;
-        marks[lo] = (uint32_t)(j + 1);
-        for (uint64_t t = (lo + kGatherTile - 1) / kGatherTile; t * kGatherTile < hi; ++t) tile_first[t] = (uint32_t)j;
+        if (record) anc[k] = (uint32_t)(gbase + i);
     }
 }
 
@@ -1337,12 +1359,12 @@ extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipSt
 }
 
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
-                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt,
-                                                  uint64_t* tile_excl, uint64_t* total, hipStream_t stream)
+                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, uint64_t* total,
+                                                  hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
     hipLaunchKernelGGL(k_normalize_scan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, status, marks,
-                       tile_first, jt, tile_excl, total);
+                       tile_first, jt, total);
     return hipGetLastError();
 }
 
@@ -1352,17 +1374,17 @@ extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, con
 {
     if (sp->ntiles == 0) return hipSuccess;
     hipLaunchKernelGGL(k_resample_gather<false>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, marks, tile_first,
-                       status, anc, record, aux, (const Rec*)nullptr);
+                       status, anc, record, aux, (const Rec*)nullptr, (uint64_t)0);
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_plan(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
-                                        const uint64_t* tile_excl, const uint64_t* totals, const uint32_t* jt, uint2* range,
-                                        uint64_t* first_last, uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off,
-                                        hipStream_t stream)
+extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
+                                                  uint64_t* status, uint32_t* marks, uint32_t* tile_first,
+                                                  const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
+                                                  uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off, hipStream_t stream)
 {
-    if (sp->ntiles) hipLaunchKernelGGL(k_plan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl, tile_excl,
-                                       totals, jt, range, first_last);
+    if (sp->ntiles) hipLaunchKernelGGL(k_segments_multi, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl,
+                                       status, marks, tile_first, totals, jt, range, first_last);
     hipLaunchKernelGGL(k_plan_counts, dim3(1), dim3(64), 0, stream, ctl, *pp, totals, jt, first_last, counts, sd_ed, send_off);
     return hipGetLastError();
 }
@@ -1385,7 +1407,7 @@ extern "C" hipError_t eslam_launch_expand_gather(DevState s0, DevState s1, const
     if (nrecv) hipLaunchKernelGGL(k_expand, dim3((uint32_t)((nrecv + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
                                   (const Rec*)recv, nrecv, W0, marks, tile_first);
     if (sp->ntiles) hipLaunchKernelGGL(k_resample_gather<true>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl,
-                                       marks, tile_first, status, anc, record, aux, (const Rec*)recv);
+                                       marks, tile_first, status, anc, record, aux, (const Rec*)recv, W0);
     return hipGetLastError();
 }
 

@@ -56,9 +56,7 @@ def _snap(rec, key, f, with_anc):
     for fld in FIELDS:
         rec[f"{key}/{fld}"] = np.array(getattr(pa, fld))
     if with_anc:
-        a = f.ancestors()
-        if a is not None:
-            rec[f"{key}/anc"] = a
+        rec[f"{key}/anc"] = f.ancestors()
 
 
 def _info(rec, key, i):
@@ -88,8 +86,9 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     stream = S.step_stream(steps, tilt=(name == "natural"))
     for k, st in enumerate(stream):
         f.step(st)
-        _info(rec, f"s{k}", info_fn(f))
-        _snap(rec, f"s{k}", f, True)
+        info = info_fn(f)
+        _info(rec, f"s{k}", info)
+        _snap(rec, f"s{k}", f, bool(info.resampled))
     rec["best"] = np.array([f.best_index()])
     rec["rng"] = np.array([f.rng_state().minstd_x])
     return rec
