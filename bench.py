@@ -46,6 +46,27 @@ def parse():
     return ap.parse_args()
 
 
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r01", "summary.json")
+
+
+def pmc_traffic(kernel, n, map_cells):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/profile.sh -> profiles/<round>/summary.json: FETCH_SIZE x2 + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md), when they were taken on this workload."""
+    try:
+        with open(PROFILE_SUMMARY) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if d.get("particles") != n or d.get("map_cells") != map_cells:
+        return None
+    for name, e in d.get("kernels", {}).items():
+        if name.startswith(kernel) and "hbm_bytes_per_dispatch" in e:
+            return {"bytes_per_launch": round(e["hbm_bytes_per_dispatch"]), "fetch_bytes": round(e["fetch_size_bytes"]),
+                    "write_bytes": round(e["write_size_bytes"]), "source": os.path.relpath(PROFILE_SUMMARY, ROOT)}
+    return None
+
+
 def cpu_baseline(args, grid):
     """The CPU oracle (a restatement of the reference path, reference-order double sums),
     single-threaded on this host, on a bounded sample of the same workload."""
@@ -144,6 +165,7 @@ def main():
     dom = max(per_kernel, key=lambda k: per_kernel[k][0])
     dom_ms, dom_bytes = per_kernel[dom]
     achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic = pmc_traffic(dom, n, args.map_cells)
     result = {
         "metric": "M particle-updates/s (predict+weight+resample) @ 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -162,7 +184,8 @@ def main():
                    "particles_per_gpu": n, "global_particles": n * world,
                    "parallelism": "dp%d (particle shards%s)" % (world, ", sharded path" if sharded else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
                      "algorithmic_bytes_per_particle": dom_bytes,
                      "avg_launch_ms": round(dom_ms, 5)},
         "kernel_ms": {k: round(v, 5) for k, v in kt.items()},

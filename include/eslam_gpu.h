@@ -15,7 +15,7 @@
  * entry point returns ESLAM_OK (0) or a negative ESLAM_ERR_* code; eslam_gpu_last_error()
  * gives the message (the reference's std::runtime_error texts where one exists).
  *
- * One context = one GPU (one process per GPU for multi-GPU; see eslam_gpu_shard_*).  A
+ * One context = one GPU (one process per GPU for multi-GPU; see eslam_gpu_set_comm).  A
  * context is not thread-safe.  Device memory is owned by the context; host buffers passed
  * in are owned by the caller and only read/written during the call.
  */
@@ -168,7 +168,8 @@ int eslam_gpu_abi_version(void);
 /* run on a caller-provided hipStream_t (NULL = the context's own stream) */
 int eslam_gpu_set_stream(eslam_ctx* ctx, void* hip_stream);
 
-/* ---- environment (PoseEstimator::setEnvironment / GridAccess::setMap, shared map) ------ */
+/* ---- environment: PoseEstimator::setEnvironment src/PoseEstimator.cpp:47-62 and
+ * GridAccess::setMap src/PoseEstimator.hpp:68-95 (shared map, useShared = true)           */
 int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* grid);
 
 /* ---- initialisation -------------------------------------------------------------------
@@ -198,11 +199,12 @@ int eslam_gpu_update(eslam_ctx* ctx, const eslam_step_input* in);
 int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info);
 
 /* ---- ParticleFilter<T> API (src/ParticleFilter.hpp:34-173) ------------------------------ */
-int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum);
-int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective);
-int eslam_gpu_resample(eslam_ctx* ctx);                       /* resample_stratified(N)   */
-int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index);
-/* PoseEstimator::getCentroid (normalises in place, Q15): position[3] + quaternion (w,x,y,z) */
+int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum);          /* getWeightsSum :34-39     */
+int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective);  /* normalizeWeights :46-70 */
+int eslam_gpu_resample(eslam_ctx* ctx);        /* resample() -> resample_stratified(N) :72-108 */
+int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index);  /* :160-173 (Q16)  */
+/* PoseEstimator::getCentroid src/PoseEstimator.cpp:354-383 (normalises in place, Q15):
+ * position[3] + quaternion (w,x,y,z)                                                        */
 int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double orientation[4]);
 
 /* ---- resume state: RNG + the filter scalars (bit-exact resume with the particles) ------- */

@@ -57,6 +57,24 @@ def build(force=False, verbose=True, defines=(), lib=None, tag=""):
     return lib
 
 
+FACADE_SRC = os.path.join(ROOT, "tests", "cpp", "test_facade.cpp")
+FACADE_BIN = os.path.join(ROOT, "tests", "cpp", "_build", "test_facade")
+
+
+def build_facade_test(verbose=True):
+    """g++ the C++ façade test (include/eslam_gpu.hpp over the C ABI) against the library."""
+    deps = [FACADE_SRC, LIB, os.path.join(ROOT, "include", "eslam_gpu.hpp"), os.path.join(ROOT, "include", "eslam_gpu.h")]
+    if not _stale(FACADE_BIN, deps):
+        return FACADE_BIN
+    os.makedirs(os.path.dirname(FACADE_BIN), exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", f"-I{os.path.join(ROOT, 'include')}", FACADE_SRC,
+           f"-L{OUT_DIR}", "-leslam_gpu", "-Wl,-rpath,$ORIGIN/../../../slam-eslam_amd/lib", "-o", FACADE_BIN]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return FACADE_BIN
+
+
 if __name__ == "__main__":
     defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
     tag = "_" + "_".join(d.lower() for d in defs) if defs else ""

@@ -161,6 +161,12 @@ def test_particle_filter_api(gpu_mod, rough_grid):
     assert gpu.normalize() == orc.normalize()
     assert_bit_identical(gpu.download(), orc.download(), "normalize")
     assert gpu.count() == n
+    # getCentroid: the device sums in the canonical chunk order + a fixed tree; the oracle
+    # uses the reference's sequential sums -> agreement to 1e-12 relative (not bit-exact)
+    gp, gq = gpu.centroid()
+    op, oq = orc.centroid()
+    assert np.allclose(gp, op, rtol=1e-12, atol=1e-15), (gp, op)
+    assert np.allclose(gq, oq, rtol=1e-12, atol=1e-15), (gq, oq)
 
 
 def test_rng_state_resume(gpu_mod, flat_grid):

@@ -11,3 +11,4 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/t
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- python3 bench.py --no-cpu-baseline $args > $out/fetch.log 2>&1 || { echo "fetch rc=$?"; tail -20 $out/fetch.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 bench.py --no-cpu-baseline $args > $out/write.log 2>&1 || { echo "write rc=$?"; tail -20 $out/write.log; exit 1; }
 find $out -name "*.csv" | head -20
+python3 tools/prof_summary.py $out > $out/summary.json && cat $out/summary.json
