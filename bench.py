@@ -22,11 +22,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "slam-eslam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-# algorithmic bytes per particle-update (DESIGN.md "roofline")
-BYTES_PREDICT_WEIGHT = 96     # read 6 x f64 state, write 6 x f64
-BYTES_NORMALIZE = 8
-BYTES_RESAMPLE = 104          # scan read 8 + gather 48 + write 48
-BYTES_TOTAL = BYTES_PREDICT_WEIGHT + BYTES_NORMALIZE + BYTES_RESAMPLE
+# algorithmic bytes per particle-update (208 B for the whole step)
+BYTES_TOTAL = 208             # predict+weight 96, normalise 8, resample 104 (scan 8, gather 48, write 48)
+# per kernel as launched: the resample gather is fused into the next step's k_project_weight
+BYTES_K1 = 104                # gathered read 6 x f64 + write 6 x f64 + 4-byte mark read/clear
+BYTES_K3 = 28                 # phase B / normalise read+write w (16), scan re-read (8), marks (4)
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -159,9 +159,8 @@ def main():
     ms_step = dt / args.steps * 1e3
 
     # roofline of the dominant kernel (HIP events around every launch of the timed region)
-    per_kernel = {"k_project_weight": (kt["project_weight_ms"], BYTES_PREDICT_WEIGHT),
-                  "k_normalize_scan": (kt["normalize_scan_ms"], BYTES_NORMALIZE + 8),
-                  "k_resample_gather": (kt["resample_ms"], BYTES_RESAMPLE - 8)}
+    per_kernel = {"k_project_weight": (kt["project_weight_ms"], BYTES_K1),
+                  "k_normalize_scan+k_segments": (kt["normalize_scan_ms"], BYTES_K3)}
     dom = max(per_kernel, key=lambda k: per_kernel[k][0])
     dom_ms, dom_bytes = per_kernel[dom]
     achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0

@@ -21,29 +21,28 @@ using namespace eslam_dev;
 
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  hipStream_t stream);
+                                                  const GatherView* gv, hipStream_t stream);
+extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
                                                 hipStream_t stream);
 extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipStream_t stream);
-extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
-                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, uint64_t* total,
-                                                  hipStream_t stream);
+extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* tile_sum,
+                                                  uint64_t* total, hipStream_t stream);
+extern "C" hipError_t eslam_launch_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const uint64_t* tile_prefix,
+                                            uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream);
+extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, uint64_t n, uint64_t gbase, Ctl* ctl,
+                                                   const GatherView* gv, uint32_t aux, hipStream_t stream);
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
-                                                  uint64_t* status, uint32_t* marks, uint32_t* tile_first,
+                                                  const uint64_t* tile_prefix, uint32_t* marks, uint32_t* tile_first,
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
                                                   uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
                                         const uint64_t* first_last, const uint64_t* sd_ed, const uint64_t* send_off,
                                         uint64_t nsend, void* send, hipStream_t stream);
-extern "C" hipError_t eslam_launch_expand_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const void* recv,
-                                                 uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* tile_first,
-                                                 uint64_t* status, uint32_t* anc, uint32_t record, uint32_t aux,
-                                                 hipStream_t stream);
+extern "C" hipError_t eslam_launch_expand(const void* recv, uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* row_first,
+                                          hipStream_t stream);
 extern "C" uint64_t eslam_record_bytes(void);
-extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint32_t* marks,
-                                                   const uint32_t* tile_first, uint64_t* status, uint32_t* anc,
-                                                   uint32_t record, uint32_t aux, hipStream_t stream);
 extern "C" hipError_t eslam_launch_init_gaussian(DevState s0, uint64_t n, uint64_t gbase, uint64_t seed, uint64_t ev,
                                                  const double mu[3], const double sigma[3], double zpos, double zsigma,
                                                  hipStream_t stream);
@@ -200,8 +199,8 @@ struct eslam_ctx {
     DevState st[2] = {};
     void* state_mem = nullptr;
     uint32_t* marks = nullptr;
-    uint32_t* tile_first = nullptr;
-    uint64_t* status = nullptr;
+    uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
+    uint64_t* tile_sum = nullptr;           // per scan tile: fixed-point total, then exclusive prefix
     uint32_t* anc = nullptr;
     bool has_anc = false;
     // statistics and control
@@ -328,6 +327,8 @@ extern "C" void eslam_config_default(eslam_config* c)
 
 extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+static int materialize(eslam_ctx* ctx);
+
 static int read_ctl(eslam_ctx* ctx)
 {
     HIPCHK(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->stream));
@@ -400,7 +401,7 @@ static void free_particles(eslam_ctx* ctx)
     hipFree(ctx->state_mem); ctx->state_mem = nullptr;
     hipFree(ctx->marks); ctx->marks = nullptr;
     hipFree(ctx->tile_first); ctx->tile_first = nullptr;
-    hipFree(ctx->status); ctx->status = nullptr;
+    hipFree(ctx->tile_sum); ctx->tile_sum = nullptr;
     hipFree(ctx->anc); ctx->anc = nullptr;
     hipFree(ctx->range); ctx->range = nullptr;
     ctx->n = ctx->cap = 0;
@@ -462,10 +463,9 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     }
     const uint64_t ntiles = (cap + kScanTile - 1) / kScanTile;
     HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
-    HIPCHK(ctx, hipMalloc(&ctx->tile_first, ntiles * 4));
-    HIPCHK(ctx, hipMalloc(&ctx->status, ntiles * 8));
+    HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
-    HIPCHK(ctx, hipMemset(ctx->status, 0, ntiles * 8));
     if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     ctx->n = n;
     ctx->cap = cap;
@@ -635,6 +635,7 @@ static int reset_ctl_for_new_particles(eslam_ctx* ctx, int wexp)
     if (rc) return rc;
     ctx->ctl_host->base = 0;
     ctx->ctl_host->flip = 0;
+    ctx->ctl_host->gather = 0;               // a pending gather of the old set is dropped
     ctx->ctl_host->wexp = wexp;
     ctx->has_anc = false;
     return write_ctl(ctx);
@@ -727,7 +728,8 @@ extern "C" int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const esla
 extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
 {
     if (!ctx || !p) return ESLAM_ERR_INVALID_ARG;
-    int rc = read_ctl(ctx);
+    int rc = materialize(ctx);
+    if (!rc) rc = read_ctl(ctx);
     if (rc) return rc;
     const DevState& s = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip];
     const uint64_t n = ctx->n, b = n * 8;
@@ -753,6 +755,31 @@ extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
 // ---------------------------------------------------------------------------------------
 // the hot path
 // ---------------------------------------------------------------------------------------
+// the pending resample gather (consumed by the next k_project_weight or materialised)
+static GatherView gather_view(eslam_ctx* ctx)
+{
+    GatherView gv;
+    memset(&gv, 0, sizeof(gv));
+    gv.marks = ctx->marks;
+    gv.row_first = ctx->tile_first;
+    gv.anc = ctx->anc;
+    gv.recs = ctx->sharded ? (const Rec*)ctx->recvbuf : nullptr;
+    gv.record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
+    gv.multi = ctx->sharded ? 1u : 0u;
+    return gv;
+}
+
+// before the particle state is read or replaced outside the hot path: run a pending
+// gather (device decides; a no-op otherwise) and commit the buffer flip
+static int materialize(eslam_ctx* ctx)
+{
+    if (!ctx->n) return ESLAM_OK;
+    const GatherView gv = gather_view(ctx);
+    const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
+    HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], ctx->n, ctx->gbase, ctx->ctl, &gv, aux, ctx->stream));
+    return ESLAM_OK;
+}
+
 static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepParams& p)
 {
     memset(&p, 0, sizeof(p));
@@ -858,19 +885,17 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     if (mode == FIN_SUM) return ESLAM_OK;
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
     sp.multi = 1;
-    HIPCHK(ctx, hipMemsetAsync(ctx->mg + mg::kTotal, 0, 8, ctx->stream));
-    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
-                                            ctx->jump, ctx->mg + mg::kTotal, ctx->stream));
+    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->mg + mg::kTotal,
+                                            ctx->stream));
     rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
     if (rc) return rc;
     const PlanParams pp = plan_params(ctx);
-    HIPCHK(ctx, eslam_launch_segments_multi(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->status, ctx->marks,
+    HIPCHK(ctx, eslam_launch_segments_multi(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->tile_sum, ctx->marks,
                                             ctx->tile_first, ctx->mg + mg::kTotals, ctx->jump, ctx->range,
                                             ctx->mg + mg::kFirstLast, ctx->mg + mg::kCounts, ctx->mg + mg::kSdEd,
                                             ctx->mg + mg::kSendOff, ctx->stream));
     if (timed) rec(ctx, 3);
     const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
-    const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
     uint64_t nrecv = 0;
     if (G > 1) {                             // particle migration between slices
         rc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
@@ -898,9 +923,8 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
             if (rc) return rc;
         }
     }
-    // the gather runs on the device's resample decision (no-op without a resample)
-    HIPCHK(ctx, eslam_launch_expand_gather(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->recvbuf, nrecv, ctx->gbase, ctx->marks,
-                                           ctx->tile_first, ctx->status, ctx->anc, record, aux, ctx->stream));
+    // marks of the migrated particles; the gather is fused into the next k_project_weight
+    HIPCHK(ctx, eslam_launch_expand(ctx->recvbuf, nrecv, ctx->gbase, ctx->marks, ctx->tile_first, ctx->stream));
     if (timed) rec(ctx, 4);
     if (record) ctx->has_anc = true;
     return ESLAM_OK;
@@ -913,15 +937,13 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
-    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->status, ctx->marks, ctx->tile_first,
-                                            ctx->jump, nullptr, ctx->stream));
+    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, nullptr, ctx->stream));
+    HIPCHK(ctx, eslam_launch_segments(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->marks, ctx->tile_first,
+                                      ctx->jump, ctx->stream));
     if (timed) rec(ctx, 3);
-    const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
-    const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
-    HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->marks, ctx->tile_first, ctx->status,
-                                             ctx->anc, record, aux, ctx->stream));
+    // the gather itself is fused into the next k_project_weight (or materialize())
     if (timed) rec(ctx, 4);
-    if (record) ctx->has_anc = true;
+    if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ctx->has_anc = true;
     return ESLAM_OK;
 }
 
@@ -933,11 +955,14 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     fill_step_params(ctx, in, p);
     p.proj_event = ctx->proj_event;
     rec(ctx, 0);
+    const GatherView gv = gather_view(ctx);
     HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                            ctx->shards, ctx->stream));
+                                            ctx->shards, &gv, ctx->stream));
     rec(ctx, 1);
     if (project) ctx->proj_event++;
-    if (weight) return run_update_tail(ctx, FIN_UPDATE, true);
+    if (gv.record) ctx->has_anc = true;
+    if (weight) return run_update_tail(ctx, FIN_UPDATE, true);   // finalize commits the flip
+    HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
     rec(ctx, 2); rec(ctx, 3); rec(ctx, 4);
     return ESLAM_OK;
 }
@@ -1024,6 +1049,8 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
 static int standalone(eslam_ctx* ctx, uint32_t mode)
 {
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    const int rc = materialize(ctx);
+    if (rc) return rc;
     const uint32_t J = dm_chunk_rows(ctx->n_global);
     HIPCHK(ctx, eslam_launch_weight_stats(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->shards, ctx->stream));
     if (mode == FIN_SUM && !ctx->sharded) {
@@ -1066,6 +1093,7 @@ extern "C" int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index
 {
     if (!ctx || !index) return ESLAM_ERR_INVALID_ARG;
     if (!ctx->n) { *index = 0; return ESLAM_OK; }
+    if (const int rc0 = materialize(ctx)) return rc0;
     uint64_t* out = reinterpret_cast<uint64_t*>(ctx->scratch);
     HIPCHK(ctx, eslam_launch_best_index(ctx->st[0], ctx->st[1], ctx->n, ctx->ctl, out, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->scratch_host, ctx->scratch, 16, hipMemcpyDeviceToHost, ctx->stream));
@@ -1148,6 +1176,7 @@ extern "C" int eslam_gpu_get_ancestors(eslam_ctx* ctx, uint32_t* out, uint64_t n
 {
     if (!ctx || !out) return ESLAM_ERR_INVALID_ARG;
     if (!ctx->has_anc || !ctx->anc) return fail(ctx, ESLAM_ERR_INVALID_ARG, "no ancestors recorded (ESLAM_FLAG_RECORD_ANCESTORS)");
+    if (const int rc = materialize(ctx)) return rc;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipMemcpy(out, ctx->anc, (n < ctx->n ? n : ctx->n) * 4, hipMemcpyDeviceToHost));
     return ESLAM_OK;

@@ -4,7 +4,7 @@
 //   state[2]   SoA fp64 x, y, theta, zpos, zsigma, weight, mprob + uint8 flags
 //              (flags = n_contact_points | floating << 7); double-buffered for resample
 //   marks      uint32 per particle: resample segment starts (particle index + 1)
-//   tile_first uint32 per resample tile: particle covering the tile's first output
+//   row_first  uint32 per 64 outputs: source covering the row's first output
 //   status     uint64 per scan tile: decoupled look-back words (2-bit tag | 62-bit value)
 //   shards     NSHARD x Shard: exact fixed-point statistics of the weighting kernel
 //   ctl        Ctl: per-step scalars decided on the device (no host round trip per step)
@@ -21,6 +21,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kScanItems = 8;            // particles per thread in the scan kernel
 constexpr int kScanTile = kBlock * kScanItems;   // 2048 particles per scan tile
 constexpr int kGatherTile = kScanTile;           // outputs per resample-gather block
+constexpr int kRow = 64;                         // outputs per row_first entry (one wave row)
 constexpr int kNShard = 16;              // statistics shards (blockIdx % kNShard)
 constexpr int kJumpBits = 11;
 constexpr int kStatsLds = 1024;          // bytes of the statistics scratch at the LDS base
@@ -48,6 +49,8 @@ struct alignas(128) Ctl {
     uint32_t uniform;                    // sumWeights <= 0 branch
     uint32_t mode;                       // finalize mode (see FinMode)
     uint32_t special;                    // 1: S NaN, 2: S inf
+    uint32_t gather;                     // a resample gather is pending (marks -> state[base^1])
+    uint32_t pad0;
     int32_t scan_shift;                  // fixed-point shift of the resample cumulative sum
     int32_t wexp;                        // weight exponent bound for the next weighting
     double S, Q, eff, fw, max_weight;
@@ -110,6 +113,28 @@ struct StepParams {
     uint32_t use_window;                 // stage the MLS window under the cloud in LDS
     double win_margin;                   // world-frame margin around the last bounding box
     ContactC c[ESLAM_MAX_CONTACTS];
+};
+
+// one particle migrating between GPUs at a multi-GPU resample (72 bytes)
+struct alignas(8) Rec {
+    double x, y, th, z, zs, w, mprob;
+    uint64_t lohi;                       // [lo, hi) of the outputs it fills (global, clipped)
+    uint64_t src;                        // flags | global source index << 8
+};
+static_assert(sizeof(Rec) == 72, "record size");
+
+// multi-GPU mark encoding (monotone in output order): records from lower ranks,
+// then this rank's own particles, then records from higher ranks
+constexpr uint32_t kMarkOwn = 1u << 30, kMarkHigh = 1u << 31;
+
+// a pending resample gather, consumed by the next k_project_weight (or k_resample_gather)
+struct GatherView {
+    uint32_t* marks;
+    const uint32_t* row_first;
+    uint32_t* anc;                       // ancestors (global indices) when record
+    const Rec* recs;                     // multi-GPU: migrated particles
+    uint32_t record;
+    uint32_t multi;                      // marks use the multi-GPU source encoding
 };
 
 struct FinParams {

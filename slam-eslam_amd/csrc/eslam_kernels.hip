@@ -356,15 +356,40 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
 // k_project_weight: PoseEstimator::project and/or updateWeights phase A, one particle per
 // lane, one canonical chunk (64 lanes x J rows) per wave.
 // ---------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+// source of a pending-gather output: expand the segment marks (inclusive max-scan) and
+// decode.  Returns the local particle index, or sets *rec for a migrated particle.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, const Rec* __restrict__ recs, const Rec** rec)
+{
+    *rec = nullptr;
+    if (multi) {
+        if (v >= kMarkOwn && v < kMarkHigh) return v - kMarkOwn;
+        *rec = recs + (v >= kMarkHigh ? v - kMarkHigh : v);
+        return 0;
+    }
+    return v;
+}
+
+#ifdef ESLAM_K1_WAVES
+#define K1_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ESLAM_K1_WAVES, ESLAM_K1_WAVES)))
+#else
+#define K1_OCCUPANCY
+#endif
+
 template <bool PROJECT, bool WEIGHT, int MAXP>
-__global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState s1, MapView map, StepParams p,
-                                                           Ctl* __restrict__ ctl, Shard* __restrict__ shards)
+__global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState s0, DevState s1, MapView map, StepParams p,
+                                                           Ctl* __restrict__ ctl, Shard* __restrict__ shards, GatherView gv)
 {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
     const uint64_t lbase = chunk * 64ull * p.J;
+    // a pending resample gather is fused here: read the ancestors from state[base],
+    // write the updated particles to state[base ^ 1] (the latest buffer)
+    const uint32_t gath = ctl->gather;
     const uint32_t cur = ctl->base ^ ctl->flip;
     const DevState st = cur ? s1 : s0;
+    const DevState si = gath ? (ctl->base ? s1 : s0) : st;
     const int wexp = ctl->wexp;
 
     double spread = 0.0;
@@ -390,9 +415,35 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
     uint64_t bb[4] = {0, 0, 0, 0};      // ~key(min x), key(max x), ~key(min y), key(max y)
 
     for (uint32_t j = 0; j < p.J; ++j) {
-        const uint64_t i = lbase + 64ull * j + lane;
+        const uint64_t row0 = lbase + 64ull * j;
+        if (row0 >= p.n) break;
+        const uint64_t i = row0 + lane;
+        uint32_t src = (uint32_t)i;
+        const Rec* rc = nullptr;
+        if (gath) {
+            // expand the segment marks of this row: inclusive max-scan + the row carry
+            uint32_t m = 0;
+            if (i < p.n) { m = gv.marks[i]; if (m) gv.marks[i] = 0; }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(m, o, 64);
+                if ((int)lane >= o) m = m > t ? m : t;
+            }
+            const uint32_t carry = gv.row_first[row0 / kRow] + 1u;
+            m = m > carry ? m : carry;
+            src = decode_source(m - 1u, gv.multi, gv.recs, &rc);
+        }
         if (i >= p.n) continue;
-        double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i], w = st.w[i];
+        double x, y, th, z, zs, w, mp_in = 0.0;
+        uint32_t fl_in = 0;
+        if (rc) {
+            x = rc->x; y = rc->y; th = rc->th; z = rc->z; zs = rc->zs; w = rc->w;
+            mp_in = rc->mprob; fl_in = (uint8_t)rc->src;
+        } else {
+            x = si.x[src]; y = si.y[src]; th = si.th[src]; z = si.z[src]; zs = si.zs[src]; w = si.w[src];
+            if (!WEIGHT && gath) { mp_in = si.mprob[src]; fl_in = si.flags[src]; }
+        }
+        if (gath && gv.record) gv.anc[i] = rc ? (uint32_t)(rc->src >> 8) : (uint32_t)(p.gbase + src);
         const double w_in = w;
         if (PROJECT) {
             const uint64_t gi = p.gbase + i;
@@ -483,10 +534,19 @@ __global__ void __launch_bounds__(kBlock) k_project_weight(DevState s0, DevState
             st.mprob[i] = mprob;
             st.flags[i] = (uint8_t)((r.ncp & 0x7fu) | (floating << 7));
         }
+        if (!PROJECT && gath) {
+            st.x[i] = x;
+            st.y[i] = y;
+            st.th[i] = th;
+        }
+        if (!WEIGHT && gath) {
+            st.mprob[i] = mp_in;
+            st.flags[i] = (uint8_t)fl_in;
+        }
         if (PROJECT || WEIGHT) {
             st.z[i] = z;
             st.zs[i] = zs;
-            if (w != w_in || w != w) st.w[i] = w;
+            if (gath || w != w_in || w != w) st.w[i] = w;
         }
         if (x == x && y == y) {
             const uint64_t kx = order_key(x), ky = order_key(y);
@@ -696,6 +756,7 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
     // commit the previous resample's buffer flip
     ctl->base ^= ctl->flip;
     ctl->flip = 0;
+    ctl->gather = 0;
     ctl->err |= err;
     ctl->tile_counter = 0;
     ctl->overruns = 0;
@@ -756,6 +817,7 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
         ctl->minstd_start = ctl->minstd;
         ctl->minstd = dm_mulmod31(dm_minstd_pow(fp.n_global), ctl->minstd);
         ctl->flip = 1;
+        ctl->gather = 1;
     }
 }
 
@@ -785,21 +847,44 @@ __device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint3
     return cnt;
 }
 
+// Walks the stratified draws in order: k = number of draws <= the last target, x = minstd
+// state of draw k.  Consecutive targets of one thread are close, so stepping draw by draw
+// replaces a jump-ahead per particle; far targets (heavy particles) jump.
+struct DrawCursor {
+    uint64_t k, N;
+    uint32_t x, xs;
+    int shift;
+    double dN;
+    const uint32_t* jt;
+
+    __device__ __forceinline__ void seek(uint64_t c)
+    {
+        k = count_draws_le(c, N, xs, shift, jt);
+        x = k < N ? dm_mulmod31(jump_pow(jt, k + 1), xs) : 0u;
+    }
+    // number of draws <= c (c >= the previous target): step, or jump after 16 steps
+    __device__ __forceinline__ uint64_t advance(uint64_t c)
+    {
+        for (int steps = 0; k < N; ++steps) {
+            if (steps == 16) { seek(c); break; }
+            const uint64_t T = fx_shift(((double)k + dm_minstd_uniform(x)) / dN, shift);
+            if (T > c) break;
+            ++k;
+            x = dm_minstd_next(x);
+        }
+        return k;
+    }
+};
+
 // ---------------------------------------------------------------------------------------
 // k_normalize_scan: phase B + normalisation, then (when resampling) the decoupled
 // look-back prefix sum of the fixed-point weights and the segment boundaries.
 // ---------------------------------------------------------------------------------------
-constexpr uint64_t kTagAgg = 1ull << 62, kTagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
 
-// multi-GPU mark encoding (monotone in output order): records from lower ranks,
-// then this rank's own particles, then records from higher ranks
-constexpr uint32_t kMarkOwn = 1u << 30, kMarkHigh = 1u << 31;
 
-// Inclusive scan of one 2048-particle tile (thread -> wave -> block) chained to the
-// previous tiles by the decoupled look-back.  In: run = this thread's total.  Returns the
-// exclusive prefix of the thread's first item (tile prefix + in-tile prefix).
-__device__ __forceinline__ uint64_t tile_scan(uint64_t run, uint32_t tile, uint64_t* __restrict__ status,
-                                              Ctl* __restrict__ ctl, uint64_t* s_wtot, uint64_t* s_excl)
+// In-tile exclusive prefix of this thread's first item (thread -> wave -> block).
+// run = this thread's total; s_wtot: kWaves words of LDS.
+__device__ __forceinline__ uint64_t block_excl(uint64_t run, uint64_t* s_wtot)
 {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint64_t tincl = run;
@@ -810,57 +895,11 @@ __device__ __forceinline__ uint64_t tile_scan(uint64_t run, uint32_t tile, uint6
     }
     if (lane == 63) s_wtot[wave] = tincl;
     __syncthreads();
-    uint64_t wexcl = 0, agg = 0;
+    uint64_t wexcl = 0;
 #pragma unroll
-    for (int wv = 0; wv < kWaves; ++wv) {
+    for (int wv = 0; wv < kWaves; ++wv)
         if ((uint32_t)wv < wave) wexcl += s_wtot[wv];
-        agg += s_wtot[wv];
-    }
-    const uint64_t texcl = wexcl + (tincl - run);
-
-    // decoupled look-back (wave 0): 8-byte {tag, value} granules, relaxed agent scope
-    if (wave == 0) {
-        uint64_t excl = 0;
-        if (tile == 0) {
-            if (lane == 0) atomic_store_agent(&status[0], kTagInc | agg);
-        } else {
-            if (lane == 0) atomic_store_agent(&status[tile], kTagAgg | agg);
-            int64_t pred = (int64_t)tile - 1;
-            uint32_t spins = 0;
-            bool timeout = false;
-            while (true) {
-                const int64_t idx = pred - (int64_t)lane;
-                uint64_t v = kTagInc;   // before tile 0: an inclusive zero
-                if (idx >= 0) {
-                    v = atomic_load_agent(&status[idx]);
-                    while ((v >> 62) == 0) {
-                        __builtin_amdgcn_s_sleep(1);
-                        v = atomic_load_agent(&status[idx]);
-                        if (++spins > (1u << 22)) { timeout = true; v = kTagInc; break; }
-                    }
-                }
-                const uint64_t incl_mask = __ballot((v >> 62) == 2);
-                uint64_t val = v & kValMask;
-                if (incl_mask) {
-                    const int first = __builtin_ctzll(incl_mask);
-                    if ((int)lane > first) val = 0;
-                    uint64_t tot = val;
-                    for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
-                    excl += tot;
-                    break;
-                }
-                uint64_t tot = val;
-                for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
-                excl += tot;
-                pred -= 64;
-            }
-            if (__ballot(timeout) != 0ull && lane == 0) atomicOr((unsigned long long*)&ctl->err, 2ull);
-            if (lane == 0) atomic_store_agent(&status[tile], kTagInc | ((excl + agg) & kValMask));
-        }
-        if (lane == 0) *s_excl = excl;
-    }
-    __syncthreads();
-    return *s_excl + texcl;
+    return wexcl + (tincl - run);
 }
 
 // mark the segment [lo, hi) (outputs relative to this rank's slice) with value v
@@ -868,44 +907,91 @@ __device__ __forceinline__ void mark_segment(uint32_t* __restrict__ marks, uint3
                                              uint64_t lo, uint64_t hi, uint32_t v)
 {
     marks[lo] = v;
-    for (uint64_t t = (lo + kGatherTile - 1) / kGatherTile; t * kGatherTile < hi; ++t) tile_first[t] = v - 1u;
+    for (uint64_t t = (lo + kRow - 1) / kRow; t * kRow < hi; ++t) tile_first[t] = v - 1u;
 }
 
-__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
-                                                           uint64_t* __restrict__ status, uint32_t* __restrict__ marks,
-                                                           uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt,
-                                                           uint64_t* __restrict__ total)
+// LDS staging of one scan tile: values in particle order, skewed by one slot every 32
+// doubles so both the striped writes and the blocked (8 per thread) reads are conflict-free
+constexpr int kSkew = 32;
+constexpr int kStageV = kScanTile + kScanTile / kSkew;
+constexpr int kMarkStage = 2 * kScanTile;       // outputs of one tile staged in LDS (16 KB)
+
+__device__ __forceinline__ int skew(int k) { return k + k / kSkew; }
+
+// this thread's 8 consecutive values (blocked) -> fixed-point inclusive running sums
+__device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uint64_t (&c)[kScanItems])
 {
-    __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_wtot[kWaves];
-    __shared__ uint64_t s_excl;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const bool resample = ctl->resample != 0;
-    uint32_t tile = blockIdx.x;
-    if (resample && !sp.multi) {
-        if (tid == 0) s_tile = (uint32_t)atomicAdd((unsigned long long*)&ctl->tile_counter, 1ull);
-        __syncthreads();
-        tile = s_tile;
+    uint64_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        run += fx_shift(s_v[skew((int)threadIdx.x * kScanItems + r)], shift);
+        c[r] = run;
     }
+    return run;
+}
+
+struct TileMarks {                       // LDS scratch of the mark flush
+    uint32_t m[kMarkStage];
+    uint64_t L, H;
+};
+
+// Write the marks of the tile's outputs [L, H) (relative to the slice).  The tile owns
+// that range exclusively, so when it fits in LDS it is written densely and coalesced
+// (zeros included); otherwise each segment start is stored directly.  seg_lo/seg_hi:
+// this thread's segments (relative; empty when equal), val: their mark values.
+__device__ __forceinline__ void flush_marks(TileMarks& tm, uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
+                                            const uint64_t (&seg_lo)[kScanItems], const uint64_t (&seg_hi)[kScanItems],
+                                            const uint32_t (&val)[kScanItems])
+{
+    const uint32_t tid = threadIdx.x;
+    const uint64_t L = tm.L, H = tm.H;
+    const bool staged = H - L <= (uint64_t)kMarkStage;
+    if (staged) {
+        for (uint64_t k = tid; k < H - L; k += kBlock) tm.m[k] = 0u;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < kScanItems; ++q) {
+        const uint64_t lo = seg_lo[q], hi = seg_hi[q];
+        if (hi <= lo) continue;
+        if (staged) tm.m[lo - L] = val[q];
+        else marks[lo] = val[q];
+        for (uint64_t t = (lo + kRow - 1) / kRow; t * kRow < hi; ++t) tile_first[t] = val[q] - 1u;
+    }
+    if (staged) {
+        __syncthreads();
+        for (uint64_t k = tid; k < H - L; k += kBlock) marks[L + k] = tm.m[k];
+    }
+}
+
+// K3a: phase B + normalisation (striped, coalesced) and, when resampling, the tile's exact
+// fixed-point weight total.  K3b sums the totals of the tiles before its own (exact
+// integers, any order): no cross-tile waiting inside a kernel.
+__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+                                                           uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total)
+{
+    __shared__ uint64_t s_wtot[kWaves];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const bool resample = ctl->resample != 0;
+    const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
-    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+    const uint64_t t0 = (uint64_t)tile * kScanTile;
     const double S = ctl->S;
     const bool uniform = ctl->uniform != 0;
     const double inv_n = ctl->inv_n;
+    const int shift = ctl->scan_shift;
     double f[DM_NBUCKETS];
 #pragma unroll
     for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
 
-    double w[kScanItems];
+    uint64_t fx_sum = 0;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const uint64_t i = i0 + r;
-        w[r] = 0.0;
+        const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
         if (i < sp.n) {
             double v = st.w[i];
             if (sp.phase_b) {
-                const uint32_t fl = st.flags[i];
-                const uint32_t ncp = fl & 0x7fu;
+                const uint32_t ncp = st.flags[i] & 0x7fu;
                 const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
                 double fb = f[0];
 #pragma unroll
@@ -915,46 +1001,99 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
             }
             if (sp.normalize) v = uniform ? inv_n : v / S;
             if (sp.phase_b || sp.normalize) st.w[i] = v;
-            w[r] = v;
+            fx_sum += fx_shift(v, shift);
         }
     }
     if (!resample) return;
 
-    const int shift = ctl->scan_shift;
-    uint64_t c[kScanItems];
-    uint64_t run = 0;
+    for (int o = 32; o >= 1; o >>= 1) fx_sum += __shfl_xor(fx_sum, o, 64);
+    if (lane == 0) s_wtot[wave] = fx_sum;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t t = 0;
+        for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
+        tile_sum[tile] = t;
+    }
+}
+
+// sum of the first `count` tile totals (one block, coalesced, any order: exact integers)
+__device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ tile_sum, uint32_t count, uint64_t* s_wtot)
+{
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint64_t acc = 0;
+    for (uint32_t k = tid; k < count; k += kBlock) acc += tile_sum[k];
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) s_wtot[wave] = acc;
+    __syncthreads();
+    uint64_t t = 0;
+#pragma unroll
+    for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
+    __syncthreads();                     // s_wtot is reused by the caller
+    return t;
+}
+
+// multi-GPU: this slice's fixed-point total (the value all-gathered between K3a and K3b)
+__global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
+                                                        uint32_t ntiles, uint64_t* __restrict__ total)
+{
+    __shared__ uint64_t s_wtot[kWaves];
+    if (!ctl->resample) return;
+    const uint64_t t = tiles_before(tile_sum, ntiles, s_wtot);
+    if (threadIdx.x == 0) *total = t;
+}
+
+// K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
+__global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+                                                     const uint64_t* __restrict__ tile_sum, uint32_t* __restrict__ marks,
+                                                     uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt)
+{
+    __shared__ uint64_t s_wtot[kWaves];
+    __shared__ double s_v[kStageV];
+    __shared__ TileMarks s_tm;
+    if (!ctl->resample) return;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const DevState st = ctl->base ? s1 : s0;
+    const uint64_t t0 = (uint64_t)tile * kScanTile;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        run += fx_shift(w[r], shift);
-        c[r] = run;
+        const int k = r * kBlock + (int)tid;
+        const uint64_t i = t0 + (uint64_t)k;
+        s_v[skew(k)] = i < sp.n ? st.w[i] : 0.0;
     }
-    if (sp.multi) {
-        // multi-GPU: only this rank's fixed-point total (exact, any order); the segments
-        // need every rank's total (k_segments_multi)
-        uint64_t t = run;
-        for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
-        if (lane == 0 && t) atomicAdd((unsigned long long*)total, (unsigned long long)t);
-        return;
-    }
-    const uint64_t base = tile_scan(run, tile, status, ctl, s_wtot, &s_excl);
+    __syncthreads();
+    const int shift = ctl->scan_shift;
+    uint64_t c[kScanItems];
+    const uint64_t run = blocked_fx(s_v, shift, c);
+    const uint64_t base = tiles_before(tile_sum, tile, s_wtot) + block_excl(run, s_wtot);
 
-    // ---- segment boundaries: particle i covers draws [lo_i, hi_i) ----
     const uint64_t N = sp.n_global;
-    const uint32_t xs = ctl->minstd_start;
-    uint64_t lo = count_draws_le(base, N, xs, shift, jt);
-    if (i0 == 0) lo = 0;
+    const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
+    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt};
+    cur.seek(base);
+    uint64_t lo = i0 == 0 ? 0 : cur.k;
+    if (tid == 0) s_tm.L = lo;
+    uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
+    uint32_t val[kScanItems];
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const uint64_t i = i0 + r;
-        if (i >= sp.n) break;
-        uint64_t hi = count_draws_le(base + c[r], N, xs, shift, jt);
-        if (i == N - 1) {
-            if (hi < N) atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
-            hi = N;
+        seg_lo[r] = seg_hi[r] = 0;
+        val[r] = (uint32_t)(i + 1);
+        if (i < sp.n) {
+            uint64_t hi = cur.advance(base + c[r]);
+            if (i == N - 1) {
+                if (hi < N) atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
+                hi = N;
+            }
+            seg_lo[r] = lo;
+            seg_hi[r] = hi;
+            if (i + 1 == sp.n || (r == kScanItems - 1 && tid == kBlock - 1)) s_tm.H = hi;
+            lo = hi;
         }
-        if (hi > lo) mark_segment(marks, tile_first, lo, hi, (uint32_t)(i + 1));
-        lo = hi;
     }
+    __syncthreads();
+    flush_marks(s_tm, marks, tile_first, seg_lo, seg_hi, val);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -975,49 +1114,58 @@ __device__ __forceinline__ void plan_bounds(const PlanParams& pp, const Ctl* ctl
 }
 
 __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState s1, ScanParams sp, PlanParams pp,
-                                                           Ctl* __restrict__ ctl, uint64_t* __restrict__ status,
+                                                           Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
                                                            uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
                                                            const uint64_t* __restrict__ totals, const uint32_t* __restrict__ jt,
                                                            uint2* __restrict__ range, uint64_t* __restrict__ first_last)
 {
-    __shared__ uint32_t s_tile;
     __shared__ uint64_t s_wtot[kWaves];
-    __shared__ uint64_t s_excl;
+    __shared__ double s_v[kStageV];
+    __shared__ TileMarks s_tm;
     if (!ctl->resample) return;
     const uint32_t tid = threadIdx.x;
-    if (tid == 0) s_tile = (uint32_t)atomicAdd((unsigned long long*)&ctl->tile_counter, 1ull);
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
-    const uint64_t i0 = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
-    const int shift = ctl->scan_shift;
-    uint64_t c[kScanItems];
-    uint64_t run = 0;
+    const uint64_t t0 = (uint64_t)tile * kScanTile;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const uint64_t i = i0 + r;
-        if (i < sp.n) run += fx_shift(st.w[i], shift);
-        c[r] = run;
+        const int k = r * kBlock + (int)tid;
+        const uint64_t i = t0 + (uint64_t)k;
+        s_v[skew(k)] = i < sp.n ? st.w[i] : 0.0;
     }
-    const uint64_t tbase = tile_scan(run, tile, status, ctl, s_wtot, &s_excl);
+    __syncthreads();
+    const int shift = ctl->scan_shift;
+    uint64_t c[kScanItems];
+    const uint64_t run = blocked_fx(s_v, shift, c);
+    const uint64_t tbase = tiles_before(tile_sum, tile, s_wtot) + block_excl(run, s_wtot);
     uint64_t off, O0, O1;
     plan_bounds(pp, ctl, totals, jt, off, O0, O1);
     const uint64_t base = off + tbase;
     const uint64_t N = pp.n_global;
     const uint64_t W0 = pp.gbase[pp.rank], W1 = pp.gbase[pp.rank + 1];
-    const uint32_t xs = ctl->minstd_start;
-    uint64_t lo = i0 == 0 ? O0 : count_draws_le(base, N, xs, shift, jt);
+    const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
+    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt};
+    cur.seek(base);
+    uint64_t lo = i0 == 0 ? O0 : cur.k;
+    // the tile's own-slice outputs: [clip(lo_first), clip(hi_last)) relative to W0
+    auto clip = [&](uint64_t v) { return (v < W0 ? W0 : (v > W1 ? W1 : v)) - W0; };
+    if (tid == 0) s_tm.L = clip(lo);
+    uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
+    uint32_t val[kScanItems];
+#pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const uint64_t i = i0 + r;
-        if (i >= sp.n) break;
-        uint64_t hi = count_draws_le(base + c[r], N, xs, shift, jt);
+        seg_lo[r] = seg_hi[r] = 0;
+        val[r] = kMarkOwn + 1u + (uint32_t)i;
+        if (i >= sp.n) continue;
+        uint64_t hi = cur.advance(base + c[r]);
         if (i + 1 == sp.n) {
             if (pp.rank == pp.nranks - 1 && hi < N)
                 atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
             hi = O1;
         }
         const uint64_t a = lo > W0 ? lo : W0, b = hi < W1 ? hi : W1;
-        if (a < b) mark_segment(marks, tile_first, a - W0, b - W0, kMarkOwn + 1u + (uint32_t)i);
+        if (a < b) { seg_lo[r] = a - W0; seg_hi[r] = b - W0; }
         // every particle a foreign destination's [first, last] run can include (empty
         // ranges too) has lo < W0 or hi > W1: record its range for k_pack
         if (lo < W0 || hi > W1) {
@@ -1033,8 +1181,11 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
                 }
             }
         }
+        if (i + 1 == sp.n || (r == kScanItems - 1 && tid == kBlock - 1)) s_tm.H = clip(hi);
         lo = hi;
     }
+    __syncthreads();
+    flush_marks(s_tm, marks, tile_first, seg_lo, seg_hi, val);
 }
 
 // counts[d] = particles this rank sends to rank d != rank (0 when not resampling), their
@@ -1061,12 +1212,6 @@ __global__ void k_plan_counts(const Ctl* __restrict__ ctl, PlanParams pp, const 
     }
 }
 
-struct alignas(8) Rec {                  // one migrating particle (72 bytes)
-    double x, y, th, z, zs, w, mprob;
-    uint64_t lohi;                       // [lo, hi) of the outputs it fills (global, clipped)
-    uint64_t src;                        // flags | global source index << 8
-};
-static_assert(sizeof(Rec) == 72, "record size");
 
 __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
                                                  const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
@@ -1104,23 +1249,18 @@ __global__ void __launch_bounds__(kBlock) k_expand(const Rec* __restrict__ recv,
 }
 
 // ---------------------------------------------------------------------------------------
-// k_resample_gather: expand the segments (inclusive max-scan of the marks) and gather
-// the particle state into the other buffer (xi_k.swap(xi_kp), src/ParticleFilter.hpp:107).
-// Weights are carried, not reset (Q4).  MULTI: marks carry the source encoding above.
+// k_resample_gather: materialise a pending resample gather (xi_k.swap(xi_kp),
+// src/ParticleFilter.hpp:107) before the state is read by anything but the next
+// k_project_weight, which gathers on the fly.  Weights are carried, not reset (Q4).
 // ---------------------------------------------------------------------------------------
-template <bool MULTI>
-__global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
-                                                            uint32_t* __restrict__ marks, const uint32_t* __restrict__ tile_first,
-                                                            uint64_t* __restrict__ status, uint32_t* __restrict__ anc,
-                                                            uint32_t record, uint32_t aux, const Rec* __restrict__ recs,
-                                                            uint64_t gbase)
+__global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevState s1, uint64_t n, uint64_t gbase,
+                                                            Ctl* __restrict__ ctl, GatherView gv, uint32_t aux)
 {
-    if (!ctl->resample) return;
+    if (!ctl->gather) return;
     __shared__ uint32_t s_wmax[kWaves];
     __shared__ uint32_t s_idx[kGatherTile];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t t = blockIdx.x;
-    if (tid == 0 && t < sp.ntiles) status[t] = 0;       // reset the look-back words for next time
     const DevState in = ctl->base ? s1 : s0;
     const DevState out = ctl->base ? s0 : s1;
     const uint64_t k0 = (uint64_t)t * kGatherTile + (uint64_t)tid * kScanItems;
@@ -1130,7 +1270,7 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
     for (int r = 0; r < kScanItems; ++r) {
         const uint64_t k = k0 + r;
         uint32_t v = 0;
-        if (k < sp.n) { v = marks[k]; if (v) marks[k] = 0; }
+        if (k < n) { v = gv.marks[k]; if (v) gv.marks[k] = 0; }
         run = run > v ? run : v;
         mk[r] = run;
     }
@@ -1142,7 +1282,7 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
     }
     if (lane == 63) s_wmax[wave] = tincl;
     __syncthreads();
-    uint32_t carry = tile_first[t] + 1u;
+    uint32_t carry = gv.row_first[(uint64_t)t * (kGatherTile / kRow)] + 1u;
     for (uint32_t wv = 0; wv < wave; ++wv) carry = carry > s_wmax[wv] ? carry : s_wmax[wv];
     uint32_t texcl = __shfl_up(tincl, 1, 64);
     if (lane == 0) texcl = 0;
@@ -1157,18 +1297,14 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
     for (int r = 0; r < kScanItems; ++r) {
         const uint32_t slot = (uint32_t)r * kBlock + tid;
         const uint64_t k = (uint64_t)t * kGatherTile + slot;
-        if (k >= sp.n) continue;
-        uint32_t i = s_idx[slot];
-        if (MULTI) {
-            if (i >= kMarkOwn && i < kMarkHigh) {
-                i -= kMarkOwn;                   // own particle
-            } else {
-                const Rec& rc = recs[i >= kMarkHigh ? i - kMarkHigh : i];
-                out.x[k] = rc.x; out.y[k] = rc.y; out.th[k] = rc.th; out.z[k] = rc.z; out.zs[k] = rc.zs; out.w[k] = rc.w;
-                if (aux) { out.mprob[k] = rc.mprob; out.flags[k] = (uint8_t)rc.src; }
-                if (record) anc[k] = (uint32_t)(rc.src >> 8);
-                continue;
-            }
+        if (k >= n) continue;
+        const Rec* rc;
+        const uint32_t i = decode_source(s_idx[slot], gv.multi, gv.recs, &rc);
+        if (rc) {
+            out.x[k] = rc->x; out.y[k] = rc->y; out.th[k] = rc->th; out.z[k] = rc->z; out.zs[k] = rc->zs; out.w[k] = rc->w;
+            if (aux) { out.mprob[k] = rc->mprob; out.flags[k] = (uint8_t)rc->src; }
+            if (gv.record) gv.anc[k] = (uint32_t)(rc->src >> 8);
+            continue;
         }
         out.x[k] = in.x[i];
         out.y[k] = in.y[i];
@@ -1180,7 +1316,18 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
             out.mprob[k] = in.mprob[i];
             out.flags[k] = in.flags[i];
         }
-        if (record) anc[k] = (uint32_t)(gbase + i);
+        if (gv.record) gv.anc[k] = (uint32_t)(gbase + i);
+    }
+}
+
+// commit a consumed gather / flip outside an update (after a project-only step or a
+// materialising gather): the latest state becomes state[base]
+__global__ void k_commit(Ctl* __restrict__ ctl)
+{
+    if (threadIdx.x == 0) {
+        ctl->base ^= ctl->flip;
+        ctl->flip = 0;
+        ctl->gather = 0;
     }
 }
 
@@ -1312,7 +1459,7 @@ using namespace eslam_dev;
 
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  hipStream_t stream)
+                                                  const GatherView* gv, hipStream_t stream)
 {
     const uint64_t csz = 64ull * p->J;
     const uint64_t chunks = (p->n + csz - 1) / csz;
@@ -1320,7 +1467,7 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     if (blocks == 0) return hipSuccess;
     dim3 g(blocks), b(kBlock);
     const size_t lds = kStatsLds + (weight ? kWindowLds : 0);
-#define ESLAM_LAUNCH(P, W, M) hipLaunchKernelGGL((k_project_weight<P, W, M>), g, b, lds, stream, s0, s1, *map, *p, ctl, shards)
+#define ESLAM_LAUNCH(P, W, M) hipLaunchKernelGGL((k_project_weight<P, W, M>), g, b, lds, stream, s0, s1, *map, *p, ctl, shards, *gv)
     if (project && !weight) ESLAM_LAUNCH(true, false, 4);
     else if (!project && weight) {
         if (maxp <= 4) ESLAM_LAUNCH(false, true, 4);
@@ -1358,33 +1505,46 @@ extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipSt
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* status,
-                                                  uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, uint64_t* total,
-                                                  hipStream_t stream)
+extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* tile_sum,
+                                                  uint64_t* total, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_normalize_scan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, status, marks,
-                       tile_first, jt, total);
+    hipLaunchKernelGGL(k_normalize_scan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total);
+    if (total) hipLaunchKernelGGL(k_slice_total, dim3(1), dim3(kBlock), 0, stream, ctl, tile_sum, sp->ntiles, total);
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint32_t* marks,
-                                                   const uint32_t* tile_first, uint64_t* status, uint32_t* anc,
-                                                   uint32_t record, uint32_t aux, hipStream_t stream)
+extern "C" hipError_t eslam_launch_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const uint64_t* tile_prefix,
+                                            uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_resample_gather<false>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, marks, tile_first,
-                       status, anc, record, aux, (const Rec*)nullptr, (uint64_t)0);
+    hipLaunchKernelGGL(k_segments, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_prefix, marks, tile_first,
+                       jt);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, uint64_t n, uint64_t gbase, Ctl* ctl,
+                                                   const GatherView* gv, uint32_t aux, hipStream_t stream)
+{
+    const uint32_t tiles = (uint32_t)((n + kGatherTile - 1) / kGatherTile);
+    if (tiles) hipLaunchKernelGGL(k_resample_gather, dim3(tiles), dim3(kBlock), 0, stream, s0, s1, n, gbase, ctl, *gv, aux);
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, stream, ctl);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, stream, ctl);
     return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
-                                                  uint64_t* status, uint32_t* marks, uint32_t* tile_first,
+                                                  const uint64_t* tile_prefix, uint32_t* marks, uint32_t* tile_first,
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
                                                   uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off, hipStream_t stream)
 {
     if (sp->ntiles) hipLaunchKernelGGL(k_segments_multi, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl,
-                                       status, marks, tile_first, totals, jt, range, first_last);
+                                       tile_prefix, marks, tile_first, totals, jt, range, first_last);
     hipLaunchKernelGGL(k_plan_counts, dim3(1), dim3(64), 0, stream, ctl, *pp, totals, jt, first_last, counts, sd_ed, send_off);
     return hipGetLastError();
 }
@@ -1399,15 +1559,11 @@ extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, cons
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_expand_gather(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const void* recv,
-                                                 uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* tile_first,
-                                                 uint64_t* status, uint32_t* anc, uint32_t record, uint32_t aux,
-                                                 hipStream_t stream)
+extern "C" hipError_t eslam_launch_expand(const void* recv, uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* row_first,
+                                          hipStream_t stream)
 {
     if (nrecv) hipLaunchKernelGGL(k_expand, dim3((uint32_t)((nrecv + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                                  (const Rec*)recv, nrecv, W0, marks, tile_first);
-    if (sp->ntiles) hipLaunchKernelGGL(k_resample_gather<true>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl,
-                                       marks, tile_first, status, anc, record, aux, (const Rec*)recv, W0);
+                                  (const Rec*)recv, nrecv, W0, marks, row_first);
     return hipGetLastError();
 }
 
