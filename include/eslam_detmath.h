@@ -43,6 +43,20 @@ DM_FN int dm_isnan(double x) { return x != x; }
 DM_FN int dm_isfinite(double x) { return (dm_bits(x) & 0x7ff0000000000000ull) != 0x7ff0000000000000ull; }
 DM_FN double dm_fabs(double x) { return dm_from_bits(dm_bits(x) & 0x7fffffffffffffffull); }
 DM_FN double dm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+/* fma(a, b, k) with k a compile-time (wave-uniform) constant.  On gfx950 the compiler
+ * emits Horner steps as v_fmac_f64 with the constant moved into the destination VGPRs
+ * (two v_mov_b32 per step); the VOP3 form reads it from an SGPR pair materialised by
+ * the scalar unit instead.  Same IEEE fma, so host and device stay bit-identical.      */
+#if defined(__HIP_DEVICE_COMPILE__)
+DM_FN double dm_fmak(double a, double b, double k)
+{
+    double r;
+    __asm__("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+#else
+DM_FN double dm_fmak(double a, double b, double k) { return __builtin_fma(a, b, k); }
+#endif
 DM_FN double dm_sqrt(double x) { return __builtin_sqrt(x); }
 DM_FN double dm_floor(double x) { return __builtin_floor(x); }
 
@@ -83,19 +97,19 @@ DM_FN double dm_rint_small(double x)
 DM_FN double dm_exp_kernel(double r)
 {
     double p = 1.6059043836821613e-10;          /* 1/13! */
-    p = dm_fma(p, r, 2.08767569878681e-09);     /* 1/12! */
-    p = dm_fma(p, r, 2.505210838544172e-08);    /* 1/11! */
-    p = dm_fma(p, r, 2.755731922398589e-07);    /* 1/10! */
-    p = dm_fma(p, r, 2.7557319223985893e-06);   /* 1/9!  */
-    p = dm_fma(p, r, 2.48015873015873e-05);     /* 1/8!  */
-    p = dm_fma(p, r, 0.0001984126984126984);    /* 1/7!  */
-    p = dm_fma(p, r, 0.001388888888888889);     /* 1/6!  */
-    p = dm_fma(p, r, 0.008333333333333333);     /* 1/5!  */
-    p = dm_fma(p, r, 0.041666666666666664);     /* 1/4!  */
-    p = dm_fma(p, r, 0.16666666666666666);      /* 1/3!  */
-    p = dm_fma(p, r, 0.5);
-    p = dm_fma(p, r, 1.0);
-    return dm_fma(p, r, 1.0);
+    p = dm_fmak(p, r, 2.08767569878681e-09);     /* 1/12! */
+    p = dm_fmak(p, r, 2.505210838544172e-08);    /* 1/11! */
+    p = dm_fmak(p, r, 2.755731922398589e-07);    /* 1/10! */
+    p = dm_fmak(p, r, 2.7557319223985893e-06);   /* 1/9!  */
+    p = dm_fmak(p, r, 2.48015873015873e-05);     /* 1/8!  */
+    p = dm_fmak(p, r, 0.0001984126984126984);    /* 1/7!  */
+    p = dm_fmak(p, r, 0.001388888888888889);     /* 1/6!  */
+    p = dm_fmak(p, r, 0.008333333333333333);     /* 1/5!  */
+    p = dm_fmak(p, r, 0.041666666666666664);     /* 1/4!  */
+    p = dm_fmak(p, r, 0.16666666666666666);      /* 1/3!  */
+    p = dm_fmak(p, r, 0.5);
+    p = dm_fmak(p, r, 1.0);
+    return dm_fmak(p, r, 1.0);
 }
 
 DM_FN double dm_exp(double x)
@@ -129,15 +143,15 @@ DM_FN double dm_log(double x)
     double z = s * s;
     /* R = 2 z/3 + 2 z^2/5 + ... + 2 z^10/21  (atanh series; truncation < 3e-17 relative) */
     double R = 0.09523809523809523;            /* 2/21 */
-    R = dm_fma(R, z, 0.10526315789473684);     /* 2/19 */
-    R = dm_fma(R, z, 0.11764705882352941);     /* 2/17 */
-    R = dm_fma(R, z, 0.13333333333333333);     /* 2/15 */
-    R = dm_fma(R, z, 0.15384615384615385);     /* 2/13 */
-    R = dm_fma(R, z, 0.18181818181818182);     /* 2/11 */
-    R = dm_fma(R, z, 0.2222222222222222);      /* 2/9  */
-    R = dm_fma(R, z, 0.2857142857142857);      /* 2/7  */
-    R = dm_fma(R, z, 0.4);                     /* 2/5  */
-    R = dm_fma(R, z, 0.6666666666666666);      /* 2/3  */
+    R = dm_fmak(R, z, 0.10526315789473684);     /* 2/19 */
+    R = dm_fmak(R, z, 0.11764705882352941);     /* 2/17 */
+    R = dm_fmak(R, z, 0.13333333333333333);     /* 2/15 */
+    R = dm_fmak(R, z, 0.15384615384615385);     /* 2/13 */
+    R = dm_fmak(R, z, 0.18181818181818182);     /* 2/11 */
+    R = dm_fmak(R, z, 0.2222222222222222);      /* 2/9  */
+    R = dm_fmak(R, z, 0.2857142857142857);      /* 2/7  */
+    R = dm_fmak(R, z, 0.4);                     /* 2/5  */
+    R = dm_fmak(R, z, 0.6666666666666666);      /* 2/3  */
     R = R * z;
     /* log(1+f) = 2 atanh(s) = 2s + s R, and 2s = f - s f  ->  f - s (f - R) */
     double l = f - s * (f - R);
@@ -157,14 +171,14 @@ DM_FN double dm_sin_kernel(double r)   /* |r| <= pi/4, Taylor to r^19 */
 {
     double z = r * r;
     double p = 8.22063524662433e-18;            /* 1/19! */
-    p = dm_fma(p, z, -2.8114572543455206e-15);  /* -1/17! */
-    p = dm_fma(p, z, 7.647163731819816e-13);    /* 1/15! */
-    p = dm_fma(p, z, -1.6059043836821613e-10);  /* -1/13! */
-    p = dm_fma(p, z, 2.505210838544172e-08);    /* 1/11! */
-    p = dm_fma(p, z, -2.7557319223985893e-06);  /* -1/9! */
-    p = dm_fma(p, z, 0.0001984126984126984);    /* 1/7!  */
-    p = dm_fma(p, z, -0.008333333333333333);    /* -1/5! */
-    p = dm_fma(p, z, 0.16666666666666666);      /* 1/3! (subtracted below) */
+    p = dm_fmak(p, z, -2.8114572543455206e-15);  /* -1/17! */
+    p = dm_fmak(p, z, 7.647163731819816e-13);    /* 1/15! */
+    p = dm_fmak(p, z, -1.6059043836821613e-10);  /* -1/13! */
+    p = dm_fmak(p, z, 2.505210838544172e-08);    /* 1/11! */
+    p = dm_fmak(p, z, -2.7557319223985893e-06);  /* -1/9! */
+    p = dm_fmak(p, z, 0.0001984126984126984);    /* 1/7!  */
+    p = dm_fmak(p, z, -0.008333333333333333);    /* -1/5! */
+    p = dm_fmak(p, z, 0.16666666666666666);      /* 1/3! (subtracted below) */
     return dm_fma(-r * z, p, r) ;
 }
 
@@ -172,16 +186,16 @@ DM_FN double dm_cos_kernel(double r)   /* |r| <= pi/4, Taylor to r^20 */
 {
     double z = r * r;
     double p = 4.110317623312165e-19;           /* 1/20! */
-    p = dm_fma(p, z, -1.5619206968586225e-16);  /* -1/18! */
-    p = dm_fma(p, z, 4.779477332387385e-14);    /* 1/16! */
-    p = dm_fma(p, z, -1.1470745597729725e-11);  /* -1/14! */
-    p = dm_fma(p, z, 2.08767569878681e-09);     /* 1/12! */
-    p = dm_fma(p, z, -2.755731922398589e-07);   /* -1/10! */
-    p = dm_fma(p, z, 2.48015873015873e-05);     /* 1/8!  */
-    p = dm_fma(p, z, -0.001388888888888889);    /* -1/6! */
-    p = dm_fma(p, z, 0.041666666666666664);     /* 1/4!  */
-    p = dm_fma(p, z, -0.5);
-    return dm_fma(p, z, 1.0);
+    p = dm_fmak(p, z, -1.5619206968586225e-16);  /* -1/18! */
+    p = dm_fmak(p, z, 4.779477332387385e-14);    /* 1/16! */
+    p = dm_fmak(p, z, -1.1470745597729725e-11);  /* -1/14! */
+    p = dm_fmak(p, z, 2.08767569878681e-09);     /* 1/12! */
+    p = dm_fmak(p, z, -2.755731922398589e-07);   /* -1/10! */
+    p = dm_fmak(p, z, 2.48015873015873e-05);     /* 1/8!  */
+    p = dm_fmak(p, z, -0.001388888888888889);    /* -1/6! */
+    p = dm_fmak(p, z, 0.041666666666666664);     /* 1/4!  */
+    p = dm_fmak(p, z, -0.5);
+    return dm_fmak(p, z, 1.0);
 }
 
 DM_FN void dm_sincos(double x, double* s, double* c)
@@ -213,7 +227,7 @@ DM_FN double dm_horner(const double* c, int n, double u)
 {
     double p = c[0];
     DM_UNROLL
-    for (int i = 1; i < n; ++i) p = dm_fma(p, u, c[i]);
+    for (int i = 1; i < n; ++i) p = dm_fmak(p, u, c[i]);
     return p;
 }
 
@@ -349,6 +363,35 @@ DM_FN void dm_box_muller(double u1, double u2, double* z0, double* z1)
     double r = dm_sqrt(-2.0 * dm_log(1.0 - u1));
     double s, c;
     dm_sincos(6.283185307179586 * u2, &s, &c);
+    *z0 = r * c;
+    *z1 = r * s;
+}
+
+/* uniform in (0, 1) from one 32-bit word: (a + 1/2) 2^-32, exact.  32-bit resolution, like
+ * the reference's 31-bit minstd_rand behind boost's uniform_real / normal_distribution. */
+DM_FN double dm_u32(uint32_t a) { return ((double)a + 0.5) * 2.3283064365386963e-10; }
+
+/* sin and cos of 2 pi u for u in (0, 1): the quarter-turn reduction t = 4u - q is exact,
+ * one rounding in r = t pi/2 (|r| <= pi/4), then the kernels of dm_sincos.             */
+DM_FN void dm_sincos2pi(double u, double* s, double* c)
+{
+    const double t = u * 4.0;
+    const double q = dm_floor(t + 0.5);
+    const double r = (t - q) * 1.5707963267948966;
+    const double sr = dm_sin_kernel(r), cr = dm_cos_kernel(r);
+    const int qi = (int)q & 3;
+    if (qi == 0) { *s = sr; *c = cr; }
+    else if (qi == 1) { *s = cr; *c = -sr; }
+    else if (qi == 2) { *s = -sr; *c = -cr; }
+    else { *s = -cr; *c = sr; }
+}
+
+/* Box-Muller from two 32-bit words (the project / init draw layout) */
+DM_FN void dm_box_muller32(uint32_t a, uint32_t b, double* z0, double* z1)
+{
+    const double r = dm_sqrt(-2.0 * dm_log(dm_u32(a)));
+    double s, c;
+    dm_sincos2pi(dm_u32(b), &s, &c);
     *z0 = r * c;
     *z1 = r * s;
 }

@@ -231,6 +231,9 @@ static double contact_likelihood_ratio(const or_contact_model* cm, double z, dou
  * The sum is kept (shape_s2) so that m^(1/n) = exp(-s2 / (2 n)) needs no log.           */
 static void evaluate_weight(or_contact_model* cm)
 {
+    /* src/ContactModel.cpp:262-317 with rounding-level restatements:
+     * 1/zvar once per point, delta = d1 * (1/d2), odiff^2 = (zdiff - delta)^2 / zvar,
+     * prod exp(-odiff^2 / 2) = exp(-s2 / 2) */
     double d1 = 0, d2 = 0;
     double iv[ESLAM_MAX_CONTACTS];
     for (uint32_t i = 0; i < cm->ncp; ++i) {
@@ -238,26 +241,28 @@ static void evaluate_weight(or_contact_model* cm)
         d1 += cm->cp[i].zdiff * iv[i];
         d2 += iv[i];
     }
-    const double delta = d1 / d2;
+    const double inv_d2 = 1.0 / d2;
+    const double delta = d1 * inv_d2;
     double s2 = 0.0;
     for (uint32_t i = 0; i < cm->ncp; ++i) {
-        const double odiff = (cm->cp[i].zdiff - delta) * sqrt(iv[i]);
-        s2 += odiff * odiff;
+        const double d = cm->cp[i].zdiff - delta;
+        s2 += (d * d) * iv[i];
     }
     /* useSlipUpdate multiplies by p.prob, which is always 1 at push time (Q8) */
     cm->shape_s2 = s2;
     cm->weight = cm->use_shape_update ? dm_exp(-0.5 * s2) : 1.0;
     cm->zdelta = -delta;
-    cm->zvar = 1.0 / d2;
+    cm->zvar = inv_d2;
 }
 
 /* contactLikelihoodRatio(z, sigma) > 1e-9 guaranteed (exact-arithmetic bounds with a wide
- * margin): for a group of ONE evaluated point the ratio cancels,
+ * margin), sigma^2 = zvar corr^2: for a group of ONE evaluated point the ratio cancels,
  * (zdiff*r)/r = zdiff, and is not evaluated (rounding-level restatement)                */
-static int ratio_surely_significant(double z, double s)
+static int ratio_surely_significant(double z, double zvar, double corr)
 {
-    if (z <= 0.0) return s < 1e8;                  /* ratio >= sqrt(2/pi)/s            */
-    return s < 40.0 && z < 5.6 * s;                /* ratio >= 0.399 exp(-16) / s      */
+    const double s2 = zvar * (corr * corr);
+    if (z <= 0.0) return s2 < 1e16;                       /* ratio >= sqrt(2/pi)/s, s < 1e8   */
+    return s2 < 1600.0 && z * z < 31.36 * s2;             /* s < 40, z < 5.6 s                */
 }
 
 /* ContactModel::evaluatePose  src/ContactModel.cpp:117-224 (group quirk Q7 kept) */
@@ -289,7 +294,7 @@ int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_va
                 const double zvar = stdev * stdev + meas_var;
                 const double sq = sqrt(zvar);
                 const int ends = (gid == -1 || i + 1 == cm->m || gid != cm->group[i + 1]);
-                if (!valid && ends && ratio_surely_significant(zdiff, sq * cm->correction)) {
+                if (!valid && ends && ratio_surely_significant(zdiff, zvar, cm->correction)) {
                     /* single-point group: push (zdiff, zvar) directly */
                     p.point[0] = w[0]; p.point[1] = w[1]; p.point[2] = mean;
                     p.zdiff = zdiff;
@@ -574,10 +579,9 @@ int or_init_gaussian(or_filter* f, uint64_t n, const double mu[3], const double 
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i) {
         dm_philox_ctr d0 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, f->gbase + i, 0);
-        dm_philox_ctr d1 = dm_draw(f->cfg.seed, DM_STREAM_INIT, f->init_count, f->gbase + i, 1);
         double n0, n1, n2, n3;
-        dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &n0, &n1);
-        dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &n2, &n3);
+        dm_box_muller32(d0.v[0], d0.v[1], &n0, &n1);
+        dm_box_muller32(d0.v[2], d0.v[3], &n2, &n3);
         f->x[i] = n0 * sigma[0] + mu[0];
         f->y[i] = n1 * sigma[1] + mu[1];
         f->th[i] = n2 * sigma[2] + mu[2];
@@ -700,17 +704,19 @@ int or_project(or_filter* f, const eslam_step_input* in)
     for (uint64_t i = 0; i < f->n; ++i) {
         double z0, z1, z2, sn0, sn1 = 0, sn2 = 0;
         const uint64_t gi = f->gbase + i;
+        /* draw layout: call 0 -> Box-Muller pairs (z0, z1), (z2, sn0); call 1 -> slip test,
+         * slip factor, spread pair (sn1, sn2)  (the odometry sampler and rand_uni/rand_norm
+         * of src/PoseEstimator.cpp:198-236, restated on Philox) */
         dm_philox_ctr d0 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 0);
         dm_philox_ctr d1 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 1);
-        dm_philox_ctr d2 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 2);
-        dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &z0, &z1);
-        dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &z2, &sn0);
+        dm_box_muller32(d0.v[0], d0.v[1], &z0, &z1);
+        dm_box_muller32(d0.v[2], d0.v[3], &z2, &sn0);
         /* odometry.getPoseDeltaSample2D(): mu + L z */
         double dx = pp.mu[0] + L[0] * z0;
         double dy = pp.mu[1] + (L[3] * z0 + L[4] * z1);
         double dth = pp.mu[2] + ((L[6] * z0 + L[7] * z1) + L[8] * z2);
-        const double u_slip = dm_u53(d2.v[0], d2.v[1]);
-        if (u_slip < c->slip_factor) dy *= dm_u53(d2.v[2], d2.v[3]);
+        const double u_slip = dm_u32(d1.v[0]);
+        if (u_slip < c->slip_factor) dy *= dm_u32(d1.v[1]);
         double s, co;
         dm_sincos(f->th[i], &s, &co);
         f->x[i] += co * dx - s * dy;
@@ -722,8 +728,7 @@ int or_project(or_filter* f, const eslam_step_input* in)
         f->z[i] += pp.z_delta;
         f->zs[i] = sqrt(f->zs[i] * f->zs[i] + pp.z_var);
         if (do_spread) {
-            dm_philox_ctr d3 = dm_draw(c->seed, DM_STREAM_PROJECT, f->project_count, gi, 3);
-            dm_box_muller(dm_u53(d3.v[0], d3.v[1]), dm_u53(d3.v[2], d3.v[3]), &sn1, &sn2);
+            dm_box_muller32(d1.v[2], d1.v[3], &sn1, &sn2);
             f->x[i] += sn0 * tf + 0.0;
             f->y[i] += sn1 * tf + 0.0;
             f->th[i] += sn2 * rf + 0.0;
@@ -1337,6 +1342,8 @@ double or_dm(int fn, double x, double y)
     case 10: return dm_erfcx_pos(x);
     case 11: return dm_ldexp(x, (int)y);
     case 12: return dm_weighting_function(x, 0.0, y, 0.0);
+    case 13: dm_sincos2pi(x, &s, &c); return s;
+    case 14: dm_sincos2pi(x, &s, &c); return c;
     default: return NAN;
     }
 }

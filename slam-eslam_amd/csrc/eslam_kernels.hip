@@ -231,12 +231,14 @@ struct CMResult {
     double weight, zdelta, zvar, posevar, s2;
 };
 
-// contactLikelihoodRatio(z, sigma) > 1e-9 guaranteed (exact-arithmetic bounds, wide margin):
-// a one-point group's ratio cancels ((zdiff*r)/r = zdiff) and is not evaluated
-__device__ __forceinline__ bool ratio_surely_significant(double z, double s)
+// contactLikelihoodRatio(z, sigma) > 1e-9 guaranteed (exact-arithmetic bounds, wide margin),
+// sigma^2 = zvar corr^2: a one-point group's ratio cancels ((zdiff*r)/r = zdiff) and is not
+// evaluated (same predicate as the oracle)
+__device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, double corr)
 {
-    if (z <= 0.0) return s < 1e8;
-    return s < 40.0 && z < 5.6 * s;
+    const double s2 = zvar * (corr * corr);
+    if (z <= 0.0) return s2 < 1e16;
+    return s2 < 1600.0 && z * z < 31.36 * s2;
 }
 
 template <int MAXP>
@@ -264,8 +266,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
                 const double zdiff = wz - mean;
                 const double pose_var = stdev * stdev;
                 const double zvar = stdev * stdev + meas_var;
-                const double sq = dm_sqrt(zvar);
-                if (!valid && c.end && ratio_surely_significant(zdiff, sq * p.corr)) {
+                if (!valid && c.end && ratio_surely_significant(zdiff, zvar, p.corr)) {
                     // single-point group: (zdiff, zvar) pushed directly
                     posevar += pose_var;
 #pragma unroll
@@ -281,7 +282,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
 #ifdef ESLAM_ABL_NO_RATIO
                 const double ratio = 1.0 + zdiff * 1e-3;
 #else
-                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, sq * p.corr);
+                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * p.corr);
 #endif
                 if (!valid) {
                     pzd = zdiff * ratio;
@@ -330,13 +331,14 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
                 d2 += cv[k];
             }
         }
-        const double delta = d1 / d2;
+        const double inv_d2 = 1.0 / d2;
+        const double delta = d1 * inv_d2;
         double s2 = 0.0;
 #pragma unroll
         for (int k = 0; k < MAXP; ++k) {
             if ((uint32_t)k < ncp) {
-                const double odiff = (cz[k] - delta) * dm_sqrt(cv[k]);
-                s2 += odiff * odiff;
+                const double d = cz[k] - delta;
+                s2 += (d * d) * cv[k];
             }
         }
         r.s2 = s2;
@@ -347,7 +349,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
 #endif
         r.weight = pz;
         r.zdelta = -delta;
-        r.zvar = 1.0 / d2;
+        r.zvar = inv_d2;
     }
     return r;
 }
@@ -447,22 +449,18 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
         const double w_in = w;
         if (PROJECT) {
             const uint64_t gi = p.gbase + i;
-#ifdef ESLAM_ABL_NO_RNG
-            dm_philox_ctr d2; d2.v[0] = (uint32_t)gi * 2654435761u; d2.v[1] = d2.v[0] ^ 0x9e3779b9u; d2.v[2] = d2.v[1] * 3u; d2.v[3] = d2.v[2] + 7u;
-            double z0 = dm_u53(d2.v[0], d2.v[1]) - 0.5, z1 = dm_u53(d2.v[2], d2.v[3]) - 0.5, z2 = z0 * z1, sn0 = z1 - z0;
-#else
-            dm_philox_ctr d0 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 0);
-            dm_philox_ctr d1 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 1);
-            dm_philox_ctr d2 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 2);
+            // draw layout: call 0 -> two Box-Muller pairs (z0, z1), (z2, sn0);
+            // call 1 -> slip test + slip factor, spread pair (sn1, sn2)
+            const dm_philox_ctr d0 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 0);
+            const dm_philox_ctr d1 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 1);
             double z0, z1, z2, sn0;
-            dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &z0, &z1);
-            dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &z2, &sn0);
-#endif
+            dm_box_muller32(d0.v[0], d0.v[1], &z0, &z1);
+            dm_box_muller32(d0.v[2], d0.v[3], &z2, &sn0);
             // odometry.getPoseDeltaSample2D() = mu + L z
             const double dx = p.mu[0] + p.L00 * z0;
             double dy = p.mu[1] + (p.L10 * z0 + p.L11 * z1);
             const double dth = p.mu[2] + ((p.L20 * z0 + p.L21 * z1) + p.L22 * z2);
-            if (dm_u53(d2.v[0], d2.v[1]) < p.slip_factor) dy *= dm_u53(d2.v[2], d2.v[3]);
+            if (dm_u32(d1.v[0]) < p.slip_factor) dy *= dm_u32(d1.v[1]);
             double s, co;
             dm_sincos(th, &s, &co);
             x += co * dx - s * dy;
@@ -474,9 +472,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
             z += p.z_delta;
             zs = dm_sqrt(zs * zs + p.z_var);
             if (do_spread) {
-                dm_philox_ctr d3 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 3);
                 double sn1, sn2;
-                dm_box_muller(dm_u53(d3.v[0], d3.v[1]), dm_u53(d3.v[2], d3.v[3]), &sn1, &sn2);
+                dm_box_muller32(d1.v[2], d1.v[3], &sn1, &sn2);
                 x += sn0 * tf + 0.0;
                 y += sn1 * tf + 0.0;
                 th += sn2 * rf + 0.0;
@@ -525,10 +522,14 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
             const uint32_t bucket = r.ncp < DM_NBUCKETS - 1 ? r.ncp : DM_NBUCKETS - 1;
             const double a = w * mprob;
             const double a2 = a * a;
+            // only the particle's bucket changes (adding +0.0 elsewhere, as the oracle's
+            // canonical sum does, can only turn a -0.0 into +0.0: same fixed point)
 #pragma unroll
             for (int b = 0; b < DM_NBUCKETS; ++b) {
-                accA[b] = accA[b] + (bucket == (uint32_t)b ? a : 0.0);
-                accB[b] = accB[b] + (bucket == (uint32_t)b ? a2 : 0.0);
+                if (bucket == (uint32_t)b) {
+                    accA[b] = accA[b] + a;
+                    accB[b] = accB[b] + a2;
+                }
             }
             accSW = accSW + sw;
             st.mprob[i] = mprob;
@@ -1342,11 +1343,10 @@ __global__ void __launch_bounds__(kBlock) k_init_gaussian(DevState s0, uint64_t 
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint64_t gi = gbase + i;
-    dm_philox_ctr d0 = dm_draw(seed, DM_STREAM_INIT, ev, gi, 0);
-    dm_philox_ctr d1 = dm_draw(seed, DM_STREAM_INIT, ev, gi, 1);
+    const dm_philox_ctr d0 = dm_draw(seed, DM_STREAM_INIT, ev, gi, 0);
     double n0, n1, n2, n3;
-    dm_box_muller(dm_u53(d0.v[0], d0.v[1]), dm_u53(d0.v[2], d0.v[3]), &n0, &n1);
-    dm_box_muller(dm_u53(d1.v[0], d1.v[1]), dm_u53(d1.v[2], d1.v[3]), &n2, &n3);
+    dm_box_muller32(d0.v[0], d0.v[1], &n0, &n1);
+    dm_box_muller32(d0.v[2], d0.v[3], &n2, &n3);
     s0.x[i] = n0 * sx + mx;
     s0.y[i] = n1 * sy + my;
     s0.th[i] = n2 * stt + mt;
@@ -1445,6 +1445,8 @@ __global__ void k_selftest_math(int fn, const double* x, const double* y, double
     case 7: r = dm_normal_pdf_cdf_ratio(x[i], y[i]); break;
     case 8: r = dm_pow(x[i], y[i]); break;
     case 9: r = dm_from_bits(dm_fx61(x[i])); break;
+    case 13: dm_sincos2pi(x[i], &s, &c); r = s; break;
+    case 14: dm_sincos2pi(x[i], &s, &c); r = c; break;
     default: r = __builtin_nan("");
     }
     out[i] = r;

@@ -56,6 +56,29 @@ def test_sincos(dm, fn, ref):
     assert worst_abs <= 4.5e-16
 
 
+@pytest.mark.parametrize("fn,ref", [(13, mp.sin), (14, mp.cos)])
+def test_sincos2pi(dm, fn, ref):
+    """sin/cos(2 pi u) of the Box-Muller angle, u = (a + 1/2) 2^-32 (dm_box_muller32)."""
+    a = _rng().integers(0, 2 ** 32, 4000, dtype=np.uint64)
+    us = np.concatenate([(a.astype(np.float64) + 0.5) * 2.0 ** -32, [0.125, 0.25, 0.5, 0.75, 0.999]])
+    worst_abs = max(abs(dm(fn, float(u)) - float(ref(2 * mp.pi * mp.mpf(float(u))))) for u in us)
+    assert worst_abs <= 4.5e-16
+
+
+def test_box_muller32_moments(oracle):
+    """Normals of the 32-bit Box-Muller draw layout: mean 0, variance 1, symmetric."""
+    z = []
+    for g in range(20000):
+        out = (C.c_uint32 * 4)()
+        oracle.lib().or_dm_philox(42, 1, 0, g, 0, out)
+        u1 = (out[0] + 0.5) * 2.0 ** -32
+        u2 = (out[1] + 0.5) * 2.0 ** -32
+        r = math.sqrt(-2.0 * math.log(u1))
+        z.append(r * math.cos(2 * math.pi * u2))
+    z = np.array(z)
+    assert abs(z.mean()) < 0.03 and abs(z.var() - 1.0) < 0.04 and abs(np.mean(z ** 3)) < 0.08
+
+
 def test_erfc(dm):
     xs = np.concatenate([_rng().uniform(-6, 27, 4000), _rng().uniform(-0.5, 0.5, 1000), [0.0, 0.5, 1.5, 3.0, 5.0, 26.5]])
     for x in xs:

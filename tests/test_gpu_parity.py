@@ -35,7 +35,7 @@ def factory(gpu_mod):
 
 
 @pytest.mark.parametrize("fn,lo,hi", [(0, -740, 700), (1, 1e-300, 1e300), (2, -50, 50), (3, -50, 50), (4, -8, 27),
-                                      (5, 0, 1e10), (8, 0, 1.5), (9, 0, 1.9)])
+                                      (5, 0, 1e10), (8, 0, 1.5), (9, 0, 1.9), (13, 0, 1), (14, 0, 1)])
 def test_gpu_math_bit_identical(gpu_mod, oracle, fn, lo, hi):
     rng = np.random.default_rng(fn)
     x = rng.uniform(lo, hi, 20000) if fn != 1 else np.exp(rng.uniform(-690, 690, 20000))
