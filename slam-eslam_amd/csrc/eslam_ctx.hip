@@ -208,6 +208,8 @@ struct eslam_ctx {
     Ctl* ctl = nullptr;
     Ctl* ctl_host = nullptr;    // pinned
     uint32_t* jump = nullptr;
+    uint32_t jump_n = 1;                    // A^n_global, cached
+    uint64_t jump_n_for = 0;
     double* scratch = nullptr;  // small device scratch (centroid, best index)
     double* scratch_host = nullptr;
     // map
@@ -864,6 +866,11 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
     fp.discount = ctx->cfg.discount_factor;
     fp.spread_threshold = ctx->cfg.spread_threshold;
     fp.mode = mode;
+    if (ctx->jump_n_for != ctx->n_global) {
+        ctx->jump_n = dm_minstd_pow(ctx->n_global);
+        ctx->jump_n_for = ctx->n_global;
+    }
+    fp.minstd_jump_n = ctx->jump_n;
     return fp;
 }
 

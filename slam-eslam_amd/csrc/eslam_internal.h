@@ -145,7 +145,7 @@ struct FinParams {
     uint32_t mode;
     int32_t wexp;                        // scale exponent used by the statistics kernel
     uint32_t record;                     // 1: write update info
-    uint32_t pad;
+    uint32_t minstd_jump_n;              // A^n_global mod (2^31 - 1): the resample's N draws
 };
 
 struct ScanParams {

@@ -711,15 +711,22 @@ __device__ __forceinline__ double acc_value(const uint64_t* L, uint64_t flags, i
 // combine field t of nrec statistics records exactly (sum / max / or by field) and zero them
 __device__ __forceinline__ uint64_t reduce_field(Shard* recs, int nrec, int t)
 {
+    // all loads first (they are independent), then combine: one memory latency, not nrec
+    uint64_t v[kMaxRanks > kNShard ? kMaxRanks : kNShard];
+    constexpr int kCap = kMaxRanks > kNShard ? kMaxRanks : kNShard;
+#pragma unroll
+    for (int k = 0; k < kCap; ++k) v[k] = k < nrec ? reinterpret_cast<const uint64_t*>(recs + k)[t] : 0ull;
+#pragma unroll
+    for (int k = 0; k < kCap; ++k)
+        if (k < nrec) reinterpret_cast<uint64_t*>(recs + k)[t] = 0;
     uint64_t acc = 0;
     const int base = 2 * DM_NBUCKETS * 4 + 4;                                  // D
-    for (int k = 0; k < nrec; ++k) {
-        uint64_t* f = reinterpret_cast<uint64_t*>(recs + k) + t;
-        const uint64_t v = *f;
-        if (t == base + 2 || t >= base + 5) acc = acc > v ? acc : v;            // maxm, bbox
-        else if (t == base + 3 || t == base + 4) acc |= v;                      // flags, err
-        else acc += v;
-        *f = 0;
+#pragma unroll
+    for (int k = 0; k < kCap; ++k) {
+        if (k >= nrec) break;
+        if (t == base + 2 || t >= base + 5) acc = acc > v[k] ? acc : v[k];      // maxm, bbox
+        else if (t == base + 3 || t == base + 4) acc |= v[k];                   // flags, err
+        else acc += v[k];
     }
     return acc;
 }
@@ -735,25 +742,38 @@ __global__ void __launch_bounds__(kBlock) k_shard_reduce(Shard* __restrict__ sha
 __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, int nrec, Ctl* __restrict__ ctl, FinParams fp)
 {
     __shared__ uint64_t s[kShardFields];
+    __shared__ double s_acc[2 * DM_NBUCKETS + 1];     // exact sums A_b, B_b, SW as doubles
+    __shared__ double s_f[DM_NBUCKETS];
     const int t = threadIdx.x;
     if (t < kShardFields) s[t] = reduce_field(recs, nrec, t);
     __syncthreads();
+    {
+        // the 13 fixed-point -> double conversions, one per lane (same values as serially)
+        const uint64_t flags_ = s[2 * DM_NBUCKETS * 4 + 7];
+        const int wexp_ = ctl->wexp;
+        if (t < 2 * DM_NBUCKETS + 1) {
+            const int scale = t < DM_NBUCKETS ? DM_FX_SCALE - wexp_
+                            : (t < 2 * DM_NBUCKETS ? DM_FX_SCALE - 2 * wexp_ : DM_FX_SCALE);
+            s_acc[t] = acc_value(s + 4 * t, flags_, t, scale);
+        }
+        __syncthreads();
+        // phase-B factors (0.9 fw)^(4 - n), one bucket per lane
+        if (fp.mode == FIN_UPDATE && t < DM_NBUCKETS) {
+            const uint64_t D_ = s[2 * DM_NBUCKETS * 4 + 4];
+            const double fw_ = D_ > 0 ? s_acc[2 * DM_NBUCKETS] / (double)D_ : 1.0;
+            s_f[t] = dm_pow(fp.discount * fw_, (double)(uint64_t)(4ull - (uint64_t)t));
+        }
+        __syncthreads();
+    }
     if (t != 0) return;
 
-    const uint64_t* sA = s;
-    const uint64_t* sB = s + DM_NBUCKETS * 4;
-    const uint64_t* sSW = s + 2 * DM_NBUCKETS * 4;
     const uint64_t D = s[2 * DM_NBUCKETS * 4 + 4];
     const uint64_t TP = s[2 * DM_NBUCKETS * 4 + 5];
     const double maxm = dm_from_bits(s[2 * DM_NBUCKETS * 4 + 6]);
-    const uint64_t flags = s[2 * DM_NBUCKETS * 4 + 7];
     const uint64_t err = s[2 * DM_NBUCKETS * 4 + 8];
     if (s[2 * DM_NBUCKETS * 4 + 10]) {                 // a weighting kernel saw particles
         for (int q = 0; q < 4; ++q) ctl->bbox[q] = s[2 * DM_NBUCKETS * 4 + 9 + q];
     }
-    const int wexp = ctl->wexp;      // the exponent the statistics kernel used
-    const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
-
     // commit the previous resample's buffer flip
     ctl->base ^= ctl->flip;
     ctl->flip = 0;
@@ -765,18 +785,13 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
 
     double S = 0.0, Q = 0.0;
     if (fp.mode == FIN_UPDATE) {
-        const double SW = acc_value(sSW, flags, 2 * DM_NBUCKETS, DM_FX_SCALE);
+        const double SW = s_acc[2 * DM_NBUCKETS];
         const double fw = D > 0 ? SW / (double)D : 1.0;
-        const double base = fp.discount * fw;
         for (int b = 0; b < DM_NBUCKETS; ++b) {
-            const uint64_t ncp = (uint64_t)b;
-            ctl->f[b] = dm_pow(base, (double)(uint64_t)(4ull - ncp));
-        }
-        for (int b = 0; b < DM_NBUCKETS; ++b) {
-            const double Ab = acc_value(sA + 4 * b, flags, b, sa);
-            const double Bb = acc_value(sB + 4 * b, flags, DM_NBUCKETS + b, sb);
-            S = S + ctl->f[b] * Ab;
-            Q = Q + (ctl->f[b] * ctl->f[b]) * Bb;
+            const double fb = s_f[b];
+            ctl->f[b] = fb;
+            S = S + fb * s_acc[b];
+            Q = Q + (fb * fb) * s_acc[DM_NBUCKETS + b];
         }
         ctl->fw = fw;
         const double last = ctl->max_weight;
@@ -787,8 +802,8 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
         ctl->total_points = TP;
         ctl->update_count += 1;
     } else {
-        S = acc_value(sA, flags, 0, sa);
-        Q = acc_value(sB, flags, DM_NBUCKETS, sb);
+        S = s_acc[0];
+        Q = s_acc[DM_NBUCKETS];
         for (int b = 0; b < DM_NBUCKETS; ++b) ctl->f[b] = 1.0;
     }
     ctl->S = S;
@@ -816,7 +831,7 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
     }
     if (ctl->resample) {
         ctl->minstd_start = ctl->minstd;
-        ctl->minstd = dm_mulmod31(dm_minstd_pow(fp.n_global), ctl->minstd);
+        ctl->minstd = dm_mulmod31(fp.minstd_jump_n, ctl->minstd);   // A^N, precomputed
         ctl->flip = 1;
         ctl->gather = 1;
     }
