@@ -212,6 +212,16 @@ DM_FN void dm_sincos(double x, double* s, double* c)
     else { *s = -cr; *c = sr; }
 }
 
+/* 1.0 / k for k = 0..32 (correctly rounded, as the division; k = 0 -> inf) */
+DM_CONST double dm_recip_tab[33] = {
+    __builtin_inf(), 1.0, 0.5, 0.3333333333333333, 0.25, 0.2, 0.16666666666666666, 0.14285714285714285,
+    0.125, 0.1111111111111111, 0.1, 0.09090909090909091, 0.08333333333333333, 0.07692307692307693,
+    0.07142857142857142, 0.06666666666666667, 0.0625, 0.058823529411764705, 0.05555555555555555,
+    0.05263157894736842, 0.05, 0.047619047619047616, 0.045454545454545456, 0.043478260869565216,
+    0.041666666666666664, 0.04, 0.038461538461538464, 0.037037037037037035, 0.03571428571428571,
+    0.034482758620689655, 0.03333333333333333, 0.03225806451612903, 0.03125};
+DM_FN double dm_recip_small(uint32_t k) { return k <= 32 ? dm_recip_tab[k] : 1.0 / (double)k; }
+
 /* ------------------------------------------------------------------------------------ */
 /* erfc                                                                                  */
 /* ------------------------------------------------------------------------------------ */

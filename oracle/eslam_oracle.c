@@ -159,9 +159,17 @@ int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_w
                      double* mean, double* stdev)
 {
     const double* A = g->global2local;
-    double lx = ((A[0] * p[0] + A[1] * p[1]) + A[2] * p[2]) + A[3];
-    double ly = ((A[4] * p[0] + A[5] * p[1]) + A[6] * p[2]) + A[7];
-    double lz = ((A[8] * p[0] + A[9] * p[1]) + A[10] * p[2]) + A[11];
+    double lx = p[0], ly = p[1], lz = p[2];
+    /* C_global2local * p; an exact identity is applied as the identity (differs from the
+     * affine multiply only for infinite / NaN coordinates) */
+    static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    int is_id = 1;
+    for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
+    if (!is_id) {
+        lx = ((A[0] * p[0] + A[1] * p[1]) + A[2] * p[2]) + A[3];
+        ly = ((A[4] * p[0] + A[5] * p[1]) + A[6] * p[2]) + A[7];
+        lz = ((A[8] * p[0] + A[9] * p[1]) + A[10] * p[2]) + A[11];
+    }
     const double q_mean = lz;
     (void)q_mean_world;
     const double inv_x = 1.0 / g->scale_x, inv_y = 1.0 / g->scale_y;

@@ -627,6 +627,10 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
     m.offset_x = g->offset_x;
     m.offset_y = g->offset_y;
     memcpy(m.g2l, g->global2local, sizeof(m.g2l));
+    static const double kId[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    m.g2l_identity = 1;
+    for (int k = 0; k < 12; ++k)
+        if (!(g->global2local[k] == kId[k])) m.g2l_identity = 0;
     ctx->has_map = true;
     return ESLAM_OK;
 }
@@ -816,6 +820,8 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
         double pos[3];
         q_rotate(yc, in->contacts[i].position, pos);
         p.c[i].px = pos[0]; p.c[i].py = pos[1]; p.c[i].pz = pos[2];
+        p.c[i].zp = 0.0 * pos[2];
+        p.c[i].zz = 0.0 * pos[0] + 0.0 * pos[1];
         p.c[i].eval = !((double)in->contacts[i].contact < 0.2) ? 1u : 0u;
         const int32_t g = in->contacts[i].group_id;
         p.c[i].end = (g == -1 || i + 1 == m || g != in->contacts[i + 1].group_id) ? 1u : 0u;

@@ -83,12 +83,16 @@ struct MapView {
     const float2* patch;                 // (mean, stdev) per patch
     const float* height;                 // nullable: all horizontal
     uint32_t width, height_cells;
+    uint32_t g2l_identity;               // global2local is exactly the identity
+    uint32_t pad;
     double inv_scale_x, inv_scale_y, offset_x, offset_y;
     double g2l[12];
 };
 
 struct ContactC {
     double px, py, pz;                   // yaw-compensated body-frame position
+    double zp;                           // 0.0 * pz: the zero terms of Affine3d * p (exact,
+    double zz;                           // (0.0 * px + 0.0 * py); uniform per step)
     uint32_t eval;                       // !(contact < 0.2)
     uint32_t end;                        // group ends after this contact
 };

@@ -78,18 +78,23 @@ __device__ __forceinline__ uint32_t jump_pow(const uint32_t* __restrict__ jt, ui
 // The window part of the grid under the particle cloud may be staged in LDS: identical
 // values, so the result never depends on whether a cell came from LDS or global memory.
 // ---------------------------------------------------------------------------------------
-struct Window {
-    int on;
-    int m0, m1, n0, n1, cols1;           // cell range [m0,m1) x [n0,n1); cols1 = m1 - m0 + 1
-    const uint32_t* cs;                  // rows x cols1 cell_start values (LDS)
-    const int32_t* rowoff;               // LDS patch offset minus the row's first global index
-    const float2* pt;                    // staged patches (LDS)
+// One window cell in LDS: its first patch inline + its patch range in global memory, so a
+// lookup is one 16-byte LDS read (further patches of multi-patch cells come from global).
+struct alignas(16) WinCell {
+    float mean0, stdev0;
+    uint32_t begin, count;
 };
 
-__device__ __forceinline__ bool patch_gate(const MapView& m, uint32_t k, float2 pf, double lz, double qv,
+struct Window {
+    int on;
+    int m0, m1, n0, n1, cols;            // cell range [m0,m1) x [n0,n1)
+    const WinCell* cells;                // rows x cols (LDS)
+};
+
+__device__ __forceinline__ bool patch_gate(const MapView& m, uint32_t k, float pmf, float psf, double lz, double qv,
                                            double& mean, double& stdev)
 {
-    const double pm = (double)pf.x, ps = (double)pf.y;
+    const double pm = (double)pmf, ps = (double)psf;
     const double ph = m.height ? (double)m.height[k] : 0.0;
     double diff;
     if (ph > 0.0) {
@@ -106,27 +111,33 @@ __device__ __forceinline__ bool patch_gate(const MapView& m, uint32_t k, float2 
 __device__ __forceinline__ bool get_patch(const MapView& m, const Window& win, double px, double py, double pz,
                                           double qv, double& mean, double& stdev)
 {
-    const double* A = m.g2l;
-    double lx = ((A[0] * px + A[1] * py) + A[2] * pz) + A[3];
-    double ly = ((A[4] * px + A[5] * py) + A[6] * pz) + A[7];
-    double lz = ((A[8] * px + A[9] * py) + A[10] * pz) + A[11];
+    double lx = px, ly = py, lz = pz;    // an identity global2local is applied as the identity
+    if (!m.g2l_identity) {
+        const double* A = m.g2l;
+        lx = ((A[0] * px + A[1] * py) + A[2] * pz) + A[3];
+        ly = ((A[4] * px + A[5] * py) + A[6] * pz) + A[7];
+        lz = ((A[8] * px + A[9] * py) + A[10] * pz) + A[11];
+    }
     double fm = floor((lx - m.offset_x) * m.inv_scale_x);
     double fn = floor((ly - m.offset_y) * m.inv_scale_y);
     if (!(fm >= 0.0 && fm < (double)m.width && fn >= 0.0 && fn < (double)m.height_cells)) return false;
     const int im = (int)fm, in = (int)fn;
+    uint32_t b, e;
     if (win.on && im >= win.m0 && im < win.m1 && in >= win.n0 && in < win.n1) {
-        const int r = in - win.n0;
-        const uint32_t* row = win.cs + r * win.cols1 + (im - win.m0);
-        const uint32_t b = row[0], e = row[1];
-        const int32_t off = win.rowoff[r];
-        for (uint32_t k = b; k < e; ++k)
-            if (patch_gate(m, k, win.pt[(int32_t)k + off], lz, qv, mean, stdev)) return true;
-        return false;
+        const WinCell wc = win.cells[(in - win.n0) * win.cols + (im - win.m0)];
+        if (wc.count == 0) return false;
+        if (patch_gate(m, wc.begin, wc.mean0, wc.stdev0, lz, qv, mean, stdev)) return true;
+        b = wc.begin + 1;
+        e = wc.begin + wc.count;
+    } else {
+        const uint64_t cell = (uint64_t)in * m.width + (uint64_t)im;
+        b = m.cell_start[cell];
+        e = m.cell_start[cell + 1];
     }
-    const uint64_t cell = (uint64_t)in * m.width + (uint64_t)im;
-    const uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
-    for (uint32_t k = b; k < e; ++k)
-        if (patch_gate(m, k, m.patch[k], lz, qv, mean, stdev)) return true;
+    for (uint32_t k = b; k < e; ++k) {
+        const float2 pf = m.patch[k];
+        if (patch_gate(m, k, pf.x, pf.y, lz, qv, mean, stdev)) return true;
+    }
     return false;
 }
 
@@ -149,7 +160,6 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
     __shared__ int s_w[8];
     Window w;
     w.on = 0;
-    uint32_t* cs = reinterpret_cast<uint32_t*>(lds);
     if (threadIdx.x == 0) {
         int on = 0;
         const uint64_t k0 = ctl->bbox[0], k1 = ctl->bbox[1], k2 = ctl->bbox[2], k3 = ctl->bbox[3];
@@ -175,10 +185,10 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
                 const int m1 = (int)(fm1 < 0 ? 0 : (fm1 > W ? W : fm1));
                 const int n0 = (int)(fn0 < 0 ? 0 : (fn0 > H ? H : fn0));
                 const int n1 = (int)(fn1 < 0 ? 0 : (fn1 > H ? H : fn1));
-                const int rows = n1 - n0, cols1 = m1 - m0 + 1;
-                if (rows > 0 && cols1 > 1 && (int64_t)rows * cols1 * 4 + rows * 4 + 64 <= kWindowLds) {
+                const int rows = n1 - n0, cols = m1 - m0;
+                if (rows > 0 && cols > 0 && (int64_t)rows * cols * (int64_t)sizeof(WinCell) <= kWindowLds) {
                     on = 1;
-                    s_w[1] = m0; s_w[2] = m1; s_w[3] = n0; s_w[4] = n1; s_w[5] = cols1;
+                    s_w[1] = m0; s_w[2] = m1; s_w[3] = n0; s_w[4] = n1; s_w[5] = cols;
                 }
             }
         }
@@ -186,39 +196,24 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
     }
     __syncthreads();
     if (!s_w[0]) return w;
-    w.m0 = s_w[1]; w.m1 = s_w[2]; w.n0 = s_w[3]; w.n1 = s_w[4]; w.cols1 = s_w[5];
-    const int rows = w.n1 - w.n0;
-    const int ncs = rows * w.cols1;
-    for (int t = threadIdx.x; t < ncs; t += kBlock) {
-        const int r = t / w.cols1, c = t - r * w.cols1;
-        cs[t] = m.cell_start[(uint64_t)(w.n0 + r) * m.width + (uint64_t)(w.m0 + c)];
-    }
-    int32_t* rowoff = reinterpret_cast<int32_t*>(cs + ((ncs + 3) & ~3));
-    float2* pt = reinterpret_cast<float2*>(rowoff + ((rows + 3) & ~3));
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int64_t cap = (kWindowLds - (int64_t)((unsigned char*)pt - (unsigned char*)cs)) / 8;
-        int64_t tot = 0;
-        for (int r = 0; r < rows; ++r) {
-            const uint32_t b = cs[r * w.cols1], e = cs[r * w.cols1 + w.cols1 - 1];
-            rowoff[r] = (int32_t)(tot - (int64_t)b);
-            tot += (int64_t)(e - b);
-        }
-        s_w[6] = tot <= cap ? 1 : 0;
-    }
-    __syncthreads();
-    if (!s_w[6]) return w;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int r = wave; r < rows; r += kWaves) {
-        const uint32_t b = cs[r * w.cols1], e = cs[r * w.cols1 + w.cols1 - 1];
-        const int32_t off = rowoff[r];
-        for (uint32_t k = b + lane; k < e; k += 64) pt[(int32_t)k + off] = m.patch[k];
+    w.m0 = s_w[1]; w.m1 = s_w[2]; w.n0 = s_w[3]; w.n1 = s_w[4]; w.cols = s_w[5];
+    WinCell* cells = reinterpret_cast<WinCell*>(lds);
+    const int ncell = (w.n1 - w.n0) * w.cols;
+    for (int t = threadIdx.x; t < ncell; t += kBlock) {
+        const int r = t / w.cols, c = t - r * w.cols;
+        const uint64_t cell = (uint64_t)(w.n0 + r) * m.width + (uint64_t)(w.m0 + c);
+        const uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
+        WinCell wc;
+        wc.begin = b;
+        wc.count = e - b;
+        wc.mean0 = 0.0f;
+        wc.stdev0 = 0.0f;
+        if (e > b) { const float2 pf = m.patch[b]; wc.mean0 = pf.x; wc.stdev0 = pf.y; }
+        cells[t] = wc;
     }
     __syncthreads();
     w.on = 1;
-    w.cs = cs;
-    w.rowoff = rowoff;
-    w.pt = pt;
+    w.cells = cells;
     return w;
 }
 
@@ -241,7 +236,8 @@ __device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, 
     return s2 < 1600.0 && z * z < 31.36 * s2;
 }
 
-template <int MAXP>
+// MAXP: bound on the contact points found (group ends); BATCH: p.m <= MAXP contacts
+template <int MAXP, bool BATCH>
 __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const MapView& map, const Window& win, double co,
                                                   double s, double r22, double x, double y, double z, double meas_var)
 {
@@ -252,17 +248,13 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
     double contact_ratio = 0, pose_var_avg = 0, posevar = 0;
     double pzd = 0, pzv = 0;
     const double qv = meas_var;
-    for (uint32_t i = 0; i < p.m; ++i) {
-        const ContactC c = p.c[i];
-        double wx = ((co * c.px + (-s) * c.py) + 0.0 * c.pz) + x;
-        double wy = ((s * c.px + co * c.py) + 0.0 * c.pz) + y;
-        double wz = ((0.0 * c.px + 0.0 * c.py) + r22 * c.pz) + z;
-        wx = wx - 0.0;
-        wy = wy - 0.0;
-        wz = wz - p.radius;
+
+    // the sequential part of one contact (group logic, Q7 poisoning): found/mean/stdev are
+    // the map lookup of its world point (used only when the contact is evaluated)
+    auto contact = [&](uint32_t i, bool found, double mean, double stdev, double wz) {
+        const ContactC& c = p.c[i];
         if (group_valid && c.eval) {
-            double mean, stdev;
-            if (get_patch(map, win, wx, wy, wz, qv, mean, stdev)) {
+            if (found) {
                 const double zdiff = wz - mean;
                 const double pose_var = stdev * stdev;
                 const double zvar = stdev * stdev + meas_var;
@@ -277,7 +269,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
                     valid = false;
                     pose_var_avg = 0;
                     contact_ratio = 0;
-                    continue;
+                    return;
                 }
 #ifdef ESLAM_ABL_NO_RATIO
                 const double ratio = 1.0 + zdiff * 1e-3;
@@ -315,6 +307,50 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
             valid = false;
             pose_var_avg = 0;
             contact_ratio = 0;
+        }
+    };
+    // pose * p with pose = Translation(x, y, z) * AngleAxis(theta, UnitZ); the zero products
+    // of the affine multiply are per-step constants, and "- 0.0" is exact
+    auto world = [&](const ContactC& c, double& wx, double& wy, double& wz) {
+        wx = ((co * c.px + (-s) * c.py) + c.zp) + x;
+        wy = ((s * c.px + co * c.py) + c.zp) + y;
+        wz = ((c.zz + r22 * c.pz) + z) - p.radius;
+    };
+    auto lookup = [&](double wx, double wy, double wz, double& mean, double& stdev) -> bool {
+#ifdef ESLAM_ABL_NO_MAP
+        mean = 0.0; stdev = 0.05;
+        return wx == wx;
+#else
+        return get_patch(map, win, wx, wy, wz, qv, mean, stdev);
+#endif
+    };
+
+    if constexpr (BATCH) {
+        // all p.m <= MAXP contacts' lookups first: independent, so their memory latencies
+        // overlap (a lookup the group logic then skips is harmless: pure function)
+        bool fnd[MAXP];
+        double mn[MAXP], sd[MAXP], wzs[MAXP];
+#pragma unroll
+        for (int i = 0; i < MAXP; ++i) {
+            fnd[i] = false; mn[i] = 0.0; sd[i] = 0.0; wzs[i] = 0.0;
+            if ((uint32_t)i < p.m) {
+                double wx, wy;
+                world(p.c[i], wx, wy, wzs[i]);
+                if (p.c[i].eval) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MAXP; ++i) {
+            if ((uint32_t)i >= p.m) break;
+            contact((uint32_t)i, fnd[i], mn[i], sd[i], wzs[i]);
+        }
+    } else {
+        for (uint32_t i = 0; i < p.m; ++i) {
+            double wx, wy, wz, mean = 0.0, stdev = 0.0;
+            world(p.c[i], wx, wy, wz);
+            bool found = false;
+            if (group_valid && p.c[i].eval) found = lookup(wx, wy, wz, mean, stdev);
+            contact(i, found, mean, stdev, wz);
         }
     }
     r.ncp = ncp;
@@ -379,7 +415,7 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #define K1_OCCUPANCY
 #endif
 
-template <bool PROJECT, bool WEIGHT, int MAXP>
+template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH>
 __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState s0, DevState s1, MapView map, StepParams p,
                                                            Ctl* __restrict__ ctl, Shard* __restrict__ shards, GatherView gv)
 {
@@ -484,18 +520,26 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
         }
         if (WEIGHT) {
             double s, co;
+#ifdef ESLAM_ABL_NO_SINCOS
+            s = th * 1e-3; co = 1.0 - s;
+#else
             dm_sincos(th, &s, &co);
+#endif
             const double r22 = (1.0 - co) + co;
             const double meas_var = zs * zs + p.me2;
             if (meas_var == 0) err = 1;
-            const CMResult r = evaluate_pose<MAXP>(p, map, win, co, s, r22, x, y, z, meas_var);
+            const CMResult r = evaluate_pose<MAXP, BATCH>(p, map, win, co, s, r22, x, y, z, meas_var);
             double mprob;
             uint32_t floating;
             double sw = 0.0;
             if (r.accepted) {
                 // ContactModel::updateZPositionEstimate  src/ContactModel.cpp:319-340
                 double zvar = zs * zs;
+#ifdef ESLAM_ABL_NO_KALMAN
+                const double pose_var = r.posevar * 0.25;
+#else
                 const double pose_var = r.posevar / (double)r.ncp;
+#endif
                 const double a = zvar - pose_var;
                 double delta_var = (a < 1e-9) ? 1e-9 : a;
                 if (!(r.zdelta * r.zdelta > delta_var)) {
@@ -512,8 +556,9 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
                 maxm = (maxm < r.weight) ? r.weight : maxm;
                 nD += 1;
                 // pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found))
-                if (!p.use_shape || r.ncp == 0) sw = dm_pow(r.weight, 1.0 / (double)r.ncp);
-                else sw = r.weight == 0.0 ? 0.0 : dm_exp((-0.5 * r.s2) * (1.0 / (double)r.ncp));
+                const double inv_n = dm_recip_small(r.ncp);     // 1.0 / found, correctly rounded
+                if (!p.use_shape || r.ncp == 0) sw = dm_pow(r.weight, inv_n);
+                else sw = r.weight == 0.0 ? 0.0 : dm_exp((-0.5 * r.s2) * inv_n);
                 nTP += r.ncp;
             } else {
                 floating = 1;
@@ -872,21 +917,28 @@ struct DrawCursor {
     int shift;
     double dN;
     const uint32_t* jt;
+    uint64_t T;                          // T_k of the current draw (valid when k < N)
 
+    __device__ __forceinline__ uint64_t draw_T() const
+    {
+        return fx_shift(((double)k + dm_minstd_uniform(x)) / dN, shift);
+    }
     __device__ __forceinline__ void seek(uint64_t c)
     {
         k = count_draws_le(c, N, xs, shift, jt);
         x = k < N ? dm_mulmod31(jump_pow(jt, k + 1), xs) : 0u;
+        if (k < N) T = draw_T();
     }
-    // number of draws <= c (c >= the previous target): step, or jump after 16 steps
+    // number of draws <= c (c >= the previous target): step, or jump after 16 steps.
+    // The draw a call stops at is kept for the next call (each draw is evaluated once).
     __device__ __forceinline__ uint64_t advance(uint64_t c)
     {
         for (int steps = 0; k < N; ++steps) {
             if (steps == 16) { seek(c); break; }
-            const uint64_t T = fx_shift(((double)k + dm_minstd_uniform(x)) / dN, shift);
             if (T > c) break;
             ++k;
             x = dm_minstd_next(x);
+            if (k < N) T = draw_T();
         }
         return k;
     }
@@ -1085,7 +1137,7 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
 
     const uint64_t N = sp.n_global;
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
-    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt};
+    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt, 0};
     cur.seek(base);
     uint64_t lo = i0 == 0 ? 0 : cur.k;
     if (tid == 0) s_tm.L = lo;
@@ -1160,7 +1212,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     const uint64_t N = pp.n_global;
     const uint64_t W0 = pp.gbase[pp.rank], W1 = pp.gbase[pp.rank + 1];
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
-    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt};
+    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt, 0};
     cur.seek(base);
     uint64_t lo = i0 == 0 ? O0 : cur.k;
     // the tile's own-slice outputs: [clip(lo_first), clip(hi_last)) relative to W0
@@ -1484,16 +1536,18 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     if (blocks == 0) return hipSuccess;
     dim3 g(blocks), b(kBlock);
     const size_t lds = kStatsLds + (weight ? kWindowLds : 0);
-#define ESLAM_LAUNCH(P, W, M) hipLaunchKernelGGL((k_project_weight<P, W, M>), g, b, lds, stream, s0, s1, *map, *p, ctl, shards, *gv)
-    if (project && !weight) ESLAM_LAUNCH(true, false, 4);
+#define ESLAM_LAUNCH(P, W, M, B) \
+    hipLaunchKernelGGL((k_project_weight<P, W, M, B>), g, b, lds, stream, s0, s1, *map, *p, ctl, shards, *gv)
+    // batched contact lookups when every contact fits the MAXP-sized arrays
+    if (project && !weight) ESLAM_LAUNCH(true, false, 4, false);
     else if (!project && weight) {
-        if (maxp <= 4) ESLAM_LAUNCH(false, true, 4);
-        else if (maxp <= 8) ESLAM_LAUNCH(false, true, 8);
-        else ESLAM_LAUNCH(false, true, ESLAM_MAX_CONTACTS);
+        if (maxp <= 4) { if (p->m <= 4) ESLAM_LAUNCH(false, true, 4, true); else ESLAM_LAUNCH(false, true, 4, false); }
+        else if (maxp <= 8) { if (p->m <= 8) ESLAM_LAUNCH(false, true, 8, true); else ESLAM_LAUNCH(false, true, 8, false); }
+        else ESLAM_LAUNCH(false, true, ESLAM_MAX_CONTACTS, false);
     } else {
-        if (maxp <= 4) ESLAM_LAUNCH(true, true, 4);
-        else if (maxp <= 8) ESLAM_LAUNCH(true, true, 8);
-        else ESLAM_LAUNCH(true, true, ESLAM_MAX_CONTACTS);
+        if (maxp <= 4) { if (p->m <= 4) ESLAM_LAUNCH(true, true, 4, true); else ESLAM_LAUNCH(true, true, 4, false); }
+        else if (maxp <= 8) { if (p->m <= 8) ESLAM_LAUNCH(true, true, 8, true); else ESLAM_LAUNCH(true, true, 8, false); }
+        else ESLAM_LAUNCH(true, true, ESLAM_MAX_CONTACTS, false);
     }
 #undef ESLAM_LAUNCH
     return hipGetLastError();
