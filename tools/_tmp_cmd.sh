@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT
-bash tools/gpu_round.sh tests || exit 1
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/bench_k3c.log 2>&1
+bash tools/profile.sh r01c --steps 20 --warmup 5 > gpurun_out/profile_r01c.txt 2>&1 || exit 1
+bash tools/pmc.sh r01c --steps 5 --warmup 2 > gpurun_out/pmc_r01c.txt 2>&1
