@@ -462,6 +462,200 @@ DM_FN double dm_minstd_uniform(uint32_t x)
 }
 
 /* ------------------------------------------------------------------------------------ */
+/* SurfaceHash pieces (host and device)                                                  */
+/* ------------------------------------------------------------------------------------ */
+/* Buckets<T>::bucketIndex  src/SurfaceHash.hpp:25-29 (int truncation toward zero, clamp);
+ * NaN maps to bucket 0 (the reference's int cast of NaN is undefined)                    */
+DM_FN int dm_bucket_index(int count, double min_val, double max_val, double value)
+{
+    const double v = (value - min_val) / (max_val - min_val) * count;
+    if (!(v == v)) return 0;
+    int idx = v >= 2147483647.0 ? 2147483647 : (v <= -2147483648.0 ? (-2147483647 - 1) : (int)v);
+    int lo = idx > 0 ? idx : 0;
+    return (count - 1) < lo ? (count - 1) : lo;
+}
+
+/* SurfaceParam::fromPoints  src/SurfaceHash.hpp:60-110: the normal equations of the plane
+ * z = a x + b y + c solved by a pivoted LDL^T (Eigen::LDLT: the largest remaining
+ * diagonal entry as pivot).  P: n points (x, y, z).                                      */
+DM_FN void dm_surface_param(const double* P, uint32_t n, double* slope_x, double* slope_y)
+{
+    double x = 0, y = 0, z = 0, xx = 0, yy = 0, xy = 0, xz = 0, yz = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const double* p = P + 3 * i;
+        x += p[0]; y += p[1]; z += p[2];
+        xx += p[0] * p[0]; yy += p[1] * p[1]; xy += p[0] * p[1];
+        xz += p[0] * p[2]; yz += p[1] * p[2];
+    }
+    double A[3][3] = {{xx, xy, x}, {xy, yy, y}, {x, y, (double)n}};
+    double b[3] = {xz, yz, z};
+    int perm[3] = {0, 1, 2};
+    for (int k = 0; k < 3; ++k) {
+        int piv = k;
+        for (int i = k + 1; i < 3; ++i) if (dm_fabs(A[i][i]) > dm_fabs(A[piv][piv])) piv = i;
+        if (piv != k) {
+            int t = perm[k]; perm[k] = perm[piv]; perm[piv] = t;
+            for (int c = 0; c < 3; ++c) { double tmp = A[k][c]; A[k][c] = A[piv][c]; A[piv][c] = tmp; }
+            for (int r = 0; r < 3; ++r) { double tmp = A[r][k]; A[r][k] = A[r][piv]; A[r][piv] = tmp; }
+        }
+        for (int j = 0; j < k; ++j) A[k][k] -= A[k][j] * A[k][j] * A[j][j];
+        for (int i = k + 1; i < 3; ++i) {
+            double sum = A[i][k];
+            for (int j = 0; j < k; ++j) sum -= A[i][j] * A[k][j] * A[j][j];
+            A[i][k] = A[k][k] != 0.0 ? sum / A[k][k] : 0.0;
+        }
+    }
+    double r[3] = {b[perm[0]], b[perm[1]], b[perm[2]]};
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < i; ++j) r[i] -= A[i][j] * r[j];
+    for (int i = 0; i < 3; ++i) r[i] = A[i][i] != 0.0 ? r[i] / A[i][i] : 0.0;
+    for (int i = 2; i >= 0; --i) for (int j = i + 1; j < 3; ++j) r[i] -= A[j][i] * r[j];
+    double res[3];
+    for (int i = 0; i < 3; ++i) res[perm[i]] = r[i];
+    *slope_x = res[0];
+    *slope_y = res[1];
+}
+
+/* ContactModel::lowestPointHeuristic(false)  src/ContactModel.cpp:48-79: per group the
+ * lowest contact (ties: lowest index, std::sort of (z, index) pairs), ungrouped contacts
+ * as they are.  pos: m yaw-compensated positions.  Returns the number of points.        */
+DM_FN uint32_t dm_lowest_points(const double* pos, const int32_t* group, uint32_t m, double* out)
+{
+    uint32_t nlow = 0;
+    int first = -1, best = -1;
+    for (uint32_t i = 0; i < m; ++i) {
+        if (group[i] >= 0) {
+            if (first < 0) { first = (int)i; best = (int)i; }
+            else if (pos[3 * i + 2] < pos[3 * best + 2]) best = (int)i;
+        }
+        if (first < 0) {
+            out[3 * nlow] = pos[3 * i]; out[3 * nlow + 1] = pos[3 * i + 1]; out[3 * nlow + 2] = pos[3 * i + 2];
+            ++nlow;
+        } else if (i + 1 == m || group[i + 1] != group[i]) {
+            out[3 * nlow] = pos[3 * best]; out[3 * nlow + 1] = pos[3 * best + 1]; out[3 * nlow + 2] = pos[3 * best + 2];
+            ++nlow;
+            first = -1;
+        }
+    }
+    return nlow;
+}
+
+/* SurfaceHash::create  src/SurfaceHash.hpp:155-231, per (segment, cell).
+ * The grid view both sides use: cell (m, n) of index n * width + m; a cell's first
+ * patch mean is mean[cell_start[c] * mean_stride] (the device interleaves mean/stdev).   */
+typedef struct {
+    const uint32_t* cell_start;
+    const float* mean;
+    uint32_t mean_stride;
+    uint32_t width, height;
+    uint32_t bins;                       /* slopeBins */
+    double scale_x, scale_y, offset_x, offset_y, inv_scale_x, inv_scale_y;
+    double g2w[12];                      /* grid2world, 3x4 row-major */
+} dm_hash_grid;
+
+/* The template feet rotated for every angular segment (the reference rotates the points
+ * BEFORE using them, so segment a uses a + 1 rotations, applied cumulatively) and the
+ * segment's particle orientation a * 2 pi / steps + yaw_offset.  pts: steps x 4 x 2.     */
+DM_FN void dm_hash_segments(uint32_t steps, const double g2w[12], double* pts, double* orient)
+{
+    double p[4][2] = {{0.25, 0.0}, {-0.25, 0.0}, {0.25, -0.5}, {-0.25, -0.5}};   /* base = 0.5 */
+    double s, c;
+    dm_sincos(2.0 * 3.141592653589793 / (double)steps, &s, &c);   /* AngleAxisd(2 pi / steps, Z) */
+    const double r00 = 0.0 * 0.0 + c, r01 = 0.0 * 0.0 - s, r10 = 0.0 * 0.0 + s, r11 = 0.0 * 0.0 + c;
+    /* yaw of grid2world's rotation: atan2(R10, R00) (base::getYaw), restated on the matrix */
+    const double yx = __builtin_sqrt(g2w[10] * g2w[10] + g2w[9] * g2w[9]);
+    const double yaw = yx > 1e-12 ? __builtin_atan2(g2w[4], g2w[0]) : 0.0;
+    for (uint32_t a = 0; a < steps; ++a) {
+        for (int i = 0; i < 4; ++i) {
+            const double x = p[i][0], y = p[i][1];
+            p[i][0] = (r00 * x + r01 * y) + 0.0 * 0.0;
+            p[i][1] = (r10 * x + r11 * y) + 0.0 * 0.0;
+            pts[8 * a + 2 * i] = p[i][0];
+            pts[8 * a + 2 * i + 1] = p[i][1];
+        }
+        orient[a] = (((double)a * 2.0) * 3.141592653589793) / (double)steps + yaw;
+    }
+}
+
+/* one (segment, cell) of the sweep: returns the bucket (bx * bins + by) of the particle it
+ * makes, or -1 (fewer than 3 of the 4 feet on cells with patches); pose: x, y, theta, z.
+ * pts: this segment's 4 rotated feet.  Cell centre = (m + 1/2) scale + offset (fromGrid);
+ * a foot's cell = floor((v - offset) * (1/scale)), off-grid feet have no patch.          */
+DM_FN int dm_hash_item(const dm_hash_grid* g, const double* pts, double orient, uint32_t m, uint32_t n, double* pose)
+{
+    const double x = ((double)m + 0.5) * g->scale_x + g->offset_x;
+    const double y = ((double)n + 0.5) * g->scale_y + g->offset_y;
+    const double op[4][2] = {{0.25, 0.0}, {-0.25, 0.0}, {0.25, -0.5}, {-0.25, -0.5}};
+    double gp[12];
+    uint32_t cnt = 0;
+    double mean_z = 0.0;
+    for (int i = 0; i < 4; ++i) {
+        const double fm = dm_floor(((x + pts[2 * i]) - g->offset_x) * g->inv_scale_x);
+        const double fn = dm_floor(((y + pts[2 * i + 1]) - g->offset_y) * g->inv_scale_y);
+        if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
+        const uint64_t cell = (uint64_t)fn * g->width + (uint64_t)fm;
+        const uint32_t b = g->cell_start[cell], e = g->cell_start[cell + 1];
+        if (e <= b) continue;
+        const double zval = (double)g->mean[(uint64_t)b * g->mean_stride];
+        mean_z += zval;
+        gp[3 * cnt] = op[i][0] + 0.0;
+        gp[3 * cnt + 1] = op[i][1] + 0.0;
+        gp[3 * cnt + 2] = 0.0 + zval;
+        ++cnt;
+    }
+    if (cnt < 3) return -1;
+    mean_z /= (double)cnt;
+    double sx, sy;
+    dm_surface_param(gp, cnt, &sx, &sy);
+    const int bx = dm_bucket_index((int)g->bins, -1.0, 1.0, sx);
+    const int by = dm_bucket_index((int)g->bins, -1.0, 1.0, sy);
+    const double* G = g->g2w;
+    pose[0] = ((G[0] * x + G[1] * y) + G[2] * mean_z) + G[3];
+    pose[1] = ((G[4] * x + G[5] * y) + G[6] * mean_z) + G[7];
+    pose[2] = orient;
+    pose[3] = (((G[8] * x + G[9] * y) + G[10] * mean_z) + G[11]) + 0.18;
+    return bx * (int)g->bins + by;
+}
+
+/* inverse of a rigid 3x4 affine [R | t]: [R^T | -R^T t] (global2local -> grid2world) */
+DM_FN void dm_affine_inverse(const double A[12], double out[12])
+{
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) out[4 * r + c] = A[4 * c + r];
+        out[4 * r + 3] = -((A[r] * A[3] + A[4 + r] * A[7]) + A[8 + r] * A[11]);
+    }
+}
+
+/* glibc rand() (random_r TYPE_3: r_i = r_{i-3} + r_{i-31}, output r_i >> 1), the
+ * generator behind the reference's unseeded rand() (seed 1) in SurfaceHash::sample.
+ * One state per filter (the reference's is process-global).                              */
+typedef struct { uint32_t r[34]; uint32_t i; uint32_t pad; } dm_libc_rand_state;
+
+DM_FN void dm_libc_srand(dm_libc_rand_state* st, uint32_t seed)
+{
+    int32_t r[344];
+    r[0] = (int32_t)(seed ? seed : 1u);
+    for (int i = 1; i < 31; ++i) {
+        const int64_t v = (16807ll * r[i - 1]) % 2147483647ll;
+        r[i] = (int32_t)(v < 0 ? v + 2147483647ll : v);
+    }
+    for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+    for (int i = 34; i < 344; ++i) r[i] = (int32_t)((uint32_t)r[i - 31] + (uint32_t)r[i - 3]);
+    for (int k = 0; k < 34; ++k) st->r[k] = (uint32_t)r[310 + k];
+    st->i = 0;
+    st->pad = 0;
+}
+
+DM_FN int32_t dm_libc_rand(dm_libc_rand_state* st)
+{
+    /* ring of the last 34 values: slot i holds r_{t-34} (t = the next index) */
+    const uint32_t i = st->i;
+    const uint32_t v = st->r[(i + 3) % 34] + st->r[(i + 31) % 34];   /* r_{t-31} + r_{t-3} */
+    st->r[i] = v;
+    st->i = (i + 1) % 34;
+    return (int32_t)(v >> 1);
+}
+
+/* ------------------------------------------------------------------------------------ */
 /* exact fixed-point helpers (order-independent sums)                                    */
 /* ------------------------------------------------------------------------------------ */
 /* trunc(v * 2^shift) for the resample cumulative sum: v >= 0 finite; saturates at 2^62-1

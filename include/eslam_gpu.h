@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 1
+#define ESLAM_ABI_VERSION 2
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -216,9 +216,28 @@ typedef struct eslam_rng_state {
     uint64_t hash_count;
     double max_weight;                     /* PoseEstimator::max_weight                      */
     double ud_pose[12];                    /* EmbodiedSlamFilter::udPose, 3x4 row-major      */
+    uint32_t libc_rand[34];                /* SurfaceHash::sample's rand() (glibc TYPE_3)    */
+    uint32_t libc_rand_pos;
+    uint32_t pad2;
 } eslam_rng_state;
 int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st);
 int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st);
+
+/* ---- SurfaceHash (useHash = true): pose hash of the map by terrain slope ----------------
+ * SurfaceHash::create  src/SurfaceHash.hpp:155-231 on the map of eslam_gpu_set_map, with
+ * the config's hash_slope_bins / hash_angular_steps (a sweep over segments x cells on the
+ * GPU).  eslam_gpu_init_pose builds it on demand when config.hash_use is set and then
+ * initialises from it (PoseEstimator::init(N, hash) src/PoseEstimator.cpp:75-86); with
+ * hash_use, every hash_period-th project (starting with the first) runs sampleFromHash
+ * (src/PoseEstimator.cpp:130-182, 238-240).  rand() is glibc's generator seeded with 1
+ * (the reference never seeds it), one state per context.                                  */
+int eslam_gpu_hash_create(eslam_ctx* ctx);
+/* PoseEstimator::init(N, hash): particle i = a uniformly drawn hash pose                   */
+int eslam_gpu_init_hash(eslam_ctx* ctx, uint64_t n);
+/* number of hash poses; bucket_sizes (slope_bins^2 entries, bucket = bx * bins + by) or NULL */
+int eslam_gpu_hash_info(eslam_ctx* ctx, uint64_t* n_poses, uint32_t* bucket_sizes);
+/* the hash poses in sweep order (x, y, theta, z) and their buckets; any pointer may be NULL */
+int eslam_gpu_hash_poses(eslam_ctx* ctx, double* x, double* y, double* theta, double* z, int32_t* bucket);
 
 /* ---- multi-GPU: one context per GPU holds a contiguous shard of ONE global filter -------
  * The library is transport-agnostic: it calls the collectives below at the three exchange

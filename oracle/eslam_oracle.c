@@ -413,52 +413,16 @@ void or_cm_update_contact_state_lph(or_contact_model* cm) { lowest_point_heurist
 /* ========================================================================================
  * SurfaceHash pieces
  * ====================================================================================== */
-/* Buckets<T>::bucketIndex  src/SurfaceHash.hpp:25-29 */
+/* Buckets<T>::bucketIndex  src/SurfaceHash.hpp:25-29 (dm_bucket_index) */
 int or_bucket_index(int count, double min_val, double max_val, double value)
 {
-    int idx = (int)((value - min_val) / (max_val - min_val) * count);
-    int lo = idx > 0 ? idx : 0;
-    return (count - 1) < lo ? (count - 1) : lo;
+    return dm_bucket_index(count, min_val, max_val, value);
 }
 
-/* SurfaceParam::fromPoints  src/SurfaceHash.hpp:60-110: normal equations solved by a
- * pivoted LDL^T (Eigen::LDLT: largest remaining diagonal as pivot)                       */
+/* SurfaceParam::fromPoints  src/SurfaceHash.hpp:60-110 (dm_surface_param: pivoted LDL^T) */
 void or_surface_param_from_points(const double* P, uint32_t n, double* slope_x, double* slope_y)
 {
-    double x = 0, y = 0, z = 0, xx = 0, yy = 0, xy = 0, xz = 0, yz = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const double* p = P + 3 * i;
-        x += p[0]; y += p[1]; z += p[2];
-        xx += p[0] * p[0]; yy += p[1] * p[1]; xy += p[0] * p[1];
-        xz += p[0] * p[2]; yz += p[1] * p[2];
-    }
-    double A[3][3] = {{xx, xy, x}, {xy, yy, y}, {x, y, (double)n}};
-    double b[3] = {xz, yz, z};
-    int perm[3] = {0, 1, 2};
-    /* in-place pivoted LDL^T */
-    for (int k = 0; k < 3; ++k) {
-        int piv = k;
-        for (int i = k + 1; i < 3; ++i) if (fabs(A[i][i]) > fabs(A[piv][piv])) piv = i;
-        if (piv != k) {
-            int t = perm[k]; perm[k] = perm[piv]; perm[piv] = t;
-            for (int c = 0; c < 3; ++c) { double tmp = A[k][c]; A[k][c] = A[piv][c]; A[piv][c] = tmp; }
-            for (int r = 0; r < 3; ++r) { double tmp = A[r][k]; A[r][k] = A[r][piv]; A[r][piv] = tmp; }
-        }
-        for (int j = 0; j < k; ++j) A[k][k] -= A[k][j] * A[k][j] * A[j][j];
-        for (int i = k + 1; i < 3; ++i) {
-            double s = A[i][k];
-            for (int j = 0; j < k; ++j) s -= A[i][j] * A[k][j] * A[j][j];
-            A[i][k] = A[k][k] != 0.0 ? s / A[k][k] : 0.0;
-        }
-    }
-    double r[3] = {b[perm[0]], b[perm[1]], b[perm[2]]};
-    for (int i = 0; i < 3; ++i) for (int j = 0; j < i; ++j) r[i] -= A[i][j] * r[j];
-    for (int i = 0; i < 3; ++i) r[i] = A[i][i] != 0.0 ? r[i] / A[i][i] : 0.0;
-    for (int i = 2; i >= 0; --i) for (int j = i + 1; j < 3; ++j) r[i] -= A[j][i] * r[j];
-    double res[3];
-    for (int i = 0; i < 3; ++i) res[perm[i]] = r[i];
-    *slope_x = res[0];
-    *slope_y = res[1];
+    dm_surface_param(P, n, slope_x, slope_y);
 }
 
 /* ========================================================================================
@@ -492,6 +456,14 @@ struct or_filter {
     eslam_update_info info;
     uint32_t* anc;
     int has_anc;
+    /* SurfaceHash (useHash): poses in sweep order, bucket lists (stable counting sort) */
+    int has_hash;
+    uint64_t hash_n;
+    double *hash_x, *hash_y, *hash_th, *hash_z;
+    int32_t* hash_bucket;
+    uint32_t* hash_bstart;               /* bins^2 + 1 */
+    uint32_t* hash_blist;
+    dm_libc_rand_state libc;             /* rand() of SurfaceHash::sample (glibc, seed 1) */
     /* sharded mode (or_set_comm): this filter is shard [gbase, gbase + n) of n_global */
     int sharded;
     eslam_comm comm;
@@ -541,6 +513,7 @@ or_filter* or_create(const eslam_config* cfg, int sum_mode)
     f->cfg = *cfg;
     f->sum_mode = sum_mode;
     f->minstd = dm_minstd_seed(cfg->seed);      /* ParticleFilter(seed) src/ParticleFilter.hpp:24-27 */
+    dm_libc_srand(&f->libc, 1);                 /* the reference never calls srand() */
     f->max_weight = 0;                          /* src/PoseEstimator.cpp:13-25 */
     f->zcomp[0] = 1.0;
     f->wexp = 1;
@@ -553,6 +526,8 @@ void or_destroy(or_filter* f)
     if (!f) return;
     or_free_particles(f);
     free(f->map_cells); free(f->map_mean); free(f->map_stdev); free(f->map_height);
+    free(f->hash_x); free(f->hash_y); free(f->hash_th); free(f->hash_z); free(f->hash_bucket);
+    free(f->hash_bstart); free(f->hash_blist);
     free(f);
 }
 
@@ -619,7 +594,13 @@ int or_init_pose(or_filter* f, const double pos[3], const double q[4])
                     f->cfg.initial_rotation_error[2]};
     uint64_t n = f->cfg.particle_count;
     if (f->sharded) n = f->gall[f->comm.rank + 1] - f->gall[f->comm.rank];
-    int rc = or_init_gaussian(f, n, mu, sg, pos[2], f->cfg.initial_translation_error[2] + 1e-3);
+    int rc;
+    if (f->cfg.hash_use) {                 /* hash.create(gridTemplate); filter.init(N, &hash) */
+        rc = f->has_hash ? 0 : or_hash_create(f);
+        if (!rc) rc = or_init_hash(f, n);
+    } else {
+        rc = or_init_gaussian(f, n, mu, sg, pos[2], f->cfg.initial_translation_error[2] + 1e-3);
+    }
     set_translation_pose(f->ud_pose, 1000, 0, 0);
     return rc;
 }
@@ -696,6 +677,164 @@ static void or_prepare(const eslam_step_input* in, or_prep* p)
     lower_cholesky(in->sample_cov, p->L);
 }
 
+
+/* ---- SurfaceHash  src/SurfaceHash.hpp:155-231 --------------------------------------------- */
+static void hash_grid_view(const or_filter* f, dm_hash_grid* g)
+{
+    memset(g, 0, sizeof(*g));
+    g->cell_start = f->map.cell_start;
+    g->mean = f->map.patch_mean;
+    g->mean_stride = 1;
+    g->width = f->map.width;
+    g->height = f->map.height;
+    g->bins = (uint32_t)f->cfg.hash_slope_bins;
+    g->scale_x = f->map.scale_x; g->scale_y = f->map.scale_y;
+    g->offset_x = f->map.offset_x; g->offset_y = f->map.offset_y;
+    g->inv_scale_x = 1.0 / f->map.scale_x; g->inv_scale_y = 1.0 / f->map.scale_y;
+    dm_affine_inverse(f->map.global2local, g->g2w);
+}
+
+int or_hash_create(or_filter* f)
+{
+    if (!f->has_map) return ESLAM_ERR_NO_MLS_GRID;
+    free(f->hash_x); free(f->hash_y); free(f->hash_th); free(f->hash_z); free(f->hash_bucket);
+    free(f->hash_bstart); free(f->hash_blist);
+    dm_hash_grid g;
+    hash_grid_view(f, &g);
+    const uint32_t steps = (uint32_t)f->cfg.hash_angular_steps, bins = g.bins;
+    double* pts = malloc(sizeof(double) * 8 * (steps ? steps : 1));
+    double* orient = malloc(sizeof(double) * (steps ? steps : 1));
+    dm_hash_segments(steps, g.g2w, pts, orient);
+    uint64_t cap = 1024, n = 0;
+    f->hash_x = malloc(cap * 8); f->hash_y = malloc(cap * 8); f->hash_th = malloc(cap * 8); f->hash_z = malloc(cap * 8);
+    f->hash_bucket = malloc(cap * 4);
+    for (uint32_t a = 0; a < steps; ++a)
+        for (uint32_t m = 0; m < g.width; ++m)
+            for (uint32_t nn = 0; nn < g.height; ++nn) {
+                double pose[4];
+                const int b = dm_hash_item(&g, pts + 8 * a, orient[a], m, nn, pose);
+                if (b < 0) continue;
+                if (n == cap) {
+                    cap *= 2;
+                    f->hash_x = realloc(f->hash_x, cap * 8); f->hash_y = realloc(f->hash_y, cap * 8);
+                    f->hash_th = realloc(f->hash_th, cap * 8); f->hash_z = realloc(f->hash_z, cap * 8);
+                    f->hash_bucket = realloc(f->hash_bucket, cap * 4);
+                }
+                f->hash_x[n] = pose[0]; f->hash_y[n] = pose[1]; f->hash_th[n] = pose[2]; f->hash_z[n] = pose[3];
+                f->hash_bucket[n] = b;
+                ++n;
+            }
+    free(pts); free(orient);
+    const uint32_t nb = bins * bins;
+    f->hash_bstart = calloc(nb + 1, 4);
+    for (uint64_t i = 0; i < n; ++i) f->hash_bstart[f->hash_bucket[i] + 1]++;
+    for (uint32_t b = 0; b < nb; ++b) f->hash_bstart[b + 1] += f->hash_bstart[b];
+    f->hash_blist = malloc((n ? n : 1) * 4);
+    uint32_t* fill = malloc((nb ? nb : 1) * 4);
+    memcpy(fill, f->hash_bstart, nb * 4);
+    for (uint64_t i = 0; i < n; ++i) f->hash_blist[fill[f->hash_bucket[i]]++] = (uint32_t)i;   /* sweep order */
+    free(fill);
+    f->hash_n = n;
+    f->has_hash = 1;
+    return 0;
+}
+
+uint64_t or_hash_info(or_filter* f, uint32_t* bucket_sizes)
+{
+    if (!f->has_hash) return 0;
+    const uint32_t nb = (uint32_t)f->cfg.hash_slope_bins * (uint32_t)f->cfg.hash_slope_bins;
+    if (bucket_sizes)
+        for (uint32_t b = 0; b < nb; ++b) bucket_sizes[b] = f->hash_bstart[b + 1] - f->hash_bstart[b];
+    return f->hash_n;
+}
+
+int or_hash_poses(or_filter* f, double* x, double* y, double* th, double* z, int32_t* bucket)
+{
+    if (!f->has_hash) return ESLAM_ERR_NOT_INITIALISED;
+    const uint64_t n = f->hash_n;
+    if (x) memcpy(x, f->hash_x, n * 8);
+    if (y) memcpy(y, f->hash_y, n * 8);
+    if (th) memcpy(th, f->hash_th, n * 8);
+    if (z) memcpy(z, f->hash_z, n * 8);
+    if (bucket) memcpy(bucket, f->hash_bucket, n * 4);
+    return 0;
+}
+
+/* PoseEstimator::init(N, hash)  src/PoseEstimator.cpp:75-86: particle i = poses[rand() %
+ * size]; PoseParticle(position, orientation, zPos) defaults: zSigma 0, weight 0, floating
+ * (mprob is uninitialised in the reference; 0 here) */
+int or_init_hash(or_filter* f, uint64_t n)
+{
+    if (!f->has_hash || f->hash_n == 0) return ESLAM_ERR_HASH_SAMPLE;
+    int rc = or_alloc_particles(f, n);
+    if (rc) return rc;
+    const uint64_t skip = f->gbase, total = f->sharded ? f->n_global : n;
+    for (uint64_t g = 0; g < total; ++g) {
+        const uint32_t idx = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&f->libc) % f->hash_n);
+        if (g < skip || g >= skip + n) continue;
+        const uint64_t i = g - skip;
+        f->x[i] = f->hash_x[idx]; f->y[i] = f->hash_y[idx]; f->th[i] = f->hash_th[idx]; f->z[i] = f->hash_z[idx];
+        f->zs[i] = 0.0; f->w[i] = 0.0; f->mprob[i] = 0.0; f->floating[i] = 1; f->ncp[i] = 0;
+    }
+    f->wexp = 1;
+    return 0;
+}
+
+typedef struct { float w; uint32_t i; } or_widx;
+
+static int widx_cmp(const void* a, const void* b)
+{
+    const or_widx* x = (const or_widx*)a;
+    const or_widx* y = (const or_widx*)b;
+    if (x->w < y->w) return -1;
+    if (y->w < x->w) return 1;
+    return x->i < y->i ? -1 : (x->i > y->i);
+}
+
+/* PoseEstimator::sampleFromHash  src/PoseEstimator.cpp:130-182 */
+static void sample_from_hash(or_filter* f, const eslam_step_input* in)
+{
+    /* contactModel.setContactPoints + getLowestPointPerGroup: yaw-compensated feet */
+    double pos[ESLAM_MAX_CONTACTS * 3], low[ESLAM_MAX_CONTACTS * 3];
+    int32_t grp[ESLAM_MAX_CONTACTS];
+    const uint32_t m = in->n_contacts < ESLAM_MAX_CONTACTS ? in->n_contacts : ESLAM_MAX_CONTACTS;
+    for (uint32_t i = 0; i < m; ++i) {
+        q_rotate(f->zcomp, in->contacts[i].position, pos + 3 * i);
+        grp[i] = in->contacts[i].group_id;
+    }
+    const uint32_t nlow = dm_lowest_points(pos, grp, m, low);
+    double sx, sy;
+    dm_surface_param(low, nlow, &sx, &sy);
+    const int bins = (int)f->cfg.hash_slope_bins;
+    const int b = dm_bucket_index(bins, -1.0, 1.0, sx) * bins + dm_bucket_index(bins, -1.0, 1.0, sy);
+    const uint32_t bsize = f->hash_bstart[b + 1] - f->hash_bstart[b];
+    const double rel = dm_pow(1.0 - 1.0 * (double)bsize / (double)f->hash_n, 3.0);
+    const uint64_t N = NG(f);
+    uint64_t k = (uint64_t)(((double)N * f->cfg.hash_percentage) * rel);
+    if (rel < 0.8) k = 0;
+    if (k > N) k = N;
+    if (k == 0 || bsize == 0) return;      /* nothing replaced, no rand() drawn */
+    const double weight = ((or_get_weights_sum(f) / (double)N) * f->cfg.hash_avg_factor) * rel;
+    or_widx* wi = malloc(sizeof(or_widx) * f->n);
+    for (uint64_t i = 0; i < f->n; ++i) {
+        float wf = (float)f->w[i];
+        if (wf == 0.0f) wf = 0.0f;                /* -0 and +0 compare equal */
+        wi[i].w = wf;
+        wi[i].i = (uint32_t)i;
+    }
+    qsort(wi, f->n, sizeof(or_widx), widx_cmp);
+    for (uint64_t j = 0; j < k; ++j) {
+        const uint32_t draw = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&f->libc) % bsize);
+        const uint32_t src = f->hash_blist[f->hash_bstart[b] + draw];
+        const uint32_t i = wi[j].i;
+        f->x[i] = f->hash_x[src]; f->y[i] = f->hash_y[src]; f->th[i] = f->hash_th[src]; f->z[i] = f->hash_z[src];
+        f->zs[i] = 0.5;
+        f->floating[i] = 1;
+        f->w[i] = weight;
+    }
+    free(wi);
+}
+
 /* ---- project  src/PoseEstimator.cpp:184-242 --------------------------------------------- */
 int or_project(or_filter* f, const eslam_step_input* in)
 {
@@ -743,7 +882,12 @@ int or_project(or_filter* f, const eslam_step_input* in)
         }
     }
     f->project_count++;
-    /* hash respawn (useHash) is not modelled here yet (next) */
+    /* the static counter of src/PoseEstimator.cpp:239 (per filter here, Q11): the hash
+     * respawn runs on the first project and every period-th after it */
+    if (c->hash_use && f->has_hash) {
+        const uint64_t period = c->hash_period ? c->hash_period : 1;
+        if ((f->hash_count++ % period) == 0) sample_from_hash(f, in);
+    }
     return 0;
 }
 
@@ -1310,6 +1454,8 @@ void or_get_rng_state(or_filter* f, eslam_rng_state* st)
     st->hash_count = f->hash_count;
     st->max_weight = f->max_weight;
     memcpy(st->ud_pose, f->ud_pose, sizeof(f->ud_pose));
+    memcpy(st->libc_rand, f->libc.r, sizeof(st->libc_rand));
+    st->libc_rand_pos = f->libc.i;
 }
 
 void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
@@ -1320,6 +1466,8 @@ void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
     f->hash_count = st->hash_count;
     f->max_weight = st->max_weight;
     memcpy(f->ud_pose, st->ud_pose, sizeof(f->ud_pose));
+    memcpy(f->libc.r, st->libc_rand, sizeof(st->libc_rand));
+    f->libc.i = st->libc_rand_pos % 34u;
 }
 
 int or_get_debug(or_filter* f, uint32_t* ncp, or_cpoint* cp, double* zdelta, double* zvar)
@@ -1368,6 +1516,13 @@ void or_dm_philox_raw(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t 
     memcpy(c.v, ctr, 16);
     c = dm_philox4x32_10(c, k0, k1);
     memcpy(out, c.v, 16);
+}
+
+void or_dm_libc_rand(uint32_t seed, uint32_t n, int32_t* out)
+{
+    dm_libc_rand_state st;
+    dm_libc_srand(&st, seed);
+    for (uint32_t i = 0; i < n; ++i) out[i] = dm_libc_rand(&st);
 }
 
 uint32_t or_dm_minstd_jump(uint32_t x, uint64_t n) { return dm_mulmod31(dm_minstd_pow(n), x); }

@@ -83,6 +83,12 @@ int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean, 
 /* ---- the filter (PoseEstimator + EmbodiedSlamFilter) -------------------------------------- */
 typedef struct or_filter or_filter;
 
+/* SurfaceHash (useHash): create from the filter's map, PoseEstimator::init(N, hash) */
+int or_hash_create(or_filter* f);
+int or_init_hash(or_filter* f, uint64_t n);
+uint64_t or_hash_info(or_filter* f, uint32_t* bucket_sizes);
+int or_hash_poses(or_filter* f, double* x, double* y, double* th, double* z, int32_t* bucket);
+
 or_filter* or_create(const eslam_config* cfg, int sum_mode);
 void or_destroy(or_filter* f);
 int or_set_map(or_filter* f, const eslam_mls_grid* g);            /* copies the grid */
@@ -116,6 +122,7 @@ double or_dm(int fn, double x, double y);
 void or_dm_philox(uint64_t seed, uint32_t stream, uint64_t ev, uint64_t gidx, uint32_t call, uint32_t out[4]);
 void or_dm_philox_raw(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
 uint32_t or_dm_minstd_jump(uint32_t x, uint64_t n);
+void or_dm_libc_rand(uint32_t seed, uint32_t n, int32_t* out);     /* glibc rand() after srand(seed) */
 double or_dm_limbs_to_double(const uint64_t L[4], int scale);
 void or_dm_fx128(double v, int scale, uint32_t limbs[4]);
 

@@ -20,7 +20,7 @@ LIB = os.path.join(OUT_DIR, "libeslam_gpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ESLAM_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["eslam_kernels.hip", "eslam_ctx.hip"]
+SOURCES = ["eslam_kernels.hip", "eslam_hash.hip", "eslam_ctx.hip"]
 HEADERS = [os.path.join(CSRC, "eslam_internal.h"), os.path.join(ROOT, "include", "eslam_gpu.h"),
            os.path.join(ROOT, "include", "eslam_detmath.h")]
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",

@@ -43,6 +43,19 @@ extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, cons
 extern "C" hipError_t eslam_launch_expand(const void* recv, uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* row_first,
                                           hipStream_t stream);
 extern "C" uint64_t eslam_record_bytes(void);
+extern "C" hipError_t eslam_launch_hash_sweep(const dm_hash_grid* g, const double* pts, const double* orient, uint32_t steps,
+                                              int32_t* out, hipStream_t stream);
+extern "C" hipError_t eslam_launch_hash_poses(const dm_hash_grid* g, const double* pts, const double* orient, const uint64_t* ids,
+                                              uint64_t count, double* hx, double* hy, double* hth, double* hz,
+                                              hipStream_t stream);
+extern "C" hipError_t eslam_launch_init_from_hash(DevState s0, const uint32_t* idx, uint64_t n, const double* hx,
+                                                  const double* hy, const double* hth, const double* hz, hipStream_t stream);
+extern "C" hipError_t eslam_hash_sort(DevState s0, DevState s1, const Ctl* ctl, uint64_t n, uint32_t* keys, uint32_t* vals,
+                                      uint32_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes, hipStream_t stream);
+extern "C" hipError_t eslam_launch_hash_replace(DevState s0, DevState s1, const Ctl* ctl, const uint32_t* order,
+                                                const uint32_t* draws, uint64_t k, const uint32_t* blist, uint32_t bstart,
+                                                const double* hx, const double* hy, const double* hth, const double* hz,
+                                                double weight, hipStream_t stream);
 extern "C" hipError_t eslam_launch_init_gaussian(DevState s0, uint64_t n, uint64_t gbase, uint64_t seed, uint64_t ev,
                                                  const double mu[3], const double sigma[3], double zpos, double zsigma,
                                                  hipStream_t stream);
@@ -235,6 +248,21 @@ struct eslam_ctx {
     void* sendbuf = nullptr; uint64_t send_cap = 0;
     void* recvbuf = nullptr; uint64_t recv_cap = 0;
     void* stage = nullptr; uint64_t stage_cap = 0;   // pinned staging (host-memory comm)
+    // SurfaceHash (useHash)
+    double map_scale[2] = {1, 1};
+    bool has_hash = false;
+    uint64_t hash_n = 0;
+    double* d_hash = nullptr;                // 4 x hash_n: x, y, theta, z
+    uint32_t* d_hash_blist = nullptr;        // pose indices grouped by bucket, sweep order
+    std::vector<uint32_t> hash_bstart;       // bins^2 + 1
+    std::vector<int32_t> hash_bucket;        // per pose (sweep order)
+    dm_libc_rand_state libc;                 // rand() of SurfaceHash::sample (glibc, seed 1)
+    uint32_t* d_sort = nullptr;              // keys, vals, keys_out, order (4 x cap)
+    uint64_t sort_cap = 0;
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    uint32_t* d_draws = nullptr;
+    uint64_t draws_cap = 0;
     // diagnostics
     std::string err;
     bool timing = false;
@@ -371,6 +399,7 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
         hipMemset(ctx->shards, 0, sizeof(Shard) * kNShard);
         memset(ctx->ctl_host, 0, sizeof(Ctl));
         ctx->ctl_host->minstd = dm_minstd_seed(cfg->seed);     // ParticleFilter(seed)
+        dm_libc_srand(&ctx->libc, 1);                            // the reference never seeds rand()
         ctx->ctl_host->max_weight = 0.0;                         // PoseEstimator ctor
         ctx->ctl_host->wexp = 1;
         ctx->ctl_host->scan_shift = 60;
@@ -427,6 +456,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     hipFree(ctx->scratch); hipHostFree(ctx->scratch_host);
     hipFree(ctx->rec_local); hipFree(ctx->recs); hipFree(ctx->mg); hipHostFree(ctx->mg_host);
     hipFree(ctx->sendbuf); hipFree(ctx->recvbuf); hipHostFree(ctx->stage);
+    hipFree(ctx->d_hash); hipFree(ctx->d_hash_blist); hipFree(ctx->d_sort); hipFree(ctx->sort_tmp); hipFree(ctx->d_draws);
     for (auto& e : ctx->ev) if (e) hipEventDestroy(e);
     for (auto& e : ctx->ring) if (e) hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
@@ -624,6 +654,9 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
     m.height_cells = g->height;
     m.inv_scale_x = 1.0 / g->scale_x;
     m.inv_scale_y = 1.0 / g->scale_y;
+    ctx->map_scale[0] = g->scale_x;
+    ctx->map_scale[1] = g->scale_y;
+    ctx->has_hash = false;                   // a new map invalidates the pose hash
     m.offset_x = g->offset_x;
     m.offset_y = g->offset_y;
     memcpy(m.g2l, g->global2local, sizeof(m.g2l));
@@ -677,9 +710,158 @@ extern "C" int eslam_gpu_init_pose(eslam_ctx* ctx, const double pos[3], const do
         if (n != ctx->n_global) return fail(ctx, ESLAM_ERR_INVALID_ARG, "sharded context: particle_count must be n_global");
         n = ctx->gall[ctx->comm.rank + 1] - ctx->gall[ctx->comm.rank];
     }
-    const int rc = eslam_gpu_init_gaussian(ctx, n, mu, sg, pos[2], ctx->cfg.initial_translation_error[2] + 1e-3);
+    int rc;
+    if (ctx->cfg.hash_use) {                   // hash.create(gridTemplate); filter.init(N, &hash)
+        rc = ctx->has_hash ? ESLAM_OK : eslam_gpu_hash_create(ctx);
+        if (!rc) rc = eslam_gpu_init_hash(ctx, n);
+    } else {
+        rc = eslam_gpu_init_gaussian(ctx, n, mu, sg, pos[2], ctx->cfg.initial_translation_error[2] + 1e-3);
+    }
     set_translation_pose(ctx->ud_pose, 1000, 0, 0);
     return rc;
+}
+
+// ---------------------------------------------------------------------------------------
+// SurfaceHash (src/SurfaceHash.hpp:155-231, src/PoseEstimator.cpp:75-86, 130-182)
+// ---------------------------------------------------------------------------------------
+static dm_hash_grid hash_grid(eslam_ctx* ctx)
+{
+    dm_hash_grid g;
+    memset(&g, 0, sizeof(g));
+    g.cell_start = ctx->d_cells;
+    g.mean = reinterpret_cast<const float*>(ctx->d_patch);   // float2 {mean, stdev}
+    g.mean_stride = 2;
+    g.width = ctx->map.width;
+    g.height = ctx->map.height_cells;
+    g.bins = (uint32_t)ctx->cfg.hash_slope_bins;
+    g.scale_x = ctx->map_scale[0];
+    g.scale_y = ctx->map_scale[1];
+    g.offset_x = ctx->map.offset_x;
+    g.offset_y = ctx->map.offset_y;
+    g.inv_scale_x = ctx->map.inv_scale_x;
+    g.inv_scale_y = ctx->map.inv_scale_y;
+    dm_affine_inverse(ctx->map.g2l, g.g2w);
+    return g;
+}
+
+extern "C" int eslam_gpu_hash_create(eslam_ctx* ctx)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
+    const uint32_t steps = (uint32_t)ctx->cfg.hash_angular_steps, bins = (uint32_t)ctx->cfg.hash_slope_bins;
+    if (steps == 0 || bins == 0 || bins > 4096) return fail(ctx, ESLAM_ERR_INVALID_ARG, "hash_angular_steps / hash_slope_bins");
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const dm_hash_grid g = hash_grid(ctx);
+    std::vector<double> pts(8 * steps), orient(steps);
+    dm_hash_segments(steps, g.g2w, pts.data(), orient.data());
+    const uint64_t cells = (uint64_t)g.width * g.height, total = cells * steps;
+    double* d_seg = nullptr;
+    int32_t* d_out = nullptr;
+    uint64_t* d_ids = nullptr;
+    std::vector<int32_t> out(total);
+    int rc = ESLAM_OK;
+    do {
+        if (hipMalloc(&d_seg, sizeof(double) * 9 * steps) != hipSuccess ||
+            hipMalloc(&d_out, sizeof(int32_t) * (total ? total : 1)) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "hash sweep buffers");
+            break;
+        }
+        hipMemcpy(d_seg, pts.data(), sizeof(double) * 8 * steps, hipMemcpyHostToDevice);
+        hipMemcpy(d_seg + 8 * steps, orient.data(), sizeof(double) * steps, hipMemcpyHostToDevice);
+        if (eslam_launch_hash_sweep(&g, d_seg, d_seg + 8 * steps, steps, d_out, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(out.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_HIP, "hash sweep");
+            break;
+        }
+        // compact in sweep order; bucket lists by a stable counting sort
+        std::vector<uint64_t> ids;
+        ctx->hash_bucket.clear();
+        for (uint64_t id = 0; id < total; ++id)
+            if (out[id] >= 0) { ids.push_back(id); ctx->hash_bucket.push_back(out[id]); }
+        const uint64_t n = ids.size();
+        const uint32_t nb = bins * bins;
+        ctx->hash_bstart.assign(nb + 1, 0);
+        for (uint64_t i = 0; i < n; ++i) ctx->hash_bstart[ctx->hash_bucket[i] + 1]++;
+        for (uint32_t b = 0; b < nb; ++b) ctx->hash_bstart[b + 1] += ctx->hash_bstart[b];
+        std::vector<uint32_t> blist(n ? n : 1), fill(ctx->hash_bstart.begin(), ctx->hash_bstart.end() - 1);
+        for (uint64_t i = 0; i < n; ++i) blist[fill[ctx->hash_bucket[i]]++] = (uint32_t)i;
+        hipFree(ctx->d_hash); ctx->d_hash = nullptr;
+        hipFree(ctx->d_hash_blist); ctx->d_hash_blist = nullptr;
+        const uint64_t cap = n ? n : 1;
+        if (hipMalloc(&ctx->d_hash, sizeof(double) * 4 * cap) != hipSuccess ||
+            hipMalloc(&ctx->d_hash_blist, sizeof(uint32_t) * cap) != hipSuccess ||
+            hipMalloc(&d_ids, sizeof(uint64_t) * cap) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "hash pose buffers");
+            break;
+        }
+        hipMemcpy(d_ids, ids.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice);
+        hipMemcpy(ctx->d_hash_blist, blist.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice);
+        double* hx = ctx->d_hash;
+        if (eslam_launch_hash_poses(&g, d_seg, d_seg + 8 * steps, d_ids, n, hx, hx + cap, hx + 2 * cap, hx + 3 * cap,
+                                    ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_HIP, "hash poses");
+            break;
+        }
+        ctx->hash_n = n;
+        ctx->has_hash = true;
+    } while (0);
+    hipFree(d_seg); hipFree(d_out); hipFree(d_ids);
+    return rc;
+}
+
+static const double* hash_field(eslam_ctx* ctx, int f)
+{
+    return ctx->d_hash + (uint64_t)f * (ctx->hash_n ? ctx->hash_n : 1);
+}
+
+extern "C" int eslam_gpu_init_hash(eslam_ctx* ctx, uint64_t n)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (!ctx->has_hash || ctx->hash_n == 0) return fail(ctx, ESLAM_ERR_HASH_SAMPLE, "could not sample from pose hash.");
+    int rc = alloc_particles(ctx, n);
+    if (rc) return rc;
+    rc = reset_ctl_for_new_particles(ctx, 1);
+    if (rc) return rc;
+    // rand() % poses.size() per particle, in global particle order (every rank walks all)
+    const uint64_t total = ctx->sharded ? ctx->n_global : n, skip = ctx->gbase;
+    std::vector<uint32_t> idx(n ? n : 1);
+    for (uint64_t gi = 0; gi < total; ++gi) {
+        const uint32_t v = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&ctx->libc) % ctx->hash_n);
+        if (gi >= skip && gi < skip + n) idx[gi - skip] = v;
+    }
+    uint32_t* d_idx = nullptr;
+    HIPCHK(ctx, hipMalloc(&d_idx, sizeof(uint32_t) * (n ? n : 1)));
+    hipError_t e = hipMemcpy(d_idx, idx.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = eslam_launch_init_from_hash(ctx->st[0], d_idx, n, hash_field(ctx, 0), hash_field(ctx, 1), hash_field(ctx, 2),
+                                        hash_field(ctx, 3), ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    hipFree(d_idx);
+    HIPCHK(ctx, e);
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_hash_info(eslam_ctx* ctx, uint64_t* n_poses, uint32_t* bucket_sizes)
+{
+    if (!ctx || !n_poses) return ESLAM_ERR_INVALID_ARG;
+    *n_poses = ctx->has_hash ? ctx->hash_n : 0;
+    if (bucket_sizes && ctx->has_hash)
+        for (size_t b = 0; b + 1 < ctx->hash_bstart.size(); ++b) bucket_sizes[b] = ctx->hash_bstart[b + 1] - ctx->hash_bstart[b];
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_hash_poses(eslam_ctx* ctx, double* x, double* y, double* theta, double* z, int32_t* bucket)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (!ctx->has_hash) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no pose hash");
+    const uint64_t n = ctx->hash_n;
+    double* dst[4] = {x, y, theta, z};
+    for (int f = 0; f < 4; ++f)
+        if (dst[f] && n) HIPCHK(ctx, hipMemcpy(dst[f], hash_field(ctx, f), n * 8, hipMemcpyDeviceToHost));
+    if (bucket && n) memcpy(bucket, ctx->hash_bucket.data(), n * 4);
+    return ESLAM_OK;
 }
 
 extern "C" int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n)
@@ -960,6 +1142,66 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     return ESLAM_OK;
 }
 
+// PoseEstimator::sampleFromHash  src/PoseEstimator.cpp:130-182 (after the project kernel)
+static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const StepParams& p)
+{
+    double pos[3 * ESLAM_MAX_CONTACTS], low[3 * ESLAM_MAX_CONTACTS];
+    int32_t grp[ESLAM_MAX_CONTACTS];
+    for (uint32_t i = 0; i < p.m; ++i) {                      // setContactPoints: yaw-compensated feet
+        pos[3 * i] = p.c[i].px; pos[3 * i + 1] = p.c[i].py; pos[3 * i + 2] = p.c[i].pz;
+        grp[i] = in->contacts[i].group_id;
+    }
+    const uint32_t nlow = dm_lowest_points(pos, grp, p.m, low);  // getLowestPointPerGroup
+    double sx, sy;
+    dm_surface_param(low, nlow, &sx, &sy);
+    const int bins = (int)ctx->cfg.hash_slope_bins;
+    const int b = dm_bucket_index(bins, -1.0, 1.0, sx) * bins + dm_bucket_index(bins, -1.0, 1.0, sy);
+    const uint32_t bsize = ctx->hash_bstart[b + 1] - ctx->hash_bstart[b];
+    const double rel = dm_pow(1.0 - 1.0 * (double)bsize / (double)ctx->hash_n, 3.0);   // getRelevance^3
+    const uint64_t N = ctx->n_global;
+    uint64_t k = (uint64_t)(((double)N * ctx->cfg.hash_percentage) * rel);
+    if (rel < 0.8) k = 0;
+    if (k > ctx->n) k = ctx->n;
+    if (k == 0 || bsize == 0) return ESLAM_OK;                // nothing replaced, no rand() drawn
+    if (ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "sampleFromHash is not implemented for a sharded filter");
+    double S = 0.0;
+    int rc = eslam_gpu_get_weights_sum(ctx, &S);
+    if (rc) return rc;
+    const double weight = ((S / (double)N) * ctx->cfg.hash_avg_factor) * rel;   // getWeightAvg() * avgFactor * rel
+    const uint64_t n = ctx->n;
+    if (ctx->sort_cap < n) {
+        hipFree(ctx->d_sort); ctx->d_sort = nullptr; ctx->sort_cap = 0;
+        hipFree(ctx->sort_tmp); ctx->sort_tmp = nullptr; ctx->sort_tmp_bytes = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->d_sort, sizeof(uint32_t) * 4 * n));
+        size_t bytes = 0;
+        HIPCHK(ctx, eslam_hash_sort(ctx->st[0], ctx->st[1], ctx->ctl, n, nullptr, nullptr, nullptr, nullptr, nullptr, &bytes,
+                                    ctx->stream));
+        HIPCHK(ctx, hipMalloc(&ctx->sort_tmp, bytes ? bytes : 1));
+        ctx->sort_tmp_bytes = bytes;
+        ctx->sort_cap = n;
+    }
+    uint32_t* keys = ctx->d_sort;
+    uint32_t* vals = keys + n;
+    uint32_t* keys_out = vals + n;
+    uint32_t* order = keys_out + n;
+    size_t bytes = ctx->sort_tmp_bytes;
+    HIPCHK(ctx, eslam_hash_sort(ctx->st[0], ctx->st[1], ctx->ctl, n, keys, vals, keys_out, order, ctx->sort_tmp, &bytes,
+                                ctx->stream));
+    std::vector<uint32_t> draws(k);
+    for (uint64_t j = 0; j < k; ++j) draws[j] = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&ctx->libc) % bsize);
+    if (ctx->draws_cap < k) {
+        hipFree(ctx->d_draws); ctx->d_draws = nullptr; ctx->draws_cap = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->d_draws, sizeof(uint32_t) * k));
+        ctx->draws_cap = k;
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_draws, draws.data(), sizeof(uint32_t) * k, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, eslam_launch_hash_replace(ctx->st[0], ctx->st[1], ctx->ctl, order, ctx->d_draws, k, ctx->d_hash_blist,
+                                          ctx->hash_bstart[b], hash_field(ctx, 0), hash_field(ctx, 1), hash_field(ctx, 2),
+                                          hash_field(ctx, 3), weight, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));          // draws (host) must outlive the copy
+    return ESLAM_OK;
+}
+
 static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project, bool weight)
 {
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
@@ -967,6 +1209,25 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     StepParams p;
     fill_step_params(ctx, in, p);
     p.proj_event = ctx->proj_event;
+    // the hash respawn (static counter of src/PoseEstimator.cpp:239, per context) runs on
+    // the first project and every period-th after it, between project and update
+    bool respawn = false;
+    if (project && ctx->cfg.hash_use && ctx->has_hash) {
+        const uint64_t period = ctx->cfg.hash_period ? ctx->cfg.hash_period : 1;
+        respawn = (ctx->hash_event++ % period) == 0;
+    }
+    if (respawn) {
+        const GatherView gv0 = gather_view(ctx);
+        HIPCHK(ctx, eslam_launch_project_weight(1, 0, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
+                                                ctx->shards, &gv0, ctx->stream));
+        HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
+        ctx->proj_event++;
+        if (gv0.record) ctx->has_anc = true;
+        const int rc = sample_from_hash(ctx, in, p);
+        if (rc) return rc;
+        project = false;                      // done; the update below is weight-only
+        if (!weight) return ESLAM_OK;
+    }
     rec(ctx, 0);
     const GatherView gv = gather_view(ctx);
     HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
@@ -1168,6 +1429,8 @@ extern "C" int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st)
     st->hash_count = ctx->hash_event;
     st->max_weight = ctx->ctl_host->max_weight;
     memcpy(st->ud_pose, ctx->ud_pose, sizeof(ctx->ud_pose));
+    memcpy(st->libc_rand, ctx->libc.r, sizeof(st->libc_rand));
+    st->libc_rand_pos = ctx->libc.i;
     return ESLAM_OK;
 }
 
@@ -1182,6 +1445,8 @@ extern "C" int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st
     ctx->hash_event = st->hash_count;
     ctx->ctl_host->max_weight = st->max_weight;
     memcpy(ctx->ud_pose, st->ud_pose, sizeof(ctx->ud_pose));
+    memcpy(ctx->libc.r, st->libc_rand, sizeof(st->libc_rand));
+    ctx->libc.i = st->libc_rand_pos % 34u;
     return write_ctl(ctx);
 }
 

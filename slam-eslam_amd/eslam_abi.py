@@ -135,6 +135,9 @@ class RngState(C.Structure):
         ("hash_count", C.c_uint64),
         ("max_weight", C.c_double),
         ("ud_pose", C.c_double * 12),
+        ("libc_rand", C.c_uint32 * 34),
+        ("libc_rand_pos", C.c_uint32),
+        ("pad2", C.c_uint32),
     ]
 
 

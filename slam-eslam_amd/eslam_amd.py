@@ -66,6 +66,10 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_get_kernel_times.argtypes = [vp, C.POINTER(A.KernelTimes)]
     L.eslam_gpu_selftest_math.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_uint64]
     L.eslam_gpu_set_comm.argtypes = [vp, C.POINTER(A.Comm), C.c_uint64, C.POINTER(C.c_uint64)]
+    L.eslam_gpu_hash_create.argtypes = [vp]
+    L.eslam_gpu_init_hash.argtypes = [vp, C.c_uint64]
+    L.eslam_gpu_hash_info.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    L.eslam_gpu_hash_poses.argtypes = [vp, dp, dp, dp, dp, C.POINTER(C.c_int32)]
     _lib = L
     return L
 
@@ -127,6 +131,28 @@ class GpuFilter:
         n = C.c_uint64()
         self._check(self.L.eslam_gpu_particle_count(self.h, C.byref(n)))
         return n.value
+
+    # -- SurfaceHash ----------------------------------------------------------------------
+    def hash_create(self):
+        self._check(self.L.eslam_gpu_hash_create(self.h))
+
+    def init_hash(self, n):
+        self._check(self.L.eslam_gpu_init_hash(self.h, n))
+
+    def hash_info(self):
+        n = C.c_uint64()
+        bins = self.cfg.hash_slope_bins
+        sizes = np.zeros(bins * bins, dtype=np.uint32)
+        self._check(self.L.eslam_gpu_hash_info(self.h, C.byref(n), sizes.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return n.value, sizes
+
+    def hash_poses(self):
+        n, _ = self.hash_info()
+        out = [np.zeros(n) for _ in range(4)]
+        bucket = np.zeros(n, dtype=np.int32)
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        self._check(self.L.eslam_gpu_hash_poses(self.h, *[ptr(a) for a in out], bucket.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out + [bucket]
 
     # -- hot path -------------------------------------------------------------------------
     def step(self, st):

@@ -96,10 +96,17 @@ def lib():
     L.or_mls_get_patch.argtypes = [C.POINTER(A.MlsGrid), C.POINTER(C.c_double), C.c_double, C.c_double,
                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.or_set_comm.argtypes = [vp, C.POINTER(A.Comm), C.c_uint64, C.POINTER(C.c_uint64)]
+    L.or_hash_create.argtypes = [vp]
+    L.or_init_hash.argtypes = [vp, C.c_uint64]
+    L.or_hash_info.restype = C.c_uint64
+    L.or_hash_info.argtypes = [vp, C.POINTER(C.c_uint32)]
+    L.or_hash_poses.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     L.or_dm.restype = C.c_double
     L.or_dm.argtypes = [C.c_int, C.c_double, C.c_double]
     L.or_dm_philox.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32)]
     L.or_dm_philox_raw.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+    L.or_dm_libc_rand.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32)]
     L.or_dm_minstd_jump.restype = C.c_uint32
     L.or_dm_minstd_jump.argtypes = [C.c_uint32, C.c_uint64]
     L.or_dm_limbs_to_double.restype = C.c_double
@@ -134,6 +141,27 @@ class OracleFilter:
         self._gb = (C.c_uint64 * len(self.bounds))(*self.bounds)
         rc = self.L.or_set_comm(self.h, C.byref(comm.struct), n_global, self._gb)
         assert rc == 0, rc
+
+    def hash_create(self):
+        assert self.L.or_hash_create(self.h) == 0
+
+    def init_hash(self, n):
+        rc = self.L.or_init_hash(self.h, n)
+        assert rc == 0, rc
+
+    def hash_info(self):
+        bins = self.cfg.hash_slope_bins
+        sizes = np.zeros(bins * bins, dtype=np.uint32)
+        n = self.L.or_hash_info(self.h, sizes.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return n, sizes
+
+    def hash_poses(self):
+        n, _ = self.hash_info()
+        out = [np.zeros(n) for _ in range(4)]
+        bucket = np.zeros(n, dtype=np.int32)
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        assert self.L.or_hash_poses(self.h, *[ptr(a) for a in out], bucket.ctypes.data_as(C.POINTER(C.c_int32))) == 0
+        return out + [bucket]
 
     def set_map(self, grid):
         self._map = grid

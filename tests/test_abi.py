@@ -41,7 +41,7 @@ def test_exports_every_declared_symbol(lib):
 
 def test_abi_version(lib):
     lib.eslam_gpu_abi_version.restype = C.c_int
-    assert lib.eslam_gpu_abi_version() == 1
+    assert lib.eslam_gpu_abi_version() == 2
 
 
 def test_config_default_matches_reference_defaults(lib):

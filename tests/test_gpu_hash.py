@@ -1,0 +1,66 @@
+"""SurfaceHash on the GPU against the oracle, bit for bit: the pose hash of
+SurfaceHash::create (sweep kernel), PoseEstimator::init(N, hash) and the sampleFromHash
+respawn inside the step (radix sort of the (float weight, index) pairs on the device)."""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from hash_util import hash_config, hash_grid, rotated_grid, slope_stream
+from parity_util import assert_bit_identical, info_tuple
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu_mod():
+    import eslam_amd
+    eslam_amd.load_library()
+    return eslam_amd
+
+
+@pytest.mark.parametrize("grid_fn", [hash_grid, rotated_grid])
+def test_hash_create_parity(gpu_mod, grid_fn):
+    grid = grid_fn(cells=60)
+    cfg = hash_config(1000, steps=8, bins=20)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    gpu = gpu_mod.GpuFilter(cfg)
+    for f in (orc, gpu):
+        f.set_map(grid)
+        f.hash_create()
+    no, so = orc.hash_info()
+    ng, sg = gpu.hash_info()
+    assert no == ng > 0 and np.array_equal(so, sg)
+    for a, b in zip(gpu.hash_poses(), orc.hash_poses()):
+        assert np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
+
+
+@pytest.mark.parametrize("mode", ["step", "split"])
+def test_hash_filter_parity(gpu_mod, mode):
+    n = 5000
+    cfg = hash_config(n, steps=8, bins=20, period=2)
+    grid = hash_grid(cells=60)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    gpu = gpu_mod.GpuFilter(cfg)
+    for f in (orc, gpu):
+        f.set_map(grid)
+        f.init_pose([0.0, 0.0, 0.0], [1.0, 0.0, 0.0, 0.0])
+    assert_bit_identical(gpu.download(), orc.download(), "init from hash")
+    replaced = 0
+    for k, st in enumerate(slope_stream(7)):
+        if mode == "step":
+            orc.step(st)
+            gpu.step(st)
+        else:
+            orc.project(st)
+            gpu.project(st)
+            pa = gpu.download()
+            assert_bit_identical(pa, orc.download(), f"project {k}")
+            replaced += int(np.count_nonzero(pa.zsigma == 0.5))
+            orc.update(st)
+            gpu.update(st)
+        gi = gpu.sync()
+        assert_bit_identical(gpu.download(), orc.download(), f"{mode} step {k}")
+        assert info_tuple(gi) == info_tuple(orc.info()), k
+    if mode == "split":
+        assert replaced > 0
+    assert gpu.rng_state().libc_rand_pos == orc.rng_state().libc_rand_pos
