@@ -677,6 +677,29 @@ DM_FN uint64_t dm_fx_shift(double v, int shift)
 
 DM_FN uint64_t dm_fx61(double v) { return dm_fx_shift(v, 61); }
 
+/* number of stratified draws T_k = fx(((k + U_k) / N), shift) with T_k <= c, U_k the
+ * boost uniform of the (k+1)-th minstd draw after xs (the device version reads the jump
+ * from tables; same values)                                                               */
+DM_FN uint64_t dm_count_draws_le(uint64_t c, uint64_t N, uint32_t xs, int shift)
+{
+    const unsigned __int128 prod = (unsigned __int128)c * N;
+    const uint64_t kstar = (uint64_t)(prod >> shift);
+    const uint64_t k0 = kstar >= 1 ? kstar - 1 : 0;
+    if (k0 >= N) return N;
+    uint64_t cnt = k0;
+    uint32_t x = dm_mulmod31(dm_minstd_pow(k0 + 1), xs);
+    const double dN = (double)N;
+    for (uint64_t k = k0; k <= kstar + 1 && k < N; ++k) {
+        const double u = dm_minstd_uniform(x);
+        const uint64_t T = dm_fx_shift(((double)k + u) / dN, shift);
+        if (T <= c) cnt = k + 1;
+        else break;
+        x = dm_minstd_next(x);
+    }
+    return cnt;
+}
+
+
 /* trunc(v * 2^scale) as an unsigned 128-bit integer split in four 32-bit limbs.
  * v >= 0 finite.  Returns 1 if saturated (v * 2^scale >= 2^127).                        */
 DM_FN int dm_fx128_limbs(double v, int scale, uint32_t limb[4])

@@ -36,10 +36,9 @@ extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, uin
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
                                                   const uint64_t* tile_prefix, uint32_t* marks, uint32_t* tile_first,
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
-                                                  uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off, hipStream_t stream);
+                                                  hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
-                                        const uint64_t* first_last, const uint64_t* sd_ed, const uint64_t* send_off,
-                                        uint64_t nsend, void* send, hipStream_t stream);
+                                        const uint64_t* first_last, uint64_t nsend, void* send, hipStream_t stream);
 extern "C" hipError_t eslam_launch_expand(const void* recv, uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* row_first,
                                           hipStream_t stream);
 extern "C" uint64_t eslam_record_bytes(void);
@@ -1065,9 +1064,10 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
 // multi-GPU update tail:
 //   shards -> rank record -> all_gather -> every rank finalises the same global scalars
 //   -> normalise + this rank's fixed-point weight total -> all_gather of the totals
-//   -> global stratified segments (outputs in this rank's slice are marked directly)
-//   -> all_gather of the send counts (one host sync) -> pack the particles whose outputs
-//   lie in other slices -> all_to_all_v -> expand + gather
+//   -> global stratified segments (outputs in this rank's slice are marked directly),
+//      while the host reads the totals and derives every rank's output range (the
+//      all_to_all_v sizes: one record per output that lands in another slice)
+//   -> pack -> all_to_all_v -> expand; the gather is fused into the next k_project_weight
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const int G = ctx->comm.nranks, me = ctx->comm.rank;
@@ -1084,44 +1084,64 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
                                             ctx->stream));
     rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
     if (rc) return rc;
-    const PlanParams pp = plan_params(ctx);
+    uint64_t* h = ctx->mg_host;
+    HIPCHK(ctx, hipMemcpyAsync(h + mg::kTotals, ctx->mg + mg::kTotals, 8ull * G, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    PlanParams pp = plan_params(ctx);
     HIPCHK(ctx, eslam_launch_segments_multi(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->tile_sum, ctx->marks,
                                             ctx->tile_first, ctx->mg + mg::kTotals, ctx->jump, ctx->range,
-                                            ctx->mg + mg::kFirstLast, ctx->mg + mg::kCounts, ctx->mg + mg::kSdEd,
-                                            ctx->mg + mg::kSendOff, ctx->stream));
+                                            ctx->mg + mg::kFirstLast, ctx->stream));
     if (timed) rec(ctx, 3);
-    const uint32_t record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
+    HIPCHK(ctx, hipEventSynchronize(ctx->ev[0]));       // the totals, not the segments kernel
+    const Ctl& c = *ctx->ctl_host;
     uint64_t nrecv = 0;
-    if (G > 1) {                             // particle migration between slices
-        rc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
-        if (rc) return rc;
-        uint64_t* h = ctx->mg_host;
-        HIPCHK(ctx, hipMemcpyAsync(h + mg::kCountsAll, ctx->mg + mg::kCountsAll, 8ull * G * G, hipMemcpyDeviceToHost,
-                                   ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (c.resample && G > 1) {
+        // every rank's outputs [O0_r, O1_r), the same counts the device computes
+        const uint64_t N = ctx->n_global;
+        uint64_t O0[kMaxRanks], O1[kMaxRanks], off = 0;
+        for (int r = 0; r < G; ++r) {
+            const uint64_t t = h[mg::kTotals + r];
+            O0[r] = r == 0 ? 0 : dm_count_draws_le(off, N, c.minstd_start, c.scan_shift);
+            O1[r] = r == G - 1 ? N : dm_count_draws_le(off + t, N, c.minstd_start, c.scan_shift);
+            off += t;
+        }
+        auto overlap = [&](int r, int d) -> uint64_t {
+            const uint64_t a = O0[r] > ctx->gall[d] ? O0[r] : ctx->gall[d];
+            const uint64_t b = O1[r] < ctx->gall[d + 1] ? O1[r] : ctx->gall[d + 1];
+            return b > a ? b - a : 0;
+        };
         const uint64_t R = eslam_record_bytes();
         uint64_t sb[kMaxRanks], rb[kMaxRanks], nsend = 0, any = 0;
-        for (int r = 0; r < G; ++r) {
-            sb[r] = h[mg::kCountsAll + me * G + r] * R;
-            rb[r] = h[mg::kCountsAll + r * G + me] * R;
-            nsend += h[mg::kCountsAll + me * G + r];
-            nrecv += h[mg::kCountsAll + r * G + me];
-            for (int d = 0; d < G; ++d) any |= h[mg::kCountsAll + r * G + d];
+        pp.send_off[0] = 0;
+        for (int d = 0; d < G; ++d) {
+            const uint64_t ns = d == me ? 0 : overlap(me, d);
+            const uint64_t nr = d == me ? 0 : overlap(d, me);
+            pp.sd[d] = O0[me] > ctx->gall[d] ? O0[me] : ctx->gall[d];
+            pp.ed[d] = pp.sd[d] + ns;
+            pp.send_off[d + 1] = pp.send_off[d] + ns;
+            sb[d] = ns * R;
+            rb[d] = nr * R;
+            nsend += ns;
+            nrecv += nr;
+            for (int r = 0; r < G; ++r) any |= (r == d ? 0 : overlap(r, d));
         }
         if (any) {
             rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
             if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
             if (rc) return rc;
-            HIPCHK(ctx, eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
-                                          ctx->mg + mg::kSdEd, ctx->mg + mg::kSendOff, nsend, ctx->sendbuf, ctx->stream));
+            HIPCHK(ctx, eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast, nsend,
+                                          ctx->sendbuf, ctx->stream));
             rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
             if (rc) return rc;
+        } else {
+            nrecv = 0;
         }
     }
-    // marks of the migrated particles; the gather is fused into the next k_project_weight
+    // marks of the migrated outputs; the gather is fused into the next k_project_weight
     HIPCHK(ctx, eslam_launch_expand(ctx->recvbuf, nrecv, ctx->gbase, ctx->marks, ctx->tile_first, ctx->stream));
     if (timed) rec(ctx, 4);
-    if (record) ctx->has_anc = true;
+    if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ctx->has_anc = true;
     return ESLAM_OK;
 }
 

@@ -166,6 +166,10 @@ struct PlanParams {
     uint64_t n_global;
     int32_t rank, nranks;
     uint64_t gbase[kMaxRanks + 1];       // first global index of every rank (+ n_global)
+    // per destination d != rank (host-computed from the all-gathered totals): this rank's
+    // outputs in d's slice [sd[d], ed[d]) and their offsets in the send buffer
+    uint64_t sd[kMaxRanks], ed[kMaxRanks];
+    uint64_t send_off[kMaxRanks + 1];
 };
 
 }  // namespace eslam_dev

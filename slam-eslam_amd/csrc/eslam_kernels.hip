@@ -1256,48 +1256,29 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     flush_marks(s_tm, marks, tile_first, seg_lo, seg_hi, val);
 }
 
-// counts[d] = particles this rank sends to rank d != rank (0 when not resampling), their
-// clipped output ranges [S_d, E_d) and the packing offsets send_off[0..nranks]
-__global__ void k_plan_counts(const Ctl* __restrict__ ctl, PlanParams pp, const uint64_t* __restrict__ totals,
-                              const uint32_t* __restrict__ jt, const uint64_t* __restrict__ first_last,
-                              uint64_t* __restrict__ counts, uint64_t* __restrict__ sd_ed, uint64_t* __restrict__ send_off)
-{
-    if (threadIdx.x != 0) return;
-    uint64_t off, O0 = 0, O1 = 0;
-    if (ctl->resample) plan_bounds(pp, ctl, totals, jt, off, O0, O1);
-    uint64_t acc = 0;
-    send_off[0] = 0;
-    for (int d = 0; d < pp.nranks; ++d) {
-        const uint64_t W0 = pp.gbase[d], W1 = pp.gbase[d + 1];
-        const uint64_t Sd = O0 > W0 ? O0 : W0, Ed = O1 < W1 ? O1 : W1;
-        uint64_t cnt = 0;
-        if (ctl->resample && d != pp.rank && Sd < Ed) cnt = first_last[2 * d + 1] - first_last[2 * d] + 1;
-        counts[d] = cnt;
-        sd_ed[2 * d] = Sd;
-        sd_ed[2 * d + 1] = Ed;
-        acc += cnt;
-        send_off[d + 1] = acc;
-    }
-}
-
-
+// one record per output of this rank that lands in another slice: send slot j of
+// destination d is output k = sd[d] + (j - send_off[d]); its source is the particle of
+// [first, last] (d's run, from k_segments_multi) whose range [lo, hi) contains k
 __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
                                                  const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
-                                                 const uint64_t* __restrict__ sd_ed, const uint64_t* __restrict__ send_off,
                                                  Rec* __restrict__ send)
 {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= send_off[pp.nranks]) return;
+    if (j >= pp.send_off[pp.nranks]) return;
     int d = 0;
-    while (j >= send_off[d + 1]) ++d;
-    const uint64_t i = first_last[2 * d] + (j - send_off[d]);
+    while (j >= pp.send_off[d + 1]) ++d;
+    const uint64_t k = pp.sd[d] + (j - pp.send_off[d]);
+    uint64_t a = first_last[2 * d], b = first_last[2 * d + 1];   // range[a].x <= k < range[b].y
+    while (a < b) {                                               // last i in [a, b] with lo_i <= k
+        const uint64_t mid = a + (b - a + 1) / 2;
+        if ((uint64_t)range[mid].x <= k) a = mid;
+        else b = mid - 1;
+    }
+    const uint64_t i = a;
     const DevState st = ctl->base ? s1 : s0;
-    const uint64_t Sd = sd_ed[2 * d], Ed = sd_ed[2 * d + 1];
-    const uint2 rg = range[i];
-    const uint64_t lo = rg.x > Sd ? rg.x : Sd, hi = rg.y < Ed ? rg.y : Ed;
     Rec r;
     r.x = st.x[i]; r.y = st.y[i]; r.th = st.th[i]; r.z = st.z[i]; r.zs = st.zs[i]; r.w = st.w[i]; r.mprob = st.mprob[i];
-    r.lohi = lo | (hi << 32);
+    r.lohi = k | ((k + 1) << 32);
     r.src = (uint64_t)st.flags[i] | ((pp.gbase[pp.rank] + i) << 8);
     send[j] = r;
 }
@@ -1612,21 +1593,19 @@ extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream)
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
                                                   const uint64_t* tile_prefix, uint32_t* marks, uint32_t* tile_first,
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
-                                                  uint64_t* counts, uint64_t* sd_ed, uint64_t* send_off, hipStream_t stream)
+                                                  hipStream_t stream)
 {
     if (sp->ntiles) hipLaunchKernelGGL(k_segments_multi, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl,
                                        tile_prefix, marks, tile_first, totals, jt, range, first_last);
-    hipLaunchKernelGGL(k_plan_counts, dim3(1), dim3(64), 0, stream, ctl, *pp, totals, jt, first_last, counts, sd_ed, send_off);
     return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
-                                        const uint64_t* first_last, const uint64_t* sd_ed, const uint64_t* send_off,
-                                        uint64_t nsend, void* send, hipStream_t stream)
+                                        const uint64_t* first_last, uint64_t nsend, void* send, hipStream_t stream)
 {
     if (!nsend) return hipSuccess;
     hipLaunchKernelGGL(k_pack, dim3((uint32_t)((nsend + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, s0, s1, ctl, *pp,
-                       range, first_last, sd_ed, send_off, (Rec*)send);
+                       range, first_last, (Rec*)send);
     return hipGetLastError();
 }
 
