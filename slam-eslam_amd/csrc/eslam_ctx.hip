@@ -649,6 +649,7 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
     m.cell_start = ctx->d_cells;
     m.patch = ctx->d_patch;
     m.height = ctx->d_height;
+    m.has_height = ctx->d_height ? 1u : 0u;
     m.width = g->width;
     m.height_cells = g->height;
     m.inv_scale_x = 1.0 / g->scale_x;
@@ -1007,6 +1008,8 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
         const int32_t g = in->contacts[i].group_id;
         p.c[i].end = (g == -1 || i + 1 == m || g != in->contacts[i + 1].group_id) ? 1u : 0u;
         ends += p.c[i].end;
+        p.eval_mask |= p.c[i].eval << i;
+        p.end_mask |= p.c[i].end << i;
     }
     ctx->maxp = ends;
     // LDS window margin: foot reach + mean motion + 6 sigma of the sampled motion + 2 cells

@@ -78,41 +78,46 @@ struct DevState {
     uint8_t* flags;
 };
 
+// K1 reads the first 64 bytes (the lookup header) with one scalar load per lookup
 struct MapView {
     const uint32_t* cell_start;
     const float2* patch;                 // (mean, stdev) per patch
-    const float* height;                 // nullable: all horizontal
+    double inv_scale_x, inv_scale_y, offset_x, offset_y;
     uint32_t width, height_cells;
     uint32_t g2l_identity;               // global2local is exactly the identity
-    uint32_t pad;
-    double inv_scale_x, inv_scale_y, offset_x, offset_y;
+    uint32_t has_height;                 // height != nullptr
+    const float* height;                 // nullable: all horizontal
     double g2l[12];
 };
 
 struct ContactC {
-    double px, py, pz;                   // yaw-compensated body-frame position
-    double zp;                           // 0.0 * pz: the zero terms of Affine3d * p (exact,
-    double zz;                           // (0.0 * px + 0.0 * py); uniform per step)
+    double px, py, zp, zz;               // yaw-compensated body-frame x, y; zp = 0.0 * pz and
+                                         // zz = (0.0 * px + 0.0 * py): the zero terms of
+                                         // Affine3d * p (exact, uniform per step)
+    double pz;
     uint32_t eval;                       // !(contact < 0.2)
     uint32_t end;                        // group ends after this contact
 };
 
+// The head of StepParams is laid out for K1's scalar loads at the point of use (field
+// order matters: see k_project_weight); the rest is read before the particle loop.
 struct StepParams {
-    // ---- project (PoseEstimator::project)
-    double yaw, z_delta, z_var;
-    double mu[3];
-    double L00, L10, L11, L20, L21, L22;
-    double slip_factor, max_yaw_dev;
-    double spread_threshold, spread_trans, spread_rot;
-    uint32_t hash_use;
-    uint32_t m;                          // number of contacts
-    uint64_t seed, proj_event;
+    // ---- project (PoseEstimator::project): Philox key, odometry sampler, z motion
+    uint64_t seed, proj_event, gbase;    // +0
+    double mu[3];                        // +24
+    double L00, L10, L11, L20, L21;      // +48
+    double L22, slip_factor, yaw, max_yaw_dev;   // +88
+    double z_delta, z_var;               // +120
     // ---- weighting (updateWeights)
-    double me2, radius, corr;
-    uint64_t min_contacts;
-    uint32_t use_shape, use_slip;
+    double me2, radius, corr;            // +136
+    uint64_t min_contacts;               // +160
+    uint32_t use_shape;                  // +168
+    uint32_t m;                          // number of contacts
+    uint32_t eval_mask, end_mask;        // bit i: contact i evaluated / ends its group
+    uint32_t hash_use, use_slip;
+    double spread_threshold, spread_trans, spread_rot;
     // ---- sizes
-    uint64_t n, gbase, n_global;
+    uint64_t n, n_global;
     uint32_t J;                          // canonical chunk rows
     uint32_t use_window;                 // stage the MLS window under the cloud in LDS
     double win_margin;                   // world-frame margin around the last bounding box
@@ -139,6 +144,17 @@ struct GatherView {
     const Rec* recs;                     // multi-GPU: migrated particles
     uint32_t record;
     uint32_t multi;                      // marks use the multi-GPU source encoding
+};
+
+// k_project_weight's single kernel argument: its fields are read with scalar loads from the
+// kernel-argument segment where they are used (offsetof), see k_project_weight
+struct K1Args {
+    StepParams p;
+    MapView map;
+    GatherView gv;
+    DevState s[2];
+    Ctl* ctl;
+    Shard* shards;
 };
 
 struct FinParams {

@@ -72,6 +72,78 @@ __device__ __forceinline__ uint32_t jump_pow(const uint32_t* __restrict__ jt, ui
 }
 
 // ---------------------------------------------------------------------------------------
+// K1 kernel arguments by scalar load at the point of use.  K1 reads ~110 uniform values
+// (contacts, sampler, map header, state pointers).  Loaded once at kernel entry they exceed
+// the 102 SGPRs, and the compiler parks them in VGPR lanes and fetches them back with
+// v_readlane (a VALU instruction) on every row.  A volatile asm load + wait cannot be
+// hoisted, so each value occupies SGPRs only where it is used; the scalar cache serves the
+// repeats.  Outputs are early-clobber: the loads are in flight while the address is live.
+// ---------------------------------------------------------------------------------------
+typedef uint32_t su2 __attribute__((ext_vector_type(2)));
+typedef uint32_t su4 __attribute__((ext_vector_type(4)));
+typedef uint32_t su8 __attribute__((ext_vector_type(8)));
+typedef uint32_t su16 __attribute__((ext_vector_type(16)));
+
+#define KOFF(f) ((uint32_t)offsetof(K1Args, f))
+
+__device__ __forceinline__ uint64_t kseg() { return (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr(); }
+
+__device__ __forceinline__ su2 kl2(uint32_t off)
+{
+    su2 r;
+    asm volatile("s_load_dwordx2 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=&s"(r) : "s"(kseg()), "s"(off));
+    return r;
+}
+__device__ __forceinline__ su4 kl4(uint32_t off)
+{
+    su4 r;
+    asm volatile("s_load_dwordx4 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=&s"(r) : "s"(kseg()), "s"(off));
+    return r;
+}
+__device__ __forceinline__ su8 kl8(uint32_t off)
+{
+    su8 r;
+    asm volatile("s_load_dwordx8 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=&s"(r) : "s"(kseg()), "s"(off));
+    return r;
+}
+__device__ __forceinline__ su16 kl16(uint32_t off)
+{
+    su16 r;
+    asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=&s"(r) : "s"(kseg()), "s"(off));
+    return r;
+}
+// two blocks, one wait
+__device__ __forceinline__ void kl8_2(uint32_t off_a, uint32_t off_b, su8& a, su2& b)
+{
+    asm volatile("s_load_dwordx8 %0, %2, %3\n\ts_load_dwordx2 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(kseg()), "s"(off_a), "s"(off_b));
+}
+template <class V> __device__ __forceinline__ uint64_t kq(const V& r, int k)
+{
+    return (uint64_t)r[2 * k] | ((uint64_t)r[2 * k + 1] << 32);
+}
+template <class V> __device__ __forceinline__ double kd(const V& r, int k) { return dm_from_bits(kq(r, k)); }
+template <class T, class V> __device__ __forceinline__ T* kp(const V& r, int k) { return (T*)(uintptr_t)kq(r, k); }
+
+// the state pointers of buffer s[b] (offset KOFF(s[b]))
+struct StatePtrs {
+    double *x, *y, *th, *z, *zs, *w, *mprob;
+    uint8_t* flags;
+};
+__device__ __forceinline__ StatePtrs kstate(uint32_t off)
+{
+    const su16 r = kl16(off);
+    return StatePtrs{kp<double>(r, 0), kp<double>(r, 1), kp<double>(r, 2), kp<double>(r, 3),
+                     kp<double>(r, 4), kp<double>(r, 5), kp<double>(r, 6), kp<uint8_t>(r, 7)};
+}
+
+static_assert(offsetof(StepParams, mu) == 24 && offsetof(StepParams, L22) == 88 && offsetof(StepParams, z_delta) == 120 &&
+                  offsetof(StepParams, me2) == 136 && offsetof(StepParams, use_shape) == 168,
+              "K1 scalar-load blocks");
+static_assert(offsetof(MapView, width) == 48 && offsetof(MapView, height) == 64, "map lookup header");
+static_assert(offsetof(ContactC, pz) == 32 && offsetof(GatherView, record) == 32, "K1 scalar-load blocks");
+
+// ---------------------------------------------------------------------------------------
 // GridAccess::get -> MLSMap::getPatch(C_global2local * p, patch, 3.0)  (src/PoseEstimator.hpp:97-105)
 // qv: the query patch variance (measVar).  Cell: floor((x - offset) * (1/scale)); the
 // 3-sigma gate |mean_p - z| < 3 sqrt(stdev_p^2 + measVar) is evaluated squared.
@@ -91,11 +163,11 @@ struct Window {
     const WinCell* cells;                // rows x cols (LDS)
 };
 
-__device__ __forceinline__ bool patch_gate(const MapView& m, uint32_t k, float pmf, float psf, double lz, double qv,
+__device__ __forceinline__ bool patch_gate(const float* height, uint32_t k, float pmf, float psf, double lz, double qv,
                                            double& mean, double& stdev)
 {
     const double pm = (double)pmf, ps = (double)psf;
-    const double ph = m.height ? (double)m.height[k] : 0.0;
+    const double ph = height ? (double)height[k] : 0.0;
     double diff;
     if (ph > 0.0) {
         if (lz > pm) diff = lz - pm;
@@ -108,35 +180,42 @@ __device__ __forceinline__ bool patch_gate(const MapView& m, uint32_t k, float p
     return false;
 }
 
-__device__ __forceinline__ bool get_patch(const MapView& m, const Window& win, double px, double py, double pz,
-                                          double qv, double& mean, double& stdev)
+// the map is K1Args::map, read by scalar loads (header: 64 bytes per lookup)
+__device__ __forceinline__ bool get_patch(const Window& win, double px, double py, double pz, double qv, double& mean,
+                                          double& stdev)
 {
+    const su16 h = kl16(KOFF(map));
+    const uint32_t width = h[12], hcells = h[13], ident = h[14], has_height = h[15];
     double lx = px, ly = py, lz = pz;    // an identity global2local is applied as the identity
-    if (!m.g2l_identity) {
-        const double* A = m.g2l;
-        lx = ((A[0] * px + A[1] * py) + A[2] * pz) + A[3];
-        ly = ((A[4] * px + A[5] * py) + A[6] * pz) + A[7];
-        lz = ((A[8] * px + A[9] * py) + A[10] * pz) + A[11];
+    if (!ident) {
+        const su16 a = kl16(KOFF(map.g2l));
+        const su8 b = kl8(KOFF(map.g2l[8]));
+        lx = ((kd(a, 0) * px + kd(a, 1) * py) + kd(a, 2) * pz) + kd(a, 3);
+        ly = ((kd(a, 4) * px + kd(a, 5) * py) + kd(a, 6) * pz) + kd(a, 7);
+        lz = ((kd(b, 0) * px + kd(b, 1) * py) + kd(b, 2) * pz) + kd(b, 3);
     }
-    double fm = floor((lx - m.offset_x) * m.inv_scale_x);
-    double fn = floor((ly - m.offset_y) * m.inv_scale_y);
-    if (!(fm >= 0.0 && fm < (double)m.width && fn >= 0.0 && fn < (double)m.height_cells)) return false;
+    double fm = floor((lx - kd(h, 4)) * kd(h, 2));
+    double fn = floor((ly - kd(h, 5)) * kd(h, 3));
+    if (!(fm >= 0.0 && fm < (double)width && fn >= 0.0 && fn < (double)hcells)) return false;
     const int im = (int)fm, in = (int)fn;
+    const float* height = has_height ? kp<const float>(kl2(KOFF(map.height)), 0) : nullptr;
     uint32_t b, e;
+    const float2* patch = kp<const float2>(h, 1);
     if (win.on && im >= win.m0 && im < win.m1 && in >= win.n0 && in < win.n1) {
         const WinCell wc = win.cells[(in - win.n0) * win.cols + (im - win.m0)];
         if (wc.count == 0) return false;
-        if (patch_gate(m, wc.begin, wc.mean0, wc.stdev0, lz, qv, mean, stdev)) return true;
+        if (patch_gate(height, wc.begin, wc.mean0, wc.stdev0, lz, qv, mean, stdev)) return true;
         b = wc.begin + 1;
         e = wc.begin + wc.count;
     } else {
-        const uint64_t cell = (uint64_t)in * m.width + (uint64_t)im;
-        b = m.cell_start[cell];
-        e = m.cell_start[cell + 1];
+        const uint32_t* cell_start = kp<const uint32_t>(h, 0);
+        const uint64_t cell = (uint64_t)in * width + (uint64_t)im;
+        b = cell_start[cell];
+        e = cell_start[cell + 1];
     }
     for (uint32_t k = b; k < e; ++k) {
-        const float2 pf = m.patch[k];
-        if (patch_gate(m, k, pf.x, pf.y, lz, qv, mean, stdev)) return true;
+        const float2 pf = patch[k];
+        if (patch_gate(height, k, pf.x, pf.y, lz, qv, mean, stdev)) return true;
     }
     return false;
 }
@@ -236,35 +315,52 @@ __device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, 
     return s2 < 1600.0 && z * z < 31.36 * s2;
 }
 
-// MAXP: bound on the contact points found (group ends); BATCH: p.m <= MAXP contacts
+// MAXP: bound on the contact points found (group ends); BATCH: p.m <= MAXP contacts.
+// StepParams (p.*) and the contacts come from scalar loads of the kernel arguments.
 template <int MAXP, bool BATCH>
-__device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const MapView& map, const Window& win, double co,
-                                                  double s, double r22, double x, double y, double z, double meas_var)
+__device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, double s, double r22, double x, double y,
+                                                  double z, double meas_var)
 {
     CMResult r;
+    // pushed contact points.  BATCH: slot = index of the contact that closed the group, so
+    // every write has a static index; the slots are summed in index order = push order.
     double cz[MAXP], cv[MAXP];
+    bool ok[MAXP];
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) ok[k] = false;
     uint32_t ncp = 0;
     bool valid = false, group_valid = true;
     double contact_ratio = 0, pose_var_avg = 0, posevar = 0;
     double pzd = 0, pzv = 0;
     const double qv = meas_var;
+    const su8 wp = kl8(KOFF(p.me2));          // me2, radius, corr, min_contacts
+    const su4 wq = kl4(KOFF(p.use_shape));    // use_shape, m, eval_mask, end_mask
+    const double radius = kd(wp, 1), corr = kd(wp, 2);
+    const uint32_t m = wq[1], eval_mask = wq[2], end_mask = wq[3];
 
+    auto push = [&](uint32_t i, double zd, double zv) {
+        if constexpr (BATCH) {
+            cz[i] = zd; cv[i] = zv; ok[i] = true;
+        } else {
+#pragma unroll
+            for (int k = 0; k < MAXP; ++k)
+                if ((uint32_t)k == ncp) { cz[k] = zd; cv[k] = zv; }
+        }
+        ++ncp;
+    };
     // the sequential part of one contact (group logic, Q7 poisoning): found/mean/stdev are
     // the map lookup of its world point (used only when the contact is evaluated)
     auto contact = [&](uint32_t i, bool found, double mean, double stdev, double wz) {
-        const ContactC& c = p.c[i];
-        if (group_valid && c.eval) {
+        const bool c_eval = (eval_mask >> i) & 1u, c_end = (end_mask >> i) & 1u;
+        if (group_valid && c_eval) {
             if (found) {
                 const double zdiff = wz - mean;
                 const double pose_var = stdev * stdev;
                 const double zvar = stdev * stdev + meas_var;
-                if (!valid && c.end && ratio_surely_significant(zdiff, zvar, p.corr)) {
+                if (!valid && c_end && ratio_surely_significant(zdiff, zvar, corr)) {
                     // single-point group: (zdiff, zvar) pushed directly
                     posevar += pose_var;
-#pragma unroll
-                    for (int k = 0; k < MAXP; ++k)
-                        if ((uint32_t)k == ncp) { cz[k] = zdiff; cv[k] = zvar; }
-                    ++ncp;
+                    push(i, zdiff, zvar);
                     group_valid = true;
                     valid = false;
                     pose_var_avg = 0;
@@ -274,7 +370,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
 #ifdef ESLAM_ABL_NO_RATIO
                 const double ratio = 1.0 + zdiff * 1e-3;
 #else
-                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * p.corr);
+                const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * corr);
 #endif
                 if (!valid) {
                     pzd = zdiff * ratio;
@@ -292,16 +388,13 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
                 group_valid = false;
             }
         }
-        if (valid && c.end) {
+        if (valid && c_end) {
             if (group_valid && contact_ratio > 1e-9) {
                 const double inv = 1.0 / contact_ratio;
                 pzd *= inv;
                 pzv *= inv;
                 posevar += pose_var_avg * inv;
-#pragma unroll
-                for (int k = 0; k < MAXP; ++k)
-                    if ((uint32_t)k == ncp) { cz[k] = pzd; cv[k] = pzv; }
-                ++ncp;
+                push(i, pzd, pzv);
             }
             group_valid = true;
             valid = false;
@@ -311,57 +404,62 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
     };
     // pose * p with pose = Translation(x, y, z) * AngleAxis(theta, UnitZ); the zero products
     // of the affine multiply are per-step constants, and "- 0.0" is exact
-    auto world = [&](const ContactC& c, double& wx, double& wy, double& wz) {
-        wx = ((co * c.px + (-s) * c.py) + c.zp) + x;
-        wy = ((s * c.px + co * c.py) + c.zp) + y;
-        wz = ((c.zz + r22 * c.pz) + z) - p.radius;
+    auto world = [&](uint32_t i, double& wx, double& wy, double& wz) {
+        su8 c;
+        su2 cpz;
+        const uint32_t off = KOFF(p.c) + i * (uint32_t)sizeof(ContactC);
+        kl8_2(off, off + (uint32_t)offsetof(ContactC, pz), c, cpz);   // px, py, zp, zz | pz
+        const double px = kd(c, 0), py = kd(c, 1), zp = kd(c, 2), zz = kd(c, 3), pz = kd(cpz, 0);
+        wx = ((co * px + (-s) * py) + zp) + x;
+        wy = ((s * px + co * py) + zp) + y;
+        wz = ((zz + r22 * pz) + z) - radius;
     };
     auto lookup = [&](double wx, double wy, double wz, double& mean, double& stdev) -> bool {
 #ifdef ESLAM_ABL_NO_MAP
         mean = 0.0; stdev = 0.05;
         return wx == wx;
 #else
-        return get_patch(map, win, wx, wy, wz, qv, mean, stdev);
+        return get_patch(win, wx, wy, wz, qv, mean, stdev);
 #endif
     };
 
     if constexpr (BATCH) {
-        // all p.m <= MAXP contacts' lookups first: independent, so their memory latencies
+        // all m <= MAXP contacts' lookups first: independent, so their memory latencies
         // overlap (a lookup the group logic then skips is harmless: pure function)
         bool fnd[MAXP];
         double mn[MAXP], sd[MAXP], wzs[MAXP];
 #pragma unroll
         for (int i = 0; i < MAXP; ++i) {
             fnd[i] = false; mn[i] = 0.0; sd[i] = 0.0; wzs[i] = 0.0;
-            if ((uint32_t)i < p.m) {
+            if ((uint32_t)i < m) {
                 double wx, wy;
-                world(p.c[i], wx, wy, wzs[i]);
-                if (p.c[i].eval) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
+                world((uint32_t)i, wx, wy, wzs[i]);
+                if ((eval_mask >> i) & 1u) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
             }
         }
 #pragma unroll
         for (int i = 0; i < MAXP; ++i) {
-            if ((uint32_t)i >= p.m) break;
+            if ((uint32_t)i >= m) break;
             contact((uint32_t)i, fnd[i], mn[i], sd[i], wzs[i]);
         }
     } else {
-        for (uint32_t i = 0; i < p.m; ++i) {
+        for (uint32_t i = 0; i < m; ++i) {
             double wx, wy, wz, mean = 0.0, stdev = 0.0;
-            world(p.c[i], wx, wy, wz);
+            world(i, wx, wy, wz);
             bool found = false;
-            if (group_valid && p.c[i].eval) found = lookup(wx, wy, wz, mean, stdev);
+            if (group_valid && ((eval_mask >> i) & 1u)) found = lookup(wx, wy, wz, mean, stdev);
             contact(i, found, mean, stdev, wz);
         }
     }
     r.ncp = ncp;
     r.posevar = posevar;
-    r.accepted = (uint64_t)ncp >= p.min_contacts;
+    r.accepted = (uint64_t)ncp >= kq(wp, 3);
     r.weight = r.zdelta = r.zvar = r.s2 = 0.0;
     if (r.accepted) {
         double d1 = 0, d2 = 0;
 #pragma unroll
         for (int k = 0; k < MAXP; ++k) {
-            if ((uint32_t)k < ncp) {
+            if (BATCH ? ok[k] : (uint32_t)k < ncp) {
                 cv[k] = 1.0 / cv[k];            // cv now holds 1/zvar
                 d1 += cz[k] * cv[k];
                 d2 += cv[k];
@@ -372,16 +470,17 @@ __device__ __forceinline__ CMResult evaluate_pose(const StepParams& p, const Map
         double s2 = 0.0;
 #pragma unroll
         for (int k = 0; k < MAXP; ++k) {
-            if ((uint32_t)k < ncp) {
+            if (BATCH ? ok[k] : (uint32_t)k < ncp) {
                 const double d = cz[k] - delta;
                 s2 += (d * d) * cv[k];
             }
         }
         r.s2 = s2;
+        const uint32_t use_shape = kl2(KOFF(p.use_shape))[0];
 #ifdef ESLAM_ABL_NO_EW
-        const double pz = p.use_shape ? 1.0 - 0.5 * s2 : 1.0;
+        const double pz = use_shape ? 1.0 - 0.5 * s2 : 1.0;
 #else
-        const double pz = p.use_shape ? dm_exp(-0.5 * s2) : 1.0;
+        const double pz = use_shape ? dm_exp(-0.5 * s2) : 1.0;
 #endif
         r.weight = pz;
         r.zdelta = -delta;
@@ -416,34 +515,38 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #endif
 
 template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH>
-__global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState s0, DevState s1, MapView map, StepParams p,
-                                                           Ctl* __restrict__ ctl, Shard* __restrict__ shards, GatherView gv)
+__global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a)
 {
+    // Inside the particle loop every argument is read by a scalar load where it is used
+    // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t n = a.p.n;
+    const uint32_t J = a.p.J;
     const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
-    const uint64_t lbase = chunk * 64ull * p.J;
+    const uint64_t lbase = chunk * 64ull * J;
+    Ctl* ctl = a.ctl;
     // a pending resample gather is fused here: read the ancestors from state[base],
     // write the updated particles to state[base ^ 1] (the latest buffer)
     const uint32_t gath = ctl->gather;
     const uint32_t cur = ctl->base ^ ctl->flip;
-    const DevState st = cur ? s1 : s0;
-    const DevState si = gath ? (ctl->base ? s1 : s0) : st;
+    const uint32_t st_off = cur ? KOFF(s[1]) : KOFF(s[0]);
+    const uint32_t si_off = gath ? (ctl->base ? KOFF(s[1]) : KOFF(s[0])) : st_off;
     const int wexp = ctl->wexp;
 
     double spread = 0.0;
     bool do_spread = false;
     double tf = 0.0, rf = 0.0;
     if (PROJECT) {
-        spread = dm_weighting_function(ctl->max_weight, 0.0, p.spread_threshold, 0.0);
-        do_spread = spread > 0 && !p.hash_use;
-        tf = p.spread_trans * spread;
-        rf = p.spread_rot * spread;
+        spread = dm_weighting_function(ctl->max_weight, 0.0, a.p.spread_threshold, 0.0);
+        do_spread = spread > 0 && !a.p.hash_use;
+        tf = a.p.spread_trans * spread;
+        rf = a.p.spread_rot * spread;
     }
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Window win;
     win.on = 0;
-    if (WEIGHT) win = stage_window(map, p, ctl, 6.0 * tf, smem + kStatsLds);
+    if (WEIGHT) win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds);
 
     double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
 #pragma unroll
@@ -452,61 +555,77 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
     uint32_t nD = 0, nTP = 0, err = 0;
     uint64_t bb[4] = {0, 0, 0, 0};      // ~key(min x), key(max x), ~key(min y), key(max y)
 
-    for (uint32_t j = 0; j < p.J; ++j) {
+    for (uint32_t j = 0; j < J; ++j) {
         const uint64_t row0 = lbase + 64ull * j;
-        if (row0 >= p.n) break;
+        if (row0 >= n) break;
         const uint64_t i = row0 + lane;
         uint32_t src = (uint32_t)i;
         const Rec* rc = nullptr;
+        uint32_t rec_anc = 0;
         if (gath) {
+            const su8 g = kl8(KOFF(gv));              // marks, row_first, anc, recs
+            const su2 gf = kl2(KOFF(gv.record));      // record, multi
+            uint32_t* marks = kp<uint32_t>(g, 0);
             // expand the segment marks of this row: inclusive max-scan + the row carry
             uint32_t m = 0;
-            if (i < p.n) { m = gv.marks[i]; if (m) gv.marks[i] = 0; }
+            if (i < n) { m = marks[i]; if (m) marks[i] = 0; }
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t t = __shfl_up(m, o, 64);
                 if ((int)lane >= o) m = m > t ? m : t;
             }
-            const uint32_t carry = gv.row_first[row0 / kRow] + 1u;
+            const uint32_t carry = kp<const uint32_t>(g, 1)[row0 / kRow] + 1u;
             m = m > carry ? m : carry;
-            src = decode_source(m - 1u, gv.multi, gv.recs, &rc);
+            src = decode_source(m - 1u, gf[1], kp<const Rec>(g, 3), &rc);
+            rec_anc = gf[0];
         }
-        if (i >= p.n) continue;
+        if (i >= n) continue;
         double x, y, th, z, zs, w, mp_in = 0.0;
         uint32_t fl_in = 0;
         if (rc) {
             x = rc->x; y = rc->y; th = rc->th; z = rc->z; zs = rc->zs; w = rc->w;
             mp_in = rc->mprob; fl_in = (uint8_t)rc->src;
         } else {
+            const StatePtrs si = kstate(si_off);
             x = si.x[src]; y = si.y[src]; th = si.th[src]; z = si.z[src]; zs = si.zs[src]; w = si.w[src];
             if (!WEIGHT && gath) { mp_in = si.mprob[src]; fl_in = si.flags[src]; }
         }
-        if (gath && gv.record) gv.anc[i] = rc ? (uint32_t)(rc->src >> 8) : (uint32_t)(p.gbase + src);
+        if (gath && rec_anc) {
+            const su2 ga = kl2(KOFF(gv.anc));
+            const uint64_t gbase = kq(kl2(KOFF(p.gbase)), 0);
+            kp<uint32_t>(ga, 0)[i] = rc ? (uint32_t)(rc->src >> 8) : (uint32_t)(gbase + src);
+        }
         const double w_in = w;
+        double mprob = 0.0;
+        uint32_t flags = 0;
         if (PROJECT) {
-            const uint64_t gi = p.gbase + i;
+            const su8 key = kl8(KOFF(p.seed));       // seed, proj_event, gbase
+            const uint64_t gi = kq(key, 2) + i;
             // draw layout: call 0 -> two Box-Muller pairs (z0, z1), (z2, sn0);
             // call 1 -> slip test + slip factor, spread pair (sn1, sn2)
-            const dm_philox_ctr d0 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 0);
-            const dm_philox_ctr d1 = dm_draw(p.seed, DM_STREAM_PROJECT, p.proj_event, gi, 1);
+            const dm_philox_ctr d0 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 0);
+            const dm_philox_ctr d1 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 1);
             double z0, z1, z2, sn0;
             dm_box_muller32(d0.v[0], d0.v[1], &z0, &z1);
             dm_box_muller32(d0.v[2], d0.v[3], &z2, &sn0);
             // odometry.getPoseDeltaSample2D() = mu + L z
-            const double dx = p.mu[0] + p.L00 * z0;
-            double dy = p.mu[1] + (p.L10 * z0 + p.L11 * z1);
-            const double dth = p.mu[2] + ((p.L20 * z0 + p.L21 * z1) + p.L22 * z2);
-            if (dm_u32(d1.v[0]) < p.slip_factor) dy *= dm_u32(d1.v[1]);
+            const su16 P = kl16(KOFF(p.mu));         // mu0 mu1 mu2 L00 L10 L11 L20 L21
+            const su8 Q = kl8(KOFF(p.L22));          // L22 slip_factor yaw max_yaw_dev
+            const double dx = kd(P, 0) + kd(P, 3) * z0;
+            double dy = kd(P, 1) + (kd(P, 4) * z0 + kd(P, 5) * z1);
+            const double dth = kd(P, 2) + ((kd(P, 6) * z0 + kd(P, 7) * z1) + kd(Q, 0) * z2);
+            if (dm_u32(d1.v[0]) < kd(Q, 1)) dy *= dm_u32(d1.v[1]);
             double s, co;
             dm_sincos(th, &s, &co);
             x += co * dx - s * dy;
             y += s * dx + co * dy;
             th += dth;
-            if (p.max_yaw_dev > 0.0) {
-                if (dm_fabs(th - p.yaw) > p.max_yaw_dev) w *= 0.7;
+            if (kd(Q, 3) > 0.0) {
+                if (dm_fabs(th - kd(Q, 2)) > kd(Q, 3)) w *= 0.7;
             }
-            z += p.z_delta;
-            zs = dm_sqrt(zs * zs + p.z_var);
+            const su4 Z = kl4(KOFF(p.z_delta));      // z_delta z_var
+            z += kd(Z, 0);
+            zs = dm_sqrt(zs * zs + kd(Z, 1));
             if (do_spread) {
                 double sn1, sn2;
                 dm_box_muller32(d1.v[2], d1.v[3], &sn1, &sn2);
@@ -514,9 +633,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
                 y += sn1 * tf + 0.0;
                 th += sn2 * rf + 0.0;
             }
-            st.x[i] = x;
-            st.y[i] = y;
-            st.th[i] = th;
         }
         if (WEIGHT) {
             double s, co;
@@ -526,10 +642,9 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
             dm_sincos(th, &s, &co);
 #endif
             const double r22 = (1.0 - co) + co;
-            const double meas_var = zs * zs + p.me2;
+            const double meas_var = zs * zs + kd(kl2(KOFF(p.me2)), 0);
             if (meas_var == 0) err = 1;
-            const CMResult r = evaluate_pose<MAXP, BATCH>(p, map, win, co, s, r22, x, y, z, meas_var);
-            double mprob;
+            const CMResult r = evaluate_pose<MAXP, BATCH>(win, co, s, r22, x, y, z, meas_var);
             uint32_t floating;
             double sw = 0.0;
             if (r.accepted) {
@@ -540,8 +655,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
 #else
                 const double pose_var = r.posevar / (double)r.ncp;
 #endif
-                const double a = zvar - pose_var;
-                double delta_var = (a < 1e-9) ? 1e-9 : a;
+                const double av = zvar - pose_var;
+                double delta_var = (av < 1e-9) ? 1e-9 : av;
                 if (!(r.zdelta * r.zdelta > delta_var)) {
                     const double gain = zvar / (zvar + r.zvar);
                     z += gain * r.zdelta;
@@ -557,7 +672,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
                 nD += 1;
                 // pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found))
                 const double inv_n = dm_recip_small(r.ncp);     // 1.0 / found, correctly rounded
-                if (!p.use_shape || r.ncp == 0) sw = dm_pow(r.weight, inv_n);
+                const uint32_t use_shape = kl2(KOFF(p.use_shape))[0];
+                if (!use_shape || r.ncp == 0) sw = dm_pow(r.weight, inv_n);
                 else sw = r.weight == 0.0 ? 0.0 : dm_exp((-0.5 * r.s2) * inv_n);
                 nTP += r.ncp;
             } else {
@@ -565,29 +681,33 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
                 mprob = 1.0;
             }
             const uint32_t bucket = r.ncp < DM_NBUCKETS - 1 ? r.ncp : DM_NBUCKETS - 1;
-            const double a = w * mprob;
-            const double a2 = a * a;
+            const double am = w * mprob;
+            const double am2 = am * am;
             // only the particle's bucket changes (adding +0.0 elsewhere, as the oracle's
             // canonical sum does, can only turn a -0.0 into +0.0: same fixed point)
 #pragma unroll
             for (int b = 0; b < DM_NBUCKETS; ++b) {
                 if (bucket == (uint32_t)b) {
-                    accA[b] = accA[b] + a;
-                    accB[b] = accB[b] + a2;
+                    accA[b] = accA[b] + am;
+                    accB[b] = accB[b] + am2;
                 }
             }
             accSW = accSW + sw;
-            st.mprob[i] = mprob;
-            st.flags[i] = (uint8_t)((r.ncp & 0x7fu) | (floating << 7));
+            flags = (r.ncp & 0x7fu) | (floating << 7);
+        } else {
+            mprob = mp_in;
+            flags = fl_in;
         }
-        if (!PROJECT && gath) {
+        // all stores of the row at the end: one scalar load of the output pointers
+        const StatePtrs st = kstate(st_off);
+        if (PROJECT || gath) {
             st.x[i] = x;
             st.y[i] = y;
             st.th[i] = th;
         }
-        if (!WEIGHT && gath) {
-            st.mprob[i] = mp_in;
-            st.flags[i] = (uint8_t)fl_in;
+        if (WEIGHT || gath) {
+            st.mprob[i] = mprob;
+            st.flags[i] = (uint8_t)flags;
         }
         if (PROJECT || WEIGHT) {
             st.z[i] = z;
@@ -611,7 +731,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(DevState
         for (int o = 32; o >= 1; o >>= 1) { const uint64_t t = __shfl_xor(v, o, 64); v = v > t ? v : t; }
         bb[q] = v;
     }
-    Shard* shb = shards + (blockIdx.x % kNShard);
+    Shard* shb = a.shards + (blockIdx.x % kNShard);
     if (lane == 0 && bb[1]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) atomicMax((unsigned long long*)&shb->bbox[q], (unsigned long long)bb[q]);
@@ -1517,8 +1637,16 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     if (blocks == 0) return hipSuccess;
     dim3 g(blocks), b(kBlock);
     const size_t lds = kStatsLds + (weight ? kWindowLds : 0);
+    K1Args args;
+    args.p = *p;
+    args.map = *map;
+    args.gv = *gv;
+    args.s[0] = s0;
+    args.s[1] = s1;
+    args.ctl = ctl;
+    args.shards = shards;
 #define ESLAM_LAUNCH(P, W, M, B) \
-    hipLaunchKernelGGL((k_project_weight<P, W, M, B>), g, b, lds, stream, s0, s1, *map, *p, ctl, shards, *gv)
+    hipLaunchKernelGGL((k_project_weight<P, W, M, B>), g, b, lds, stream, args)
     // batched contact lookups when every contact fits the MAXP-sized arrays
     if (project && !weight) ESLAM_LAUNCH(true, false, 4, false);
     else if (!project && weight) {

@@ -20,6 +20,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchsharded) run bench_sharded 600 python bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline ;;
+    benchfast) run bench 600 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
     benchshort) run bench 600 python bench.py --steps 20 --warmup 5 --cpu-steps 2 ;;
   esac
 done
