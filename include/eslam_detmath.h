@@ -57,6 +57,35 @@ DM_FN double dm_fmak(double a, double b, double k)
 #else
 DM_FN double dm_fmak(double a, double b, double k) { return __builtin_fma(a, b, k); }
 #endif
+/* fma(a, b, c) with c one of the hardware's inline constants (no register at all) */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DM_FMA_INLINE(name, val)                                                            \
+    DM_FN double name(double a, double b)                                                   \
+    {                                                                                       \
+        double r;                                                                           \
+        __asm__("v_fma_f64 %0, %1, %2, " #val : "=v"(r) : "v"(a), "v"(b));                 \
+        return r;                                                                           \
+    }
+#else
+#define DM_FMA_INLINE(name, val) DM_FN double name(double a, double b) { return __builtin_fma(a, b, (val)); }
+#endif
+DM_FMA_INLINE(dm_fma_1, 1.0)
+DM_FMA_INLINE(dm_fma_h, 0.5)
+DM_FMA_INLINE(dm_fma_mh, -0.5)
+
+/* Horner tables (highest degree first): p = c[0]; p = fma(p, u, c[i]).  Unrolled, every
+ * coefficient is a compile-time constant (dm_fmak: an SGPR pair on the device).  Keeping
+ * the tables in constant memory and scalar-loading them per evaluation was measured
+ * slower (the loads raise SGPR pressure into spills).                                  */
+#define DM_POLY_TABLE(name, n, ...) DM_CONST double name[n] = {__VA_ARGS__};
+#define DM_POLY(name, n, u) dm_horner_k(name, n, (u))
+DM_FN double dm_horner_k(const double* c, int n, double u)
+{
+    double p = c[0];
+    DM_UNROLL
+    for (int i = 1; i < n; ++i) p = dm_fmak(p, u, c[i]);
+    return p;
+}
 DM_FN double dm_sqrt(double x) { return __builtin_sqrt(x); }
 DM_FN double dm_floor(double x) { return __builtin_floor(x); }
 
@@ -94,22 +123,18 @@ DM_FN double dm_rint_small(double x)
 #define DM_INV_LN2 1.44269504088896338700e+00
 
 /* e^r on |r| <= 0.3466: Taylor series to r^13 (truncation < 6e-18 relative), fma Horner */
+DM_POLY_TABLE(dm_c_exp, 11, 1.6059043836821613e-10 /* 1/13! */, 2.08767569878681e-09 /* 1/12! */,
+              2.505210838544172e-08 /* 1/11! */, 2.755731922398589e-07 /* 1/10! */,
+              2.7557319223985893e-06 /* 1/9! */, 2.48015873015873e-05 /* 1/8! */,
+              0.0001984126984126984 /* 1/7! */, 0.001388888888888889 /* 1/6! */,
+              0.008333333333333333 /* 1/5! */, 0.041666666666666664 /* 1/4! */,
+              0.16666666666666666 /* 1/3! */)
 DM_FN double dm_exp_kernel(double r)
 {
-    double p = 1.6059043836821613e-10;          /* 1/13! */
-    p = dm_fmak(p, r, 2.08767569878681e-09);     /* 1/12! */
-    p = dm_fmak(p, r, 2.505210838544172e-08);    /* 1/11! */
-    p = dm_fmak(p, r, 2.755731922398589e-07);    /* 1/10! */
-    p = dm_fmak(p, r, 2.7557319223985893e-06);   /* 1/9!  */
-    p = dm_fmak(p, r, 2.48015873015873e-05);     /* 1/8!  */
-    p = dm_fmak(p, r, 0.0001984126984126984);    /* 1/7!  */
-    p = dm_fmak(p, r, 0.001388888888888889);     /* 1/6!  */
-    p = dm_fmak(p, r, 0.008333333333333333);     /* 1/5!  */
-    p = dm_fmak(p, r, 0.041666666666666664);     /* 1/4!  */
-    p = dm_fmak(p, r, 0.16666666666666666);      /* 1/3!  */
-    p = dm_fmak(p, r, 0.5);
-    p = dm_fmak(p, r, 1.0);
-    return dm_fmak(p, r, 1.0);
+    double p = DM_POLY(dm_c_exp, 11, r);
+    p = dm_fma_h(p, r);
+    p = dm_fma_1(p, r);
+    return dm_fma_1(p, r);
 }
 
 DM_FN double dm_exp(double x)
@@ -127,6 +152,10 @@ DM_FN double dm_exp(double x)
 /* ------------------------------------------------------------------------------------ */
 /* log                                                                                   */
 /* ------------------------------------------------------------------------------------ */
+DM_POLY_TABLE(dm_c_log, 10, 0.09523809523809523 /* 2/21 */, 0.10526315789473684 /* 2/19 */,
+              0.11764705882352941 /* 2/17 */, 0.13333333333333333 /* 2/15 */, 0.15384615384615385 /* 2/13 */,
+              0.18181818181818182 /* 2/11 */, 0.2222222222222222 /* 2/9 */, 0.2857142857142857 /* 2/7 */,
+              0.4 /* 2/5 */, 0.6666666666666666 /* 2/3 */)
 DM_FN double dm_log(double x)
 {
     if (x != x) return x;
@@ -142,16 +171,7 @@ DM_FN double dm_log(double x)
     double s = f / (2.0 + f);           /* (m-1)/(m+1), |s| <= 0.1716 */
     double z = s * s;
     /* R = 2 z/3 + 2 z^2/5 + ... + 2 z^10/21  (atanh series; truncation < 3e-17 relative) */
-    double R = 0.09523809523809523;            /* 2/21 */
-    R = dm_fmak(R, z, 0.10526315789473684);     /* 2/19 */
-    R = dm_fmak(R, z, 0.11764705882352941);     /* 2/17 */
-    R = dm_fmak(R, z, 0.13333333333333333);     /* 2/15 */
-    R = dm_fmak(R, z, 0.15384615384615385);     /* 2/13 */
-    R = dm_fmak(R, z, 0.18181818181818182);     /* 2/11 */
-    R = dm_fmak(R, z, 0.2222222222222222);      /* 2/9  */
-    R = dm_fmak(R, z, 0.2857142857142857);      /* 2/7  */
-    R = dm_fmak(R, z, 0.4);                     /* 2/5  */
-    R = dm_fmak(R, z, 0.6666666666666666);      /* 2/3  */
+    double R = DM_POLY(dm_c_log, 10, z);
     R = R * z;
     /* log(1+f) = 2 atanh(s) = 2s + s R, and 2s = f - s f  ->  f - s (f - R) */
     double l = f - s * (f - R);
@@ -167,35 +187,29 @@ DM_FN double dm_log(double x)
 #define DM_PIO2_3 2.02226624871116645580e-21   /* next 33 bits          */
 #define DM_INV_PIO2 6.36619772367581382433e-01
 
+DM_POLY_TABLE(dm_c_sin, 9, 8.22063524662433e-18 /* 1/19! */, -2.8114572543455206e-15 /* -1/17! */,
+              7.647163731819816e-13 /* 1/15! */, -1.6059043836821613e-10 /* -1/13! */,
+              2.505210838544172e-08 /* 1/11! */, -2.7557319223985893e-06 /* -1/9! */,
+              0.0001984126984126984 /* 1/7! */, -0.008333333333333333 /* -1/5! */,
+              0.16666666666666666 /* 1/3! (subtracted below) */)
 DM_FN double dm_sin_kernel(double r)   /* |r| <= pi/4, Taylor to r^19 */
 {
     double z = r * r;
-    double p = 8.22063524662433e-18;            /* 1/19! */
-    p = dm_fmak(p, z, -2.8114572543455206e-15);  /* -1/17! */
-    p = dm_fmak(p, z, 7.647163731819816e-13);    /* 1/15! */
-    p = dm_fmak(p, z, -1.6059043836821613e-10);  /* -1/13! */
-    p = dm_fmak(p, z, 2.505210838544172e-08);    /* 1/11! */
-    p = dm_fmak(p, z, -2.7557319223985893e-06);  /* -1/9! */
-    p = dm_fmak(p, z, 0.0001984126984126984);    /* 1/7!  */
-    p = dm_fmak(p, z, -0.008333333333333333);    /* -1/5! */
-    p = dm_fmak(p, z, 0.16666666666666666);      /* 1/3! (subtracted below) */
+    double p = DM_POLY(dm_c_sin, 9, z);
     return dm_fma(-r * z, p, r) ;
 }
 
+DM_POLY_TABLE(dm_c_cos, 9, 4.110317623312165e-19 /* 1/20! */, -1.5619206968586225e-16 /* -1/18! */,
+              4.779477332387385e-14 /* 1/16! */, -1.1470745597729725e-11 /* -1/14! */,
+              2.08767569878681e-09 /* 1/12! */, -2.755731922398589e-07 /* -1/10! */,
+              2.48015873015873e-05 /* 1/8! */, -0.001388888888888889 /* -1/6! */,
+              0.041666666666666664 /* 1/4! */)
 DM_FN double dm_cos_kernel(double r)   /* |r| <= pi/4, Taylor to r^20 */
 {
     double z = r * r;
-    double p = 4.110317623312165e-19;           /* 1/20! */
-    p = dm_fmak(p, z, -1.5619206968586225e-16);  /* -1/18! */
-    p = dm_fmak(p, z, 4.779477332387385e-14);    /* 1/16! */
-    p = dm_fmak(p, z, -1.1470745597729725e-11);  /* -1/14! */
-    p = dm_fmak(p, z, 2.08767569878681e-09);     /* 1/12! */
-    p = dm_fmak(p, z, -2.755731922398589e-07);   /* -1/10! */
-    p = dm_fmak(p, z, 2.48015873015873e-05);     /* 1/8!  */
-    p = dm_fmak(p, z, -0.001388888888888889);    /* -1/6! */
-    p = dm_fmak(p, z, 0.041666666666666664);     /* 1/4!  */
-    p = dm_fmak(p, z, -0.5);
-    return dm_fmak(p, z, 1.0);
+    double p = DM_POLY(dm_c_cos, 9, z);
+    p = dm_fma_mh(p, z);
+    return dm_fma_1(p, z);
 }
 
 DM_FN void dm_sincos(double x, double* s, double* c)
@@ -788,9 +802,12 @@ DM_FN double dm_limbs_to_double(const uint64_t L[4], int scale)
 #define DM_FX_SCALE 112          /* fixed-point scale of a chunk total bounded by 2^10 */
 #define DM_NBUCKETS 6            /* cpoints.size() buckets 0,1,2,3,4,>=5 (phase B)     */
 
+/* J = the largest power of two <= min(16, n_global / 2^20): from 1M particles on there are
+ * ~16384 chunks (the weighting kernel runs one chunk per wave, so the 256 CUs x 3 waves per
+ * SIMD are refilled ~5 times and the last partial round stays short)                   */
 DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
 {
-    uint64_t q = n_global / 262144u;
+    uint64_t q = n_global / 1048576u;
     uint32_t j = 1;
     while (j < 16u && (uint64_t)(j * 2u) <= q) j *= 2u;
     return j;

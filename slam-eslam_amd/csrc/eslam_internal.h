@@ -24,7 +24,7 @@ constexpr int kGatherTile = kScanTile;           // outputs per resample-gather 
 constexpr int kRow = 64;                         // outputs per row_first entry (one wave row)
 constexpr int kNShard = 16;              // statistics shards (blockIdx % kNShard)
 constexpr int kJumpBits = 11;
-constexpr int kStatsLds = 1024;          // bytes of the statistics scratch at the LDS base
+constexpr int kStatsLds = 2048;          // bytes of the statistics scratch at the LDS base
 constexpr int kWindowLds = 40 * 1024;    // bytes of the MLS window after it
 
 // one statistics shard: exact sums as 4 limbs of 32-bit columns (uint64 each)

@@ -125,6 +125,27 @@ template <class V> __device__ __forceinline__ uint64_t kq(const V& r, int k)
 template <class V> __device__ __forceinline__ double kd(const V& r, int k) { return dm_from_bits(kq(r, k)); }
 template <class T, class V> __device__ __forceinline__ T* kp(const V& r, int k) { return (T*)(uintptr_t)kq(r, k); }
 
+// ESLAM_K1_PROF (diagnostic builds only): per-region shader-clock time of K1, summed by
+// lane 0 of every wave into k1_prof[] (LDS per block, one global atomic per region).
+#ifdef ESLAM_K1_PROF
+__device__ unsigned long long k1_prof[32];      // [0,16): K1 regions, [16,32): K3b regions
+#define PROF_INIT() __shared__ unsigned long long s_prof[16]; if (threadIdx.x < 16) s_prof[threadIdx.x] = 0; \
+    uint64_t prof_t = __builtin_readcyclecounter()
+#define PROF(k) do { const uint64_t t_ = __builtin_readcyclecounter(); \
+    if ((threadIdx.x & 63u) == 0) atomicAdd(&s_prof[k], (unsigned long long)(t_ - prof_t)); prof_t = t_; } while (0)
+#define PROF_FLUSH_AT(base) do { __syncthreads(); if (threadIdx.x < 16) atomicAdd(&k1_prof[(base) + threadIdx.x], s_prof[threadIdx.x]); } while (0)
+#define PROF_FLUSH() PROF_FLUSH_AT(0)
+#define PROF_PARAM , uint64_t& prof_t, unsigned long long* s_prof
+#define PROF_ARG , prof_t, s_prof
+#else
+#define PROF_PARAM
+#define PROF_ARG
+#define PROF_INIT() do {} while (0)
+#define PROF(k) do {} while (0)
+#define PROF_FLUSH() do {} while (0)
+#define PROF_FLUSH_AT(base) do {} while (0)
+#endif
+
 // the state pointers of buffer s[b] (offset KOFF(s[b]))
 struct StatePtrs {
     double *x, *y, *th, *z, *zs, *w, *mprob;
@@ -319,7 +340,7 @@ __device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, 
 // StepParams (p.*) and the contacts come from scalar loads of the kernel arguments.
 template <int MAXP, bool BATCH>
 __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, double s, double r22, double x, double y,
-                                                  double z, double meas_var)
+                                                  double z, double meas_var PROF_PARAM)
 {
     CMResult r;
     // pushed contact points.  BATCH: slot = index of the contact that closed the group, so
@@ -437,11 +458,13 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
                 if ((eval_mask >> i) & 1u) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
             }
         }
+        PROF(6);
 #pragma unroll
         for (int i = 0; i < MAXP; ++i) {
             if ((uint32_t)i >= m) break;
             contact((uint32_t)i, fnd[i], mn[i], sd[i], wzs[i]);
         }
+        PROF(7);
     } else {
         for (uint32_t i = 0; i < m; ++i) {
             double wx, wy, wz, mean = 0.0, stdev = 0.0;
@@ -522,17 +545,16 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t n = a.p.n;
     const uint32_t J = a.p.J;
-    const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
-    const uint64_t lbase = chunk * 64ull * J;
+    const uint64_t csz = 64ull * J;
+    const uint64_t nchunks = (n + csz - 1) / csz;
     Ctl* ctl = a.ctl;
     // a pending resample gather is fused here: read the ancestors from state[base],
     // write the updated particles to state[base ^ 1] (the latest buffer)
     const uint32_t gath = ctl->gather;
     const uint32_t cur = ctl->base ^ ctl->flip;
-    const uint32_t st_off = cur ? KOFF(s[1]) : KOFF(s[0]);
-    const uint32_t si_off = gath ? (ctl->base ? KOFF(s[1]) : KOFF(s[0])) : st_off;
+    const uint32_t st_off = __builtin_amdgcn_readfirstlane(cur ? KOFF(s[1]) : KOFF(s[0]));
+    const uint32_t si_off = __builtin_amdgcn_readfirstlane(gath ? (ctl->base ? KOFF(s[1]) : KOFF(s[0])) : st_off);
     const int wexp = ctl->wexp;
-
     double spread = 0.0;
     bool do_spread = false;
     double tf = 0.0, rf = 0.0;
@@ -548,12 +570,25 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     win.on = 0;
     if (WEIGHT) win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds);
 
+    // order-free per-lane state, kept across chunks
+    double maxm = 0.0;
+    uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
+    uint64_t bb[4] = {0, 0, 0, 0};      // ~key(min x), key(max x), ~key(min y), key(max y)
+    uint64_t limb = 0;                  // lane t < 52: column t & 3 of exact accumulator t >> 2
+    const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
+
+    // Persistent waves stride over the canonical chunks (64 x J particles), so the last
+    // round is one chunk long whatever N is.  Chunk sums are exact (fixed point), hence the
+    // result does not depend on which wave took which chunk.
+    PROF_INIT();
+    PROF(0);
+    const uint64_t wstride = (uint64_t)gridDim.x * kWaves;
+    for (uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave; chunk < nchunks; chunk += wstride) {
+    const uint64_t lbase = chunk * csz;
     double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
 #pragma unroll
     for (int b = 0; b < DM_NBUCKETS; ++b) { accA[b] = 0.0; accB[b] = 0.0; }
-    double accSW = 0.0, maxm = 0.0;
-    uint32_t nD = 0, nTP = 0, err = 0;
-    uint64_t bb[4] = {0, 0, 0, 0};      // ~key(min x), key(max x), ~key(min y), key(max y)
+    double accSW = 0.0;
 
     for (uint32_t j = 0; j < J; ++j) {
         const uint64_t row0 = lbase + 64ull * j;
@@ -579,6 +614,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             src = decode_source(m - 1u, gf[1], kp<const Rec>(g, 3), &rc);
             rec_anc = gf[0];
         }
+        PROF(1);
         if (i >= n) continue;
         double x, y, th, z, zs, w, mp_in = 0.0;
         uint32_t fl_in = 0;
@@ -608,6 +644,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             double z0, z1, z2, sn0;
             dm_box_muller32(d0.v[0], d0.v[1], &z0, &z1);
             dm_box_muller32(d0.v[2], d0.v[3], &z2, &sn0);
+            PROF(2);
             // odometry.getPoseDeltaSample2D() = mu + L z
             const su16 P = kl16(KOFF(p.mu));         // mu0 mu1 mu2 L00 L10 L11 L20 L21
             const su8 Q = kl8(KOFF(p.L22));          // L22 slip_factor yaw max_yaw_dev
@@ -633,6 +670,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
                 y += sn1 * tf + 0.0;
                 th += sn2 * rf + 0.0;
             }
+            PROF(3);
         }
         if (WEIGHT) {
             double s, co;
@@ -641,10 +679,12 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
 #else
             dm_sincos(th, &s, &co);
 #endif
+            PROF(4);
             const double r22 = (1.0 - co) + co;
             const double meas_var = zs * zs + kd(kl2(KOFF(p.me2)), 0);
             if (meas_var == 0) err = 1;
-            const CMResult r = evaluate_pose<MAXP, BATCH>(win, co, s, r22, x, y, z, meas_var);
+            const CMResult r = evaluate_pose<MAXP, BATCH>(win, co, s, r22, x, y, z, meas_var PROF_ARG);
+            PROF(8);
             uint32_t floating;
             double sw = 0.0;
             if (r.accepted) {
@@ -694,6 +734,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             }
             accSW = accSW + sw;
             flags = (r.ncp & 0x7fu) | (floating << 7);
+            PROF(9);
         } else {
             mprob = mp_in;
             flags = fl_in;
@@ -721,7 +762,30 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             bb[2] = bb[2] > ~ky ? bb[2] : ~ky;
             bb[3] = bb[3] > ky ? bb[3] : ky;
         }
+        PROF(10);
     }
+
+    if (WEIGHT) {
+        // chunk totals (sub-lane sums + xor butterfly) -> exact fixed point -> lane columns
+#pragma unroll
+        for (int q = 0; q < 2 * DM_NBUCKETS + 1; ++q) {
+            double v = q < DM_NBUCKETS ? accA[q] : (q < 2 * DM_NBUCKETS ? accB[q - DM_NBUCKETS] : accSW);
+            const int scale = q < DM_NBUCKETS ? sa : (q < 2 * DM_NBUCKETS ? sb : DM_FX_SCALE);
+            if (__ballot(v != 0.0) != 0ull) {
+                v = wave_sum_butterfly(v);
+                uint32_t l[4] = {0, 0, 0, 0};
+                if (v != v) flag |= 1u << q;
+                else if (!dm_isfinite(v)) flag |= 1u << (q + 16);
+                else dm_fx128_limbs(v, scale, l);
+                if ((lane >> 2) == (uint32_t)q) {
+                    const uint32_t c = lane & 3u;
+                    limb += c == 0 ? l[0] : (c == 1 ? l[1] : (c == 2 ? l[2] : l[3]));
+                }
+            }
+        }
+    }
+        PROF(11);
+    }   // chunk loop
 
     // bounding box of the cloud for the next step's LDS window (exact maxima, any order)
 #pragma unroll
@@ -739,47 +803,24 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
 
     if (!WEIGHT) return;
 
-    // ---- exact statistics: chunk totals -> fixed point -> block -> sharded atomics ----
+    // ---- exact statistics: wave columns -> block (LDS) -> sharded atomics ----
     struct StatsLds {
-        uint32_t limb[kWaves][2 * DM_NBUCKETS + 1][4];
+        uint64_t limb[kWaves][(2 * DM_NBUCKETS + 1) * 4];
         uint32_t flag[kWaves];
         uint32_t cnt[kWaves][2];
         double mx[kWaves];
     };
     static_assert(sizeof(StatsLds) <= kStatsLds, "stats scratch");
     StatsLds& sl = *reinterpret_cast<StatsLds*>(smem);
-    auto& s_limb = sl.limb;
-    auto& s_flag = sl.flag;
-    auto& s_cnt = sl.cnt;
-    auto& s_max = sl.mx;
-    uint32_t flag = 0;
-    const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
-#pragma unroll
-    for (int q = 0; q < 2 * DM_NBUCKETS + 1; ++q) {
-        double v = q < DM_NBUCKETS ? accA[q] : (q < 2 * DM_NBUCKETS ? accB[q - DM_NBUCKETS] : accSW);
-        const int scale = q < DM_NBUCKETS ? sa : (q < 2 * DM_NBUCKETS ? sb : DM_FX_SCALE);
-        uint32_t l[4] = {0, 0, 0, 0};
-        if (__ballot(v != 0.0) != 0ull) {
-            v = wave_sum_butterfly(v);
-            if (v != v) flag |= 1u << q;
-            else if (!dm_isfinite(v)) flag |= 1u << (q + 16);
-            else dm_fx128_limbs(v, scale, l);
-        }
-        if (lane == 0) {
-            s_limb[wave][q][0] = l[0];
-            s_limb[wave][q][1] = l[1];
-            s_limb[wave][q][2] = l[2];
-            s_limb[wave][q][3] = l[3];
-        }
-    }
     const double wmax = wave_max_butterfly(maxm);
     const uint32_t wD = wave_sum_u32(nD), wTP = wave_sum_u32(nTP);
     const uint32_t werr = __ballot(err != 0) != 0ull ? 1u : 0u;
+    if (lane < (2 * DM_NBUCKETS + 1) * 4) sl.limb[wave][lane] = limb;
     if (lane == 0) {
-        s_flag[wave] = flag | (werr << 31);
-        s_cnt[wave][0] = wD;
-        s_cnt[wave][1] = wTP;
-        s_max[wave] = wmax;
+        sl.flag[wave] = flag | (werr << 31);
+        sl.cnt[wave][0] = wD;
+        sl.cnt[wave][1] = wTP;
+        sl.mx[wave] = wmax;
     }
     __syncthreads();
     Shard* sh = shb;
@@ -788,7 +829,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         const int q = t >> 2, j = t & 3;
         uint64_t v = 0;
 #pragma unroll
-        for (int wv = 0; wv < kWaves; ++wv) v += s_limb[wv][q][j];
+        for (int wv = 0; wv < kWaves; ++wv) v += sl.limb[wv][t];
         if (v) {
             uint64_t* dst = q < DM_NBUCKETS ? &sh->A[q][j] : (q < 2 * DM_NBUCKETS ? &sh->B[q - DM_NBUCKETS][j] : &sh->SW[j]);
             atomicAdd((unsigned long long*)dst, (unsigned long long)v);
@@ -798,10 +839,10 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         uint32_t f = 0;
         double mx = 0.0;
         for (int wv = 0; wv < kWaves; ++wv) {
-            d += s_cnt[wv][0];
-            tp += s_cnt[wv][1];
-            f |= s_flag[wv];
-            mx = (mx < s_max[wv]) ? s_max[wv] : mx;
+            d += sl.cnt[wv][0];
+            tp += sl.cnt[wv][1];
+            f |= sl.flag[wv];
+            mx = (mx < sl.mx[wv]) ? sl.mx[wv] : mx;
         }
         if (d) atomicAdd((unsigned long long*)&sh->D, (unsigned long long)d);
         if (tp) atomicAdd((unsigned long long*)&sh->TP, (unsigned long long)tp);
@@ -809,6 +850,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         if (f & 0x7fffffffu) atomicOr((unsigned long long*)&sh->flags, (unsigned long long)(f & 0x7fffffffu));
         if (f >> 31) atomicOr((unsigned long long*)&sh->err, 1ull);
     }
+    PROF(12);
+    PROF_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1118,8 +1161,18 @@ __device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uin
     return run;
 }
 
-struct TileMarks {                       // LDS scratch of the mark flush
+constexpr int kWaveDraws = 1056;         // stratified draws one wave evaluates in LDS (K3b)
+
+// K3b's LDS: the staged weights, then the wave's draws, then the staged marks (each dead
+// before the next is written)
+union K3bLds {
+    double v[kStageV];
+    uint64_t T[kWaves][kWaveDraws];
     uint32_t m[kMarkStage];
+};
+
+struct TileMarks {                       // LDS scratch of the mark flush
+    uint32_t* m;                         // kMarkStage words
     uint64_t L, H;
 };
 
@@ -1231,35 +1284,105 @@ __global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ 
 }
 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
+// Draw counting (#{k : T_k <= C}) for the particles of one wave: when the wave's outputs
+// [K0, K1) number at most kWaveDraws, its lanes evaluate T_k for all of them in parallel
+// (lane l: k = K0 + l + 64 j, one jump then a 64-stride minstd step), store them in LDS and
+// every particle binary-searches its cumulative sum there.  No per-lane serial walk, no
+// divergence.  Heavier waves fall back to the per-lane cursor.
+// #{j < D : sT[j] <= v[r]} for the kScanItems targets at once (sT sorted): the searches
+// advance together so their LDS reads are in flight together
+__device__ __forceinline__ void wave_count_le(const uint64_t* sT, uint32_t D, const uint64_t (&v)[kScanItems],
+                                              uint32_t (&pos)[kScanItems])
+{
+    uint32_t top = 0;
+    if (D) { top = 1; while (top * 2 <= D) top *= 2; }
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) pos[r] = 0;
+    for (uint32_t step = top; step > 0; step >>= 1) {
+        uint64_t t[kScanItems];
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) t[r] = pos[r] + step <= D ? sT[pos[r] + step - 1] : ~0ull;
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) if (pos[r] + step <= D && t[r] <= v[r]) pos[r] += step;
+    }
+}
+
+// K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
 __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                      const uint64_t* __restrict__ tile_sum, uint32_t* __restrict__ marks,
                                                      uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt)
 {
     __shared__ uint64_t s_wtot[kWaves];
-    __shared__ double s_v[kStageV];
+    __shared__ K3bLds s_u;
     __shared__ TileMarks s_tm;
     if (!ctl->resample) return;
-    const uint32_t tid = threadIdx.x;
+    PROF_INIT();
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * kScanTile;
+    if (tid == 0) s_tm.m = s_u.m;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const int k = r * kBlock + (int)tid;
         const uint64_t i = t0 + (uint64_t)k;
-        s_v[skew(k)] = i < sp.n ? st.w[i] : 0.0;
+        s_u.v[skew(k)] = i < sp.n ? st.w[i] : 0.0;
     }
     __syncthreads();
+    PROF(0);
     const int shift = ctl->scan_shift;
     uint64_t c[kScanItems];
-    const uint64_t run = blocked_fx(s_v, shift, c);
-    const uint64_t base = tiles_before(tile_sum, tile, s_wtot) + block_excl(run, s_wtot);
+    const uint64_t run = blocked_fx(s_u.v, shift, c);
+    PROF(1);
+    const uint64_t tb = tiles_before(tile_sum, tile, s_wtot);
+    PROF(2);
+    const uint64_t base = tb + block_excl(run, s_wtot);     // (syncs: s_u.v is dead after it)
+    PROF(3);
 
     const uint64_t N = sp.n_global;
+    const uint32_t xs = ctl->minstd_start;
+    const double dN = (double)N;
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
-    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt, 0};
-    cur.seek(base);
-    uint64_t lo = i0 == 0 ? 0 : cur.k;
+    // the wave's cumulative range (wlo, whi] and its draws [K0, K1)
+    const uint64_t wlo = __shfl(base, 0, 64), whi = __shfl(base + run, 63, 64);
+    uint64_t kk = 0;
+    if (lane < 2) kk = count_draws_le(lane == 0 ? wlo : whi, N, xs, shift, jt);
+    const uint64_t K0 = __shfl(kk, 0, 64), K1 = __shfl(kk, 1, 64);
+    const uint64_t D = K1 - K0;
+    uint64_t hi_r[kScanItems];
+    uint64_t lo;
+    if (D <= (uint64_t)kWaveDraws) {
+        uint64_t* sT = s_u.T[wave];
+        if (K0 + lane < K1) {
+            uint32_t x = dm_mulmod31(jump_pow(jt, K0 + lane + 1), xs);
+            const uint32_t a64 = jt[64];                       // A^64
+#pragma unroll 4
+            for (uint64_t k = K0 + lane; k < K1; k += 64) {
+                sT[k - K0] = fx_shift(((double)k + dm_minstd_uniform(x)) / dN, shift);
+                x = dm_mulmod31(x, a64);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint64_t v[kScanItems];
+        uint32_t pos[kScanItems];
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) v[r] = base + c[r];
+        wave_count_le(sT, (uint32_t)D, v, pos);
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) hi_r[r] = K0 + pos[r];
+        const uint64_t prev = __shfl_up(hi_r[kScanItems - 1], 1, 64);
+        lo = lane == 0 ? K0 : prev;
+    } else {
+        DrawCursor cur{0, N, 0u, xs, shift, dN, jt, 0};
+        cur.seek(base);
+        lo = cur.k;
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) hi_r[r] = i0 + r < sp.n ? cur.advance(base + c[r]) : cur.k;
+    }
+    PROF(4);
+    if (i0 == 0) lo = 0;
     if (tid == 0) s_tm.L = lo;
     uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
     uint32_t val[kScanItems];
@@ -1269,7 +1392,7 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
         seg_lo[r] = seg_hi[r] = 0;
         val[r] = (uint32_t)(i + 1);
         if (i < sp.n) {
-            uint64_t hi = cur.advance(base + c[r]);
+            uint64_t hi = hi_r[r];
             if (i == N - 1) {
                 if (hi < N) atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
                 hi = N;
@@ -1280,8 +1403,12 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
             lo = hi;
         }
     }
+    PROF(5);
     __syncthreads();
+    PROF(6);
     flush_marks(s_tm, marks, tile_first, seg_lo, seg_hi, val);
+    PROF(7);
+    PROF_FLUSH_AT(16);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1308,9 +1435,11 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
                                                            uint2* __restrict__ range, uint64_t* __restrict__ first_last)
 {
     __shared__ uint64_t s_wtot[kWaves];
-    __shared__ double s_v[kStageV];
+    __shared__ K3bLds s_u;
     __shared__ TileMarks s_tm;
+    double* s_v = s_u.v;
     if (!ctl->resample) return;
+    if (threadIdx.x == 0) s_tm.m = s_u.m;
     const uint32_t tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
@@ -1627,15 +1756,18 @@ __global__ void k_selftest_math(int fn, const double* x, const double* y, double
 // ---------------------------------------------------------------------------------------
 using namespace eslam_dev;
 
+// One canonical chunk per wave (dm_chunk_rows sizes the chunks so that there are ~16k of
+// them from 1M particles on).  A persistent grid striding over chunks was measured slower:
+// its loop state spills SGPRs, and the LDS window it saves is staged from L2 anyway.
+static uint32_t k1_grid(uint64_t chunks) { return (uint32_t)((chunks + kWaves - 1) / kWaves); }
+
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
                                                   const GatherView* gv, hipStream_t stream)
 {
     const uint64_t csz = 64ull * p->J;
     const uint64_t chunks = (p->n + csz - 1) / csz;
-    const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
-    if (blocks == 0) return hipSuccess;
-    dim3 g(blocks), b(kBlock);
+    if (chunks == 0) return hipSuccess;
     const size_t lds = kStatsLds + (weight ? kWindowLds : 0);
     K1Args args;
     args.p = *p;
@@ -1645,8 +1777,9 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     args.s[1] = s1;
     args.ctl = ctl;
     args.shards = shards;
-#define ESLAM_LAUNCH(P, W, M, B) \
-    hipLaunchKernelGGL((k_project_weight<P, W, M, B>), g, b, lds, stream, args)
+#define ESLAM_LAUNCH(P, W, M, B)                                                                      \
+    hipLaunchKernelGGL((k_project_weight<P, W, M, B>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
+                       stream, args)
     // batched contact lookups when every contact fits the MAXP-sized arrays
     if (project && !weight) ESLAM_LAUNCH(true, false, 4, false);
     else if (!project && weight) {
@@ -1805,3 +1938,13 @@ extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n
     hipFreeAsync(tmp, stream);
     return e;
 }
+
+#ifdef ESLAM_K1_PROF
+// diagnostic builds: read and clear the K1 region clocks
+extern "C" int eslam_debug_k1_prof(unsigned long long* out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(k1_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    static const unsigned long long zero[32] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(k1_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
