@@ -137,16 +137,23 @@ DM_FN double dm_exp_kernel(double r)
     return dm_fma_1(p, r);
 }
 
+/* Branch-free on the device's hot path: the special cases are selected afterwards (same
+ * values), so several calls interleave in one basic block; only a result outside the
+ * normal range takes dm_ldexp.                                                          */
 DM_FN double dm_exp(double x)
 {
-    if (x != x) return x;
-    if (x > 709.782712893384) return dm_from_bits(0x7ff0000000000000ull);
-    if (x < -745.1332191019412) return 0.0;
-    double kd = dm_rint_small(x * DM_INV_LN2);
-    double hi = x - kd * DM_LN2_HI;   /* exact: kd has <= 11 bits, LN2_HI 32 bits */
+    const int nan_ = x != x, over = x > 709.782712893384, under = x < -745.1332191019412;
+    const double xs = (nan_ | over | under) ? 0.0 : x;
+    double kd = dm_rint_small(xs * DM_INV_LN2);
+    double hi = xs - kd * DM_LN2_HI;   /* exact: kd has <= 11 bits, LN2_HI 32 bits */
     double r = hi - kd * DM_LN2_LO;
-    double p = dm_exp_kernel(r);
-    return dm_ldexp(p, (int)kd);
+    double p = dm_exp_kernel(r);       /* in [0.7, 1.42] */
+    const int ki = (int)kd;
+    /* p * 2^ki is normal (exact) for -1021 <= ki <= 1022: what dm_ldexp returns there */
+    double res = (ki >= -1021 && ki <= 1022) ? p * dm_pow2i(ki) : dm_ldexp(p, ki);
+    res = under ? 0.0 : res;
+    res = over ? dm_from_bits(0x7ff0000000000000ull) : res;
+    return nan_ ? x : res;
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -158,15 +165,18 @@ DM_POLY_TABLE(dm_c_log, 10, 0.09523809523809523 /* 2/21 */, 0.10526315789473684 
               0.4 /* 2/5 */, 0.6666666666666666 /* 2/3 */)
 DM_FN double dm_log(double x)
 {
-    if (x != x) return x;
-    if (x <= 0.0) return x == 0.0 ? -dm_from_bits(0x7ff0000000000000ull) : dm_from_bits(0x7ff8000000000000ull);
-    if (!dm_isfinite(x)) return x;
-    int k = 0;
-    uint64_t b = dm_bits(x);
-    if ((b >> 52) == 0) { x *= 18014398509481984.0; /* 2^54 */ b = dm_bits(x); k = -54; }
-    k += (int)(b >> 52) - 1023;
+    /* branch-free: NaN, x <= 0 and +inf are selected at the end (same values) */
+    const int special = !(x > 0.0) || !dm_isfinite(x);
+    double xs = special ? 1.0 : x;
+    uint64_t b = dm_bits(xs);
+    const int sub = (b >> 52) == 0;
+    xs = sub ? xs * 18014398509481984.0 /* 2^54 */ : xs;
+    b = dm_bits(xs);
+    int k = (sub ? -54 : 0) + (int)(b >> 52) - 1023;
     double m = dm_from_bits((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull); /* [1,2) */
-    if (m > 1.4142135623730951) { m *= 0.5; k += 1; }
+    const int big = m > 1.4142135623730951;
+    m = big ? m * 0.5 : m;
+    k += big;
     double f = m - 1.0;                 /* exact (Sterbenz) */
     double s = f / (2.0 + f);           /* (m-1)/(m+1), |s| <= 0.1716 */
     double z = s * s;
@@ -176,7 +186,11 @@ DM_FN double dm_log(double x)
     /* log(1+f) = 2 atanh(s) = 2s + s R, and 2s = f - s f  ->  f - s (f - R) */
     double l = f - s * (f - R);
     double kd = (double)k;
-    return kd * DM_LN2_HI + (l + kd * DM_LN2_LO);
+    const double res = kd * DM_LN2_HI + (l + kd * DM_LN2_LO);
+    if (!special) return res;
+    if (x != x) return x;
+    if (x <= 0.0) return x == 0.0 ? -dm_from_bits(0x7ff0000000000000ull) : dm_from_bits(0x7ff8000000000000ull);
+    return x;                           /* +inf */
 }
 
 /* ------------------------------------------------------------------------------------ */
@@ -212,18 +226,26 @@ DM_FN double dm_cos_kernel(double r)   /* |r| <= pi/4, Taylor to r^20 */
     return dm_fma_1(p, z);
 }
 
+/* quadrant q of (sin, cos) from the kernels on the reduced argument, by selects */
+DM_FN void dm_quadrant(int q, double sr, double cr, double* s, double* c)
+{
+    const int swap = q & 1, neg_s = q & 2, neg_c = (q == 1) | (q == 2);
+    const double ss = swap ? cr : sr, cc = swap ? sr : cr;
+    *s = neg_s ? -ss : ss;
+    *c = neg_c ? -cc : cc;
+}
+
 DM_FN void dm_sincos(double x, double* s, double* c)
 {
-    if (!dm_isfinite(x)) { *s = x - x; *c = x - x; return; }
-    double n = dm_rint_small(x * DM_INV_PIO2);
-    if (dm_fabs(n) > 1048576.0) n = dm_floor(x * DM_INV_PIO2 + 0.5); /* huge |x|: deterministic, inexact */
-    double r = ((x - n * DM_PIO2_1) - n * DM_PIO2_2) - n * DM_PIO2_3;
+    const int fin = dm_isfinite(x);
+    const double xs = fin ? x : 0.0;
+    double n = dm_rint_small(xs * DM_INV_PIO2);
+    n = dm_fabs(n) > 1048576.0 ? dm_floor(xs * DM_INV_PIO2 + 0.5) : n; /* huge |x|: deterministic, inexact */
+    double r = ((xs - n * DM_PIO2_1) - n * DM_PIO2_2) - n * DM_PIO2_3;
     double sr = dm_sin_kernel(r), cr = dm_cos_kernel(r);
     int64_t q = (int64_t)(n - 4.0 * dm_floor(n * 0.25));  /* n mod 4 in [0,3] */
-    if (q == 0) { *s = sr; *c = cr; }
-    else if (q == 1) { *s = cr; *c = -sr; }
-    else if (q == 2) { *s = -sr; *c = -cr; }
-    else { *s = -cr; *c = sr; }
+    dm_quadrant((int)q, sr, cr, s, c);
+    if (!fin) { *s = x - x; *c = x - x; }
 }
 
 /* 1.0 / k for k = 0..32 (correctly rounded, as the division; k = 0 -> inf) */
@@ -357,9 +379,12 @@ DM_FN double dm_normal_pdf_cdf_ratio(double z, double s)
 /* ------------------------------------------------------------------------------------ */
 typedef struct { uint32_t v[4]; } dm_philox_ctr;
 
+#ifndef ESLAM_ABL_PHILOX_ROUNDS          /* ablation builds only (timing, wrong bits) */
+#define ESLAM_ABL_PHILOX_ROUNDS 10
+#endif
 DM_FN dm_philox_ctr dm_philox4x32_10(dm_philox_ctr c, uint32_t k0, uint32_t k1)
 {
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < ESLAM_ABL_PHILOX_ROUNDS; ++r) {
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         uint64_t p0 = (uint64_t)0xD2511F53u * c.v[0];
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c.v[2];
@@ -403,11 +428,7 @@ DM_FN void dm_sincos2pi(double u, double* s, double* c)
     const double q = dm_floor(t + 0.5);
     const double r = (t - q) * 1.5707963267948966;
     const double sr = dm_sin_kernel(r), cr = dm_cos_kernel(r);
-    const int qi = (int)q & 3;
-    if (qi == 0) { *s = sr; *c = cr; }
-    else if (qi == 1) { *s = cr; *c = -sr; }
-    else if (qi == 2) { *s = -sr; *c = -cr; }
-    else { *s = -cr; *c = sr; }
+    dm_quadrant((int)q & 3, sr, cr, s, c);
 }
 
 /* Box-Muller from two 32-bit words (the project / init draw layout) */

@@ -178,11 +178,26 @@ struct alignas(16) WinCell {
     uint32_t begin, count;
 };
 
+// The window's bounds stay in LDS (k1_win) and are re-read where used: held in registers
+// across the particle loop they would be 6 more long-lived SGPRs, which K1 cannot afford.
+__shared__ __attribute__((aligned(16))) int k1_win[8];   // on, m0, m1, n0, n1, cols
+
 struct Window {
-    int on;
-    int m0, m1, n0, n1, cols;            // cell range [m0,m1) x [n0,n1)
+    int on;                              // staged (block-uniform)
     const WinCell* cells;                // rows x cols (LDS)
 };
+
+struct WinBounds {
+    int on, m0, m1, n0, n1, cols;        // cell range [m0,m1) x [n0,n1)
+};
+__device__ __forceinline__ WinBounds win_bounds()
+{
+    typedef int vi4 __attribute__((ext_vector_type(4)));
+    typedef int vi2 __attribute__((ext_vector_type(2)));
+    const vi4 a = *reinterpret_cast<const volatile vi4*>(&k1_win[0]);
+    const vi2 b = *reinterpret_cast<const volatile vi2*>(&k1_win[4]);
+    return WinBounds{a.x, a.y, a.z, a.w, b.x, b.y};
+}
 
 __device__ __forceinline__ bool patch_gate(const float* height, uint32_t k, float pmf, float psf, double lz, double qv,
                                            double& mean, double& stdev)
@@ -222,8 +237,9 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     const float* height = has_height ? kp<const float>(kl2(KOFF(map.height)), 0) : nullptr;
     uint32_t b, e;
     const float2* patch = kp<const float2>(h, 1);
-    if (win.on && im >= win.m0 && im < win.m1 && in >= win.n0 && in < win.n1) {
-        const WinCell wc = win.cells[(in - win.n0) * win.cols + (im - win.m0)];
+    const WinBounds wb = win_bounds();
+    if (wb.on && im >= wb.m0 && im < wb.m1 && in >= wb.n0 && in < wb.n1) {
+        const WinCell wc = win.cells[(in - wb.n0) * wb.cols + (im - wb.m0)];
         if (wc.count == 0) return false;
         if (patch_gate(height, wc.begin, wc.mean0, wc.stdev0, lz, qv, mean, stdev)) return true;
         b = wc.begin + 1;
@@ -257,7 +273,7 @@ __device__ __forceinline__ double key_value(uint64_t k)
 __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl* ctl, double extra_margin,
                                unsigned char* lds)
 {
-    __shared__ int s_w[8];
+    int* s_w = k1_win;
     Window w;
     w.on = 0;
     if (threadIdx.x == 0) {
@@ -296,12 +312,12 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
     }
     __syncthreads();
     if (!s_w[0]) return w;
-    w.m0 = s_w[1]; w.m1 = s_w[2]; w.n0 = s_w[3]; w.n1 = s_w[4]; w.cols = s_w[5];
+    const int wm0 = s_w[1], wn0 = s_w[3], wn1 = s_w[4], wcols = s_w[5];
     WinCell* cells = reinterpret_cast<WinCell*>(lds);
-    const int ncell = (w.n1 - w.n0) * w.cols;
+    const int ncell = (wn1 - wn0) * wcols;
     for (int t = threadIdx.x; t < ncell; t += kBlock) {
-        const int r = t / w.cols, c = t - r * w.cols;
-        const uint64_t cell = (uint64_t)(w.n0 + r) * m.width + (uint64_t)(w.m0 + c);
+        const int r = t / wcols, c = t - r * wcols;
+        const uint64_t cell = (uint64_t)(wn0 + r) * m.width + (uint64_t)(wm0 + c);
         const uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
         WinCell wc;
         wc.begin = b;
@@ -577,13 +593,11 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     uint64_t limb = 0;                  // lane t < 52: column t & 3 of exact accumulator t >> 2
     const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
 
-    // Persistent waves stride over the canonical chunks (64 x J particles), so the last
-    // round is one chunk long whatever N is.  Chunk sums are exact (fixed point), hence the
-    // result does not depend on which wave took which chunk.
+    // one canonical chunk (64 x J particles) per wave; its totals go to exact fixed point
     PROF_INIT();
     PROF(0);
-    const uint64_t wstride = (uint64_t)gridDim.x * kWaves;
-    for (uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave; chunk < nchunks; chunk += wstride) {
+    const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
+    if (chunk < nchunks) {
     const uint64_t lbase = chunk * csz;
     double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
 #pragma unroll
@@ -785,7 +799,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         }
     }
         PROF(11);
-    }   // chunk loop
+    }
 
     // bounding box of the cloud for the next step's LDS window (exact maxima, any order)
 #pragma unroll
