@@ -45,6 +45,21 @@ __device__ __forceinline__ double wave_max_butterfly(double v)
     return v;
 }
 
+// inclusive max-scan over the 64 lanes with DPP (VALU lane moves, no LDS round trips):
+// row_shr 1,2,4,8 inside each row of 16, then row_bcast:15 and row_bcast:31 across rows.
+// 0 is the identity (lanes without a source keep it).
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t m)
+{
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x111, 0xf, 0xf, false); m = m > t ? m : t;   // row_shr:1
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x112, 0xf, 0xf, false); m = m > t ? m : t;   // row_shr:2
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x114, 0xf, 0xf, false); m = m > t ? m : t;   // row_shr:4
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x118, 0xf, 0xf, false); m = m > t ? m : t;   // row_shr:8
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x142, 0xa, 0xf, false); m = m > t ? m : t;   // row_bcast:15
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x143, 0xc, 0xf, false); m = m > t ? m : t;   // row_bcast:31
+    return m;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
 #pragma unroll
@@ -413,6 +428,10 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
                     contact_ratio = 0;
                     return;
                 }
+#ifdef ESLAM_K1_PROF
+                if ((threadIdx.x & 63u) == __builtin_ctzll(__ballot(1))) atomicAdd(&k1_prof[14], 1ull);
+                atomicAdd(&k1_prof[15], 1ull);
+#endif
 #ifdef ESLAM_ABL_NO_RATIO
                 const double ratio = 1.0 + zdiff * 1e-3;
 #else
@@ -627,11 +646,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             // expand the segment marks of this row: inclusive max-scan + the row carry
             uint32_t m = 0;
             if (i < n) { m = marks[i]; if (m) marks[i] = 0; }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(m, o, 64);
-                if ((int)lane >= o) m = m > t ? m : t;
-            }
+            m = wave_incl_max_u32(m);
             const uint32_t carry = kp<const uint32_t>(g, 1)[row0 / kRow] + 1u;
             m = m > carry ? m : carry;
             src = decode_source(m - 1u, gf[1], kp<const Rec>(g, 3), &rc);
@@ -1595,12 +1610,7 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
         run = run > v ? run : v;
         mk[r] = run;
     }
-    uint32_t tincl = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t x = __shfl_up(tincl, o, 64);
-        if ((int)lane >= o) tincl = tincl > x ? tincl : x;
-    }
+    const uint32_t tincl = wave_incl_max_u32(run);
     if (lane == 63) s_wmax[wave] = tincl;
     __syncthreads();
     uint32_t carry = gv.row_first[(uint64_t)t * (kGatherTile / kRow)] + 1u;

@@ -40,6 +40,8 @@ tot = sum(buf[k] for k in marks)
 for name, k in zip(NAMES, marks):
     print(f"{name:18s} {buf[k] / tot * 100:6.1f} %   {buf[k] / steps / (n / 64):9.0f} clk/row")
 print(f"total {tot / steps / (n / 64):.0f} clk per wave-row")
+print(f"ratio path: {buf[14] / steps:.0f} waves/step, {buf[15] / steps:.0f} lane-contacts/step of {n * 4} "
+      f"(rows {n / 64:.0f})")
 K3 = ["load w", "blocked fx", "tiles_before", "block_excl", "seek", "advance", "sync", "flush marks"]
 tot3 = sum(buf[16 + k] for k in range(len(K3)))
 waves3 = n / 512
