@@ -62,8 +62,14 @@ def pmc_traffic(kernel, n, map_cells):
         return None
     for name, e in d.get("kernels", {}).items():
         if name.startswith(kernel) and "hbm_bytes_per_dispatch" in e:
-            return {"bytes_per_launch": round(e["hbm_bytes_per_dispatch"]), "fetch_bytes": round(e["fetch_size_bytes"]),
-                    "write_bytes": round(e["write_size_bytes"]), "source": os.path.relpath(PROFILE_SUMMARY, ROOT)}
+            out = {"bytes_per_launch": round(e["hbm_bytes_per_dispatch"]), "fetch_bytes": round(e["fetch_size_bytes"]),
+                   "write_bytes": round(e["write_size_bytes"]), "source": os.path.relpath(PROFILE_SUMMARY, ROOT)}
+            # what actually bounds the kernel: the VALU (rocprofv3 derived metrics, same run)
+            if "valubusy_pct" in e:
+                out["valu_busy_pct"] = round(e["valubusy_pct"], 1)
+            if "valuutilization_pct" in e:
+                out["valu_lane_utilization_pct"] = round(e["valuutilization_pct"], 1)
+            return out
     return None
 
 

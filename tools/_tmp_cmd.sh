@@ -1,2 +1,2 @@
 cd $GRAFT_REPO_ROOT
-bash tools/gpu_round.sh testsall benchsharded
+bash tools/gpu_round.sh testsall smoke bench benchsharded

@@ -41,6 +41,18 @@ def main(d):
             raw = sum(v) / len(v) * 1024.0
             e[counter.lower() + "_raw_bytes"] = raw
             e[counter.lower() + "_bytes"] = raw * corr
+    # derived metrics (percent, per dispatch): VALUBusy = SQ_ACTIVE_INST_VALU / CUs / GRBM_GUI_ACTIVE,
+    # VALUUtilization = active lanes per VALU instruction
+    for counter, sub in (("VALUBusy", "valu"), ("VALUUtilization", "valuutil")):
+        files = glob.glob(os.path.join(d, sub, "*counter_collection.csv"))
+        if not files:
+            continue
+        acc = defaultdict(list)
+        for row in csv.DictReader(open(files[0])):
+            if row["Counter_Name"] == counter:
+                acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+        for k, v in acc.items():
+            out["kernels"].setdefault(k, {})[counter.lower() + "_pct"] = sum(v) / len(v)
     for k, e in out["kernels"].items():
         if "fetch_size_bytes" in e and "write_size_bytes" in e:
             e["hbm_bytes_per_dispatch"] = e["fetch_size_bytes"] + e["write_size_bytes"]
