@@ -617,7 +617,9 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
-    uint64_t bb[4] = {0, 0, 0, 0};      // ~key(min x), key(max x), ~key(min y), key(max y)
+    // -min x, max x, -min y, max y of the cloud, rounded to float (the window only needs a
+    // box that holds the cloud; it is widened by the float rounding in bbox_keys)
+    float bb[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     uint64_t limb = 0;                  // lane t < 52: column t & 3 of exact accumulator t >> 2
     const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
 
@@ -793,12 +795,13 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             st.zs[i] = zs;
             if (gath || w != w_in || w != w) st.w[i] = w;
         }
-        if (x == x && y == y) {
-            const uint64_t kx = order_key(x), ky = order_key(y);
-            bb[0] = bb[0] > ~kx ? bb[0] : ~kx;
-            bb[1] = bb[1] > kx ? bb[1] : kx;
-            bb[2] = bb[2] > ~ky ? bb[2] : ~ky;
-            bb[3] = bb[3] > ky ? bb[3] : ky;
+        {
+            // v_max_f32 returns the other operand for a NaN: NaN coordinates are skipped
+            const float xf = (float)x, yf = (float)y;
+            bb[0] = __builtin_fmaxf(bb[0], -xf);
+            bb[1] = __builtin_fmaxf(bb[1], xf);
+            bb[2] = __builtin_fmaxf(bb[2], -yf);
+            bb[3] = __builtin_fmaxf(bb[3], yf);
         }
         PROF(10);
     }
@@ -825,18 +828,24 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         PROF(11);
     }
 
-    // bounding box of the cloud for the next step's LDS window (exact maxima, any order)
+    // bounding box of the cloud for the next step's LDS window (maxima, any order)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        uint64_t v = bb[q];
+        float v = bb[q];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) { const uint64_t t = __shfl_xor(v, o, 64); v = v > t ? v : t; }
+        for (int o = 32; o >= 1; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o, 64));
         bb[q] = v;
     }
     Shard* shb = a.shards + (blockIdx.x % kNShard);
-    if (lane == 0 && bb[1]) {
+    if (lane == 0 && bb[1] > -INFINITY) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) atomicMax((unsigned long long*)&shb->bbox[q], (unsigned long long)bb[q]);
+        for (int q = 0; q < 4; ++q) {
+            // |x - (float)x| <= 2^-24 |x| + 2^-150: widen outward, then the order key
+            const double v = (double)bb[q];
+            const double wv = v + (dm_fabs(v) * 0x1p-22 + 0x1p-140);
+            const uint64_t k = order_key((q & 1) ? wv : -wv);
+            atomicMax((unsigned long long*)&shb->bbox[q], (unsigned long long)((q & 1) ? k : ~k));
+        }
     }
 
     if (!WEIGHT) return;
