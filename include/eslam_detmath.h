@@ -496,6 +496,30 @@ DM_FN double dm_minstd_uniform(uint32_t x)
     return ((double)(x - 1u) / 2147483646.0) * 1.0 + 0.0;
 }
 
+/* a / b correctly rounded from y = RN(1/b), without a division (the device's fp64 division
+ * is a ten-instruction sequence around a quarter-rate v_rcp_f64).  q0 = RN(a y) is within
+ * 2 ulp of a/b; one correction q1 = RN(q0 + RN(a - b q0) y) makes it faithful; then
+ * r1 = a - b q1 is exact (fma) and RN(q1 + r1 y) = RN(a/b) (Markstein's theorem: y within
+ * half an ulp of 1/b, q1 faithful).  Used where b is a per-step constant, with
+ * 0 <= a < 2^64 and 1 <= b < 2^53 (no overflow, no subnormal quotient other than 0).
+ * tests/c/check_div.c checks it against the division: exhaustively for the minstd
+ * uniform below, and over random and edge (a, b) for the stratified draws.             */
+DM_FN double dm_div_recip(double a, double b, double y)
+{
+    const double q0 = a * y;
+    const double q1 = dm_fma(dm_fma(-b, q0, a), y, q0);
+    return dm_fma(dm_fma(-b, q1, a), y, q1);
+}
+
+#define DM_INV_MINSTD_RANGE 4.656612877414201e-10   /* RN(1 / 2147483646) = 0x1.00000004p-31 */
+
+/* dm_minstd_uniform without the division (bit-identical for every x in [1, 2^31 - 1];
+ * the result is >= +0, so "* 1.0 + 0.0" is the identity on it) */
+DM_FN double dm_minstd_uniform_fast(uint32_t x)
+{
+    return dm_div_recip((double)(x - 1u), 2147483646.0, DM_INV_MINSTD_RANGE);
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* SurfaceHash pieces (host and device)                                                  */
 /* ------------------------------------------------------------------------------------ */

@@ -1098,6 +1098,13 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t fx_shift(double v, int shift) { return dm_fx_shift(v, shift); }
 
+// T_k = fx((k + U_k) / N): both divisions as dm_div_recip (bit-identical to "/", checked by
+// tests/c/check_div.c); inv_N = 1.0 / N
+__device__ __forceinline__ uint64_t draw_fx(uint64_t k, uint32_t x, double dN, double inv_N, int shift)
+{
+    return fx_shift(dm_div_recip((double)k + dm_minstd_uniform_fast(x), dN, inv_N), shift);
+}
+
 __device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint32_t xs, int shift,
                                                    const uint32_t* __restrict__ jt)
 {
@@ -1107,10 +1114,9 @@ __device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint3
     if (k0 >= N) return N;
     uint64_t cnt = k0;
     uint32_t x = dm_mulmod31(jump_pow(jt, k0 + 1), xs);
-    const double dN = (double)N;
+    const double dN = (double)N, inv_N = 1.0 / dN;
     for (uint64_t k = k0; k <= kstar + 1 && k < N; ++k) {
-        const double u = dm_minstd_uniform(x);
-        const uint64_t T = fx_shift(((double)k + u) / dN, shift);
+        const uint64_t T = draw_fx(k, x, dN, inv_N, shift);
         if (T <= c) cnt = k + 1;
         else break;
         x = dm_minstd_next(x);
@@ -1125,14 +1131,11 @@ struct DrawCursor {
     uint64_t k, N;
     uint32_t x, xs;
     int shift;
-    double dN;
+    double dN, inv_N;
     const uint32_t* jt;
     uint64_t T;                          // T_k of the current draw (valid when k < N)
 
-    __device__ __forceinline__ uint64_t draw_T() const
-    {
-        return fx_shift(((double)k + dm_minstd_uniform(x)) / dN, shift);
-    }
+    __device__ __forceinline__ uint64_t draw_T() const { return draw_fx(k, x, dN, inv_N, shift); }
     __device__ __forceinline__ void seek(uint64_t c)
     {
         k = count_draws_le(c, N, xs, shift, jt);
@@ -1330,28 +1333,40 @@ __global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ 
     if (threadIdx.x == 0) *total = t;
 }
 
-// K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
+// K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs.
 // Draw counting (#{k : T_k <= C}) for the particles of one wave: when the wave's outputs
 // [K0, K1) number at most kWaveDraws, its lanes evaluate T_k for all of them in parallel
-// (lane l: k = K0 + l + 64 j, one jump then a 64-stride minstd step), store them in LDS and
-// every particle binary-searches its cumulative sum there.  No per-lane serial walk, no
-// divergence.  Heavier waves fall back to the per-lane cursor.
-// #{j < D : sT[j] <= v[r]} for the kScanItems targets at once (sT sorted): the searches
-// advance together so their LDS reads are in flight together
-__device__ __forceinline__ void wave_count_le(const uint64_t* sT, uint32_t D, const uint64_t (&v)[kScanItems],
-                                              uint32_t (&pos)[kScanItems])
+// (lane l: k = K0 + l + 64 j, one jump then a 64-stride minstd step) and store them in LDS;
+// every particle then reads the (at most three) draws around floor(C N) there.  No per-lane
+// serial walk, no divergence.  Heavier waves fall back to the per-lane cursor.
+// count_draws_le with the wave's draws [K0, K1) read from LDS instead of evaluated.  The
+// count of a target c is k* - 1 plus the draws among k* - 1, k*, k* + 1 (k* = floor(c N))
+// that are <= c; for the wave's targets (wlo <= c <= whi) draws below K0 are <= c and draws
+// from K1 on are > c, so at most three LDS reads and no search.
+__device__ __forceinline__ uint64_t count_draws_le_lds(uint64_t c, uint64_t N, int shift, const uint64_t* sT,
+                                                       uint64_t K0, uint64_t K1)
 {
-    uint32_t top = 0;
-    if (D) { top = 1; while (top * 2 <= D) top *= 2; }
+    const unsigned __int128 prod = (unsigned __int128)c * N;
+    const uint64_t kstar = (uint64_t)(prod >> shift);
+    const uint64_t k0 = kstar >= 1 ? kstar - 1 : 0;
+    if (k0 >= N) return N;
+    uint64_t T[3];
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) pos[r] = 0;
-    for (uint32_t step = top; step > 0; step >>= 1) {
-        uint64_t t[kScanItems];
-#pragma unroll
-        for (int r = 0; r < kScanItems; ++r) t[r] = pos[r] + step <= D ? sT[pos[r] + step - 1] : ~0ull;
-#pragma unroll
-        for (int r = 0; r < kScanItems; ++r) if (pos[r] + step <= D && t[r] <= v[r]) pos[r] += step;
+    for (int d = 0; d < 3; ++d) {
+        const uint64_t k = k0 + d;
+        const bool in = k >= K0 && k < K1;
+        const uint64_t t = sT[in ? k - K0 : 0];             // slot 0 is in LDS; used only when in
+        T[d] = k < K0 ? 0ull : (in ? t : ~0ull);
     }
+    uint64_t cnt = k0;
+    bool go = true;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const uint64_t k = k0 + d;
+        go = go && k <= kstar + 1 && k < N && T[d] <= c;
+        cnt = go ? k + 1 : cnt;
+    }
+    return cnt;
 }
 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
@@ -1388,7 +1403,7 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
 
     const uint64_t N = sp.n_global;
     const uint32_t xs = ctl->minstd_start;
-    const double dN = (double)N;
+    const double dN = (double)N, inv_N = 1.0 / dN;
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
     // the wave's cumulative range (wlo, whi] and its draws [K0, K1)
     const uint64_t wlo = __shfl(base, 0, 64), whi = __shfl(base + run, 63, 64);
@@ -1405,24 +1420,19 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
             const uint32_t a64 = jt[64];                       // A^64
 #pragma unroll 4
             for (uint64_t k = K0 + lane; k < K1; k += 64) {
-                sT[k - K0] = fx_shift(((double)k + dm_minstd_uniform(x)) / dN, shift);
+                sT[k - K0] = draw_fx(k, x, dN, inv_N, shift);
                 x = dm_mulmod31(x, a64);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint64_t v[kScanItems];
-        uint32_t pos[kScanItems];
 #pragma unroll
-        for (int r = 0; r < kScanItems; ++r) v[r] = base + c[r];
-        wave_count_le(sT, (uint32_t)D, v, pos);
-#pragma unroll
-        for (int r = 0; r < kScanItems; ++r) hi_r[r] = K0 + pos[r];
+        for (int r = 0; r < kScanItems; ++r) hi_r[r] = count_draws_le_lds(base + c[r], N, shift, sT, K0, K1);
         const uint64_t prev = __shfl_up(hi_r[kScanItems - 1], 1, 64);
         lo = lane == 0 ? K0 : prev;
     } else {
-        DrawCursor cur{0, N, 0u, xs, shift, dN, jt, 0};
+        DrawCursor cur{0, N, 0u, xs, shift, dN, inv_N, jt, 0};
         cur.seek(base);
         lo = cur.k;
 #pragma unroll
@@ -1508,7 +1518,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     const uint64_t N = pp.n_global;
     const uint64_t W0 = pp.gbase[pp.rank], W1 = pp.gbase[pp.rank + 1];
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
-    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, jt, 0};
+    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, 1.0 / (double)N, jt, 0};
     cur.seek(base);
     uint64_t lo = i0 == 0 ? O0 : cur.k;
     // the tile's own-slice outputs: [clip(lo_first), clip(hi_last)) relative to W0
