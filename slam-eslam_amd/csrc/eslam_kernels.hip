@@ -138,7 +138,10 @@ template <class V> __device__ __forceinline__ uint64_t kq(const V& r, int k)
     return (uint64_t)r[2 * k] | ((uint64_t)r[2 * k + 1] << 32);
 }
 template <class V> __device__ __forceinline__ double kd(const V& r, int k) { return dm_from_bits(kq(r, k)); }
-template <class T, class V> __device__ __forceinline__ T* kp(const V& r, int k) { return (T*)(uintptr_t)kq(r, k); }
+// pointers from the kernel arguments are global memory: the explicit address space gives
+// global_load/store (SGPR base + 32-bit offset, vmcnt only) instead of flat accesses
+template <class T> using gmem = __attribute__((address_space(1))) T;
+template <class T, class V> __device__ __forceinline__ gmem<T>* kp(const V& r, int k) { return (gmem<T>*)(uintptr_t)kq(r, k); }
 
 // ESLAM_K1_PROF (diagnostic builds only): per-region shader-clock time of K1, summed by
 // lane 0 of every wave into k1_prof[] (LDS per block, one global atomic per region).
@@ -163,8 +166,8 @@ __device__ unsigned long long k1_prof[32];      // [0,16): K1 regions, [16,32): 
 
 // the state pointers of buffer s[b] (offset KOFF(s[b]))
 struct StatePtrs {
-    double *x, *y, *th, *z, *zs, *w, *mprob;
-    uint8_t* flags;
+    gmem<double> *x, *y, *th, *z, *zs, *w, *mprob;
+    gmem<uint8_t>* flags;
 };
 __device__ __forceinline__ StatePtrs kstate(uint32_t off)
 {
@@ -209,12 +212,16 @@ __device__ __forceinline__ WinBounds win_bounds()
 {
     typedef int vi4 __attribute__((ext_vector_type(4)));
     typedef int vi2 __attribute__((ext_vector_type(2)));
-    const vi4 a = *reinterpret_cast<const volatile vi4*>(&k1_win[0]);
-    const vi2 b = *reinterpret_cast<const volatile vi2*>(&k1_win[4]);
+    // volatile keeps the reads where they are used; the explicit LDS address space keeps
+    // them ds_read (a volatile generic pointer became a flat load + vmcnt(0) wait)
+    typedef const volatile __attribute__((address_space(3))) vi4 lds_vi4;
+    typedef const volatile __attribute__((address_space(3))) vi2 lds_vi2;
+    const vi4 a = *(lds_vi4*)(&k1_win[0]);
+    const vi2 b = *(lds_vi2*)(&k1_win[4]);
     return WinBounds{a.x, a.y, a.z, a.w, b.x, b.y};
 }
 
-__device__ __forceinline__ bool patch_gate(const float* height, uint32_t k, float pmf, float psf, double lz, double qv,
+__device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint32_t k, float pmf, float psf, double lz, double qv,
                                            double& mean, double& stdev)
 {
     const double pm = (double)pmf, ps = (double)psf;
@@ -262,21 +269,23 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     stdev = ps;
     if (gate0) return true;
     if (!in_grid || (in_win && wc.count <= 1)) return false;
-    const float* height = has_height ? kp<const float>(kl2(KOFF(map.height)), 0) : nullptr;
-    const float2* patch = kp<const float2>(h, 1);
+    const gmem<const float>* height = has_height ? kp<const float>(kl2(KOFF(map.height)), 0) : nullptr;
+    const gmem<const float2>* patch = kp<const float2>(h, 1);
     uint32_t b, e;
     if (in_win) {
         b = wc.begin + 1;
         e = wc.begin + wc.count;
     } else {
-        const uint32_t* cell_start = kp<const uint32_t>(h, 0);
+        const gmem<const uint32_t>* cell_start = kp<const uint32_t>(h, 0);
         const uint64_t cell = (uint64_t)in * width + (uint64_t)im;
         b = cell_start[cell];
         e = cell_start[cell + 1];
     }
     for (uint32_t k = b; k < e; ++k) {
-        const float2 pf = patch[k];
-        if (patch_gate(height, k, pf.x, pf.y, lz, qv, mean, stdev)) return true;
+        const uint64_t pf = reinterpret_cast<const gmem<const uint64_t>*>(patch)[k];   // float2 {mean, stdev}
+        if (patch_gate(height, k, __uint_as_float((uint32_t)pf), __uint_as_float((uint32_t)(pf >> 32)), lz, qv, mean,
+                       stdev))
+            return true;
     }
     return false;
 }
@@ -564,7 +573,8 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
 // source of a pending-gather output: expand the segment marks (inclusive max-scan) and
 // decode.  Returns the local particle index, or sets *rec for a migrated particle.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, const Rec* __restrict__ recs, const Rec** rec)
+__device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, const gmem<const Rec>* __restrict__ recs,
+                                                  const gmem<const Rec>** rec)
 {
     *rec = nullptr;
     if (multi) {
@@ -639,12 +649,12 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         if (row0 >= n) break;
         const uint64_t i = row0 + lane;
         uint32_t src = (uint32_t)i;
-        const Rec* rc = nullptr;
+        const gmem<const Rec>* rc = nullptr;
         uint32_t rec_anc = 0;
         if (gath) {
             const su8 g = kl8(KOFF(gv));              // marks, row_first, anc, recs
             const su2 gf = kl2(KOFF(gv.record));      // record, multi
-            uint32_t* marks = kp<uint32_t>(g, 0);
+            gmem<uint32_t>* marks = kp<uint32_t>(g, 0);
             // expand the segment marks of this row: inclusive max-scan + the row carry
             uint32_t m = 0;
             if (i < n) { m = marks[i]; if (m) marks[i] = 0; }
@@ -1648,8 +1658,8 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
         const uint32_t slot = (uint32_t)r * kBlock + tid;
         const uint64_t k = (uint64_t)t * kGatherTile + slot;
         if (k >= n) continue;
-        const Rec* rc;
-        const uint32_t i = decode_source(s_idx[slot], gv.multi, gv.recs, &rc);
+        const gmem<const Rec>* rc;
+        const uint32_t i = decode_source(s_idx[slot], gv.multi, (const gmem<const Rec>*)gv.recs, &rc);
         if (rc) {
             out.x[k] = rc->x; out.y[k] = rc->y; out.th[k] = rc->th; out.z[k] = rc->z; out.zs[k] = rc->zs; out.w[k] = rc->w;
             if (aux) { out.mprob[k] = rc->mprob; out.flags[k] = (uint8_t)rc->src; }
