@@ -1221,7 +1221,8 @@ __device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uin
     return run;
 }
 
-constexpr int kWaveDraws = 1056;         // stratified draws one wave evaluates in LDS (K3b)
+constexpr int kWaveDraws = 576;          // stratified draws one wave holds in LDS at a time (K3b)
+constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * kWaveDraws: per-target windows
 
 // K3b's LDS: the staged weights, then the wave's draws, then the staged marks (each dead
 // before the next is written)
@@ -1344,39 +1345,59 @@ __global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ 
 }
 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs.
-// Draw counting (#{k : T_k <= C}) for the particles of one wave: when the wave's outputs
-// [K0, K1) number at most kWaveDraws, its lanes evaluate T_k for all of them in parallel
-// (lane l: k = K0 + l + 64 j, one jump then a 64-stride minstd step) and store them in LDS;
-// every particle then reads the (at most three) draws around floor(C N) there.  No per-lane
-// serial walk, no divergence.  Heavier waves fall back to the per-lane cursor.
-// count_draws_le with the wave's draws [K0, K1) read from LDS instead of evaluated.  The
-// count of a target c is k* - 1 plus the draws among k* - 1, k*, k* + 1 (k* = floor(c N))
-// that are <= c; for the wave's targets (wlo <= c <= whi) draws below K0 are <= c and draws
-// from K1 on are > c, so at most three LDS reads and no search.
-__device__ __forceinline__ uint64_t count_draws_le_lds(uint64_t c, uint64_t N, int shift, const uint64_t* sT,
-                                                       uint64_t K0, uint64_t K1)
+// Draw counting (#{k : T_k <= C}) for the particles of one wave: the counts of its targets
+// only read the draws [dlo, dhi) around floor(C N) of its first and last target.  Its lanes
+// evaluate those draws in parallel, kWaveDraws at a time (lane l: k = q0 + l + 64 j, one jump
+// then a 64-stride minstd step), store them in LDS, and every target reads the (at most
+// three) draws of its window there.  No per-lane serial walk, no search, no divergence.
+// Waves with more than kWaveChunks chunks of draws (heavy weights) evaluate each target's
+// window directly (count_draws_le).
+//
+// count_draws_le with the draws read from LDS instead of evaluated.  The count of a target c
+// is k0 = k* - 1 plus the leading draws among k0, k0 + 1, k0 + 2 (at most k* + 1, below N)
+// that are <= c, k* = floor(c N) (draws below k0 are <= c, draws above k* + 1 are > c).
+__device__ __forceinline__ uint64_t kstar_of(uint64_t c, uint64_t N, int shift)
 {
-    const unsigned __int128 prod = (unsigned __int128)c * N;
-    const uint64_t kstar = (uint64_t)(prod >> shift);
+    return (uint64_t)(((unsigned __int128)c * N) >> shift);
+}
+
+// The window of target c as one word: bits 0..15 k0 - dlo (< kWaveChunks * kWaveDraws),
+// 16..17 the number of window draws (k0 + d <= k* + 1, < N), bit 18 "k0 >= N" (count N),
+// bits 19..21 set by draws_le_chunk: window draw d is <= c.
+__device__ __forceinline__ uint32_t window_of(uint64_t c, uint64_t N, int shift, uint64_t dlo)
+{
+    const uint64_t kstar = kstar_of(c, N, shift);
     const uint64_t k0 = kstar >= 1 ? kstar - 1 : 0;
-    if (k0 >= N) return N;
-    uint64_t T[3];
+    if (k0 >= N) return 1u << 18;
+    uint32_t nd = 0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) nd += (k0 + d <= kstar + 1 && k0 + d < N) ? 1u : 0u;
+    return (uint32_t)(k0 - dlo) | (nd << 16);
+}
+
+__device__ __forceinline__ uint32_t draws_le_chunk(uint32_t w, uint64_t c, const uint64_t* sT, uint64_t dlo, uint64_t q0,
+                                                   uint64_t q1)
+{
+    const uint64_t k0 = dlo + (w & 0xffffu);
+    const uint32_t nd = (w >> 16) & 3u;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         const uint64_t k = k0 + d;
-        const bool in = k >= K0 && k < K1;
-        const uint64_t t = sT[in ? k - K0 : 0];             // slot 0 is in LDS; used only when in
-        T[d] = k < K0 ? 0ull : (in ? t : ~0ull);
+        const bool in = (uint32_t)d < nd && k >= q0 && k < q1;
+        const uint64_t t = sT[in ? k - q0 : 0];             // slot 0 is in LDS; used only when in
+        w |= (in && t <= c) ? 1u << (19 + d) : 0u;
     }
-    uint64_t cnt = k0;
-    bool go = true;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const uint64_t k = k0 + d;
-        go = go && k <= kstar + 1 && k < N && T[d] <= c;
-        cnt = go ? k + 1 : cnt;
-    }
-    return cnt;
+    return w;
+}
+
+__device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, uint64_t N)
+{
+    if ((w >> 18) & 1u) return N;
+    const uint64_t k0 = dlo + (w & 0xffffu);
+    const uint32_t le = (w >> 19) & 7u;
+    // leading draws <= c (draws are nondecreasing in k; le has no bits beyond nd)
+    const uint32_t lead = (le & 1u) ? ((le & 2u) ? ((le & 4u) ? 3u : 2u) : 1u) : 0u;
+    return k0 + lead;
 }
 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
@@ -1415,38 +1436,54 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     const uint32_t xs = ctl->minstd_start;
     const double dN = (double)N, inv_N = 1.0 / dN;
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
-    // the wave's cumulative range (wlo, whi] and its draws [K0, K1)
+    // the wave's cumulative range [wlo, whi]: every count it needs reads only draws in
+    // [dlo, dhi) (the windows k* - 1 .. k* + 1 of wlo and whi, clamped to [0, N))
     const uint64_t wlo = __shfl(base, 0, 64), whi = __shfl(base + run, 63, 64);
-    uint64_t kk = 0;
-    if (lane < 2) kk = count_draws_le(lane == 0 ? wlo : whi, N, xs, shift, jt);
-    const uint64_t K0 = __shfl(kk, 0, 64), K1 = __shfl(kk, 1, 64);
-    const uint64_t D = K1 - K0;
+    const uint64_t ks_lo = kstar_of(wlo, N, shift), ks_hi = kstar_of(whi, N, shift);
+    const uint64_t dlo = ks_lo >= 1 ? ks_lo - 1 : 0;
+    const uint64_t dhi = ks_hi + 2 < N ? ks_hi + 2 : N;
     uint64_t hi_r[kScanItems];
     uint64_t lo;
-    if (D <= (uint64_t)kWaveDraws) {
+    if (dlo >= dhi || dhi - dlo <= (uint64_t)kWaveChunks * kWaveDraws) {
+        // draws in LDS, kWaveDraws at a time (one chunk unless the wave holds heavy weights);
+        // le[r] bit d: draw k0_r + d of target r (r = kScanItems: wlo) is <= its target
         uint64_t* sT = s_u.T[wave];
-        if (K0 + lane < K1) {
-            uint32_t x = dm_mulmod31(jump_pow(jt, K0 + lane + 1), xs);
-            const uint32_t a64 = jt[64];                       // A^64
-#pragma unroll 4
-            for (uint64_t k = K0 + lane; k < K1; k += 64) {
-                sT[k - K0] = draw_fx(k, x, dN, inv_N, shift);
-                x = dm_mulmod31(x, a64);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t win[kScanItems + 1];
 #pragma unroll
-        for (int r = 0; r < kScanItems; ++r) hi_r[r] = count_draws_le_lds(base + c[r], N, shift, sT, K0, K1);
+        for (int r = 0; r <= kScanItems; ++r) win[r] = window_of(r < kScanItems ? base + c[r] : wlo, N, shift, dlo);
+        const uint32_t a64 = jt[64], a_lane = jt[lane];            // A^64, A^lane
+        for (uint64_t q0 = dlo; q0 < dhi; q0 += kWaveDraws) {
+            const uint64_t q1 = dhi - q0 < (uint64_t)kWaveDraws ? dhi : q0 + kWaveDraws;
+            if (q0 + lane < q1) {
+                uint32_t x = dm_mulmod31(dm_mulmod31(jump_pow(jt, q0 + 1), xs), a_lane);
+#pragma unroll 4
+                for (uint64_t k = q0 + lane; k < q1; k += 64) {
+                    sT[k - q0] = draw_fx(k, x, dN, inv_N, shift);
+                    x = dm_mulmod31(x, a64);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r <= kScanItems; ++r)
+                win[r] = draws_le_chunk(win[r], r < kScanItems ? base + c[r] : wlo, sT, dlo, q0, q1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) hi_r[r] = count_from_window(win[r], dlo, N);
+        const uint64_t K0 = count_from_window(win[kScanItems], dlo, N);
         const uint64_t prev = __shfl_up(hi_r[kScanItems - 1], 1, 64);
         lo = lane == 0 ? K0 : prev;
     } else {
-        DrawCursor cur{0, N, 0u, xs, shift, dN, inv_N, jt, 0};
-        cur.seek(base);
-        lo = cur.k;
+        // heavy weights: each target's window evaluated directly (jump + at most three draws)
 #pragma unroll
-        for (int r = 0; r < kScanItems; ++r) hi_r[r] = i0 + r < sp.n ? cur.advance(base + c[r]) : cur.k;
+        for (int r = 0; r < kScanItems; ++r) hi_r[r] = count_draws_le(base + c[r], N, xs, shift, jt);
+        const uint64_t K0 = count_draws_le(wlo, N, xs, shift, jt);
+        const uint64_t prev = __shfl_up(hi_r[kScanItems - 1], 1, 64);
+        lo = lane == 0 ? K0 : prev;
     }
     PROF(4);
     if (i0 == 0) lo = 0;

@@ -192,3 +192,39 @@ def test_rng_state_resume(gpu_mod, flat_grid):
         b.step(st)
     b.sync()
     assert_bit_identical(b.download(), a.download(), "resume")
+
+
+@pytest.mark.parametrize("profile", ["chunks", "heavy", "single"])
+def test_resample_concentrated_weights(gpu_mod, profile):
+    """Stratified resample where one wave's particles receive far more than 512 draws: two LDS
+    chunks of draws (profile "chunks"), the per-target window path ("heavy"), one particle with
+    all the weight ("single").  Ancestors and particles bit-exact against the oracle."""
+    n = 20000
+    rng = np.random.default_rng(23)
+    pa = A.ParticleArrays(n)
+    pa.x[:] = rng.normal(0, 0.2, n)
+    pa.y[:] = rng.normal(0, 0.2, n)
+    pa.orientation[:] = rng.normal(0, 0.1, n)
+    pa.zpos[:] = 0.18
+    pa.zsigma[:] = 0.2
+    w = rng.uniform(0.5, 1.5, n)
+    if profile == "chunks":
+        w[4096:6144] *= 1.7              # ~1.7x the draws of an average wave over four waves
+    elif profile == "heavy":
+        w[5000] = 4000.0                 # ~17 % of all draws on one particle
+        w[12000:12010] = 300.0
+    else:
+        w[:] = 0.0
+        w[7777] = 0.25
+    pa.weight[:] = w
+    cfg = A.default_config()
+    cfg.flags |= A.FLAG_RECORD_ANCESTORS
+    orc = O.OracleFilter(cfg)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc.upload(pa)
+    gpu.upload(pa)
+    gpu.resample()
+    orc.resample()
+    gpu.sync()
+    assert np.array_equal(gpu.ancestors(), orc.ancestors())
+    assert_bit_identical(gpu.download(), orc.download(), "resample " + profile)
