@@ -850,9 +850,12 @@ DM_FN double dm_limbs_to_double(const uint64_t L[4], int scale)
 /* J = the largest power of two <= min(16, n_global / 2^20): from 1M particles on there are
  * ~16384 chunks (the weighting kernel runs one chunk per wave, so the 256 CUs x 3 waves per
  * SIMD are refilled ~5 times and the last partial round stays short)                   */
+#ifndef ESLAM_CHUNK_UNIT                 /* experiment builds only (changes the sum order) */
+#define ESLAM_CHUNK_UNIT 1048576u
+#endif
 DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
 {
-    uint64_t q = n_global / 1048576u;
+    uint64_t q = n_global / ESLAM_CHUNK_UNIT;
     uint32_t j = 1;
     while (j < 16u && (uint64_t)(j * 2u) <= q) j *= 2u;
     return j;

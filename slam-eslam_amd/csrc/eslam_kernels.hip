@@ -591,6 +591,12 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #define K1_OCCUPANCY
 #endif
 
+#ifdef ESLAM_ABL_NO_BM           // ablation builds only (timing, wrong bits)
+#define K1_BOX_MULLER(a, b, z0, z1) (*(z0) = dm_u32(a) - 0.5, *(z1) = dm_u32(b) - 0.5)
+#else
+#define K1_BOX_MULLER dm_box_muller32
+#endif
+
 template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH>
 __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a)
 {
@@ -692,8 +698,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             const dm_philox_ctr d0 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 0);
             const dm_philox_ctr d1 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 1);
             double z0, z1, z2, sn0;
-            dm_box_muller32(d0.v[0], d0.v[1], &z0, &z1);
-            dm_box_muller32(d0.v[2], d0.v[3], &z2, &sn0);
+            K1_BOX_MULLER(d0.v[0], d0.v[1], &z0, &z1);
+            K1_BOX_MULLER(d0.v[2], d0.v[3], &z2, &sn0);
             PROF(2);
             // odometry.getPoseDeltaSample2D() = mu + L z
             const su16 P = kl16(KOFF(p.mu));         // mu0 mu1 mu2 L00 L10 L11 L20 L21
@@ -715,7 +721,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             zs = dm_sqrt(zs * zs + kd(Z, 1));
             if (do_spread) {
                 double sn1, sn2;
-                dm_box_muller32(d1.v[2], d1.v[3], &sn1, &sn2);
+                K1_BOX_MULLER(d1.v[2], d1.v[3], &sn1, &sn2);
                 x += sn0 * tf + 0.0;
                 y += sn1 * tf + 0.0;
                 th += sn2 * rf + 0.0;
