@@ -847,11 +847,12 @@ DM_FN double dm_limbs_to_double(const uint64_t L[4], int scale)
 #define DM_FX_SCALE 112          /* fixed-point scale of a chunk total bounded by 2^10 */
 #define DM_NBUCKETS 6            /* cpoints.size() buckets 0,1,2,3,4,>=5 (phase B)     */
 
-/* J = the largest power of two <= min(16, n_global / 2^20): from 1M particles on there are
- * ~16384 chunks (the weighting kernel runs one chunk per wave, so the 256 CUs x 3 waves per
- * SIMD are refilled ~5 times and the last partial round stays short)                   */
+/* J = the largest power of two <= min(16, n_global / 2^19): from 512k particles on there are
+ * ~8192 chunks of 64 x J (the weighting kernel runs one chunk per wave: 4M particles give
+ * 8 rows per wave, 8192 waves = 2 refills of the 256 CUs x 4 waves per SIMD; measured 2-3 %
+ * faster K1 than 2^20, interleaved A/B on MI355X)                                       */
 #ifndef ESLAM_CHUNK_UNIT                 /* experiment builds only (changes the sum order) */
-#define ESLAM_CHUNK_UNIT 1048576u
+#define ESLAM_CHUNK_UNIT 524288u
 #endif
 DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
 {

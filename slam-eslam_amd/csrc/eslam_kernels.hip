@@ -629,6 +629,9 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     Window win;
     win.on = 0;
     if (WEIGHT) win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds);
+#ifdef ESLAM_ABL_STAGE_TWICE            // ablation builds only: the staging cost
+    if (WEIGHT) { __syncthreads(); win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds); }
+#endif
 
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;

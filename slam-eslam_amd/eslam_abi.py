@@ -172,7 +172,7 @@ MAX_RANKS = 16
 
 def chunk_rows(n_global):
     """dm_chunk_rows (include/eslam_detmath.h): rows of 64 lanes per canonical summation chunk."""
-    q = n_global // 1048576
+    q = n_global // 524288
     j = 1
     while j < 16 and j * 2 <= q:
         j *= 2
