@@ -122,16 +122,15 @@ DM_FN double dm_rint_small(double x)
 #define DM_LN2_LO 1.90821492927058770002e-10  /* ln2 - DM_LN2_HI                        */
 #define DM_INV_LN2 1.44269504088896338700e+00
 
-/* e^r on |r| <= 0.3466: Taylor series to r^13 (truncation < 6e-18 relative), fma Horner */
-DM_POLY_TABLE(dm_c_exp, 11, 1.6059043836821613e-10 /* 1/13! */, 2.08767569878681e-09 /* 1/12! */,
-              2.505210838544172e-08 /* 1/11! */, 2.755731922398589e-07 /* 1/10! */,
-              2.7557319223985893e-06 /* 1/9! */, 2.48015873015873e-05 /* 1/8! */,
-              0.0001984126984126984 /* 1/7! */, 0.001388888888888889 /* 1/6! */,
-              0.008333333333333333 /* 1/5! */, 0.041666666666666664 /* 1/4! */,
-              0.16666666666666666 /* 1/3! */)
+/* e^r on |r| <= 0.3466: e^r = 1 + r (1 + r (1/2 + r P(r))), P a degree-9 near-minimax fit
+ * (tools/gen_minimax.py: Chebyshev, mpmath 60 digits; error of P's contribution < 1e-18
+ * relative), fma Horner                                                                 */
+DM_POLY_TABLE(dm_c_exp, 10, 2.0911229928855294e-09, 2.510037611136142e-08, 2.7557282983637385e-07,
+              2.7557268479724004e-06, 2.4801587317135435e-05, 0.00019841269863040922,
+              0.0013888888888886554, 0.008333333333330065, 0.041666666666666664, 0.16666666666666669)
 DM_FN double dm_exp_kernel(double r)
 {
-    double p = DM_POLY(dm_c_exp, 11, r);
+    double p = DM_POLY(dm_c_exp, 10, r);
     p = dm_fma_h(p, r);
     p = dm_fma_1(p, r);
     return dm_fma_1(p, r);
@@ -159,10 +158,10 @@ DM_FN double dm_exp(double x)
 /* ------------------------------------------------------------------------------------ */
 /* log                                                                                   */
 /* ------------------------------------------------------------------------------------ */
-DM_POLY_TABLE(dm_c_log, 10, 0.09523809523809523 /* 2/21 */, 0.10526315789473684 /* 2/19 */,
-              0.11764705882352941 /* 2/17 */, 0.13333333333333333 /* 2/15 */, 0.15384615384615385 /* 2/13 */,
-              0.18181818181818182 /* 2/11 */, 0.2222222222222222 /* 2/9 */, 0.2857142857142857 /* 2/7 */,
-              0.4 /* 2/5 */, 0.6666666666666666 /* 2/3 */)
+/* P(z) = 2 (atanh(sqrt z)/sqrt z - 1) / z on z <= 0.02944, degree-6 minimax (Remez,
+ * tools/gen_minimax.py; contribution < 1.5e-18 relative to log(1+f))                    */
+DM_POLY_TABLE(dm_c_log, 7, 0.14795474282318508, 0.15314098921479188, 0.1818356240187849,
+              0.22222198610842994, 0.2857142874201498, 0.39999999999416375, 0.6666666666666734)
 DM_FN double dm_log(double x)
 {
     /* branch-free: NaN, x <= 0 and +inf are selected at the end (same values) */
@@ -180,8 +179,8 @@ DM_FN double dm_log(double x)
     double f = m - 1.0;                 /* exact (Sterbenz) */
     double s = f / (2.0 + f);           /* (m-1)/(m+1), |s| <= 0.1716 */
     double z = s * s;
-    /* R = 2 z/3 + 2 z^2/5 + ... + 2 z^10/21  (atanh series; truncation < 3e-17 relative) */
-    double R = DM_POLY(dm_c_log, 10, z);
+    /* R = z P(z) ~ 2 z/3 + 2 z^2/5 + ...  (the atanh series, minimax-fitted) */
+    double R = DM_POLY(dm_c_log, 7, z);
     R = R * z;
     /* log(1+f) = 2 atanh(s) = 2s + s R, and 2s = f - s f  ->  f - s (f - R) */
     double l = f - s * (f - R);
@@ -201,27 +200,25 @@ DM_FN double dm_log(double x)
 #define DM_PIO2_3 2.02226624871116645580e-21   /* next 33 bits          */
 #define DM_INV_PIO2 6.36619772367581382433e-01
 
-DM_POLY_TABLE(dm_c_sin, 9, 8.22063524662433e-18 /* 1/19! */, -2.8114572543455206e-15 /* -1/17! */,
-              7.647163731819816e-13 /* 1/15! */, -1.6059043836821613e-10 /* -1/13! */,
-              2.505210838544172e-08 /* 1/11! */, -2.7557319223985893e-06 /* -1/9! */,
-              0.0001984126984126984 /* 1/7! */, -0.008333333333333333 /* -1/5! */,
-              0.16666666666666666 /* 1/3! (subtracted below) */)
-DM_FN double dm_sin_kernel(double r)   /* |r| <= pi/4, Taylor to r^19 */
+/* sin(r) = r - r z P(z), P(z) = (1 - sin(sqrt z)/sqrt z) / z, z <= (pi/4)^2: degree-5
+ * weighted minimax (Remez, tools/gen_minimax.py; |z (P - p)| < 5.4e-18)                 */
+DM_POLY_TABLE(dm_c_sin, 6, -1.5896827930152048e-10, 2.505075865328765e-08, -2.7557313695226595e-06,
+              0.0001984126982981695, -0.008333333333322425, 0.16666666666666632)
+DM_FN double dm_sin_kernel(double r)   /* |r| <= pi/4, degree 13 */
 {
     double z = r * r;
-    double p = DM_POLY(dm_c_sin, 9, z);
+    double p = DM_POLY(dm_c_sin, 6, z);
     return dm_fma(-r * z, p, r) ;
 }
 
-DM_POLY_TABLE(dm_c_cos, 9, 4.110317623312165e-19 /* 1/20! */, -1.5619206968586225e-16 /* -1/18! */,
-              4.779477332387385e-14 /* 1/16! */, -1.1470745597729725e-11 /* -1/14! */,
-              2.08767569878681e-09 /* 1/12! */, -2.755731922398589e-07 /* -1/10! */,
-              2.48015873015873e-05 /* 1/8! */, -0.001388888888888889 /* -1/6! */,
-              0.041666666666666664 /* 1/4! */)
-DM_FN double dm_cos_kernel(double r)   /* |r| <= pi/4, Taylor to r^20 */
+/* cos(r) = 1 + z (-1/2 + z P(z)), P(z) = (cos(sqrt z) - 1 + z/2) / z^2: degree-5 weighted
+ * minimax (Remez, tools/gen_minimax.py; |z^2 (P - p)| / cos r < 1.2e-18)                */
+DM_POLY_TABLE(dm_c_cos, 6, -1.1358536517414803e-11, 2.0875700841892227e-09, -2.755731417929608e-07,
+              2.48015872888517e-05, -0.0013888888888873056, 0.041666666666666595)
+DM_FN double dm_cos_kernel(double r)   /* |r| <= pi/4, degree 14 */
 {
     double z = r * r;
-    double p = DM_POLY(dm_c_cos, 9, z);
+    double p = DM_POLY(dm_c_cos, 6, z);
     p = dm_fma_mh(p, z);
     return dm_fma_1(p, z);
 }
