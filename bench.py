@@ -73,6 +73,15 @@ def pmc_traffic(kernel, n, map_cells):
     return None
 
 
+def workload_name(n, world, rough):
+    """the BASELINE.json configuration a run corresponds to (per-GPU size, weak scaling)"""
+    if rough:
+        return "configs[4]-style terrain"
+    if world == 1:
+        return {262144: "configs[1]", 4 * 1024 * 1024: "configs[2]"}.get(n, "custom size")
+    return "configs[2] per GPU, weak-scaled" if n == 4 * 1024 * 1024 else "custom size, weak-scaled"
+
+
 def cpu_baseline(args, grid):
     """The CPU oracle (a restatement of the reference path, reference-order double sums),
     single-threaded on this host, on a bounded sample of the same workload."""
@@ -194,9 +203,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (flat 100x100 m MLS map @0.1 m; odometry + 4 foot contacts per step)",
-        "config": {"workload": "configs[2]: %d particles/GPU, 1 MI355X per rank, MLS %dx%d @0.1 m, 4 contacts, "
-                               "resample forced every step" % (n, args.map_cells, args.map_cells),
+        "data": "synthetic (%s %gx%g m MLS map @0.1 m; odometry + 4 foot contacts per step)"
+                % ("rough multi-patch" if args.rough else "flat", args.map_cells / 10, args.map_cells / 10),
+        "config": {"workload": "%s: %d particles/GPU, 1 MI355X per rank, %sMLS %dx%d @0.1 m, 4 contacts, "
+                               "resample forced every step" % (workload_name(n, world, args.rough), n,
+                                                               "rough " if args.rough else "", args.map_cells,
+                                                               args.map_cells),
                    "particles_per_gpu": n, "global_particles": n * world,
                    "parallelism": "dp%d (particle shards%s)" % (world, ", sharded path" if sharded else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
