@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (sharded, RCCL) path even on one rank (measures its overhead)")
+    ap.add_argument("--comm", choices=["rccl", "torch"], default=os.environ.get("ESLAM_COMM", "rccl"),
+                    help="multi-GPU exchanges: the library's own RCCL communicator, or torch.distributed callbacks")
     ap.add_argument("--cpu-sample", type=int, default=1048576, help="particles in the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=48)
     return ap.parse_args()
@@ -137,8 +139,11 @@ def main():
         # one global filter of n * world particles, sharded over the ranks: RCCL all_gathers
         # of the statistics / totals / counts and an all_to_all_v of the migrating particles
         import eslam_dist
-        comm = eslam_dist.TorchComm(device_memory=True, device=local_rank)
-        f = eslam_dist.ShardedGpuFilter(cfg, n * world, comm, device=local_rank)
+        if args.comm == "rccl":
+            f = eslam_dist.RcclShardedGpuFilter(cfg, n * world, rank, world, device=local_rank)
+        else:
+            comm = eslam_dist.TorchComm(device_memory=True, device=local_rank)
+            f = eslam_dist.ShardedGpuFilter(cfg, n * world, comm, device=local_rank)
         assert f.n_local == n, (f.n_local, n)
     else:
         f = eslam_amd.GpuFilter(cfg, device=0)
@@ -210,7 +215,8 @@ def main():
                                                                "rough " if args.rough else "", args.map_cells,
                                                                args.map_cells),
                    "particles_per_gpu": n, "global_particles": n * world,
-                   "parallelism": "dp%d (particle shards%s)" % (world, ", sharded path" if sharded else "")},
+                   "parallelism": "dp%d (particle shards%s)" % (world, (", sharded path, %s exchanges" % args.comm)
+                                                                   if sharded else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,

@@ -274,6 +274,20 @@ typedef struct eslam_comm {
  * returns ESLAM_ERR_UNSUPPORTED.  comm == NULL returns the context to one GPU.        */
 int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase);
 
+/* ---- multi-GPU over RCCL, driven from the library (no callback into the host language) --
+ * SURVEY.md 8(b) "comm_init(nranks, rank, ncclUniqueId*)"; the reference has one CPU
+ * filter and no distribution (src/EmbodiedSlamFilter.hpp:29-39 owns it by value).
+ * eslam_gpu_rccl_unique_id: rank 0 creates the 128-byte RCCL id (ncclGetUniqueId) that the
+ * caller broadcasts to every rank by any means.  eslam_gpu_set_comm_rccl: every rank then
+ * joins the communicator (ncclCommInitRank, collective: all ranks must call it) and the
+ * context becomes shard `rank` exactly as eslam_gpu_set_comm makes it; the exchanges are
+ * ncclAllGather and grouped ncclSend/ncclRecv on the context's stream.  RCCL is loaded at
+ * run time (librccl.so.1); without it these return ESLAM_ERR_UNSUPPORTED.                 */
+#define ESLAM_RCCL_ID_BYTES 128
+int eslam_gpu_rccl_unique_id(uint8_t id[ESLAM_RCCL_ID_BYTES]);
+int eslam_gpu_set_comm_rccl(eslam_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[ESLAM_RCCL_ID_BYTES],
+                            uint64_t n_global, const uint64_t* shard_gbase);
+
 /* ---- diagnostics ------------------------------------------------------------------------- */
 /* ancestor index of every particle of the last resample (needs ESLAM_FLAG_RECORD_ANCESTORS) */
 int eslam_gpu_get_ancestors(eslam_ctx* ctx, uint32_t* out, uint64_t n);

@@ -7,6 +7,8 @@
 // touches particles runs on the GPU; the resample decision is taken on the device, so a
 // step is four asynchronous launches with no host round trip.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <math.h>
 #include <stdio.h>
@@ -26,7 +28,6 @@ extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
                                                 hipStream_t stream);
 extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream);
-extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* tile_sum,
                                                   uint64_t* total, hipStream_t stream);
 extern "C" hipError_t eslam_launch_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const uint64_t* tile_prefix,
@@ -239,9 +240,9 @@ struct eslam_ctx {
     bool sharded = false;
     eslam_comm comm = {};
     std::vector<uint64_t> gall;             // first global index of every rank (+ n_global)
-    Shard* rec_local = nullptr;             // this rank's statistics record
     Shard* recs = nullptr;                  // gathered records of all ranks
     uint64_t* mg = nullptr;                 // MgBlock (device)
+    void* rccl = nullptr;                   // ncclComm_t of eslam_gpu_set_comm_rccl (owned)
     uint64_t* mg_host = nullptr;            // pinned
     uint2* range = nullptr;                 // per particle: [lo, hi) of its global outputs
     void* sendbuf = nullptr; uint64_t send_cap = 0;
@@ -286,7 +287,8 @@ static constexpr uint32_t kRingSteps = 2048;
 namespace mg {
 constexpr int kTotal = 0;                                   // this rank's fixed-point weight total
 constexpr int kTotals = kTotal + 1;                         // [kMaxRanks] gathered totals
-constexpr int kCounts = kTotals + kMaxRanks;                // [kMaxRanks] records sent to each rank
+constexpr int kMirror = kTotals + kMaxRanks;                // [3] resample, minstd_start, scan_shift (k_finalize)
+constexpr int kCounts = kMirror + 3;                        // [kMaxRanks] records sent to each rank
 constexpr int kCountsAll = kCounts + kMaxRanks;             // [kMaxRanks^2] gathered counts
 constexpr int kSendOff = kCountsAll + kMaxRanks * kMaxRanks;   // [kMaxRanks + 1]
 constexpr int kSdEd = kSendOff + kMaxRanks + 1;             // [2 kMaxRanks]
@@ -445,15 +447,18 @@ static void free_map(eslam_ctx* ctx)
     ctx->has_map = false;
 }
 
+namespace { void rccl_release(eslam_ctx* ctx); }
+
 extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
 {
     if (!ctx) return;
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    rccl_release(ctx);
     free_particles(ctx);
     free_map(ctx);
     hipFree(ctx->shards); hipFree(ctx->ctl); hipHostFree(ctx->ctl_host); hipFree(ctx->jump);
     hipFree(ctx->scratch); hipHostFree(ctx->scratch_host);
-    hipFree(ctx->rec_local); hipFree(ctx->recs); hipFree(ctx->mg); hipHostFree(ctx->mg_host);
+    hipFree(ctx->recs); hipFree(ctx->mg); hipHostFree(ctx->mg_host);
     hipFree(ctx->sendbuf); hipFree(ctx->recvbuf); hipHostFree(ctx->stage);
     hipFree(ctx->d_hash); hipFree(ctx->d_hash_blist); hipFree(ctx->d_sort); hipFree(ctx->sort_tmp); hipFree(ctx->d_draws);
     for (auto& e : ctx->ev) if (e) hipEventDestroy(e);
@@ -610,12 +615,10 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
             return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: shard starts must be multiples of the summation chunk");
     }
     if (!ctx->mg) {
-        HIPCHK(ctx, hipMalloc(&ctx->rec_local, sizeof(Shard)));
-        HIPCHK(ctx, hipMalloc(&ctx->recs, sizeof(Shard) * kMaxRanks));
+        HIPCHK(ctx, hipMalloc(&ctx->recs, sizeof(Shard) * kNShard * kMaxRanks));
         HIPCHK(ctx, hipMalloc(&ctx->mg, mg::kWords * 8));
         HIPCHK(ctx, hipHostMalloc(&ctx->mg_host, mg::kWords * 8));
-        HIPCHK(ctx, hipMemset(ctx->rec_local, 0, sizeof(Shard)));
-        HIPCHK(ctx, hipMemset(ctx->recs, 0, sizeof(Shard) * kMaxRanks));
+        HIPCHK(ctx, hipMemset(ctx->recs, 0, sizeof(Shard) * kNShard * kMaxRanks));
         HIPCHK(ctx, hipMemset(ctx->mg, 0, mg::kWords * 8));
     }
     ctx->comm = *comm;
@@ -624,6 +627,128 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
     ctx->n_global = n_global;
     ctx->gbase = shard_gbase[comm->rank];
     return ESLAM_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// RCCL transport (eslam_gpu_set_comm_rccl): the eslam_comm callbacks implemented in C++ on
+// the context's stream, RCCL resolved at run time (the process's librccl.so.1 -- the one
+// torch loaded, if any -- so one RCCL serves both)
+// ---------------------------------------------------------------------------------------
+namespace {
+struct RcclApi {
+    bool ok = false;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const RcclApi& rccl_api()
+{
+    static RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return a;
+#define ESLAM_SYM(f, name) a.f = reinterpret_cast<decltype(a.f)>(dlsym(h, name))
+        ESLAM_SYM(get_unique_id, "ncclGetUniqueId");
+        ESLAM_SYM(comm_init_rank, "ncclCommInitRank");
+        ESLAM_SYM(comm_destroy, "ncclCommDestroy");
+        ESLAM_SYM(all_gather, "ncclAllGather");
+        ESLAM_SYM(send, "ncclSend");
+        ESLAM_SYM(recv, "ncclRecv");
+        ESLAM_SYM(group_start, "ncclGroupStart");
+        ESLAM_SYM(group_end, "ncclGroupEnd");
+        ESLAM_SYM(error_string, "ncclGetErrorString");
+#undef ESLAM_SYM
+        a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather && a.send && a.recv &&
+               a.group_start && a.group_end && a.error_string;
+        return a;
+    }();
+    return api;
+}
+
+int rccl_allgather_cb(void* user, const void* send, void* recv, uint64_t bytes, void* stream)
+{
+    eslam_ctx* ctx = static_cast<eslam_ctx*>(user);
+    const RcclApi& a = rccl_api();
+    return a.all_gather(send, recv, bytes, ncclUint8, static_cast<ncclComm_t>(ctx->rccl), static_cast<hipStream_t>(stream)) ==
+                   ncclSuccess ? 0 : 1;
+}
+
+int rccl_alltoallv_cb(void* user, const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes,
+                      void* stream)
+{
+    eslam_ctx* ctx = static_cast<eslam_ctx*>(user);
+    const RcclApi& a = rccl_api();
+    const ncclComm_t comm = static_cast<ncclComm_t>(ctx->rccl);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t so = 0, ro = 0;
+    if (a.group_start() != ncclSuccess) return 1;
+    int bad = 0;
+    for (int r = 0; r < ctx->comm.nranks; ++r) {
+        if (send_bytes[r]) bad |= a.send(static_cast<const char*>(send) + so, send_bytes[r], ncclUint8, r, comm, st) != ncclSuccess;
+        if (recv_bytes[r]) bad |= a.recv(static_cast<char*>(recv) + ro, recv_bytes[r], ncclUint8, r, comm, st) != ncclSuccess;
+        so += send_bytes[r];
+        ro += recv_bytes[r];
+    }
+    bad |= a.group_end() != ncclSuccess;
+    return bad;
+}
+
+void rccl_release(eslam_ctx* ctx)
+{
+    if (ctx->rccl) rccl_api().comm_destroy(static_cast<ncclComm_t>(ctx->rccl));
+    ctx->rccl = nullptr;
+}
+}  // namespace
+
+extern "C" int eslam_gpu_rccl_unique_id(uint8_t id[ESLAM_RCCL_ID_BYTES])
+{
+    if (!id) return ESLAM_ERR_INVALID_ARG;
+    const RcclApi& a = rccl_api();
+    if (!a.ok) return ESLAM_ERR_UNSUPPORTED;
+    ncclUniqueId u;
+    if (a.get_unique_id(&u) != ncclSuccess) return ESLAM_ERR_COMM;
+    static_assert(sizeof(u) == ESLAM_RCCL_ID_BYTES, "ncclUniqueId size");
+    memcpy(id, &u, sizeof(u));
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_set_comm_rccl(eslam_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[ESLAM_RCCL_ID_BYTES],
+                                       uint64_t n_global, const uint64_t* shard_gbase)
+{
+    if (!ctx || !id) return ESLAM_ERR_INVALID_ARG;
+    const RcclApi& a = rccl_api();
+    if (!a.ok) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "eslam_gpu_set_comm_rccl: librccl.so.1 not found");
+    if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm_rccl: bad communicator (1 <= nranks <= 16)");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    rccl_release(ctx);
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = a.comm_init_rank(&comm, nranks, u, rank);
+    if (r != ncclSuccess)
+        return fail(ctx, ESLAM_ERR_COMM, (std::string("ncclCommInitRank: ") + a.error_string(r)).c_str());
+    ctx->rccl = comm;
+    eslam_comm c;
+    memset(&c, 0, sizeof(c));
+    c.user = ctx;
+    c.rank = rank;
+    c.nranks = nranks;
+    c.device_memory = 1;
+    c.allgather = rccl_allgather_cb;
+    c.alltoallv = rccl_alltoallv_cb;
+    const int rc = eslam_gpu_set_comm(ctx, &c, n_global, shard_gbase);
+    if (rc) rccl_release(ctx);
+    return rc;
 }
 
 extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
@@ -1065,7 +1190,8 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
 }
 
 // multi-GPU update tail:
-//   shards -> rank record -> all_gather -> every rank finalises the same global scalars
+//   the rank's 16 statistics shards -> all_gather -> every rank finalises the same global
+//   scalars from all ranks' shards
 //   -> normalise + this rank's fixed-point weight total -> all_gather of the totals
 //   -> global stratified segments (outputs in this rank's slice are marked directly),
 //      while the host reads the totals and derives every rank's output range (the
@@ -1074,11 +1200,12 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const int G = ctx->comm.nranks, me = ctx->comm.rank;
-    HIPCHK(ctx, eslam_launch_shard_reduce(ctx->shards, ctx->rec_local, ctx->stream));
-    int rc = comm_allgather(ctx, ctx->rec_local, ctx->recs, sizeof(Shard));
+    int rc = comm_allgather(ctx, ctx->shards, ctx->recs, sizeof(Shard) * kNShard);
     if (rc) return rc;
-    const FinParams fp = fin_params(ctx, mode);
-    HIPCHK(ctx, eslam_launch_finalize(ctx->recs, G, ctx->ctl, &fp, ctx->stream));
+    FinParams fp = fin_params(ctx, mode);
+    fp.local_shards = ctx->shards;
+    fp.mirror = ctx->mg + mg::kMirror;
+    HIPCHK(ctx, eslam_launch_finalize(ctx->recs, G * kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     if (mode == FIN_SUM) return ESLAM_OK;
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
@@ -1088,8 +1215,9 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
     if (rc) return rc;
     uint64_t* h = ctx->mg_host;
-    HIPCHK(ctx, hipMemcpyAsync(h + mg::kTotals, ctx->mg + mg::kTotals, 8ull * G, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->stream));
+    // the gathered totals and the finalize mirror: one copy
+    HIPCHK(ctx, hipMemcpyAsync(h + mg::kTotals, ctx->mg + mg::kTotals, 8ull * (kMaxRanks + 3), hipMemcpyDeviceToHost,
+                               ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     PlanParams pp = plan_params(ctx);
     HIPCHK(ctx, eslam_launch_segments_multi(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->tile_sum, ctx->marks,
@@ -1097,16 +1225,18 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
                                             ctx->mg + mg::kFirstLast, ctx->stream));
     if (timed) rec(ctx, 3);
     HIPCHK(ctx, hipEventSynchronize(ctx->ev[0]));       // the totals, not the segments kernel
-    const Ctl& c = *ctx->ctl_host;
+    const uint64_t c_resample = h[mg::kMirror];
+    const uint32_t c_minstd_start = (uint32_t)h[mg::kMirror + 1];
+    const int c_scan_shift = (int)(int64_t)h[mg::kMirror + 2];
     uint64_t nrecv = 0;
-    if (c.resample && G > 1) {
+    if (c_resample && G > 1) {
         // every rank's outputs [O0_r, O1_r), the same counts the device computes
         const uint64_t N = ctx->n_global;
         uint64_t O0[kMaxRanks], O1[kMaxRanks], off = 0;
         for (int r = 0; r < G; ++r) {
             const uint64_t t = h[mg::kTotals + r];
-            O0[r] = r == 0 ? 0 : dm_count_draws_le(off, N, c.minstd_start, c.scan_shift);
-            O1[r] = r == G - 1 ? N : dm_count_draws_le(off + t, N, c.minstd_start, c.scan_shift);
+            O0[r] = r == 0 ? 0 : dm_count_draws_le(off, N, c_minstd_start, c_scan_shift);
+            O1[r] = r == G - 1 ? N : dm_count_draws_le(off + t, N, c_minstd_start, c_scan_shift);
             off += t;
         }
         auto overlap = [&](int r, int d) -> uint64_t {

@@ -166,6 +166,11 @@ struct FinParams {
     int32_t wexp;                        // scale exponent used by the statistics kernel
     uint32_t record;                     // 1: write update info
     uint32_t minstd_jump_n;              // A^n_global mod (2^31 - 1): the resample's N draws
+    // multi-GPU only (null otherwise): the shards this rank all-gathered, zeroed once read,
+    // and 3 words next to the gathered totals (resample, minstd_start, scan_shift) so the
+    // host reads everything it needs for the all_to_all_v sizes with one copy
+    Shard* local_shards;
+    uint64_t* mirror;
 };
 
 struct ScanParams {

@@ -983,33 +983,29 @@ __device__ __forceinline__ double acc_value(const uint64_t* L, uint64_t flags, i
 }
 
 // combine field t of nrec statistics records exactly (sum / max / or by field) and zero them
+// (exact integers: any grouping gives the same value)
 __device__ __forceinline__ uint64_t reduce_field(Shard* recs, int nrec, int t)
 {
-    // all loads first (they are independent), then combine: one memory latency, not nrec
-    uint64_t v[kMaxRanks > kNShard ? kMaxRanks : kNShard];
-    constexpr int kCap = kMaxRanks > kNShard ? kMaxRanks : kNShard;
-#pragma unroll
-    for (int k = 0; k < kCap; ++k) v[k] = k < nrec ? reinterpret_cast<const uint64_t*>(recs + k)[t] : 0ull;
-#pragma unroll
-    for (int k = 0; k < kCap; ++k)
-        if (k < nrec) reinterpret_cast<uint64_t*>(recs + k)[t] = 0;
+    constexpr int kCap = kNShard;
     uint64_t acc = 0;
     const int base = 2 * DM_NBUCKETS * 4 + 4;                                  // D
+    for (int k0 = 0; k0 < nrec; k0 += kCap) {
+        // a group's loads first (they are independent), then combine: one memory latency
+        uint64_t v[kCap];
 #pragma unroll
-    for (int k = 0; k < kCap; ++k) {
-        if (k >= nrec) break;
-        if (t == base + 2 || t >= base + 5) acc = acc > v[k] ? acc : v[k];      // maxm, bbox
-        else if (t == base + 3 || t == base + 4) acc |= v[k];                   // flags, err
-        else acc += v[k];
+        for (int k = 0; k < kCap; ++k) v[k] = k0 + k < nrec ? reinterpret_cast<const uint64_t*>(recs + k0 + k)[t] : 0ull;
+#pragma unroll
+        for (int k = 0; k < kCap; ++k)
+            if (k0 + k < nrec) reinterpret_cast<uint64_t*>(recs + k0 + k)[t] = 0;
+#pragma unroll
+        for (int k = 0; k < kCap; ++k) {
+            if (k0 + k >= nrec) break;
+            if (t == base + 2 || t >= base + 5) acc = acc > v[k] ? acc : v[k];      // maxm, bbox
+            else if (t == base + 3 || t == base + 4) acc |= v[k];                   // flags, err
+            else acc += v[k];
+        }
     }
     return acc;
-}
-
-// multi-GPU phase 1: this rank's shards -> one record (sent to every rank)
-__global__ void __launch_bounds__(kBlock) k_shard_reduce(Shard* __restrict__ shards, Shard* __restrict__ out)
-{
-    const int t = threadIdx.x;
-    if (t < kShardFields) reinterpret_cast<uint64_t*>(out)[t] = reduce_field(shards, kNShard, t);
 }
 
 // recs: kNShard local shards (one GPU) or the gathered per-rank records (multi-GPU)
@@ -1019,7 +1015,12 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
     __shared__ double s_acc[2 * DM_NBUCKETS + 1];     // exact sums A_b, B_b, SW as doubles
     __shared__ double s_f[DM_NBUCKETS];
     const int t = threadIdx.x;
-    if (t < kShardFields) s[t] = reduce_field(recs, nrec, t);
+    if (t < kShardFields) {
+        s[t] = reduce_field(recs, nrec, t);
+        // multi-GPU: the local shards were all-gathered (stream order: already read)
+        if (fp.local_shards)
+            for (int k = 0; k < kNShard; ++k) reinterpret_cast<uint64_t*>(fp.local_shards + k)[t] = 0;
+    }
     __syncthreads();
     {
         // the 13 fixed-point -> double conversions, one per lane (same values as serially)
@@ -1102,6 +1103,11 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
         ctl->scan_shift = 61 - (dm_weight_exp(S) + 1);
     } else {
         ctl->resample = 0;
+    }
+    if (fp.mirror) {
+        fp.mirror[0] = ctl->resample;
+        fp.mirror[1] = ctl->resample ? ctl->minstd : ctl->minstd_start;   // minstd_start below
+        fp.mirror[2] = (uint64_t)(int64_t)ctl->scan_shift;
     }
     if (ctl->resample) {
         ctl->minstd_start = ctl->minstd;
@@ -1343,7 +1349,10 @@ __device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ ti
     return t;
 }
 
-// multi-GPU: this slice's fixed-point total (the value all-gathered between K3a and K3b)
+
+// multi-GPU: this slice's fixed-point total (the value all-gathered between K3a and K3b).
+// A separate one-block kernel: a last-block-done ticket in K3a serialised 2048 atomics on
+// one counter and cost 55 us (measured)
 __global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
                                                         uint32_t ntiles, uint64_t* __restrict__ total)
 {
@@ -1917,12 +1926,6 @@ extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64
 extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, stream, recs, nrec, ctl, *fp);
-    return hipGetLastError();
-}
-
-extern "C" hipError_t eslam_launch_shard_reduce(Shard* shards, Shard* out, hipStream_t stream)
-{
-    hipLaunchKernelGGL(k_shard_reduce, dim3(1), dim3(kBlock), 0, stream, shards, out);
     return hipGetLastError();
 }
 

@@ -66,6 +66,9 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_get_kernel_times.argtypes = [vp, C.POINTER(A.KernelTimes)]
     L.eslam_gpu_selftest_math.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_uint64]
     L.eslam_gpu_set_comm.argtypes = [vp, C.POINTER(A.Comm), C.c_uint64, C.POINTER(C.c_uint64)]
+    L.eslam_gpu_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+    L.eslam_gpu_set_comm_rccl.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_uint64,
+                                          C.POINTER(C.c_uint64)]
     L.eslam_gpu_hash_create.argtypes = [vp]
     L.eslam_gpu_init_hash.argtypes = [vp, C.c_uint64]
     L.eslam_gpu_hash_info.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]

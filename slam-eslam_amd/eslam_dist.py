@@ -12,6 +12,11 @@ points of an update (SURVEY.md 8e -- the reference has one CPU filter, no distri
 (backend "nccl", device_memory=1, the collectives are queued on the context's HIP stream)
 or gloo on host buffers (device_memory=0; the library stages through pinned memory) --
 the CPU tests run the oracle's sharded mode through the same callbacks.
+
+``RcclShardedGpuFilter`` skips the host language altogether: the library joins an RCCL
+communicator itself (eslam_gpu_set_comm_rccl) and issues ncclAllGather / grouped
+ncclSend+ncclRecv on the context's stream; torch.distributed only broadcasts the 128-byte
+RCCL id once.  No callback and no cross-stream hand-off sits on the step's critical path.
 """
 import ctypes as C
 
@@ -128,6 +133,40 @@ class ShardedGpuFilter:
         self.n_global = n_global
         self.gbase = self.bounds[comm.rank]
         self.n_local = self.bounds[comm.rank + 1] - self.gbase
+
+    def __getattr__(self, name):
+        return getattr(self.f, name)
+
+    def close(self):
+        self.f.close()
+
+
+class RcclShardedGpuFilter:
+    """ShardedGpuFilter whose exchanges the library drives over its own RCCL communicator.
+    Collective: every rank of the torch.distributed group constructs it together."""
+
+    def __init__(self, cfg, n_global, rank, nranks, device=0, group=None):
+        import torch
+        import torch.distributed as dist
+        import eslam_amd
+        L = eslam_amd.load_library()
+        self.bounds = A.shard_bounds(n_global, nranks)
+        cfg.particle_count = n_global
+        self.f = eslam_amd.GpuFilter(cfg, device=device)
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            self.f._check(L.eslam_gpu_rccl_unique_id(uid))
+        # one broadcast of the id (device tensor: the nccl backend moves CUDA tensors)
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8,
+                         device=f"cuda:{device}" if dist.get_backend(group) == "nccl" else "cpu")
+        dist.broadcast(t, src=0, group=group)
+        uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+        gb = (C.c_uint64 * len(self.bounds))(*self.bounds)
+        self._gb = gb
+        self.f._check(L.eslam_gpu_set_comm_rccl(self.f.h, nranks, rank, uid, n_global, gb))
+        self.n_global = n_global
+        self.gbase = self.bounds[rank]
+        self.n_local = self.bounds[rank + 1] - self.gbase
 
     def __getattr__(self, name):
         return getattr(self.f, name)

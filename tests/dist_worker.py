@@ -5,7 +5,8 @@
 
 oracle: the CPU oracle's sharded mode over gloo (host-memory callbacks);
 gpu:    libeslam_gpu sharded over gloo (host staging) or, with 'device', RCCL on device
-        buffers (one rank per GPU).
+        buffers through the torch.distributed callbacks, or, with 'rccl', over the library's
+        own RCCL communicator (eslam_gpu_set_comm_rccl; one rank per GPU).
 """
 import os
 import sys
@@ -26,12 +27,12 @@ def main():
     import eslam_dist
     from dist_scenarios import run_scenario, scenario_config
     rank = int(os.environ["RANK"])
-    if kind == "gpu" and mem == "device":
+    if kind == "gpu" and mem in ("device", "rccl"):
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         dist.init_process_group("nccl")
     else:
         dist.init_process_group("gloo")
-    comm = eslam_dist.TorchComm(device_memory=(mem == "device"))
+    comm = eslam_dist.TorchComm(device_memory=(mem in ("device", "rccl")))
     cfg = scenario_config(name, n_global)
     bounds = A.shard_bounds(n_global, comm.nranks)
     lo, hi = bounds[rank], bounds[rank + 1]
@@ -41,7 +42,11 @@ def main():
         f.set_comm(comm, n_global)
         rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.info())
     else:
-        f = eslam_dist.ShardedGpuFilter(cfg, n_global, comm, device=int(os.environ.get("LOCAL_RANK", "0")))
+        dev = int(os.environ.get("LOCAL_RANK", "0"))
+        if mem == "rccl":
+            f = eslam_dist.RcclShardedGpuFilter(cfg, n_global, rank, comm.nranks, device=dev)
+        else:
+            f = eslam_dist.ShardedGpuFilter(cfg, n_global, comm, device=dev)
         rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.sync())
         f.close()
     if comm.error is not None:

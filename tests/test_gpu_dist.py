@@ -2,7 +2,8 @@
 against the one-process CPU oracle, bit for bit.  On a one-GPU box the ranks share the
 card: gloo with host staging for 2 and 3 ranks, and RCCL on device buffers with one rank
 (the full exchange sequence -- statistics all_gather, totals, counts, all_to_all_v --
-runs through RCCL to itself)."""
+runs through RCCL to itself), both through the torch.distributed callbacks and over the
+library's own RCCL communicator (eslam_gpu_set_comm_rccl)."""
 import pytest
 
 from test_dist_cpu import assert_same, launch, merge, single_oracle
@@ -23,3 +24,10 @@ def test_sharded_gpu_rccl_one_rank(oracle, tmp_path, name, n_global):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, 1, str(tmp_path), mem="device", timeout=400))
     assert_same(got, want, f"gpu rccl {name} N={n_global}")
+
+
+@pytest.mark.parametrize("name,n_global", [("forced", 5000), ("upload", 2000)])
+def test_sharded_gpu_native_rccl_one_rank(oracle, tmp_path, name, n_global):
+    want = single_oracle(name, n_global)
+    got = merge(launch("gpu", name, n_global, 1, str(tmp_path), mem="rccl", timeout=400))
+    assert_same(got, want, f"gpu native rccl {name} N={n_global}")
