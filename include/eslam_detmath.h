@@ -89,6 +89,29 @@ DM_FN double dm_horner_k(const double* c, int n, double u)
 DM_FN double dm_sqrt(double x) { return __builtin_sqrt(x); }
 DM_FN double dm_floor(double x) { return __builtin_floor(x); }
 
+/* sqrt(x) for a positive normal finite x, correctly rounded like dm_sqrt.  On the device
+ * it is the compiler's own fp64 sqrt sequence (v_rsq_f64, Goldschmidt iteration, two
+ * corrections) without the subnormal scaling and the zero/inf fix-up that such an x never
+ * needs.  Used for the Box-Muller radius, whose argument -2 log(u), u = (a + 1/2) 2^-32,
+ * lies in [2.3e-10, 44.4]; tests/test_gpu_parity.py compares it with dm_sqrt on the device
+ * for all 2^32 values of a.                                                             */
+DM_FN double dm_sqrt_pos(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = dm_fma(-h, g, 0.5);
+    g = dm_fma(g, r, g);
+    h = dm_fma(h, r, h);
+    double d = dm_fma(-g, g, x);
+    g = dm_fma(d, h, g);
+    d = dm_fma(-g, g, x);
+    return dm_fma(d, h, g);
+#else
+    return __builtin_sqrt(x);
+#endif
+}
+
 /* 2^k for k in [-1022, 1023], exact */
 DM_FN double dm_pow2i(int k) { return dm_from_bits((uint64_t)(k + 1023) << 52); }
 
@@ -162,16 +185,12 @@ DM_FN double dm_exp(double x)
  * tools/gen_minimax.py; contribution < 1.5e-18 relative to log(1+f))                    */
 DM_POLY_TABLE(dm_c_log, 7, 0.14795474282318508, 0.15314098921479188, 0.1818356240187849,
               0.22222198610842994, 0.2857142874201498, 0.39999999999416375, 0.6666666666666734)
-DM_FN double dm_log(double x)
+/* log(xs 2^kadj) for a positive normal finite xs: the arithmetic of dm_log without its
+ * special-case and subnormal selects */
+DM_FN double dm_log_core(double xs, int kadj)
 {
-    /* branch-free: NaN, x <= 0 and +inf are selected at the end (same values) */
-    const int special = !(x > 0.0) || !dm_isfinite(x);
-    double xs = special ? 1.0 : x;
-    uint64_t b = dm_bits(xs);
-    const int sub = (b >> 52) == 0;
-    xs = sub ? xs * 18014398509481984.0 /* 2^54 */ : xs;
-    b = dm_bits(xs);
-    int k = (sub ? -54 : 0) + (int)(b >> 52) - 1023;
+    const uint64_t b = dm_bits(xs);
+    int k = kadj + (int)(b >> 52) - 1023;
     double m = dm_from_bits((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull); /* [1,2) */
     const int big = m > 1.4142135623730951;
     m = big ? m * 0.5 : m;
@@ -185,7 +204,20 @@ DM_FN double dm_log(double x)
     /* log(1+f) = 2 atanh(s) = 2s + s R, and 2s = f - s f  ->  f - s (f - R) */
     double l = f - s * (f - R);
     double kd = (double)k;
-    const double res = kd * DM_LN2_HI + (l + kd * DM_LN2_LO);
+    return kd * DM_LN2_HI + (l + kd * DM_LN2_LO);
+}
+
+/* log(x) of a positive normal finite x: equal to dm_log(x) bit for bit */
+DM_FN double dm_log_pos(double x) { return dm_log_core(x, 0); }
+
+DM_FN double dm_log(double x)
+{
+    /* branch-free: NaN, x <= 0 and +inf are selected at the end (same values) */
+    const int special = !(x > 0.0) || !dm_isfinite(x);
+    double xs = special ? 1.0 : x;
+    const int sub = (dm_bits(xs) >> 52) == 0;
+    xs = sub ? xs * 18014398509481984.0 /* 2^54 */ : xs;
+    const double res = dm_log_core(xs, sub ? -54 : 0);
     if (!special) return res;
     if (x != x) return x;
     if (x <= 0.0) return x == 0.0 ? -dm_from_bits(0x7ff0000000000000ull) : dm_from_bits(0x7ff8000000000000ull);
@@ -431,7 +463,8 @@ DM_FN void dm_sincos2pi(double u, double* s, double* c)
 /* Box-Muller from two 32-bit words (the project / init draw layout) */
 DM_FN void dm_box_muller32(uint32_t a, uint32_t b, double* z0, double* z1)
 {
-    const double r = dm_sqrt(-2.0 * dm_log(dm_u32(a)));
+    /* u in [2^-33, 1): positive normal, so the range-restricted log and sqrt apply */
+    const double r = dm_sqrt_pos(-2.0 * dm_log_pos(dm_u32(a)));
     double s, c;
     dm_sincos2pi(dm_u32(b), &s, &c);
     *z0 = r * c;

@@ -1629,6 +1629,24 @@ extern "C" int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t)
     return ESLAM_OK;
 }
 
+extern "C" hipError_t eslam_launch_selftest_bm_radius(unsigned long long* bad, hipStream_t stream);
+
+extern "C" int eslam_gpu_selftest_bm_radius(int device, uint64_t* mismatches)
+{
+    if (!mismatches) return ESLAM_ERR_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return ESLAM_ERR_HIP;
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 8) != hipSuccess) return ESLAM_ERR_OUT_OF_MEMORY;
+    hipError_t e = hipMemset(d, 0, 8);
+    if (e == hipSuccess) e = eslam_launch_selftest_bm_radius(d, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+    hipFree(d);
+    *mismatches = h;
+    return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
+}
+
 extern "C" int eslam_gpu_selftest_math(int device, int fn, const double* x, const double* y, double* out, uint64_t n)
 {
     if (hipSetDevice(device) != hipSuccess) return ESLAM_ERR_HIP;

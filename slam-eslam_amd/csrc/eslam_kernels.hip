@@ -1866,6 +1866,22 @@ __global__ void k_selftest_math(int fn, const double* x, const double* y, double
     out[i] = r;
 }
 
+// every Box-Muller radius: the range-restricted log/sqrt against the general ones, for all
+// 2^32 uniform words (counts the words whose radius differs in any bit)
+__global__ void __launch_bounds__(kBlock) k_selftest_bm_radius(unsigned long long* bad)
+{
+    uint32_t cnt = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x; a < (1ull << 32); a += stride) {
+        const double u = dm_u32((uint32_t)a);
+        const double fast = dm_sqrt_pos(-2.0 * dm_log_pos(u));
+        const double ref = dm_sqrt(-2.0 * dm_log(u));
+        cnt += dm_bits(fast) != dm_bits(ref) ? 1u : 0u;
+    }
+    cnt = wave_sum_u32(cnt);
+    if ((threadIdx.x & 63u) == 0 && cnt) atomicAdd(bad, (unsigned long long)cnt);
+}
+
 }  // namespace eslam_dev
 
 // ---------------------------------------------------------------------------------------
@@ -2007,6 +2023,12 @@ extern "C" hipError_t eslam_launch_selftest_math(int fn, const double* x, const 
 {
     const uint32_t blocks = (uint32_t)((n + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_selftest_math, dim3(blocks), dim3(kBlock), 0, stream, fn, x, y, out, n);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_selftest_bm_radius(unsigned long long* bad, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_selftest_bm_radius, dim3(4096), dim3(kBlock), 0, stream, bad);
     return hipGetLastError();
 }
 

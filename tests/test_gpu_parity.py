@@ -47,6 +47,17 @@ def test_gpu_math_bit_identical(gpu_mod, oracle, fn, lo, hi):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), f"fn {fn}: {np.count_nonzero(got != want)} differ"
 
 
+def test_box_muller_radius_all_words(gpu_mod):
+    """dm_sqrt_pos(-2 dm_log_pos(u)) == dm_sqrt(-2 dm_log(u)) bit for bit on the device for
+    every one of the 2^32 uniform words: the range-restricted functions of the project
+    kernel's Box-Muller are correctly rounded there (the oracle uses the general ones)."""
+    import ctypes as C
+    L = gpu_mod.load_library()
+    bad = C.c_uint64(1)
+    assert L.eslam_gpu_selftest_bm_radius(0, C.byref(bad)) == 0
+    assert bad.value == 0
+
+
 def test_gpu_div_and_ratio(gpu_mod, oracle):
     rng = np.random.default_rng(7)
     x = rng.normal(size=20000) * 10.0 ** rng.uniform(-5, 5, 20000)
