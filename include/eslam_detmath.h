@@ -268,8 +268,8 @@ DM_FN void dm_sincos(double x, double* s, double* c)
 {
     const int fin = dm_isfinite(x);
     const double xs = fin ? x : 0.0;
+    /* |n| > 2^20 (|x| > 1.6e6 rad): the three-part reduction is inexact but deterministic */
     double n = dm_rint_small(xs * DM_INV_PIO2);
-    n = dm_fabs(n) > 1048576.0 ? dm_floor(xs * DM_INV_PIO2 + 0.5) : n; /* huge |x|: deterministic, inexact */
     double r = ((xs - n * DM_PIO2_1) - n * DM_PIO2_2) - n * DM_PIO2_3;
     double sr = dm_sin_kernel(r), cr = dm_cos_kernel(r);
     int64_t q = (int64_t)(n - 4.0 * dm_floor(n * 0.25));  /* n mod 4 in [0,3] */
