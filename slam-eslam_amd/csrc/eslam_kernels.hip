@@ -254,17 +254,18 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     }
     double fm = floor((lx - kd(h, 4)) * kd(h, 2));
     double fn = floor((ly - kd(h, 5)) * kd(h, 3));
-    const bool in_grid = fm >= 0.0 && fm < (double)width && fn >= 0.0 && fn < (double)hcells;
+    // non-short-circuit & of pure compares: selects, no exec-mask branches
+    const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     const int im = in_grid ? (int)fm : 0, in = in_grid ? (int)fn : 0;
     // fast path without branches: an in-window cell whose first patch passes the gate (the
     // window is only staged for maps without heights).  Everything else -- off the window,
     // heights, a failing first patch of a multi-patch cell -- takes the loop below.
     const WinBounds wb = win_bounds();
-    const bool in_win = in_grid && wb.on && im >= wb.m0 && im < wb.m1 && in >= wb.n0 && in < wb.n1;
+    const bool in_win = in_grid & (wb.on != 0) & (im >= wb.m0) & (im < wb.m1) & (in >= wb.n0) & (in < wb.n1);
     const WinCell wc = win.cells[in_win ? (in - wb.n0) * wb.cols + (im - wb.m0) : 0];
     const double pm = (double)wc.mean0, ps = (double)wc.stdev0;
     const double diff = dm_fabs(pm - lz);
-    const bool gate0 = in_win && wc.count > 0 && diff * diff < 9.0 * (ps * ps + qv);
+    const bool gate0 = in_win & (wc.count > 0) & (diff * diff < 9.0 * (ps * ps + qv));
     mean = pm;
     stdev = ps;
     if (gate0) return true;
