@@ -45,7 +45,8 @@ def build(force=False, verbose=True, defines=(), lib=None, tag=""):
         obj = os.path.join(OUT_DIR, src + tag + ".o")
         objs.append(obj)
         if force or _stale(obj, [path] + HEADERS):
-            cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-c", path, "-o", obj]
+            extra = os.environ.get("ESLAM_EXTRA_FLAGS", "").split()     # experiment builds only
+            cmd = [HIPCC] + FLAGS + extra + ["-D" + d for d in defines] + ["-c", path, "-o", obj]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
