@@ -110,6 +110,11 @@ def cpu_baseline(args, grid):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: native libraries (RCCL prints a version banner
+    # when a communicator is created) write to stderr until the result is printed
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -230,6 +235,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, grid)
+    sys.stdout.flush()
+    os.dup2(json_fd, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     f.close()

@@ -1224,7 +1224,14 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
                                             ctx->tile_first, ctx->mg + mg::kTotals, ctx->jump, ctx->range,
                                             ctx->mg + mg::kFirstLast, ctx->stream));
     if (timed) rec(ctx, 3);
-    HIPCHK(ctx, hipEventSynchronize(ctx->ev[0]));       // the totals, not the segments kernel
+    // the totals, not the segments kernel.  Spin on the event: a blocking synchronize
+    // wakes the thread tens of microseconds late, and the GPU runs dry before the next
+    // step's launches if the host is late here (the segments kernel is all it has queued)
+    {
+        hipError_t q;
+        while ((q = hipEventQuery(ctx->ev[0])) == hipErrorNotReady) {}
+        HIPCHK(ctx, q);
+    }
     const uint64_t c_resample = h[mg::kMirror];
     const uint32_t c_minstd_start = (uint32_t)h[mg::kMirror + 1];
     const int c_scan_shift = (int)(int64_t)h[mg::kMirror + 2];
