@@ -164,6 +164,24 @@ public:
         return (size_t)n;
     }
 
+    // multi-GPU (the reference has one CPU filter): this estimator becomes shard `rank` of an
+    // nGlobal-particle filter over an RCCL communicator the library drives itself.  Rank 0
+    // calls rcclUniqueId(), the caller broadcasts the id, every rank calls setCommRccl
+    // (collective) before init; shardGbase: the first global index of every rank + nGlobal.
+    static std::vector<uint8_t> rcclUniqueId()
+    {
+        std::vector<uint8_t> id(ESLAM_RCCL_ID_BYTES);
+        if (eslam_gpu_rccl_unique_id(id.data()) != ESLAM_OK) throw std::runtime_error("eslam_gpu_rccl_unique_id failed");
+        return id;
+    }
+    void setCommRccl(int nranks, int rank, const std::vector<uint8_t>& id, uint64_t nGlobal,
+                     const std::vector<uint64_t>& shardGbase)
+    {
+        if (id.size() != ESLAM_RCCL_ID_BYTES || shardGbase.size() != (size_t)nranks + 1)
+            throw std::runtime_error("setCommRccl: bad id or shard table");
+        check(ctx_, eslam_gpu_set_comm_rccl(ctx_, nranks, rank, id.data(), nGlobal, shardGbase.data()));
+    }
+
     const eslam_update_info& lastUpdate() const { return last_; }
     eslam_ctx* handle() { return ctx_; }
 
