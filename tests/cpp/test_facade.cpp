@@ -97,6 +97,32 @@ int main()
     Pose c = filter.getCentroid();
     EXPECT(std::isfinite(c.position[0]) && std::fabs(c.position[0] - x) < 0.2, "centroid near the odometry pose");
 
+    // one shard of a 3000-particle filter over the library's own RCCL communicator (one
+    // rank): the same particles, bit for bit, as the single-GPU filter
+    {
+        PoseEstimator shard(cfg);
+        shard.setCommRccl(1, 0, PoseEstimator::rcclUniqueId(), 3000, std::vector<uint64_t>{0, 3000});
+        shard.setEnvironment(grid);
+        EXPECT(eslam_gpu_init_pose(shard.handle(), start.position, start.orientation) == ESLAM_OK, "shard init");
+        double syaw = 0, sx = 0, sy = 0;
+        for (int s = 0; s < 6; ++s) {
+            syaw += 0.002;
+            sx += 0.02 * std::cos(syaw);
+            sy += 0.02 * std::sin(syaw);
+            Pose b2o;
+            b2o.position[0] = sx; b2o.position[1] = sy;
+            b2o.orientation[0] = std::cos(syaw / 2); b2o.orientation[3] = std::sin(syaw / 2);
+            eslam_step_input in = PoseEstimator::make_input(bs, b2o.orientation, b2o.position, odo, 0);
+            int u = 0;
+            EXPECT(eslam_gpu_step(shard.handle(), &in, &u) == ESLAM_OK, "shard step");
+        }
+        std::vector<PoseParticle> b = shard.getParticles();
+        size_t sdiff = b.size() == n ? 0 : 1;
+        for (size_t i = 0; i < n && !sdiff; ++i)
+            sdiff += std::memcmp(&a[i], &b[i], sizeof(double) * 6) != 0;
+        EXPECT(sdiff == 0, "RCCL shard (1 rank) == single GPU, bit for bit");
+    }
+
     // error mapping: PoseEstimator::update without an environment
     PoseEstimator bare(cfg);
     bare.init(100, Pose2D{}, Pose2D{0.1, 0.1, 0.1}, 0.18, 1.0);
