@@ -1457,7 +1457,15 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
     // the wave's cumulative range [wlo, whi]: every count it needs reads only draws in
     // [dlo, dhi) (the windows k* - 1 .. k* + 1 of wlo and whi, clamped to [0, N))
-    const uint64_t wlo = __shfl(base, 0, 64), whi = __shfl(base + run, 63, 64);
+    // wave-uniform by construction: moved to SGPRs, so the window bounds, the loop and the
+    // jump-ahead table reads of the first draw are scalar (readfirstlane returns int: each
+    // half is widened as unsigned)
+    auto rfl64 = [](uint64_t v) {
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        return ((uint64_t)hi << 32) | (uint64_t)lo;
+    };
+    const uint64_t wlo = rfl64(__shfl(base, 0, 64)), whi = rfl64(__shfl(base + run, 63, 64));
     const uint64_t ks_lo = kstar_of(wlo, N, shift), ks_hi = kstar_of(whi, N, shift);
     const uint64_t dlo = ks_lo >= 1 ? ks_lo - 1 : 0;
     const uint64_t dhi = ks_hi + 2 < N ? ks_hi + 2 : N;
