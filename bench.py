@@ -45,6 +45,9 @@ def parse():
                     help="multi-GPU exchanges: the library's own RCCL communicator, or torch.distributed callbacks")
     ap.add_argument("--cpu-sample", type=int, default=1048576, help="particles in the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=48)
+    ap.add_argument("--cpu-threads", type=int, default=1,
+                    help="OpenMP threads of the oracle's per-particle loops (1 = the reference default, "
+                         "USE_OPENMP off; results are identical for any count)")
     return ap.parse_args()
 
 
@@ -85,8 +88,9 @@ def workload_name(n, world, rough):
 
 
 def cpu_baseline(args, grid):
-    """The CPU oracle (a restatement of the reference path, reference-order double sums),
-    single-threaded on this host, on a bounded sample of the same workload."""
+    """The CPU oracle (a restatement of the reference path, reference-order double sums) on
+    this host, on a bounded sample of the same workload: one thread by default (the
+    reference's build default), --cpu-threads for its OpenMP per-particle loops."""
     import eslam_abi as A
     import oracle_ffi as O
     import synthetic as S
@@ -94,6 +98,7 @@ def cpu_baseline(args, grid):
     stream = S.step_stream(args.cpu_steps + 1)
     cfg = S.bench_config(A.default_config(), n)
     f = O.OracleFilter(cfg, O.SUM_REFERENCE)
+    f.set_threads(args.cpu_threads)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
     f.step(stream[0])                     # first step (uniform reset) untimed
@@ -103,9 +108,9 @@ def cpu_baseline(args, grid):
         f.step(st)
         k += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": 1, "kind": "port",
+    return {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": args.cpu_threads, "kind": "port",
             "sample": f"{n} particles x {k} steps of the same workload (flat map, forced update+resample), "
-                      f"oracle/eslam_oracle.c in reference-sum mode, 1 thread, {dt:.1f} s"}
+                      f"oracle/eslam_oracle.c in reference-sum mode, {args.cpu_threads} thread(s), {dt:.1f} s"}
 
 
 def main():

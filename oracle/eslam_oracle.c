@@ -469,6 +469,10 @@ struct or_filter {
     eslam_comm comm;
     uint64_t n_global, gbase;
     uint64_t gall[ESLAM_ORACLE_MAX_RANKS + 1];
+    /* host threads of the per-particle loops (or_set_threads; 1 = the reference default,
+     * USE_OPENMP off).  Results do not depend on it: the loops write per-particle outputs
+     * only and every sum stays sequential or in the canonical chunk order. */
+    int threads;
 };
 
 /* global particle count: the N of every formula of the reference */
@@ -512,6 +516,7 @@ or_filter* or_create(const eslam_config* cfg, int sum_mode)
     or_filter* f = calloc(1, sizeof(or_filter));
     f->cfg = *cfg;
     f->sum_mode = sum_mode;
+    f->threads = 1;
     f->minstd = dm_minstd_seed(cfg->seed);      /* ParticleFilter(seed) src/ParticleFilter.hpp:24-27 */
     dm_libc_srand(&f->libc, 1);                 /* the reference never calls srand() */
     f->max_weight = 0;                          /* src/PoseEstimator.cpp:13-25 */
@@ -520,6 +525,8 @@ or_filter* or_create(const eslam_config* cfg, int sum_mode)
     set_translation_pose(f->ud_pose, 1000, 0, 0);
     return f;
 }
+
+void or_set_threads(or_filter* f, int threads) { f->threads = threads > 1 ? threads : 1; }
 
 void or_destroy(or_filter* f)
 {
@@ -848,7 +855,9 @@ int or_project(or_filter* f, const eslam_step_input* in)
     const double tf = c->spread_translation_factor * spread;
     const double rf = c->spread_rotation_factor * spread;
     const double* L = pp.L;
-    for (uint64_t i = 0; i < f->n; ++i) {
+    const int64_t n = (int64_t)f->n;
+#pragma omp parallel for schedule(static) num_threads(f->threads) if (f->threads > 1)
+    for (int64_t i = 0; i < n; ++i) {
         double z0, z1, z2, sn0, sn1 = 0, sn2 = 0;
         const uint64_t gi = f->gbase + i;
         /* draw layout: call 0 -> Box-Muller pairs (z0, z1), (z2, sn0); call 1 -> slip test,
@@ -971,9 +980,9 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
 {
     if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
     const eslam_config* c = &f->cfg;
-    or_contact_model cm;
-    or_cm_init(&cm, c);
-    or_cm_set_contact_points(&cm, in->n_contacts, in->contacts, in->body2odometry_rot);
+    or_contact_model cm0;
+    or_cm_init(&cm0, c);
+    or_cm_set_contact_points(&cm0, in->n_contacts, in->contacts, in->body2odometry_rot);
 
     uint64_t total_points = 0, data_particles = 0;
     double sum_data_weights = 0.0;      /* reference mode */
@@ -985,7 +994,13 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     uint8_t* bucket = malloc(f->n);
     int err = 0;
 
-    for (uint64_t i = 0; i < f->n; ++i) {
+    int zero_var = 0;
+    const int64_t n = (int64_t)f->n;
+#pragma omp parallel num_threads(f->threads) if (f->threads > 1) reduction(+ : total_points, data_particles) reduction(max : maxw) reduction(| : zero_var)
+    {
+    or_contact_model cm = cm0;            /* per-thread scratch of evaluatePose */
+#pragma omp for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
         double s, co;
         dm_sincos(f->th[i], &s, &co);
         const double r22 = (1.0 - co) + co;
@@ -993,7 +1008,7 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         double T[12] = {co, -s, 0.0, f->x[i], s, co, 0.0, f->y[i], 0.0, 0.0, r22, f->z[i]};
         const double meas_var = f->zs[i] * f->zs[i] + me2;
         int acc = or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
-        if (acc < 0) { err = ESLAM_ERR_ZERO_MEAS_VAR; break; }
+        if (acc < 0) { zero_var = 1; acc = 0; }
         sw_val[i] = 0.0;
         if (acc) {
             double zvar = f->zs[i] * f->zs[i];
@@ -1009,7 +1024,6 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
             /* pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found)) */
             if (!cm.use_shape_update || found == 0) sw_val[i] = dm_pow(weight, 1.0 / (double)found);
             else sw_val[i] = weight == 0.0 ? 0.0 : dm_exp((-0.5 * cm.shape_s2) * (1.0 / (double)found));
-            sum_data_weights += sw_val[i];
             total_points += found;
         } else {
             f->floating[i] = 1;
@@ -1023,7 +1037,11 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         f->dbg_zdelta[i] = acc ? cm.zdelta : 0.0;
         f->dbg_zvar[i] = acc ? cm.zvar : 0.0;
     }
+    }
+    if (zero_var) err = ESLAM_ERR_ZERO_MEAS_VAR;
     if (err) { free(a_val); free(sw_val); free(bucket); return err; }
+    /* reference mode: the sequential sum in particle order (non-data particles add +0.0) */
+    for (uint64_t i = 0; i < f->n; ++i) sum_data_weights += sw_val[i];
 
     const uint32_t J = dm_chunk_rows(NG(f));
     /* contract mode: every exact partial sum of the update; sharded filters combine them

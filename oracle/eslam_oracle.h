@@ -91,6 +91,9 @@ int or_hash_poses(or_filter* f, double* x, double* y, double* th, double* z, int
 
 or_filter* or_create(const eslam_config* cfg, int sum_mode);
 void or_destroy(or_filter* f);
+/* host threads (OpenMP) of the per-particle project / updateWeights loops; default 1.
+ * Results are identical for every thread count. */
+void or_set_threads(or_filter* f, int threads);
 int or_set_map(or_filter* f, const eslam_mls_grid* g);            /* copies the grid */
 int or_init_gaussian(or_filter* f, uint64_t n, const double mu[3], const double sigma[3],
                      double zpos, double zsigma);

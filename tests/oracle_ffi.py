@@ -59,6 +59,7 @@ def lib():
     L.or_create.restype = vp
     L.or_create.argtypes = [C.POINTER(A.Config), C.c_int]
     L.or_destroy.argtypes = [vp]
+    L.or_set_threads.argtypes = [vp, C.c_int]
     L.or_set_map.argtypes = [vp, C.POINTER(A.MlsGrid)]
     L.or_init_gaussian.argtypes = [vp, C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double, C.c_double]
     L.or_init_pose.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -133,6 +134,10 @@ class OracleFilter:
         if getattr(self, "h", None):
             self.L.or_destroy(self.h)
             self.h = None
+
+    def set_threads(self, threads):
+        """OpenMP threads of the per-particle loops (results identical for any count)."""
+        self.L.or_set_threads(self.h, int(threads))
 
     def set_comm(self, comm, n_global):
         """Sharded mode over a host-memory eslam_comm (slam-eslam_amd/eslam_dist.TorchComm)."""
