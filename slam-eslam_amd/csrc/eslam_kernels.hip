@@ -1221,7 +1221,6 @@ __device__ __forceinline__ void mark_segment(uint32_t* __restrict__ marks, uint3
 // doubles so both the striped writes and the blocked (8 per thread) reads are conflict-free
 constexpr int kSkew = 32;
 constexpr int kStageV = kScanTile + kScanTile / kSkew;
-constexpr int kMarkStage = 2 * kScanTile;       // outputs of one tile staged in LDS (16 KB)
 
 __device__ __forceinline__ int skew(int k) { return k + k / kSkew; }
 
@@ -1240,45 +1239,28 @@ __device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uin
 constexpr int kWaveDraws = 576;          // stratified draws one wave holds in LDS at a time (K3b)
 constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * kWaveDraws: per-target windows
 
-// K3b's LDS: the staged weights, then the wave's draws, then the staged marks (each dead
-// before the next is written)
+// K3b's LDS: the staged weights, then the wave's draws (the weights are dead before the
+// draws are written)
 union K3bLds {
     double v[kStageV];
     uint64_t T[kWaves][kWaveDraws];
-    uint32_t m[kMarkStage];
 };
 
-struct TileMarks {                       // LDS scratch of the mark flush
-    uint32_t* m;                         // kMarkStage words
-    uint64_t L, H;
-};
-
-// Write the marks of the tile's outputs [L, H) (relative to the slice).  The tile owns
-// that range exclusively, so when it fits in LDS it is written densely and coalesced
-// (zeros included); otherwise each segment start is stored directly.  seg_lo/seg_hi:
-// this thread's segments (relative; empty when equal), val: their mark values.
-__device__ __forceinline__ void flush_marks(TileMarks& tm, uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
+// Write the marks of the tile's segment starts (relative to the slice) and the row carries
+// of tile_first.  The marks buffer is all zero here (the gather clears every mark it
+// reads), so only the segment starts are stored: direct stores measured ~1 µs faster per
+// step than staging the tile's output range in LDS and writing it densely.
+// seg_lo/seg_hi: this thread's segments (relative; empty when equal), val: their values.
+__device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
                                             const uint64_t (&seg_lo)[kScanItems], const uint64_t (&seg_hi)[kScanItems],
                                             const uint32_t (&val)[kScanItems])
 {
-    const uint32_t tid = threadIdx.x;
-    const uint64_t L = tm.L, H = tm.H;
-    const bool staged = H - L <= (uint64_t)kMarkStage;
-    if (staged) {
-        for (uint64_t k = tid; k < H - L; k += kBlock) tm.m[k] = 0u;
-        __syncthreads();
-    }
 #pragma unroll
     for (int q = 0; q < kScanItems; ++q) {
         const uint64_t lo = seg_lo[q], hi = seg_hi[q];
         if (hi <= lo) continue;
-        if (staged) tm.m[lo - L] = val[q];
-        else marks[lo] = val[q];
+        marks[lo] = val[q];
         for (uint64_t t = (lo + kRow - 1) / kRow; t * kRow < hi; ++t) tile_first[t] = val[q] - 1u;
-    }
-    if (staged) {
-        __syncthreads();
-        for (uint64_t k = tid; k < H - L; k += kBlock) marks[L + k] = tm.m[k];
     }
 }
 
@@ -1426,14 +1408,12 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
 {
     __shared__ uint64_t s_wtot[kWaves];
     __shared__ K3bLds s_u;
-    __shared__ TileMarks s_tm;
     if (!ctl->resample) return;
     PROF_INIT();
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * kScanTile;
-    if (tid == 0) s_tm.m = s_u.m;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const int k = r * kBlock + (int)tid;
@@ -1514,7 +1494,6 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     }
     PROF(4);
     if (i0 == 0) lo = 0;
-    if (tid == 0) s_tm.L = lo;
     uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
     uint32_t val[kScanItems];
 #pragma unroll
@@ -1530,14 +1509,12 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
             }
             seg_lo[r] = lo;
             seg_hi[r] = hi;
-            if (i + 1 == sp.n || (r == kScanItems - 1 && tid == kBlock - 1)) s_tm.H = hi;
             lo = hi;
         }
     }
     PROF(5);
-    __syncthreads();
     PROF(6);
-    flush_marks(s_tm, marks, tile_first, seg_lo, seg_hi, val);
+    flush_marks(marks, tile_first, seg_lo, seg_hi, val);
     PROF(7);
     PROF_FLUSH_AT(16);
 }
@@ -1567,10 +1544,8 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
 {
     __shared__ uint64_t s_wtot[kWaves];
     __shared__ K3bLds s_u;
-    __shared__ TileMarks s_tm;
     double* s_v = s_u.v;
     if (!ctl->resample) return;
-    if (threadIdx.x == 0) s_tm.m = s_u.m;
     const uint32_t tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
@@ -1595,9 +1570,6 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, 1.0 / (double)N, jt, 0};
     cur.seek(base);
     uint64_t lo = i0 == 0 ? O0 : cur.k;
-    // the tile's own-slice outputs: [clip(lo_first), clip(hi_last)) relative to W0
-    auto clip = [&](uint64_t v) { return (v < W0 ? W0 : (v > W1 ? W1 : v)) - W0; };
-    if (tid == 0) s_tm.L = clip(lo);
     uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
     uint32_t val[kScanItems];
 #pragma unroll
@@ -1629,11 +1601,9 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
                 }
             }
         }
-        if (i + 1 == sp.n || (r == kScanItems - 1 && tid == kBlock - 1)) s_tm.H = clip(hi);
         lo = hi;
     }
-    __syncthreads();
-    flush_marks(s_tm, marks, tile_first, seg_lo, seg_hi, val);
+    flush_marks(marks, tile_first, seg_lo, seg_hi, val);
 }
 
 // one record per output of this rank that lands in another slice: send slot j of
