@@ -307,10 +307,10 @@ static void rec(eslam_ctx* ctx, int k)
     if (!ctx->timing) return;
     if (ctx->ring.empty()) {
         ctx->ring.resize(5 * kRingSteps);
-        for (auto& e : ctx->ring) hipEventCreate(&e);
+        for (auto& e : ctx->ring) (void)hipEventCreate(&e);   // timing is diagnostic: best effort
     }
     if (ctx->ring_steps >= kRingSteps) return;
-    hipEventRecord(ctx->ring[5 * ctx->ring_steps + k], ctx->stream);
+    (void)hipEventRecord(ctx->ring[5 * ctx->ring_steps + k], ctx->stream);
     if (k == 4) ctx->ring_steps++;
 }
 
@@ -397,14 +397,17 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
             rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "device allocation failed");
             break;
         }
-        hipMemset(ctx->shards, 0, sizeof(Shard) * kNShard);
+        if (hipMemset(ctx->shards, 0, sizeof(Shard) * kNShard) != hipSuccess) { rc = fail(ctx, ESLAM_ERR_HIP, "shard reset"); break; }
         memset(ctx->ctl_host, 0, sizeof(Ctl));
         ctx->ctl_host->minstd = dm_minstd_seed(cfg->seed);     // ParticleFilter(seed)
         dm_libc_srand(&ctx->libc, 1);                            // the reference never seeds rand()
         ctx->ctl_host->max_weight = 0.0;                         // PoseEstimator ctor
         ctx->ctl_host->wexp = 1;
         ctx->ctl_host->scan_shift = 60;
-        hipMemcpy(ctx->ctl, ctx->ctl_host, sizeof(Ctl), hipMemcpyHostToDevice);
+        if (hipMemcpy(ctx->ctl, ctx->ctl_host, sizeof(Ctl), hipMemcpyHostToDevice) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_HIP, "control block upload");
+            break;
+        }
         // minstd jump tables
         std::vector<uint32_t> jt(2048 + 2048 + 1024);
         uint32_t a = 1;
@@ -415,8 +418,13 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
         const uint32_t a22 = dm_minstd_pow(1ull << 22);
         a = 1;
         for (int i = 0; i < 1024; ++i) { jt[4096 + i] = a; a = dm_mulmod31(a, a22); }
-        hipMemcpy(ctx->jump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice);
-        for (auto& e2 : ctx->ev) hipEventCreate(&e2);
+        if (hipMemcpy(ctx->jump, jt.data(), jt.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            rc = fail(ctx, ESLAM_ERR_HIP, "jump table upload");
+            break;
+        }
+        bool ev_ok = true;
+        for (auto& e2 : ctx->ev) ev_ok &= hipEventCreate(&e2) == hipSuccess;
+        if (!ev_ok) { rc = fail(ctx, ESLAM_ERR_HIP, "event create"); break; }
         if (hipDeviceSynchronize() != hipSuccess) { rc = fail(ctx, ESLAM_ERR_HIP, "device synchronize"); break; }
     } while (0);
     if (rc != ESLAM_OK) {
@@ -430,19 +438,19 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
 
 static void free_particles(eslam_ctx* ctx)
 {
-    hipFree(ctx->state_mem); ctx->state_mem = nullptr;
-    hipFree(ctx->marks); ctx->marks = nullptr;
-    hipFree(ctx->tile_first); ctx->tile_first = nullptr;
-    hipFree(ctx->tile_sum); ctx->tile_sum = nullptr;
-    hipFree(ctx->anc); ctx->anc = nullptr;
-    hipFree(ctx->range); ctx->range = nullptr;
+    (void)hipFree(ctx->state_mem); ctx->state_mem = nullptr;
+    (void)hipFree(ctx->marks); ctx->marks = nullptr;
+    (void)hipFree(ctx->tile_first); ctx->tile_first = nullptr;
+    (void)hipFree(ctx->tile_sum); ctx->tile_sum = nullptr;
+    (void)hipFree(ctx->anc); ctx->anc = nullptr;
+    (void)hipFree(ctx->range); ctx->range = nullptr;
     ctx->n = ctx->cap = 0;
     ctx->has_anc = false;
 }
 
 static void free_map(eslam_ctx* ctx)
 {
-    hipFree(ctx->d_cells); hipFree(ctx->d_patch); hipFree(ctx->d_height);
+    (void)hipFree(ctx->d_cells); (void)hipFree(ctx->d_patch); (void)hipFree(ctx->d_height);
     ctx->d_cells = nullptr; ctx->d_patch = nullptr; ctx->d_height = nullptr;
     ctx->has_map = false;
 }
@@ -452,18 +460,18 @@ namespace { void rccl_release(eslam_ctx* ctx); }
 extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
 {
     if (!ctx) return;
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     rccl_release(ctx);
     free_particles(ctx);
     free_map(ctx);
-    hipFree(ctx->shards); hipFree(ctx->ctl); hipHostFree(ctx->ctl_host); hipFree(ctx->jump);
-    hipFree(ctx->scratch); hipHostFree(ctx->scratch_host);
-    hipFree(ctx->recs); hipFree(ctx->mg); hipHostFree(ctx->mg_host);
-    hipFree(ctx->sendbuf); hipFree(ctx->recvbuf); hipHostFree(ctx->stage);
-    hipFree(ctx->d_hash); hipFree(ctx->d_hash_blist); hipFree(ctx->d_sort); hipFree(ctx->sort_tmp); hipFree(ctx->d_draws);
-    for (auto& e : ctx->ev) if (e) hipEventDestroy(e);
-    for (auto& e : ctx->ring) if (e) hipEventDestroy(e);
-    if (ctx->own_stream && ctx->stream) hipStreamDestroy(ctx->stream);
+    (void)hipFree(ctx->shards); (void)hipFree(ctx->ctl); (void)hipHostFree(ctx->ctl_host); (void)hipFree(ctx->jump);
+    (void)hipFree(ctx->scratch); (void)hipHostFree(ctx->scratch_host);
+    (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
+    (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
+    (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
+    for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
@@ -472,7 +480,7 @@ extern "C" int eslam_gpu_set_stream(eslam_ctx* ctx, void* s)
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (s) {
-        if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+        if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
         ctx->stream = (hipStream_t)s;
         ctx->own_stream = false;
     }
@@ -523,11 +531,11 @@ static int grow(eslam_ctx* ctx, void** buf, uint64_t* cap, uint64_t bytes, bool 
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t want = bytes + bytes / 4 + 4096;
     if (pinned) {
-        hipHostFree(*buf);
+        (void)hipHostFree(*buf);
         *buf = nullptr; *cap = 0;
         HIPCHK(ctx, hipHostMalloc(buf, want));
     } else {
-        hipFree(*buf);
+        (void)hipFree(*buf);
         *buf = nullptr; *cap = 0;
         HIPCHK(ctx, hipMalloc(buf, want));
     }
@@ -891,9 +899,9 @@ extern "C" int eslam_gpu_hash_create(eslam_ctx* ctx)
             rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "hash sweep buffers");
             break;
         }
-        hipMemcpy(d_seg, pts.data(), sizeof(double) * 8 * steps, hipMemcpyHostToDevice);
-        hipMemcpy(d_seg + 8 * steps, orient.data(), sizeof(double) * steps, hipMemcpyHostToDevice);
-        if (eslam_launch_hash_sweep(&g, d_seg, d_seg + 8 * steps, steps, d_out, ctx->stream) != hipSuccess ||
+        if (hipMemcpy(d_seg, pts.data(), sizeof(double) * 8 * steps, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(d_seg + 8 * steps, orient.data(), sizeof(double) * steps, hipMemcpyHostToDevice) != hipSuccess ||
+            eslam_launch_hash_sweep(&g, d_seg, d_seg + 8 * steps, steps, d_out, ctx->stream) != hipSuccess ||
             hipMemcpyAsync(out.data(), d_out, sizeof(int32_t) * total, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
             hipStreamSynchronize(ctx->stream) != hipSuccess) {
             rc = fail(ctx, ESLAM_ERR_HIP, "hash sweep");
@@ -911,8 +919,8 @@ extern "C" int eslam_gpu_hash_create(eslam_ctx* ctx)
         for (uint32_t b = 0; b < nb; ++b) ctx->hash_bstart[b + 1] += ctx->hash_bstart[b];
         std::vector<uint32_t> blist(n ? n : 1), fill(ctx->hash_bstart.begin(), ctx->hash_bstart.end() - 1);
         for (uint64_t i = 0; i < n; ++i) blist[fill[ctx->hash_bucket[i]]++] = (uint32_t)i;
-        hipFree(ctx->d_hash); ctx->d_hash = nullptr;
-        hipFree(ctx->d_hash_blist); ctx->d_hash_blist = nullptr;
+        (void)hipFree(ctx->d_hash); ctx->d_hash = nullptr;
+        (void)hipFree(ctx->d_hash_blist); ctx->d_hash_blist = nullptr;
         const uint64_t cap = n ? n : 1;
         if (hipMalloc(&ctx->d_hash, sizeof(double) * 4 * cap) != hipSuccess ||
             hipMalloc(&ctx->d_hash_blist, sizeof(uint32_t) * cap) != hipSuccess ||
@@ -920,10 +928,10 @@ extern "C" int eslam_gpu_hash_create(eslam_ctx* ctx)
             rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "hash pose buffers");
             break;
         }
-        hipMemcpy(d_ids, ids.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice);
-        hipMemcpy(ctx->d_hash_blist, blist.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice);
         double* hx = ctx->d_hash;
-        if (eslam_launch_hash_poses(&g, d_seg, d_seg + 8 * steps, d_ids, n, hx, hx + cap, hx + 2 * cap, hx + 3 * cap,
+        if ((n && hipMemcpy(d_ids, ids.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice) != hipSuccess) ||
+            (n && hipMemcpy(ctx->d_hash_blist, blist.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) ||
+            eslam_launch_hash_poses(&g, d_seg, d_seg + 8 * steps, d_ids, n, hx, hx + cap, hx + 2 * cap, hx + 3 * cap,
                                     ctx->stream) != hipSuccess ||
             hipStreamSynchronize(ctx->stream) != hipSuccess) {
             rc = fail(ctx, ESLAM_ERR_HIP, "hash poses");
@@ -932,7 +940,7 @@ extern "C" int eslam_gpu_hash_create(eslam_ctx* ctx)
         ctx->hash_n = n;
         ctx->has_hash = true;
     } while (0);
-    hipFree(d_seg); hipFree(d_out); hipFree(d_ids);
+    (void)hipFree(d_seg); (void)hipFree(d_out); (void)hipFree(d_ids);
     return rc;
 }
 
@@ -963,7 +971,7 @@ extern "C" int eslam_gpu_init_hash(eslam_ctx* ctx, uint64_t n)
         e = eslam_launch_init_from_hash(ctx->st[0], d_idx, n, hash_field(ctx, 0), hash_field(ctx, 1), hash_field(ctx, 2),
                                         hash_field(ctx, 3), ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    hipFree(d_idx);
+    (void)hipFree(d_idx);
     HIPCHK(ctx, e);
     return ESLAM_OK;
 }
@@ -1330,8 +1338,8 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
     const double weight = ((S / (double)N) * ctx->cfg.hash_avg_factor) * rel;   // getWeightAvg() * avgFactor * rel
     const uint64_t n = ctx->n;
     if (ctx->sort_cap < n) {
-        hipFree(ctx->d_sort); ctx->d_sort = nullptr; ctx->sort_cap = 0;
-        hipFree(ctx->sort_tmp); ctx->sort_tmp = nullptr; ctx->sort_tmp_bytes = 0;
+        (void)hipFree(ctx->d_sort); ctx->d_sort = nullptr; ctx->sort_cap = 0;
+        (void)hipFree(ctx->sort_tmp); ctx->sort_tmp = nullptr; ctx->sort_tmp_bytes = 0;
         HIPCHK(ctx, hipMalloc(&ctx->d_sort, sizeof(uint32_t) * 4 * n));
         size_t bytes = 0;
         HIPCHK(ctx, eslam_hash_sort(ctx->st[0], ctx->st[1], ctx->ctl, n, nullptr, nullptr, nullptr, nullptr, nullptr, &bytes,
@@ -1350,7 +1358,7 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
     std::vector<uint32_t> draws(k);
     for (uint64_t j = 0; j < k; ++j) draws[j] = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&ctx->libc) % bsize);
     if (ctx->draws_cap < k) {
-        hipFree(ctx->d_draws); ctx->d_draws = nullptr; ctx->draws_cap = 0;
+        (void)hipFree(ctx->d_draws); ctx->d_draws = nullptr; ctx->draws_cap = 0;
         HIPCHK(ctx, hipMalloc(&ctx->d_draws, sizeof(uint32_t) * k));
         ctx->draws_cap = k;
     }
@@ -1456,8 +1464,8 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         for (uint32_t k = 0; k < ctx->ring_steps; ++k) {
             hipEvent_t* e = &ctx->ring[5 * k];
             float ms;
-            for (int j = 0; j < 4; ++j) { ms = 0; hipEventElapsedTime(&ms, e[j], e[j + 1]); acc[j] += ms; }
-            ms = 0; hipEventElapsedTime(&ms, e[0], e[4]); acc[4] += ms;
+            for (int j = 0; j < 4; ++j) { ms = 0; (void)hipEventElapsedTime(&ms, e[j], e[j + 1]); acc[j] += ms; }
+            ms = 0; (void)hipEventElapsedTime(&ms, e[0], e[4]); acc[4] += ms;
         }
         eslam_kernel_times& t = ctx->times;
         const double inv = 1.0 / ctx->ring_steps;
@@ -1649,7 +1657,7 @@ extern "C" int eslam_gpu_selftest_bm_radius(int device, uint64_t* mismatches)
     if (e == hipSuccess) e = hipDeviceSynchronize();
     unsigned long long h = 0;
     if (e == hipSuccess) e = hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
-    hipFree(d);
+    (void)hipFree(d);
     *mismatches = h;
     return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
 }
@@ -1661,12 +1669,11 @@ extern "C" int eslam_gpu_selftest_math(int device, int fn, const double* x, cons
     const uint64_t b = (n ? n : 1) * 8;
     if (hipMalloc(&dx, b) != hipSuccess || hipMalloc(&dy, b) != hipSuccess || hipMalloc(&dout, b) != hipSuccess)
         return ESLAM_ERR_OUT_OF_MEMORY;
-    hipMemcpy(dx, x, n * 8, hipMemcpyHostToDevice);
-    if (y) hipMemcpy(dy, y, n * 8, hipMemcpyHostToDevice);
-    else hipMemset(dy, 0, b);
-    hipError_t e = eslam_launch_selftest_math(fn, dx, dy, dout, n, nullptr);
+    hipError_t e = n ? hipMemcpy(dx, x, n * 8, hipMemcpyHostToDevice) : hipSuccess;
+    if (e == hipSuccess) e = (y && n) ? hipMemcpy(dy, y, n * 8, hipMemcpyHostToDevice) : hipMemset(dy, 0, b);
+    if (e == hipSuccess) e = eslam_launch_selftest_math(fn, dx, dy, dout, n, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
-    hipFree(dx); hipFree(dy); hipFree(dout);
+    (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dout);
     return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
 }

@@ -2035,7 +2035,8 @@ extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n
     if (e != hipSuccess) return e;
     double* a = tmp;
     double* b = tmp + cap * 5;
-    hipMemsetAsync(a, 0, 5 * sizeof(double), stream);
+    e = hipMemsetAsync(a, 0, 5 * sizeof(double), stream);
+    if (e != hipSuccess) { (void)hipFreeAsync(tmp, stream); return e; }
     const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
     if (blocks) hipLaunchKernelGGL(k_centroid_chunks, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, J, ctl, a);
     uint64_t m = chunks;
@@ -2045,9 +2046,9 @@ extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n
         double* t = a; a = b; b = t;
         m = m2;
     }
-    hipMemcpyAsync(out, a, 5 * sizeof(double), hipMemcpyDeviceToDevice, stream);
     e = hipGetLastError();
-    hipFreeAsync(tmp, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, a, 5 * sizeof(double), hipMemcpyDeviceToDevice, stream);
+    (void)hipFreeAsync(tmp, stream);
     return e;
 }
 
