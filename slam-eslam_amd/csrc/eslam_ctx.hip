@@ -213,7 +213,7 @@ struct eslam_ctx {
     void* state_mem = nullptr;
     uint32_t* marks = nullptr;
     uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
-    uint64_t* tile_sum = nullptr;           // per scan tile: fixed-point total, then exclusive prefix
+    uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total
     uint32_t* anc = nullptr;
     bool has_anc = false;
     // statistics and control
@@ -1481,7 +1481,6 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         write_ctl(ctx);
         return fail(ctx, ESLAM_ERR_ZERO_MEAS_VAR, "using a zero measurement variance leads to singularities");
     }
-    if (c.err & 2ull) return fail(ctx, ESLAM_ERR_HIP, "prefix-sum look-back timed out");
     return ESLAM_OK;
 }
 

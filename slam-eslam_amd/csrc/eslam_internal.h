@@ -5,7 +5,7 @@
 //              (flags = n_contact_points | floating << 7); double-buffered for resample
 //   marks      uint32 per particle: resample segment starts (particle index + 1)
 //   row_first  uint32 per 64 outputs: source covering the row's first output
-//   status     uint64 per scan tile: decoupled look-back words (2-bit tag | 62-bit value)
+//   tile_sum   uint64 per scan tile: exact fixed-point weight total (K3a), read by K3b
 //   shards     NSHARD x Shard: exact fixed-point statistics of the weighting kernel
 //   ctl        Ctl: per-step scalars decided on the device (no host round trip per step)
 //   jump       minstd jump-ahead tables A^(i), A^(i*2^11), A^(i*2^22)

@@ -11,10 +11,16 @@
 //   k_finalize        one block: floating weight, phase-B factors, normalisation sum,
 //                     effective count and the resample decision (src/PoseEstimator.cpp:329,
 //                     src/ParticleFilter.hpp:46-70, src/PoseEstimator.cpp:250)
-//   k_normalize_scan  phase B + normalisation + decoupled look-back prefix sum of the
-//                     fixed-point weights + the stratified-draw segment boundaries
-//                     (src/PoseEstimator.cpp:332-345, src/ParticleFilter.hpp:85-108)
-//   k_resample_gather expand the segments (max-scan) and gather the particle state
+//   k_normalize_scan  phase B + normalisation (src/PoseEstimator.cpp:332-345,
+//                     src/ParticleFilter.hpp:46-70) and, when resampling, each tile's exact
+//                     fixed-point weight total
+//   k_segments        stratified resample (src/ParticleFilter.hpp:85-108): the tile prefix
+//                     (sum of the preceding tile totals), a blocked fixed-point scan, the
+//                     wave's draws in LDS, and the segment-start marks of every ancestor
+//
+// The resample gather (expand the marks by a max-scan, copy the ancestor's state) is fused
+// into the next step's k_project_weight; k_resample_gather materialises a pending gather
+// when the state is read (download, the standalone PoseEstimator API) before that.
 //
 // Everything is wave64: 256-thread blocks, butterfly reductions with __shfl_xor over 64
 // lanes, ballots as 64-bit masks.  All arithmetic goes through include/eslam_detmath.h and
@@ -1184,8 +1190,9 @@ struct DrawCursor {
 };
 
 // ---------------------------------------------------------------------------------------
-// k_normalize_scan: phase B + normalisation, then (when resampling) the decoupled
-// look-back prefix sum of the fixed-point weights and the segment boundaries.
+// k_normalize_scan (K3a): phase B + normalisation and the tile totals; k_segments (K3b):
+// the prefix of the fixed-point weights and the segment boundaries.  No cross-tile waiting
+// inside a kernel: K3b re-sums the preceding tile totals (exact integers, any order).
 // ---------------------------------------------------------------------------------------
 
 
