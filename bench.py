@@ -23,10 +23,13 @@ sys.path.insert(0, os.path.join(ROOT, "slam-eslam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 # algorithmic bytes per particle-update (208 B for the whole step)
-BYTES_TOTAL = 208             # predict+weight 96, normalise 8, resample 104 (scan 8, gather 48, write 48)
+BYTES_REFERENCE = 208         # the reference algorithm's passes: predict+weight 96, normalise 8,
+                              # resample 104 (scan 8, gather 48, write 48) -- reported, not the roofline
 # per kernel as launched: the resample gather is fused into the next step's k_project_weight
 BYTES_K1 = 104                # gathered read 6 x f64 + write 6 x f64 + 4-byte mark read/clear
 BYTES_K3 = 28                 # phase B / normalise read+write w (16), scan re-read (8), marks (4)
+BYTES_STEP = BYTES_K1 + BYTES_K3   # what the fused step moves per particle-update: the step roofline
+CONFIG3_GLOBAL = 16 * 1024 * 1024  # BASELINE configs[3]: 16M particles over 8 GPUs
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -35,7 +38,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--particles", type=int, default=4 * 1024 * 1024, help="particles per GPU")
+    ap.add_argument("--particles", type=int, default=None,
+                    help="particles per GPU (default: configs[2]'s 4M on one GPU; configs[3]'s 2M per GPU "
+                         "-- 16M global at 8 GPUs -- on several)")
     ap.add_argument("--map-cells", type=int, default=1000)
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -84,7 +89,25 @@ def workload_name(n, world, rough):
         return "configs[4]-style terrain"
     if world == 1:
         return {262144: "configs[1]", 4 * 1024 * 1024: "configs[2]"}.get(n, "custom size")
+    if n * world == CONFIG3_GLOBAL:
+        return "configs[3]"
+    if n == CONFIG3_GLOBAL // 8:
+        return "configs[3]'s 2M-per-GPU shard, weak-scaled to %d GPUs" % world
     return "configs[2] per GPU, weak-scaled" if n == 4 * 1024 * 1024 else "custom size, weak-scaled"
+
+
+def host_cpu():
+    """model name and logical CPU count of this host (the CPU baseline's machine)"""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
 
 
 def cpu_baseline(args, grid):
@@ -108,13 +131,48 @@ def cpu_baseline(args, grid):
         f.step(st)
         k += 1
     dt = time.perf_counter() - t0
+    model, ncpu = host_cpu()
     return {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": args.cpu_threads, "kind": "port",
+            "cpu_model": model, "host_logical_cpus": ncpu,
             "sample": f"{n} particles x {k} steps of the same workload (flat map, forced update+resample), "
                       f"oracle/eslam_oracle.c in reference-sum mode, {args.cpu_threads} thread(s), {dt:.1f} s"}
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N ranks of this script as child processes
+    (fresh interpreters, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), forward rank 0's JSON line
+    and exit with the worst exit code.  The parent never touches the GPU: it counts devices
+    (no HIP initialisation on this image) and execs nothing."""
+    import subprocess
+    import socket
+    import torch
+    visible = torch.cuda.device_count()
+    if visible < args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible\n")
+        sys.exit(2)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    bad = [r for r in rcs if r]
+    sys.exit(0 if not bad else (bad[0] if bad[0] > 0 else 128 - bad[0]))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args)
+    if args.particles is None:
+        args.particles = 4 * 1024 * 1024 if args.gpus == 1 else CONFIG3_GLOBAL // 8
     # stdout carries exactly one JSON line: native libraries (RCCL prints a version banner
     # when a communicator is created) write to stderr until the result is printed
     sys.stdout.flush()
@@ -123,6 +181,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
+        sys.exit(2)
     dist = None
     sharded = world > 1 or args.sharded
     if sharded:
@@ -235,7 +296,11 @@ def main():
         "kernel_ms": {k: round(v, 5) for k, v in kt.items()},
         "kernel_ms_note": "HIP events around every launch on the context stream, over a second pass of "
                           "the same K steps (ms_per_step with events: %.4f)" % (dt_ev / args.steps * 1e3),
-        "step_roofline_frac": round(BYTES_TOTAL * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "step_roofline_frac": round(BYTES_STEP * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "step_roofline_note": "%d B per particle-update: the fused step's algorithmic bytes (K1 %d + K3 %d); the "
+                              "reference algorithm's unfused passes would move %d B (fraction %.4f)"
+                              % (BYTES_STEP, BYTES_K1, BYTES_K3, BYTES_REFERENCE,
+                                 BYTES_REFERENCE * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world)),
         "last_update": {"effective": info.effective, "resampled": info.resampled},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

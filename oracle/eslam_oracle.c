@@ -230,7 +230,40 @@ void or_cm_set_contact_points(or_contact_model* cm, uint32_t n, const eslam_cont
 /* ContactModel::contactLikelihoodRatio  src/ContactModel.cpp:104-115 */
 static double contact_likelihood_ratio(const or_contact_model* cm, double z, double sigma)
 {
+    if (cm->literal) {
+        /* boost::math::normal n(0, sd): pdf = exp(-(z - 0)^2 / (2 sd^2)) / (sd sqrt(2 pi)),
+         * cdf = erfc(-(z - 0) / (sd sqrt 2)) / 2  (boost/math/distributions/normal.hpp) */
+        const double sd = sigma * cm->correction;
+        double exponent = z * z;
+        exponent /= -2.0 * sd * sd;
+        const double pdf = exp(exponent) / (sd * 2.50662827463100050242);
+        const double cdf = erfc(-(z / (sd * 1.41421356237309504880))) / 2.0;
+        return pdf / cdf;
+    }
     return dm_normal_pdf_cdf_ratio(z, sigma * cm->correction);
+}
+
+/* src/ContactModel.cpp:262-317 literally: d1 += zdiff / zvar, d2 += 1 / zvar, delta = d1 / d2,
+ * pz *= exp(-(odiff^2) / 2) with odiff = (zdiff - delta) / sqrt(zvar) */
+static void evaluate_weight_literal(or_contact_model* cm)
+{
+    double d1 = 0, d2 = 0;
+    for (uint32_t i = 0; i < cm->ncp; ++i) {
+        d1 += cm->cp[i].zdiff / cm->cp[i].zvar;
+        d2 += 1.0 / cm->cp[i].zvar;
+    }
+    const double delta = d1 / d2;
+    double pz = 1.0, s2 = 0.0;
+    for (uint32_t i = 0; i < cm->ncp; ++i) {
+        const double odiff = (cm->cp[i].zdiff - delta) / sqrt(cm->cp[i].zvar);
+        const double zk = exp(-(odiff * odiff) / (2.0));
+        if (cm->use_shape_update) pz *= zk;
+        s2 += odiff * odiff;
+    }
+    cm->shape_s2 = s2;
+    cm->weight = pz;
+    cm->zdelta = -delta;
+    cm->zvar = 1.0 / d2;
 }
 
 /* ContactModel::evaluateWeight  src/ContactModel.cpp:262-317, restated at the rounding
@@ -239,6 +272,7 @@ static double contact_likelihood_ratio(const or_contact_model* cm, double z, dou
  * The sum is kept (shape_s2) so that m^(1/n) = exp(-s2 / (2 n)) needs no log.           */
 static void evaluate_weight(or_contact_model* cm)
 {
+    if (cm->literal) { evaluate_weight_literal(cm); return; }
     /* src/ContactModel.cpp:262-317 with rounding-level restatements:
      * 1/zvar once per point, delta = d1 * (1/d2), odiff^2 = (zdiff - delta)^2 / zvar,
      * prod exp(-odiff^2 / 2) = exp(-s2 / 2) */
@@ -298,11 +332,11 @@ int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_va
             double mean, stdev;
             if (map(user, w, w[2], meas_var, &mean, &stdev)) {
                 const double zdiff = w[2] - mean;
-                const double pose_var = stdev * stdev;
-                const double zvar = stdev * stdev + meas_var;
+                const double pose_var = cm->literal ? pow(stdev, 2) : stdev * stdev;
+                const double zvar = (cm->literal ? pow(stdev, 2) : stdev * stdev) + meas_var;
                 const double sq = sqrt(zvar);
                 const int ends = (gid == -1 || i + 1 == cm->m || gid != cm->group[i + 1]);
-                if (!valid && ends && ratio_surely_significant(zdiff, zvar, cm->correction)) {
+                if (!cm->literal && !valid && ends && ratio_surely_significant(zdiff, zvar, cm->correction)) {
                     /* single-point group: push (zdiff, zvar) directly */
                     p.point[0] = w[0]; p.point[1] = w[1]; p.point[2] = mean;
                     p.zdiff = zdiff;
@@ -337,10 +371,16 @@ int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_va
         }
         if (valid && (gid == -1 || i + 1 == cm->m || gid != cm->group[i + 1])) {
             if (group_valid && contact_ratio > 1e-9) {
-                const double inv = 1.0 / contact_ratio;
-                p.zdiff *= inv;
-                p.zvar *= inv;
-                cm->posevar += pose_var_avg * inv;
+                if (cm->literal) {                /* src/ContactModel.cpp:201-203 */
+                    p.zdiff /= contact_ratio;
+                    p.zvar /= contact_ratio;
+                    cm->posevar += pose_var_avg / contact_ratio;
+                } else {
+                    const double inv = 1.0 / contact_ratio;
+                    p.zdiff *= inv;
+                    p.zvar *= inv;
+                    cm->posevar += pose_var_avg * inv;
+                }
                 cm->cp[cm->ncp++] = p;
                 /* useSlipUpdate: p.prob *= matchTerrain(...) happens after the push (Q8) */
             }
@@ -365,7 +405,7 @@ int or_cm_update_z(const or_contact_model* cm, double* z_pos, double* z_var)
     double delta_var = (a < 1e-9) ? 1e-9 : a;         /* std::max(a, 1e-9) */
     const double z_delta = cm->zdelta;
     /* |z_delta / sqrt(delta_var)| > 1 (the "3-sigma" gate is 1 sigma, Q9), squared */
-    if (z_delta * z_delta > delta_var) return 0;
+    if (cm->literal ? fabs(z_delta / sqrt(delta_var)) > 1.0 : z_delta * z_delta > delta_var) return 0;
     double gain = *z_var / (*z_var + cm->zvar);
     *z_pos += gain * z_delta;
     double var_gain = delta_var / (delta_var + cm->zvar);
@@ -473,6 +513,8 @@ struct or_filter {
      * USE_OPENMP off).  Results do not depend on it: the loops write per-particle outputs
      * only and every sum stays sequential or in the canonical chunk order. */
     int threads;
+    int literal;                         /* or_set_literal */
+    int debug;                           /* or_set_debug */
 };
 
 /* global particle count: the N of every formula of the reference */
@@ -504,11 +546,14 @@ static int or_alloc_particles(or_filter* f, uint64_t n)
     f->x = calloc(b, 8); f->y = calloc(b, 8); f->th = calloc(b, 8); f->z = calloc(b, 8);
     f->zs = calloc(b, 8); f->w = calloc(b, 8); f->mprob = calloc(b, 8);
     f->floating = calloc(b, 1); f->ncp = calloc(b, 1); f->anc = calloc(b, 4);
-    f->dbg_ncp = calloc(b, 4);
-    f->dbg_cp = calloc(b * ESLAM_MAX_CONTACTS, sizeof(or_cpoint));
-    f->dbg_zdelta = calloc(b, 8); f->dbg_zvar = calloc(b, 8);
+    if (f->debug) {
+        f->dbg_ncp = calloc(b, 4);
+        f->dbg_cp = calloc(b * ESLAM_MAX_CONTACTS, sizeof(or_cpoint));
+        f->dbg_zdelta = calloc(b, 8); f->dbg_zvar = calloc(b, 8);
+        if (!f->dbg_cp) return ESLAM_ERR_OUT_OF_MEMORY;
+    }
     f->has_anc = 0;
-    return (f->x && f->dbg_cp) ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
+    return f->x ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
 }
 
 or_filter* or_create(const eslam_config* cfg, int sum_mode)
@@ -527,6 +572,30 @@ or_filter* or_create(const eslam_config* cfg, int sum_mode)
 }
 
 void or_set_threads(or_filter* f, int threads) { f->threads = threads > 1 ? threads : 1; }
+
+void or_set_literal(or_filter* f, int literal) { f->literal = literal ? 1 : 0; }
+
+void or_set_debug(or_filter* f, int on)
+{
+    f->debug = on ? 1 : 0;
+    if (f->debug && f->n && !f->dbg_ncp) {
+        const size_t b = (size_t)f->n;
+        f->dbg_ncp = calloc(b, 4);
+        f->dbg_cp = calloc(b * ESLAM_MAX_CONTACTS, sizeof(or_cpoint));
+        f->dbg_zdelta = calloc(b, 8); f->dbg_zvar = calloc(b, 8);
+    }
+}
+
+/* sin and cos of a particle angle: the contract's dm_sincos, or libm (Eigen's Rotation2D /
+ * AngleAxis call std::sin / std::cos) in literal mode */
+static void or_sincos(const or_filter* f, double a, double* s, double* c)
+{
+    if (f->literal) { *s = sin(a); *c = cos(a); }
+    else dm_sincos(a, s, c);
+}
+
+/* std::pow in literal mode, the contract's dm_pow otherwise */
+static double or_pow(const or_filter* f, double x, double y) { return f->literal ? pow(x, y) : dm_pow(x, y); }
 
 void or_destroy(or_filter* f)
 {
@@ -874,7 +943,7 @@ int or_project(or_filter* f, const eslam_step_input* in)
         const double u_slip = dm_u32(d1.v[0]);
         if (u_slip < c->slip_factor) dy *= dm_u32(d1.v[1]);
         double s, co;
-        dm_sincos(f->th[i], &s, &co);
+        or_sincos(f, f->th[i], &s, &co);
         f->x[i] += co * dx - s * dy;
         f->y[i] += s * dx + co * dy;
         f->th[i] += dth;
@@ -983,6 +1052,7 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     or_contact_model cm0;
     or_cm_init(&cm0, c);
     or_cm_set_contact_points(&cm0, in->n_contacts, in->contacts, in->body2odometry_rot);
+    cm0.literal = f->literal;
 
     uint64_t total_points = 0, data_particles = 0;
     double sum_data_weights = 0.0;      /* reference mode */
@@ -1002,11 +1072,11 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
         double s, co;
-        dm_sincos(f->th[i], &s, &co);
+        or_sincos(f, f->th[i], &s, &co);
         const double r22 = (1.0 - co) + co;
         /* Translation3d(x, y, zPos) * AngleAxisd(theta, UnitZ) */
         double T[12] = {co, -s, 0.0, f->x[i], s, co, 0.0, f->y[i], 0.0, 0.0, r22, f->z[i]};
-        const double meas_var = f->zs[i] * f->zs[i] + me2;
+        const double meas_var = f->literal ? pow(f->zs[i], 2) + pow(c->measurement_error, 2) : f->zs[i] * f->zs[i] + me2;
         int acc = or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
         if (acc < 0) { zero_var = 1; acc = 0; }
         sw_val[i] = 0.0;
@@ -1022,7 +1092,8 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
             data_particles++;
             const uint64_t found = cm.ncp;
             /* pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found)) */
-            if (!cm.use_shape_update || found == 0) sw_val[i] = dm_pow(weight, 1.0 / (double)found);
+            if (f->literal) sw_val[i] = pow(weight, 1.0 / (double)found);   /* src/PoseEstimator.cpp:309 */
+            else if (!cm.use_shape_update || found == 0) sw_val[i] = dm_pow(weight, 1.0 / (double)found);
             else sw_val[i] = weight == 0.0 ? 0.0 : dm_exp((-0.5 * cm.shape_s2) * (1.0 / (double)found));
             total_points += found;
         } else {
@@ -1032,10 +1103,12 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         f->ncp[i] = (uint8_t)cm.ncp;
         bucket[i] = (uint8_t)(cm.ncp < DM_NBUCKETS - 1 ? cm.ncp : DM_NBUCKETS - 1);
         a_val[i] = f->w[i] * f->mprob[i];
-        f->dbg_ncp[i] = cm.ncp;
-        memcpy(&f->dbg_cp[i * ESLAM_MAX_CONTACTS], cm.cp, cm.ncp * sizeof(or_cpoint));
-        f->dbg_zdelta[i] = acc ? cm.zdelta : 0.0;
-        f->dbg_zvar[i] = acc ? cm.zvar : 0.0;
+        if (f->dbg_ncp) {
+            f->dbg_ncp[i] = cm.ncp;
+            memcpy(&f->dbg_cp[i * ESLAM_MAX_CONTACTS], cm.cp, cm.ncp * sizeof(or_cpoint));
+            f->dbg_zdelta[i] = acc ? cm.zdelta : 0.0;
+            f->dbg_zvar[i] = acc ? cm.zvar : 0.0;
+        }
     }
     }
     if (zero_var) err = ESLAM_ERR_ZERO_MEAS_VAR;
@@ -1080,7 +1153,7 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     for (int b = 0; b < DM_NBUCKETS; ++b) {
         uint64_t ncp = (uint64_t)b;                      /* bucket 5 = every n >= 5 */
         double expo = (double)(uint64_t)(4ull - ncp);    /* size_t arithmetic (Q2) */
-        ph->f[b] = dm_pow(base, expo);
+        ph->f[b] = or_pow(f, base, expo);
     }
     /* phase B  src/PoseEstimator.cpp:332-345 */
     for (uint64_t i = 0; i < f->n; ++i) {
@@ -1490,6 +1563,7 @@ void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
 
 int or_get_debug(or_filter* f, uint32_t* ncp, or_cpoint* cp, double* zdelta, double* zvar)
 {
+    if (!f->dbg_ncp) return ESLAM_ERR_NOT_INITIALISED;
     uint64_t n = f->n;
     if (ncp) memcpy(ncp, f->dbg_ncp, n * 4);
     if (cp) memcpy(cp, f->dbg_cp, n * ESLAM_MAX_CONTACTS * sizeof(or_cpoint));

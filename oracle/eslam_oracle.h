@@ -56,6 +56,9 @@ typedef struct or_contact_model {
     /* lowest points per group */
     uint32_t nlow;
     double low[ESLAM_MAX_CONTACTS][3];
+    /* 1: the reference's literal arithmetic (or_set_literal), 0: the build's contract */
+    int32_t literal;
+    int32_t pad_literal;
 } or_contact_model;
 
 void or_cm_init(or_contact_model* cm, const eslam_config* cfg);
@@ -94,6 +97,16 @@ void or_destroy(or_filter* f);
 /* host threads (OpenMP) of the per-particle project / updateWeights loops; default 1.
  * Results are identical for every thread count. */
 void or_set_threads(or_filter* f, int threads);
+/* Arithmetic of the per-particle formulas.  0 (default): the build's contract, which the GPU
+ * reproduces bit for bit (eslam_detmath.h transcendentals, the rounding-level restatements of
+ * DESIGN.md 2).  1: the reference's literal expressions -- contactLikelihoodRatio as boost's
+ * pdf / cdf (here libm exp / erfc), the ratio evaluated for every point, the divisions of
+ * src/ContactModel.cpp:201-203 and 270-301, the exp of every point, std::pow for m^(1/n) and
+ * the discount factor, the 1-sigma test through fabs/sqrt, libm sin/cos (Eigen rotations). */
+void or_set_literal(or_filter* f, int literal);
+/* capture per-particle contact points / zDelta / zVar of every updateWeights (or_get_debug);
+ * off by default (1.5 KB per particle) */
+void or_set_debug(or_filter* f, int on);
 int or_set_map(or_filter* f, const eslam_mls_grid* g);            /* copies the grid */
 int or_init_gaussian(or_filter* f, uint64_t n, const double mu[3], const double sigma[3],
                      double zpos, double zsigma);

@@ -1370,6 +1370,19 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
     return ESLAM_OK;
 }
 
+// the device's zero-measurement-variance flag (k_finalize aborted the update): clear it and
+// report the reference's exception text
+static int take_update_error(eslam_ctx* ctx)
+{
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    if (!(ctx->ctl_host->err & 1ull)) return ESLAM_OK;
+    ctx->ctl_host->err = 0;
+    rc = write_ctl(ctx);
+    if (rc) return rc;
+    return fail(ctx, ESLAM_ERR_ZERO_MEAS_VAR, "using a zero measurement variance leads to singularities");
+}
+
 static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project, bool weight)
 {
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
@@ -1403,7 +1416,16 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     rec(ctx, 1);
     if (project) ctx->proj_event++;
     if (gv.record) ctx->has_anc = true;
-    if (weight) return run_update_tail(ctx, FIN_UPDATE, true);   // finalize commits the flip
+    if (weight) {
+        const int rc = run_update_tail(ctx, FIN_UPDATE, true);   // finalize commits the flip
+        if (rc) return rc;
+        // measVar = zSigma^2 + measurementError^2 is zero only when measurementError^2 is: in
+        // that configuration the update is checked at once, so the error surfaces from this
+        // call like the reference's throw (src/ContactModel.cpp:122-123) and the caller's
+        // update gate pose is not advanced (src/EmbodiedSlamFilter.cpp:361-362)
+        if (p.me2 == 0.0) return take_update_error(ctx);
+        return ESLAM_OK;
+    }
     HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
     rec(ctx, 2); rec(ctx, 3); rec(ctx, 4);
     return ESLAM_OK;
@@ -1476,12 +1498,7 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         t.total_ms = (float)(acc[4] * inv);
         ctx->ring_steps = 0;
     }
-    if (c.err & 1ull) {
-        ctx->ctl_host->err = 0;
-        write_ctl(ctx);
-        return fail(ctx, ESLAM_ERR_ZERO_MEAS_VAR, "using a zero measurement variance leads to singularities");
-    }
-    return ESLAM_OK;
+    return take_update_error(ctx);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -50,7 +50,8 @@ struct alignas(128) Ctl {
     uint32_t mode;                       // finalize mode (see FinMode)
     uint32_t special;                    // 1: S NaN, 2: S inf
     uint32_t gather;                     // a resample gather is pending (marks -> state[base^1])
-    uint32_t pad0;
+    uint32_t aborted;                    // the update hit the zero-measurement-variance error (phase B,
+                                         // normalisation and resample skipped, as the reference's throw)
     int32_t scan_shift;                  // fixed-point shift of the resample cumulative sum
     int32_t wexp;                        // weight exponent bound for the next weighting
     double S, Q, eff, fw, max_weight;

@@ -1063,7 +1063,17 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
     ctl->err |= err;
     ctl->tile_counter = 0;
     ctl->overruns = 0;
+    ctl->aborted = 0;
     const double N = (double)fp.n_global;
+    if (fp.mode == FIN_UPDATE && err) {
+        // evaluatePose threw (src/ContactModel.cpp:122-123): updateWeights stops after its
+        // particle loop has run, before the floating weight, phase B, the max-weight update,
+        // normalizeWeights and resample (src/PoseEstimator.cpp:276-352, 244-255)
+        ctl->aborted = 1;
+        ctl->resample = 0;
+        if (fp.mirror) { fp.mirror[0] = 0; fp.mirror[1] = ctl->minstd_start; fp.mirror[2] = (uint64_t)(int64_t)ctl->scan_shift; }
+        return;
+    }
 
     double S = 0.0, Q = 0.0;
     if (fp.mode == FIN_UPDATE) {
@@ -1279,6 +1289,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
 {
     __shared__ uint64_t s_wtot[kWaves];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    if (ctl->aborted) return;            // the update threw (k_finalize): weights stay as phase A left them
     const bool resample = ctl->resample != 0;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;

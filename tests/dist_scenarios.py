@@ -10,14 +10,15 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload")
+SCENARIOS = ("forced", "natural", "upload", "config3")
+CONFIG3_STEPS = 3
 
 
 def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name == "forced":
+    if name in ("forced", "config3"):
         S.bench_config(cfg, n_global)
     else:
         cfg.particle_count = n_global
@@ -28,7 +29,31 @@ def scenario_config(name, n_global):
 
 
 def scenario_grid(name):
+    if name == "config3":
+        return S.flat_map(cells=1000)             # the bench's 100 x 100 m map
     return S.rough_map(cells=120) if name != "forced" else S.rough_map(cells=120, multi=False)
+
+
+def digest(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8)).hexdigest()
+
+
+def run_config3(f, n_global, lo, hi, info_fn):
+    """BASELINE configs[3]'s workload (bench map, forced update + resample, init as the bench)
+    for CONFIG3_STEPS steps; records per-step info and, at the end, a SHA-256 of every field of
+    this shard / slice [lo, hi) and of the last step's ancestors (a 16M-particle snapshot is
+    too large to ship between processes)."""
+    rec = {}
+    f.set_map(scenario_grid("config3"))
+    f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    for k, st in enumerate(S.step_stream(CONFIG3_STEPS)):
+        f.step(st)
+        _info(rec, f"s{k}", info_fn(f))
+    pa = f.download()
+    anc = f.ancestors()
+    return rec, {fld: np.array(getattr(pa, fld)) for fld in FIELDS}, np.asarray(anc), np.array([f.best_index()]), \
+        np.array([f.rng_state().minstd_x])
 
 
 def upload_arrays(n_global, lo, hi):

@@ -47,7 +47,17 @@ def main():
             f = eslam_dist.RcclShardedGpuFilter(cfg, n_global, rank, comm.nranks, device=dev)
         else:
             f = eslam_dist.ShardedGpuFilter(cfg, n_global, comm, device=dev)
-        rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.sync())
+        if name == "config3":
+            from dist_scenarios import digest, run_config3
+            rec, fields, anc, best, rng = run_config3(f, n_global, lo, hi, info_fn=lambda g: g.sync())
+            for fld, v in fields.items():
+                rec[f"sha/{fld}"] = np.array(digest(v))
+            rec["sha/anc"] = np.array(digest(anc.astype(np.uint32)))
+            rec["best"] = best
+            rec["rng"] = rng
+            rec["range"] = np.array([lo, hi])
+        else:
+            rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.sync())
         f.close()
     if comm.error is not None:
         raise comm.error

@@ -34,6 +34,7 @@ class ContactModelS(C.Structure):
         ("shape_s2", C.c_double),
         ("nlow", C.c_uint32),
         ("low", (C.c_double * 3) * A.MAX_CONTACTS),
+        ("literal", C.c_int32), ("pad_literal", C.c_int32),
     ]
 
 
@@ -60,6 +61,8 @@ def lib():
     L.or_create.argtypes = [C.POINTER(A.Config), C.c_int]
     L.or_destroy.argtypes = [vp]
     L.or_set_threads.argtypes = [vp, C.c_int]
+    L.or_set_literal.argtypes = [vp, C.c_int]
+    L.or_set_debug.argtypes = [vp, C.c_int]
     L.or_set_map.argtypes = [vp, C.POINTER(A.MlsGrid)]
     L.or_init_gaussian.argtypes = [vp, C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double, C.c_double]
     L.or_init_pose.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -138,6 +141,14 @@ class OracleFilter:
     def set_threads(self, threads):
         """OpenMP threads of the per-particle loops (results identical for any count)."""
         self.L.or_set_threads(self.h, int(threads))
+
+    def set_literal(self, on=True):
+        """the reference's literal arithmetic instead of the build's contract (or_set_literal)"""
+        self.L.or_set_literal(self.h, int(bool(on)))
+
+    def set_debug(self, on=True):
+        """capture the per-particle contact-model outputs of every update (or_get_debug)"""
+        self.L.or_set_debug(self.h, int(bool(on)))
 
     def set_comm(self, comm, n_global):
         """Sharded mode over a host-memory eslam_comm (slam-eslam_amd/eslam_dist.TorchComm)."""
@@ -248,8 +259,9 @@ class OracleFilter:
         cp = (CPoint * (n * A.MAX_CONTACTS))()
         zd = np.zeros(n)
         zv = np.zeros(n)
-        self.L.or_get_debug(self.h, ncp.ctypes.data_as(C.POINTER(C.c_uint32)), cp,
-                            zd.ctypes.data_as(C.POINTER(C.c_double)), zv.ctypes.data_as(C.POINTER(C.c_double)))
+        rc = self.L.or_get_debug(self.h, ncp.ctypes.data_as(C.POINTER(C.c_uint32)), cp,
+                                 zd.ctypes.data_as(C.POINTER(C.c_double)), zv.ctypes.data_as(C.POINTER(C.c_double)))
+        assert rc == 0, "debug capture is off (set_debug)"
         return ncp, cp, zd, zv
 
 

@@ -1,5 +1,6 @@
 """Shared helpers for the GPU-vs-oracle parity tests (test infrastructure)."""
 import math
+import os
 import struct
 
 import numpy as np
@@ -48,12 +49,13 @@ def info_tuple(i):
 
 
 def run_pair(cfg, grid, stream, n, init=None, gpu_factory=None, record=True, check_every=True,
-             mode="step", label=""):
+             mode="step", label="", oracle_threads=1):
     """Run the same inputs through the oracle (contract sums) and the GPU, comparing after
     every step.  Returns (gpu filter, oracle filter)."""
     if record:
         cfg.flags |= A.FLAG_RECORD_ANCESTORS
     orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    orc.set_threads(min(oracle_threads, os.cpu_count() or 1))
     gpu = gpu_factory(cfg)
     orc.set_map(grid)
     gpu.set_map(grid)
@@ -88,3 +90,24 @@ def run_pair(cfg, grid, stream, n, init=None, gpu_factory=None, record=True, che
                 if oi.resampled and record:
                     assert np.array_equal(gpu.ancestors(), orc.ancestors()), f"{label} step {k}: ancestors differ"
     return gpu, orc
+
+
+def check_resample_properties(anc, after, n):
+    """Size-independent properties of one stratified resample (src/ParticleFilter.hpp:72-108):
+    ancestors nondecreasing and in range; the copies of one ancestor identical in every field
+    (the gather copies, Q4: the weights are not reset); each ancestor a copied c_a times with
+    |c_a - N w_a| < 2, w_a being its normalised weight (which the copies carry)."""
+    anc = np.asarray(anc).astype(np.int64)
+    assert anc.shape == (n,)
+    assert anc[0] >= 0 and anc[-1] < n and np.all(np.diff(anc) >= 0)
+    first = np.r_[True, anc[1:] != anc[:-1]]
+    starts = np.nonzero(first)[0]
+    copies = np.diff(np.r_[starts, n])
+    group = np.cumsum(first) - 1
+    for f in FLOAT_FIELDS + BYTE_FIELDS:
+        v = getattr(after, f)
+        v = v.view(np.uint64) if v.dtype == np.float64 else v
+        assert np.array_equal(v, v[starts][group]), f"copies of one ancestor differ in {f}"
+    w = after.weight[starts]
+    assert np.all(np.abs(copies - n * w) < 2.0)
+    assert float(np.sum(w)) <= 1.0 + 1e-9

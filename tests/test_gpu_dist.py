@@ -4,6 +4,7 @@ card: gloo with host staging for 2 and 3 ranks, and RCCL on device buffers with 
 (the full exchange sequence -- statistics all_gather, totals, counts, all_to_all_v --
 runs through RCCL to itself), both through the torch.distributed callbacks and over the
 library's own RCCL communicator (eslam_gpu_set_comm_rccl)."""
+import numpy as np
 import pytest
 
 from test_dist_cpu import assert_same, launch, merge, single_oracle
@@ -43,3 +44,37 @@ def test_sharded_gpu_two_row_chunks(oracle, tmp_path, mem, world):
     want = single_oracle("forced", n_global)
     got = merge(launch("gpu", "forced", n_global, world, str(tmp_path), mem=mem, timeout=280))
     assert_same(got, want, f"gpu {mem} forced N={n_global} world={world}")
+
+
+@pytest.mark.timeout(1200)
+def test_config3_eight_ranks_equal_single_context(oracle, tmp_path):
+    """BASELINE configs[3]'s decomposition on one GPU: 16M particles as 8 ranks x 2M (gloo,
+    host staging; the ranks share the card), 3 steps of the bench workload with a forced
+    resample each.  Every rank's shard equals the same slice of ONE 16M-particle context bit
+    for bit (all fields, the last resample's ancestors as global indices), every rank reports
+    the single context's update info, best index and RNG state, and the single context's last
+    resample passes the stratified-resample properties (src/ParticleFilter.hpp:85-108)."""
+    import eslam_abi as A
+    import eslam_amd
+    from dist_scenarios import CONFIG3_STEPS, FIELDS, digest, run_config3, scenario_config
+    from parity_util import check_resample_properties
+    n_global, world = 16 * 1024 * 1024, 8
+    parts = launch("gpu", "config3", n_global, world, str(tmp_path), mem="host", timeout=900)
+    f = eslam_amd.GpuFilter(scenario_config("config3", n_global))
+    rec, fields, anc, best, rng = run_config3(f, n_global, 0, n_global, info_fn=lambda g: g.sync())
+    bounds = A.shard_bounds(n_global, world)
+    for r, p in enumerate(parts):
+        lo, hi = bounds[r], bounds[r + 1]
+        assert tuple(p["range"]) == (lo, hi)
+        for fld in FIELDS:
+            assert str(p[f"sha/{fld}"]) == digest(fields[fld][lo:hi]), f"rank {r}: {fld} differs"
+        assert str(p["sha/anc"]) == digest(anc[lo:hi].astype(np.uint32)), f"rank {r}: ancestors differ"
+        for k in range(CONFIG3_STEPS):
+            assert np.array_equal(p[f"s{k}/info"].view(np.uint64), rec[f"s{k}/info"].view(np.uint64)), (r, k)
+        assert int(p["best"][0]) == int(best[0]) and int(p["rng"][0]) == int(rng[0])
+    assert rec[f"s{CONFIG3_STEPS - 1}/info"][6] == 1.0        # resampled
+    after = A.ParticleArrays(n_global)
+    for fld in FIELDS:
+        getattr(after, fld)[:] = fields[fld]
+    check_resample_properties(anc, after, n_global)
+    f.close()

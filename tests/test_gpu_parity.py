@@ -239,3 +239,75 @@ def test_resample_concentrated_weights(gpu_mod, profile):
     gpu.sync()
     assert np.array_equal(gpu.ancestors(), orc.ancestors())
     assert_bit_identical(gpu.download(), orc.download(), "resample " + profile)
+
+
+def test_resample_window_bounds_low_half_bit31(gpu_mod):
+    """K3b keeps each wave's cumulative-sum range [wlo, whi] in SGPRs (readfirstlane of the two
+    32-bit halves).  A build once widened the low half with sign extension, which turned every
+    bound whose low half has bit 31 set into 0xffffffff in the high word and faulted the GPU
+    (DESIGN.md 4).  Here every wave boundary of the only tile has exactly that low half:
+    weights 1.0 except w[0] = 1 + 2^-17, so at the resample's fixed-point shift of 48 (sum 2048:
+    61 - (12 + 1)) the prefix at 512 k is (512 k) 2^48 + 2^31.  Ancestors bit-exact vs the oracle
+    (src/ParticleFilter.hpp:85-108)."""
+    n = 2048
+    pa = A.ParticleArrays(n)
+    pa.x[:] = np.arange(n) * 1e-3
+    pa.zpos[:] = 0.18
+    pa.zsigma[:] = 0.2
+    pa.weight[:] = 1.0
+    pa.weight[0] = 1.0 + 2.0 ** -17
+    shift = 61 - (12 + 1)
+    for k in (1, 2, 3):
+        fx = (512 * k) * 2 ** shift + 2 ** 31        # exact prefix at the wave boundary
+        assert (fx & 0xffffffff) >> 31 == 1 and fx >> 32 != 0
+    cfg = A.default_config()
+    cfg.flags |= A.FLAG_RECORD_ANCESTORS
+    orc = O.OracleFilter(cfg)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc.upload(pa)
+    gpu.upload(pa)
+    gpu.resample()
+    orc.resample()
+    gpu.sync()
+    anc = gpu.ancestors()
+    assert np.array_equal(anc, orc.ancestors())
+    assert_bit_identical(gpu.download(), orc.download(), "bit31 bounds")
+
+
+def test_zero_measurement_variance_stops_the_update(gpu_mod, oracle):
+    """measurementError = 0 and zSigma = 0 make measVar = 0: evaluatePose throws
+    (src/ContactModel.cpp:122-123) from inside updateWeights' particle loop.  The step reports
+    ESLAM_ERR_ZERO_MEAS_VAR from the call itself; phase A has run on every particle, phase B,
+    normalizeWeights and resample have not, and the update gate pose is not advanced
+    (src/EmbodiedSlamFilter.cpp:361-362) -- so the gate fires again on the next step.  Natural
+    gate thresholds; the oracle returns the same code from or_step.  Bit-exact after every step."""
+    import ctypes as C
+    n = 1000
+    grid = S.flat_map(cells=200)
+    cfg = A.default_config()
+    cfg.particle_count = n
+    cfg.measurement_error = 0.0
+    cfg.flags |= A.FLAG_RECORD_ANCESTORS
+    stream = S.step_stream(14)
+    for st in stream:
+        st.position_error_zz = 0.0                  # project keeps zSigma = 0
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 0.0)
+    errors = 0
+    for k, st in enumerate(stream):
+        u = C.c_int(0)
+        orc_rc = orc.L.or_step(orc.h, C.byref(st), C.byref(u))
+        try:
+            gpu.step(st)
+            gpu_rc = 0
+        except gpu_mod.EslamError as e:
+            gpu_rc = e.code
+        assert gpu_rc == orc_rc, (k, gpu_rc, orc_rc)
+        errors += gpu_rc == A.ERR_ZERO_MEAS_VAR
+        gpu.sync()
+        assert_bit_identical(gpu.download(), orc.download(), f"zero-var step {k}")
+        assert info_tuple(gpu.sync()) == info_tuple(orc.info()), k
+    assert errors >= 2                              # the gate fired again after the first throw
