@@ -188,7 +188,12 @@ int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n);
 /* ---- the hot path ----------------------------------------------------------------------- */
 /* EmbodiedSlamFilter::update(body2odometry, bs, ltc): project, then the measurement update
  * when UpdateThreshold::test(udPose^-1 * body2odometry) (angle/distance swapped, Q6) or
- * ltc_count > 0.  *updated receives the bool.  Asynchronous on the context stream.         */
+ * ltc_count > 0.  *updated receives the bool.  Asynchronous on the context stream.
+ * A zero measurement variance (measurementError = 0 and zSigma = 0; the throw of
+ * src/ContactModel.cpp:122-123) returns ESLAM_ERR_ZERO_MEAS_VAR from this call: phase A has
+ * run (such particles count as rejected with no contact points), phase B, normalisation and
+ * the resample have not, and the update gate pose is not advanced.  Deviation: the reference
+ * aborts its particle loop at the first such particle, leaving the later ones projected only. */
 int eslam_gpu_step(eslam_ctx* ctx, const eslam_step_input* in, int* updated);
 /* PoseEstimator::project(state, orientation)                                              */
 int eslam_gpu_project(eslam_ctx* ctx, const eslam_step_input* in);

@@ -310,8 +310,8 @@ static int ratio_surely_significant(double z, double zvar, double corr)
 /* ContactModel::evaluatePose  src/ContactModel.cpp:117-224 (group quirk Q7 kept) */
 int or_cm_evaluate_pose(or_contact_model* cm, const double T[12], double meas_var, or_map_fn map, void* user)
 {
-    if (meas_var == 0) return -1;
     cm->ncp = 0;
+    if (meas_var == 0) return -1;       /* the throw of src/ContactModel.cpp:122-123 */
     or_cpoint p = {{0, 0, 0}, INFINITY, INFINITY, 1.0};
     int valid = 0, group_valid = 1;
     const double contact_threshold = 0.2;

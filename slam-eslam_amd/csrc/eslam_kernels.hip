@@ -748,8 +748,12 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             PROF(4);
             const double r22 = (1.0 - co) + co;
             const double meas_var = zs * zs + kd(kl2(KOFF(p.me2)), 0);
-            if (meas_var == 0) err = 1;
-            const CMResult r = evaluate_pose<MAXP, BATCH>(win, co, s, r22, x, y, z, meas_var PROF_ARG);
+            CMResult r = evaluate_pose<MAXP, BATCH>(win, co, s, r22, x, y, z, meas_var PROF_ARG);
+            if (meas_var == 0) {            // evaluatePose throws (src/ContactModel.cpp:122): no contact points
+                err = 1;
+                r.accepted = false;
+                r.ncp = 0;
+            }
             PROF(8);
             uint32_t floating;
             double sw = 0.0;

@@ -15,8 +15,8 @@ run() {  # run <name> <timeout> <cmd...>; exit codes 0/1 (test failures) continu
 rocm-smi --showproductname > gpurun_out/gpu.txt 2>&1; nproc >> gpurun_out/gpu.txt; lscpu | grep "Model name" >> gpurun_out/gpu.txt
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-    testsall) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    testsall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchsharded) run bench_sharded 600 python bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline ;;
