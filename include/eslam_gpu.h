@@ -308,7 +308,8 @@ int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable);
 int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t);
 /* evaluate the deterministic math on the device for n inputs (tests/test_gpu_math.py):
  * fn: 0 exp, 1 log, 2 sin, 3 cos, 4 erfc, 5 sqrt, 6 div(x, y), 7 pdf/cdf ratio(x, y),
- *     8 pow(x, y), 9 fx61(x) as bits, 13 sin(2 pi x), 14 cos(2 pi x) (Box-Muller angle)      */
+ *     8 pow(x, y), 9 fx61(x) as bits, 13 sin(2 pi x), 14 cos(2 pi x) (Box-Muller angle),
+ *     20..25: the butterflies' lane exchange, out[i] = x[i ^ 2^(fn - 20)] (n a multiple of 256) */
 int eslam_gpu_selftest_math(int device, int fn, const double* x, const double* y, double* out, uint64_t n);
 /* the Box-Muller radius sqrt(-2 log u) with the range-restricted dm_log_pos / dm_sqrt_pos
  * against the general dm_log / dm_sqrt, on the device, for all 2^32 uniform words: the

@@ -34,21 +34,63 @@ namespace eslam_dev {
 // ---------------------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------------------
+// lane i receives lane i ^ O's value without the LDS crossbar (ds_bpermute: ~100+ cycles of
+// latency per step).  O = 1, 2: DPP quad_perm; O = 4, 8: DPP row_shl / row_shr, each writing
+// only the banks (4-lane groups of a row) whose partner lies in that direction; O = 16, 32:
+// gfx950's v_permlane16_swap / v_permlane32_swap (odd rows <-> even rows, upper half <->
+// lower half) with both operands the value, then a per-lane pick of the swapped copy.
+template <int O> __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t v)
+{
+    static_assert(O == 1 || O == 2 || O == 4 || O == 8 || O == 16 || O == 32, "xor distance");
+    if constexpr (O == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);   // r[0]: [lo, lo], r[1]: [hi, hi]
+        return (threadIdx.x & 32u) ? r[0] : r[1];
+    } else if constexpr (O == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);   // r[0]: even rows, r[1]: odd rows
+        return (threadIdx.x & 16u) ? r[0] : r[1];
+    } else if constexpr (O == 8) {
+        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xf, 0x3, false);     // row_shl:8, banks 0-1
+        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
+    } else if constexpr (O == 4) {
+        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xf, 0x5, false);     // row_shl:4, banks 0, 2
+        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x114, 0xf, 0xa, false);  // row_shr:4, banks 1, 3
+    } else if constexpr (O == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    } else {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    }
+}
+
+template <int O> __device__ __forceinline__ uint64_t xor_lane_u64(uint64_t v)
+{
+    return (uint64_t)xor_lane_u32<O>((uint32_t)v) | ((uint64_t)xor_lane_u32<O>((uint32_t)(v >> 32)) << 32);
+}
+template <int O> __device__ __forceinline__ double xor_lane(double v) { return dm_from_bits(xor_lane_u64<O>(dm_bits(v))); }
+template <int O> __device__ __forceinline__ float xor_lane(float v) { return __uint_as_float(xor_lane_u32<O>(__float_as_uint(v))); }
+template <int O> __device__ __forceinline__ uint32_t xor_lane(uint32_t v) { return xor_lane_u32<O>(v); }
+template <int O> __device__ __forceinline__ uint64_t xor_lane(uint64_t v) { return xor_lane_u64<O>(v); }
+
+// xor butterfly over the 64 lanes, distances 32, 16, ..., 1 (the sum contract's chunk tree:
+// every stage adds the same pair in both lanes, so all lanes end with the same bits)
+template <class T, class Op> __device__ __forceinline__ T wave_butterfly(T v, Op op)
+{
+    v = op(v, xor_lane<32>(v));
+    v = op(v, xor_lane<16>(v));
+    v = op(v, xor_lane<8>(v));
+    v = op(v, xor_lane<4>(v));
+    v = op(v, xor_lane<2>(v));
+    v = op(v, xor_lane<1>(v));
+    return v;
+}
+
 __device__ __forceinline__ double wave_sum_butterfly(double v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
-    return v;
+    return wave_butterfly(v, [](double a, double b) { return a + b; });
 }
 
 __device__ __forceinline__ double wave_max_butterfly(double v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        double t = __shfl_xor(v, o, 64);
-        v = (v < t) ? t : v;
-    }
-    return v;
+    return wave_butterfly(v, [](double a, double b) { return (a < b) ? b : a; });
 }
 
 // inclusive max-scan over the 64 lanes with DPP (VALU lane moves, no LDS round trips):
@@ -68,9 +110,12 @@ __device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t m)
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return wave_butterfly(v, [](uint32_t a, uint32_t b) { return a + b; });
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+    return wave_butterfly(v, [](uint64_t a, uint64_t b) { return a + b; });
 }
 
 __device__ __forceinline__ uint64_t atomic_load_agent(const uint64_t* p)
@@ -861,10 +906,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     // bounding box of the cloud for the next step's LDS window (maxima, any order)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        float v = bb[q];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o, 64));
-        bb[q] = v;
+        bb[q] = wave_butterfly(bb[q], [](float a, float b) { return __builtin_fmaxf(a, b); });
     }
     Shard* shb = a.shards + (blockIdx.x % kNShard);
     if (lane == 0 && bb[1] > -INFINITY) {
@@ -1328,7 +1370,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     }
     if (!resample) return;
 
-    for (int o = 32; o >= 1; o >>= 1) fx_sum += __shfl_xor(fx_sum, o, 64);
+    fx_sum = wave_sum_u64(fx_sum);
     if (lane == 0) s_wtot[wave] = fx_sum;
     __syncthreads();
     if (tid == 0) {
@@ -1344,7 +1386,7 @@ __device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ ti
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint64_t acc = 0;
     for (uint32_t k = tid; k < count; k += kBlock) acc += tile_sum[k];
-    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    acc = wave_sum_u64(acc);
     if (lane == 0) s_wtot[wave] = acc;
     __syncthreads();
     uint64_t t = 0;
@@ -1847,6 +1889,21 @@ __global__ void __launch_bounds__(kBlock) k_tree_level(const double* __restrict_
 __global__ void k_selftest_math(int fn, const double* x, const double* y, double* out, uint64_t n)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (fn >= 20 && fn <= 25) {
+        // lane exchanges of the butterflies: x[i ^ 2^(fn - 20)] (n a multiple of the block)
+        const double v = i < n ? x[i] : 0.0;
+        double r = 0.0;
+        switch (fn) {
+        case 20: r = xor_lane<1>(v); break;
+        case 21: r = xor_lane<2>(v); break;
+        case 22: r = xor_lane<4>(v); break;
+        case 23: r = xor_lane<8>(v); break;
+        case 24: r = xor_lane<16>(v); break;
+        default: r = xor_lane<32>(v); break;
+        }
+        if (i < n) out[i] = r;
+        return;
+    }
     if (i >= n) return;
     double s, c, r = 0;
     switch (fn) {

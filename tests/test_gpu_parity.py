@@ -58,6 +58,17 @@ def test_box_muller_radius_all_words(gpu_mod):
     assert bad.value == 0
 
 
+def test_lane_exchange(gpu_mod):
+    """The DPP / permlane lane exchanges behind every wave butterfly (the sum contract's chunk
+    tree): lane i receives exactly lane i ^ 2^k's 64-bit value, k = 0..5."""
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal(1024)
+    idx = np.arange(x.size)
+    for k in range(6):
+        got = gpu_mod.selftest_math(20 + k, x)
+        assert np.array_equal(got.view(np.uint64), x[idx ^ (1 << k)].view(np.uint64)), f"xor {1 << k}"
+
+
 def test_gpu_div_and_ratio(gpu_mod, oracle):
     rng = np.random.default_rng(7)
     x = rng.normal(size=20000) * 10.0 ** rng.uniform(-5, 5, 20000)
