@@ -11,6 +11,7 @@
 #include <dlfcn.h>
 
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -505,7 +506,7 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
         for (int j = 0; j < 7; ++j) { *f[j] = (double*)p; p += al(cap * 8); }
         s.flags = (uint8_t*)p;
     }
-    const uint64_t ntiles = (cap + kScanTile - 1) / kScanTile;
+    const uint64_t ntiles = (cap + 2 * kBlock - 1) / (2 * kBlock);      // the smallest scan tile (scan_items)
     HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
@@ -1167,7 +1168,24 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
     p.J = dm_chunk_rows(ctx->n_global);
 }
 
-static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normalize)
+// particles per thread of K3a/K3b on one GPU: small filters take 512-particle tiles so the
+// two scan kernels still spread over every CU (256k particles: 512 blocks instead of 128);
+// ESLAM_SCAN_ITEMS (2, 4, 8) overrides, for measurements.  Exact integer tile totals: the
+// tile size never changes a result.
+static uint32_t scan_items(uint64_t n)
+{
+    static const int forced = [] {
+        const char* e = getenv("ESLAM_SCAN_ITEMS");
+        const int v = e ? atoi(e) : 0;
+        return (v == 2 || v == 4 || v == kScanItems) ? v : 0;
+    }();
+    if (forced) return (uint32_t)forced;
+    // measured (tools/ab_items.sh, bench step at 256k / 1M / 4M / 16M): 2 items +19 % at
+    // 256k, 2 or 4 items +4 % at 1M, 8 items best from 4M on (fewer tiles_before re-sums)
+    return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)kScanItems);
+}
+
+static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normalize, bool multi)
 {
     ScanParams sp;
     memset(&sp, 0, sizeof(sp));
@@ -1176,7 +1194,9 @@ static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normali
     sp.n_global = ctx->n_global;
     sp.phase_b = phase_b;
     sp.normalize = normalize;
-    sp.ntiles = (uint32_t)((ctx->n + kScanTile - 1) / kScanTile);
+    sp.items = multi ? (uint32_t)kScanItems : scan_items(ctx->n);
+    const uint64_t tile = (uint64_t)kBlock * sp.items;
+    sp.ntiles = (uint32_t)((ctx->n + tile - 1) / tile);
     return sp;
 }
 
@@ -1216,7 +1236,7 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     HIPCHK(ctx, eslam_launch_finalize(ctx->recs, G * kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     if (mode == FIN_SUM) return ESLAM_OK;
-    ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
+    ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, true);
     sp.multi = 1;
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->mg + mg::kTotal,
                                             ctx->stream));
@@ -1299,7 +1319,7 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     const FinParams fp = fin_params(ctx, mode);
     HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
-    const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE);
+    const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, false);
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, nullptr, ctx->stream));
     HIPCHK(ctx, eslam_launch_segments(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->marks, ctx->tile_first,
                                       ctx->jump, ctx->stream));

@@ -180,6 +180,8 @@ struct ScanParams {
     uint32_t normalize;                  // divide by S
     uint32_t ntiles;
     uint32_t multi;                      // multi-GPU: tile prefixes + rank total, no marks
+    uint32_t items;                      // particles per thread of K3a/K3b: tile = kBlock * items
+                                         // (2, 4 or kScanItems; sharded: kScanItems)
 };
 
 constexpr int kMaxRanks = 16;

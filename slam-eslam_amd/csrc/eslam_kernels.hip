@@ -215,6 +215,17 @@ __device__ unsigned long long k1_prof[32];      // [0,16): K1 regions, [16,32): 
 #define PROF_FLUSH_AT(base) do {} while (0)
 #endif
 
+// ESLAM_K1_TL (diagnostic builds only): per-wave timeline of K1 in s_memrealtime ticks
+// (100 MHz): entry, window staged, exit (few stamps: each costs registers, and at 129
+// VGPRs the kernel drops to 3 waves per SIMD)
+#ifdef ESLAM_K1_TL
+__device__ unsigned long long k1_tl[8192 * 8];
+#define TL(k) do { const uint32_t gw_ = blockIdx.x * kWaves + (threadIdx.x >> 6); \
+    if ((threadIdx.x & 63u) == 0 && gw_ < 8192u) k1_tl[gw_ * 8u + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TL(k) do {} while (0)
+#endif
+
 // the state pointers of buffer s[b] (offset KOFF(s[b]))
 struct StatePtrs {
     gmem<double> *x, *y, *th, *z, *zs, *w, *mprob;
@@ -654,6 +665,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
     // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
+    TL(0);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t n = a.p.n;
     const uint32_t J = a.p.J;
@@ -685,6 +697,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     if (WEIGHT) { __syncthreads(); win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds); }
 #endif
 
+    TL(1);
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
@@ -971,6 +984,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     }
     PROF(12);
     PROF_FLUSH();
+    TL(5);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1288,12 +1302,13 @@ constexpr int kStageV = kScanTile + kScanTile / kSkew;
 __device__ __forceinline__ int skew(int k) { return k + k / kSkew; }
 
 // this thread's 8 consecutive values (blocked) -> fixed-point inclusive running sums
-__device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uint64_t (&c)[kScanItems])
+template <int ITEMS>
+__device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uint64_t (&c)[ITEMS])
 {
     uint64_t run = 0;
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        run += fx_shift(s_v[skew((int)threadIdx.x * kScanItems + r)], shift);
+    for (int r = 0; r < ITEMS; ++r) {
+        run += fx_shift(s_v[skew((int)threadIdx.x * ITEMS + r)], shift);
         c[r] = run;
     }
     return run;
@@ -1314,12 +1329,13 @@ union K3bLds {
 // reads), so only the segment starts are stored: direct stores measured ~1 µs faster per
 // step than staging the tile's output range in LDS and writing it densely.
 // seg_lo/seg_hi: this thread's segments (relative; empty when equal), val: their values.
+template <int ITEMS>
 __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
-                                            const uint64_t (&seg_lo)[kScanItems], const uint64_t (&seg_hi)[kScanItems],
-                                            const uint32_t (&val)[kScanItems])
+                                            const uint64_t (&seg_lo)[ITEMS], const uint64_t (&seg_hi)[ITEMS],
+                                            const uint32_t (&val)[ITEMS])
 {
 #pragma unroll
-    for (int q = 0; q < kScanItems; ++q) {
+    for (int q = 0; q < ITEMS; ++q) {
         const uint64_t lo = seg_lo[q], hi = seg_hi[q];
         if (hi <= lo) continue;
         marks[lo] = val[q];
@@ -1330,6 +1346,7 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
 // K3a: phase B + normalisation (striped, coalesced) and, when resampling, the tile's exact
 // fixed-point weight total.  K3b sums the totals of the tiles before its own (exact
 // integers, any order): no cross-tile waiting inside a kernel.
+template <int ITEMS>
 __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                            uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total)
 {
@@ -1339,7 +1356,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     const bool resample = ctl->resample != 0;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
-    const uint64_t t0 = (uint64_t)tile * kScanTile;
+    const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
     const double S = ctl->S;
     const bool uniform = ctl->uniform != 0;
     const double inv_n = ctl->inv_n;
@@ -1350,7 +1367,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
 
     uint64_t fx_sum = 0;
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
         if (i < sp.n) {
             double v = st.w[i];
@@ -1466,6 +1483,7 @@ __device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, 
 }
 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
+template <int ITEMS>
 __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                      const uint64_t* __restrict__ tile_sum, uint32_t* __restrict__ marks,
                                                      uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt)
@@ -1477,9 +1495,9 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const DevState st = ctl->base ? s1 : s0;
-    const uint64_t t0 = (uint64_t)tile * kScanTile;
+    const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int k = r * kBlock + (int)tid;
         const uint64_t i = t0 + (uint64_t)k;
         s_u.v[skew(k)] = i < sp.n ? st.w[i] : 0.0;
@@ -1487,7 +1505,7 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     __syncthreads();
     PROF(0);
     const int shift = ctl->scan_shift;
-    uint64_t c[kScanItems];
+    uint64_t c[ITEMS];
     const uint64_t run = blocked_fx(s_u.v, shift, c);
     PROF(1);
     const uint64_t tb = tiles_before(tile_sum, tile, s_wtot);
@@ -1498,7 +1516,7 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     const uint64_t N = sp.n_global;
     const uint32_t xs = ctl->minstd_start;
     const double dN = (double)N, inv_N = 1.0 / dN;
-    const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
+    const uint64_t i0 = t0 + (uint64_t)tid * ITEMS;
     // the wave's cumulative range [wlo, whi]: every count it needs reads only draws in
     // [dlo, dhi) (the windows k* - 1 .. k* + 1 of wlo and whi, clamped to [0, N))
     // wave-uniform by construction: moved to SGPRs, so the window bounds, the loop and the
@@ -1513,15 +1531,15 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     const uint64_t ks_lo = kstar_of(wlo, N, shift), ks_hi = kstar_of(whi, N, shift);
     const uint64_t dlo = ks_lo >= 1 ? ks_lo - 1 : 0;
     const uint64_t dhi = ks_hi + 2 < N ? ks_hi + 2 : N;
-    uint64_t hi_r[kScanItems];
+    uint64_t hi_r[ITEMS];
     uint64_t lo;
     if (dlo >= dhi || dhi - dlo <= (uint64_t)kWaveChunks * kWaveDraws) {
         // draws in LDS, kWaveDraws at a time (one chunk unless the wave holds heavy weights);
-        // le[r] bit d: draw k0_r + d of target r (r = kScanItems: wlo) is <= its target
+        // le[r] bit d: draw k0_r + d of target r (r = ITEMS: wlo) is <= its target
         uint64_t* sT = s_u.T[wave];
-        uint32_t win[kScanItems + 1];
+        uint32_t win[ITEMS + 1];
 #pragma unroll
-        for (int r = 0; r <= kScanItems; ++r) win[r] = window_of(r < kScanItems ? base + c[r] : wlo, N, shift, dlo);
+        for (int r = 0; r <= ITEMS; ++r) win[r] = window_of(r < ITEMS ? base + c[r] : wlo, N, shift, dlo);
         const uint32_t a64 = jt[64], a_lane = jt[lane];            // A^64, A^lane
         for (uint64_t q0 = dlo; q0 < dhi; q0 += kWaveDraws) {
             const uint64_t q1 = dhi - q0 < (uint64_t)kWaveDraws ? dhi : q0 + kWaveDraws;
@@ -1537,31 +1555,31 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-            for (int r = 0; r <= kScanItems; ++r)
-                win[r] = draws_le_chunk(win[r], r < kScanItems ? base + c[r] : wlo, sT, dlo, q0, q1);
+            for (int r = 0; r <= ITEMS; ++r)
+                win[r] = draws_le_chunk(win[r], r < ITEMS ? base + c[r] : wlo, sT, dlo, q0, q1);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
 #pragma unroll
-        for (int r = 0; r < kScanItems; ++r) hi_r[r] = count_from_window(win[r], dlo, N);
-        const uint64_t K0 = count_from_window(win[kScanItems], dlo, N);
-        const uint64_t prev = __shfl_up(hi_r[kScanItems - 1], 1, 64);
+        for (int r = 0; r < ITEMS; ++r) hi_r[r] = count_from_window(win[r], dlo, N);
+        const uint64_t K0 = count_from_window(win[ITEMS], dlo, N);
+        const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
         lo = lane == 0 ? K0 : prev;
     } else {
         // heavy weights: each target's window evaluated directly (jump + at most three draws)
 #pragma unroll
-        for (int r = 0; r < kScanItems; ++r) hi_r[r] = count_draws_le(base + c[r], N, xs, shift, jt);
+        for (int r = 0; r < ITEMS; ++r) hi_r[r] = count_draws_le(base + c[r], N, xs, shift, jt);
         const uint64_t K0 = count_draws_le(wlo, N, xs, shift, jt);
-        const uint64_t prev = __shfl_up(hi_r[kScanItems - 1], 1, 64);
+        const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
         lo = lane == 0 ? K0 : prev;
     }
     PROF(4);
     if (i0 == 0) lo = 0;
-    uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
-    uint32_t val[kScanItems];
+    uint64_t seg_lo[ITEMS], seg_hi[ITEMS];
+    uint32_t val[ITEMS];
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = i0 + r;
         seg_lo[r] = seg_hi[r] = 0;
         val[r] = (uint32_t)(i + 1);
@@ -1623,7 +1641,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     __syncthreads();
     const int shift = ctl->scan_shift;
     uint64_t c[kScanItems];
-    const uint64_t run = blocked_fx(s_v, shift, c);
+    const uint64_t run = blocked_fx<kScanItems>(s_v, shift, c);
     const uint64_t tbase = tiles_before(tile_sum, tile, s_wtot) + block_excl(run, s_wtot);
     uint64_t off, O0, O1;
     plan_bounds(pp, ctl, totals, jt, off, O0, O1);
@@ -2007,7 +2025,14 @@ extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, cons
                                                   uint64_t* total, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_normalize_scan, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total);
+    switch (sp->items) {
+    case 2: hipLaunchKernelGGL(k_normalize_scan<2>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total); break;
+    case 4: hipLaunchKernelGGL(k_normalize_scan<4>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total); break;
+    case kScanItems:
+        hipLaunchKernelGGL(k_normalize_scan<kScanItems>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total);
+        break;
+    default: return hipErrorInvalidValue;
+    }
     if (total) hipLaunchKernelGGL(k_slice_total, dim3(1), dim3(kBlock), 0, stream, ctl, tile_sum, sp->ntiles, total);
     return hipGetLastError();
 }
@@ -2016,8 +2041,15 @@ extern "C" hipError_t eslam_launch_segments(DevState s0, DevState s1, const Scan
                                             uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_segments, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_prefix, marks, tile_first,
-                       jt);
+#define ESLAM_SEG(I) hipLaunchKernelGGL(k_segments<I>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_prefix, \
+                                        marks, tile_first, jt)
+    switch (sp->items) {
+    case 2: ESLAM_SEG(2); break;
+    case 4: ESLAM_SEG(4); break;
+    case kScanItems: ESLAM_SEG(kScanItems); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef ESLAM_SEG
     return hipGetLastError();
 }
 
@@ -2041,6 +2073,7 @@ extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, cons
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
                                                   hipStream_t stream)
 {
+    if (sp->items != kScanItems) return hipErrorInvalidValue;       // the sharded scan uses full tiles
     if (sp->ntiles) hipLaunchKernelGGL(k_segments_multi, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl,
                                        tile_prefix, marks, tile_first, totals, jt, range, first_last);
     return hipGetLastError();
@@ -2131,6 +2164,18 @@ extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n
     return e;
 }
 
+// blocks per CU of the main K1 instantiation (diagnostics: tools/k1_timeline.py)
+extern "C" int eslam_debug_k1_occupancy(int* blocks_per_cu, int lds)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_project_weight<true, true, 4, true>, kBlock,
+                                                        lds < 0 ? kStatsLds + kWindowLds : lds) == hipSuccess ? 0 : -1;
+}
+#ifdef ESLAM_K1_TL
+extern "C" int eslam_debug_k1_tl(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(k1_tl), sizeof(unsigned long long) * 8192 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef ESLAM_K1_PROF
 // diagnostic builds: read and clear the K1 region clocks
 extern "C" int eslam_debug_k1_prof(unsigned long long* out)
