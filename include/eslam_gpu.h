@@ -85,6 +85,8 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_RECORD_ANCESTORS 0x1u   /* keep the last resample's ancestor indices     */
 #define ESLAM_FLAG_NO_MAP_LDS 0x2u         /* disable the LDS map window (global lookups)   */
 #define ESLAM_FLAG_NO_AUX_GATHER 0x4u      /* do not carry mprob/floating through resample  */
+#define ESLAM_FLAG_RECORD_CONTACTS 0x8u    /* keep every update's cpoints, meas_pos, meas_theta
+                                              (also on with log_debug); one GPU only          */
 
 void eslam_config_default(eslam_config* cfg);
 
@@ -183,6 +185,36 @@ int eslam_gpu_init_pose(eslam_ctx* ctx, const double position[3], const double o
 /* replace the particle set (getParticles() is a mutable reference in the reference)       */
 int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const eslam_particles* p);
 int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p);
+
+/* ---- PoseParticle records with the debug fields (getParticles() for logging / viz) ------ */
+/* ContactPoint  src/PoseParticle.hpp:20-43: one contact point evaluatePose pushed           */
+typedef struct eslam_cpoint {
+    double point[3];                       /* surface point: world x, y of the group's first
+                                              valid contact and the patch mean (:163-171)   */
+    double zdiff, zvar;                    /* ratio-weighted group averages                 */
+    double prob;                           /* 1 (the slip update never reaches it, Q8)      */
+} eslam_cpoint;
+
+/* PoseParticle  src/PoseParticle.hpp:52-86 as the viz reads it (viz/ParticleVisualization.cpp) */
+typedef struct eslam_particle_record {
+    double position[2];
+    double orientation, zpos, zsigma, mprob, weight;
+    double meas_pos[3];                    /* (x, y, zPos) at the last updateWeights          */
+    double meas_theta;                     /* orientation at the last updateWeights           */
+    uint64_t index;                        /* global particle index                          */
+    uint32_t n_cpoints;                    /* cpoints.size()                                 */
+    uint8_t floating;
+    uint8_t pad[3];
+} eslam_particle_record;
+
+/* Particles first, first + stride, ... (count of them) as records, gathered on the device
+ * (one copy of count records; a strided subsample keeps logging cheap at millions of
+ * particles).  With ESLAM_FLAG_RECORD_CONTACTS (or log_debug) the meas_* fields and up to
+ * max_cpoints contact points per particle (cpoints: count x max_cpoints, may be NULL) are
+ * those of the last update, carried through its resample like the reference's vectors;
+ * otherwise meas_* are 0 and n_cpoints = the count of the last update.                    */
+int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64_t stride, uint64_t count,
+                               eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints);
 int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n);
 
 /* ---- the hot path ----------------------------------------------------------------------- */

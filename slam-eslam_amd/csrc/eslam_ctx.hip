@@ -22,6 +22,12 @@
 
 using namespace eslam_dev;
 
+extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
+                                                   const DebugRec* d, hipStream_t stream);
+extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
+                                                uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
+                                                eslam_particle_record* out, eslam_cpoint* cps, uint32_t max_cp,
+                                                hipStream_t stream);
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
                                                   const GatherView* gv, hipStream_t stream);
@@ -217,6 +223,10 @@ struct eslam_ctx {
     uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total
     uint32_t* anc = nullptr;
     bool has_anc = false;
+    // logDebug records of the last update (ESLAM_FLAG_RECORD_CONTACTS / log_debug)
+    DebugRec dbg = {};
+    uint64_t dbg_cap = 0;
+    bool dbg_valid = false;
     // statistics and control
     Shard* shards = nullptr;
     Ctl* ctl = nullptr;
@@ -437,8 +447,28 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
     return ESLAM_OK;
 }
 
+// ancestors are kept when asked for, and always while contact records are (the records of
+// output i are those of its ancestor)
+static bool record_contacts(const eslam_ctx* ctx)
+{
+    return (ctx->cfg.flags & ESLAM_FLAG_RECORD_CONTACTS) || ctx->cfg.log_debug;
+}
+static bool keep_ancestors(const eslam_ctx* ctx)
+{
+    return (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) || record_contacts(ctx);
+}
+
+static void free_debug(eslam_ctx* ctx)
+{
+    (void)hipFree(ctx->dbg.meas); (void)hipFree(ctx->dbg.ncp); (void)hipFree(ctx->dbg.cp); (void)hipFree(ctx->dbg.resampled);
+    ctx->dbg = DebugRec{};
+    ctx->dbg_cap = 0;
+    ctx->dbg_valid = false;
+}
+
 static void free_particles(eslam_ctx* ctx)
 {
+    free_debug(ctx);
     (void)hipFree(ctx->state_mem); ctx->state_mem = nullptr;
     (void)hipFree(ctx->marks); ctx->marks = nullptr;
     (void)hipFree(ctx->tile_first); ctx->tile_first = nullptr;
@@ -511,7 +541,7 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
-    if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
+    if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     ctx->n = n;
     ctx->cap = cap;
     if (ctx->sharded) {
@@ -1074,6 +1104,38 @@ extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
     return ESLAM_OK;
 }
 
+extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64_t stride, uint64_t count,
+                                          eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints)
+{
+    if (!ctx || (!out && count)) return ESLAM_ERR_INVALID_ARG;
+    if (!count) return ESLAM_OK;
+    if (!stride) stride = 1;
+    if (first >= ctx->n || (count - 1) > (ctx->n - 1 - first) / stride)
+        return fail(ctx, ESLAM_ERR_INVALID_ARG, "download_records: range beyond the particles");
+    if (!cpoints) max_cpoints = 0;
+    int rc = materialize(ctx);                // the pending gather writes the ancestors too
+    if (rc) return rc;
+    const DebugRec none = {};
+    const DebugRec& d = ctx->dbg_valid ? ctx->dbg : none;
+    eslam_particle_record* d_out = nullptr;
+    eslam_cpoint* d_cp = nullptr;
+    HIPCHK(ctx, hipMalloc(&d_out, count * sizeof(eslam_particle_record)));
+    if (max_cpoints) {
+        hipError_t e = hipMalloc(&d_cp, count * max_cpoints * sizeof(eslam_cpoint));
+        if (e == hipSuccess) e = hipMemsetAsync(d_cp, 0, count * max_cpoints * sizeof(eslam_cpoint), ctx->stream);
+        if (e != hipSuccess) { (void)hipFree(d_out); (void)hipFree(d_cp); return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e)); }
+    }
+    hipError_t e = eslam_launch_pack_records(ctx->st[0], ctx->st[1], ctx->ctl, first, stride, count, ctx->gbase, ctx->anc, &d,
+                                             d_out, d_cp, max_cpoints, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, count * sizeof(eslam_particle_record), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && max_cpoints) e = hipMemcpy(cpoints, d_cp, count * max_cpoints * sizeof(eslam_cpoint), hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cp);
+    if (e != hipSuccess) return fail(ctx, ESLAM_ERR_HIP, (std::string("download_records: ") + hipGetErrorString(e)).c_str());
+    return ESLAM_OK;
+}
+
 // ---------------------------------------------------------------------------------------
 // the hot path
 // ---------------------------------------------------------------------------------------
@@ -1086,7 +1148,7 @@ static GatherView gather_view(eslam_ctx* ctx)
     gv.row_first = ctx->tile_first;
     gv.anc = ctx->anc;
     gv.recs = ctx->sharded ? (const Rec*)ctx->recvbuf : nullptr;
-    gv.record = (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ? 1u : 0u;
+    gv.record = keep_ancestors(ctx) ? 1u : 0u;
     gv.multi = ctx->sharded ? 1u : 0u;
     return gv;
 }
@@ -1309,7 +1371,7 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     // marks of the migrated outputs; the gather is fused into the next k_project_weight
     HIPCHK(ctx, eslam_launch_expand(ctx->recvbuf, nrecv, ctx->gbase, ctx->marks, ctx->tile_first, ctx->stream));
     if (timed) rec(ctx, 4);
-    if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ctx->has_anc = true;
+    if (keep_ancestors(ctx)) ctx->has_anc = true;
     return ESLAM_OK;
 }
 
@@ -1326,7 +1388,7 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     if (timed) rec(ctx, 3);
     // the gather itself is fused into the next k_project_weight (or materialize())
     if (timed) rec(ctx, 4);
-    if (ctx->cfg.flags & ESLAM_FLAG_RECORD_ANCESTORS) ctx->has_anc = true;
+    if (keep_ancestors(ctx)) ctx->has_anc = true;
     return ESLAM_OK;
 }
 
@@ -1417,17 +1479,35 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
         const uint64_t period = ctx->cfg.hash_period ? ctx->cfg.hash_period : 1;
         respawn = (ctx->hash_event++ % period) == 0;
     }
-    if (respawn) {
+    // logDebug records: the update's contact points are recorded on the projected state, so
+    // the project runs as its own launch first (bit-identical to the fused kernel)
+    const bool records = weight && record_contacts(ctx) && !ctx->sharded;
+    if (respawn || (records && project)) {
         const GatherView gv0 = gather_view(ctx);
         HIPCHK(ctx, eslam_launch_project_weight(1, 0, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
                                                 ctx->shards, &gv0, ctx->stream));
         HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
         ctx->proj_event++;
         if (gv0.record) ctx->has_anc = true;
-        const int rc = sample_from_hash(ctx, in, p);
-        if (rc) return rc;
+        if (respawn) {
+            const int rc = sample_from_hash(ctx, in, p);
+            if (rc) return rc;
+        }
         project = false;                      // done; the update below is weight-only
         if (!weight) return ESLAM_OK;
+    }
+    if (records) {
+        const uint32_t maxc = p.m ? p.m : 1u;
+        if (ctx->dbg_cap < ctx->n || ctx->dbg.maxc < maxc) {
+            free_debug(ctx);
+            HIPCHK(ctx, hipMalloc(&ctx->dbg.meas, ctx->cap * 32));
+            HIPCHK(ctx, hipMalloc(&ctx->dbg.ncp, ctx->cap));
+            HIPCHK(ctx, hipMalloc(&ctx->dbg.cp, ctx->cap * 48ull * maxc));
+            HIPCHK(ctx, hipMalloc(&ctx->dbg.resampled, 4));
+            ctx->dbg.maxc = maxc;
+            ctx->dbg_cap = ctx->cap;
+        }
+        HIPCHK(ctx, eslam_launch_contact_records(ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl, &ctx->dbg, ctx->stream));
     }
     rec(ctx, 0);
     const GatherView gv = gather_view(ctx);
@@ -1439,6 +1519,11 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     if (weight) {
         const int rc = run_update_tail(ctx, FIN_UPDATE, true);   // finalize commits the flip
         if (rc) return rc;
+        if (records) {
+            // the records describe this update; its resample decision maps outputs to them
+            HIPCHK(ctx, hipMemcpyAsync(ctx->dbg.resampled, &ctx->ctl->resample, 4, hipMemcpyDeviceToDevice, ctx->stream));
+            ctx->dbg_valid = true;
+        }
         // measVar = zSigma^2 + measurementError^2 is zero only when measurementError^2 is: in
         // that configuration the update is checked at once, so the error surfaces from this
         // call like the reference's throw (src/ContactModel.cpp:122-123) and the caller's
@@ -1564,6 +1649,7 @@ extern "C" int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective)
 extern "C" int eslam_gpu_resample(eslam_ctx* ctx)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    ctx->dbg_valid = false;                  // the records no longer follow the particles
     return standalone(ctx, FIN_RESAMPLE);
 }
 

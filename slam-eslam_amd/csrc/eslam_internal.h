@@ -158,6 +158,17 @@ struct K1Args {
     Shard* shards;
 };
 
+// logDebug records of the last update (k_contact_records), indexed by the particle's
+// position during that update: meas 4 doubles (x, y, zPos, theta), ncp, and maxc contact
+// points of 6 doubles (surface point xyz, zdiff, zvar, prob)
+struct DebugRec {
+    double* meas;
+    uint8_t* ncp;
+    double* cp;
+    uint32_t* resampled;                 // the update's resample decision (copied from Ctl)
+    uint32_t maxc;
+};
+
 struct FinParams {
     uint64_t n_global;
     uint64_t min_effective;

@@ -26,6 +26,7 @@
 // lanes, ballots as 64-bit masks.  All arithmetic goes through include/eslam_detmath.h and
 // the file is compiled with -ffp-contract=off, so results equal the CPU oracle bit for bit.
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include "eslam_internal.h"
 
@@ -985,6 +986,138 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     PROF(12);
     PROF_FLUSH();
     TL(5);
+}
+
+// ---------------------------------------------------------------------------------------
+// k_contact_records (Configuration::logDebug / ESLAM_FLAG_RECORD_CONTACTS): the debug fields
+// updateWeights stores in every PoseParticle (src/PoseEstimator.cpp:285-287, 322-325):
+// meas_pos, meas_theta and cpoints.  Runs on the projected state between a project-only and
+// a weight-only k_project_weight, so the weighting sees exactly the state these records
+// describe.  ContactModel::evaluatePose (src/ContactModel.cpp:117-224) evaluated in contact
+// order with the same arithmetic as evaluate_pose (the same pushes, bit for bit), recording
+// each pushed ContactPoint: the surface point of the group's first valid contact (world x,
+// y and the patch mean, :163-171), zdiff, zvar and prob = 1 (Q8).  One particle per thread,
+// map lookups through the global CSR (the same values as the LDS window).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_contact_records(K1Args a, DebugRec d)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if (threadIdx.x < 8) k1_win[threadIdx.x] = 0;          // no LDS window: get_patch reads k1_win
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.p.n) return;
+    const Ctl* ctl = a.ctl;
+    const DevState& st = (ctl->base ^ ctl->flip) ? a.s[1] : a.s[0];
+    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
+    Window win;
+    win.on = 0;
+    win.cells = reinterpret_cast<const WinCell*>(smem);
+    double s, co;
+    dm_sincos(th, &s, &co);
+    const double r22 = (1.0 - co) + co;
+    const double meas_var = zs * zs + a.p.me2;
+    d.meas[4 * i + 0] = x;
+    d.meas[4 * i + 1] = y;
+    d.meas[4 * i + 2] = z;
+    d.meas[4 * i + 3] = th;
+    uint32_t ncp = 0;
+    if (meas_var != 0) {
+        bool valid = false, group_valid = true;
+        double contact_ratio = 0, pzd = 0, pzv = 0, gx = 0, gy = 0, gm = 0;
+        const double corr = a.p.corr;
+        double* cp = d.cp + (uint64_t)6 * d.maxc * i;
+        auto push = [&](double px, double py, double pm, double zd, double zv) {
+            if (ncp < d.maxc) {
+                double* r = cp + 6 * ncp;
+                r[0] = px; r[1] = py; r[2] = pm; r[3] = zd; r[4] = zv; r[5] = 1.0;
+            }
+            ++ncp;
+        };
+        for (uint32_t k = 0; k < a.p.m; ++k) {
+            const ContactC& c = a.p.c[k];
+            const bool c_eval = (a.p.eval_mask >> k) & 1u, c_end = (a.p.end_mask >> k) & 1u;
+            const double wx = ((co * c.px + (-s) * c.py) + c.zp) + x;
+            const double wy = ((s * c.px + co * c.py) + c.zp) + y;
+            const double wz = ((c.zz + r22 * c.pz) + z) - a.p.radius;
+            if (group_valid && c_eval) {
+                double mean = 0.0, stdev = 0.0;
+                if (get_patch(win, wx, wy, wz, meas_var, mean, stdev)) {
+                    const double zdiff = wz - mean;
+                    const double zvar = stdev * stdev + meas_var;
+                    if (!valid && c_end && ratio_surely_significant(zdiff, zvar, corr)) {
+                        push(wx, wy, mean, zdiff, zvar);       // single-point group
+                        continue;
+                    }
+                    const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * corr);
+                    if (!valid) {
+                        pzd = zdiff * ratio; pzv = zvar * ratio; contact_ratio = ratio;
+                        gx = wx; gy = wy; gm = mean;
+                    } else {
+                        pzd += zdiff * ratio; pzv += zvar * ratio; contact_ratio += ratio;
+                    }
+                    valid = true;
+                } else {
+                    group_valid = false;
+                }
+            }
+            if (valid && c_end) {
+                if (group_valid && contact_ratio > 1e-9) {
+                    const double inv = 1.0 / contact_ratio;
+                    push(gx, gy, gm, pzd * inv, pzv * inv);
+                }
+                group_valid = true;
+                valid = false;
+                contact_ratio = 0;
+            }
+        }
+    }
+    d.ncp[i] = (uint8_t)(ncp < 255u ? ncp : 255u);
+}
+
+// eslam_gpu_download_records: particles first + k * stride as PoseParticle records with their
+// debug fields.  Particle i's records are those of the particle it descends from at the last
+// update's resample (anc, global indices) -- the reference copies cpoints with the particle.
+__global__ void __launch_bounds__(kBlock) k_pack_records(DevState s0, DevState s1, const Ctl* __restrict__ ctl, uint64_t first,
+                                                         uint64_t stride, uint64_t count, uint64_t gbase,
+                                                         const uint32_t* __restrict__ anc, DebugRec d,
+                                                         eslam_particle_record* __restrict__ out,
+                                                         eslam_cpoint* __restrict__ cps, uint32_t max_cp)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= count) return;
+    const uint64_t i = first + k * stride;
+    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    eslam_particle_record r;
+    r.position[0] = st.x[i];
+    r.position[1] = st.y[i];
+    r.orientation = st.th[i];
+    r.zpos = st.z[i];
+    r.zsigma = st.zs[i];
+    r.mprob = st.mprob[i];
+    r.weight = st.w[i];
+    const uint8_t fl = st.flags[i];
+    r.floating = fl >> 7;
+    r.index = i + gbase;
+    uint32_t n = 0;
+    if (d.ncp) {
+        const uint64_t src = *d.resampled ? (uint64_t)anc[i] - gbase : i;
+        for (int q = 0; q < 3; ++q) r.meas_pos[q] = d.meas[4 * src + q];
+        r.meas_theta = d.meas[4 * src + 3];
+        n = d.ncp[src];
+        const uint32_t kept = n < d.maxc ? n : d.maxc;
+        for (uint32_t q = 0; q < kept && q < max_cp; ++q) {
+            const double* c = d.cp + (uint64_t)6 * (d.maxc * src + q);
+            eslam_cpoint& o = cps[(uint64_t)max_cp * k + q];
+            o.point[0] = c[0]; o.point[1] = c[1]; o.point[2] = c[2];
+            o.zdiff = c[3]; o.zvar = c[4]; o.prob = c[5];
+        }
+    } else {
+        r.meas_pos[0] = r.meas_pos[1] = r.meas_pos[2] = 0.0;
+        r.meas_theta = 0.0;
+        n = fl & 0x7fu;
+    }
+    r.n_cpoints = n;
+    out[k] = r;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2001,6 +2134,33 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
         else ESLAM_LAUNCH(true, true, ESLAM_MAX_CONTACTS, false);
     }
 #undef ESLAM_LAUNCH
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
+                                                   const DebugRec* d, hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((p->n + kBlock - 1) / kBlock);
+    if (!blocks) return hipSuccess;
+    K1Args args;
+    memset(&args, 0, sizeof(args));
+    args.p = *p;
+    args.map = *map;
+    args.s[0] = s0;
+    args.s[1] = s1;
+    args.ctl = ctl;
+    hipLaunchKernelGGL(k_contact_records, dim3(blocks), dim3(kBlock), 16, stream, args, *d);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
+                                                uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d, eslam_particle_record* out, eslam_cpoint* cps,
+                                                uint32_t max_cp, hipStream_t stream)
+{
+    const uint32_t blocks = (uint32_t)((count + kBlock - 1) / kBlock);
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_records, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, ctl, first, stride, count, gbase, anc,
+                       *d, out, cps, max_cp);
     return hipGetLastError();
 }
 

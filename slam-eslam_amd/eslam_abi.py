@@ -21,6 +21,7 @@ ERR_OUT_OF_MEMORY = -9
 FLAG_RECORD_ANCESTORS = 0x1
 FLAG_NO_MAP_LDS = 0x2
 FLAG_NO_AUX_GATHER = 0x4
+FLAG_RECORD_CONTACTS = 0x8
 
 
 class Config(C.Structure):
@@ -105,6 +106,34 @@ class Particles(C.Structure):
         ("mprob", C.POINTER(C.c_double)),
         ("floating", C.POINTER(C.c_uint8)),
         ("n_contact_points", C.POINTER(C.c_uint8)),
+    ]
+
+
+class CPoint(C.Structure):
+    """eslam_cpoint: ContactPoint (src/PoseParticle.hpp:20-43)"""
+    _fields_ = [
+        ("point", C.c_double * 3),
+        ("zdiff", C.c_double),
+        ("zvar", C.c_double),
+        ("prob", C.c_double),
+    ]
+
+
+class ParticleRecord(C.Structure):
+    """eslam_particle_record: PoseParticle with its debug fields (src/PoseParticle.hpp:52-86)"""
+    _fields_ = [
+        ("position", C.c_double * 2),
+        ("orientation", C.c_double),
+        ("zpos", C.c_double),
+        ("zsigma", C.c_double),
+        ("mprob", C.c_double),
+        ("weight", C.c_double),
+        ("meas_pos", C.c_double * 3),
+        ("meas_theta", C.c_double),
+        ("index", C.c_uint64),
+        ("n_cpoints", C.c_uint32),
+        ("floating", C.c_uint8),
+        ("pad", C.c_uint8 * 3),
     ]
 
 

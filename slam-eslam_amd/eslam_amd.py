@@ -49,6 +49,8 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_init_pose.argtypes = [vp, dp, dp]
     L.eslam_gpu_upload_particles.argtypes = [vp, C.c_uint64, C.POINTER(A.Particles)]
     L.eslam_gpu_download_particles.argtypes = [vp, C.POINTER(A.Particles)]
+    L.eslam_gpu_download_records.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(A.ParticleRecord),
+                                             C.POINTER(A.CPoint), C.c_uint32]
     L.eslam_gpu_particle_count.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.eslam_gpu_step.argtypes = [vp, C.POINTER(A.StepInput), C.POINTER(C.c_int)]
     L.eslam_gpu_project.argtypes = [vp, C.POINTER(A.StepInput)]
@@ -131,6 +133,20 @@ class GpuFilter:
         v = pa.view()
         self._check(self.L.eslam_gpu_download_particles(self.h, C.byref(v)))
         return pa
+
+    def download_records(self, first=0, stride=1, count=None, max_cpoints=0):
+        """eslam_gpu_download_records: particles first + k * stride as PoseParticle records
+        (numpy structured array) and, with max_cpoints, their contact points
+        (count x max_cpoints eslam_cpoint, numpy structured)."""
+        n = self.count()
+        if count is None:
+            count = 0 if first >= n else (n - 1 - first) // max(stride, 1) + 1
+        recs = (A.ParticleRecord * max(count, 1))()
+        cps = (A.CPoint * max(count * max_cpoints, 1))() if max_cpoints else None
+        self._check(self.L.eslam_gpu_download_records(self.h, first, stride, count, recs, cps, max_cpoints))
+        r = np.ctypeslib.as_array(recs)[:count].copy()
+        c = np.ctypeslib.as_array(cps)[:count * max_cpoints].reshape(count, max_cpoints).copy() if max_cpoints else None
+        return r, c
 
     def count(self):
         n = C.c_uint64()

@@ -18,3 +18,11 @@ def oracle():
     import oracle_ffi
     oracle_ffi.build()
     return oracle_ffi
+
+
+@pytest.fixture(scope="session")
+def gpu_mod():
+    """the product wrapper over libeslam_gpu.so (fails loudly when the library is missing)"""
+    import eslam_amd
+    eslam_amd.load_library()
+    return eslam_amd

@@ -15,13 +15,6 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def gpu_mod():
-    import eslam_amd
-    eslam_amd.load_library()
-    return eslam_amd
-
-
-@pytest.fixture(scope="module")
 def bench_grid():
     return S.flat_map(cells=1000)
 

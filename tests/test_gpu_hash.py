@@ -11,13 +11,6 @@ from parity_util import assert_bit_identical, info_tuple
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def gpu_mod():
-    import eslam_amd
-    eslam_amd.load_library()
-    return eslam_amd
-
-
 @pytest.mark.parametrize("grid_fn", [hash_grid, rotated_grid])
 def test_hash_create_parity(gpu_mod, grid_fn):
     grid = grid_fn(cells=60)

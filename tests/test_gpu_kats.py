@@ -14,13 +14,6 @@ from parity_util import assert_bit_identical, info_tuple
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def gpu_mod():
-    import eslam_amd
-    eslam_amd.load_library()
-    return eslam_amd
-
-
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_gpu_kat(gpu_mod, oracle, name):
     cfg, grid, st, pa, exp = kat_setup(name)
