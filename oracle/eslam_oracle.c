@@ -1505,25 +1505,108 @@ uint64_t or_best_index(or_filter* f)
     return index;
 }
 
-/* PoseEstimator::getCentroid  src/PoseEstimator.cpp:354-383 (reference arithmetic) */
+/* getCentroid's five sums (x w, y w, theta w, z w, w) under the sum contract: per canonical
+ * chunk (64 lanes x J rows; lane l adds rows in order), an xor butterfly over the lanes
+ * (distances 32 .. 1), then a fixed pairwise tree over the chunks in global order
+ * (dst[i] = src[2i] + src[2i+1], an odd tail moves up).  A sharded filter all-gathers its
+ * chunk records (the shards are chunk-aligned), so every rank gets the one-filter sums.    */
+static void centroid_contract(or_filter* f, double out[5])
+{
+    const uint32_t J = dm_chunk_rows(NG(f));
+    const uint64_t csz = 64ull * J;
+    const uint64_t nch = (f->n + csz - 1) / csz;
+    int G = f->sharded ? f->comm.nranks : 1;
+    uint64_t maxch = nch ? nch : 1;
+    if (f->sharded) {
+        maxch = 1;
+        for (int r = 0; r < G; ++r) {
+            const uint64_t c = (f->gall[r + 1] - f->gall[r] + csz - 1) / csz;
+            maxch = c > maxch ? c : maxch;
+        }
+    }
+    double* mine = calloc(maxch * 5, sizeof(double));
+    for (uint64_t c = 0; c < nch; ++c) {
+        double lane[64][5];
+        for (int l = 0; l < 64; ++l) {
+            double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+            for (uint32_t j = 0; j < J; ++j) {
+                const uint64_t i = c * csz + 64ull * j + (uint64_t)l;
+                if (i >= f->n) continue;
+                const double w = f->w[i];
+                a[0] = a[0] + f->x[i] * w;
+                a[1] = a[1] + f->y[i] * w;
+                a[2] = a[2] + f->th[i] * w;
+                a[3] = a[3] + f->z[i] * w;
+                a[4] = a[4] + w;
+            }
+            memcpy(lane[l], a, sizeof(a));
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            double nxt[64][5];
+            for (int l = 0; l < 64; ++l)
+                for (int q = 0; q < 5; ++q) nxt[l][q] = lane[l][q] + lane[l ^ o][q];
+            memcpy(lane, nxt, sizeof(lane));
+        }
+        memcpy(&mine[c * 5], lane[0], 5 * sizeof(double));
+    }
+    uint64_t total = nch;
+    double* rec = mine;
+    if (f->sharded) {
+        double* all = malloc((size_t)G * maxch * 5 * sizeof(double));
+        comm_allgather(f, mine, all, maxch * 5 * sizeof(double));
+        rec = calloc((size_t)G * maxch * 5 + 5, sizeof(double));
+        total = 0;
+        for (int r = 0; r < G; ++r) {
+            const uint64_t c = (f->gall[r + 1] - f->gall[r] + csz - 1) / csz;
+            memcpy(&rec[total * 5], &all[(uint64_t)r * maxch * 5], c * 5 * sizeof(double));
+            total += c;
+        }
+        free(all);
+    }
+    uint64_t m = total;
+    while (m > 1) {
+        const uint64_t h = m / 2, m2 = (m + 1) / 2;
+        for (uint64_t i = 0; i < h; ++i)
+            for (int q = 0; q < 5; ++q) rec[i * 5 + q] = rec[(2 * i) * 5 + q] + rec[(2 * i + 1) * 5 + q];
+        if (m & 1)
+            for (int q = 0; q < 5; ++q) rec[h * 5 + q] = rec[(m - 1) * 5 + q];
+        m = m2;
+    }
+    for (int q = 0; q < 5; ++q) out[q] = total ? rec[q] : 0.0;
+    if (rec != mine) free(rec);
+    free(mine);
+}
+
+/* PoseEstimator::getCentroid  src/PoseEstimator.cpp:354-383: normalises the weights in place
+ * (Q15), then the weighted means with theta averaged linearly.  Reference mode: the
+ * sequential sums of :357-366 (sharded: each rank's sequential sums, added in rank order);
+ * contract mode: centroid_contract (what the device computes, bit for bit).                */
 void or_get_centroid(or_filter* f, double position[3], double q[4])
 {
-    if (f->sharded) {          /* not defined for a sharded filter (device: ERR_UNSUPPORTED) */
-        position[0] = position[1] = position[2] = NAN;
-        q[0] = q[1] = q[2] = q[3] = NAN;
-        return;
-    }
     or_normalize_weights(f);
-    double mx = 0, my = 0, mo = 0, zm = 0, sw = 0;
-    for (uint64_t i = 0; i < f->n; ++i) {
-        mx += f->x[i] * f->w[i];
-        my += f->y[i] * f->w[i];
-        mo += f->th[i] * f->w[i];
-        zm += f->z[i] * f->w[i];
-        sw += f->w[i];
+    double s[5] = {0, 0, 0, 0, 0};
+    if (f->sum_mode == OR_SUM_CONTRACT) {
+        centroid_contract(f, s);
+    } else {
+        for (uint64_t i = 0; i < f->n; ++i) {
+            s[0] += f->x[i] * f->w[i];
+            s[1] += f->y[i] * f->w[i];
+            s[2] += f->th[i] * f->w[i];
+            s[3] += f->z[i] * f->w[i];
+            s[4] += f->w[i];
+        }
+        if (f->sharded) {
+            double all[5 * ESLAM_ORACLE_MAX_RANKS];
+            comm_allgather(f, s, all, sizeof(s));
+            for (int k = 0; k < 5; ++k) {
+                s[k] = 0.0;
+                for (int r = 0; r < f->comm.nranks; ++r) s[k] += all[5 * r + k];
+            }
+        }
     }
-    mx /= sw; my /= sw; mo /= sw; zm /= sw;
-    position[0] = mx; position[1] = my; position[2] = zm;
+    const double sw = s[4];
+    position[0] = s[0] / sw; position[1] = s[1] / sw; position[2] = s[3] / sw;
+    const double mo = s[2] / sw;
     double a[4];
     q_from_yaw(mo, a);
     q_mul(a, f->zcomp, q);

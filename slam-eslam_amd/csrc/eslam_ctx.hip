@@ -28,6 +28,9 @@ extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const 
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
                                                 eslam_particle_record* out, eslam_cpoint* cps, uint32_t max_cp,
                                                 hipStream_t stream);
+extern "C" hipError_t eslam_launch_centroid_chunks(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl,
+                                                   double* chunk_out, hipStream_t stream);
+extern "C" hipError_t eslam_launch_centroid_tree(double* a, double* b, uint64_t m, double* out, hipStream_t stream);
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
                                                   const GatherView* gv, hipStream_t stream);
@@ -1688,11 +1691,49 @@ extern "C" int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index
 extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double orientation[4])
 {
     if (!ctx || !position || !orientation) return ESLAM_ERR_INVALID_ARG;
-    if (ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "getCentroid is not implemented for a sharded filter");
     int rc = eslam_gpu_normalize_weights(ctx, nullptr);     // side effect, Q15
     if (rc) return rc;
     const uint32_t J = dm_chunk_rows(ctx->n_global);
-    HIPCHK(ctx, eslam_launch_centroid(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->scratch, ctx->stream));
+    if (!ctx->sharded) {
+        HIPCHK(ctx, eslam_launch_centroid(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->scratch, ctx->stream));
+    } else {
+        // the shards are chunk-aligned: every rank's chunk records, all-gathered (padded to
+        // the largest shard) and laid out in global chunk order, feed the same fixed tree
+        // as on one GPU, so every rank computes the one-GPU centroid bit for bit
+        rc = materialize(ctx);
+        if (rc) return rc;
+        const int G = ctx->comm.nranks;
+        const uint64_t csz = 64ull * J;
+        std::vector<uint64_t> nch(G);
+        uint64_t maxch = 1, total = 0;
+        for (int r = 0; r < G; ++r) {
+            nch[r] = (ctx->gall[r + 1] - ctx->gall[r] + csz - 1) / csz;
+            maxch = nch[r] > maxch ? nch[r] : maxch;
+            total += nch[r];
+        }
+        const uint64_t rec = 5 * sizeof(double);
+        double* buf = nullptr;
+        HIPCHK(ctx, hipMalloc(&buf, (maxch + G * maxch + 2 * (total ? total : 1)) * rec));
+        double* mine = buf;
+        double* all = mine + maxch * 5;
+        double* a = all + G * maxch * 5;
+        double* b = a + (total ? total : 1) * 5;
+        hipError_t e = hipMemsetAsync(mine, 0, maxch * rec, ctx->stream);
+        if (e == hipSuccess) e = eslam_launch_centroid_chunks(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, mine, ctx->stream);
+        if (e != hipSuccess) { (void)hipFree(buf); return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e)); }
+        rc = comm_allgather(ctx, mine, all, maxch * rec);
+        if (rc) { (void)hipFree(buf); return rc; }
+        uint64_t off = 0;
+        for (int r = 0; r < G && e == hipSuccess; ++r) {
+            if (nch[r]) e = hipMemcpyAsync(a + off * 5, all + (uint64_t)r * maxch * 5, nch[r] * rec, hipMemcpyDeviceToDevice,
+                                           ctx->stream);
+            off += nch[r];
+        }
+        if (e == hipSuccess) e = eslam_launch_centroid_tree(a, b, total, ctx->scratch, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        (void)hipFree(buf);
+        if (e != hipSuccess) return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e));
+    }
     HIPCHK(ctx, hipMemcpyAsync(ctx->scratch_host, ctx->scratch, 5 * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const double* h = ctx->scratch_host;       // sum x w, y w, theta w, z w, w

@@ -2296,6 +2296,39 @@ extern "C" hipError_t eslam_launch_best_index(DevState s0, DevState s1, uint64_t
     return hipGetLastError();
 }
 
+// the fixed pairwise tree over m chunk records of 5 doubles at a (b: scratch of the same
+// size; both are overwritten); the total goes to out
+static hipError_t centroid_tree(double* a, double* b, uint64_t m, double* out, hipStream_t stream)
+{
+    while (m > 1) {
+        const uint64_t m2 = (m + 1) / 2;
+        hipLaunchKernelGGL(k_tree_level, dim3((uint32_t)((m2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, a, b, m);
+        double* t = a; a = b; b = t;
+        m = m2;
+    }
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, a, 5 * sizeof(double), hipMemcpyDeviceToDevice, stream);
+    return e;
+}
+
+// per canonical chunk (64 x J particles) of this context: sum x w, y w, theta w, z w, w
+extern "C" hipError_t eslam_launch_centroid_chunks(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl,
+                                                   double* chunk_out, hipStream_t stream)
+{
+    const uint64_t csz = 64ull * J;
+    const uint64_t chunks = (n + csz - 1) / csz;
+    const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
+    if (blocks) hipLaunchKernelGGL(k_centroid_chunks, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, J, ctl, chunk_out);
+    return hipGetLastError();
+}
+
+// sharded getCentroid: the tree over the all-gathered chunk records (m chunks at a, b scratch)
+extern "C" hipError_t eslam_launch_centroid_tree(double* a, double* b, uint64_t m, double* out, hipStream_t stream)
+{
+    if (m == 0) return hipMemsetAsync(out, 0, 5 * sizeof(double), stream);
+    return centroid_tree(a, b, m, out, stream);
+}
+
 extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, double* out,
                                             hipStream_t stream)
 {
@@ -2308,18 +2341,8 @@ extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n
     double* a = tmp;
     double* b = tmp + cap * 5;
     e = hipMemsetAsync(a, 0, 5 * sizeof(double), stream);
-    if (e != hipSuccess) { (void)hipFreeAsync(tmp, stream); return e; }
-    const uint32_t blocks = (uint32_t)((chunks + kWaves - 1) / kWaves);
-    if (blocks) hipLaunchKernelGGL(k_centroid_chunks, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, n, J, ctl, a);
-    uint64_t m = chunks;
-    while (m > 1) {
-        const uint64_t m2 = (m + 1) / 2;
-        hipLaunchKernelGGL(k_tree_level, dim3((uint32_t)((m2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, a, b, m);
-        double* t = a; a = b; b = t;
-        m = m2;
-    }
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(out, a, 5 * sizeof(double), hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) e = eslam_launch_centroid_chunks(s0, s1, n, J, ctl, a, stream);
+    if (e == hipSuccess) e = centroid_tree(a, b, chunks, out, stream);
     (void)hipFreeAsync(tmp, stream);
     return e;
 }

@@ -52,8 +52,10 @@ def run_config3(f, n_global, lo, hi, info_fn):
         _info(rec, f"s{k}", info_fn(f))
     pa = f.download()
     anc = f.ancestors()
-    return rec, {fld: np.array(getattr(pa, fld)) for fld in FIELDS}, np.asarray(anc), np.array([f.best_index()]), \
-        np.array([f.rng_state().minstd_x])
+    best, rng = np.array([f.best_index()]), np.array([f.rng_state().minstd_x])
+    pos, quat = f.centroid()
+    rec["centroid"] = np.array(list(pos) + list(quat))
+    return rec, {fld: np.array(getattr(pa, fld)) for fld in FIELDS}, np.asarray(anc), best, rng
 
 
 def upload_arrays(n_global, lo, hi):
@@ -116,4 +118,7 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         _snap(rec, f"s{k}", f, bool(info.resampled))
     rec["best"] = np.array([f.best_index()])
     rec["rng"] = np.array([f.rng_state().minstd_x])
+    pos, quat = f.centroid()                 # getCentroid (normalises in place, Q15)
+    rec["centroid"] = np.array(list(pos) + list(quat))
+    _snap(rec, "centroid", f, False)
     return rec

@@ -69,6 +69,7 @@ def test_config3_eight_ranks_equal_single_context(oracle, tmp_path):
         for fld in FIELDS:
             assert str(p[f"sha/{fld}"]) == digest(fields[fld][lo:hi]), f"rank {r}: {fld} differs"
         assert str(p["sha/anc"]) == digest(anc[lo:hi].astype(np.uint32)), f"rank {r}: ancestors differ"
+        assert np.array_equal(p["centroid"].view(np.uint64), rec["centroid"].view(np.uint64)), f"rank {r}: centroid"
         for k in range(CONFIG3_STEPS):
             assert np.array_equal(p[f"s{k}/info"].view(np.uint64), rec[f"s{k}/info"].view(np.uint64)), (r, k)
         assert int(p["best"][0]) == int(best[0]) and int(p["rng"][0]) == int(rng[0])

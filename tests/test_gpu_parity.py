@@ -176,12 +176,16 @@ def test_particle_filter_api(gpu_mod, rough_grid):
     assert gpu.normalize() == orc.normalize()
     assert_bit_identical(gpu.download(), orc.download(), "normalize")
     assert gpu.count() == n
-    # getCentroid: the device sums in the canonical chunk order + a fixed tree; the oracle
-    # uses the reference's sequential sums -> agreement to 1e-12 relative (not bit-exact)
+    # getCentroid: the device sums in the canonical chunk order + a fixed tree, as the
+    # contract oracle does (bit for bit); the reference's sequential sums agree to 1e-12
+    ref = O.OracleFilter(cfg, O.SUM_REFERENCE)
+    ref.upload(orc.download())
     gp, gq = gpu.centroid()
     op, oq = orc.centroid()
-    assert np.allclose(gp, op, rtol=1e-12, atol=1e-15), (gp, op)
-    assert np.allclose(gq, oq, rtol=1e-12, atol=1e-15), (gq, oq)
+    rp, rq = ref.centroid()
+    assert np.array_equal(np.array(gp + gq).view(np.uint64), np.array(op + oq).view(np.uint64)), (gp, op)
+    assert np.allclose(gp, rp, rtol=1e-12, atol=1e-15), (gp, rp)
+    assert np.allclose(gq, rq, rtol=1e-12, atol=1e-15), (gq, rq)
 
 
 def test_rng_state_resume(gpu_mod, flat_grid):
