@@ -302,6 +302,7 @@ def main():
                               % (BYTES_STEP, BYTES_K1, BYTES_K3, BYTES_REFERENCE,
                                  BYTES_REFERENCE * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world)),
         "last_update": {"effective": info.effective, "resampled": info.resampled},
+        "build_id": eslam_amd.build_id(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, grid)

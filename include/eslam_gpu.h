@@ -167,6 +167,9 @@ int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx** out);
 void eslam_gpu_destroy(eslam_ctx* ctx);
 const char* eslam_gpu_last_error(const eslam_ctx* ctx);
 int eslam_gpu_abi_version(void);
+/* SHA-256 (hex) of the sources, headers and compiler flags the library was built from
+ * (slam-eslam_amd/build_lib.py source_hash): identifies the exact build a run loaded      */
+const char* eslam_gpu_build_id(void);
 /* run on a caller-provided hipStream_t (NULL = the context's own stream) */
 int eslam_gpu_set_stream(eslam_ctx* ctx, void* hip_stream);
 

@@ -336,6 +336,12 @@ static int fail(eslam_ctx* ctx, int code, const char* msg)
 
 extern "C" int eslam_gpu_abi_version(void) { return ESLAM_ABI_VERSION; }
 
+#ifndef ESLAM_BUILD_ID
+#define ESLAM_BUILD_ID "unknown"
+#endif
+// SHA-256 of the sources, headers and flags this library was compiled from (build_lib.py)
+extern "C" const char* eslam_gpu_build_id(void) { return ESLAM_BUILD_ID; }
+
 extern "C" void eslam_config_default(eslam_config* c)
 {
     memset(c, 0, sizeof(*c));

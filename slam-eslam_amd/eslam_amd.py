@@ -25,6 +25,11 @@ class EslamError(RuntimeError):
         self.code = code
 
 
+def build_id():
+    """SHA-256 of the sources the loaded library was built from (eslam_gpu_build_id)."""
+    return load_library().eslam_gpu_build_id().decode()
+
+
 def load_library(path=LIB_PATH):
     """Load libeslam_gpu.so and declare every entry point of include/eslam_gpu.h."""
     global _lib
@@ -33,6 +38,14 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"libeslam_gpu.so not built ({path}); run __graft_entry__.build()")
     L = C.CDLL(path)
+    L.eslam_gpu_build_id.restype = C.c_char_p
+    if "ESLAM_GPU_LIB" not in os.environ:
+        # the in-tree library must be the build of these sources (build_lib.source_hash)
+        import build_lib
+        want, got = build_lib.source_hash(), L.eslam_gpu_build_id().decode()
+        if got != want:
+            raise RuntimeError(f"{path} was built from other sources (build id {got[:12]}, sources {want[:12]}); "
+                               "run __graft_entry__.build()")
     vp = C.c_void_p
     dp = C.POINTER(C.c_double)
     L.eslam_config_default.argtypes = [C.POINTER(A.Config)]

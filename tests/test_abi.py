@@ -39,6 +39,15 @@ def test_exports_every_declared_symbol(lib):
     assert not missing, missing
 
 
+def test_library_built_from_these_sources(lib):
+    """provenance: the shipped library reports the SHA-256 of the current sources and flags"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "slam-eslam_amd"))
+    import build_lib
+    lib.eslam_gpu_build_id.restype = C.c_char_p
+    assert lib.eslam_gpu_build_id().decode() == build_lib.source_hash()
+
+
 def test_abi_version(lib):
     lib.eslam_gpu_abi_version.restype = C.c_int
     assert lib.eslam_gpu_abi_version() == 2
