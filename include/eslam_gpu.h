@@ -350,6 +350,9 @@ int eslam_gpu_selftest_math(int device, int fn, const double* x, const double* y
  * against the general dm_log / dm_sqrt, on the device, for all 2^32 uniform words: the
  * number of words whose results differ in any bit (0 expected)                           */
 int eslam_gpu_selftest_bm_radius(int device, uint64_t* mismatches);
+/* the device's stable radix sort of (key, value) pairs (the hash respawn's select order)  */
+int eslam_gpu_selftest_sort(int device, const uint32_t* keys, const uint32_t* vals, uint64_t n, uint32_t* keys_out,
+                            uint32_t* vals_out);
 
 #ifdef __cplusplus
 }

@@ -43,7 +43,8 @@ def source_hash(defines=(), extra=()):
         h.update(os.path.basename(path).encode())
         with open(path, "rb") as fh:
             h.update(fh.read())
-    h.update(repr((FLAGS, PER_SOURCE, list(defines), list(extra), ARCH)).encode())
+    flags = [f.replace(ROOT, "<root>") for f in FLAGS]      # location-independent (the GPU box's copy)
+    h.update(repr((flags, PER_SOURCE, list(defines), list(extra), ARCH)).encode())
     return h.hexdigest()
 
 

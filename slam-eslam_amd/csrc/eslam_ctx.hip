@@ -1831,6 +1831,31 @@ extern "C" int eslam_gpu_selftest_bm_radius(int device, uint64_t* mismatches)
     return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
 }
 
+extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_out, uint32_t* order, uint64_t n,
+                                             void* tmp, size_t* tmp_bytes, hipStream_t stream);
+
+extern "C" int eslam_gpu_selftest_sort(int device, const uint32_t* keys, const uint32_t* vals, uint64_t n, uint32_t* keys_out,
+                                       uint32_t* vals_out)
+{
+    if ((!keys || !vals || !keys_out || !vals_out) && n) return ESLAM_ERR_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return ESLAM_ERR_HIP;
+    size_t bytes = 0;
+    eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, n, nullptr, &bytes, nullptr);
+    const uint64_t b = (n ? n : 1) * 4;
+    uint32_t* d = nullptr;
+    void* tmp = nullptr;
+    if (hipMalloc(&d, 4 * b) != hipSuccess || hipMalloc(&tmp, bytes) != hipSuccess) return ESLAM_ERR_OUT_OF_MEMORY;
+    hipError_t e = hipMemcpy(d, keys, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + b / 4, vals, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = eslam_radix_sort_pairs(d, d + b / 4, d + 2 * b / 4, d + 3 * b / 4, n, tmp, &bytes, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(keys_out, d + 2 * b / 4, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(vals_out, d + 3 * b / 4, n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    (void)hipFree(tmp);
+    return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
+}
+
 extern "C" int eslam_gpu_selftest_math(int device, int fn, const double* x, const double* y, double* out, uint64_t n)
 {
     if (hipSetDevice(device) != hipSuccess) return ESLAM_ERR_HIP;

@@ -7,10 +7,13 @@
 //   k_hash_keys + radix sort + k_hash_replace
 //                     PoseEstimator::sampleFromHash  src/PoseEstimator.cpp:130-182: the
 //                     replace_count lowest (float weight, index) pairs get hash poses
+//   k_radix_hist / k_radix_scan / k_radix_scatter
+//                     a stable LSD radix sort of (u32 key, u32 value) pairs, 8 bits per
+//                     pass: per-tile digit histograms, one exclusive scan in digit-major
+//                     order, and a scatter that ranks each tile's elements stably with
+//                     wave ballots (peers of a digit) and per-wave digit counts in LDS
 // Not on the per-step hot path (init, and every hash_period-th project).
 #include <hip/hip_runtime.h>
-
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "eslam_internal.h"
 
@@ -58,6 +61,97 @@ __global__ void __launch_bounds__(kBlock) k_init_from_hash(DevState s0, const ui
     s0.x[i] = hx[k]; s0.y[i] = hy[k]; s0.th[i] = hth[k]; s0.z[i] = hz[k];
     s0.zs[i] = 0.0; s0.w[i] = 0.0; s0.mprob[i] = 0.0;
     s0.flags[i] = (uint8_t)(1u << 7);
+}
+
+// ---- stable LSD radix sort of (key, value) pairs -------------------------------------
+constexpr int kSortItems = 8;                        // elements per thread of a tile
+constexpr int kSortTile = kBlock * kSortItems;       // elements per tile (block)
+constexpr int kDigits = 256;
+
+// tile b's count of every digit of bits [shift, shift + 8): hist[d * ntiles + b]
+__global__ void __launch_bounds__(kBlock) k_radix_hist(const uint32_t* __restrict__ keys, uint64_t n, int shift,
+                                                       uint32_t* __restrict__ hist, uint32_t ntiles)
+{
+    __shared__ uint32_t s_cnt[kDigits];
+    s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint64_t e = base + (uint64_t)r * kBlock + threadIdx.x;
+        if (e < n) atomicAdd(&s_cnt[(keys[e] >> shift) & 0xffu], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = s_cnt[threadIdx.x];
+}
+
+// exclusive prefix sum of m counts in place (one block: each thread a contiguous segment)
+__global__ void __launch_bounds__(1024) k_radix_scan(uint32_t* __restrict__ a, uint64_t m)
+{
+    __shared__ uint32_t s_sum[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    uint32_t t = 0;
+    for (uint64_t i = lo; i < hi; ++i) t += a[i];
+    s_sum[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {             // Hillis-Steele inclusive scan of the segment sums
+        const uint32_t v = threadIdx.x >= (uint32_t)o ? s_sum[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_sum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_sum[threadIdx.x] - t;
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t v = a[i];
+        a[i] = run;
+        run += v;
+    }
+}
+
+// tile b's elements to their sorted positions: offs[d * ntiles + b] (scanned histogram) +
+// the element's rank among the tile's elements of digit d, in element order (stable).
+// Rounds of 256 consecutive elements; in a round, lanes of one wave with the same digit
+// (the AND of 8 ballots) rank by lane, waves by the per-wave digit counts in LDS.
+__global__ void __launch_bounds__(kBlock) k_radix_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint64_t n,
+                                                          int shift, const uint32_t* __restrict__ offs, uint32_t ntiles)
+{
+    __shared__ uint32_t s_run[kDigits];              // elements of each digit placed so far
+    __shared__ uint32_t s_wcnt[kWaves][kDigits];     // this round: per wave, per digit
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    s_run[tid] = offs[(uint64_t)tid * ntiles + blockIdx.x];
+    for (int w = 0; w < kWaves; ++w) s_wcnt[w][tid] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int r = 0; r < kSortItems; ++r) {
+        const uint64_t e = base + (uint64_t)r * kBlock + tid;
+        const bool valid = e < n;
+        const uint32_t key = valid ? kin[e] : 0u;
+        const uint32_t val = valid ? vin[e] : 0u;
+        const uint32_t d = (key >> shift) & 0xffu;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t in_wave = (uint32_t)__popcll(peers & below);
+        if (valid && in_wave == 0) s_wcnt[wave][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = s_run[d] + in_wave;
+            for (uint32_t w = 0; w < wave; ++w) pos += s_wcnt[w][d];
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+        __syncthreads();
+        uint32_t add = 0;
+        for (int w = 0; w < kWaves; ++w) { add += s_wcnt[w][tid]; s_wcnt[w][tid] = 0; }
+        s_run[tid] += add;
+        __syncthreads();
+    }
 }
 
 // sort keys of (float weight, index): ascending float order, -0 == +0, ties by index
@@ -123,16 +217,47 @@ extern "C" hipError_t eslam_launch_init_from_hash(DevState s0, const uint32_t* i
     return hipGetLastError();
 }
 
-// the k lowest particles by (float weight, index) into order[0..k): keys + stable radix sort.
+// stable radix sort of n (key, value) pairs: keys/vals in, sorted into keys_out/order.
+// tmp: scratch for the digit histograms and one ping-pong pair (query its size with
+// tmp == NULL).  Four passes of 8 bits; the pass results alternate so the last lands in
+// keys_out/order.
+extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_out, uint32_t* order, uint64_t n,
+                                             void* tmp, size_t* tmp_bytes, hipStream_t stream)
+{
+    const uint32_t ntiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
+    const uint64_t hist_words = (uint64_t)kDigits * (ntiles ? ntiles : 1);
+    const size_t need = hist_words * 4 + 2 * (n ? n : 1) * 4;
+    if (!tmp) { *tmp_bytes = need; return hipSuccess; }
+    if (*tmp_bytes < need) return hipErrorInvalidValue;
+    if (!n) return hipSuccess;
+    uint32_t* hist = (uint32_t*)tmp;
+    uint32_t* tk = hist + hist_words;
+    uint32_t* tv = tk + n;
+    // passes: keys -> (tk, tv) -> (keys_out, order) -> (tk, tv) -> (keys_out, order)
+    const uint32_t* ki = keys;
+    const uint32_t* vi = vals;
+    for (int pass = 0; pass < 4; ++pass) {
+        uint32_t* ko = (pass & 1) ? keys_out : tk;
+        uint32_t* vo = (pass & 1) ? order : tv;
+        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kBlock), 0, stream, ki, n, 8 * pass, hist, ntiles);
+        hipLaunchKernelGGL(k_radix_scan, dim3(1), dim3(1024), 0, stream, hist, hist_words);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kBlock), 0, stream, ki, vi, ko, vo, n, 8 * pass, hist, ntiles);
+        ki = ko;
+        vi = vo;
+    }
+    return hipGetLastError();
+}
+
+// the k lowest particles by (float weight, index) into order[0..k): keys + the stable sort.
 // tmp/tmp_bytes: caller-owned scratch (query with tmp == NULL)
 extern "C" hipError_t eslam_hash_sort(DevState s0, DevState s1, const Ctl* ctl, uint64_t n, uint32_t* keys, uint32_t* vals,
                                       uint32_t* keys_out, uint32_t* order, void* tmp, size_t* tmp_bytes, hipStream_t stream)
 {
-    if (!tmp) return rocprim::radix_sort_pairs(nullptr, *tmp_bytes, keys, keys_out, vals, order, (uint32_t)n, 0u, 32u, stream);
+    if (!tmp) return eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, n, nullptr, tmp_bytes, stream);
     if (n) hipLaunchKernelGGL(k_hash_keys, dim3(blocks_for(n)), dim3(kBlock), 0, stream, s0, s1, ctl, n, keys, vals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return rocprim::radix_sort_pairs(tmp, *tmp_bytes, keys, keys_out, vals, order, (uint32_t)n, 0u, 32u, stream);
+    return eslam_radix_sort_pairs(keys, vals, keys_out, order, n, tmp, tmp_bytes, stream);
 }
 
 extern "C" hipError_t eslam_launch_hash_replace(DevState s0, DevState s1, const Ctl* ctl, const uint32_t* order,

@@ -80,6 +80,8 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_enable_timing.argtypes = [vp, C.c_int]
     L.eslam_gpu_get_kernel_times.argtypes = [vp, C.POINTER(A.KernelTimes)]
     L.eslam_gpu_selftest_math.argtypes = [C.c_int, C.c_int, dp, dp, dp, C.c_uint64]
+    up = C.POINTER(C.c_uint32)
+    L.eslam_gpu_selftest_sort.argtypes = [C.c_int, up, up, C.c_uint64, up, up]
     if hasattr(L, "eslam_gpu_selftest_bm_radius"):       # absent from older builds (A/B runs)
         L.eslam_gpu_selftest_bm_radius.argtypes = [C.c_int, C.POINTER(C.c_uint64)]
     L.eslam_gpu_set_comm.argtypes = [vp, C.POINTER(A.Comm), C.c_uint64, C.POINTER(C.c_uint64)]

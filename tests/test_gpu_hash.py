@@ -57,3 +57,20 @@ def test_hash_filter_parity(gpu_mod, mode):
     if mode == "split":
         assert replaced > 0
     assert gpu.rng_state().libc_rand_pos == orc.rng_state().libc_rand_pos
+
+
+@pytest.mark.parametrize("n,distinct", [(1, 4), (1000, 3), (2048 * 3 + 17, 50), (1 << 20, 1 << 31)])
+def test_radix_sort_stable(gpu_mod, n, distinct):
+    """The hand-written radix sort behind sampleFromHash's (float weight, index) order: equal
+    to numpy's stable argsort, many-way ties included (the respawn's draws follow this order)."""
+    import ctypes as C
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, distinct, n, dtype=np.uint64).astype(np.uint32) * np.uint32(0x9E3779B1)
+    vals = np.arange(n, dtype=np.uint32)
+    ko = np.zeros(n, np.uint32)
+    vo = np.zeros(n, np.uint32)
+    L = gpu_mod.load_library()
+    p = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))
+    assert L.eslam_gpu_selftest_sort(0, p(keys), p(vals), n, p(ko), p(vo)) == 0
+    order = np.argsort(keys, kind="stable")
+    assert np.array_equal(vo, vals[order]) and np.array_equal(ko, keys[order])
