@@ -891,23 +891,51 @@ static void sample_from_hash(or_filter* f, const eslam_step_input* in)
     if (k > N) k = N;
     if (k == 0 || bsize == 0) return;      /* nothing replaced, no rand() drawn */
     const double weight = ((or_get_weights_sum(f) / (double)N) * f->cfg.hash_avg_factor) * rel;
-    or_widx* wi = malloc(sizeof(or_widx) * f->n);
+    /* (float weight, global index) of every particle; sharded: all ranks' pairs, gathered
+     * in rank order, so every rank sorts the one-filter list and replaces what it holds   */
+    or_widx* wi = malloc(sizeof(or_widx) * (f->n ? f->n : 1));
     for (uint64_t i = 0; i < f->n; ++i) {
         float wf = (float)f->w[i];
         if (wf == 0.0f) wf = 0.0f;                /* -0 and +0 compare equal */
         wi[i].w = wf;
-        wi[i].i = (uint32_t)i;
+        wi[i].i = (uint32_t)(f->gbase + i);
     }
-    qsort(wi, f->n, sizeof(or_widx), widx_cmp);
+    or_widx* all = wi;
+    uint64_t total = f->n;
+    if (f->sharded) {
+        const int G = f->comm.nranks;
+        uint64_t maxn = 1;
+        for (int r = 0; r < G; ++r) {
+            const uint64_t nr = f->gall[r + 1] - f->gall[r];
+            maxn = nr > maxn ? nr : maxn;
+        }
+        or_widx* pad = calloc(maxn, sizeof(or_widx));
+        memcpy(pad, wi, f->n * sizeof(or_widx));
+        or_widx* g = malloc((size_t)G * maxn * sizeof(or_widx));
+        comm_allgather(f, pad, g, maxn * sizeof(or_widx));
+        all = malloc((size_t)N * sizeof(or_widx));
+        total = 0;
+        for (int r = 0; r < G; ++r) {
+            const uint64_t nr = f->gall[r + 1] - f->gall[r];
+            memcpy(all + total, g + (uint64_t)r * maxn, nr * sizeof(or_widx));
+            total += nr;
+        }
+        free(pad);
+        free(g);
+    }
+    qsort(all, total, sizeof(or_widx), widx_cmp);
     for (uint64_t j = 0; j < k; ++j) {
         const uint32_t draw = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&f->libc) % bsize);
         const uint32_t src = f->hash_blist[f->hash_bstart[b] + draw];
-        const uint32_t i = wi[j].i;
+        const uint64_t gi = all[j].i;
+        if (gi < f->gbase || gi >= f->gbase + f->n) continue;
+        const uint64_t i = gi - f->gbase;
         f->x[i] = f->hash_x[src]; f->y[i] = f->hash_y[src]; f->th[i] = f->hash_th[src]; f->z[i] = f->hash_z[src];
         f->zs[i] = 0.5;
         f->floating[i] = 1;
         f->w[i] = weight;
     }
+    if (all != wi) free(all);
     free(wi);
 }
 

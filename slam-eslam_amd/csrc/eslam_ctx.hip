@@ -31,6 +31,16 @@ extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const 
 extern "C" hipError_t eslam_launch_centroid_chunks(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl,
                                                    double* chunk_out, hipStream_t stream);
 extern "C" hipError_t eslam_launch_centroid_tree(double* a, double* b, uint64_t m, double* out, hipStream_t stream);
+extern "C" hipError_t eslam_launch_hash_candidates(const uint32_t* keys, const uint32_t* order, uint64_t cnt, uint64_t gbase,
+                                                   int nranks, void* send, hipStream_t stream);
+extern "C" hipError_t eslam_launch_hash_unpack(const void* recv, uint64_t m, uint32_t* keys, uint32_t* vals, hipStream_t stream);
+extern "C" hipError_t eslam_launch_hash_replace_global(DevState s0, DevState s1, const Ctl* ctl, const uint32_t* gorder,
+                                                       const uint32_t* draws, uint64_t k, uint64_t gbase, uint64_t n,
+                                                       const uint32_t* blist, uint32_t bstart, const double* hx,
+                                                       const double* hy, const double* hth, const double* hz, double weight,
+                                                       hipStream_t stream);
+extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_out, uint32_t* order, uint64_t n,
+                                             void* tmp, size_t* tmp_bytes, hipStream_t stream);
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
                                                   const GatherView* gv, hipStream_t stream);
@@ -271,6 +281,9 @@ struct eslam_ctx {
     std::vector<uint32_t> hash_bstart;       // bins^2 + 1
     std::vector<int32_t> hash_bucket;        // per pose (sweep order)
     dm_libc_rand_state libc;                 // rand() of SurfaceHash::sample (glibc, seed 1)
+    void* hsend = nullptr; uint64_t hsend_cap = 0;   // sharded respawn: candidate pairs out / in
+    void* hrecv = nullptr; uint64_t hrecv_cap = 0;
+    void* hsort = nullptr; uint64_t hsort_cap = 0;   // their keys, vals, sorted keys, order + sort scratch
     uint32_t* d_sort = nullptr;              // keys, vals, keys_out, order (4 x cap)
     uint64_t sort_cap = 0;
     void* sort_tmp = nullptr;
@@ -509,6 +522,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
     (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
+    (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1420,9 +1434,8 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
     const uint64_t N = ctx->n_global;
     uint64_t k = (uint64_t)(((double)N * ctx->cfg.hash_percentage) * rel);
     if (rel < 0.8) k = 0;
-    if (k > ctx->n) k = ctx->n;
+    if (k > N) k = N;
     if (k == 0 || bsize == 0) return ESLAM_OK;                // nothing replaced, no rand() drawn
-    if (ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "sampleFromHash is not implemented for a sharded filter");
     double S = 0.0;
     int rc = eslam_gpu_get_weights_sum(ctx, &S);
     if (rc) return rc;
@@ -1446,6 +1459,36 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
     size_t bytes = ctx->sort_tmp_bytes;
     HIPCHK(ctx, eslam_hash_sort(ctx->st[0], ctx->st[1], ctx->ctl, n, keys, vals, keys_out, order, ctx->sort_tmp, &bytes,
                                 ctx->stream));
+    // sharded: the global order of the k lowest.  Rank r contributes its min(k, n_r) lowest
+    // pairs (any of the k lowest lies among them); every rank sorts the same concatenation.
+    const uint32_t* gorder = order;
+    if (ctx->sharded) {
+        const int G = ctx->comm.nranks, me = ctx->comm.rank;
+        std::vector<uint64_t> cnt(G), sb(G), rb(G);
+        uint64_t total = 0;
+        for (int r = 0; r < G; ++r) {
+            const uint64_t nr = ctx->gall[r + 1] - ctx->gall[r];
+            cnt[r] = k < nr ? k : nr;
+            total += cnt[r];
+        }
+        for (int d = 0; d < G; ++d) { sb[d] = cnt[me] * 8; rb[d] = cnt[d] * 8; }
+        rc = grow(ctx, &ctx->hsend, &ctx->hsend_cap, G * cnt[me] * 8 + 8, false);
+        if (!rc) rc = grow(ctx, &ctx->hrecv, &ctx->hrecv_cap, total * 8 + 8, false);
+        size_t sbytes = 0;
+        eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, total, nullptr, &sbytes, ctx->stream);
+        if (!rc) rc = grow(ctx, &ctx->hsort, &ctx->hsort_cap, 16 * (total + 1) + sbytes, false);
+        if (rc) return rc;
+        HIPCHK(ctx, eslam_launch_hash_candidates(keys_out, order, cnt[me], ctx->gbase, G, ctx->hsend, ctx->stream));
+        rc = comm_alltoallv(ctx, ctx->hsend, sb.data(), ctx->hrecv, rb.data());
+        if (rc) return rc;
+        uint32_t* ck = (uint32_t*)ctx->hsort;
+        uint32_t* cv = ck + total + 1;
+        uint32_t* sk = cv + total + 1;
+        uint32_t* so = sk + total + 1;
+        HIPCHK(ctx, eslam_launch_hash_unpack(ctx->hrecv, total, ck, cv, ctx->stream));
+        HIPCHK(ctx, eslam_radix_sort_pairs(ck, cv, sk, so, total, so + total + 1, &sbytes, ctx->stream));
+        gorder = so;
+    }
     std::vector<uint32_t> draws(k);
     for (uint64_t j = 0; j < k; ++j) draws[j] = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&ctx->libc) % bsize);
     if (ctx->draws_cap < k) {
@@ -1454,9 +1497,15 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
         ctx->draws_cap = k;
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_draws, draws.data(), sizeof(uint32_t) * k, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, eslam_launch_hash_replace(ctx->st[0], ctx->st[1], ctx->ctl, order, ctx->d_draws, k, ctx->d_hash_blist,
-                                          ctx->hash_bstart[b], hash_field(ctx, 0), hash_field(ctx, 1), hash_field(ctx, 2),
-                                          hash_field(ctx, 3), weight, ctx->stream));
+    if (ctx->sharded)
+        HIPCHK(ctx, eslam_launch_hash_replace_global(ctx->st[0], ctx->st[1], ctx->ctl, gorder, ctx->d_draws, k, ctx->gbase,
+                                                     ctx->n, ctx->d_hash_blist, ctx->hash_bstart[b], hash_field(ctx, 0),
+                                                     hash_field(ctx, 1), hash_field(ctx, 2), hash_field(ctx, 3), weight,
+                                                     ctx->stream));
+    else
+        HIPCHK(ctx, eslam_launch_hash_replace(ctx->st[0], ctx->st[1], ctx->ctl, order, ctx->d_draws, k, ctx->d_hash_blist,
+                                              ctx->hash_bstart[b], hash_field(ctx, 0), hash_field(ctx, 1), hash_field(ctx, 2),
+                                              hash_field(ctx, 3), weight, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));          // draws (host) must outlive the copy
     return ESLAM_OK;
 }
@@ -1830,9 +1879,6 @@ extern "C" int eslam_gpu_selftest_bm_radius(int device, uint64_t* mismatches)
     *mismatches = h;
     return e == hipSuccess ? ESLAM_OK : ESLAM_ERR_HIP;
 }
-
-extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_out, uint32_t* order, uint64_t n,
-                                             void* tmp, size_t* tmp_bytes, hipStream_t stream);
 
 extern "C" int eslam_gpu_selftest_sort(int device, const uint32_t* keys, const uint32_t* vals, uint64_t n, uint32_t* keys_out,
                                        uint32_t* vals_out)

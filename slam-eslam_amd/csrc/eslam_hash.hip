@@ -187,6 +187,50 @@ __global__ void __launch_bounds__(kBlock) k_hash_replace(DevState s0, DevState s
     st.w[i] = weight;
 }
 
+// ---- sharded sampleFromHash: every rank's cnt lowest (key, global index) pairs go to every
+// rank (an all_to_all_v used as an all-gather of uneven parts, rank order); the stable sort of
+// their concatenation by key puts equal keys in global index order, so its first k entries
+// are the one-filter order of src/PoseEstimator.cpp:146-152 on every rank
+__global__ void __launch_bounds__(kBlock) k_hash_candidates(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ order,
+                                                            uint64_t cnt, uint64_t gbase, int nranks, uint2* __restrict__ send)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= cnt) return;
+    const uint2 pr = make_uint2(keys[e], (uint32_t)(gbase + order[e]));
+    for (int d = 0; d < nranks; ++d) send[(uint64_t)d * cnt + e] = pr;
+}
+
+__global__ void __launch_bounds__(kBlock) k_hash_unpack(const uint2* __restrict__ recv, uint64_t m, uint32_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= m) return;
+    keys[e] = recv[e].x;
+    vals[e] = recv[e].y;
+}
+
+// the j-th lowest (j < k, global order) gets hash pose draws[j] if this rank holds it
+__global__ void __launch_bounds__(kBlock) k_hash_replace_global(DevState s0, DevState s1, const Ctl* __restrict__ ctl,
+                                                                const uint32_t* __restrict__ gorder,
+                                                                const uint32_t* __restrict__ draws, uint64_t k, uint64_t gbase,
+                                                                uint64_t n, const uint32_t* __restrict__ blist, uint32_t bstart,
+                                                                const double* __restrict__ hx, const double* __restrict__ hy,
+                                                                const double* __restrict__ hth, const double* __restrict__ hz,
+                                                                double weight)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= k) return;
+    const uint64_t gi = gorder[j];
+    if (gi < gbase || gi >= gbase + n) return;
+    const uint64_t i = gi - gbase;
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    const uint32_t src = blist[bstart + draws[j]];
+    st.x[i] = hx[src]; st.y[i] = hy[src]; st.th[i] = hth[src]; st.z[i] = hz[src];
+    st.zs[i] = 0.5;
+    st.flags[i] = (uint8_t)(st.flags[i] | (1u << 7));
+    st.w[i] = weight;
+}
+
 }  // namespace eslam_dev
 
 using namespace eslam_dev;
@@ -267,5 +311,30 @@ extern "C" hipError_t eslam_launch_hash_replace(DevState s0, DevState s1, const 
 {
     if (k) hipLaunchKernelGGL(k_hash_replace, dim3(blocks_for(k)), dim3(kBlock), 0, stream, s0, s1, ctl, order, draws, k,
                               blist, bstart, hx, hy, hth, hz, weight);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_hash_candidates(const uint32_t* keys, const uint32_t* order, uint64_t cnt, uint64_t gbase,
+                                                   int nranks, void* send, hipStream_t stream)
+{
+    if (cnt) hipLaunchKernelGGL(k_hash_candidates, dim3(blocks_for(cnt)), dim3(kBlock), 0, stream, keys, order, cnt, gbase,
+                                nranks, (uint2*)send);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_hash_unpack(const void* recv, uint64_t m, uint32_t* keys, uint32_t* vals, hipStream_t stream)
+{
+    if (m) hipLaunchKernelGGL(k_hash_unpack, dim3(blocks_for(m)), dim3(kBlock), 0, stream, (const uint2*)recv, m, keys, vals);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_hash_replace_global(DevState s0, DevState s1, const Ctl* ctl, const uint32_t* gorder,
+                                                       const uint32_t* draws, uint64_t k, uint64_t gbase, uint64_t n,
+                                                       const uint32_t* blist, uint32_t bstart, const double* hx,
+                                                       const double* hy, const double* hth, const double* hz, double weight,
+                                                       hipStream_t stream)
+{
+    if (k) hipLaunchKernelGGL(k_hash_replace_global, dim3(blocks_for(k)), dim3(kBlock), 0, stream, s0, s1, ctl, gorder, draws,
+                              k, gbase, n, blist, bstart, hx, hy, hth, hz, weight);
     return hipGetLastError();
 }

@@ -10,11 +10,16 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "config3")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3")
 CONFIG3_STEPS = 3
 
 
 def scenario_config(name, n_global):
+    if name == "hash":                           # useHash: init from the hash, respawn every 2nd step
+        from hash_util import hash_config
+        cfg = hash_config(n_global, steps=8, bins=20, period=2, percentage=0.2)
+        cfg.seed = 1234
+        return cfg
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
@@ -29,6 +34,9 @@ def scenario_config(name, n_global):
 
 
 def scenario_grid(name):
+    if name == "hash":
+        from hash_util import hash_grid
+        return hash_grid(cells=60)
     if name == "config3":
         return S.flat_map(cells=1000)             # the bench's 100 x 100 m map
     return S.rough_map(cells=120) if name != "forced" else S.rough_map(cells=120, multi=False)
@@ -106,11 +114,17 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         _snap(rec, "norm", f, False)
         f.resample()
         _snap(rec, "res", f, True)
+    elif name == "hash":
+        f.init_pose([0.0, 0.0, 0.18], [1.0, 0.0, 0.0, 0.0])       # SurfaceHash::create + init(N, hash)
     else:
         sigma = [0.1, 0.1, 0.1] if name == "forced" else [0.6, 0.6, 0.3]
         f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], sigma, 0.18, 1.001)
     _snap(rec, "init", f, False)
-    stream = S.step_stream(steps, tilt=(name == "natural"))
+    if name == "hash":
+        from hash_util import slope_stream
+        stream = slope_stream(steps)
+    else:
+        stream = S.step_stream(steps, tilt=(name == "natural"))
     for k, st in enumerate(stream):
         f.step(st)
         info = info_fn(f)
