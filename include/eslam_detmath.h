@@ -875,6 +875,9 @@ DM_FN double dm_limbs_to_double(const uint64_t L[4], int scale)
  * only on the GLOBAL particle count, so any sharding over GPUs gives the same bits.     */
 #define DM_CHUNK_LANES 64
 #define DM_FX_SCALE 112          /* fixed-point scale of a chunk total bounded by 2^10 */
+/* per-particle map store: the first probe slot of a cell (multiplicative hash, 32 slots) */
+DM_FN uint32_t dm_store_hash(uint32_t cell) { return (cell * 2654435761u) >> 27; }
+
 #define DM_NBUCKETS 6            /* cpoints.size() buckets 0,1,2,3,4,>=5 (phase B)     */
 
 /* J = the largest power of two <= min(16, n_global / 2^19): from 512k particles on there are

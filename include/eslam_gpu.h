@@ -85,6 +85,8 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_RECORD_ANCESTORS 0x1u   /* keep the last resample's ancestor indices     */
 #define ESLAM_FLAG_NO_MAP_LDS 0x2u         /* disable the LDS map window (global lookups)   */
 #define ESLAM_FLAG_NO_AUX_GATHER 0x4u      /* do not carry mprob/floating through resample  */
+#define ESLAM_FLAG_PARTICLE_MAPS 0x10u     /* useSharedMap = false: every particle its own local
+                                              map (eslam_gpu_map_update); one GPU only       */
 #define ESLAM_FLAG_RECORD_CONTACTS 0x8u    /* keep every update's cpoints, meas_pos, meas_theta
                                               (also on with log_debug); one GPU only          */
 
@@ -188,6 +190,27 @@ int eslam_gpu_init_pose(eslam_ctx* ctx, const double position[3], const double o
 /* replace the particle set (getParticles() is a mutable reference in the reference)       */
 int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const eslam_particles* p);
 int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p);
+
+/* ---- per-particle local maps (useSharedMap = false) -----------------
+ * EmbodiedSlamFilter::processMap(scanMap, match=false, update=true)
+ * (src/EmbodiedSlamFilter.cpp:179-232) after PoseEstimator::cloneMaps (src/PoseEstimator.cpp:
+ * 31-47): every particle's map is the shared grid plus its own patches in cells the grid
+ * leaves empty.  A map update places the scan patches at each particle's pose
+ * (Translation(x, y, 0) * Rz(theta); offset patch zPos, zSigma) and, per patch, inserts it
+ * into an empty cell or fuses it (variance-weighted) with the particle's patch there when
+ * within 3 sigma; cells of the shared grid are not changed, a particle holds at most 24
+ * patches.  The contact update then reads each particle's own map.  Particles that a
+ * resample copied share their patches until the next map update copies them (copy on
+ * write).  Only the insert-into-empty-cell rule is pinned by the reference
+ * (test/testMap.cpp:307-316); envire's MLSGrid::merge is not in the reference.            */
+typedef struct eslam_scan_patch {
+    double position[3];                    /* yaw-free body frame (the scan MLS's cells)    */
+    double stdev;                          /* sensor sigma of the patch                      */
+} eslam_scan_patch;
+int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);   /* count <= 64 */
+/* particle index's own patches (cell = n * width + m, mean, stdev); *count = how many it has */
+int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32_t* cells, float* mean, float* stdev,
+                               uint32_t capacity, uint32_t* count);
 
 /* ---- PoseParticle records with the debug fields (getParticles() for logging / viz) ------ */
 /* ContactPoint  src/PoseParticle.hpp:20-43: one contact point evaluatePose pushed           */

@@ -200,6 +200,51 @@ static int grid_map_fn(void* user, const double p[3], double q_mean, double q_va
     return or_mls_get_patch((const eslam_mls_grid*)user, p, q_mean, q_var, mean, stdev);
 }
 
+#define OR_STORE_SLOTS 32u            /* per-particle map store: slots, patches at most */
+#define OR_STORE_CAP 24u
+
+/* per-particle maps: GridAccess::get on the particle's own map = the shared grid, and for a
+ * cell the grid leaves empty the particle's patch there (same 3-sigma gate)               */
+typedef struct {
+    const eslam_mls_grid* g;
+    const uint32_t* key;                 /* the particle's 32 slots */
+    const float* val;
+} or_pmap;
+
+static int particle_map_fn(void* user, const double p[3], double q_mean, double q_var, double* mean, double* stdev)
+{
+    const or_pmap* pm = (const or_pmap*)user;
+    const eslam_mls_grid* g = pm->g;
+    if (or_mls_get_patch(g, p, q_mean, q_var, mean, stdev)) return 1;
+    const double* A = g->global2local;
+    static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    int is_id = 1;
+    for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
+    double lx = p[0], ly = p[1], lz = p[2];
+    if (!is_id) {
+        lx = ((A[0] * p[0] + A[1] * p[1]) + A[2] * p[2]) + A[3];
+        ly = ((A[4] * p[0] + A[5] * p[1]) + A[6] * p[2]) + A[7];
+        lz = ((A[8] * p[0] + A[9] * p[1]) + A[10] * p[2]) + A[11];
+    }
+    const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
+    const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
+    if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) return 0;
+    const uint32_t cell = (uint32_t)fn * g->width + (uint32_t)fm;
+    if (g->cell_start[cell] != g->cell_start[cell + 1]) return 0;       /* the grid's cell: no patch passed */
+    uint32_t h = dm_store_hash(cell);
+    for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
+        if (pm->key[h] == cell + 1u) {
+            const double m = (double)pm->val[2 * h], sd = (double)pm->val[2 * h + 1];
+            const double diff = fabs(m - lz);
+            if (diff * diff < 9.0 * (sd * sd + q_var)) { *mean = m; *stdev = sd; return 1; }
+            return 0;
+        }
+        if (pm->key[h] == 0) return 0;
+        h = (h + 1u) & (OR_STORE_SLOTS - 1u);
+    }
+    return 0;
+}
+
 /* ========================================================================================
  * ContactModel
  * ====================================================================================== */
@@ -515,7 +560,13 @@ struct or_filter {
     int threads;
     int literal;                         /* or_set_literal */
     int debug;                           /* or_set_debug */
+    /* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): each particle's own patches in cells the
+     * shared grid leaves empty, 32 open-addressing slots (key = cell + 1), at most 24 */
+    uint32_t* pm_key;                    /* n x 32 */
+    float* pm_val;                       /* n x 32 x {mean, stdev} */
+    uint32_t* pm_count;                  /* n */
 };
+
 
 /* global particle count: the N of every formula of the reference */
 static uint64_t NG(const or_filter* f) { return f->sharded ? f->n_global : f->n; }
@@ -530,6 +581,8 @@ static void or_free_particles(or_filter* f)
     free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob);
     free(f->floating); free(f->ncp); free(f->anc);
     free(f->dbg_ncp); free(f->dbg_cp); free(f->dbg_zdelta); free(f->dbg_zvar);
+    free(f->pm_key); free(f->pm_val); free(f->pm_count);
+    f->pm_key = NULL; f->pm_val = NULL; f->pm_count = NULL;
     f->x = f->y = f->th = f->z = f->zs = f->w = f->mprob = NULL;
     f->floating = f->ncp = NULL;
     f->anc = NULL;
@@ -551,6 +604,12 @@ static int or_alloc_particles(or_filter* f, uint64_t n)
         f->dbg_cp = calloc(b * ESLAM_MAX_CONTACTS, sizeof(or_cpoint));
         f->dbg_zdelta = calloc(b, 8); f->dbg_zvar = calloc(b, 8);
         if (!f->dbg_cp) return ESLAM_ERR_OUT_OF_MEMORY;
+    }
+    if (f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS) {      /* every particle's map: still empty */
+        f->pm_key = calloc(b * OR_STORE_SLOTS, 4);
+        f->pm_val = calloc(b * OR_STORE_SLOTS * 2, 4);
+        f->pm_count = calloc(b, 4);
+        if (!f->pm_key || !f->pm_val || !f->pm_count) return ESLAM_ERR_OUT_OF_MEMORY;
     }
     f->has_anc = 0;
     return f->x ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
@@ -1105,7 +1164,10 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         /* Translation3d(x, y, zPos) * AngleAxisd(theta, UnitZ) */
         double T[12] = {co, -s, 0.0, f->x[i], s, co, 0.0, f->y[i], 0.0, 0.0, r22, f->z[i]};
         const double meas_var = f->literal ? pow(f->zs[i], 2) + pow(c->measurement_error, 2) : f->zs[i] * f->zs[i] + me2;
-        int acc = or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
+        or_pmap pmc = {&f->map, f->pm_key ? f->pm_key + (uint64_t)i * OR_STORE_SLOTS : NULL,
+                       f->pm_val ? f->pm_val + (uint64_t)i * OR_STORE_SLOTS * 2 : NULL};
+        int acc = f->pm_key ? or_cm_evaluate_pose(&cm, T, meas_var, particle_map_fn, &pmc)
+                            : or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
         if (acc < 0) { zero_var = 1; acc = 0; }
         sw_val[i] = 0.0;
         if (acc) {
@@ -1281,6 +1343,19 @@ static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
     }
     free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob); free(f->floating); free(f->ncp);
     f->x = nx; f->y = ny; f->th = nt; f->z = nz; f->zs = ns; f->w = nw; f->mprob = nm; f->floating = nf; f->ncp = nc;
+    if (f->pm_key) {                      /* a copied particle carries its map (a deep copy) */
+        uint32_t* nk = malloc(samples * OR_STORE_SLOTS * 4);
+        float* nv = malloc(samples * OR_STORE_SLOTS * 8);
+        uint32_t* ncn = malloc(samples * 4);
+        for (uint64_t k = 0; k < samples; ++k) {
+            const uint32_t i = anc[k];
+            memcpy(nk + k * OR_STORE_SLOTS, f->pm_key + (uint64_t)i * OR_STORE_SLOTS, OR_STORE_SLOTS * 4);
+            memcpy(nv + k * OR_STORE_SLOTS * 2, f->pm_val + (uint64_t)i * OR_STORE_SLOTS * 2, OR_STORE_SLOTS * 8);
+            ncn[k] = f->pm_count[i];
+        }
+        free(f->pm_key); free(f->pm_val); free(f->pm_count);
+        f->pm_key = nk; f->pm_val = nv; f->pm_count = ncn;
+    }
 }
 
 /* shift: fixed-point shift of the contract-mode cumulative sum (device ctl->scan_shift) */
@@ -1670,6 +1745,93 @@ void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
     memcpy(f->ud_pose, st->ud_pose, sizeof(f->ud_pose));
     memcpy(f->libc.r, st->libc_rand, sizeof(st->libc_rand));
     f->libc.i = st->libc_rand_pos % 34u;
+}
+
+/* EmbodiedSlamFilter::processMap(scanMap, match = false, update = true)
+ * (src/EmbodiedSlamFilter.cpp:179-232) on per-particle maps: every scan patch at the
+ * particle's pose (scanFrame = Translation(x, y, 0) * Rz(theta), :186-189; the offset patch
+ * adds zPos and zSigma^2, :213-214) into the cell it lands in -- inserted into a cell empty
+ * in both the shared grid and the particle's map (test/testMap.cpp:307-316), fused
+ * (variance-weighted) with the particle's patch there when within 3 sigma, ignored on the
+ * shared grid's cells and when the particle already holds 24 patches.  (cloneMaps' copies
+ * are the deep copies of gather().)                                                       */
+int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
+{
+    if (!f->pm_key) return ESLAM_ERR_INVALID_ARG;
+    if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
+    const eslam_mls_grid* g = &f->map;
+    const double* A = g->global2local;
+    static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    int is_id = 1;
+    for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
+    for (uint64_t i = 0; i < f->n; ++i) {
+        uint32_t* key = f->pm_key + i * OR_STORE_SLOTS;
+        float* val = f->pm_val + i * OR_STORE_SLOTS * 2;
+        uint32_t count = f->pm_count[i];
+        double sn, co;
+        dm_sincos(f->th[i], &sn, &co);
+        const double zvar = f->zs[i] * f->zs[i];
+        for (uint32_t k = 0; k < m; ++k) {
+            const double wx = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[i];
+            const double wy = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[i];
+            const double wz = sp[k].position[2] + f->z[i];
+            double lx = wx, ly = wy;
+            if (!is_id) {
+                lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+                ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+            }
+            const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
+            const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
+            if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
+            const uint32_t cell = (uint32_t)fn * g->width + (uint32_t)fm;
+            if (g->cell_start[cell] != g->cell_start[cell + 1]) continue;
+            const double var = sp[k].stdev * sp[k].stdev + zvar;
+            uint32_t h = dm_store_hash(cell);
+            for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
+                if (key[h] == cell + 1u) {
+                    const double m1 = (double)val[2 * h], s1 = (double)val[2 * h + 1];
+                    const double v1 = s1 * s1, d = wz - m1;
+                    if (d * d <= 9.0 * (v1 + var)) {
+                        const double mm = (m1 * var + wz * v1) / (v1 + var);
+                        const double vv = (v1 * var) / (v1 + var);
+                        val[2 * h] = (float)mm;
+                        val[2 * h + 1] = (float)dm_sqrt(vv);
+                    }
+                    break;
+                }
+                if (key[h] == 0) {
+                    if (count < OR_STORE_CAP) {
+                        key[h] = cell + 1u;
+                        val[2 * h] = (float)wz;
+                        val[2 * h + 1] = (float)dm_sqrt(var);
+                        ++count;
+                    }
+                    break;
+                }
+                h = (h + 1u) & (OR_STORE_SLOTS - 1u);
+            }
+        }
+        f->pm_count[i] = count;
+    }
+    return 0;
+}
+
+/* particle i's own patches in slot order (cells, mean, stdev); returns how many it holds */
+uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* mean, float* stdev, uint32_t cap)
+{
+    if (!f->pm_key || i >= f->n) return 0;
+    uint32_t c = 0;
+    for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
+        const uint32_t k = f->pm_key[i * OR_STORE_SLOTS + t];
+        if (!k) continue;
+        if (c < cap) {
+            cells[c] = k - 1u;
+            mean[c] = f->pm_val[(i * OR_STORE_SLOTS + t) * 2];
+            stdev[c] = f->pm_val[(i * OR_STORE_SLOTS + t) * 2 + 1];
+        }
+        ++c;
+    }
+    return c;
 }
 
 int or_get_debug(or_filter* f, uint32_t* ncp, or_cpoint* cp, double* zdelta, double* zvar)

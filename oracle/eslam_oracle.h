@@ -142,6 +142,10 @@ void or_dm_libc_rand(uint32_t seed, uint32_t n, int32_t* out);     /* glibc rand
 double or_dm_limbs_to_double(const uint64_t L[4], int scale);
 void or_dm_fx128(double v, int scale, uint32_t limbs[4]);
 
+/* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): processMap's merge, and a particle's patches */
+int or_map_update(or_filter* f, const eslam_scan_patch* patches, uint32_t count);
+uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* mean, float* stdev, uint32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

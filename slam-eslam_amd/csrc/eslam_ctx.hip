@@ -23,7 +23,14 @@
 using namespace eslam_dev;
 
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
-                                                   const DebugRec* d, hipStream_t stream);
+                                                   const DebugRec* d, const MapStore* store, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
+                                             hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint64_t ndup,
+                                              hipStream_t stream);
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const MapStore* ms,
+                                             const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
                                                 eslam_particle_record* out, eslam_cpoint* cps, uint32_t max_cp,
@@ -43,7 +50,7 @@ extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uin
                                              void* tmp, size_t* tmp_bytes, hipStream_t stream);
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  const GatherView* gv, hipStream_t stream);
+                                                  const GatherView* gv, const MapStore* store, hipStream_t stream);
 extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
                                                 hipStream_t stream);
@@ -236,7 +243,12 @@ struct eslam_ctx {
     uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total
     uint32_t* anc = nullptr;
     bool has_anc = false;
+    // per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): the map stores and the copy-on-write scratch
+    MapStore store = {};
+    uint32_t* sid_mem = nullptr;             // 2 x cap: DevState::sid of both state buffers
+    uint32_t* cow = nullptr;                 // owner, counts, free and sharing lists + the copy count
     // logDebug records of the last update (ESLAM_FLAG_RECORD_CONTACTS / log_debug)
+    uint32_t last_map_copies = 0;            // stores copied by the last map update
     DebugRec dbg = {};
     uint64_t dbg_cap = 0;
     bool dbg_valid = false;
@@ -488,9 +500,19 @@ static void free_debug(eslam_ctx* ctx)
     ctx->dbg_valid = false;
 }
 
+static bool particle_maps(const eslam_ctx* ctx) { return (ctx->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS) != 0; }
+
+static const MapStore* store_of(const eslam_ctx* ctx) { return particle_maps(ctx) ? &ctx->store : nullptr; }
+
 static void free_particles(eslam_ctx* ctx)
 {
     free_debug(ctx);
+    (void)hipFree(ctx->store.key); (void)hipFree(ctx->store.val); (void)hipFree(ctx->store.count);
+    (void)hipFree(ctx->sid_mem); (void)hipFree(ctx->cow);
+    ctx->store = MapStore{};
+    ctx->sid_mem = nullptr;
+    ctx->cow = nullptr;
+    ctx->st[0].sid = ctx->st[1].sid = nullptr;
     (void)hipFree(ctx->state_mem); ctx->state_mem = nullptr;
     (void)hipFree(ctx->marks); ctx->marks = nullptr;
     (void)hipFree(ctx->tile_first); ctx->tile_first = nullptr;
@@ -565,6 +587,20 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
     if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
+    if (particle_maps(ctx)) {
+        // one store per particle; particle i starts with store i, empty (cloneMaps of a fresh
+        // filter over the shared map: every particle its own, still empty, local patches)
+        HIPCHK(ctx, hipMalloc(&ctx->sid_mem, 2 * cap * 4));
+        ctx->st[0].sid = ctx->sid_mem;
+        ctx->st[1].sid = ctx->sid_mem + cap;
+        HIPCHK(ctx, hipMalloc(&ctx->store.key, cap * kStoreSlots * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->store.val, cap * kStoreSlots * sizeof(float2)));
+        HIPCHK(ctx, hipMalloc(&ctx->store.count, cap * 4));
+        const uint64_t tiles = (cap + 2047) / 2048;
+        HIPCHK(ctx, hipMalloc(&ctx->cow, (3 * cap + 2 * tiles + 2 + 1) * 4));
+        HIPCHK(ctx, eslam_launch_store_init(ctx->st[0].sid, &ctx->store, cap, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
     ctx->n = n;
     ctx->cap = cap;
     if (ctx->sharded) {
@@ -1160,6 +1196,70 @@ extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64
 }
 
 // ---------------------------------------------------------------------------------------
+// per-particle local maps
+// ---------------------------------------------------------------------------------------
+extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count)
+{
+    if (!ctx || (!patches && count)) return ESLAM_ERR_INVALID_ARG;
+    if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update needs per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
+    if (ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "per-particle maps are kept on one GPU");
+    if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
+    if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
+    if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    int rc = materialize(ctx);
+    if (rc) return rc;
+    rc = read_ctl(ctx);                       // the current buffer (base ^ flip after the commit)
+    if (rc) return rc;
+    uint32_t* sid = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip].sid;
+    // cloneMaps (src/PoseEstimator.cpp:31-47): particles that share a store get private copies
+    uint32_t* ndup_dev = ctx->cow + 3 * ctx->cap + 2 * ((ctx->cap + 2047) / 2048) + 2;
+    HIPCHK(ctx, eslam_launch_store_cow(sid, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->stream));
+    uint32_t ndup = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&ndup, ndup_dev, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_copy(sid, &ctx->store, ctx->n, ctx->cow, ndup, ctx->stream));
+    MergeParams mp;
+    memset(&mp, 0, sizeof(mp));
+    mp.n = ctx->n;
+    mp.m = count;
+    for (uint32_t k = 0; k < count; ++k)
+        mp.sp[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
+    HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->store, &mp, ctx->stream));
+    ctx->last_map_copies = ndup;
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32_t* cells, float* mean, float* stdev,
+                                          uint32_t capacity, uint32_t* count)
+{
+    if (!ctx || !count) return ESLAM_ERR_INVALID_ARG;
+    if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "no per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
+    if (index >= ctx->n) return fail(ctx, ESLAM_ERR_INVALID_ARG, "particle index out of range");
+    int rc = materialize(ctx);
+    if (!rc) rc = read_ctl(ctx);
+    if (rc) return rc;
+    const uint32_t* sid = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip].sid;
+    uint32_t s = 0;
+    HIPCHK(ctx, hipMemcpy(&s, sid + index, 4, hipMemcpyDeviceToHost));
+    uint32_t key[kStoreSlots];
+    float2 val[kStoreSlots];
+    HIPCHK(ctx, hipMemcpy(key, ctx->store.key + (uint64_t)s * kStoreSlots, sizeof(key), hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(val, ctx->store.val + (uint64_t)s * kStoreSlots, sizeof(val), hipMemcpyDeviceToHost));
+    uint32_t c = 0;
+    for (uint32_t t = 0; t < kStoreSlots; ++t) {
+        if (!key[t]) continue;
+        if (c < capacity) {
+            if (cells) cells[c] = key[t] - 1u;
+            if (mean) mean[c] = val[t].x;
+            if (stdev) stdev[c] = val[t].y;
+        }
+        ++c;
+    }
+    *count = c;
+    return ESLAM_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // the hot path
 // ---------------------------------------------------------------------------------------
 // the pending resample gather (consumed by the next k_project_weight or materialised)
@@ -1537,13 +1637,19 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
         const uint64_t period = ctx->cfg.hash_period ? ctx->cfg.hash_period : 1;
         respawn = (ctx->hash_event++ % period) == 0;
     }
+    // per-particle maps: the resample gather is materialised (it carries the store names), so
+    // no k_project_weight consumes one
+    if (particle_maps(ctx)) {
+        const int rc = materialize(ctx);
+        if (rc) return rc;
+    }
     // logDebug records: the update's contact points are recorded on the projected state, so
     // the project runs as its own launch first (bit-identical to the fused kernel)
     const bool records = weight && record_contacts(ctx) && !ctx->sharded;
     if (respawn || (records && project)) {
         const GatherView gv0 = gather_view(ctx);
         HIPCHK(ctx, eslam_launch_project_weight(1, 0, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                                ctx->shards, &gv0, ctx->stream));
+                                                ctx->shards, &gv0, nullptr, ctx->stream));
         HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
         ctx->proj_event++;
         if (gv0.record) ctx->has_anc = true;
@@ -1565,12 +1671,13 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
             ctx->dbg.maxc = maxc;
             ctx->dbg_cap = ctx->cap;
         }
-        HIPCHK(ctx, eslam_launch_contact_records(ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl, &ctx->dbg, ctx->stream));
+        HIPCHK(ctx, eslam_launch_contact_records(ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl, &ctx->dbg, store_of(ctx),
+                                                 ctx->stream));
     }
     rec(ctx, 0);
     const GatherView gv = gather_view(ctx);
     HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                            ctx->shards, &gv, ctx->stream));
+                                            ctx->shards, &gv, store_of(ctx), ctx->stream));
     rec(ctx, 1);
     if (project) ctx->proj_event++;
     if (gv.record) ctx->has_anc = true;

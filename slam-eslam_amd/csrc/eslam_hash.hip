@@ -7,7 +7,7 @@
 //   k_hash_keys + radix sort + k_hash_replace
 //                     PoseEstimator::sampleFromHash  src/PoseEstimator.cpp:130-182: the
 //                     replace_count lowest (float weight, index) pairs get hash poses
-//   k_radix_hist / k_radix_scan / k_radix_scatter
+//   k_radix_hist / (k_scan_excl) / k_radix_scatter
 //                     a stable LSD radix sort of (u32 key, u32 value) pairs, 8 bits per
 //                     pass: per-tile digit histograms, one exclusive scan in digit-major
 //                     order, and a scatter that ranks each tile's elements stably with
@@ -82,30 +82,6 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const uint32_t* __restric
     }
     __syncthreads();
     hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = s_cnt[threadIdx.x];
-}
-
-// exclusive prefix sum of m counts in place (one block: each thread a contiguous segment)
-__global__ void __launch_bounds__(1024) k_radix_scan(uint32_t* __restrict__ a, uint64_t m)
-{
-    __shared__ uint32_t s_sum[1024];
-    const uint64_t per = (m + 1023) / 1024;
-    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
-    uint32_t t = 0;
-    for (uint64_t i = lo; i < hi; ++i) t += a[i];
-    s_sum[threadIdx.x] = t;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {             // Hillis-Steele inclusive scan of the segment sums
-        const uint32_t v = threadIdx.x >= (uint32_t)o ? s_sum[threadIdx.x - o] : 0u;
-        __syncthreads();
-        s_sum[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = s_sum[threadIdx.x] - t;
-    for (uint64_t i = lo; i < hi; ++i) {
-        const uint32_t v = a[i];
-        a[i] = run;
-        run += v;
-    }
 }
 
 // tile b's elements to their sorted positions: offs[d * ntiles + b] (scanned histogram) +
@@ -237,6 +213,8 @@ using namespace eslam_dev;
 
 static uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
+extern "C" hipError_t eslam_launch_scan_excl(uint32_t* a, uint64_t m, hipStream_t stream);   // eslam_kernels.hip
+
 extern "C" hipError_t eslam_launch_hash_sweep(const dm_hash_grid* g, const double* pts, const double* orient, uint32_t steps,
                                               int32_t* out, hipStream_t stream)
 {
@@ -284,7 +262,7 @@ extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uin
         uint32_t* ko = (pass & 1) ? keys_out : tk;
         uint32_t* vo = (pass & 1) ? order : tv;
         hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kBlock), 0, stream, ki, n, 8 * pass, hist, ntiles);
-        hipLaunchKernelGGL(k_radix_scan, dim3(1), dim3(1024), 0, stream, hist, hist_words);
+        eslam_launch_scan_excl(hist, hist_words, stream);
         hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kBlock), 0, stream, ki, vi, ko, vo, n, 8 * pass, hist, ntiles);
         ki = ko;
         vi = vo;

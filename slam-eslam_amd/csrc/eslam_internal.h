@@ -77,6 +77,21 @@ enum FinMode : uint32_t {
 struct DevState {
     double* x; double* y; double* th; double* z; double* zs; double* w; double* mprob;
     uint8_t* flags;
+    uint32_t* sid;                       // per-particle maps only: the particle's map store
+};
+
+// Per-particle local maps (useSharedMap = false, ESLAM_FLAG_PARTICLE_MAPS): the shared grid
+// plus, per particle, a store of patches in cells the shared grid leaves empty.  A store is
+// kStoreSlots open-addressing slots (key = cell + 1, 0 = free; linear probing from
+// dm_store_hash(cell)) holding one patch {mean, stdev} each, at most kStoreCap of them.
+// Particles name their store (DevState::sid); the resample copies the name, and the next map
+// update gives every later copy of an ancestor a private copy of its store (copy on write).
+constexpr uint32_t kStoreSlots = 32;
+constexpr uint32_t kStoreCap = 24;
+struct MapStore {
+    uint32_t* key;                       // n stores x kStoreSlots
+    float2* val;                         // n stores x kStoreSlots: {mean, stdev}
+    uint32_t* count;                     // patches per store
 };
 
 // K1 reads the first 64 bytes (the lookup header) with one scalar load per lookup
@@ -156,6 +171,19 @@ struct K1Args {
     DevState s[2];
     Ctl* ctl;
     Shard* shards;
+    MapStore store;                      // per-particle maps (the DELTA instantiations only)
+};
+
+// one scan patch of a map update (the scan MLS of processMap, in the yaw-free body frame)
+struct ScanPatch {
+    double x, y, z, stdev;
+};
+constexpr int kMaxScanPatches = 64;
+struct MergeParams {
+    uint64_t n;
+    uint32_t m;                          // scan patches
+    uint32_t pad;
+    ScanPatch sp[kMaxScanPatches];
 };
 
 // logDebug records of the last update (k_contact_records), indexed by the particle's

@@ -301,9 +301,33 @@ __device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint
     return false;
 }
 
-// the map is K1Args::map, read by scalar loads (header: 64 bytes per lookup)
+// per-particle maps: the patch of a cell the shared grid leaves empty, from the particle's
+// store (K1Args::store), with the same 3-sigma gate as a grid patch
+__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double lz, double qv, double& mean, double& stdev)
+{
+    const su8 st = kl8(KOFF(store));                  // key, val, count
+    const gmem<const uint32_t>* key = kp<const uint32_t>(st, 0) + (uint64_t)sid * kStoreSlots;
+    const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
+                                      (uint64_t)sid * kStoreSlots;
+    uint32_t h = dm_store_hash(cell);
+    for (uint32_t t = 0; t < kStoreSlots; ++t) {
+        const uint32_t k = key[h];
+        if (k == cell + 1u) {
+            const uint64_t pf = val[h];
+            return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), __uint_as_float((uint32_t)(pf >> 32)), lz, qv, mean,
+                              stdev);
+        }
+        if (k == 0) return false;
+        h = (h + 1u) & (kStoreSlots - 1u);
+    }
+    return false;
+}
+
+// the map is K1Args::map, read by scalar loads (header: 64 bytes per lookup).  DELTA: the
+// particle's own map store answers for cells the shared grid leaves empty.
+template <bool DELTA = false>
 __device__ __forceinline__ bool get_patch(const Window& win, double px, double py, double pz, double qv, double& mean,
-                                          double& stdev)
+                                          double& stdev, uint32_t sid = 0)
 {
     const su16 h = kl16(KOFF(map));
     const uint32_t width = h[12], hcells = h[13], ident = h[14], has_height = h[15];
@@ -332,7 +356,12 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     mean = pm;
     stdev = ps;
     if (gate0) return true;
-    if (!in_grid || (in_win && wc.count <= 1)) return false;
+    if constexpr (DELTA) {
+        if (!in_grid || (in_win && wc.count == 1)) return false;
+        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, lz, qv, mean, stdev);
+    } else {
+        if (!in_grid || (in_win && wc.count <= 1)) return false;
+    }
     const gmem<const float>* height = has_height ? kp<const float>(kl2(KOFF(map.height)), 0) : nullptr;
     const gmem<const float2>* patch = kp<const float2>(h, 1);
     uint32_t b, e;
@@ -344,6 +373,9 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         const uint64_t cell = (uint64_t)in * width + (uint64_t)im;
         b = cell_start[cell];
         e = cell_start[cell + 1];
+        if constexpr (DELTA) {
+            if (b == e) return store_patch(sid, (uint32_t)cell, lz, qv, mean, stdev);
+        }
     }
     for (uint32_t k = b; k < e; ++k) {
         const uint64_t pf = reinterpret_cast<const gmem<const uint64_t>*>(patch)[k];   // float2 {mean, stdev}
@@ -451,9 +483,9 @@ __device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, 
 
 // MAXP: bound on the contact points found (group ends); BATCH: p.m <= MAXP contacts.
 // StepParams (p.*) and the contacts come from scalar loads of the kernel arguments.
-template <int MAXP, bool BATCH>
+template <int MAXP, bool BATCH, bool DELTA = false>
 __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, double s, double r22, double x, double y,
-                                                  double z, double meas_var PROF_PARAM)
+                                                  double z, double meas_var, uint32_t sid PROF_PARAM)
 {
     CMResult r;
     // pushed contact points.  BATCH: slot = index of the contact that closed the group, so
@@ -557,7 +589,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
         mean = 0.0; stdev = 0.05;
         return wx == wx;
 #else
-        return get_patch(win, wx, wy, wz, qv, mean, stdev);
+        return get_patch<DELTA>(win, wx, wy, wz, qv, mean, stdev, sid);
 #endif
     };
 
@@ -661,7 +693,7 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #define K1_BOX_MULLER dm_box_muller32
 #endif
 
-template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH>
+template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false>
 __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a)
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
@@ -807,7 +839,13 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             PROF(4);
             const double r22 = (1.0 - co) + co;
             const double meas_var = zs * zs + kd(kl2(KOFF(p.me2)), 0);
-            CMResult r = evaluate_pose<MAXP, BATCH>(win, co, s, r22, x, y, z, meas_var PROF_ARG);
+            uint32_t sid = 0;
+            if constexpr (DELTA) {
+                // per-particle maps: the host materialises every gather first, so particle i
+                // is at i; its store name sits next to the state (DevState::sid)
+                sid = kp<const uint32_t>(kl2(st_off + (uint32_t)offsetof(DevState, sid)), 0)[i];
+            }
+            CMResult r = evaluate_pose<MAXP, BATCH, DELTA>(win, co, s, r22, x, y, z, meas_var, sid PROF_ARG);
             if (meas_var == 0) {            // evaluatePose throws (src/ContactModel.cpp:122): no contact points
                 err = 1;
                 r.accepted = false;
@@ -999,6 +1037,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
 // y and the patch mean, :163-171), zdiff, zvar and prob = 1 (Q8).  One particle per thread,
 // map lookups through the global CSR (the same values as the LDS window).
 // ---------------------------------------------------------------------------------------
+template <bool DELTA>
 __global__ void __launch_bounds__(kBlock) k_contact_records(K1Args a, DebugRec d)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1041,7 +1080,7 @@ __global__ void __launch_bounds__(kBlock) k_contact_records(K1Args a, DebugRec d
             const double wz = ((c.zz + r22 * c.pz) + z) - a.p.radius;
             if (group_valid && c_eval) {
                 double mean = 0.0, stdev = 0.0;
-                if (get_patch(win, wx, wy, wz, meas_var, mean, stdev)) {
+                if (get_patch<DELTA>(win, wx, wy, wz, meas_var, mean, stdev, DELTA ? st.sid[i] : 0u)) {
                     const double zdiff = wz - mean;
                     const double zvar = stdev * stdev + meas_var;
                     if (!valid && c_end && ratio_surely_significant(zdiff, zvar, corr)) {
@@ -1118,6 +1157,189 @@ __global__ void __launch_bounds__(kBlock) k_pack_records(DevState s0, DevState s
     }
     r.n_cpoints = n;
     out[k] = r;
+}
+
+// exclusive prefix sum of m counts in place (one block: each thread a contiguous segment)
+__global__ void __launch_bounds__(1024) k_scan_excl(uint32_t* __restrict__ a, uint64_t m)
+{
+    __shared__ uint32_t s_sum[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    uint32_t t = 0;
+    for (uint64_t i = lo; i < hi; ++i) t += a[i];
+    s_sum[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {             // Hillis-Steele inclusive scan of the segment sums
+        const uint32_t v = threadIdx.x >= (uint32_t)o ? s_sum[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_sum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_sum[threadIdx.x] - t;
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t v = a[i];
+        a[i] = run;
+        run += v;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-particle local maps (useSharedMap = false): processMap's merge of a
+// scan into every particle's map (src/EmbodiedSlamFilter.cpp:179-232) and cloneMaps' "no two
+// particles share a map" (src/PoseEstimator.cpp:31-47) as copy on write of the map stores.
+// ---------------------------------------------------------------------------------------
+// fresh maps: particle i names store i, every store empty
+__global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ sid, MapStore ms, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    sid[i] = (uint32_t)i;
+    ms.count[i] = 0;
+    for (uint32_t t = 0; t < kStoreSlots; ++t) ms.key[i * kStoreSlots + t] = 0;
+}
+
+// owner[s] = the lowest particle naming store s (~0: no particle does, the store is free)
+__global__ void __launch_bounds__(kBlock) k_store_owner(const uint32_t* __restrict__ sid, uint64_t n, uint32_t* __restrict__ owner)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) atomicMin(&owner[sid[i]], (uint32_t)i);
+}
+
+// compaction, mode 0: free stores (no owner) in store order; mode 1: particles that share
+// their store with a lower particle, in particle order.  The two lists have equal length.
+__device__ __forceinline__ bool compact_pred(int mode, uint64_t i, const uint32_t* owner, const uint32_t* sid)
+{
+    return mode == 0 ? owner[i] == ~0u : owner[sid[i]] != (uint32_t)i;
+}
+
+constexpr int kCompactItems = 8;
+constexpr int kCompactTile = kBlock * kCompactItems;
+
+__global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, const uint32_t* __restrict__ owner,
+                                                          const uint32_t* __restrict__ sid, uint32_t* __restrict__ counts)
+{
+    __shared__ uint32_t s_w[kWaves];
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile;
+    uint32_t c = 0;
+    for (int r = 0; r < kCompactItems; ++r) {
+        const uint64_t i = base + (uint64_t)r * kBlock + threadIdx.x;
+        if (i < n && compact_pred(mode, i, owner, sid)) ++c;
+    }
+    c = wave_sum_u32(c);
+    if ((threadIdx.x & 63u) == 0) s_w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// offs: exclusive prefix of counts; each selected i goes to out[offs[b] + its rank in the tile]
+__global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, const uint32_t* __restrict__ owner,
+                                                          const uint32_t* __restrict__ sid, const uint32_t* __restrict__ offs,
+                                                          uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t s_w[kWaves];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactTile;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t run = offs[blockIdx.x];
+    for (int r = 0; r < kCompactItems; ++r) {       // rounds of 256 consecutive items, in order
+        const uint64_t i = base + (uint64_t)r * kBlock + threadIdx.x;
+        const bool sel = i < n && compact_pred(mode, i, owner, sid);
+        const uint64_t b = __ballot(sel);
+        if (lane == 0) s_w[wave] = (uint32_t)__popcll(b);
+        __syncthreads();
+        uint32_t pos = run + (uint32_t)__popcll(b & below);
+        for (uint32_t w = 0; w < wave; ++w) pos += s_w[w];
+        if (sel) out[pos] = (uint32_t)i;
+        run += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+    }
+}
+
+// copy on write: the j-th sharing particle takes the j-th free store, a copy of the one it
+// shared (one thread per slot)
+__global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
+                                                       uint64_t ndup, uint32_t* __restrict__ sid, MapStore ms)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= ndup * kStoreSlots) return;
+    const uint64_t j = t / kStoreSlots;
+    const uint32_t slot = (uint32_t)(t - j * kStoreSlots);
+    const uint32_t p = dups[j], from = sid[p], to = frees[j];
+    ms.key[(uint64_t)to * kStoreSlots + slot] = ms.key[(uint64_t)from * kStoreSlots + slot];
+    ms.val[(uint64_t)to * kStoreSlots + slot] = ms.val[(uint64_t)from * kStoreSlots + slot];
+    if (slot == 0) ms.count[to] = ms.count[from];
+}
+
+__global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
+                                                         uint64_t ndup, uint32_t* __restrict__ sid)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < ndup) sid[dups[j]] = frees[j];
+}
+
+// processMap(scanMap, match = false, update = true) per particle: every scan patch, placed at
+// the particle's pose (Translation(x, y, 0) * Rz(theta); the offset patch adds zPos and
+// zSigma^2, src/EmbodiedSlamFilter.cpp:186-189, 213-214), merges into a cell of its map.  The
+// shared grid's cells stay as they are; a cell it leaves empty gets the patch (the
+// insert-into-empty-cell rule of test/testMap.cpp:307-316) or, holding one already, fuses
+// with it when within 3 sigma (the MLS variance-weighted update; envire's merge is not in the
+// reference: parity unpinned).  A full store keeps its patches.
+__global__ void __launch_bounds__(kBlock) k_map_merge(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+                                                      MapStore ms, MergeParams mp)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= mp.n) return;
+    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
+    const uint32_t sid = st.sid[i];
+    uint32_t* key = ms.key + (uint64_t)sid * kStoreSlots;
+    float2* val = ms.val + (uint64_t)sid * kStoreSlots;
+    uint32_t count = ms.count[sid];
+    double sn, co;
+    dm_sincos(th, &sn, &co);
+    const double zvar = zs * zs;
+    for (uint32_t k = 0; k < mp.m; ++k) {
+        const ScanPatch sp = mp.sp[k];
+        const double wx = (co * sp.x + (-sn) * sp.y) + x;
+        const double wy = (sn * sp.x + co * sp.y) + y;
+        const double wz = sp.z + z;
+        double lx = wx, ly = wy;
+        if (!map.g2l_identity) {
+            const double* A = map.g2l;
+            lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+            ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+        }
+        const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+        const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+        if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
+        const uint32_t cell = (uint32_t)fn * map.width + (uint32_t)fm;
+        if (map.cell_start[cell] != map.cell_start[cell + 1]) continue;          // the shared grid has it
+        const double var = sp.stdev * sp.stdev + zvar;
+        uint32_t h = dm_store_hash(cell);
+        for (uint32_t t = 0; t < kStoreSlots; ++t) {
+            const uint32_t kk = key[h];
+            if (kk == cell + 1u) {
+                const double m1 = (double)val[h].x, s1 = (double)val[h].y;
+                const double v1 = s1 * s1, d = wz - m1;
+                if (d * d <= 9.0 * (v1 + var)) {
+                    const double m = (m1 * var + wz * v1) / (v1 + var);
+                    const double v = (v1 * var) / (v1 + var);
+                    val[h] = make_float2((float)m, (float)dm_sqrt(v));
+                }
+                break;
+            }
+            if (kk == 0) {
+                if (count < kStoreCap) {
+                    key[h] = cell + 1u;
+                    val[h] = make_float2((float)wz, (float)dm_sqrt(var));
+                    ++count;
+                }
+                break;
+            }
+            h = (h + 1u) & (kStoreSlots - 1u);
+        }
+    }
+    ms.count[sid] = count;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1925,6 +2147,7 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
             out.mprob[k] = in.mprob[i];
             out.flags[k] = in.flags[i];
         }
+        if (in.sid) out.sid[k] = in.sid[i];            // per-particle maps: the store's name
         if (gv.record) gv.anc[k] = (uint32_t)(gbase + i);
     }
 }
@@ -2105,7 +2328,7 @@ static uint32_t k1_grid(uint64_t chunks) { return (uint32_t)((chunks + kWaves - 
 
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  const GatherView* gv, hipStream_t stream)
+                                                  const GatherView* gv, const MapStore* store, hipStream_t stream)
 {
     const uint64_t csz = 64ull * p->J;
     const uint64_t chunks = (p->n + csz - 1) / csz;
@@ -2119,9 +2342,22 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     args.s[1] = s1;
     args.ctl = ctl;
     args.shards = shards;
+    memset(&args.store, 0, sizeof(args.store));
+    if (store) args.store = *store;
 #define ESLAM_LAUNCH(P, W, M, B)                                                                      \
     hipLaunchKernelGGL((k_project_weight<P, W, M, B>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
                        stream, args)
+#define ESLAM_LAUNCH_D(P, W, M, B)                                                                          \
+    hipLaunchKernelGGL((k_project_weight<P, W, M, B, true>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
+                       stream, args)
+    if (weight && store) {
+        // per-particle maps: the lookups fall back to the particle's store (every pending
+        // gather has been materialised by the host)
+        if (project) { if (p->m <= 4 && maxp <= 4) ESLAM_LAUNCH_D(true, true, 4, true); else ESLAM_LAUNCH_D(true, true, ESLAM_MAX_CONTACTS, false); }
+        else { if (p->m <= 4 && maxp <= 4) ESLAM_LAUNCH_D(false, true, 4, true); else ESLAM_LAUNCH_D(false, true, ESLAM_MAX_CONTACTS, false); }
+        return hipGetLastError();
+    }
+#undef ESLAM_LAUNCH_D
     // batched contact lookups when every contact fits the MAXP-sized arrays
     if (project && !weight) ESLAM_LAUNCH(true, false, 4, false);
     else if (!project && weight) {
@@ -2138,7 +2374,7 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
 }
 
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
-                                                   const DebugRec* d, hipStream_t stream)
+                                                   const DebugRec* d, const MapStore* store, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p->n + kBlock - 1) / kBlock);
     if (!blocks) return hipSuccess;
@@ -2149,7 +2385,9 @@ extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, con
     args.s[0] = s0;
     args.s[1] = s1;
     args.ctl = ctl;
-    hipLaunchKernelGGL(k_contact_records, dim3(blocks), dim3(kBlock), 16, stream, args, *d);
+    if (store) args.store = *store;
+    if (s0.sid) hipLaunchKernelGGL(k_contact_records<true>, dim3(blocks), dim3(kBlock), 16, stream, args, *d);
+    else hipLaunchKernelGGL(k_contact_records<false>, dim3(blocks), dim3(kBlock), 16, stream, args, *d);
     return hipGetLastError();
 }
 
@@ -2161,6 +2399,71 @@ extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const 
     if (!blocks) return hipSuccess;
     hipLaunchKernelGGL(k_pack_records, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, ctl, first, stride, count, gbase, anc,
                        *d, out, cps, max_cp);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_scan_excl(uint32_t* a, uint64_t m, hipStream_t stream)
+{
+    if (m) hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, stream, a, m);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, hipStream_t stream)
+{
+    if (n) hipLaunchKernelGGL(k_store_init, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, *ms, n);
+    return hipGetLastError();
+}
+
+// copy on write of the map stores (before a merge): owner, the free-store and the sharing-
+// particle lists (compactions), the copies, the renames.  scratch: owner (n) + counts and
+// offsets (2 x tiles) + frees (n) + dups (n) words.  *ndup_dev: the number of copies (device).
+extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
+                                             hipStream_t stream)
+{
+    if (!n) return hipSuccess;
+    const uint32_t tiles = (uint32_t)((n + kCompactTile - 1) / kCompactTile);
+    uint32_t* owner = scratch;
+    uint32_t* counts = owner + n;
+    uint32_t* frees = counts + 2ull * tiles + 2;
+    uint32_t* dups = frees + n;
+    const uint32_t nb = (uint32_t)((n + kBlock - 1) / kBlock);
+    hipError_t e = hipMemsetAsync(owner, 0xff, n * 4, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_store_owner, dim3(nb), dim3(kBlock), 0, stream, sid, n, owner);
+    for (int mode = 0; mode < 2; ++mode) {
+        uint32_t* c = counts + (uint64_t)mode * (tiles + 1);
+        hipLaunchKernelGGL(k_compact_count, dim3(tiles), dim3(kBlock), 0, stream, mode, n, owner, sid, c);
+        // exclusive prefix over tiles + 1 entries: entry tiles becomes the total
+        e = hipMemsetAsync(c + tiles, 0, 4, stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, stream, c, (uint64_t)tiles + 1);
+        hipLaunchKernelGGL(k_compact_write, dim3(tiles), dim3(kBlock), 0, stream, mode, n, owner, sid, c, mode == 0 ? frees : dups);
+    }
+    e = hipMemcpyAsync(ndup_dev, counts + (tiles + 1) + tiles, 4, hipMemcpyDeviceToDevice, stream);
+    return e != hipSuccess ? e : hipGetLastError();
+}
+
+// the copies and renames for ndup sharing particles (host-read count)
+extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint64_t ndup,
+                                              hipStream_t stream)
+{
+    if (!ndup) return hipSuccess;
+    const uint32_t tiles = (uint32_t)((n + kCompactTile - 1) / kCompactTile);
+    uint32_t* frees = scratch + n + 2ull * tiles + 2;
+    uint32_t* dups = frees + n;
+    const uint64_t slots = ndup * kStoreSlots;
+    hipLaunchKernelGGL(k_store_copy, dim3((uint32_t)((slots + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, dups, frees, ndup,
+                       sid, *ms);
+    hipLaunchKernelGGL(k_store_rename, dim3((uint32_t)((ndup + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, dups, frees, ndup,
+                       sid);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const MapStore* ms,
+                                             const MergeParams* mp, hipStream_t stream)
+{
+    if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, s0, s1,
+                                  ctl, *map, *ms, *mp);
     return hipGetLastError();
 }
 

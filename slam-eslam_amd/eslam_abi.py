@@ -22,6 +22,7 @@ FLAG_RECORD_ANCESTORS = 0x1
 FLAG_NO_MAP_LDS = 0x2
 FLAG_NO_AUX_GATHER = 0x4
 FLAG_RECORD_CONTACTS = 0x8
+FLAG_PARTICLE_MAPS = 0x10
 
 
 class Config(C.Structure):
@@ -106,6 +107,14 @@ class Particles(C.Structure):
         ("mprob", C.POINTER(C.c_double)),
         ("floating", C.POINTER(C.c_uint8)),
         ("n_contact_points", C.POINTER(C.c_uint8)),
+    ]
+
+
+class ScanPatch(C.Structure):
+    """eslam_scan_patch: one cell of the scan MLS merged by a map update"""
+    _fields_ = [
+        ("position", C.c_double * 3),
+        ("stdev", C.c_double),
     ]
 
 

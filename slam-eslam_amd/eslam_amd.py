@@ -62,6 +62,9 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_init_pose.argtypes = [vp, dp, dp]
     L.eslam_gpu_upload_particles.argtypes = [vp, C.c_uint64, C.POINTER(A.Particles)]
     L.eslam_gpu_download_particles.argtypes = [vp, C.POINTER(A.Particles)]
+    L.eslam_gpu_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
+    L.eslam_gpu_get_particle_map.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_float),
+                                             C.POINTER(C.c_float), C.c_uint32, C.POINTER(C.c_uint32)]
     L.eslam_gpu_download_records.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(A.ParticleRecord),
                                              C.POINTER(A.CPoint), C.c_uint32]
     L.eslam_gpu_particle_count.argtypes = [vp, C.POINTER(C.c_uint64)]
@@ -162,6 +165,22 @@ class GpuFilter:
         r = np.ctypeslib.as_array(recs)[:count].copy()
         c = np.ctypeslib.as_array(cps)[:count * max_cpoints].reshape(count, max_cpoints).copy() if max_cpoints else None
         return r, c
+
+    def map_update(self, patches):
+        """eslam_gpu_map_update: processMap's merge of a scan into every particle's map"""
+        self._check(self.L.eslam_gpu_map_update(self.h, patches, len(patches)))
+
+    def particle_map(self, i, cap=64):
+        """particle i's own patches: (cells, mean, stdev) in slot order"""
+        cells = np.zeros(cap, np.uint32)
+        mean = np.zeros(cap, np.float32)
+        sd = np.zeros(cap, np.float32)
+        c = C.c_uint32()
+        self._check(self.L.eslam_gpu_get_particle_map(self.h, i, cells.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                      mean.ctypes.data_as(C.POINTER(C.c_float)),
+                                                      sd.ctypes.data_as(C.POINTER(C.c_float)), cap, C.byref(c)))
+        k = min(c.value, cap)
+        return cells[:k], mean[:k], sd[:k]
 
     def count(self):
         n = C.c_uint64()

@@ -11,6 +11,9 @@ benchmarks and parity tests run on:
                stdev ~ U(0.02, 0.1), seed 7                               (config 5)
 * stream     : per step delta = (0.02 m, 0, 0.002 rad), Sigma = diag(1e-4, 1e-4, 1e-5),
                4 feet at (+-0.25, 0, -0.18), (+-0.25, -0.5, -0.18), contact 1, ungrouped.
+* mapping    : (config 5's per-particle local maps) the map without its cells beyond x0
+               (terrain the robot has not mapped yet) and a scan of the ground ahead of the
+               robot, 8 x 6 patches in the yaw-free body frame.
 """
 import math
 
@@ -110,3 +113,34 @@ def bench_config(cfg, n):
     cfg.measurement_threshold_distance = -1.0
     cfg.measurement_threshold_angle = -1.0
     return cfg
+
+
+def unmapped_beyond(grid, x0):
+    """The grid with no patches in the cells whose centre lies at x >= x0 (unmapped terrain)."""
+    w, h = grid.width, grid.height
+    xc = grid.offset[0] + (np.arange(w) + 0.5) * grid.scale[0]
+    keep_cell = np.tile(xc < x0, h)                              # cell n * w + m
+    counts = np.diff(grid.cell_start.astype(np.int64))
+    keep_patch = np.repeat(keep_cell, counts)
+    new_counts = np.where(keep_cell, counts, 0)
+    cell_start = np.zeros(w * h + 1, dtype=np.uint64)
+    np.cumsum(new_counts, out=cell_start[1:])
+    ph = None if grid.patch_height is None else grid.patch_height[keep_patch]
+    return GridArrays(w, h, grid.scale, grid.offset, cell_start.astype(np.uint32), grid.mean[keep_patch],
+                      grid.stdev[keep_patch], ph, grid.g2l)
+
+
+def scan_patches(nx=8, ny=6, x0=0.35, x1=0.95, y0=-0.7, y1=0.2, z=-0.18, stdev=0.03):
+    """A scan of the ground ahead: nx x ny patches (x, y, z, stdev) in the yaw-free body
+    frame (the cells of processMap's scan MLS), with a gentle height pattern."""
+    import eslam_abi as A
+    out = (A.ScanPatch * (nx * ny))()
+    k = 0
+    for i in range(nx):
+        for j in range(ny):
+            x = x0 + (x1 - x0) * i / max(nx - 1, 1)
+            y = y0 + (y1 - y0) * j / max(ny - 1, 1)
+            out[k].position[:] = [x, y, z + 0.01 * math.sin(3.0 * x + 2.0 * y)]
+            out[k].stdev = stdev
+            k += 1
+    return out

@@ -86,6 +86,10 @@ def lib():
     L.or_get_ancestors.argtypes = [vp, C.POINTER(C.c_uint32), C.c_uint64]
     L.or_get_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
     L.or_set_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
+    L.or_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
+    L.or_get_particle_map.restype = C.c_uint32
+    L.or_get_particle_map.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                      C.c_uint32]
     L.or_get_debug.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(CPoint), C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.or_cm_init.argtypes = [C.POINTER(ContactModelS), C.POINTER(A.Config)]
     L.or_cm_set_contact_points.argtypes = [C.POINTER(ContactModelS), C.c_uint32, C.POINTER(A.ContactPoint), C.POINTER(C.c_double)]
@@ -252,6 +256,19 @@ class OracleFilter:
 
     def set_rng_state(self, s):
         self.L.or_set_rng_state(self.h, C.byref(s))
+
+    def map_update(self, patches):
+        assert self.L.or_map_update(self.h, patches, len(patches)) == 0
+
+    def particle_map(self, i, cap=64):
+        cells = np.zeros(cap, np.uint32)
+        mean = np.zeros(cap, np.float32)
+        sd = np.zeros(cap, np.float32)
+        c = self.L.or_get_particle_map(self.h, i, cells.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       mean.ctypes.data_as(C.POINTER(C.c_float)), sd.ctypes.data_as(C.POINTER(C.c_float)),
+                                       cap)
+        k = min(c, cap)
+        return cells[:k], mean[:k], sd[:k]
 
     def debug(self):
         n = self.count()

@@ -70,7 +70,7 @@ def test_config_default_matches_reference_defaults(lib):
 STRUCTS = {"eslam_config": A.Config, "eslam_mls_grid": A.MlsGrid, "eslam_contact_point": A.ContactPoint,
            "eslam_step_input": A.StepInput, "eslam_particles": A.Particles, "eslam_update_info": A.UpdateInfo,
            "eslam_rng_state": A.RngState, "eslam_kernel_times": A.KernelTimes, "eslam_comm": A.Comm,
-           "eslam_cpoint": A.CPoint, "eslam_particle_record": A.ParticleRecord}
+           "eslam_cpoint": A.CPoint, "eslam_particle_record": A.ParticleRecord, "eslam_scan_patch": A.ScanPatch}
 
 
 def test_struct_layouts_match_ctypes(tmp_path):

@@ -1,0 +1,70 @@
+"""Per-particle local maps on the GPU (useSharedMap = false): every
+particle's map is the shared grid plus its own patches (eslam_gpu_map_update = processMap's
+merge, src/EmbodiedSlamFilter.cpp:179-232), copied on write after a resample (cloneMaps,
+src/PoseEstimator.cpp:31-47), read by the contact update.  Bit-exact against the oracle,
+which deep-copies every map at every resample: particles after every step and every
+particle's own patches.  Parity with the reference is pinned only by the insert-into-
+empty-cell rule (test/testMap.cpp:307-316); the fuse rule is the build's own."""
+import numpy as np
+import pytest
+
+import eslam_abi as A
+import oracle_ffi as O
+import synthetic as S
+from parity_util import assert_bit_identical
+
+pytestmark = pytest.mark.gpu
+
+
+def u32(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("terrain,n,records", [("flat", 600, False), ("rough", 5003, False), ("rough", 2048, True)])
+def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
+    if records:
+        cfg.flags |= A.FLAG_RECORD_CONTACTS
+    base = S.flat_map(cells=80) if terrain == "flat" else S.rough_map(cells=80)
+    grid = S.unmapped_beyond(base, 0.3)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    if records:
+        orc.set_debug(True)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    scan = S.scan_patches()
+    stream = S.step_stream(24, tilt=(terrain == "rough"))
+    for k, st in enumerate(stream):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+        gpu.sync()
+        assert_bit_identical(gpu.download(), orc.download(), f"{terrain} n={n} step {k}")
+        if k % 6 == 5:
+            for i in list(range(0, n, max(n // 40, 1))) + [n - 1]:
+                gc, gm, gs = gpu.particle_map(i)
+                oc, om, os_ = orc.particle_map(i)
+                go, oo = np.argsort(gc), np.argsort(oc)
+                assert np.array_equal(gc[go], oc[oo]), (k, i)
+                assert np.array_equal(u32(gm[go]), u32(om[oo])) and np.array_equal(u32(gs[go]), u32(os_[oo])), (k, i)
+    if records:
+        rec, cps = gpu.download_records(max_cpoints=4)
+        ncp, cp, _, _ = orc.debug()
+        anc = orc.ancestors().astype(np.int64)
+        assert np.array_equal(rec["n_cpoints"], ncp[anc])
+    # the front feet stand beyond x0 = 0.3 on cells only the scans mapped (on the rough map
+    # the rear feet's terrain and the flat scan disagree more often)
+    p = gpu.download()
+    assert np.mean(p.n_contact_points == 4) > (0.5 if terrain == "flat" else 0.1)
+
+
+def test_map_update_needs_the_flag(gpu_mod):
+    cfg = S.bench_config(A.default_config(), 100)
+    gpu = gpu_mod.GpuFilter(cfg)
+    gpu.set_map(S.flat_map(cells=50))
+    gpu.init_gaussian(100, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    with pytest.raises(gpu_mod.EslamError):
+        gpu.map_update(S.scan_patches())
