@@ -57,8 +57,9 @@ extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64
 extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* tile_sum,
                                                   uint64_t* total, hipStream_t stream);
-extern "C" hipError_t eslam_launch_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const uint64_t* tile_prefix,
-                                            uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream);
+extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl,
+                                                      uint64_t* tile_pub, uint32_t* marks, uint32_t* tile_first,
+                                                      const uint32_t* jt, hipStream_t stream);
 extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, uint64_t n, uint64_t gbase, Ctl* ctl,
                                                    const GatherView* gv, uint32_t aux, hipStream_t stream);
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
@@ -240,7 +241,9 @@ struct eslam_ctx {
     void* state_mem = nullptr;
     uint32_t* marks = nullptr;
     uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
-    uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total
+    uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total (sharded K3a), or
+                                            // one GPU: tag << 61 | total published by K3 (zeroed at allocation)
+    uint32_t scan_tag = 0;                  // the last K3 launch's tag (1..7)
     uint32_t* anc = nullptr;
     bool has_anc = false;
     // per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): the map stores and the copy-on-write scratch
@@ -585,6 +588,7 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
+    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, ntiles * 8));                  // tag 0: never published
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
     if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     if (particle_maps(ctx)) {
@@ -1504,10 +1508,10 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     const FinParams fp = fin_params(ctx, mode);
     HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
-    const ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, false);
-    HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, nullptr, ctx->stream));
-    HIPCHK(ctx, eslam_launch_segments(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->marks, ctx->tile_first,
-                                      ctx->jump, ctx->stream));
+    ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, false);
+    sp.tag = ctx->scan_tag = ctx->scan_tag % 7u + 1u;         // differs from the previous launch's
+    HIPCHK(ctx, eslam_launch_normalize_segments(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->marks,
+                                                ctx->tile_first, ctx->jump, ctx->stream));
     if (timed) rec(ctx, 3);
     // the gather itself is fused into the next k_project_weight (or materialize())
     if (timed) rec(ctx, 4);
@@ -1616,10 +1620,13 @@ static int take_update_error(eslam_ctx* ctx)
 {
     int rc = read_ctl(ctx);
     if (rc) return rc;
-    if (!(ctx->ctl_host->err & 1ull)) return ESLAM_OK;
+    const uint64_t err = ctx->ctl_host->err;
+    if (!(err & 5ull)) return ESLAM_OK;
     ctx->ctl_host->err = 0;
     rc = write_ctl(ctx);
     if (rc) return rc;
+    if (err & 4ull)    // K3 waited in vain for a preceding tile's total (never expected: see k_normalize_segments)
+        return fail(ctx, ESLAM_ERR_HIP, "resample scan: a preceding tile's total was not published in time");
     return fail(ctx, ESLAM_ERR_ZERO_MEAS_VAR, "using a zero measurement variance leads to singularities");
 }
 

@@ -219,8 +219,10 @@ struct ScanParams {
     uint32_t normalize;                  // divide by S
     uint32_t ntiles;
     uint32_t multi;                      // multi-GPU: tile prefixes + rank total, no marks
-    uint32_t items;                      // particles per thread of K3a/K3b: tile = kBlock * items
+    uint32_t items;                      // particles per thread of K3: tile = kBlock * items
                                          // (2, 4 or kScanItems; sharded: kScanItems)
+    uint32_t tag;                        // one GPU: this launch's tile-total tag (1..7, cycled per launch)
+    uint32_t pad;
 };
 
 constexpr int kMaxRanks = 16;

@@ -1555,11 +1555,24 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t fx_shift(double v, int shift) { return dm_fx_shift(v, shift); }
 
+// dm_fx_shift(q, shift) for 0 <= q <= 1 without branches: then sh = e - 1075 + shift <= 9
+// (shift <= 61), inside the general function's "m << sh" range, and q = +0 or subnormal
+// (e = 0) gives 0 as there
+__device__ __forceinline__ uint64_t fx_unit(double q, int shift)
+{
+    const uint64_t b = dm_bits(q);
+    const uint32_t e = (uint32_t)(b >> 52);
+    const uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
+    const int sh = (int)e - 1075 + shift;
+    const uint64_t r = sh >= 0 ? (m << (sh & 63)) : (m >> ((-sh) & 63));
+    return (e == 0u) | (sh <= -64) ? 0ull : r;
+}
+
 // T_k = fx((k + U_k) / N): both divisions as dm_div_recip (bit-identical to "/", checked by
-// tests/c/check_div.c); inv_N = 1.0 / N
+// tests/c/check_div.c); inv_N = 1.0 / N.  k < N < 2^32, so (k + U_k) / N <= 1.
 __device__ __forceinline__ uint64_t draw_fx(uint64_t k, uint32_t x, double dN, double inv_N, int shift)
 {
-    return fx_shift(dm_div_recip((double)k + dm_minstd_uniform_fast(x), dN, inv_N), shift);
+    return fx_unit(dm_div_recip((double)(uint32_t)k + dm_minstd_uniform_fast(x), dN, inv_N), shift);
 }
 
 __device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint32_t xs, int shift,
@@ -1795,6 +1808,12 @@ __global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ 
 // that are <= c, k* = floor(c N) (draws below k0 are <= c, draws above k* + 1 are > c).
 __device__ __forceinline__ uint64_t kstar_of(uint64_t c, uint64_t N, int shift)
 {
+    // c * N with N < 2^32 as two 32 x 32 -> 64 products: (hi << 32) + lo, and for shift >= 32
+    // (the update path: 60) the shift needs only hi + (lo >> 32) (< 2^62, no carry out)
+    if (shift >= 32) {
+        const uint64_t lo = (uint64_t)(uint32_t)c * (uint32_t)N, hi = (c >> 32) * (uint64_t)(uint32_t)N;
+        return (hi + (lo >> 32)) >> ((shift - 32) & 63);
+    }
     return (uint64_t)(((unsigned __int128)c * N) >> shift);
 }
 
@@ -1806,22 +1825,23 @@ __device__ __forceinline__ uint32_t window_of(uint64_t c, uint64_t N, int shift,
     const uint64_t kstar = kstar_of(c, N, shift);
     const uint64_t k0 = kstar >= 1 ? kstar - 1 : 0;
     if (k0 >= N) return 1u << 18;
-    uint32_t nd = 0;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) nd += (k0 + d <= kstar + 1 && k0 + d < N) ? 1u : 0u;
+    // draws k0 + d with k0 + d <= k* + 1 and k0 + d < N
+    const uint64_t room = N - k0;
+    uint32_t nd = kstar >= 1 ? 3u : 2u;
+    nd = room < (uint64_t)nd ? (uint32_t)room : nd;
     return (uint32_t)(k0 - dlo) | (nd << 16);
 }
 
-__device__ __forceinline__ uint32_t draws_le_chunk(uint32_t w, uint64_t c, const uint64_t* sT, uint64_t dlo, uint64_t q0,
-                                                   uint64_t q1)
+// rq0, rq1: the LDS chunk [q0, q1) relative to dlo (u32: the wave's draws span < 2^16)
+__device__ __forceinline__ uint32_t draws_le_chunk(uint32_t w, uint64_t c, const uint64_t* sT, uint32_t rq0, uint32_t rq1)
 {
-    const uint64_t k0 = dlo + (w & 0xffffu);
+    const uint32_t r0 = w & 0xffffu;
     const uint32_t nd = (w >> 16) & 3u;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        const uint64_t k = k0 + d;
-        const bool in = (uint32_t)d < nd && k >= q0 && k < q1;
-        const uint64_t t = sT[in ? k - q0 : 0];             // slot 0 is in LDS; used only when in
+        const uint32_t r = r0 + (uint32_t)d;
+        const bool in = ((uint32_t)d < nd) & (r >= rq0) & (r < rq1);
+        const uint64_t t = sT[in ? r - rq0 : 0u];           // slot 0 is in LDS; used only when in
         w |= (in && t <= c) ? 1u << (19 + d) : 0u;
     }
     return w;
@@ -1837,25 +1857,123 @@ __device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, 
     return k0 + lead;
 }
 
-// K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs
-template <int ITEMS>
-__global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
-                                                     const uint64_t* __restrict__ tile_sum, uint32_t* __restrict__ marks,
-                                                     uint32_t* __restrict__ tile_first, const uint32_t* __restrict__ jt)
+// ---------------------------------------------------------------------------------------
+// K3 (one GPU): phase B + normalisation, the tile's exact fixed-point total, the prefix of
+// the preceding tiles and the segment marks, in one pass.  Each tile publishes its total as
+// one 64-bit word, tag << 61 | total (fixed point < 2^61: the weights are normalised with
+// shift 60, or scaled below 2^61 by k_finalize's shift for a standalone resample); the host
+// cycles the tag per launch and every launch writes every tile's word, so a word still
+// holding the previous launch's value never carries the current tag.  A tile sums its
+// predecessors' words (exact integers, any order), waiting for those not yet published.
+// The wait needs only that a tile's predecessors get scheduled: workgroups are dispatched in
+// order (per XCD), and a predecessor publishes before it waits on anything itself.  A
+// bounded spin turns a violated assumption into ctl->err bit 2 instead of a hang.
+// ---------------------------------------------------------------------------------------
+constexpr uint64_t kPubMask = (1ull << 61) - 1;
+constexpr uint32_t kPubSpinLimit = 1u << 18;       // x s_sleep(8) (512 clocks): ~60 ms
+
+// sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
+// them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
+// polls (light on the memory system the tiles it waits for are still streaming through);
+// the other waves wait at the barrier.
+__device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, uint32_t tag,
+                                                     uint64_t* s_red, Ctl* __restrict__ ctl)
 {
-    __shared__ uint64_t s_wtot[kWaves];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) {
+        uint64_t acc = 0;
+        bool timeout = false;
+        for (uint32_t b0 = 0; b0 < count; b0 += 8u * 64u) {
+            uint64_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                v[q] = k < count ? atomic_load_agent(pub + k) : ((uint64_t)tag << 61);
+            }
+            uint32_t spins = 0;
+            for (;;) {
+                bool ready = true;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
+                if (__ballot(!ready) == 0ull) break;
+                if (++spins == kPubSpinLimit) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                    if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
+        }
+        if (timeout && tid == 0) atomicOr((unsigned long long*)&ctl->err, 4ull);
+        acc = wave_sum_u64(acc);
+        if (tid == 0) s_red[0] = acc;
+    }
+    __syncthreads();
+    return s_red[0];
+}
+
+#ifdef ESLAM_K3_WAVES                    // experiment builds: waves per SIMD of the fused K3
+#define K3_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ESLAM_K3_WAVES, ESLAM_K3_WAVES)))
+#else
+#define K3_OCCUPANCY
+#endif
+
+template <int ITEMS>
+__global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+                                                               uint64_t* __restrict__ tile_pub, uint32_t* __restrict__ marks,
+                                                               uint32_t* __restrict__ tile_first,
+                                                               const uint32_t* __restrict__ jt)
+{
+    __shared__ uint64_t s_wtot[kWaves], s_red[kWaves];
     __shared__ K3bLds s_u;
-    if (!ctl->resample) return;
-    PROF_INIT();
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
+    const uint64_t tagw = (uint64_t)sp.tag << 61;
+    if (ctl->aborted) {                  // the update threw (k_finalize): weights stay as phase A left them
+        if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+        return;
+    }
+    PROF_INIT();
+    const bool resample = ctl->resample != 0;
     const DevState st = ctl->base ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
+    {
+        // phase B + normalisation, striped (coalesced); the values are staged in LDS for the
+        // blocked scan below
+        const double S = ctl->S;
+        const bool uniform = ctl->uniform != 0;
+        const double inv_n = ctl->inv_n;
+        double f[DM_NBUCKETS];
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const int k = r * kBlock + (int)tid;
-        const uint64_t i = t0 + (uint64_t)k;
-        s_u.v[skew(k)] = i < sp.n ? st.w[i] : 0.0;
+        for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const int k = r * kBlock + (int)tid;
+            const uint64_t i = t0 + (uint64_t)k;
+            double v = 0.0;
+            if (i < sp.n) {
+                v = st.w[i];
+                if (sp.phase_b) {
+                    const uint32_t ncp = st.flags[i] & 0x7fu;
+                    const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
+                    double fb = f[0];
+#pragma unroll
+                    for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
+                    const double factor = st.mprob[i] * fb;
+                    v *= factor;
+                }
+                if (sp.normalize) v = uniform ? inv_n : v / S;
+                if (sp.phase_b || sp.normalize) st.w[i] = v;
+            }
+            s_u.v[skew(k)] = v;
+        }
+    }
+    if (!resample) {
+        if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+        return;
     }
     __syncthreads();
     PROF(0);
@@ -1863,9 +1981,26 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
     uint64_t c[ITEMS];
     const uint64_t run = blocked_fx(s_u.v, shift, c);
     PROF(1);
-    const uint64_t tb = tiles_before(tile_sum, tile, s_wtot);
+    // in-tile exclusive prefix and the tile total (wave scans -> LDS)
+    uint64_t tincl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_up(tincl, o, 64);
+        if ((int)lane >= o) tincl += t;
+    }
+    if (lane == 63) s_wtot[wave] = tincl;
+    __syncthreads();                     // (s_u.v is dead after it)
+    uint64_t wexcl = 0, agg = 0;
+#pragma unroll
+    for (int wv = 0; wv < kWaves; ++wv) {
+        const uint64_t t = s_wtot[wv];
+        if ((uint32_t)wv < wave) wexcl += t;
+        agg += t;
+    }
+    if (tid == 0) atomic_store_agent(tile_pub + tile, tagw | (agg & kPubMask));
     PROF(2);
-    const uint64_t base = tb + block_excl(run, s_wtot);     // (syncs: s_u.v is dead after it)
+    const uint64_t tb = tiles_before_pub(tile_pub, tile, sp.tag, s_red, ctl);
+    const uint64_t base = tb + wexcl + (tincl - run);
     PROF(3);
 
     const uint64_t N = sp.n_global;
@@ -1911,7 +2046,8 @@ __global__ void __launch_bounds__(kBlock) k_segments(DevState s0, DevState s1, S
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
             for (int r = 0; r <= ITEMS; ++r)
-                win[r] = draws_le_chunk(win[r], r < ITEMS ? base + c[r] : wlo, sT, dlo, q0, q1);
+                win[r] = draws_le_chunk(win[r], r < ITEMS ? base + c[r] : wlo, sT, (uint32_t)(q0 - dlo),
+                                        (uint32_t)(q1 - dlo));
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2500,12 +2636,14 @@ extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, cons
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, const uint64_t* tile_prefix,
-                                            uint32_t* marks, uint32_t* tile_first, const uint32_t* jt, hipStream_t stream)
+extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl,
+                                                      uint64_t* tile_pub, uint32_t* marks, uint32_t* tile_first,
+                                                      const uint32_t* jt, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
-#define ESLAM_SEG(I) hipLaunchKernelGGL(k_segments<I>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_prefix, \
-                                        marks, tile_first, jt)
+    if (sp->tag < 1 || sp->tag > 7) return hipErrorInvalidValue;
+#define ESLAM_SEG(I) hipLaunchKernelGGL(k_normalize_segments<I>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, \
+                                        tile_pub, marks, tile_first, jt)
     switch (sp->items) {
     case 2: ESLAM_SEG(2); break;
     case 4: ESLAM_SEG(4); break;

@@ -42,9 +42,10 @@ for name, k in zip(NAMES, marks):
 print(f"total {tot / steps / (n / 64):.0f} clk per wave-row")
 print(f"ratio path: {buf[14] / steps:.0f} waves/step, {buf[15] / steps:.0f} lane-contacts/step of {n * 4} "
       f"(rows {n / 64:.0f})")
-K3 = ["load w", "blocked fx", "tiles_before", "block_excl", "seek", "advance", "sync", "flush marks"]
+K3 = ["load+normalize", "blocked fx", "scan+publish", "wait preds", "seek", "segments", "-", "flush marks"]
 tot3 = sum(buf[16 + k] for k in range(len(K3)))
-waves3 = n / 512
+items = 2 if n <= 512 * 1024 else (4 if n <= 2 * 1024 * 1024 else 8)     # scan_items() of eslam_ctx.hip
+waves3 = n / (64 * items)
 for k, name in enumerate(K3):
-    print(f"K3b {name:14s} {buf[16 + k] / max(tot3, 1) * 100:6.1f} %   {buf[16 + k] / steps / waves3:9.0f} clk/wave")
+    print(f"K3 {name:14s} {buf[16 + k] / max(tot3, 1) * 100:6.1f} %   {buf[16 + k] / steps / waves3:9.0f} clk/wave")
 f.close()
