@@ -1366,7 +1366,7 @@ static uint32_t scan_items(uint64_t n)
     static const int forced = [] {
         const char* e = getenv("ESLAM_SCAN_ITEMS");
         const int v = e ? atoi(e) : 0;
-        return (v == 2 || v == 4 || v == kScanItems) ? v : 0;
+        return (v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
     }();
     if (forced) return (uint32_t)forced;
     // measured (tools/ab_items.sh, bench step at 256k / 1M / 4M / 16M): 2 items +19 % at

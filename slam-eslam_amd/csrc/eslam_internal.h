@@ -25,7 +25,10 @@ constexpr int kRow = 64;                         // outputs per row_first entry 
 constexpr int kNShard = 16;              // statistics shards (blockIdx % kNShard)
 constexpr int kJumpBits = 11;
 constexpr int kStatsLds = 2048;          // bytes of the statistics scratch at the LDS base
-constexpr int kWindowLds = 38400;        // bytes of the MLS window after it (2400 cells: 40 KB per block with the stats, 4 blocks per CU)
+#ifndef ESLAM_WINDOW_LDS                 // experiment builds may shrink it
+#define ESLAM_WINDOW_LDS 38400
+#endif
+constexpr int kWindowLds = ESLAM_WINDOW_LDS;   // bytes of the MLS window after it (2400 cells: 40 KB per block with the stats, 4 blocks per CU)
 
 // one statistics shard: exact sums as 4 limbs of 32-bit columns (uint64 each)
 struct alignas(128) Shard {

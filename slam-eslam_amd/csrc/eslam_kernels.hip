@@ -444,17 +444,41 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
     const int wm0 = s_w[1], wn0 = s_w[3], wn1 = s_w[4], wcols = s_w[5];
     WinCell* cells = reinterpret_cast<WinCell*>(lds);
     const int ncell = (wn1 - wn0) * wcols;
-    for (int t = threadIdx.x; t < ncell; t += kBlock) {
-        const int r = t / wcols, c = t - r * wcols;
-        const uint64_t cell = (uint64_t)(wn0 + r) * m.width + (uint64_t)(wm0 + c);
-        const uint32_t b = m.cell_start[cell], e = m.cell_start[cell + 1];
-        WinCell wc;
-        wc.begin = b;
-        wc.count = e - b;
-        wc.mean0 = 0.0f;
-        wc.stdev0 = 0.0f;
-        if (e > b) { const float2 pf = m.patch[b]; wc.mean0 = pf.x; wc.stdev0 = pf.y; }
-        cells[t] = wc;
+    // two memory round trips per batch of kPer cells per thread: the batch's cell ranges
+    // first, then their first patches (a loop that waits per cell costs two round trips per
+    // cell); batches of 5 keep the prologue inside K1's register budget
+    constexpr int kPer = 5;
+    for (int t0 = 0; t0 < ncell; t0 += kPer * kBlock) {
+        uint32_t b[kPer], e[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int t = t0 + (int)threadIdx.x + q * kBlock;
+            b[q] = e[q] = 0;
+            if (t < ncell) {
+                const int r = t / wcols, c = t - r * wcols;
+                const uint64_t cell = (uint64_t)(wn0 + r) * m.width + (uint64_t)(wm0 + c);
+                b[q] = m.cell_start[cell];
+                e[q] = m.cell_start[cell + 1];
+            }
+        }
+        float2 pf[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            pf[q] = make_float2(0.0f, 0.0f);
+            if (e[q] > b[q]) pf[q] = m.patch[b[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int t = t0 + (int)threadIdx.x + q * kBlock;
+            if (t < ncell) {
+                WinCell wc;
+                wc.begin = b[q];
+                wc.count = e[q] - b[q];
+                wc.mean0 = pf[q].x;
+                wc.stdev0 = pf[q].y;
+                cells[t] = wc;
+            }
+        }
     }
     __syncthreads();
     w.on = 1;
@@ -1665,7 +1689,6 @@ __device__ __forceinline__ void mark_segment(uint32_t* __restrict__ marks, uint3
 // LDS staging of one scan tile: values in particle order, skewed by one slot every 32
 // doubles so both the striped writes and the blocked (8 per thread) reads are conflict-free
 constexpr int kSkew = 32;
-constexpr int kStageV = kScanTile + kScanTile / kSkew;
 
 __device__ __forceinline__ int skew(int k) { return k + k / kSkew; }
 
@@ -1682,14 +1705,17 @@ __device__ __forceinline__ uint64_t blocked_fx(const double* s_v, int shift, uin
     return run;
 }
 
-constexpr int kWaveDraws = 576;          // stratified draws one wave holds in LDS at a time (K3b)
-constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * kWaveDraws: per-target windows
+constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * wave_draws: per-target windows
 
-// K3b's LDS: the staged weights, then the wave's draws (the weights are dead before the
+// stratified draws one wave holds in LDS at a time: its particles' share plus a row of slack
+// (at least 576)
+template <int ITEMS> constexpr int wave_draws() { return 64 * ITEMS + 64 > 576 ? 64 * ITEMS + 64 : 576; }
+
+// K3's LDS: the staged weights, then the wave's draws (the weights are dead before the
 // draws are written)
-union K3bLds {
-    double v[kStageV];
-    uint64_t T[kWaves][kWaveDraws];
+template <int ITEMS> union K3Lds {
+    double v[kBlock * ITEMS + kBlock * ITEMS / kSkew];
+    uint64_t T[kWaves][wave_draws<ITEMS>()];
 };
 
 // Write the marks of the tile's segment starts (relative to the slice) and the row carries
@@ -1797,7 +1823,7 @@ __global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs.
 // Draw counting (#{k : T_k <= C}) for the particles of one wave: the counts of its targets
 // only read the draws [dlo, dhi) around floor(C N) of its first and last target.  Its lanes
-// evaluate those draws in parallel, kWaveDraws at a time (lane l: k = q0 + l + 64 j, one jump
+// evaluate those draws in parallel, wave_draws at a time (lane l: k = q0 + l + 64 j, one jump
 // then a 64-stride minstd step), store them in LDS, and every target reads the (at most
 // three) draws of its window there.  No per-lane serial walk, no search, no divergence.
 // Waves with more than kWaveChunks chunks of draws (heavy weights) evaluate each target's
@@ -1817,7 +1843,7 @@ __device__ __forceinline__ uint64_t kstar_of(uint64_t c, uint64_t N, int shift)
     return (uint64_t)(((unsigned __int128)c * N) >> shift);
 }
 
-// The window of target c as one word: bits 0..15 k0 - dlo (< kWaveChunks * kWaveDraws),
+// The window of target c as one word: bits 0..15 k0 - dlo (< kWaveChunks * wave_draws),
 // 16..17 the number of window draws (k0 + d <= k* + 1, < N), bit 18 "k0 >= N" (count N),
 // bits 19..21 set by draws_le_chunk: window draw d is <= c.
 __device__ __forceinline__ uint32_t window_of(uint64_t c, uint64_t N, int shift, uint64_t dlo)
@@ -1928,7 +1954,7 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
                                                                const uint32_t* __restrict__ jt)
 {
     __shared__ uint64_t s_wtot[kWaves], s_red[kWaves];
-    __shared__ K3bLds s_u;
+    __shared__ K3Lds<ITEMS> s_u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
@@ -2023,16 +2049,16 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
     const uint64_t dhi = ks_hi + 2 < N ? ks_hi + 2 : N;
     uint64_t hi_r[ITEMS];
     uint64_t lo;
-    if (dlo >= dhi || dhi - dlo <= (uint64_t)kWaveChunks * kWaveDraws) {
-        // draws in LDS, kWaveDraws at a time (one chunk unless the wave holds heavy weights);
+    if (dlo >= dhi || dhi - dlo <= (uint64_t)kWaveChunks * wave_draws<ITEMS>()) {
+        // draws in LDS, wave_draws at a time (one chunk unless the wave holds heavy weights);
         // le[r] bit d: draw k0_r + d of target r (r = ITEMS: wlo) is <= its target
         uint64_t* sT = s_u.T[wave];
         uint32_t win[ITEMS + 1];
 #pragma unroll
         for (int r = 0; r <= ITEMS; ++r) win[r] = window_of(r < ITEMS ? base + c[r] : wlo, N, shift, dlo);
         const uint32_t a64 = jt[64], a_lane = jt[lane];            // A^64, A^lane
-        for (uint64_t q0 = dlo; q0 < dhi; q0 += kWaveDraws) {
-            const uint64_t q1 = dhi - q0 < (uint64_t)kWaveDraws ? dhi : q0 + kWaveDraws;
+        for (uint64_t q0 = dlo; q0 < dhi; q0 += wave_draws<ITEMS>()) {
+            const uint64_t q1 = dhi - q0 < (uint64_t)wave_draws<ITEMS>() ? dhi : q0 + wave_draws<ITEMS>();
             if (q0 + lane < q1) {
                 uint32_t x = dm_mulmod31(dm_mulmod31(jump_pow(jt, q0 + 1), xs), a_lane);
 #pragma unroll 4
@@ -2116,7 +2142,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
                                                            uint2* __restrict__ range, uint64_t* __restrict__ first_last)
 {
     __shared__ uint64_t s_wtot[kWaves];
-    __shared__ K3bLds s_u;
+    __shared__ K3Lds<kScanItems> s_u;
     double* s_v = s_u.v;
     if (!ctl->resample) return;
     const uint32_t tid = threadIdx.x;
@@ -2647,7 +2673,8 @@ extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, 
     switch (sp->items) {
     case 2: ESLAM_SEG(2); break;
     case 4: ESLAM_SEG(4); break;
-    case kScanItems: ESLAM_SEG(kScanItems); break;
+    case 8: ESLAM_SEG(8); break;
+    case 16: ESLAM_SEG(16); break;
     default: return hipErrorInvalidValue;
     }
 #undef ESLAM_SEG

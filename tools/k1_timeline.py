@@ -46,11 +46,15 @@ occ = C.c_int(0)
 for lds in (-1, 0, 16384, 32768, 36864, 38912, 39936, 40448, 40960):
     lib.eslam_debug_k1_occupancy(C.byref(occ), lds)
     print("occupancy API: dynamic LDS", lds, "blocks per CU", occ.value)
-import torch
-p = torch.cuda.get_device_properties(0)
-print("shared mem per MP:", getattr(p, "shared_memory_per_multiprocessor", None), "per block:", getattr(p, "shared_memory_per_block", None),
+try:
+    import torch
+    p = torch.cuda.get_device_properties(0)
+except RuntimeError:
+    p = None
+if p is not None:
+    print("shared mem per MP:", getattr(p, "shared_memory_per_multiprocessor", None), "per block:", getattr(p, "shared_memory_per_block", None),
       "regs per MP:", getattr(p, "regs_per_multiprocessor", None), "MPs:", p.multi_processor_count)
-for a, b in ((0, 1), (1, 5), (0, 5)):
+for a, b in ((0, 1), (1, 5), (0, 5)):  # noqa: E305
     d = (t[:, b] - t[:, a]) / 100.0
     print(f"{names[a]:>12s} -> {names[b]:12s} median {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
 f.close()
