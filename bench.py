@@ -30,6 +30,7 @@ BYTES_K1 = 104                # gathered read 6 x f64 + write 6 x f64 + 4-byte m
 BYTES_K3 = 28                 # phase B / normalise read+write w (16), scan re-read (8), marks (4)
 BYTES_STEP = BYTES_K1 + BYTES_K3   # what the fused step moves per particle-update: the step roofline
 CONFIG3_GLOBAL = 16 * 1024 * 1024  # BASELINE configs[3]: 16M particles over 8 GPUs
+CONFIG4_GLOBAL = 64 * 1024 * 1024  # BASELINE configs[4]: 64M particles over 8 GPUs
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -43,13 +44,18 @@ def parse():
                          "-- 16M global at 8 GPUs -- on several)")
     ap.add_argument("--map-cells", type=int, default=1000)
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
+    ap.add_argument("--local-maps", action="store_true",
+                    help="configs[4]'s per-particle local maps (useSharedMap = false): rough terrain, unmapped "
+                         "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles (one "
+                         "GPU's share of 64M over 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (sharded, RCCL) path even on one rank (measures its overhead)")
     ap.add_argument("--comm", choices=["rccl", "torch"], default=os.environ.get("ESLAM_COMM", "rccl"),
                     help="multi-GPU exchanges: the library's own RCCL communicator, or torch.distributed callbacks")
-    ap.add_argument("--cpu-sample", type=int, default=1048576, help="particles in the CPU baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=48)
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="particles in the CPU baseline sample (default 1M; 256k with --local-maps)")
+    ap.add_argument("--cpu-steps", type=int, default=None, help="steps of the CPU baseline (default 48; 24 with --local-maps)")
     ap.add_argument("--cpu-threads", type=int, default=1,
                     help="OpenMP threads of the oracle's per-particle loops (1 = the reference default, "
                          "USE_OPENMP off; results are identical for any count)")
@@ -83,8 +89,11 @@ def pmc_traffic(kernel, n, map_cells):
     return None
 
 
-def workload_name(n, world, rough):
+def workload_name(n, world, rough, local_maps=False):
     """the BASELINE.json configuration a run corresponds to (per-GPU size, weak scaling)"""
+    if local_maps:
+        return ("configs[4] per GPU (%d of 64M particles over 8 GPUs)" % n) if n == CONFIG4_GLOBAL // 8 \
+            else "configs[4]-style per-particle maps"
     if rough:
         return "configs[4]-style terrain"
     if world == 1:
@@ -110,7 +119,7 @@ def host_cpu():
     return model, os.cpu_count()
 
 
-def cpu_baseline(args, grid):
+def cpu_baseline(args, grid, flags=0, scan=None):
     """The CPU oracle (a restatement of the reference path, reference-order double sums) on
     this host, on a bounded sample of the same workload: one thread by default (the
     reference's build default), --cpu-threads for its OpenMP per-particle loops."""
@@ -118,24 +127,30 @@ def cpu_baseline(args, grid):
     import oracle_ffi as O
     import synthetic as S
     n = args.cpu_sample
-    stream = S.step_stream(args.cpu_steps + 1)
+    stream = S.step_stream(args.cpu_steps + 1, tilt=scan is not None)
     cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= flags
     f = O.OracleFilter(cfg, O.SUM_REFERENCE)
     f.set_threads(args.cpu_threads)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
     f.step(stream[0])                     # first step (uniform reset) untimed
+    if scan is not None:
+        f.map_update(scan)
     t0 = time.perf_counter()
     k = 0
     for st in stream[1:1 + args.cpu_steps]:
         f.step(st)
+        if scan is not None:
+            f.map_update(scan)
         k += 1
     dt = time.perf_counter() - t0
     model, ncpu = host_cpu()
     return {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": args.cpu_threads, "kind": "port",
             "cpu_model": model, "host_logical_cpus": ncpu,
-            "sample": f"{n} particles x {k} steps of the same workload (flat map, forced update+resample), "
-                      f"oracle/eslam_oracle.c in reference-sum mode, {args.cpu_threads} thread(s), {dt:.1f} s"}
+            "sample": f"{n} particles x {k} steps of the same workload ({'rough map, per-particle maps + map update' if scan is not None else 'flat map'}"
+                      f", forced update+resample), oracle/eslam_oracle.c in reference-sum mode, "
+                      f"{args.cpu_threads} thread(s), {dt:.1f} s"}
 
 
 def spawn_ranks(args):
@@ -171,8 +186,20 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args)
+    if args.local_maps:
+        args.rough = True
+        if args.gpus != 1 or args.sharded:
+            sys.stderr.write("bench.py: --local-maps runs on one GPU (per-particle maps are not sharded)\n")
+            sys.exit(2)
+    if args.cpu_sample is None:
+        args.cpu_sample = 262144 if args.local_maps else 1048576
+    if args.cpu_steps is None:
+        args.cpu_steps = 24 if args.local_maps else 48
     if args.particles is None:
-        args.particles = 4 * 1024 * 1024 if args.gpus == 1 else CONFIG3_GLOBAL // 8
+        if args.local_maps:
+            args.particles = CONFIG4_GLOBAL // 8
+        else:
+            args.particles = 4 * 1024 * 1024 if args.gpus == 1 else CONFIG3_GLOBAL // 8
     # stdout carries exactly one JSON line: native libraries (RCCL prints a version banner
     # when a communicator is created) write to stderr until the result is printed
     sys.stdout.flush()
@@ -204,8 +231,14 @@ def main():
 
     n = args.particles
     grid = S.rough_map(cells=args.map_cells) if args.rough else S.flat_map(cells=args.map_cells)
-    stream = S.step_stream(args.warmup + 2 * args.steps + 1)
+    scan = None
+    if args.local_maps:
+        grid = S.unmapped_beyond(grid, 0.3)    # the front feet stand on cells only the scans map
+        scan = S.scan_patches()
+    stream = S.step_stream(args.warmup + 2 * args.steps + 1, tilt=args.local_maps)
     cfg = S.bench_config(A.default_config(), n * world)
+    if args.local_maps:
+        cfg.flags |= A.FLAG_PARTICLE_MAPS
     if sharded:
         # one global filter of n * world particles, sharded over the ranks: RCCL all_gathers
         # of the statistics / totals / counts and an all_to_all_v of the migrating particles
@@ -220,6 +253,16 @@ def main():
         f = eslam_amd.GpuFilter(cfg, device=0)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    if scan is not None:
+        step_one = f.step
+
+        def step_and_map(st):                  # EmbodiedSlamFilter::update + processMap(scan, update)
+            r = step_one(st)
+            f.map_update(scan)
+            return r
+        f_step = step_and_map
+    else:
+        f_step = f.step
 
     def barrier():
         f.sync()
@@ -229,13 +272,13 @@ def main():
             dist.barrier()
 
     for st in stream[:args.warmup]:
-        f.step(st)
+        f_step(st)
     barrier()
     # timed region: K steps back to back, no per-kernel events (HIP event records between
     # the launches cost ~10 % of a step here)
     t0 = time.perf_counter()
     for st in stream[args.warmup:args.warmup + args.steps]:
-        f.step(st)
+        f_step(st)
     info = f.sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -245,7 +288,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     for st in stream[args.warmup + args.steps:args.warmup + 2 * args.steps]:
-        f.step(st)
+        f_step(st)
     f.sync()
     barrier()
     dt_ev = time.perf_counter() - t1
@@ -279,12 +322,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (%s %gx%g m MLS map @0.1 m; odometry + 4 foot contacts per step)"
-                % ("rough multi-patch" if args.rough else "flat", args.map_cells / 10, args.map_cells / 10),
+        "data": "synthetic (%s %gx%g m MLS map @0.1 m; odometry + 4 foot contacts per step%s)"
+                % ("rough multi-patch" if args.rough else "flat", args.map_cells / 10, args.map_cells / 10,
+                   "; unmapped beyond x = 0.3 m, a %d-patch scan merged into every particle's map per step"
+                   % len(scan) if scan is not None else ""),
         "config": {"workload": "%s: %d particles/GPU, 1 MI355X per rank, %sMLS %dx%d @0.1 m, 4 contacts, "
-                               "resample forced every step" % (workload_name(n, world, args.rough), n,
-                                                               "rough " if args.rough else "", args.map_cells,
-                                                               args.map_cells),
+                               "resample forced every step%s" % (workload_name(n, world, args.rough, args.local_maps), n,
+                                                                 "rough " if args.rough else "", args.map_cells,
+                                                                 args.map_cells,
+                                                                 ", per-particle local maps + map update per step"
+                                                                 if args.local_maps else ""),
                    "particles_per_gpu": n, "global_particles": n * world,
                    "parallelism": "dp%d (particle shards%s)" % (world, (", sharded path, %s exchanges" % args.comm)
                                                                    if sharded else "")},
@@ -305,7 +352,7 @@ def main():
         "build_id": eslam_amd.build_id(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, grid)
+        result["cpu_baseline"] = cpu_baseline(args, grid, cfg.flags & A.FLAG_PARTICLE_MAPS, scan)
     sys.stdout.flush()
     os.dup2(json_fd, 1)
     if rank == 0:

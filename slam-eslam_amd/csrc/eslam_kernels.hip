@@ -1308,62 +1308,136 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 // insert-into-empty-cell rule of test/testMap.cpp:307-316) or, holding one already, fuses
 // with it when within 3 sigma (the MLS variance-weighted update; envire's merge is not in the
 // reference: parity unpinned).  A full store keeps its patches.
-__global__ void __launch_bounds__(kBlock) k_map_merge(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
-                                                      MapStore ms, MergeParams mp)
+// One wave merges the scan into the stores of its 64 particles.  The stores are staged in
+// LDS, transposed (slot-major, a padded row per slot: lane p's probes of any slots are
+// conflict-free), loaded and written back as whole contiguous stores (two 128-B key blocks /
+// two 256-B value blocks per wave instruction), so the 48-patch probe loop never touches
+// global memory for them; a thread-per-store loop over global memory thrashed L2 (each
+// in-flight lane keeps a 384-B store hot).
+constexpr int kMergeBlock = 128;                 // 2 waves: 48 KB of LDS, 3 blocks per CU
+constexpr int kMergePad = 65;
+__global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+                                                           MapStore ms, MergeParams mp)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= mp.n) return;
+    __shared__ uint32_t s_key[kMergeBlock / 64][kStoreSlots][kMergePad];
+    __shared__ float2 s_val[kMergeBlock / 64][kStoreSlots][kMergePad];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kMergeBlock + (uint64_t)w * 64u;
+    if (i0 >= mp.n) return;                       // wave-uniform
+    const uint64_t i = i0 + lane;
+    const bool valid = i < mp.n;
     const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
-    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
-    const uint32_t sid = st.sid[i];
-    uint32_t* key = ms.key + (uint64_t)sid * kStoreSlots;
-    float2* val = ms.val + (uint64_t)sid * kStoreSlots;
-    uint32_t count = ms.count[sid];
-    double sn, co;
-    dm_sincos(th, &sn, &co);
-    const double zvar = zs * zs;
-    for (uint32_t k = 0; k < mp.m; ++k) {
-        const ScanPatch sp = mp.sp[k];
-        const double wx = (co * sp.x + (-sn) * sp.y) + x;
-        const double wy = (sn * sp.x + co * sp.y) + y;
-        const double wz = sp.z + z;
-        double lx = wx, ly = wy;
-        if (!map.g2l_identity) {
-            const double* A = map.g2l;
-            lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-            ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+    const uint32_t sid = valid ? st.sid[i] : 0u;
+    // stage: two particles per wave instruction (lanes 0-31: particle 2q, 32-63: 2q + 1)
+    const uint32_t slot = lane & 31u, half = lane >> 5;
+    for (uint32_t q0 = 0; q0 < 32; q0 += 8) {              // 8 loads of each kind in flight
+        uint32_t kv[8];
+        float2 vv[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t pp = 2u * (q0 + q) + half;
+            const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
+            kv[q] = 0u;
+            vv[q] = make_float2(0.0f, 0.0f);
+            if (i0 + pp < mp.n) {
+                kv[q] = ms.key[(uint64_t)sp_ * kStoreSlots + slot];
+                vv[q] = ms.val[(uint64_t)sp_ * kStoreSlots + slot];
+            }
         }
-        const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
-        const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
-        if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
-        const uint32_t cell = (uint32_t)fn * map.width + (uint32_t)fm;
-        if (map.cell_start[cell] != map.cell_start[cell + 1]) continue;          // the shared grid has it
-        const double var = sp.stdev * sp.stdev + zvar;
-        uint32_t h = dm_store_hash(cell);
-        for (uint32_t t = 0; t < kStoreSlots; ++t) {
-            const uint32_t kk = key[h];
-            if (kk == cell + 1u) {
-                const double m1 = (double)val[h].x, s1 = (double)val[h].y;
-                const double v1 = s1 * s1, d = wz - m1;
-                if (d * d <= 9.0 * (v1 + var)) {
-                    const double m = (m1 * var + wz * v1) / (v1 + var);
-                    const double v = (v1 * var) / (v1 + var);
-                    val[h] = make_float2((float)m, (float)dm_sqrt(v));
-                }
-                break;
-            }
-            if (kk == 0) {
-                if (count < kStoreCap) {
-                    key[h] = cell + 1u;
-                    val[h] = make_float2((float)wz, (float)dm_sqrt(var));
-                    ++count;
-                }
-                break;
-            }
-            h = (h + 1u) & (kStoreSlots - 1u);
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t pp = 2u * (q0 + q) + half;
+            s_key[w][slot][pp] = kv[q];
+            s_val[w][slot][pp] = vv[q];
         }
     }
-    ms.count[sid] = count;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (valid) {
+        const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
+        uint32_t count = ms.count[sid];
+        const uint32_t count0 = count;
+        double sn, co;
+        dm_sincos(th, &sn, &co);
+        const double zvar = zs * zs;
+        // patches in groups of 8: the group's cells and their shared-grid ranges are loaded
+        // first (one memory latency per group, not per patch), then merged in patch order
+        constexpr uint32_t kGroup = 8;
+        for (uint32_t k0 = 0; k0 < mp.m; k0 += kGroup) {
+            uint32_t cellq[kGroup];
+            uint2 rng[kGroup];
+#pragma unroll
+            for (uint32_t q = 0; q < kGroup; ++q) {
+                cellq[q] = 0xffffffffu;
+                rng[q] = make_uint2(0u, 1u);
+                const uint32_t k = k0 + q;
+                if (k >= mp.m) continue;
+                const ScanPatch sp = mp.sp[k];
+                const double wx = (co * sp.x + (-sn) * sp.y) + x;
+                const double wy = (sn * sp.x + co * sp.y) + y;
+                const double wz = sp.z + z;
+                double lx = wx, ly = wy;
+                if (!map.g2l_identity) {
+                    const double* A = map.g2l;
+                    lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+                    ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                }
+                const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+                const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+                if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
+                const uint32_t cell = (uint32_t)fn * map.width + (uint32_t)fm;
+                cellq[q] = cell;
+                rng[q] = make_uint2(map.cell_start[cell], map.cell_start[cell + 1]);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kGroup; ++q) {
+                const uint32_t cell = cellq[q];
+                if (cell == 0xffffffffu || rng[q].x != rng[q].y) continue;   // off the grid / the shared grid has it
+                const ScanPatch sp = mp.sp[k0 + q];
+                const double wz = sp.z + z;
+                const double var = sp.stdev * sp.stdev + zvar;
+                uint32_t h = dm_store_hash(cell);
+                for (uint32_t t = 0; t < kStoreSlots; ++t) {
+                    const uint32_t kk = s_key[w][h][lane];
+                    if (kk == cell + 1u) {
+                        const float2 pv = s_val[w][h][lane];
+                        const double m1 = (double)pv.x, s1 = (double)pv.y;
+                        const double v1 = s1 * s1, d = wz - m1;
+                        if (d * d <= 9.0 * (v1 + var)) {
+                            const double m = (m1 * var + wz * v1) / (v1 + var);
+                            const double v = (v1 * var) / (v1 + var);
+                            s_val[w][h][lane] = make_float2((float)m, (float)dm_sqrt(v));
+                        }
+                        break;
+                    }
+                    if (kk == 0) {
+                        if (count < kStoreCap) {
+                            s_key[w][h][lane] = cell + 1u;
+                            s_val[w][h][lane] = make_float2((float)wz, (float)dm_sqrt(var));
+                            ++count;
+                        }
+                        break;
+                    }
+                    h = (h + 1u) & (kStoreSlots - 1u);
+                }
+            }
+        }
+        if (count != count0) ms.count[sid] = count;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // write back (a fuse changes only values; written whole, like the staging)
+#pragma unroll 4
+    for (uint32_t q = 0; q < 32; ++q) {
+        const uint32_t pp = 2u * q + half;
+        const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
+        if (i0 + pp < mp.n) {
+            ms.key[(uint64_t)sp_ * kStoreSlots + slot] = s_key[w][slot][pp];
+            ms.val[(uint64_t)sp_ * kStoreSlots + slot] = s_val[w][slot][pp];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2624,8 +2698,8 @@ extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms,
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream)
 {
-    if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, s0, s1,
-                                  ctl, *map, *ms, *mp);
+    if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kMergeBlock - 1) / kMergeBlock)), dim3(kMergeBlock), 0,
+                                  stream, s0, s1, ctl, *map, *ms, *mp);
     return hipGetLastError();
 }
 

@@ -68,3 +68,34 @@ def test_map_update_needs_the_flag(gpu_mod):
     gpu.init_gaussian(100, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
     with pytest.raises(gpu_mod.EslamError):
         gpu.map_update(S.scan_patches())
+
+
+def test_particle_maps_bench_workload(gpu_mod, oracle):
+    """bench.py --local-maps' workload (configs[4]'s terrain: rough multi-patch map, unmapped
+    beyond x = 0.3 m, tilted body, one map update per step) at 256k particles on the 1000 x
+    1000 map: bit-exact against the oracle (16 threads) for 4 steps, and the maps of sampled
+    particles equal."""
+    n = 262144
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS
+    grid = S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    orc.set_threads(16)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    scan = S.scan_patches()
+    for k, st in enumerate(S.step_stream(4, tilt=True)):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+    gpu.sync()
+    assert_bit_identical(gpu.download(), orc.download(), "local maps 256k")
+    for i in [0, 1, 4097, n // 2, n - 1]:
+        gc, gm, gs = gpu.particle_map(i)
+        oc, om, os_ = orc.particle_map(i)
+        go, oo = np.argsort(gc), np.argsort(oc)
+        assert np.array_equal(gc[go], oc[oo]), i
+        assert np.array_equal(u32(gm[go]), u32(om[oo])) and np.array_equal(u32(gs[go]), u32(os_[oo])), i
+    assert np.mean(gpu.download().n_contact_points >= 2) > 0.1
