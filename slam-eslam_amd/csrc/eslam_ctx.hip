@@ -1251,7 +1251,7 @@ extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32
     HIPCHK(ctx, hipMemcpy(val, ctx->store.val + (uint64_t)s * kStoreSlots, sizeof(val), hipMemcpyDeviceToHost));
     uint32_t c = 0;
     for (uint32_t t = 0; t < kStoreSlots; ++t) {
-        if (!key[t]) continue;
+        if (key[t] == kStoreFree) continue;
         if (c < capacity) {
             if (cells) cells[c] = key[t] - 1u;
             if (mean) mean[c] = val[t].x;

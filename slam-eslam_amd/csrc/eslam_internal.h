@@ -85,12 +85,16 @@ struct DevState {
 
 // Per-particle local maps (useSharedMap = false, ESLAM_FLAG_PARTICLE_MAPS): the shared grid
 // plus, per particle, a store of patches in cells the shared grid leaves empty.  A store is
-// kStoreSlots open-addressing slots (key = cell + 1, 0 = free; linear probing from
-// dm_store_hash(cell)) holding one patch {mean, stdev} each, at most kStoreCap of them.
+// kStoreSlots slots holding one patch {mean, stdev} each, at most kStoreCap of them, kept
+// sorted by key = cell + 1 (free slots, all after the used ones, hold kStoreFree): a lookup is
+// a 5-step binary search with no data-dependent trip count (the oracle's open-addressing
+// table holds the same set: membership and values do not depend on the layout).
 // Particles name their store (DevState::sid); the resample copies the name, and the next map
 // update gives every later copy of an ancestor a private copy of its store (copy on write).
 constexpr uint32_t kStoreSlots = 32;
 constexpr uint32_t kStoreCap = 24;
+constexpr uint32_t kStoreFree = 0xffffffffu;
+static_assert(kStoreSlots == 32 && kStoreCap < kStoreSlots, "store search: 5 halving steps, a free slot at the end");
 struct MapStore {
     uint32_t* key;                       // n stores x kStoreSlots
     float2* val;                         // n stores x kStoreSlots: {mean, stdev}

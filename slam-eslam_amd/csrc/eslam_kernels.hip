@@ -309,16 +309,14 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double 
     const gmem<const uint32_t>* key = kp<const uint32_t>(st, 0) + (uint64_t)sid * kStoreSlots;
     const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
                                       (uint64_t)sid * kStoreSlots;
-    uint32_t h = dm_store_hash(cell);
-    for (uint32_t t = 0; t < kStoreSlots; ++t) {
-        const uint32_t k = key[h];
-        if (k == cell + 1u) {
-            const uint64_t pf = val[h];
-            return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), __uint_as_float((uint32_t)(pf >> 32)), lz, qv, mean,
-                              stdev);
-        }
-        if (k == 0) return false;
-        h = (h + 1u) & (kStoreSlots - 1u);
+    const uint32_t target = cell + 1u;
+    uint32_t pos = 0;                                  // lower bound in the sorted keys
+#pragma unroll
+    for (uint32_t step = kStoreSlots / 2; step; step >>= 1) pos += key[pos + step - 1] < target ? step : 0u;
+    if (key[pos] == target) {
+        const uint64_t pf = val[pos];
+        return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), __uint_as_float((uint32_t)(pf >> 32)), lz, qv, mean,
+                          stdev);
     }
     return false;
 }
@@ -1219,7 +1217,7 @@ __global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ si
     if (i >= n) return;
     sid[i] = (uint32_t)i;
     ms.count[i] = 0;
-    for (uint32_t t = 0; t < kStoreSlots; ++t) ms.key[i * kStoreSlots + t] = 0;
+    for (uint32_t t = 0; t < kStoreSlots; ++t) ms.key[i * kStoreSlots + t] = kStoreFree;
 }
 
 // owner[s] = the lowest particle naming store s (~0: no particle does, the store is free)
@@ -1397,29 +1395,29 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 const ScanPatch sp = mp.sp[k0 + q];
                 const double wz = sp.z + z;
                 const double var = sp.stdev * sp.stdev + zvar;
-                uint32_t h = dm_store_hash(cell);
-                for (uint32_t t = 0; t < kStoreSlots; ++t) {
-                    const uint32_t kk = s_key[w][h][lane];
-                    if (kk == cell + 1u) {
-                        const float2 pv = s_val[w][h][lane];
-                        const double m1 = (double)pv.x, s1 = (double)pv.y;
-                        const double v1 = s1 * s1, d = wz - m1;
-                        if (d * d <= 9.0 * (v1 + var)) {
-                            const double m = (m1 * var + wz * v1) / (v1 + var);
-                            const double v = (v1 * var) / (v1 + var);
-                            s_val[w][h][lane] = make_float2((float)m, (float)dm_sqrt(v));
-                        }
-                        break;
+                const uint32_t target = cell + 1u;
+                uint32_t pos = 0;                      // lower bound in the sorted keys
+#pragma unroll
+                for (uint32_t step = kStoreSlots / 2; step; step >>= 1)
+                    pos += s_key[w][pos + step - 1][lane] < target ? step : 0u;
+                if (s_key[w][pos][lane] == target) {
+                    const float2 pv = s_val[w][pos][lane];
+                    const double m1 = (double)pv.x, s1 = (double)pv.y;
+                    const double v1 = s1 * s1, d = wz - m1;
+                    if (d * d <= 9.0 * (v1 + var)) {
+                        const double m = (m1 * var + wz * v1) / (v1 + var);
+                        const double v = (v1 * var) / (v1 + var);
+                        s_val[w][pos][lane] = make_float2((float)m, (float)dm_sqrt(v));
                     }
-                    if (kk == 0) {
-                        if (count < kStoreCap) {
-                            s_key[w][h][lane] = cell + 1u;
-                            s_val[w][h][lane] = make_float2((float)wz, (float)dm_sqrt(var));
-                            ++count;
-                        }
-                        break;
+                } else if (count < kStoreCap) {
+                    // insert at pos: shift the larger keys up one slot (count < kStoreCap < kStoreSlots)
+                    for (uint32_t t = count; t > pos; --t) {
+                        s_key[w][t][lane] = s_key[w][t - 1][lane];
+                        s_val[w][t][lane] = s_val[w][t - 1][lane];
                     }
-                    h = (h + 1u) & (kStoreSlots - 1u);
+                    s_key[w][pos][lane] = target;
+                    s_val[w][pos][lane] = make_float2((float)wz, (float)dm_sqrt(var));
+                    ++count;
                 }
             }
         }
