@@ -310,10 +310,19 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double 
     const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
                                       (uint64_t)sid * kStoreSlots;
     const uint32_t target = cell + 1u;
-    uint32_t pos = 0;                                  // lower bound in the sorted keys
+    // lower bound in the sorted keys in two memory round trips: the middle key picks the half,
+    // whose 16 keys come in four 16-byte loads
+    const uint32_t h0 = key[kStoreSlots / 2 - 1] < target ? kStoreSlots / 2 : 0u;
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const gmem<const u4>* kv = reinterpret_cast<const gmem<const u4>*>(key + h0);
+    uint32_t pos = h0, hit = 0;
 #pragma unroll
-    for (uint32_t step = kStoreSlots / 2; step; step >>= 1) pos += key[pos + step - 1] < target ? step : 0u;
-    if (key[pos] == target) {
+    for (int q = 0; q < 4; ++q) {
+        const u4 k4 = kv[q];
+        pos += (k4.x < target) + (k4.y < target) + (k4.z < target) + (k4.w < target);
+        hit |= (k4.x == target) | (k4.y == target) | (k4.z == target) | (k4.w == target);
+    }
+    if (hit) {
         const uint64_t pf = val[pos];
         return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), __uint_as_float((uint32_t)(pf >> 32)), lz, qv, mean,
                           stdev);
