@@ -208,6 +208,11 @@ typedef struct eslam_scan_patch {
     double stdev;                          /* sensor sigma of the patch                      */
 } eslam_scan_patch;
 int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);   /* count <= 64 */
+/* PoseEstimator::setEnvironment(env, map, useShared)  src/PoseEstimator.cpp:49-62: on = 1
+ * gives every particle its own map (ESLAM_FLAG_PARTICLE_MAPS), 0 the shared map only.  Before
+ * the particles are initialised (ESLAM_ERR_INVALID_ARG after); one GPU only
+ * (ESLAM_ERR_UNSUPPORTED on a sharded context).                                            */
+int eslam_gpu_set_particle_maps(eslam_ctx* ctx, int on);
 /* particle index's own patches (cell = n * width + m, mean, stdev); *count = how many it has */
 int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32_t* cells, float* mean, float* stdev,
                                uint32_t capacity, uint32_t* count);

@@ -540,6 +540,13 @@ private:
 // ---------------------------------------------------------------------------------------
 // PoseEstimator  src/PoseEstimator.hpp:120-134 (+ the ParticleFilter<T> members it inherits)
 // ---------------------------------------------------------------------------------------
+// one cell of the scan's MLS (the scanMap of processMap): position in the yaw-free body
+// frame, sensor sigma
+struct ScanPatch {
+    Vector3d position;
+    double stdev = 0.0;
+};
+
 struct SurfaceHash {                      // src/SurfaceHash.hpp:155-231: built on the device
     SurfaceHashConfig config;
     void setConfiguration(const SurfaceHashConfig& c) { config = c; }
@@ -561,14 +568,30 @@ public:
     PoseEstimator(const PoseEstimator&) = delete;
     PoseEstimator& operator=(const PoseEstimator&) = delete;
 
-    // setEnvironment(env, map, useShared)  src/PoseEstimator.cpp:31-62
+    // setEnvironment(env, map, useShared)  src/PoseEstimator.cpp:49-62: useShared = false gives
+    // every particle its own map (the shared grid plus its own patches; before init)
     void setEnvironment(const MlsGrid& env, bool useShared = true)
     {
-        if (!useShared) throw std::runtime_error("per-particle maps (useShared = false) are not supported by the MI355X filter");
         const eslam_mls_grid g = env.toC();
         check(ctx_, eslam_gpu_set_map(ctx_, &g));
+        check(ctx_, eslam_gpu_set_particle_maps(ctx_, useShared ? 0 : 1));
     }
-    void cloneMaps() {}                   // shared map: nothing to clone (src/PoseEstimator.cpp:31-47)
+    // cloneMaps  src/PoseEstimator.cpp:31-47: the copies a resample made share their ancestor's
+    // patches until the next map update gives each a private copy (copy on write), so there is
+    // nothing to do here
+    void cloneMaps() {}
+    // the merge half of EmbodiedSlamFilter::processMap(scanMap, match, update)
+    // (src/EmbodiedSlamFilter.cpp:179-232) for per-particle maps: the scan's patches in the
+    // yaw-free body frame, placed at every particle's pose
+    void updateMaps(const std::vector<ScanPatch>& scan)
+    {
+        std::vector<eslam_scan_patch> p(scan.size());
+        for (size_t k = 0; k < scan.size(); ++k) {
+            for (int i = 0; i < 3; ++i) p[k].position[i] = scan[k].position[i];
+            p[k].stdev = scan[k].stdev;
+        }
+        check(ctx_, eslam_gpu_map_update(ctx_, p.data(), (uint32_t)p.size()));
+    }
 
     // init(numParticles, hash)  src/PoseEstimator.cpp:75-86 (the hash is built on the device
     // from the environment's grid; the SurfaceHashConfig was given at construction)
@@ -768,9 +791,9 @@ public:
     void init(const MlsGrid& env, const Pose& pose, bool useSharedMap = true,
               const SurfaceHashConfig& hashConfig = SurfaceHashConfig())
     {
-        if (!useSharedMap) throw std::runtime_error("per-particle maps (useSharedMap = false) are not supported by the MI355X filter");
         filter_.reset(new PoseEstimator(odometry_, eslamConfig_, device_, hashConfig));
-        filter_->setEnvironment(env, true);
+        filter_->setEnvironment(env, useSharedMap);
+        sharedMap_ = useSharedMap;
         const double p[3] = {pose.position.x(), pose.position.y(), pose.position.z()};
         const double q[4] = {pose.orientation.w(), pose.orientation.x(), pose.orientation.y(), pose.orientation.z()};
         check(filter_->handle(), eslam_gpu_init_pose(filter_->handle(), p, q));
@@ -792,6 +815,16 @@ public:
         last_state_ = bs;
         last_orientation_ = orientation;
         return updated != 0;
+    }
+
+    // processMap(scanMap, match, update)  src/EmbodiedSlamFilter.cpp:179-232 with the scan's
+    // MLS as patches: update merges them into every particle's own map (useSharedMap = false;
+    // the reference's update-only call, src/EmbodiedSlamFilter.cpp:340-342); the visual match
+    // weighting (match = true, envire's MLSGrid::match) is not built
+    void processMap(const std::vector<ScanPatch>& scanMap, bool match, bool update)
+    {
+        if (match) throw std::runtime_error("processMap: the visual match update is not supported by the MI355X filter");
+        if (update && !sharedMap_) estimator().updateMaps(scanMap);
     }
 
     std::vector<PoseParticle>& getParticles() { return estimator().getParticles(); }
@@ -845,6 +878,7 @@ private:
     FootContact odometry_;
     int device_;
     Holder filter_;
+    bool sharedMap_ = true;
     uint64_t update_idx_ = 0;
     BodyContactState last_state_;
     Quaterniond last_orientation_;

@@ -1233,6 +1233,18 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     return ESLAM_OK;
 }
 
+extern "C" int eslam_gpu_set_particle_maps(eslam_ctx* ctx, int on)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    const bool cur = particle_maps(ctx);
+    if ((on != 0) == cur) return ESLAM_OK;
+    if (ctx->n) return fail(ctx, ESLAM_ERR_INVALID_ARG, "the map mode is chosen before the particles are initialised");
+    if (on && ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "per-particle maps are kept on one GPU");
+    if (on) ctx->cfg.flags |= ESLAM_FLAG_PARTICLE_MAPS;
+    else ctx->cfg.flags &= ~ESLAM_FLAG_PARTICLE_MAPS;
+    return ESLAM_OK;
+}
+
 extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32_t* cells, float* mean, float* stdev,
                                           uint32_t capacity, uint32_t* count)
 {

@@ -1321,13 +1321,14 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 // two 256-B value blocks per wave instruction), so the 48-patch probe loop never touches
 // global memory for them; a thread-per-store loop over global memory thrashed L2 (each
 // in-flight lane keeps a 384-B store hot).
-constexpr int kMergeBlock = 128;                 // 2 waves: 48 KB of LDS, 3 blocks per CU
+constexpr int kMergeBlock = 128;                 // 2 waves: 37 KB of LDS, 4 blocks per CU
 constexpr int kMergePad = 65;
 __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
                                                            MapStore ms, MergeParams mp)
 {
-    __shared__ uint32_t s_key[kMergeBlock / 64][kStoreSlots][kMergePad];
-    __shared__ float2 s_val[kMergeBlock / 64][kStoreSlots][kMergePad];
+    // only the kStoreCap slots that can be used are staged (the rest stay free in memory)
+    __shared__ uint32_t s_key[kMergeBlock / 64][kStoreCap][kMergePad];
+    __shared__ float2 s_val[kMergeBlock / 64][kStoreCap][kMergePad];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t i0 = (uint64_t)blockIdx.x * kMergeBlock + (uint64_t)w * 64u;
     if (i0 >= mp.n) return;                       // wave-uniform
@@ -1337,11 +1338,13 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     const uint32_t sid = valid ? st.sid[i] : 0u;
     // stage: two particles per wave instruction (lanes 0-31: particle 2q, 32-63: 2q + 1)
     const uint32_t slot = lane & 31u, half = lane >> 5;
-    for (uint32_t q0 = 0; q0 < 32; q0 += 8) {              // 8 loads of each kind in flight
-        uint32_t kv[8];
-        float2 vv[8];
+    // all 64 stores' loads in flight at once (96 VGPRs: LDS caps the kernel at 6 waves per CU,
+    // so a wave may hold up to 256)
+    for (uint32_t q0 = 0; q0 < 32; q0 += 32) {
+        uint32_t kv[32];
+        float2 vv[32];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
+        for (uint32_t q = 0; q < 32; ++q) {
             const uint32_t pp = 2u * (q0 + q) + half;
             const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
             kv[q] = 0u;
@@ -1352,10 +1355,12 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
             }
         }
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
+        for (uint32_t q = 0; q < 32; ++q) {
             const uint32_t pp = 2u * (q0 + q) + half;
-            s_key[w][slot][pp] = kv[q];
-            s_val[w][slot][pp] = vv[q];
+            if (slot < kStoreCap) {
+                s_key[w][slot][pp] = kv[q];
+                s_val[w][slot][pp] = vv[q];
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1368,9 +1373,9 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
         double sn, co;
         dm_sincos(th, &sn, &co);
         const double zvar = zs * zs;
-        // patches in groups of 8: the group's cells and their shared-grid ranges are loaded
+        // patches in groups of 24: the group's cells and their shared-grid ranges are loaded
         // first (one memory latency per group, not per patch), then merged in patch order
-        constexpr uint32_t kGroup = 8;
+        constexpr uint32_t kGroup = 24;
         for (uint32_t k0 = 0; k0 < mp.m; k0 += kGroup) {
             uint32_t cellq[kGroup];
             uint2 rng[kGroup];
@@ -1407,9 +1412,11 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 const uint32_t target = cell + 1u;
                 uint32_t pos = 0;                      // lower bound in the sorted keys
 #pragma unroll
-                for (uint32_t step = kStoreSlots / 2; step; step >>= 1)
-                    pos += s_key[w][pos + step - 1][lane] < target ? step : 0u;
-                if (s_key[w][pos][lane] == target) {
+                for (uint32_t step = kStoreSlots / 2; step; step >>= 1) {
+                    const uint32_t r = pos + step - 1;                // slots >= kStoreCap are free
+                    pos += (r < kStoreCap ? s_key[w][r < kStoreCap ? r : 0][lane] : kStoreFree) < target ? step : 0u;
+                }
+                if (pos < kStoreCap && s_key[w][pos][lane] == target) {
                     const float2 pv = s_val[w][pos][lane];
                     const double m1 = (double)pv.x, s1 = (double)pv.y;
                     const double v1 = s1 * s1, d = wz - m1;
@@ -1440,7 +1447,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     for (uint32_t q = 0; q < 32; ++q) {
         const uint32_t pp = 2u * q + half;
         const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
-        if (i0 + pp < mp.n) {
+        if (i0 + pp < mp.n && slot < kStoreCap) {
             ms.key[(uint64_t)sp_ * kStoreSlots + slot] = s_key[w][slot][pp];
             ms.val[(uint64_t)sp_ * kStoreSlots + slot] = s_val[w][slot][pp];
         }

@@ -63,6 +63,7 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_upload_particles.argtypes = [vp, C.c_uint64, C.POINTER(A.Particles)]
     L.eslam_gpu_download_particles.argtypes = [vp, C.POINTER(A.Particles)]
     L.eslam_gpu_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
+    L.eslam_gpu_set_particle_maps.argtypes = [vp, C.c_int]
     L.eslam_gpu_get_particle_map.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_float),
                                              C.POINTER(C.c_float), C.c_uint32, C.POINTER(C.c_uint32)]
     L.eslam_gpu_download_records.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(A.ParticleRecord),
@@ -165,6 +166,10 @@ class GpuFilter:
         r = np.ctypeslib.as_array(recs)[:count].copy()
         c = np.ctypeslib.as_array(cps)[:count * max_cpoints].reshape(count, max_cpoints).copy() if max_cpoints else None
         return r, c
+
+    def set_particle_maps(self, on=True):
+        """PoseEstimator::setEnvironment(..., useShared=not on) before init: per-particle maps"""
+        self._check(self.L.eslam_gpu_set_particle_maps(self.h, 1 if on else 0))
 
     def map_update(self, patches):
         """eslam_gpu_map_update: processMap's merge of a scan into every particle's map"""

@@ -243,6 +243,74 @@ int main()
         EXPECT(hf.getParticles().size() == 800, "hash filter steps");
     }
 
+    // ---- init(env, pose, false): per-particle maps, processMap(scanMap, false, true) ------
+    {
+        // the flat grid with no patches in the cells whose centre lies at x >= 0.3 m
+        eslam_ns::MlsGrid pm;
+        pm.width = pm.height = 200;
+        pm.scaleX = pm.scaleY = 0.1;
+        pm.offsetX = pm.offsetY = -10.0;
+        pm.cellStart.assign(200 * 200 + 1, 0);
+        for (uint32_t c = 0; c < 200u * 200u; ++c) {
+            const bool mapped = -10.0 + ((c % 200) + 0.5) * 0.1 < 0.3;
+            pm.cellStart[c + 1] = pm.cellStart[c] + (mapped ? 1u : 0u);
+            if (mapped) { pm.mean.push_back(0.0f); pm.stdev.push_back(0.05f); }
+        }
+        std::vector<eslam_ns::ScanPatch> scan;
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 4; ++j) {
+                eslam_ns::ScanPatch sp;
+                sp.position = eslam_ns::Vector3d(0.35 + 0.1 * i, -0.6 + 0.2 * j, -0.18);
+                sp.stdev = 0.03;
+                scan.push_back(sp);
+            }
+        eslam_ns::Configuration mc = eslamConfig;
+        mc.particleCount = 2000;
+        eslam_ns::EmbodiedSlamFilter mf(odometryConfig, mc);
+        mf.init(pm, startPose, false);
+        eslam_ns::FootContact odo(odometryConfig);
+        eslam_ns::PoseEstimator raw(odo, mc);
+        const eslam_mls_grid g = pm.toC();
+        EXPECT(eslam_gpu_set_map(raw.handle(), &g) == ESLAM_OK && eslam_gpu_set_particle_maps(raw.handle(), 1) == ESLAM_OK,
+               "raw: per-particle maps");
+        const double p0[3] = {0, 0, 0.18}, q0[4] = {1, 0, 0, 0};
+        EXPECT(eslam_gpu_init_pose(raw.handle(), p0, q0) == ESLAM_OK, "raw init");
+        EXPECT(eslam_gpu_set_particle_maps(raw.handle(), 0) != ESLAM_OK, "the map mode is fixed once initialised");
+        std::vector<eslam_scan_patch> rs(scan.size());
+        for (size_t k = 0; k < scan.size(); ++k) {
+            for (int i = 0; i < 3; ++i) rs[k].position[i] = scan[k].position[i];
+            rs[k].stdev = scan[k].stdev;
+        }
+        double mx = 0;
+        for (int s = 0; s < 6; ++s) {
+            mx += 0.02;
+            const eslam_ns::Affine3d T = body_pose(mx, 0, 0);
+            const eslam_ns::BodyContactState bs = body_state(mx, 0, 0);
+            mf.update(T, bs, terrainClassification);
+            mf.processMap(scan, false, true);
+            const eslam_ns::Quaterniond q(T.linear());
+            odo.update(bs, q);
+            const eslam_step_input in = raw.makeInput(bs, q, T.translation(), 0);
+            int u = 0;
+            EXPECT(eslam_gpu_step(raw.handle(), &in, &u) == ESLAM_OK, "raw step (maps)");
+            EXPECT(eslam_gpu_map_update(raw.handle(), rs.data(), (uint32_t)rs.size()) == ESLAM_OK, "raw map update");
+        }
+        std::vector<eslam_ns::PoseParticle>& a = mf.getParticles();
+        std::vector<eslam_ns::PoseParticle>& b = raw.getParticles();
+        size_t diff = a.size() != b.size();
+        for (size_t i = 0; i < a.size() && i < b.size(); ++i)
+            diff += std::memcmp(&a[i].position.v[0], &b[i].position.v[0], 16) || std::memcmp(&a[i].weight, &b[i].weight, 8) ||
+                    std::memcmp(&a[i].zPos, &b[i].zPos, 8) || std::memcmp(&a[i].zSigma, &b[i].zSigma, 8);
+        EXPECT(diff == 0, "per-particle maps: façade == raw ABI, bit for bit");
+        uint32_t cells[64], cnt = 0;
+        float mean[64], sd[64];
+        EXPECT(eslam_gpu_get_particle_map(mf.estimator().handle(), 0, cells, mean, sd, 64, &cnt) == ESLAM_OK && cnt > 0,
+               "particle 0 holds patches from the scans");
+        bool threw = false;
+        try { mf.processMap(scan, true, false); } catch (const std::runtime_error&) { threw = true; }
+        EXPECT(threw, "processMap(match = true) is not built: throws");
+    }
+
     // ---- one shard of a 3000-particle filter over the library's own RCCL communicator ----
     {
         eslam_ns::FootContact odo(odometryConfig);
