@@ -26,8 +26,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 BYTES_REFERENCE = 208         # the reference algorithm's passes: predict+weight 96, normalise 8,
                               # resample 104 (scan 8, gather 48, write 48) -- reported, not the roofline
 # per kernel as launched: the resample gather is fused into the next step's k_project_weight
-BYTES_K1 = 104                # gathered read 6 x f64 + write 6 x f64 + 4-byte mark read/clear
-BYTES_K3 = 28                 # phase B / normalise read+write w (16), scan re-read (8), marks (4)
+BYTES_K1 = 113                # gathered read x, y, th, z, zs, w (48) + write x, y, th, z, zs, w, mprob, flags (57)
+                              # + the 4-byte segment mark read and cleared (8)
+BYTES_K3 = 29                 # k_normalize_segments: read w, mprob, flags (17), write w (8), segment marks (4)
 BYTES_STEP = BYTES_K1 + BYTES_K3   # what the fused step moves per particle-update: the step roofline
 CONFIG3_GLOBAL = 16 * 1024 * 1024  # BASELINE configs[3]: 16M particles over 8 GPUs
 CONFIG4_GLOBAL = 64 * 1024 * 1024  # BASELINE configs[4]: 64M particles over 8 GPUs
@@ -62,10 +63,10 @@ def parse():
     return ap.parse_args()
 
 
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r01", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r02", "summary.json")
 
 
-def pmc_traffic(kernel, n, map_cells):
+def pmc_traffic(kernel, n, map_cells, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (tools/profile.sh -> profiles/<round>/summary.json: FETCH_SIZE x2 + WRITE_SIZE, the
     gfx950 correction of MI355X_MICROARCH.md), when they were taken on this workload."""
@@ -74,7 +75,7 @@ def pmc_traffic(kernel, n, map_cells):
             d = json.load(fh)
     except (OSError, ValueError):
         return None
-    if d.get("particles") != n or d.get("map_cells") != map_cells:
+    if d.get("particles") != n or d.get("map_cells") != map_cells or d.get("workload", "flat") != workload:
         return None
     for name, e in d.get("kernels", {}).items():
         if name.startswith(kernel) and "hbm_bytes_per_dispatch" in e:
@@ -305,11 +306,12 @@ def main():
 
     # roofline of the dominant kernel (HIP events around every launch of the timed region)
     per_kernel = {"k_project_weight": (kt["project_weight_ms"], BYTES_K1),
-                  "k_normalize_scan+k_segments": (kt["normalize_scan_ms"], BYTES_K3)}
+                  "k_normalize_segments": (kt["normalize_scan_ms"], BYTES_K3)}
     dom = max(per_kernel, key=lambda k: per_kernel[k][0])
     dom_ms, dom_bytes = per_kernel[dom]
     achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    traffic = pmc_traffic(dom, n, args.map_cells)
+    workload = "local-maps" if args.local_maps else ("rough" if args.rough else "flat")
+    traffic = pmc_traffic(dom, n, args.map_cells, workload) if not sharded else None
     result = {
         "metric": "M particle-updates/s (predict+weight+resample) @ 1/2/4/8 MI355X",
         "value": round(value, 3),

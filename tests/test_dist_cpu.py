@@ -23,6 +23,16 @@ def free_port():
 
 
 def launch(kind, name, n_global, world, tmp, mem="host", timeout=240):
+    """Run the ranks; a rendezvous port another process took between free_port() and the
+    bind (EADDRINUSE) is retried on a new port, at most twice (no GPU work has started)."""
+    for attempt in range(3):
+        res = _launch_once(kind, name, n_global, world, tmp, mem, timeout)
+        if res is not None:
+            return res
+    raise AssertionError("rendezvous port in use three times")
+
+
+def _launch_once(kind, name, n_global, world, tmp, mem, timeout):
     port = free_port()
     procs, outs = [], []
     for r in range(world):
@@ -41,6 +51,8 @@ def launch(kind, name, n_global, world, tmp, mem="host", timeout=240):
                 q.kill()
             raise
         logs.append(o.decode(errors="replace"))
+    if any(p.returncode != 0 for p in procs) and any("EADDRINUSE" in log for log in logs):
+        return None
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
     return [dict(np.load(o)) for o in outs]
