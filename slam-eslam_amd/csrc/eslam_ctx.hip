@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <string>
+#include <chrono>
 #include <vector>
 
 #include "eslam_internal.h"
@@ -1426,6 +1427,20 @@ static FinParams fin_params(eslam_ctx* ctx, uint32_t mode)
 //      while the host reads the totals and derives every rank's output range (the
 //      all_to_all_v sizes: one record per output that lands in another slice)
 //   -> pack -> all_to_all_v -> expand; the gather is fused into the next k_project_weight
+// a sharded step that fails after k_segments_multi has written own-slice segment marks:
+// the marks buffer must be all zero for the next gather (flush_marks stores only segment
+// starts) and no gather may stay pending on partial marks, so both are reset before the
+// error is returned (the filter keeps the pre-resample particles)
+static int abort_pending_gather(eslam_ctx* ctx, hipError_t e, int rc = ESLAM_ERR_HIP)
+{
+    if (e != hipSuccess) fail(ctx, ESLAM_ERR_HIP, (std::string("sharded resample: ") + hipGetErrorString(e)).c_str());
+    (void)hipMemsetAsync(ctx->marks, 0, ctx->cap * 4, ctx->stream);
+    (void)hipMemsetAsync(&ctx->ctl->flip, 0, sizeof(uint32_t), ctx->stream);
+    (void)hipMemsetAsync(&ctx->ctl->gather, 0, sizeof(uint32_t), ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
+    return rc;
+}
+
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const int G = ctx->comm.nranks, me = ctx->comm.rank;
@@ -1439,6 +1454,7 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     if (mode == FIN_SUM) return ESLAM_OK;
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, true);
     sp.multi = 1;
+    sp.tag = ctx->scan_tag = ctx->scan_tag % 7u + 1u;         // differs from the previous launch's
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->mg + mg::kTotal,
                                             ctx->stream));
     rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
@@ -1457,9 +1473,17 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     // wakes the thread tens of microseconds late, and the GPU runs dry before the next
     // step's launches if the host is late here (the segments kernel is all it has queued)
     {
+        // bounded: after ~200 us (a hung collective or kernel, or a late GPU) fall back to a
+        // blocking wait instead of burning a host core next to the RCCL proxy threads
         hipError_t q;
-        while ((q = hipEventQuery(ctx->ev[0])) == hipErrorNotReady) {}
-        HIPCHK(ctx, q);
+        const auto t0 = std::chrono::steady_clock::now();
+        while ((q = hipEventQuery(ctx->ev[0])) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+                q = hipEventSynchronize(ctx->ev[0]);
+                break;
+            }
+        }
+        if (q != hipSuccess) return abort_pending_gather(ctx, q);
     }
     const uint64_t c_resample = h[mg::kMirror];
     const uint32_t c_minstd_start = (uint32_t)h[mg::kMirror + 1];
@@ -1498,11 +1522,12 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
         if (any) {
             rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
             if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
-            if (rc) return rc;
-            HIPCHK(ctx, eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast, nsend,
-                                          ctx->sendbuf, ctx->stream));
+            if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
+            const hipError_t e = eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
+                                                   nsend, ctx->sendbuf, ctx->stream);
+            if (e != hipSuccess) return abort_pending_gather(ctx, e);
             rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
-            if (rc) return rc;
+            if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
         } else {
             nrecv = 0;
         }

@@ -1825,18 +1825,87 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
     }
 }
 
-// K3a: phase B + normalisation (striped, coalesced) and, when resampling, the tile's exact
-// fixed-point weight total.  K3b sums the totals of the tiles before its own (exact
-// integers, any order): no cross-tile waiting inside a kernel.
+constexpr uint64_t kPubMask = (1ull << 61) - 1;
+constexpr uint32_t kPubSpinLimit = 1u << 18;       // x s_sleep(8) (512 clocks): ~60 ms
+
+// sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
+// them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
+// polls (light on the memory system the tiles it waits for are still streaming through);
+// the other waves wait at the barrier.
+__device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, uint32_t tag,
+                                                     uint64_t* s_red, Ctl* __restrict__ ctl)
+{
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) {
+        uint64_t acc = 0;
+        bool timeout = false;
+        for (uint32_t b0 = 0; b0 < count; b0 += 8u * 64u) {
+            uint64_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                v[q] = k < count ? atomic_load_agent(pub + k) : ((uint64_t)tag << 61);
+            }
+            uint32_t spins = 0;
+            for (;;) {
+                bool ready = true;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
+                if (__ballot(!ready) == 0ull) break;
+                if (++spins == kPubSpinLimit) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                    if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
+        }
+        if (timeout && tid == 0) atomicOr((unsigned long long*)&ctl->err, 4ull);
+        acc = wave_sum_u64(acc);
+        if (tid == 0) s_red[0] = acc;
+    }
+    __syncthreads();
+    return s_red[0];
+}
+
+// sum of the first `count` tile totals of a finished K3a (one block, coalesced, any order:
+// exact integers; the words carry K3a's launch tag above bit 61)
+__device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ tile_sum, uint32_t count, uint64_t* s_wtot)
+{
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint64_t acc = 0;
+    for (uint32_t k = tid; k < count; k += kBlock) acc += tile_sum[k] & kPubMask;
+    acc = wave_sum_u64(acc);
+    if (lane == 0) s_wtot[wave] = acc;
+    __syncthreads();
+    uint64_t t = 0;
+#pragma unroll
+    for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
+    __syncthreads();                     // s_wtot is reused by the caller
+    return t;
+}
+
+// K3a (multi-GPU): phase B + normalisation (striped, coalesced) and, when resampling, the
+// tile's exact fixed-point weight total, published as tag << 61 | total like the one-GPU
+// K3's words (every launch writes every word).  The last tile waits for the others' words
+// and writes this slice's total (the value all-gathered before K3b), so no separate kernel
+// sums the tiles; K3b re-sums the words before its own tile (any order: exact integers).
 template <int ITEMS>
 __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                            uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total)
 {
-    __shared__ uint64_t s_wtot[kWaves];
+    __shared__ uint64_t s_wtot[kWaves], s_red[kWaves];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    if (ctl->aborted) return;            // the update threw (k_finalize): weights stay as phase A left them
-    const bool resample = ctl->resample != 0;
     const uint32_t tile = blockIdx.x;
+    const uint64_t tagw = (uint64_t)sp.tag << 61;
+    if (ctl->aborted) {                  // the update threw (k_finalize): weights stay as phase A left them
+        if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+        return;
+    }
+    const bool resample = ctl->resample != 0;
     const DevState st = ctl->base ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
     const double S = ctl->S;
@@ -1867,45 +1936,22 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
             fx_sum += fx_shift(v, shift);
         }
     }
-    if (!resample) return;
+    if (!resample) {
+        if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+        return;
+    }
 
     fx_sum = wave_sum_u64(fx_sum);
     if (lane == 0) s_wtot[wave] = fx_sum;
     __syncthreads();
-    if (tid == 0) {
-        uint64_t t = 0;
-        for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
-        tile_sum[tile] = t;
-    }
-}
-
-// sum of the first `count` tile totals (one block, coalesced, any order: exact integers)
-__device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ tile_sum, uint32_t count, uint64_t* s_wtot)
-{
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    uint64_t acc = 0;
-    for (uint32_t k = tid; k < count; k += kBlock) acc += tile_sum[k];
-    acc = wave_sum_u64(acc);
-    if (lane == 0) s_wtot[wave] = acc;
-    __syncthreads();
     uint64_t t = 0;
 #pragma unroll
     for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
-    __syncthreads();                     // s_wtot is reused by the caller
-    return t;
-}
-
-
-// multi-GPU: this slice's fixed-point total (the value all-gathered between K3a and K3b).
-// A separate one-block kernel: a last-block-done ticket in K3a serialised 2048 atomics on
-// one counter and cost 55 us (measured)
-__global__ void __launch_bounds__(kBlock) k_slice_total(const Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
-                                                        uint32_t ntiles, uint64_t* __restrict__ total)
-{
-    __shared__ uint64_t s_wtot[kWaves];
-    if (!ctl->resample) return;
-    const uint64_t t = tiles_before(tile_sum, ntiles, s_wtot);
-    if (threadIdx.x == 0) *total = t;
+    if (tid == 0) atomic_store_agent(tile_sum + tile, tagw | (t & kPubMask));
+    if (total && tile + 1 == sp.ntiles) {
+        const uint64_t before = tiles_before_pub(tile_sum, tile, sp.tag, s_red, ctl);
+        if (tid == 0) *total = before + t;
+    }
 }
 
 // K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs.
@@ -1983,52 +2029,6 @@ __device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, 
 // order (per XCD), and a predecessor publishes before it waits on anything itself.  A
 // bounded spin turns a violated assumption into ctl->err bit 2 instead of a hang.
 // ---------------------------------------------------------------------------------------
-constexpr uint64_t kPubMask = (1ull << 61) - 1;
-constexpr uint32_t kPubSpinLimit = 1u << 18;       // x s_sleep(8) (512 clocks): ~60 ms
-
-// sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
-// them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
-// polls (light on the memory system the tiles it waits for are still streaming through);
-// the other waves wait at the barrier.
-__device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, uint32_t tag,
-                                                     uint64_t* s_red, Ctl* __restrict__ ctl)
-{
-    const uint32_t tid = threadIdx.x;
-    if (tid < 64) {
-        uint64_t acc = 0;
-        bool timeout = false;
-        for (uint32_t b0 = 0; b0 < count; b0 += 8u * 64u) {
-            uint64_t v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t k = b0 + (uint32_t)q * 64u + tid;
-                v[q] = k < count ? atomic_load_agent(pub + k) : ((uint64_t)tag << 61);
-            }
-            uint32_t spins = 0;
-            for (;;) {
-                bool ready = true;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
-                if (__ballot(!ready) == 0ull) break;
-                if (++spins == kPubSpinLimit) { timeout = true; break; }
-                __builtin_amdgcn_s_sleep(8);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t k = b0 + (uint32_t)q * 64u + tid;
-                    if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
-        }
-        if (timeout && tid == 0) atomicOr((unsigned long long*)&ctl->err, 4ull);
-        acc = wave_sum_u64(acc);
-        if (tid == 0) s_red[0] = acc;
-    }
-    __syncthreads();
-    return s_red[0];
-}
-
 #ifdef ESLAM_K3_WAVES                    // experiment builds: waves per SIMD of the fused K3
 #define K3_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ESLAM_K3_WAVES, ESLAM_K3_WAVES)))
 #else
@@ -2738,6 +2738,7 @@ extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, cons
                                                   uint64_t* total, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
+    if (sp->tag < 1 || sp->tag > 7) return hipErrorInvalidValue;
     switch (sp->items) {
     case 2: hipLaunchKernelGGL(k_normalize_scan<2>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total); break;
     case 4: hipLaunchKernelGGL(k_normalize_scan<4>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total); break;
@@ -2746,7 +2747,6 @@ extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, cons
         break;
     default: return hipErrorInvalidValue;
     }
-    if (total) hipLaunchKernelGGL(k_slice_total, dim3(1), dim3(kBlock), 0, stream, ctl, tile_sum, sp->ntiles, total);
     return hipGetLastError();
 }
 
