@@ -47,8 +47,8 @@ def parse():
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
     ap.add_argument("--local-maps", action="store_true",
                     help="configs[4]'s per-particle local maps (useSharedMap = false): rough terrain, unmapped "
-                         "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles (one "
-                         "GPU's share of 64M over 8)")
+                         "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles per "
+                         "GPU (64M over 8 GPUs with --gpus 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (sharded, RCCL) path even on one rank (measures its overhead)")
@@ -93,8 +93,10 @@ def pmc_traffic(kernel, n, map_cells, workload):
 def workload_name(n, world, rough, local_maps=False):
     """the BASELINE.json configuration a run corresponds to (per-GPU size, weak scaling)"""
     if local_maps:
-        return ("configs[4] per GPU (%d of 64M particles over 8 GPUs)" % n) if n == CONFIG4_GLOBAL // 8 \
-            else "configs[4]-style per-particle maps"
+        if n * world == CONFIG4_GLOBAL:
+            return "configs[4]"
+        return ("configs[4]'s 8M-per-GPU shard (of 64M over 8 GPUs)%s" % (", weak-scaled to %d GPUs" % world if world > 1 else "")) \
+            if n == CONFIG4_GLOBAL // 8 else "configs[4]-style per-particle maps"
     if rough:
         return "configs[4]-style terrain"
     if world == 1:
@@ -189,9 +191,6 @@ def main():
         spawn_ranks(args)
     if args.local_maps:
         args.rough = True
-        if args.gpus != 1 or args.sharded:
-            sys.stderr.write("bench.py: --local-maps runs on one GPU (per-particle maps are not sharded)\n")
-            sys.exit(2)
     if args.cpu_sample is None:
         args.cpu_sample = 262144 if args.local_maps else 1048576
     if args.cpu_steps is None:

@@ -86,7 +86,7 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_NO_MAP_LDS 0x2u         /* disable the LDS map window (global lookups)   */
 #define ESLAM_FLAG_NO_AUX_GATHER 0x4u      /* do not carry mprob/floating through resample  */
 #define ESLAM_FLAG_PARTICLE_MAPS 0x10u     /* useSharedMap = false: every particle its own local
-                                              map (eslam_gpu_map_update); one GPU only       */
+                                              map (eslam_gpu_map_update)                      */
 #define ESLAM_FLAG_RECORD_CONTACTS 0x8u    /* keep every update's cpoints, meas_pos, meas_theta
                                               (also on with log_debug); one GPU only          */
 
@@ -210,8 +210,8 @@ typedef struct eslam_scan_patch {
 int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);   /* count <= 64 */
 /* PoseEstimator::setEnvironment(env, map, useShared)  src/PoseEstimator.cpp:49-62: on = 1
  * gives every particle its own map (ESLAM_FLAG_PARTICLE_MAPS), 0 the shared map only.  Before
- * the particles are initialised (ESLAM_ERR_INVALID_ARG after); one GPU only
- * (ESLAM_ERR_UNSUPPORTED on a sharded context).                                            */
+ * the particles are initialised (ESLAM_ERR_INVALID_ARG after).  On a sharded filter a
+ * particle that a resample moves to another rank carries its own patches.                 */
 int eslam_gpu_set_particle_maps(eslam_ctx* ctx, int on);
 /* particle index's own patches (cell = n * width + m, mean, stdev); *count = how many it has */
 int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32_t* cells, float* mean, float* stdev,
@@ -338,8 +338,9 @@ typedef struct eslam_comm {
  * of 64 * dm_chunk_rows(n_global) (the canonical summation chunk) except the last.
  * The context's config particle_count is the global count.  Sharded contexts support
  * the hot path (step/project/update/sync), init, upload/download of the local shard,
- * weights sum / normalise / resample and the best particle (global index); the centroid
- * returns ESLAM_ERR_UNSUPPORTED.  comm == NULL returns the context to one GPU.        */
+ * weights sum / normalise / resample, the best particle (global index), the centroid, the
+ * hash respawn and per-particle maps, each equal to one GPU bit for bit.  comm == NULL
+ * returns the context to one GPU.                                                      */
 int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase);
 
 /* ---- multi-GPU over RCCL, driven from the library (no callback into the host language) --

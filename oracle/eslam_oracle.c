@@ -1407,6 +1407,10 @@ typedef struct {
     double x, y, th, z, zs, w, mprob;
     uint64_t lo, hi, src;          /* global output range, global source index */
     uint8_t floating, ncp, pad[6];
+    /* per-particle maps: the source particle's own patches travel with it (a deep copy) */
+    uint32_t pm_count, pm_pad;
+    uint32_t pm_key[OR_STORE_SLOTS];
+    float pm_val[2 * OR_STORE_SLOTS];
 } or_mig;
 
 static void resample_sharded(or_filter* f, int shift)
@@ -1460,6 +1464,11 @@ static void resample_sharded(or_filter* f, int shift)
             m->w = f->w[i]; m->mprob = f->mprob[i];
             m->floating = f->floating[i]; m->ncp = f->ncp[i];
             m->lo = a; m->hi = b; m->src = f->gbase + i;
+            if (f->pm_key) {
+                m->pm_count = f->pm_count[i];
+                memcpy(m->pm_key, f->pm_key + i * OR_STORE_SLOTS, sizeof(m->pm_key));
+                memcpy(m->pm_val, f->pm_val + i * OR_STORE_SLOTS * 2, sizeof(m->pm_val));
+            }
         }
     free(lo); free(hi);
     uint64_t all[ESLAM_ORACLE_MAX_RANKS * ESLAM_ORACLE_MAX_RANKS];
@@ -1486,6 +1495,11 @@ static void resample_sharded(or_filter* f, int shift)
         f->x[o] = m->x; f->y[o] = m->y; f->th[o] = m->th; f->z[o] = m->z; f->zs[o] = m->zs;
         f->w[o] = m->w; f->mprob[o] = m->mprob; f->floating[o] = m->floating; f->ncp[o] = m->ncp;
         f->anc[o] = anc[o];
+        if (f->pm_key) {
+            f->pm_count[o] = m->pm_count;
+            memcpy(f->pm_key + o * OR_STORE_SLOTS, m->pm_key, sizeof(m->pm_key));
+            memcpy(f->pm_val + o * OR_STORE_SLOTS * 2, m->pm_val, sizeof(m->pm_val));
+        }
     }
     free(src); free(anc);
     f->info.resample_overruns = overruns;

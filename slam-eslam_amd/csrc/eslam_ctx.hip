@@ -29,7 +29,7 @@ extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms,
 extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
                                              hipStream_t stream);
 extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint64_t ndup,
-                                              hipStream_t stream);
+                                              const void* payloads, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
@@ -68,7 +68,8 @@ extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, cons
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
                                                   hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
-                                        const uint64_t* first_last, uint64_t nsend, void* send, hipStream_t stream);
+                                        const uint64_t* first_last, uint64_t nsend, void* send, const MapStore* ms,
+                                        void* payloads, hipStream_t stream);
 extern "C" hipError_t eslam_launch_expand(const void* recv, uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* row_first,
                                           hipStream_t stream);
 extern "C" uint64_t eslam_record_bytes(void);
@@ -287,6 +288,11 @@ struct eslam_ctx {
     uint2* range = nullptr;                 // per particle: [lo, hi) of its global outputs
     void* sendbuf = nullptr; uint64_t send_cap = 0;
     void* recvbuf = nullptr; uint64_t recv_cap = 0;
+    // per-particle maps on a sharded filter: the migrated particles' stores (StorePayload per
+    // record, in the records' order) and whether a store copy on write is still owed to them
+    void* sendpay = nullptr; uint64_t sendpay_cap = 0;
+    void* recvpay = nullptr; uint64_t recvpay_cap = 0;
+    bool cow_pending = false;
     void* stage = nullptr; uint64_t stage_cap = 0;   // pinned staging (host-memory comm)
     // SurfaceHash (useHash)
     double map_scale[2] = {1, 1};
@@ -408,6 +414,7 @@ extern "C" void eslam_config_default(eslam_config* c)
 extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 static int materialize(eslam_ctx* ctx);
+static int store_cow(eslam_ctx* ctx, uint32_t* ndup_out);
 
 static int read_ctl(eslam_ctx* ctx)
 {
@@ -547,6 +554,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->scratch); (void)hipHostFree(ctx->scratch_host);
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
+    (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay);
     (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
     (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -1207,22 +1215,14 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
 {
     if (!ctx || (!patches && count)) return ESLAM_ERR_INVALID_ARG;
     if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update needs per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
-    if (ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "per-particle maps are kept on one GPU");
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
     if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
     int rc = materialize(ctx);
     if (rc) return rc;
-    rc = read_ctl(ctx);                       // the current buffer (base ^ flip after the commit)
-    if (rc) return rc;
-    uint32_t* sid = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip].sid;
-    // cloneMaps (src/PoseEstimator.cpp:31-47): particles that share a store get private copies
-    uint32_t* ndup_dev = ctx->cow + 3 * ctx->cap + 2 * ((ctx->cap + 2047) / 2048) + 2;
-    HIPCHK(ctx, eslam_launch_store_cow(sid, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->stream));
     uint32_t ndup = 0;
-    HIPCHK(ctx, hipMemcpyAsync(&ndup, ndup_dev, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    HIPCHK(ctx, eslam_launch_store_copy(sid, &ctx->store, ctx->n, ctx->cow, ndup, ctx->stream));
+    rc = store_cow(ctx, &ndup);
+    if (rc) return rc;
     MergeParams mp;
     memset(&mp, 0, sizeof(mp));
     mp.n = ctx->n;
@@ -1240,7 +1240,6 @@ extern "C" int eslam_gpu_set_particle_maps(eslam_ctx* ctx, int on)
     const bool cur = particle_maps(ctx);
     if ((on != 0) == cur) return ESLAM_OK;
     if (ctx->n) return fail(ctx, ESLAM_ERR_INVALID_ARG, "the map mode is chosen before the particles are initialised");
-    if (on && ctx->sharded) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "per-particle maps are kept on one GPU");
     if (on) ctx->cfg.flags |= ESLAM_FLAG_PARTICLE_MAPS;
     else ctx->cfg.flags &= ~ESLAM_FLAG_PARTICLE_MAPS;
     return ESLAM_OK;
@@ -1295,12 +1294,34 @@ static GatherView gather_view(eslam_ctx* ctx)
 
 // before the particle state is read or replaced outside the hot path: run a pending
 // gather (device decides; a no-op otherwise) and commit the buffer flip
+// cloneMaps (src/PoseEstimator.cpp:31-47) as copy on write: particles that share a store get
+// private copies, and particles received from another rank (sid = kSidRecord | record) get a
+// free store filled from their record's payload.  *ndup: the copies made.
+static int store_cow(eslam_ctx* ctx, uint32_t* ndup_out)
+{
+    int rc = read_ctl(ctx);                   // the current buffer (base ^ flip after the commit)
+    if (rc) return rc;
+    uint32_t* sid = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip].sid;
+    uint32_t* ndup_dev = ctx->cow + 3 * ctx->cap + 2 * ((ctx->cap + 2047) / 2048) + 2;
+    HIPCHK(ctx, eslam_launch_store_cow(sid, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->stream));
+    uint32_t ndup = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&ndup, ndup_dev, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_copy(sid, &ctx->store, ctx->n, ctx->cow, ndup, ctx->recvpay, ctx->stream));
+    ctx->cow_pending = false;
+    if (ndup_out) *ndup_out = ndup;
+    return ESLAM_OK;
+}
+
 static int materialize(eslam_ctx* ctx)
 {
     if (!ctx->n) return ESLAM_OK;
     const GatherView gv = gather_view(ctx);
     const uint32_t aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
     HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], ctx->n, ctx->gbase, ctx->ctl, &gv, aux, ctx->stream));
+    // a sharded resample handed this rank particles whose stores are still in the received
+    // payloads: they get local stores before anything reads a store
+    if (ctx->cow_pending) return store_cow(ctx, nullptr);
     return ESLAM_OK;
 }
 
@@ -1520,13 +1541,25 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
             for (int r = 0; r < G; ++r) any |= (r == d ? 0 : overlap(r, d));
         }
         if (any) {
+            const bool maps = particle_maps(ctx);
+            const uint64_t P = sizeof(StorePayload);
             rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
             if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
+            if (!rc && maps) rc = grow(ctx, &ctx->sendpay, &ctx->sendpay_cap, nsend * P, false);
+            if (!rc && maps) rc = grow(ctx, &ctx->recvpay, &ctx->recvpay_cap, nrecv * P, false);
             if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
             const hipError_t e = eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
-                                                   nsend, ctx->sendbuf, ctx->stream);
+                                                   nsend, ctx->sendbuf, &ctx->store, maps ? ctx->sendpay : nullptr,
+                                                   ctx->stream);
             if (e != hipSuccess) return abort_pending_gather(ctx, e);
             rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
+            if (!rc && maps) {
+                // the migrated stores, in the records' order (the same peers, P bytes per record)
+                uint64_t sp_[kMaxRanks], rp_[kMaxRanks];
+                for (int d = 0; d < G; ++d) { sp_[d] = sb[d] / R * P; rp_[d] = rb[d] / R * P; }
+                rc = comm_alltoallv(ctx, ctx->sendpay, sp_, ctx->recvpay, rp_);
+                ctx->cow_pending = !rc && nrecv > 0;
+            }
             if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
         } else {
             nrecv = 0;

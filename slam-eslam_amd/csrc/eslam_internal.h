@@ -94,6 +94,15 @@ struct DevState {
 constexpr uint32_t kStoreSlots = 32;
 constexpr uint32_t kStoreCap = 24;
 constexpr uint32_t kStoreFree = 0xffffffffu;
+// sharded filters: a particle that a resample received from another rank names no local store
+// yet; its sid is kSidRecord | the record index, and the store copy on write that follows the
+// gather gives it a free store filled from the record's payload (the migrated store)
+constexpr uint32_t kSidRecord = 0x80000000u;
+struct alignas(8) StorePayload {
+    uint32_t count, pad;
+    uint32_t key[kStoreCap];
+    float2 val[kStoreCap];
+};
 static_assert(kStoreSlots == 32 && kStoreCap < kStoreSlots, "store search: 5 halving steps, a free slot at the end");
 struct MapStore {
     uint32_t* key;                       // n stores x kStoreSlots

@@ -1233,14 +1233,14 @@ __global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ si
 __global__ void __launch_bounds__(kBlock) k_store_owner(const uint32_t* __restrict__ sid, uint64_t n, uint32_t* __restrict__ owner)
 {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) atomicMin(&owner[sid[i]], (uint32_t)i);
+    if (i < n && !(sid[i] & kSidRecord)) atomicMin(&owner[sid[i]], (uint32_t)i);
 }
 
 // compaction, mode 0: free stores (no owner) in store order; mode 1: particles that share
 // their store with a lower particle, in particle order.  The two lists have equal length.
 __device__ __forceinline__ bool compact_pred(int mode, uint64_t i, const uint32_t* owner, const uint32_t* sid)
 {
-    return mode == 0 ? owner[i] == ~0u : owner[sid[i]] != (uint32_t)i;
+    return mode == 0 ? owner[i] == ~0u : ((sid[i] & kSidRecord) || owner[sid[i]] != (uint32_t)i);
 }
 
 constexpr int kCompactItems = 8;
@@ -1287,15 +1287,24 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, 
 }
 
 // copy on write: the j-th sharing particle takes the j-th free store, a copy of the one it
-// shared (one thread per slot)
+// shared (one thread per slot); a particle received from another rank, a copy of its record's
+// payload (pay: the received payloads, sharded filters)
 __global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                       uint64_t ndup, uint32_t* __restrict__ sid, MapStore ms)
+                                                       uint64_t ndup, uint32_t* __restrict__ sid, MapStore ms,
+                                                       const StorePayload* __restrict__ pay)
 {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= ndup * kStoreSlots) return;
     const uint64_t j = t / kStoreSlots;
     const uint32_t slot = (uint32_t)(t - j * kStoreSlots);
     const uint32_t p = dups[j], from = sid[p], to = frees[j];
+    if (from & kSidRecord) {
+        const StorePayload& q = pay[from & ~kSidRecord];
+        ms.key[(uint64_t)to * kStoreSlots + slot] = slot < kStoreCap ? q.key[slot] : kStoreFree;
+        ms.val[(uint64_t)to * kStoreSlots + slot] = slot < kStoreCap ? q.val[slot] : make_float2(0.0f, 0.0f);
+        if (slot == 0) ms.count[to] = q.count;
+        return;
+    }
     ms.key[(uint64_t)to * kStoreSlots + slot] = ms.key[(uint64_t)from * kStoreSlots + slot];
     ms.val[(uint64_t)to * kStoreSlots + slot] = ms.val[(uint64_t)from * kStoreSlots + slot];
     if (slot == 0) ms.count[to] = ms.count[from];
@@ -1954,7 +1963,6 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     }
 }
 
-// K3b (one GPU): segment boundaries of every particle and the marks of the tile's outputs.
 // Draw counting (#{k : T_k <= C}) for the particles of one wave: the counts of its targets
 // only read the draws [dlo, dhi) around floor(C N) of its first and last target.  Its lanes
 // evaluate those draws in parallel, wave_draws at a time (lane l: k = q0 + l + 64 j, one jump
@@ -2298,7 +2306,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
 // [first, last] (d's run, from k_segments_multi) whose range [lo, hi) contains k
 __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
                                                  const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
-                                                 Rec* __restrict__ send)
+                                                 Rec* __restrict__ send, MapStore ms, StorePayload* __restrict__ pay)
 {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= pp.send_off[pp.nranks]) return;
@@ -2318,6 +2326,16 @@ __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const
     r.lohi = k | ((k + 1) << 32);
     r.src = (uint64_t)st.flags[i] | ((pp.gbase[pp.rank] + i) << 8);
     send[j] = r;
+    if (pay) {                           // per-particle maps: the source particle's store travels too
+        const uint32_t s = st.sid[i];
+        StorePayload& q = pay[j];
+        q.count = ms.count[s];
+        q.pad = 0;
+        for (uint32_t t = 0; t < kStoreCap; ++t) {
+            q.key[t] = ms.key[(uint64_t)s * kStoreSlots + t];
+            q.val[t] = ms.val[(uint64_t)s * kStoreSlots + t];
+        }
+    }
 }
 
 // records -> marks (lower ranks: 1 + j, higher ranks: kMarkHigh + 1 + j)
@@ -2385,6 +2403,7 @@ __global__ void __launch_bounds__(kBlock) k_resample_gather(DevState s0, DevStat
             out.x[k] = rc->x; out.y[k] = rc->y; out.th[k] = rc->th; out.z[k] = rc->z; out.zs[k] = rc->zs; out.w[k] = rc->w;
             if (aux) { out.mprob[k] = rc->mprob; out.flags[k] = (uint8_t)rc->src; }
             if (gv.record) gv.anc[k] = (uint32_t)(rc->src >> 8);
+            if (in.sid) out.sid[k] = kSidRecord | (uint32_t)(rc - (const gmem<const Rec>*)gv.recs);   // store: the record's
             continue;
         }
         out.x[k] = in.x[i];
@@ -2695,7 +2714,7 @@ extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, 
 
 // the copies and renames for ndup sharing particles (host-read count)
 extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint64_t ndup,
-                                              hipStream_t stream)
+                                              const void* payloads, hipStream_t stream)
 {
     if (!ndup) return hipSuccess;
     const uint32_t tiles = (uint32_t)((n + kCompactTile - 1) / kCompactTile);
@@ -2703,7 +2722,7 @@ extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms,
     uint32_t* dups = frees + n;
     const uint64_t slots = ndup * kStoreSlots;
     hipLaunchKernelGGL(k_store_copy, dim3((uint32_t)((slots + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, dups, frees, ndup,
-                       sid, *ms);
+                       sid, *ms, (const StorePayload*)payloads);
     hipLaunchKernelGGL(k_store_rename, dim3((uint32_t)((ndup + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, dups, frees, ndup,
                        sid);
     return hipGetLastError();
@@ -2796,11 +2815,12 @@ extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, cons
 }
 
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
-                                        const uint64_t* first_last, uint64_t nsend, void* send, hipStream_t stream)
+                                        const uint64_t* first_last, uint64_t nsend, void* send, const MapStore* ms,
+                                        void* payloads, hipStream_t stream)
 {
     if (!nsend) return hipSuccess;
     hipLaunchKernelGGL(k_pack, dim3((uint32_t)((nsend + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, s0, s1, ctl, *pp,
-                       range, first_last, (Rec*)send);
+                       range, first_last, (Rec*)send, *ms, (StorePayload*)payloads);
     return hipGetLastError();
 }
 

@@ -10,7 +10,7 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "hash", "config3")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "maps")
 CONFIG3_STEPS = 3
 
 
@@ -23,8 +23,10 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3"):
+    if name in ("forced", "config3", "maps"):
         S.bench_config(cfg, n_global)
+        if name == "maps":                       # useSharedMap = false: per-particle maps
+            cfg.flags |= A.FLAG_PARTICLE_MAPS
     else:
         cfg.particle_count = n_global
         cfg.min_effective = (n_global * 9) // 10
@@ -39,6 +41,8 @@ def scenario_grid(name):
         return hash_grid(cells=60)
     if name == "config3":
         return S.flat_map(cells=1000)             # the bench's 100 x 100 m map
+    if name == "maps":                            # the front feet stand on cells only the scans map
+        return S.unmapped_beyond(S.rough_map(cells=120), 0.3)
     return S.rough_map(cells=120) if name != "forced" else S.rough_map(cells=120, multi=False)
 
 
@@ -116,6 +120,8 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         _snap(rec, "res", f, True)
     elif name == "hash":
         f.init_pose([0.0, 0.0, 0.18], [1.0, 0.0, 0.0, 0.0])       # SurfaceHash::create + init(N, hash)
+    elif name == "maps":
+        f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
     else:
         sigma = [0.1, 0.1, 0.1] if name == "forced" else [0.6, 0.6, 0.3]
         f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], sigma, 0.18, 1.001)
@@ -124,12 +130,25 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         from hash_util import slope_stream
         stream = slope_stream(steps)
     else:
-        stream = S.step_stream(steps, tilt=(name == "natural"))
+        stream = S.step_stream(steps, tilt=(name in ("natural", "maps")))
+    scan = S.scan_patches() if name == "maps" else None
     for k, st in enumerate(stream):
         f.step(st)
         info = info_fn(f)
         _info(rec, f"s{k}", info)
         _snap(rec, f"s{k}", f, bool(info.resampled))
+        if scan is not None:                     # processMap(scan, false, true)
+            f.map_update(scan)
+    if scan is not None:                         # every particle's own patches, sorted by cell
+        n = hi - lo
+        cells = np.full((n, 24), 0xffffffff, np.uint32)
+        mean = np.zeros((n, 24), np.float32)
+        sd = np.zeros((n, 24), np.float32)
+        for i in range(n):
+            c, m, s_ = f.particle_map(i)
+            o = np.argsort(c)
+            cells[i, :len(c)], mean[i, :len(c)], sd[i, :len(c)] = c[o], m[o], s_[o]
+        rec["maps/cells"], rec["maps/mean"], rec["maps/stdev"] = cells, mean, sd
     rec["best"] = np.array([f.best_index()])
     rec["rng"] = np.array([f.rng_state().minstd_x])
     pos, quat = f.centroid()                 # getCentroid (normalises in place, Q15)

@@ -89,11 +89,18 @@ def single_oracle(name, n_global):
 
 @pytest.mark.parametrize("name,n_global,world", [("forced", 3000, 2), ("natural", 2500, 2), ("upload", 2000, 2),
                                                  ("forced", 1000, 3), ("upload", 700, 3), ("hash", 2000, 2),
-                                                 ("hash", 1500, 3)])
+                                                 ("hash", 1500, 3), ("maps", 3000, 2), ("maps", 1500, 3)])
 def test_sharded_oracle_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("oracle", name, n_global, world, str(tmp_path)))
     assert_same(got, want, f"{name} N={n_global} world={world}")
+    if name == "maps":
+        # particles (and their own maps) did migrate between ranks
+        import eslam_abi as A
+        g = A.shard_bounds(n_global, world)
+        owner = np.searchsorted(g, np.arange(n_global), side="right") - 1
+        moved = sum(int(np.count_nonzero(owner[want[k].astype(np.int64)] != owner)) for k in want if k.endswith("/anc"))
+        assert moved > 0
 
 
 def test_shard_bounds_chunk_aligned():

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name,n_global,world", [("forced", 5000, 2), ("natural", 2500, 2), ("upload", 2000, 2),
-                                                 ("upload", 700, 3), ("hash", 3000, 2), ("hash", 1500, 3)])
+                                                 ("upload", 700, 3), ("hash", 3000, 2), ("hash", 1500, 3),
+                                                 ("maps", 3000, 2), ("maps", 1500, 3)])
 def test_sharded_gpu_gloo_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, world, str(tmp_path), mem="host", timeout=400))
@@ -27,7 +28,7 @@ def test_sharded_gpu_rccl_one_rank(oracle, tmp_path, name, n_global):
     assert_same(got, want, f"gpu rccl {name} N={n_global}")
 
 
-@pytest.mark.parametrize("name,n_global", [("forced", 5000), ("upload", 2000), ("hash", 3000)])
+@pytest.mark.parametrize("name,n_global", [("forced", 5000), ("upload", 2000), ("hash", 3000), ("maps", 2000)])
 def test_sharded_gpu_native_rccl_one_rank(oracle, tmp_path, name, n_global):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, 1, str(tmp_path), mem="rccl", timeout=400))
