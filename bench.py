@@ -50,6 +50,8 @@ def parse():
                          "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles per "
                          "GPU (64M over 8 GPUs with --gpus 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-aos", action="store_true",
+                    help="skip cpu_baseline.aos, the oracle with the reference's 288-byte particle records")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (sharded, RCCL) path even on one rank (measures its overhead)")
     ap.add_argument("--comm", choices=["rccl", "torch"], default=os.environ.get("ESLAM_COMM", "rccl"),
@@ -122,38 +124,54 @@ def host_cpu():
     return model, os.cpu_count()
 
 
-def cpu_baseline(args, grid, flags=0, scan=None):
-    """The CPU oracle (a restatement of the reference path, reference-order double sums) on
-    this host, on a bounded sample of the same workload: one thread by default (the
-    reference's build default), --cpu-threads for its OpenMP per-particle loops."""
+def time_oracle(args, grid, flags, scan, steps, aos):
+    """Seconds for `steps` steps of the bench workload on a cpu_sample-particle oracle filter
+    (first step, the uniform reset, untimed)."""
     import eslam_abi as A
     import oracle_ffi as O
     import synthetic as S
     n = args.cpu_sample
-    stream = S.step_stream(args.cpu_steps + 1, tilt=scan is not None)
+    stream = S.step_stream(steps + 1, tilt=scan is not None)
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= flags
-    f = O.OracleFilter(cfg, O.SUM_REFERENCE)
+    f = O.OracleFilter(cfg, O.SUM_REFERENCE, aos=aos)
     f.set_threads(args.cpu_threads)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
-    f.step(stream[0])                     # first step (uniform reset) untimed
+    f.step(stream[0])
     if scan is not None:
         f.map_update(scan)
     t0 = time.perf_counter()
-    k = 0
-    for st in stream[1:1 + args.cpu_steps]:
+    for st in stream[1:1 + steps]:
         f.step(st)
         if scan is not None:
             f.map_update(scan)
-        k += 1
-    dt = time.perf_counter() - t0
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(args, grid, flags=0, scan=None):
+    """The CPU oracle (a restatement of the reference path, reference-order double sums) on
+    this host, on a bounded sample of the same workload: one thread by default (the
+    reference's build default), --cpu-threads for its OpenMP per-particle loops.  `aos`: the
+    same oracle built with the reference's 288-byte particle records (src/PoseParticle.hpp:52-86
+    + src/PoseEstimator.hpp:108-117; whole-record copies at resample) on half the steps --
+    closer to the reference's memory behaviour than the SoA figure."""
+    n, k = args.cpu_sample, args.cpu_steps
+    dt = time_oracle(args, grid, flags, scan, k, aos=False)
     model, ncpu = host_cpu()
-    return {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": args.cpu_threads, "kind": "port",
-            "cpu_model": model, "host_logical_cpus": ncpu,
-            "sample": f"{n} particles x {k} steps of the same workload ({'rough map, per-particle maps + map update' if scan is not None else 'flat map'}"
-                      f", forced update+resample), oracle/eslam_oracle.c in reference-sum mode, "
-                      f"{args.cpu_threads} thread(s), {dt:.1f} s"}
+    what = "rough map, per-particle maps + map update" if scan is not None else "flat map"
+    out = {"value": round(n * k / dt / 1e6, 4), "unit": "M particle-updates/s", "cores": args.cpu_threads, "kind": "port",
+           "cpu_model": model, "host_logical_cpus": ncpu,
+           "sample": f"{n} particles x {k} steps of the same workload ({what}, forced update+resample), "
+                     f"oracle/eslam_oracle.c (SoA state) in reference-sum mode, {args.cpu_threads} thread(s), {dt:.1f} s"}
+    if not args.no_cpu_aos:
+        ka = max(1, k // 2)
+        da = time_oracle(args, grid, flags, scan, ka, aos=True)
+        out["aos"] = {"value": round(n * ka / da / 1e6, 4), "unit": "M particle-updates/s", "cores": args.cpu_threads,
+                      "kind": "port",
+                      "sample": f"{n} particles x {ka} steps, the same oracle built -DOR_AOS (288-byte particle "
+                                f"records, whole-record resample copies), {da:.1f} s"}
+    return out
 
 
 def spawn_ranks(args):

@@ -513,12 +513,32 @@ void or_surface_param_from_points(const double* P, uint32_t n, double* slope_x, 
 /* ========================================================================================
  * the filter
  * ====================================================================================== */
+/* Particle state layout.  The default build keeps one array per field (SoA).  Built with
+ * -DOR_AOS (oracle/_build/liboracle_aos.so, bench.py's second cpu_baseline figure only) the
+ * state is one 288-byte record per particle, the size of the reference's PoseParticleGA
+ * (src/PoseParticle.hpp:52-86 + src/PoseEstimator.hpp:108-117): x..mprob at doubles 0..6,
+ * floating and ncp at bytes 56 and 57, the rest standing in for the reference's other
+ * members (contact points, meas_pos, the map handle).  Every access goes through OD / OB,
+ * and a resample copies whole records, as the reference's particle vector does
+ * (src/ParticleFilter.hpp:85-108).  Results are identical in both layouts. */
+#ifdef OR_AOS
+#define OR_REC_BYTES 288u
+#define OR_DSTRIDE (OR_REC_BYTES / 8u)
+#define OR_BSTRIDE OR_REC_BYTES
+#else
+#define OR_DSTRIDE 1u
+#define OR_BSTRIDE 1u
+#endif
+#define OD(i) ((uint64_t)(i) * OR_DSTRIDE)
+#define OB(i) ((uint64_t)(i) * OR_BSTRIDE)
+
 struct or_filter {
     eslam_config cfg;
     int sum_mode;
     uint64_t n;
-    double *x, *y, *th, *z, *zs, *w, *mprob;
+    double *x, *y, *th, *z, *zs, *w, *mprob;   /* field views (strided records with OR_AOS) */
     uint8_t *floating, *ncp;
+    void* rec;                                 /* OR_AOS: the record buffer the views point into */
     /* debug of the last updateWeights */
     uint32_t* dbg_ncp;
     or_cpoint* dbg_cp;
@@ -576,10 +596,54 @@ static int comm_allgather(or_filter* f, const void* send, void* recv, uint64_t b
     return f->comm.allgather(f->comm.user, send, recv, bytes, NULL);
 }
 
+/* point the field views at a state buffer: one record per particle (OR_AOS) */
+static void set_views(or_filter* f, void* rec)
+{
+    f->rec = rec;
+#ifdef OR_AOS
+    double* d = rec;
+    f->x = d; f->y = d + 1; f->th = d + 2; f->z = d + 3; f->zs = d + 4; f->w = d + 5; f->mprob = d + 6;
+    f->floating = (uint8_t*)rec + 56; f->ncp = (uint8_t*)rec + 57;
+#endif
+}
+
+static void free_state(or_filter* f)
+{
+#ifdef OR_AOS
+    free(f->rec);
+#else
+    free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob);
+    free(f->floating); free(f->ncp);
+#endif
+    f->rec = NULL;
+}
+
+/* strided copies between the caller's field arrays and the state */
+static void put_d(double* dst, const double* src, uint64_t n)
+{
+    if (OR_DSTRIDE == 1) { memcpy(dst, src, n * 8); return; }
+    for (uint64_t i = 0; i < n; ++i) dst[OD(i)] = src[i];
+}
+static void get_d(double* dst, const double* src, uint64_t n)
+{
+    if (OR_DSTRIDE == 1) { memcpy(dst, src, n * 8); return; }
+    for (uint64_t i = 0; i < n; ++i) dst[i] = src[OD(i)];
+}
+static void put_b(uint8_t* dst, const uint8_t* src, uint64_t n)
+{
+    if (OR_BSTRIDE == 1) { memcpy(dst, src, n); return; }
+    for (uint64_t i = 0; i < n; ++i) dst[OB(i)] = src[i];
+}
+static void get_b(uint8_t* dst, const uint8_t* src, uint64_t n)
+{
+    if (OR_BSTRIDE == 1) { memcpy(dst, src, n); return; }
+    for (uint64_t i = 0; i < n; ++i) dst[i] = src[OB(i)];
+}
+
 static void or_free_particles(or_filter* f)
 {
-    free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob);
-    free(f->floating); free(f->ncp); free(f->anc);
+    free_state(f);
+    free(f->anc);
     free(f->dbg_ncp); free(f->dbg_cp); free(f->dbg_zdelta); free(f->dbg_zvar);
     free(f->pm_key); free(f->pm_val); free(f->pm_count);
     f->pm_key = NULL; f->pm_val = NULL; f->pm_count = NULL;
@@ -596,9 +660,15 @@ static int or_alloc_particles(or_filter* f, uint64_t n)
     or_free_particles(f);
     f->n = n;
     size_t b = (size_t)(n ? n : 1);
+#ifdef OR_AOS
+    set_views(f, calloc(b, OR_REC_BYTES));
+    if (!f->rec) return ESLAM_ERR_OUT_OF_MEMORY;
+#else
     f->x = calloc(b, 8); f->y = calloc(b, 8); f->th = calloc(b, 8); f->z = calloc(b, 8);
     f->zs = calloc(b, 8); f->w = calloc(b, 8); f->mprob = calloc(b, 8);
-    f->floating = calloc(b, 1); f->ncp = calloc(b, 1); f->anc = calloc(b, 4);
+    f->floating = calloc(b, 1); f->ncp = calloc(b, 1);
+#endif
+    f->anc = calloc(b, 4);
     if (f->debug) {
         f->dbg_ncp = calloc(b, 4);
         f->dbg_cp = calloc(b * ESLAM_MAX_CONTACTS, sizeof(or_cpoint));
@@ -700,15 +770,15 @@ int or_init_gaussian(or_filter* f, uint64_t n, const double mu[3], const double 
         double n0, n1, n2, n3;
         dm_box_muller32(d0.v[0], d0.v[1], &n0, &n1);
         dm_box_muller32(d0.v[2], d0.v[3], &n2, &n3);
-        f->x[i] = n0 * sigma[0] + mu[0];
-        f->y[i] = n1 * sigma[1] + mu[1];
-        f->th[i] = n2 * sigma[2] + mu[2];
-        f->z[i] = zpos;
-        f->zs[i] = zsigma;
-        f->w[i] = 0;            /* PoseParticle ctor: weight(0), Q3 */
-        f->mprob[i] = 0;
-        f->floating[i] = 1;
-        f->ncp[i] = 0;
+        f->x[OD(i)] = n0 * sigma[0] + mu[0];
+        f->y[OD(i)] = n1 * sigma[1] + mu[1];
+        f->th[OD(i)] = n2 * sigma[2] + mu[2];
+        f->z[OD(i)] = zpos;
+        f->zs[OD(i)] = zsigma;
+        f->w[OD(i)] = 0;            /* PoseParticle ctor: weight(0), Q3 */
+        f->mprob[OD(i)] = 0;
+        f->floating[OB(i)] = 1;
+        f->ncp[OB(i)] = 0;
     }
     f->init_count++;
     f->wexp = 1;
@@ -744,13 +814,13 @@ int or_upload(or_filter* f, uint64_t n, const eslam_particles* p)
 {
     int rc = or_alloc_particles(f, n);
     if (rc) return rc;
-    memcpy(f->x, p->x, n * 8); memcpy(f->y, p->y, n * 8); memcpy(f->th, p->orientation, n * 8);
-    memcpy(f->z, p->zpos, n * 8); memcpy(f->zs, p->zsigma, n * 8); memcpy(f->w, p->weight, n * 8);
-    if (p->mprob) memcpy(f->mprob, p->mprob, n * 8);
-    if (p->floating) memcpy(f->floating, p->floating, n);
-    if (p->n_contact_points) memcpy(f->ncp, p->n_contact_points, n);
+    put_d(f->x, p->x, n); put_d(f->y, p->y, n); put_d(f->th, p->orientation, n);
+    put_d(f->z, p->zpos, n); put_d(f->zs, p->zsigma, n); put_d(f->w, p->weight, n);
+    if (p->mprob) put_d(f->mprob, p->mprob, n);
+    if (p->floating) put_b(f->floating, p->floating, n);
+    if (p->n_contact_points) put_b(f->ncp, p->n_contact_points, n);
     double mx = 0;
-    for (uint64_t i = 0; i < n; ++i) if (f->w[i] > mx) mx = f->w[i];
+    for (uint64_t i = 0; i < n; ++i) if (f->w[OD(i)] > mx) mx = f->w[OD(i)];
     if (f->sharded) {
         double all[ESLAM_ORACLE_MAX_RANKS];
         if (comm_allgather(f, &mx, all, 8)) return ESLAM_ERR_COMM;
@@ -763,15 +833,15 @@ int or_upload(or_filter* f, uint64_t n, const eslam_particles* p)
 int or_download(or_filter* f, eslam_particles* p)
 {
     uint64_t n = f->n;
-    if (p->x) memcpy(p->x, f->x, n * 8);
-    if (p->y) memcpy(p->y, f->y, n * 8);
-    if (p->orientation) memcpy(p->orientation, f->th, n * 8);
-    if (p->zpos) memcpy(p->zpos, f->z, n * 8);
-    if (p->zsigma) memcpy(p->zsigma, f->zs, n * 8);
-    if (p->weight) memcpy(p->weight, f->w, n * 8);
-    if (p->mprob) memcpy(p->mprob, f->mprob, n * 8);
-    if (p->floating) memcpy(p->floating, f->floating, n);
-    if (p->n_contact_points) memcpy(p->n_contact_points, f->ncp, n);
+    if (p->x) get_d(p->x, f->x, n);
+    if (p->y) get_d(p->y, f->y, n);
+    if (p->orientation) get_d(p->orientation, f->th, n);
+    if (p->zpos) get_d(p->zpos, f->z, n);
+    if (p->zsigma) get_d(p->zsigma, f->zs, n);
+    if (p->weight) get_d(p->weight, f->w, n);
+    if (p->mprob) get_d(p->mprob, f->mprob, n);
+    if (p->floating) get_b(p->floating, f->floating, n);
+    if (p->n_contact_points) get_b(p->n_contact_points, f->ncp, n);
     return 0;
 }
 
@@ -908,8 +978,8 @@ int or_init_hash(or_filter* f, uint64_t n)
         const uint32_t idx = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&f->libc) % f->hash_n);
         if (g < skip || g >= skip + n) continue;
         const uint64_t i = g - skip;
-        f->x[i] = f->hash_x[idx]; f->y[i] = f->hash_y[idx]; f->th[i] = f->hash_th[idx]; f->z[i] = f->hash_z[idx];
-        f->zs[i] = 0.0; f->w[i] = 0.0; f->mprob[i] = 0.0; f->floating[i] = 1; f->ncp[i] = 0;
+        f->x[OD(i)] = f->hash_x[idx]; f->y[OD(i)] = f->hash_y[idx]; f->th[OD(i)] = f->hash_th[idx]; f->z[OD(i)] = f->hash_z[idx];
+        f->zs[OD(i)] = 0.0; f->w[OD(i)] = 0.0; f->mprob[OD(i)] = 0.0; f->floating[OB(i)] = 1; f->ncp[OB(i)] = 0;
     }
     f->wexp = 1;
     return 0;
@@ -954,7 +1024,7 @@ static void sample_from_hash(or_filter* f, const eslam_step_input* in)
      * in rank order, so every rank sorts the one-filter list and replaces what it holds   */
     or_widx* wi = malloc(sizeof(or_widx) * (f->n ? f->n : 1));
     for (uint64_t i = 0; i < f->n; ++i) {
-        float wf = (float)f->w[i];
+        float wf = (float)f->w[OD(i)];
         if (wf == 0.0f) wf = 0.0f;                /* -0 and +0 compare equal */
         wi[i].w = wf;
         wi[i].i = (uint32_t)(f->gbase + i);
@@ -989,10 +1059,10 @@ static void sample_from_hash(or_filter* f, const eslam_step_input* in)
         const uint64_t gi = all[j].i;
         if (gi < f->gbase || gi >= f->gbase + f->n) continue;
         const uint64_t i = gi - f->gbase;
-        f->x[i] = f->hash_x[src]; f->y[i] = f->hash_y[src]; f->th[i] = f->hash_th[src]; f->z[i] = f->hash_z[src];
-        f->zs[i] = 0.5;
-        f->floating[i] = 1;
-        f->w[i] = weight;
+        f->x[OD(i)] = f->hash_x[src]; f->y[OD(i)] = f->hash_y[src]; f->th[OD(i)] = f->hash_th[src]; f->z[OD(i)] = f->hash_z[src];
+        f->zs[OD(i)] = 0.5;
+        f->floating[OB(i)] = 1;
+        f->w[OD(i)] = weight;
     }
     if (all != wi) free(all);
     free(wi);
@@ -1030,20 +1100,20 @@ int or_project(or_filter* f, const eslam_step_input* in)
         const double u_slip = dm_u32(d1.v[0]);
         if (u_slip < c->slip_factor) dy *= dm_u32(d1.v[1]);
         double s, co;
-        or_sincos(f, f->th[i], &s, &co);
-        f->x[i] += co * dx - s * dy;
-        f->y[i] += s * dx + co * dy;
-        f->th[i] += dth;
+        or_sincos(f, f->th[OD(i)], &s, &co);
+        f->x[OD(i)] += co * dx - s * dy;
+        f->y[OD(i)] += s * dx + co * dy;
+        f->th[OD(i)] += dth;
         if (c->max_yaw_deviation > 0.0) {
-            if (fabs(f->th[i] - pp.yaw) > c->max_yaw_deviation) f->w[i] *= 0.7;
+            if (fabs(f->th[OD(i)] - pp.yaw) > c->max_yaw_deviation) f->w[OD(i)] *= 0.7;
         }
-        f->z[i] += pp.z_delta;
-        f->zs[i] = sqrt(f->zs[i] * f->zs[i] + pp.z_var);
+        f->z[OD(i)] += pp.z_delta;
+        f->zs[OD(i)] = sqrt(f->zs[OD(i)] * f->zs[OD(i)] + pp.z_var);
         if (do_spread) {
             dm_box_muller32(d1.v[2], d1.v[3], &sn1, &sn2);
-            f->x[i] += sn0 * tf + 0.0;
-            f->y[i] += sn1 * tf + 0.0;
-            f->th[i] += sn2 * rf + 0.0;
+            f->x[OD(i)] += sn0 * tf + 0.0;
+            f->y[OD(i)] += sn1 * tf + 0.0;
+            f->th[OD(i)] += sn2 * rf + 0.0;
         }
     }
     f->project_count++;
@@ -1106,8 +1176,9 @@ static double butterfly64(double* v)
 }
 
 /* chunk sums of vals[i] restricted to sel(i) (bucket match), accumulated into acc */
-static void chunk_reduce(const double* vals, const uint8_t* bucket, int want_bucket, uint64_t n, uint32_t J,
-                         or_acc* acc, int scale)
+/* vstride: element stride of vals (OR_DSTRIDE for the state's weights) */
+static void chunk_reduce(const double* vals, uint64_t vstride, const uint8_t* bucket, int want_bucket,
+                         uint64_t n, uint32_t J, or_acc* acc, int scale)
 {
     const uint64_t csz = 64ull * J;
     for (uint64_t c0 = 0; c0 < n; c0 += csz) {
@@ -1117,7 +1188,7 @@ static void chunk_reduce(const double* vals, const uint8_t* bucket, int want_buc
             for (uint32_t j = 0; j < J; ++j) {
                 uint64_t i = c0 + 64ull * j + (uint64_t)s;
                 if (i >= n) continue;
-                double v = (bucket == NULL || (int)bucket[i] == want_bucket) ? vals[i] : 0.0;
+                double v = (bucket == NULL || (int)bucket[i] == want_bucket) ? vals[i * vstride] : 0.0;
                 a = a + v;
             }
             lane[s] = a;
@@ -1159,11 +1230,11 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
         double s, co;
-        or_sincos(f, f->th[i], &s, &co);
+        or_sincos(f, f->th[OD(i)], &s, &co);
         const double r22 = (1.0 - co) + co;
         /* Translation3d(x, y, zPos) * AngleAxisd(theta, UnitZ) */
-        double T[12] = {co, -s, 0.0, f->x[i], s, co, 0.0, f->y[i], 0.0, 0.0, r22, f->z[i]};
-        const double meas_var = f->literal ? pow(f->zs[i], 2) + pow(c->measurement_error, 2) : f->zs[i] * f->zs[i] + me2;
+        double T[12] = {co, -s, 0.0, f->x[OD(i)], s, co, 0.0, f->y[OD(i)], 0.0, 0.0, r22, f->z[OD(i)]};
+        const double meas_var = f->literal ? pow(f->zs[OD(i)], 2) + pow(c->measurement_error, 2) : f->zs[OD(i)] * f->zs[OD(i)] + me2;
         or_pmap pmc = {&f->map, f->pm_key ? f->pm_key + (uint64_t)i * OR_STORE_SLOTS : NULL,
                        f->pm_val ? f->pm_val + (uint64_t)i * OR_STORE_SLOTS * 2 : NULL};
         int acc = f->pm_key ? or_cm_evaluate_pose(&cm, T, meas_var, particle_map_fn, &pmc)
@@ -1171,13 +1242,13 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         if (acc < 0) { zero_var = 1; acc = 0; }
         sw_val[i] = 0.0;
         if (acc) {
-            double zvar = f->zs[i] * f->zs[i];
-            or_cm_update_z(&cm, &f->z[i], &zvar);
-            f->zs[i] = sqrt(zvar);
+            double zvar = f->zs[OD(i)] * f->zs[OD(i)];
+            or_cm_update_z(&cm, &f->z[OD(i)], &zvar);
+            f->zs[OD(i)] = sqrt(zvar);
             const double weight = cm.weight;
-            f->w[i] *= weight;
-            f->mprob[i] = weight;
-            f->floating[i] = 0;
+            f->w[OD(i)] *= weight;
+            f->mprob[OD(i)] = weight;
+            f->floating[OB(i)] = 0;
             maxw = (maxw < weight) ? weight : maxw;
             data_particles++;
             const uint64_t found = cm.ncp;
@@ -1187,12 +1258,12 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
             else sw_val[i] = weight == 0.0 ? 0.0 : dm_exp((-0.5 * cm.shape_s2) * (1.0 / (double)found));
             total_points += found;
         } else {
-            f->floating[i] = 1;
-            f->mprob[i] = 1.0;
+            f->floating[OB(i)] = 1;
+            f->mprob[OD(i)] = 1.0;
         }
-        f->ncp[i] = (uint8_t)cm.ncp;
+        f->ncp[OB(i)] = (uint8_t)cm.ncp;
         bucket[i] = (uint8_t)(cm.ncp < DM_NBUCKETS - 1 ? cm.ncp : DM_NBUCKETS - 1);
-        a_val[i] = f->w[i] * f->mprob[i];
+        a_val[i] = f->w[OD(i)] * f->mprob[OD(i)];
         if (f->dbg_ncp) {
             f->dbg_ncp[i] = cm.ncp;
             memcpy(&f->dbg_cp[i * ESLAM_MAX_CONTACTS], cm.cp, cm.ncp * sizeof(or_cpoint));
@@ -1213,12 +1284,12 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     memset(accs, 0, sizeof(accs));
     const int sa = DM_FX_SCALE - f->wexp, sb = DM_FX_SCALE - 2 * f->wexp;
     if (f->sum_mode == OR_SUM_CONTRACT) {
-        chunk_reduce(sw_val, NULL, 0, f->n, J, &accs[2 * DM_NBUCKETS], DM_FX_SCALE);
+        chunk_reduce(sw_val, 1, NULL, 0, f->n, J, &accs[2 * DM_NBUCKETS], DM_FX_SCALE);
         double* a2 = malloc(f->n * 8 + 8);
         for (uint64_t i = 0; i < f->n; ++i) a2[i] = a_val[i] * a_val[i];
         for (int b = 0; b < DM_NBUCKETS; ++b) {
-            chunk_reduce(a_val, bucket, b, f->n, J, &accs[b], sa);
-            chunk_reduce(a2, bucket, b, f->n, J, &accs[DM_NBUCKETS + b], sb);
+            chunk_reduce(a_val, 1, bucket, b, f->n, J, &accs[b], sa);
+            chunk_reduce(a2, 1, bucket, b, f->n, J, &accs[DM_NBUCKETS + b], sb);
         }
         free(a2);
         if (combine_accs(f, accs, 2 * DM_NBUCKETS + 1)) { free(a_val); free(sw_val); free(bucket); return ESLAM_ERR_COMM; }
@@ -1247,8 +1318,8 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     }
     /* phase B  src/PoseEstimator.cpp:332-345 */
     for (uint64_t i = 0; i < f->n; ++i) {
-        double factor = f->mprob[i] * ph->f[bucket[i]];
-        f->w[i] *= factor;
+        double factor = f->mprob[OD(i)] * ph->f[bucket[i]];
+        f->w[OD(i)] *= factor;
     }
     if (f->sum_mode == OR_SUM_CONTRACT) {
         double S = 0.0, Q = 0.0;
@@ -1278,16 +1349,16 @@ static double normalize_with(or_filter* f, double S, double Q, int have_sums)
     if (f->sum_mode == OR_SUM_REFERENCE || !have_sums) {
         if (f->sum_mode == OR_SUM_REFERENCE) {
             S = 0;
-            for (uint64_t i = 0; i < n; ++i) S += f->w[i];
+            for (uint64_t i = 0; i < n; ++i) S += f->w[OD(i)];
         } else {
             const uint32_t J = dm_chunk_rows(N);
             int e = f->wexp;
             double* w2 = malloc(n * 8 + 8);
-            for (uint64_t i = 0; i < n; ++i) w2[i] = f->w[i] * f->w[i];
+            for (uint64_t i = 0; i < n; ++i) w2[i] = f->w[OD(i)] * f->w[OD(i)];
             or_acc AB[2];
             memset(AB, 0, sizeof(AB));
-            chunk_reduce(f->w, NULL, 0, n, J, &AB[0], DM_FX_SCALE - e);
-            chunk_reduce(w2, NULL, 0, n, J, &AB[1], DM_FX_SCALE - 2 * e);
+            chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, n, J, &AB[0], DM_FX_SCALE - e);
+            chunk_reduce(w2, 1, NULL, 0, n, J, &AB[1], DM_FX_SCALE - 2 * e);
             free(w2);
             combine_accs(f, AB, 2);
             S = acc_value(&AB[0], DM_FX_SCALE - e);
@@ -1299,15 +1370,15 @@ static double normalize_with(or_filter* f, double S, double Q, int have_sums)
     if (S <= 0.0) {
         f->info.uniform_reset = 1;
         for (uint64_t i = 0; i < n; ++i) {
-            double* w = &f->w[i];
+            double* w = &f->w[OD(i)];
             *w = 1.0 / (double)N;
             effective += *w * *w;
         }
         if (f->sum_mode == OR_SUM_CONTRACT) effective = 1.0 / (double)N;   /* eff := N */
     } else {
         for (uint64_t i = 0; i < n; ++i) {
-            f->w[i] /= S;
-            effective += f->w[i] * f->w[i];
+            f->w[OD(i)] /= S;
+            effective += f->w[OD(i)] * f->w[OD(i)];
         }
         if (f->sum_mode == OR_SUM_CONTRACT) effective = Q / (S * S);
     }
@@ -1321,11 +1392,11 @@ double or_get_weights_sum(or_filter* f)
 {
     if (f->sum_mode == OR_SUM_REFERENCE) {
         double s = 0;
-        for (uint64_t i = 0; i < f->n; ++i) s += f->w[i];
+        for (uint64_t i = 0; i < f->n; ++i) s += f->w[OD(i)];
         return s;
     }
     or_acc A = {{0}};
-    chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
+    chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
     combine_accs(f, &A, 1);
     return acc_value(&A, DM_FX_SCALE - f->wexp);
 }
@@ -1333,6 +1404,14 @@ double or_get_weights_sum(or_filter* f)
 /* ---- resample_stratified  src/ParticleFilter.hpp:85-108 ------------------------------------ */
 static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
 {
+#ifdef OR_AOS
+    uint8_t* nr = malloc((samples ? samples : 1) * OR_REC_BYTES);  /* whole 288-byte records */
+    const uint8_t* r = f->rec;
+    for (uint64_t k = 0; k < samples; ++k)
+        memcpy(nr + k * OR_REC_BYTES, r + (uint64_t)anc[k] * OR_REC_BYTES, OR_REC_BYTES);
+    free_state(f);
+    set_views(f, nr);
+#else
     double *nx = malloc(samples * 8), *ny = malloc(samples * 8), *nt = malloc(samples * 8), *nz = malloc(samples * 8),
            *ns = malloc(samples * 8), *nw = malloc(samples * 8), *nm = malloc(samples * 8);
     uint8_t *nf = malloc(samples), *nc = malloc(samples);
@@ -1341,8 +1420,9 @@ static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
         nx[k] = f->x[i]; ny[k] = f->y[i]; nt[k] = f->th[i]; nz[k] = f->z[i]; ns[k] = f->zs[i];
         nw[k] = f->w[i]; nm[k] = f->mprob[i]; nf[k] = f->floating[i]; nc[k] = f->ncp[i];
     }
-    free(f->x); free(f->y); free(f->th); free(f->z); free(f->zs); free(f->w); free(f->mprob); free(f->floating); free(f->ncp);
+    free_state(f);
     f->x = nx; f->y = ny; f->th = nt; f->z = nz; f->zs = ns; f->w = nw; f->mprob = nm; f->floating = nf; f->ncp = nc;
+#endif
     if (f->pm_key) {                      /* a copied particle carries its map (a deep copy) */
         uint32_t* nk = malloc(samples * OR_STORE_SLOTS * 4);
         float* nv = malloc(samples * OR_STORE_SLOTS * 8);
@@ -1366,19 +1446,19 @@ static void resample_stratified(or_filter* f, uint64_t samples, int shift)
     uint64_t overruns = 0;
     uint64_t idx = 0;
     if (f->sum_mode == OR_SUM_REFERENCE) {
-        double sum_w = f->w[idx];
+        double sum_w = f->w[OD(idx)];
         for (uint64_t k = 0; k < samples; ++k) {
             f->minstd = dm_minstd_next(f->minstd);
             double sum_r = ((double)k + dm_minstd_uniform(f->minstd)) / (double)samples;
             while (sum_w < sum_r) {
                 if (idx + 1 >= n) { overruns++; break; }   /* Q5: clamp instead of UB */
                 ++idx;
-                sum_w += f->w[idx];
+                sum_w += f->w[OD(idx)];
             }
             anc[k] = (uint32_t)idx;
         }
     } else {
-        uint64_t sum_w = dm_fx_shift(f->w[idx], shift);
+        uint64_t sum_w = dm_fx_shift(f->w[OD(idx)], shift);
         for (uint64_t k = 0; k < samples; ++k) {
             f->minstd = dm_minstd_next(f->minstd);
             double sum_r = ((double)k + dm_minstd_uniform(f->minstd)) / (double)samples;
@@ -1386,7 +1466,7 @@ static void resample_stratified(or_filter* f, uint64_t samples, int shift)
             while (sum_w < t) {
                 if (idx + 1 >= n) { overruns++; break; }
                 ++idx;
-                sum_w += dm_fx_shift(f->w[idx], shift);
+                sum_w += dm_fx_shift(f->w[OD(idx)], shift);
             }
             anc[k] = (uint32_t)idx;
         }
@@ -1418,7 +1498,7 @@ static void resample_sharded(or_filter* f, int shift)
     const int G = f->comm.nranks, me = f->comm.rank;
     const uint64_t N = f->n_global, n = f->n;
     uint64_t total = 0;
-    for (uint64_t i = 0; i < n; ++i) total += dm_fx_shift(f->w[i], shift);
+    for (uint64_t i = 0; i < n; ++i) total += dm_fx_shift(f->w[OD(i)], shift);
     uint64_t totals[ESLAM_ORACLE_MAX_RANKS];
     comm_allgather(f, &total, totals, 8);
     uint64_t off = 0;
@@ -1435,7 +1515,7 @@ static void resample_sharded(or_filter* f, int shift)
     while (k < N && T[k] <= c) ++k;
     for (uint64_t i = 0; i < n; ++i) {
         lo[i] = (f->gbase + i == 0) ? 0 : k;
-        c += dm_fx_shift(f->w[i], shift);
+        c += dm_fx_shift(f->w[OD(i)], shift);
         while (k < N && T[k] <= c) ++k;
         hi[i] = k;
         if (f->gbase + i == N - 1) { overruns = N - k; hi[i] = N; }
@@ -1460,9 +1540,9 @@ static void resample_sharded(or_filter* f, int shift)
             if (a >= b) continue;
             or_mig* m = &send[j++];
             memset(m, 0, sizeof(*m));
-            m->x = f->x[i]; m->y = f->y[i]; m->th = f->th[i]; m->z = f->z[i]; m->zs = f->zs[i];
-            m->w = f->w[i]; m->mprob = f->mprob[i];
-            m->floating = f->floating[i]; m->ncp = f->ncp[i];
+            m->x = f->x[OD(i)]; m->y = f->y[OD(i)]; m->th = f->th[OD(i)]; m->z = f->z[OD(i)]; m->zs = f->zs[OD(i)];
+            m->w = f->w[OD(i)]; m->mprob = f->mprob[OD(i)];
+            m->floating = f->floating[OB(i)]; m->ncp = f->ncp[OB(i)];
             m->lo = a; m->hi = b; m->src = f->gbase + i;
             if (f->pm_key) {
                 m->pm_count = f->pm_count[i];
@@ -1492,8 +1572,8 @@ static void resample_sharded(or_filter* f, int shift)
     free(recv);
     for (uint64_t o = 0; o < n; ++o) {
         const or_mig* m = &src[o];
-        f->x[o] = m->x; f->y[o] = m->y; f->th[o] = m->th; f->z[o] = m->z; f->zs[o] = m->zs;
-        f->w[o] = m->w; f->mprob[o] = m->mprob; f->floating[o] = m->floating; f->ncp[o] = m->ncp;
+        f->x[OD(o)] = m->x; f->y[OD(o)] = m->y; f->th[OD(o)] = m->th; f->z[OD(o)] = m->z; f->zs[OD(o)] = m->zs;
+        f->w[OD(o)] = m->w; f->mprob[OD(o)] = m->mprob; f->floating[OB(o)] = m->floating; f->ncp[OB(o)] = m->ncp;
         f->anc[o] = anc[o];
         if (f->pm_key) {
             f->pm_count[o] = m->pm_count;
@@ -1530,7 +1610,7 @@ void or_resample(or_filter* f)
     int shift = 60;
     if (f->sum_mode == OR_SUM_CONTRACT) {
         or_acc A = {{0}};
-        chunk_reduce(f->w, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
+        chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
         combine_accs(f, &A, 1);
         shift = 61 - (dm_weight_exp(acc_value(&A, DM_FX_SCALE - f->wexp)) + 1);
     }
@@ -1548,13 +1628,13 @@ void or_resample_multinomial(or_filter* f, uint64_t samples)
         double r = dm_minstd_uniform(f->minstd);
         double sum = 0;
         for (uint64_t i = 0; i < f->n; ++i) {
-            sum += f->w[i];
+            sum += f->w[OD(i)];
             if (r <= sum) { anc[m++] = (uint32_t)i; break; }
         }
     }
     gather(f, anc, m);
     f->n = m;
-    for (uint64_t i = 0; i < m; ++i) f->w[i] = 1.0 / (double)m;
+    for (uint64_t i = 0; i < m; ++i) f->w[OD(i)] = 1.0 / (double)m;
     free(anc);
 }
 
@@ -1610,7 +1690,7 @@ uint64_t or_best_index(or_filter* f)
     uint64_t index = 0;
     double weight = -INFINITY;
     for (uint64_t i = 0; i < f->n; ++i)
-        if (f->w[i] > weight) { index = i; weight = f->w[i]; }
+        if (f->w[OD(i)] > weight) { index = i; weight = f->w[OD(i)]; }
     if (f->sharded) {          /* the same scan over the ranks' results in rank order */
         double mine[2] = {weight, (double)(f->gbase + index)}, all[2 * ESLAM_ORACLE_MAX_RANKS];
         comm_allgather(f, mine, all, sizeof(mine));
@@ -1649,11 +1729,11 @@ static void centroid_contract(or_filter* f, double out[5])
             for (uint32_t j = 0; j < J; ++j) {
                 const uint64_t i = c * csz + 64ull * j + (uint64_t)l;
                 if (i >= f->n) continue;
-                const double w = f->w[i];
-                a[0] = a[0] + f->x[i] * w;
-                a[1] = a[1] + f->y[i] * w;
-                a[2] = a[2] + f->th[i] * w;
-                a[3] = a[3] + f->z[i] * w;
+                const double w = f->w[OD(i)];
+                a[0] = a[0] + f->x[OD(i)] * w;
+                a[1] = a[1] + f->y[OD(i)] * w;
+                a[2] = a[2] + f->th[OD(i)] * w;
+                a[3] = a[3] + f->z[OD(i)] * w;
                 a[4] = a[4] + w;
             }
             memcpy(lane[l], a, sizeof(a));
@@ -1706,11 +1786,11 @@ void or_get_centroid(or_filter* f, double position[3], double q[4])
         centroid_contract(f, s);
     } else {
         for (uint64_t i = 0; i < f->n; ++i) {
-            s[0] += f->x[i] * f->w[i];
-            s[1] += f->y[i] * f->w[i];
-            s[2] += f->th[i] * f->w[i];
-            s[3] += f->z[i] * f->w[i];
-            s[4] += f->w[i];
+            s[0] += f->x[OD(i)] * f->w[OD(i)];
+            s[1] += f->y[OD(i)] * f->w[OD(i)];
+            s[2] += f->th[OD(i)] * f->w[OD(i)];
+            s[3] += f->z[OD(i)] * f->w[OD(i)];
+            s[4] += f->w[OD(i)];
         }
         if (f->sharded) {
             double all[5 * ESLAM_ORACLE_MAX_RANKS];
@@ -1783,12 +1863,12 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
         float* val = f->pm_val + i * OR_STORE_SLOTS * 2;
         uint32_t count = f->pm_count[i];
         double sn, co;
-        dm_sincos(f->th[i], &sn, &co);
-        const double zvar = f->zs[i] * f->zs[i];
+        dm_sincos(f->th[OD(i)], &sn, &co);
+        const double zvar = f->zs[OD(i)] * f->zs[OD(i)];
         for (uint32_t k = 0; k < m; ++k) {
-            const double wx = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[i];
-            const double wy = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[i];
-            const double wz = sp[k].position[2] + f->z[i];
+            const double wx = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[OD(i)];
+            const double wy = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
+            const double wz = sp[k].position[2] + f->z[OD(i)];
             double lx = wx, ly = wy;
             if (!is_id) {
                 lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];

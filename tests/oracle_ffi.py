@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.join(ROOT, "slam-eslam_amd"))
 import eslam_abi as A  # noqa: E402
 
 LIB_PATH = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+# the same oracle with 288-byte particle records (-DOR_AOS, oracle/Makefile)
+LIB_PATH_AOS = os.path.join(ROOT, "oracle", "_build", "liboracle_aos.so")
 
 SUM_CONTRACT = 0
 SUM_REFERENCE = 1
@@ -46,16 +48,17 @@ def build():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def lib(aos=False):
+    """The oracle library: SoA state (default) or 288-byte AoS records (aos=True)."""
+    if aos in _libs:
+        return _libs[aos]
+    path = LIB_PATH_AOS if aos else LIB_PATH
+    if not os.path.exists(path):
         build()
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp = C.c_void_p
     L.or_create.restype = vp
     L.or_create.argtypes = [C.POINTER(A.Config), C.c_int]
@@ -120,7 +123,7 @@ def lib():
     L.or_dm_limbs_to_double.restype = C.c_double
     L.or_dm_limbs_to_double.argtypes = [C.POINTER(C.c_uint64), C.c_int]
     L.or_dm_fx128.argtypes = [C.c_double, C.c_int, C.POINTER(C.c_uint32)]
-    _lib = L
+    _libs[aos] = L
     return L
 
 
@@ -131,8 +134,8 @@ def dvec(v):
 class OracleFilter:
     """The oracle PoseEstimator / EmbodiedSlamFilter."""
 
-    def __init__(self, cfg, sum_mode=SUM_CONTRACT):
-        self.L = lib()
+    def __init__(self, cfg, sum_mode=SUM_CONTRACT, aos=False):
+        self.L = lib(aos)
         self.cfg = cfg
         self.h = self.L.or_create(C.byref(cfg), sum_mode)
         self._map = None
