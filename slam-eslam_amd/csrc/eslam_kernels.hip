@@ -348,21 +348,27 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     }
     double fm = floor((lx - kd(h, 4)) * kd(h, 2));
     double fn = floor((ly - kd(h, 5)) * kd(h, 3));
-    // non-short-circuit & of pure compares: selects, no exec-mask branches
-    const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
-    const int im = in_grid ? (int)fm : 0, in = in_grid ? (int)fn : 0;
     // fast path without branches: an in-window cell whose first patch passes the gate (the
     // window is only staged for maps without heights).  Everything else -- off the window,
-    // heights, a failing first patch of a multi-patch cell -- takes the loop below.
+    // heights, a failing first patch of a multi-patch cell -- takes the loop below.  The
+    // window lies inside the grid, so the window test alone decides the fast path: the
+    // conversions clamp out-of-range values (far outside the window) and only a NaN, which
+    // converts to 0, needs its own test.
+    int im, in;                          // v_cvt_i32_f64 itself: defined for every input
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(im) : "v"(fm));
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(in) : "v"(fn));
+    const bool num = (fm + fn) == (fm + fn);
     const WinBounds wb = win_bounds();
-    const bool in_win = in_grid & (wb.on != 0) & (im >= wb.m0) & (im < wb.m1) & (in >= wb.n0) & (in < wb.n1);
-    const WinCell wc = win.cells[in_win ? (in - wb.n0) * wb.cols + (im - wb.m0) : 0];
+    const uint32_t wm = (uint32_t)im - (uint32_t)wb.m0, wn = (uint32_t)in - (uint32_t)wb.n0;
+    const bool in_win = num & (wb.on != 0) & (wm < (uint32_t)wb.cols) & (wn < (uint32_t)(wb.n1 - wb.n0));
+    const WinCell wc = win.cells[in_win ? wn * (uint32_t)wb.cols + wm : 0u];
     const double pm = (double)wc.mean0, ps = (double)wc.stdev0;
     const double diff = dm_fabs(pm - lz);
     const bool gate0 = in_win & (wc.count > 0) & (diff * diff < 9.0 * (ps * ps + qv));
     mean = pm;
     stdev = ps;
     if (gate0) return true;
+    const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     if constexpr (DELTA) {
         if (!in_grid || (in_win && wc.count == 1)) return false;
         if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, lz, qv, mean, stdev);
@@ -718,6 +724,19 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #define K1_OCCUPANCY
 #endif
 
+#ifdef ESLAM_ABL_NO_PHILOX       // ablation builds only (timing, wrong bits)
+__device__ __forceinline__ dm_philox_ctr k1_draw(uint64_t seed, uint32_t, uint64_t ev, uint64_t gi, uint32_t call)
+{
+    dm_philox_ctr c;
+    const uint32_t h = (uint32_t)gi * 0x9E3779B9u ^ (uint32_t)seed ^ (uint32_t)ev ^ call;
+    c.v[0] = h; c.v[1] = h ^ 0x85ebca6bu; c.v[2] = h + 0xc2b2ae35u; c.v[3] = h ^ 0x27d4eb2fu;
+    return c;
+}
+#define K1_DRAW k1_draw
+#else
+#define K1_DRAW dm_draw
+#endif
+
 #ifdef ESLAM_ABL_NO_BM           // ablation builds only (timing, wrong bits)
 #define K1_BOX_MULLER(a, b, z0, z1) (*(z0) = dm_u32(a) - 0.5, *(z1) = dm_u32(b) - 0.5)
 #else
@@ -827,8 +846,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             const uint64_t gi = kq(key, 2) + i;
             // draw layout: call 0 -> two Box-Muller pairs (z0, z1), (z2, sn0);
             // call 1 -> slip test + slip factor, spread pair (sn1, sn2)
-            const dm_philox_ctr d0 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 0);
-            const dm_philox_ctr d1 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 1);
+            const dm_philox_ctr d0 = K1_DRAW(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 0);
+            const dm_philox_ctr d1 = K1_DRAW(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 1);
             double z0, z1, z2, sn0;
             K1_BOX_MULLER(d0.v[0], d0.v[1], &z0, &z1);
             K1_BOX_MULLER(d0.v[2], d0.v[3], &z2, &sn0);
@@ -921,15 +940,27 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             const uint32_t bucket = r.ncp < DM_NBUCKETS - 1 ? r.ncp : DM_NBUCKETS - 1;
             const double am = w * mprob;
             const double am2 = am * am;
-            // only the particle's bucket changes (adding +0.0 elsewhere, as the oracle's
-            // canonical sum does, can only turn a -0.0 into +0.0: same fixed point)
+            // per bucket b the lane adds am if it holds b, else +0.0 (the oracle's canonical
+            // per-bucket sums add +0.0 for the other buckets' particles: the same bits).  The
+            // wave walks its distinct buckets (usually one): each pass adds to one bucket's two
+            // sums, chosen by a scalar branch, instead of selecting over every bucket per lane.
+            // ncp <= MAXP: the buckets above MAXP stay empty
+            constexpr int kBuckets = MAXP + 1 < DM_NBUCKETS ? MAXP + 1 : DM_NBUCKETS;
+            uint64_t todo = __ballot(1);
+            do {
+                const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
+                const bool mine = bucket == b0;
+                const double a1 = mine ? am : 0.0, a2 = mine ? am2 : 0.0;
 #pragma unroll
-            for (int b = 0; b < DM_NBUCKETS; ++b) {
-                if (bucket == (uint32_t)b) {
-                    accA[b] = accA[b] + am;
-                    accB[b] = accB[b] + am2;
+                for (int b = 0; b < kBuckets; ++b) {
+                    if (b0 == (uint32_t)b) {
+                        asm volatile("");           // a real scalar branch, not a select per bucket
+                        accA[b] = accA[b] + a1;
+                        accB[b] = accB[b] + a2;
+                    }
                 }
-            }
+                todo &= ~__ballot(mine);
+            } while (todo);
             accSW = accSW + sw;
             flags = (r.ncp & 0x7fu) | (floating << 7);
             PROF(9);

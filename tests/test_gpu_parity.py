@@ -319,3 +319,35 @@ def test_zero_measurement_variance_stops_the_update(gpu_mod, oracle):
         assert_bit_identical(gpu.download(), orc.download(), f"zero-var step {k}")
         assert info_tuple(gpu.sync()) == info_tuple(orc.info()), k
     assert errors >= 2                              # the gate fired again after the first throw
+
+
+@pytest.mark.parametrize("case", ["nan_in_window", "far_and_inf"])
+def test_nonfinite_and_off_grid_particles(gpu_mod, rough_grid, case):
+    """Particles with NaN, infinite, far-off and grid-edge coordinates take the map lookup's
+    window test and its global fallback exactly as the oracle's getPatch: NaN coordinates
+    inside a staged LDS window (the cloud's box skips them), and off-grid values that clamp
+    in the cell conversion with the window off."""
+    n = 4096
+    rng = np.random.default_rng(5)
+    pa = A.ParticleArrays(n)
+    pa.x[:] = rng.normal(0.0, 0.1, n)
+    pa.y[:] = rng.normal(0.0, 0.1, n)
+    pa.orientation[:] = rng.normal(0.0, 0.05, n)
+    pa.zpos[:] = 0.18
+    pa.zsigma[:] = 0.5
+    pa.weight[:] = 1.0
+    pa.mprob[:] = 1.0
+    pa.floating[:] = 1
+    pa.n_contact_points[:] = 0
+    idx = rng.choice(n, 300, replace=False)
+    if case == "nan_in_window":
+        pa.x[idx[:100]] = math.nan
+        pa.y[idx[100:200]] = math.nan
+        pa.x[idx[200:]] = math.nan
+        pa.y[idx[200:]] = math.nan
+    else:
+        vals = np.array([math.inf, -math.inf, 1e12, -1e12, -10.05, 10.05, 9.999, -9.999, 3e9, -3e9])
+        pa.x[idx[:150]] = rng.choice(vals, 150)
+        pa.y[idx[150:]] = rng.choice(vals, 150)
+    cfg = S.bench_config(A.default_config(), n)
+    run_pair(cfg, rough_grid, S.step_stream(4), n, init=pa, gpu_factory=factory(gpu_mod), label=case)
