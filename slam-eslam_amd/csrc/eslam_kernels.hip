@@ -1582,12 +1582,21 @@ __device__ __forceinline__ uint64_t reduce_field(Shard* recs, int nrec, int t)
     return acc;
 }
 
-// recs: kNShard local shards (one GPU) or the gathered per-rank records (multi-GPU)
-__global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, int nrec, Ctl* __restrict__ ctl, FinParams fp)
+// LDS of the finalize: the combined shard fields, the exact sums A_b, B_b, SW as doubles and
+// the phase-B factors
+struct FinLds {
+    uint64_t s[kShardFields];
+    double acc[2 * DM_NBUCKETS + 1];
+    double f[DM_NBUCKETS];
+};
+
+// the finalize of one block (every thread calls it).  recs: kNShard local shards (one GPU)
+// or the gathered per-rank records (multi-GPU)
+__device__ __forceinline__ void finalize_block(Shard* __restrict__ recs, int nrec, Ctl* __restrict__ ctl, const FinParams& fp, FinLds& L)
 {
-    __shared__ uint64_t s[kShardFields];
-    __shared__ double s_acc[2 * DM_NBUCKETS + 1];     // exact sums A_b, B_b, SW as doubles
-    __shared__ double s_f[DM_NBUCKETS];
+    uint64_t* s = L.s;
+    double* s_acc = L.acc;
+    double* s_f = L.f;
     const int t = threadIdx.x;
     if (t < kShardFields) {
         s[t] = reduce_field(recs, nrec, t);
@@ -1701,6 +1710,12 @@ __global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, i
     }
 }
 
+__global__ void __launch_bounds__(kBlock) k_finalize(Shard* __restrict__ recs, int nrec, Ctl* __restrict__ ctl, FinParams fp)
+{
+    __shared__ FinLds L;
+    finalize_block(recs, nrec, ctl, fp, L);
+}
+
 // ---------------------------------------------------------------------------------------
 // count of stratified draws T_k = fx(((k + U_k) / N), shift) that are <= c
 // (U_k = boost uniform_real of the (k+1)-th minstd draw after x_start)
@@ -1778,6 +1793,61 @@ struct DrawCursor {
         return k;
     }
 };
+
+// phase B (updateWeights' second pass, src/PoseEstimator.cpp:332-344) + normalisation
+// (src/ParticleFilter.hpp:46-70) of one tile's items r * kBlock + tid, in place; v[r] is the
+// final weight (0 past the filter's end).  Every load of the tile is issued first (indices
+// clamped into the filter: no branches between them), so their latencies overlap instead of
+// costing one memory round trip per item.
+template <int ITEMS>
+__device__ __forceinline__ void phase_b_tile(const DevState& st, const ScanParams& sp, const Ctl* ctl, uint64_t t0,
+                                             uint32_t tid, double (&v)[ITEMS])
+{
+    const double S = ctl->S;
+    const bool uniform = ctl->uniform != 0;
+    const double inv_n = ctl->inv_n;
+    double f[DM_NBUCKETS];
+#pragma unroll
+    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
+    double mp[ITEMS];
+    uint32_t fl[ITEMS];
+    const uint64_t last = sp.n - 1;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
+        v[r] = st.w[i < sp.n ? i : last];
+    }
+    if (sp.phase_b) {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
+            const uint64_t ic = i < sp.n ? i : last;
+            fl[r] = st.flags[ic];
+            mp[r] = st.mprob[ic];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
+        double x = v[r];
+        if (sp.phase_b) {
+            const uint32_t ncp = fl[r] & 0x7fu;
+            const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
+            double fb = f[0];
+#pragma unroll
+            for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
+            const double factor = mp[r] * fb;
+            x *= factor;
+        }
+        if (sp.normalize) x = uniform ? inv_n : x / S;
+        if (i < sp.n) {
+            if (sp.phase_b || sp.normalize) st.w[i] = x;
+        } else {
+            x = 0.0;
+        }
+        v[r] = x;
+    }
+}
 
 // ---------------------------------------------------------------------------------------
 // k_normalize_scan (K3a): phase B + normalisation and the tile totals; k_segments (K3b):
@@ -1948,34 +2018,12 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     const bool resample = ctl->resample != 0;
     const DevState st = ctl->base ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
-    const double S = ctl->S;
-    const bool uniform = ctl->uniform != 0;
-    const double inv_n = ctl->inv_n;
     const int shift = ctl->scan_shift;
-    double f[DM_NBUCKETS];
-#pragma unroll
-    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
-
+    double v[ITEMS];
+    phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
     uint64_t fx_sum = 0;
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
-        if (i < sp.n) {
-            double v = st.w[i];
-            if (sp.phase_b) {
-                const uint32_t ncp = st.flags[i] & 0x7fu;
-                const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
-                double fb = f[0];
-#pragma unroll
-                for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
-                const double factor = st.mprob[i] * fb;
-                v *= factor;
-            }
-            if (sp.normalize) v = uniform ? inv_n : v / S;
-            if (sp.phase_b || sp.normalize) st.w[i] = v;
-            fx_sum += fx_shift(v, shift);
-        }
-    }
+    for (int r = 0; r < ITEMS; ++r) fx_sum += fx_shift(v[r], shift);   // 0 past the end
     if (!resample) {
         if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
         return;
@@ -2096,33 +2144,10 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
     {
         // phase B + normalisation, striped (coalesced); the values are staged in LDS for the
         // blocked scan below
-        const double S = ctl->S;
-        const bool uniform = ctl->uniform != 0;
-        const double inv_n = ctl->inv_n;
-        double f[DM_NBUCKETS];
+        double v[ITEMS];
+        phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
 #pragma unroll
-        for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const int k = r * kBlock + (int)tid;
-            const uint64_t i = t0 + (uint64_t)k;
-            double v = 0.0;
-            if (i < sp.n) {
-                v = st.w[i];
-                if (sp.phase_b) {
-                    const uint32_t ncp = st.flags[i] & 0x7fu;
-                    const uint32_t bucket = ncp < DM_NBUCKETS - 1 ? ncp : DM_NBUCKETS - 1;
-                    double fb = f[0];
-#pragma unroll
-                    for (int b = 1; b < DM_NBUCKETS; ++b) fb = (bucket == (uint32_t)b) ? f[b] : fb;
-                    const double factor = st.mprob[i] * fb;
-                    v *= factor;
-                }
-                if (sp.normalize) v = uniform ? inv_n : v / S;
-                if (sp.phase_b || sp.normalize) st.w[i] = v;
-            }
-            s_u.v[skew(k)] = v;
-        }
+        for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
     if (!resample) {
         if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
