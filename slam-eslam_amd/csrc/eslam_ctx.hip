@@ -593,7 +593,7 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
         for (int j = 0; j < 7; ++j) { *f[j] = (double*)p; p += al(cap * 8); }
         s.flags = (uint8_t*)p;
     }
-    const uint64_t ntiles = (cap + 2 * kBlock - 1) / (2 * kBlock);      // the smallest scan tile (scan_items)
+    const uint64_t ntiles = (cap + kBlock - 1) / kBlock;                // the smallest scan tile (scan_items)
     HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
@@ -1400,7 +1400,7 @@ static uint32_t scan_items(uint64_t n)
     static const int forced = [] {
         const char* e = getenv("ESLAM_SCAN_ITEMS");
         const int v = e ? atoi(e) : 0;
-        return (v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
+        return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
     }();
     if (forced) return (uint32_t)forced;
     // measured (tools/ab_items.sh, bench step at 256k / 1M / 4M / 16M): 2 items +19 % at

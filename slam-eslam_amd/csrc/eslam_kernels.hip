@@ -2834,6 +2834,7 @@ extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, 
 #define ESLAM_SEG(I) hipLaunchKernelGGL(k_normalize_segments<I>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, \
                                         tile_pub, marks, tile_first, jt)
     switch (sp->items) {
+    case 1: ESLAM_SEG(1); break;
     case 2: ESLAM_SEG(2); break;
     case 4: ESLAM_SEG(4); break;
     case 8: ESLAM_SEG(8); break;
