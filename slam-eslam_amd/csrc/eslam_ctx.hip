@@ -1391,9 +1391,9 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
     p.J = dm_chunk_rows(ctx->n_global);
 }
 
-// particles per thread of K3a/K3b on one GPU: small filters take 512-particle tiles so the
-// two scan kernels still spread over every CU (256k particles: 512 blocks instead of 128);
-// ESLAM_SCAN_ITEMS (2, 4, 8) overrides, for measurements.  Exact integer tile totals: the
+// particles per thread of the one-GPU K3: small filters take small tiles so the scan still
+// spreads over every CU (256k particles: 1024 blocks instead of 128); ESLAM_SCAN_ITEMS (1, 2,
+// 4, 8, 16) overrides, for measurements.  Exact integer tile totals: the
 // tile size never changes a result.
 static uint32_t scan_items(uint64_t n)
 {
@@ -1403,8 +1403,10 @@ static uint32_t scan_items(uint64_t n)
         return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
     }();
     if (forced) return (uint32_t)forced;
-    // measured (tools/ab_items.sh, bench step at 256k / 1M / 4M / 16M): 2 items +19 % at
-    // 256k, 2 or 4 items +4 % at 1M, 8 items best from 4M on (fewer tiles_before re-sums)
+    // measured (tools/ab_items.sh, bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
+    // 64k and 256k (over 2 items, themselves +19 % over 8 at 256k), 2 or 4 items +4 % at 1M,
+    // 8 items best from 4M on (fewer tiles_before re-sums)
+    if (n <= (1ull << 18)) return 1u;
     return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)kScanItems);
 }
 
