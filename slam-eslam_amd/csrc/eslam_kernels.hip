@@ -84,6 +84,20 @@ template <class T, class Op> __device__ __forceinline__ T wave_butterfly(T v, Op
     return v;
 }
 
+// one stage of a transposed xor butterfly over 2H totals per lane (see K1's chunk flush):
+// the lane with bit O set keeps the upper H totals, its partner the lower H, and each adds
+// the partner's copy of the totals it keeps
+template <int O, int H> __device__ __forceinline__ void transpose_add(double (&v)[16], uint32_t lane)
+{
+    const bool up = (lane & (uint32_t)O) != 0u;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const double send = up ? v[j] : v[H + j];
+        const double keep = up ? v[H + j] : v[j];
+        v[j] = keep + xor_lane<O>(send);
+    }
+}
+
 __device__ __forceinline__ double wave_sum_butterfly(double v)
 {
     return wave_butterfly(v, [](double a, double b) { return a + b; });
@@ -996,22 +1010,37 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     }
 
     if (WEIGHT) {
-        // chunk totals (sub-lane sums + xor butterfly) -> exact fixed point -> lane columns
+        // chunk totals (sub-lane sums + the xor butterfly of the sum contract) -> exact fixed
+        // point -> lane columns.  The butterfly runs transposed over the 2 * NB + 1 totals
+        // (padded to 16): at distances 32, 16, 8 and 4 each lane pair splits the totals it
+        // holds in halves and adds the half it keeps, so total q ends in lanes 4q..4q+3 after
+        // the same pairwise additions as its own butterfly (the same bits); distances 2 and 1
+        // finish it there, and each lane converts its total once and keeps limb lane & 3.
+        constexpr int kQ = 2 * DM_NBUCKETS + 1;
+        static_assert(kQ <= 16, "16 totals over the 64 lanes");
+        double v[16];
 #pragma unroll
-        for (int q = 0; q < 2 * DM_NBUCKETS + 1; ++q) {
-            double v = q < DM_NBUCKETS ? accA[q] : (q < 2 * DM_NBUCKETS ? accB[q - DM_NBUCKETS] : accSW);
-            const int scale = q < DM_NBUCKETS ? sa : (q < 2 * DM_NBUCKETS ? sb : DM_FX_SCALE);
-            if (__ballot(v != 0.0) != 0ull) {
-                v = wave_sum_butterfly(v);
-                uint32_t l[4] = {0, 0, 0, 0};
-                if (v != v) flag |= 1u << q;
-                else if (!dm_isfinite(v)) flag |= 1u << (q + 16);
-                else dm_fx128_limbs(v, scale, l);
-                if ((lane >> 2) == (uint32_t)q) {
-                    const uint32_t c = lane & 3u;
-                    limb += c == 0 ? l[0] : (c == 1 ? l[1] : (c == 2 ? l[2] : l[3]));
-                }
-            }
+        for (int q = 0; q < 16; ++q)
+            v[q] = q < DM_NBUCKETS ? accA[q] : (q < 2 * DM_NBUCKETS ? accB[q - DM_NBUCKETS] : (q == kQ - 1 ? accSW : 0.0));
+        transpose_add<32, 8>(v, lane);
+        transpose_add<16, 4>(v, lane);
+        transpose_add<8, 2>(v, lane);
+        transpose_add<4, 1>(v, lane);
+        double t = v[0];
+        t = t + xor_lane<2>(t);
+        t = t + xor_lane<1>(t);
+        const uint32_t q = lane >> 2;
+        const int scale = q < DM_NBUCKETS ? sa : (q < 2 * DM_NBUCKETS ? sb : DM_FX_SCALE);
+        const bool nan_ = t != t, inf_ = !nan_ && !dm_isfinite(t);
+        uint32_t l[4] = {0, 0, 0, 0};
+        if (!nan_ && !inf_) dm_fx128_limbs(t, scale, l);          // padding totals are 0: limbs 0
+        const uint32_t c = lane & 3u;
+        limb += c == 0 ? l[0] : (c == 1 ? l[1] : (c == 2 ? l[2] : l[3]));
+        const uint64_t mn = __ballot(nan_), mi = __ballot(inf_);
+#pragma unroll
+        for (int k = 0; k < kQ; ++k) {
+            if ((mn >> (4 * k)) & 1ull) flag |= 1u << k;
+            if ((mi >> (4 * k)) & 1ull) flag |= 1u << (k + 16);
         }
     }
         PROF(11);
