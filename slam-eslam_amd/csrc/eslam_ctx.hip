@@ -60,7 +60,7 @@ extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, cons
                                                   uint64_t* total, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl,
                                                       uint64_t* tile_pub, uint32_t* marks, uint32_t* tile_first,
-                                                      const uint32_t* jt, hipStream_t stream);
+                                                      const uint32_t* jt, const FusedFin* ff, hipStream_t stream);
 extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, uint64_t n, uint64_t gbase, Ctl* ctl,
                                                    const GatherView* gv, uint32_t aux, hipStream_t stream);
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
@@ -243,6 +243,8 @@ struct eslam_ctx {
     void* state_mem = nullptr;
     uint32_t* marks = nullptr;
     uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
+    uint64_t* fin_word = nullptr;           // the fused finalize's epoch word (after the tile words)
+    uint64_t fin_epoch = 0;                 // fused finalize launches so far
     uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total (sharded K3a), or
                                             // one GPU: tag << 61 | total published by K3 (zeroed at allocation)
     uint32_t scan_tag = 0;                  // the last K3 launch's tag (1..7)
@@ -596,8 +598,11 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     const uint64_t ntiles = (cap + kBlock - 1) / kBlock;                // the smallest scan tile (scan_items)
     HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
-    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ntiles * 8));
-    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, ntiles * 8));                  // tag 0: never published
+    // the tile words, then (in a line of its own) the fused finalize's epoch word
+    const uint64_t fin_at = (ntiles + 15) & ~15ull;
+    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, (fin_at + 16) * 8));
+    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, (fin_at + 16) * 8));          // tag / epoch 0: never published
+    ctx->fin_word = ctx->tile_sum + fin_at;
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
     if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     if (particle_maps(ctx)) {
@@ -1574,16 +1579,30 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     return ESLAM_OK;
 }
 
+// ESLAM_FUSED_FINALIZE=0 keeps the separate k_finalize launch (measurements; same results)
+static bool fused_finalize()
+{
+    static const bool on = [] {
+        const char* e = getenv("ESLAM_FUSED_FINALIZE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     if (ctx->sharded) return run_update_tail_multi(ctx, mode, timed);
     const FinParams fp = fin_params(ctx, mode);
-    HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
+    // an update step folds the finalize into K3's block 0 (one launch fewer per step); the
+    // standalone normalise / resample / sum keep k_finalize
+    const bool fused = mode == FIN_UPDATE && fused_finalize();
+    if (!fused) HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, false);
     sp.tag = ctx->scan_tag = ctx->scan_tag % 7u + 1u;         // differs from the previous launch's
+    FusedFin ff{ctx->shards, fp, ctx->fin_word, ++ctx->fin_epoch};
     HIPCHK(ctx, eslam_launch_normalize_segments(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->marks,
-                                                ctx->tile_first, ctx->jump, ctx->stream));
+                                                ctx->tile_first, ctx->jump, fused ? &ff : nullptr, ctx->stream));
     if (timed) rec(ctx, 3);
     // the gather itself is fused into the next k_project_weight (or materialize())
     if (timed) rec(ctx, 4);

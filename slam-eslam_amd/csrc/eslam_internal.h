@@ -68,6 +68,8 @@ struct alignas(128) Ctl {
     uint64_t update_count;
     uint64_t err;
     uint64_t bbox[4];                    // particle bounding box of the last weighting (keys)
+    uint32_t k3_base;                    // the buffer the last weighting kernel wrote (base ^ flip at
+                                         // its start): the fused K3 reads it while block 0 commits
 };
 
 enum FinMode : uint32_t {
@@ -228,6 +230,16 @@ struct FinParams {
     Shard* local_shards;
     uint64_t* mirror;
 };
+
+// the finalize fused into the one-GPU K3 (k_normalize_segments<ITEMS, true>): block 0 runs
+// k_finalize's block over the local shards and publishes epoch in *fin_word
+struct FusedFin {
+    Shard* shards;
+    FinParams fp;
+    uint64_t* fin_word;
+    uint64_t epoch;
+};
+
 
 struct ScanParams {
     uint64_t n, gbase, n_global;

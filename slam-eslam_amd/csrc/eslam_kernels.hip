@@ -773,6 +773,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     // write the updated particles to state[base ^ 1] (the latest buffer)
     const uint32_t gath = ctl->gather;
     const uint32_t cur = ctl->base ^ ctl->flip;
+    if (WEIGHT && blockIdx.x == 0 && threadIdx.x == 0) ctl->k3_base = cur;
     const uint32_t st_off = __builtin_amdgcn_readfirstlane(cur ? KOFF(s[1]) : KOFF(s[0]));
     const uint32_t si_off = __builtin_amdgcn_readfirstlane(gath ? (ctl->base ? KOFF(s[1]) : KOFF(s[0])) : st_off);
     const int wexp = ctl->wexp;
@@ -1828,18 +1829,17 @@ struct DrawCursor {
 // final weight (0 past the filter's end).  Every load of the tile is issued first (indices
 // clamped into the filter: no branches between them), so their latencies overlap instead of
 // costing one memory round trip per item.
-template <int ITEMS>
-__device__ __forceinline__ void phase_b_tile(const DevState& st, const ScanParams& sp, const Ctl* ctl, uint64_t t0,
-                                             uint32_t tid, double (&v)[ITEMS])
+__device__ __forceinline__ uint32_t sgpr_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ double sgpr_f64(double v)
 {
-    const double S = ctl->S;
-    const bool uniform = ctl->uniform != 0;
-    const double inv_n = ctl->inv_n;
-    double f[DM_NBUCKETS];
-#pragma unroll
-    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = ctl->f[b];
-    double mp[ITEMS];
-    uint32_t fl[ITEMS];
+    const uint64_t b = dm_bits(v);
+    return dm_from_bits(((uint64_t)sgpr_u32((uint32_t)(b >> 32)) << 32) | sgpr_u32((uint32_t)b));
+}
+
+template <int ITEMS>
+__device__ __forceinline__ void phase_b_load(const DevState& st, const ScanParams& sp, uint64_t t0, uint32_t tid,
+                                             double (&v)[ITEMS], double (&mp)[ITEMS], uint32_t (&fl)[ITEMS])
+{
     const uint64_t last = sp.n - 1;
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -1855,6 +1855,21 @@ __device__ __forceinline__ void phase_b_tile(const DevState& st, const ScanParam
             mp[r] = st.mprob[ic];
         }
     }
+}
+
+// ctl: k_finalize's outputs (S, uniform, inv_n, f)
+template <int ITEMS>
+__device__ __forceinline__ void phase_b_apply(const DevState& st, const ScanParams& sp, const Ctl* ctl, uint64_t t0,
+                                              uint32_t tid, double (&v)[ITEMS], const double (&mp)[ITEMS],
+                                              const uint32_t (&fl)[ITEMS])
+{
+    // block-uniform values (the fused K3 reads them from LDS): kept in SGPRs
+    const double S = sgpr_f64(ctl->S);
+    const bool uniform = sgpr_u32(ctl->uniform) != 0;
+    const double inv_n = sgpr_f64(ctl->inv_n);
+    double f[DM_NBUCKETS];
+#pragma unroll
+    for (int b = 0; b < DM_NBUCKETS; ++b) f[b] = sgpr_f64(ctl->f[b]);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
@@ -1876,6 +1891,47 @@ __device__ __forceinline__ void phase_b_tile(const DevState& st, const ScanParam
         }
         v[r] = x;
     }
+}
+
+template <int ITEMS>
+__device__ __forceinline__ void phase_b_tile(const DevState& st, const ScanParams& sp, const Ctl* ctl, uint64_t t0,
+                                             uint32_t tid, double (&v)[ITEMS])
+{
+    double mp[ITEMS];
+    uint32_t fl[ITEMS];
+    phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
+    phase_b_apply<ITEMS>(st, sp, ctl, t0, tid, v, mp, fl);
+}
+
+// ---------------------------------------------------------------------------------------
+// The fused finalize (one-GPU update step): block 0 of K3 runs k_finalize's block
+// (finalize_block) and then publishes the launch's epoch in one word with an agent-scope
+// release store; every block waits for that word (one lane polls, with a sleep) and copies
+// the control block into LDS with agent-scope loads (its lines may be stale in this XCD's
+// L2).  Block 0 is dispatched first and waits on nothing before it publishes, so the wait
+// terminates; a bounded spin turns a violated assumption into ctl->err bit 2.  The epoch is
+// a per-context launch counter: a word left by an earlier launch never equals it.
+// ---------------------------------------------------------------------------------------
+constexpr int kCtlWords = (int)(sizeof(Ctl) / 8);
+static_assert(sizeof(Ctl) % 8 == 0 && kCtlWords <= 64, "the control block is copied by one wave");
+
+__device__ __forceinline__ void fin_wait_copy(const Ctl* ctl, const uint64_t* fin_word, uint64_t epoch, uint64_t* s_img,
+                                              Ctl* ctl_err)
+{
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) {
+        bool timeout = false;
+        if (tid == 0) {
+            uint32_t spins = 0;
+            while (atomic_load_agent(fin_word) != epoch) {
+                if (++spins == (1u << 18)) { timeout = true; break; }      // x s_sleep(8): ~60 ms
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        if (tid < (uint32_t)kCtlWords) s_img[tid] = atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + tid);
+        if (timeout) atomicOr((unsigned long long*)&ctl_err->err, 4ull);
+    }
+    __syncthreads();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2148,43 +2204,75 @@ __device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, 
 #ifdef ESLAM_K3_WAVES                    // experiment builds: waves per SIMD of the fused K3
 #define K3_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ESLAM_K3_WAVES, ESLAM_K3_WAVES)))
 #else
-#define K3_OCCUPANCY
+// 8 items: the 6 waves per SIMD the unfused kernel reaches by itself (<= 80 VGPRs; the fused
+// one would take 86 and run at 5)
+#define K3_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? 6 : 1)))
 #endif
 
-template <int ITEMS>
+template <int ITEMS, bool FUSED>
 __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                                uint64_t* __restrict__ tile_pub, uint32_t* __restrict__ marks,
                                                                uint32_t* __restrict__ tile_first,
-                                                               const uint32_t* __restrict__ jt)
+                                                               const uint32_t* __restrict__ jt, FusedFin ff)
 {
     __shared__ uint64_t s_wtot[kWaves], s_red[kWaves];
     __shared__ K3Lds<ITEMS> s_u;
+    __shared__ uint64_t s_img[FUSED ? kCtlWords : 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
-    if (ctl->aborted) {                  // the update threw (k_finalize): weights stay as phase A left them
-        if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
-        return;
+    if constexpr (FUSED) {
+        if (tile == 0) {
+            __shared__ FinLds s_fin;
+            finalize_block(ff.shards, kNShard, ctl, ff.fp, s_fin);
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    PROF_INIT();
-    const bool resample = ctl->resample != 0;
-    const DevState st = ctl->base ? s1 : s0;
+    // the finalize's outputs: ctl itself (k_finalize ran before this launch), or its copy in
+    // LDS once block 0 has published (fused)
+    const Ctl* cv = FUSED ? reinterpret_cast<const Ctl*>(s_img) : ctl;
+    // the buffer the weighting kernel wrote (= base after the finalize's commit)
+    const DevState st = (FUSED ? ctl->k3_base : ctl->base) ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
+    bool resample = false;
+    if constexpr (!FUSED) {
+        if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
+            if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+            return;
+        }
+        resample = cv->resample != 0;
+    }
     {
         // phase B + normalisation, striped (coalesced); the values are staged in LDS for the
-        // blocked scan below
+        // blocked scan below.  Fused: the loads do not depend on the finalize, so they are
+        // issued before its wait.
         double v[ITEMS];
-        phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
+        if constexpr (FUSED) {
+            double mp[ITEMS];
+            uint32_t fl[ITEMS];
+            phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
+            fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, ctl);
+            if (cv->aborted) {           // the update threw (k_finalize): weights stay as phase A left them
+                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+                return;
+            }
+            phase_b_apply<ITEMS>(st, sp, cv, t0, tid, v, mp, fl);
+            resample = sgpr_u32(cv->resample) != 0;
+        } else {
+            phase_b_tile<ITEMS>(st, sp, cv, t0, tid, v);
+        }
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
+    PROF_INIT();
     if (!resample) {
         if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
         return;
     }
     __syncthreads();
     PROF(0);
-    const int shift = ctl->scan_shift;
+    const int shift = (int)sgpr_u32((uint32_t)cv->scan_shift);
     uint64_t c[ITEMS];
     const uint64_t run = blocked_fx(s_u.v, shift, c);
     PROF(1);
@@ -2211,7 +2299,7 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
     PROF(3);
 
     const uint64_t N = sp.n_global;
-    const uint32_t xs = ctl->minstd_start;
+    const uint32_t xs = sgpr_u32(cv->minstd_start);
     const double dN = (double)N, inv_N = 1.0 / dN;
     const uint64_t i0 = t0 + (uint64_t)tid * ITEMS;
     // the wave's cumulative range [wlo, whi]: every count it needs reads only draws in
@@ -2856,12 +2944,18 @@ extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, cons
 
 extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl,
                                                       uint64_t* tile_pub, uint32_t* marks, uint32_t* tile_first,
-                                                      const uint32_t* jt, hipStream_t stream)
+                                                      const uint32_t* jt, const FusedFin* ff, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
     if (sp->tag < 1 || sp->tag > 7) return hipErrorInvalidValue;
-#define ESLAM_SEG(I) hipLaunchKernelGGL(k_normalize_segments<I>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, \
-                                        tile_pub, marks, tile_first, jt)
+    if (ff && (!ff->shards || !ff->fin_word || ff->fp.mode != FIN_UPDATE || ff->fp.mirror)) return hipErrorInvalidValue;
+    const FusedFin none{};
+#define ESLAM_SEG(I) do { \
+        if (ff) hipLaunchKernelGGL((k_normalize_segments<I, true>), dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, \
+                                   tile_pub, marks, tile_first, jt, *ff); \
+        else hipLaunchKernelGGL((k_normalize_segments<I, false>), dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, \
+                                tile_pub, marks, tile_first, jt, none); \
+    } while (0)
     switch (sp->items) {
     case 1: ESLAM_SEG(1); break;
     case 2: ESLAM_SEG(2); break;
