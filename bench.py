@@ -361,7 +361,9 @@ def main():
                      "avg_launch_ms": round(dom_ms, 5)},
         "kernel_ms": {k: round(v, 5) for k, v in kt.items()},
         "kernel_ms_note": "HIP events around every launch on the context stream, over a second pass of "
-                          "the same K steps (ms_per_step with events: %.4f)" % (dt_ev / args.steps * 1e3),
+                          "the same K steps (ms_per_step with events: %.4f); single-GPU update steps fold the finalize "
+                          "into k_normalize_segments (block 0), so finalize_ms times an empty region there"
+                          % (dt_ev / args.steps * 1e3),
         "step_roofline_frac": round(BYTES_STEP * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world), 4),
         "step_roofline_note": "%d B per particle-update: the fused step's algorithmic bytes (K1 %d + K3 %d); the "
                               "reference algorithm's unfused passes would move %d B (fraction %.4f)"

@@ -1628,6 +1628,15 @@ __device__ __forceinline__ void finalize_block(Shard* __restrict__ recs, int nre
     double* s_acc = L.acc;
     double* s_f = L.f;
     const int t = threadIdx.x;
+    // the control fields the finalize reads, loaded with the shards (one memory round trip)
+    const int wexp_ = ctl->wexp;
+    uint32_t base0 = 0, flip0 = 0, minstd0 = 0;
+    double last_max = 0.0;
+    uint64_t updates0 = 0;
+    if (t == 0) {
+        base0 = ctl->base; flip0 = ctl->flip; minstd0 = ctl->minstd;
+        last_max = ctl->max_weight; updates0 = ctl->update_count;
+    }
     if (t < kShardFields) {
         s[t] = reduce_field(recs, nrec, t);
         // multi-GPU: the local shards were all-gathered (stream order: already read)
@@ -1638,7 +1647,6 @@ __device__ __forceinline__ void finalize_block(Shard* __restrict__ recs, int nre
     {
         // the 13 fixed-point -> double conversions, one per lane (same values as serially)
         const uint64_t flags_ = s[2 * DM_NBUCKETS * 4 + 7];
-        const int wexp_ = ctl->wexp;
         if (t < 2 * DM_NBUCKETS + 1) {
             const int scale = t < DM_NBUCKETS ? DM_FX_SCALE - wexp_
                             : (t < 2 * DM_NBUCKETS ? DM_FX_SCALE - 2 * wexp_ : DM_FX_SCALE);
@@ -1663,10 +1671,10 @@ __device__ __forceinline__ void finalize_block(Shard* __restrict__ recs, int nre
         for (int q = 0; q < 4; ++q) ctl->bbox[q] = s[2 * DM_NBUCKETS * 4 + 9 + q];
     }
     // commit the previous resample's buffer flip
-    ctl->base ^= ctl->flip;
+    ctl->base = base0 ^ flip0;
     ctl->flip = 0;
     ctl->gather = 0;
-    ctl->err |= err;
+    if (err) atomicOr((unsigned long long*)&ctl->err, (unsigned long long)err);   // K3 blocks may OR in too
     ctl->tile_counter = 0;
     ctl->overruns = 0;
     ctl->aborted = 0;
@@ -1692,13 +1700,13 @@ __device__ __forceinline__ void finalize_block(Shard* __restrict__ recs, int nre
             Q = Q + (fb * fb) * s_acc[DM_NBUCKETS + b];
         }
         ctl->fw = fw;
-        const double last = ctl->max_weight;
+        const double last = last_max;
         double mw = maxm;
         if (TP == 0) mw = last * fp.discount;
         ctl->max_weight = mw;
         ctl->data_particles = D;
         ctl->total_points = TP;
-        ctl->update_count += 1;
+        ctl->update_count = updates0 + 1;
     } else {
         S = s_acc[0];
         Q = s_acc[DM_NBUCKETS];
@@ -1729,12 +1737,12 @@ __device__ __forceinline__ void finalize_block(Shard* __restrict__ recs, int nre
     }
     if (fp.mirror) {
         fp.mirror[0] = ctl->resample;
-        fp.mirror[1] = ctl->resample ? ctl->minstd : ctl->minstd_start;   // minstd_start below
+        fp.mirror[1] = ctl->resample ? minstd0 : ctl->minstd_start;      // minstd_start below
         fp.mirror[2] = (uint64_t)(int64_t)ctl->scan_shift;
     }
     if (ctl->resample) {
-        ctl->minstd_start = ctl->minstd;
-        ctl->minstd = dm_mulmod31(fp.minstd_jump_n, ctl->minstd);   // A^N, precomputed
+        ctl->minstd_start = minstd0;
+        ctl->minstd = dm_mulmod31(fp.minstd_jump_n, minstd0);       // A^N, precomputed
         ctl->flip = 1;
         ctl->gather = 1;
     }
