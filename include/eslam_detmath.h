@@ -880,18 +880,23 @@ DM_FN uint32_t dm_store_hash(uint32_t cell) { return (cell * 2654435761u) >> 27;
 
 #define DM_NBUCKETS 6            /* cpoints.size() buckets 0,1,2,3,4,>=5 (phase B)     */
 
-/* J = the largest power of two <= min(16, n_global / 2^19): from 512k particles on there are
- * ~8192 chunks of 64 x J (the weighting kernel runs one chunk per wave: 4M particles give
- * 8 rows per wave, 8192 waves = 2 refills of the 256 CUs x 4 waves per SIMD; measured 2-3 %
- * faster K1 than 2^20, interleaved A/B on MI355X)                                       */
+/* J = the largest power of two <= min(8, n_global / 2^18): from 256k particles on there are
+ * ~4096 chunks of 64 x J up to 2M, and 8 rows per chunk beyond (the weighting kernel runs one
+ * chunk per wave; 4096 waves fill the 256 CUs x 4 waves per SIMD once).  Measured on MI355X
+ * (interleaved A/B against 2^19 and a cap of 16): 1M +6.5 %, 2M +3 %, 4M unchanged per step;
+ * the cap of 8 keeps a sharded rank at 4096 waves per GPU (configs[3]: 16M over 8 GPUs, 2M
+ * per GPU), where 16 rows would leave 2 waves per SIMD.                                   */
 #ifndef ESLAM_CHUNK_UNIT                 /* experiment builds only (changes the sum order) */
-#define ESLAM_CHUNK_UNIT 524288u
+#define ESLAM_CHUNK_UNIT 262144u
+#endif
+#ifndef ESLAM_CHUNK_CAP
+#define ESLAM_CHUNK_CAP 8u
 #endif
 DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
 {
     uint64_t q = n_global / ESLAM_CHUNK_UNIT;
     uint32_t j = 1;
-    while (j < 16u && (uint64_t)(j * 2u) <= q) j *= 2u;
+    while (j < ESLAM_CHUNK_CAP && (uint64_t)(j * 2u) <= q) j *= 2u;
     return j;
 }
 

@@ -210,9 +210,9 @@ MAX_RANKS = 16
 
 def chunk_rows(n_global):
     """dm_chunk_rows (include/eslam_detmath.h): rows of 64 lanes per canonical summation chunk."""
-    q = n_global // 524288
+    q = n_global // 262144
     j = 1
-    while j < 16 and j * 2 <= q:
+    while j < 8 and j * 2 <= q:
         j *= 2
     return j
 

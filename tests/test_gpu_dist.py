@@ -37,10 +37,10 @@ def test_sharded_gpu_native_rccl_one_rank(oracle, tmp_path, name, n_global):
 
 @pytest.mark.parametrize("mem,world", [("host", 2), ("rccl", 1)])
 def test_sharded_gpu_two_row_chunks(oracle, tmp_path, mem, world):
-    """1.05M particles: canonical summation chunks of two rows (dm_chunk_rows = 2), which
+    """525k particles: canonical summation chunks of two rows (dm_chunk_rows = 2), which
     the small cases above never reach, through gloo (2 ranks) and the library's RCCL."""
     import eslam_abi as A
-    n_global = 1050000
+    n_global = 525000
     assert A.chunk_rows(n_global) == 2
     want = single_oracle("forced", n_global)
     got = merge(launch("gpu", "forced", n_global, world, str(tmp_path), mem=mem, timeout=280))

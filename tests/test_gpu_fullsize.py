@@ -41,7 +41,7 @@ def test_rough_terrain_4m_bit_exact(gpu_mod):
              gpu_factory=lambda c: gpu_mod.GpuFilter(c), label="rough 4M", oracle_threads=16)
 
 
-@pytest.mark.parametrize("n", [1, 63, 65, 2 * 524288 + 4097])
+@pytest.mark.parametrize("n", [1, 63, 65, 2 * 262144 + 4097])
 def test_edge_sizes_bit_exact(gpu_mod, n):
     """single particle, partial first row, one row + 1, and a ragged two-row-chunk layout"""
     grid = S.flat_map(cells=200)
