@@ -757,6 +757,17 @@ __device__ __forceinline__ dm_philox_ctr k1_draw(uint64_t seed, uint32_t, uint64
 #define K1_BOX_MULLER dm_box_muller32
 #endif
 
+// The state written by K1 (and w by K3) is streamed: each value is read once, by the next
+// kernel, from another XCD.  Non-temporal stores (nt) leave fewer lines for the kernel-end L2
+// writeback (interleaved A/B on MI355X: 256k +3 %, 4M +0.7 %, 16M +1.6 % per step; plain
+// stores and agent-coherent sc1 stores measured beside them).  Same values, same bits.
+#define K1_ST(p, v) __builtin_nontemporal_store((v), (p))
+#ifdef ESLAM_NT_LOADS                    // experiment: streaming loads of the state as well
+#define K1_LD(p) __builtin_nontemporal_load(p)
+#else
+#define K1_LD(p) (*(p))
+#endif
+
 template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false>
 __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a)
 {
@@ -845,7 +856,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             mp_in = rc->mprob; fl_in = (uint8_t)rc->src;
         } else {
             const StatePtrs si = kstate(si_off);
-            x = si.x[src]; y = si.y[src]; th = si.th[src]; z = si.z[src]; zs = si.zs[src]; w = si.w[src];
+            x = K1_LD(si.x + src); y = K1_LD(si.y + src); th = K1_LD(si.th + src); z = K1_LD(si.z + src);
+            zs = K1_LD(si.zs + src); w = K1_LD(si.w + src);
             if (!WEIGHT && gath) { mp_in = si.mprob[src]; fl_in = si.flags[src]; }
         }
         if (gath && rec_anc) {
@@ -986,18 +998,18 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         // all stores of the row at the end: one scalar load of the output pointers
         const StatePtrs st = kstate(st_off);
         if (PROJECT || gath) {
-            st.x[i] = x;
-            st.y[i] = y;
-            st.th[i] = th;
+            K1_ST(st.x + i, x);
+            K1_ST(st.y + i, y);
+            K1_ST(st.th + i, th);
         }
         if (WEIGHT || gath) {
-            st.mprob[i] = mprob;
-            st.flags[i] = (uint8_t)flags;
+            K1_ST(st.mprob + i, mprob);
+            K1_ST(st.flags + i, (uint8_t)flags);
         }
         if (PROJECT || WEIGHT) {
-            st.z[i] = z;
-            st.zs[i] = zs;
-            if (gath || w != w_in || w != w) st.w[i] = w;
+            K1_ST(st.z + i, z);
+            K1_ST(st.zs + i, zs);
+            if (gath || w != w_in || w != w) K1_ST(st.w + i, w);
         }
         {
             // v_max_f32 returns the other operand for a NaN: NaN coordinates are skipped
@@ -1852,15 +1864,15 @@ __device__ __forceinline__ void phase_b_load(const DevState& st, const ScanParam
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
-        v[r] = st.w[i < sp.n ? i : last];
+        v[r] = K1_LD(st.w + (i < sp.n ? i : last));
     }
     if (sp.phase_b) {
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
             const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
             const uint64_t ic = i < sp.n ? i : last;
-            fl[r] = st.flags[ic];
-            mp[r] = st.mprob[ic];
+            fl[r] = K1_LD(st.flags + ic);
+            mp[r] = K1_LD(st.mprob + ic);
         }
     }
 }
@@ -1893,7 +1905,7 @@ __device__ __forceinline__ void phase_b_apply(const DevState& st, const ScanPara
         }
         if (sp.normalize) x = uniform ? inv_n : x / S;
         if (i < sp.n) {
-            if (sp.phase_b || sp.normalize) st.w[i] = x;
+            if (sp.phase_b || sp.normalize) K1_ST(st.w + i, x);
         } else {
             x = 0.0;
         }
