@@ -1670,7 +1670,7 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
         rc = grow(ctx, &ctx->hsend, &ctx->hsend_cap, G * cnt[me] * 8 + 8, false);
         if (!rc) rc = grow(ctx, &ctx->hrecv, &ctx->hrecv_cap, total * 8 + 8, false);
         size_t sbytes = 0;
-        eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, total, nullptr, &sbytes, ctx->stream);
+        (void)eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, total, nullptr, &sbytes, ctx->stream);
         if (!rc) rc = grow(ctx, &ctx->hsort, &ctx->hsort_cap, 16 * (total + 1) + sbytes, false);
         if (rc) return rc;
         HIPCHK(ctx, eslam_launch_hash_candidates(keys_out, order, cnt[me], ctx->gbase, G, ctx->hsend, ctx->stream));
@@ -2091,7 +2091,7 @@ extern "C" int eslam_gpu_selftest_sort(int device, const uint32_t* keys, const u
     if ((!keys || !vals || !keys_out || !vals_out) && n) return ESLAM_ERR_INVALID_ARG;
     if (hipSetDevice(device) != hipSuccess) return ESLAM_ERR_HIP;
     size_t bytes = 0;
-    eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, n, nullptr, &bytes, nullptr);
+    (void)eslam_radix_sort_pairs(nullptr, nullptr, nullptr, nullptr, n, nullptr, &bytes, nullptr);
     const uint64_t b = (n ? n : 1) * 4;
     uint32_t* d = nullptr;
     void* tmp = nullptr;

@@ -262,7 +262,7 @@ extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uin
         uint32_t* ko = (pass & 1) ? keys_out : tk;
         uint32_t* vo = (pass & 1) ? order : tv;
         hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kBlock), 0, stream, ki, n, 8 * pass, hist, ntiles);
-        eslam_launch_scan_excl(hist, hist_words, stream);
+        (void)eslam_launch_scan_excl(hist, hist_words, stream);
         hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kBlock), 0, stream, ki, vi, ko, vo, n, 8 * pass, hist, ntiles);
         ki = ko;
         vi = vo;

@@ -1782,7 +1782,7 @@ __device__ __forceinline__ uint64_t fx_unit(double q, int shift)
     const uint64_t m = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
     const int sh = (int)e - 1075 + shift;
     const uint64_t r = sh >= 0 ? (m << (sh & 63)) : (m >> ((-sh) & 63));
-    return (e == 0u) | (sh <= -64) ? 0ull : r;
+    return ((e == 0u) | (sh <= -64)) ? 0ull : r;
 }
 
 // T_k = fx((k + U_k) / N): both divisions as dm_div_recip (bit-identical to "/", checked by
