@@ -1469,6 +1469,20 @@ static int abort_pending_gather(eslam_ctx* ctx, hipError_t e, int rc = ESLAM_ERR
     return rc;
 }
 
+// host spin bound of the sharded step's wait for the slice totals (ESLAM_SPIN_US, microseconds;
+// measurements).  The wait starts while the step's weighting kernel still runs; a 2 ms bound
+// (which covers K1 + the exchanges of a 4M shard) measured the same as 200 us on one rank at
+// 2M and 4M (profiles/r02/ab_spin.log), so the shorter bound stays
+static long spin_bound_us()
+{
+    static const long us = [] {
+        const char* e = getenv("ESLAM_SPIN_US");
+        const long v = e ? atol(e) : 200;
+        return v < 0 ? 0 : v;
+    }();
+    return us;
+}
+
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const int G = ctx->comm.nranks, me = ctx->comm.rank;
@@ -1501,12 +1515,13 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     // wakes the thread tens of microseconds late, and the GPU runs dry before the next
     // step's launches if the host is late here (the segments kernel is all it has queued)
     {
-        // bounded: after ~200 us (a hung collective or kernel, or a late GPU) fall back to a
-        // blocking wait instead of burning a host core next to the RCCL proxy threads
+        // bounded (spin_bound_us): past it (a hung collective or kernel, or a late GPU) fall
+        // back to a blocking wait instead of burning a host core next to the RCCL proxy threads
         hipError_t q;
         const auto t0 = std::chrono::steady_clock::now();
+        const auto bound = std::chrono::microseconds(spin_bound_us());
         while ((q = hipEventQuery(ctx->ev[0])) == hipErrorNotReady) {
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+            if (std::chrono::steady_clock::now() - t0 > bound) {
                 q = hipEventSynchronize(ctx->ev[0]);
                 break;
             }
