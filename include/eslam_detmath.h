@@ -89,6 +89,28 @@ DM_FN double dm_horner_k(const double* c, int n, double u)
 DM_FN double dm_sqrt(double x) { return __builtin_sqrt(x); }
 DM_FN double dm_floor(double x) { return __builtin_floor(x); }
 
+/* a / b correctly rounded, for operands that need none of the device division's scaling
+ * (|b| and |a / b| well inside the normal range, a == 0 allowed) and no special-value
+ * fix-up (finite a, b != 0).  On the device it is the compiler's own fp64 division sequence
+ * (v_rcp_f64, two Newton steps, the quotient and its one correction) without v_div_scale /
+ * v_div_fixup, which return their inputs unchanged for such operands, so the bits are those
+ * of the division; the host divides.  Callers state why their operands qualify.          */
+DM_FN double dm_div_inrange(double a, double b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y0 = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y0, 1.0);
+    const double y1 = __builtin_fma(y0, e, y0);
+    e = __builtin_fma(-b, y1, 1.0);
+    const double y2 = __builtin_fma(y1, e, y1);
+    const double q0 = a * y2;
+    const double r = __builtin_fma(-b, q0, a);
+    return __builtin_fma(r, y2, q0);
+#else
+    return a / b;
+#endif
+}
+
 /* sqrt(x) for a positive normal finite x, correctly rounded like dm_sqrt.  On the device
  * it is the compiler's own fp64 sqrt sequence (v_rsq_f64, Goldschmidt iteration, two
  * corrections) without the subnormal scaling and the zero/inf fix-up that such an x never
@@ -107,6 +129,20 @@ DM_FN double dm_sqrt_pos(double x)
     g = dm_fma(d, h, g);
     d = dm_fma(-g, g, x);
     return dm_fma(d, h, g);
+#else
+    return __builtin_sqrt(x);
+#endif
+}
+
+/* dm_sqrt with the range test in front: x in [2^-767, DBL_MAX] takes dm_sqrt_pos (the same
+ * sequence the compiler emits there without its scaling and class fix-up, so the same
+ * bits), anything else -- zero, subnormal-range, inf, NaN, negative -- the full sqrt.  On
+ * the device the test is a branch that a wave skips when no lane needs the full path.    */
+DM_FN double dm_sqrt_fast(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (x >= 0x1p-767 && x <= 1.7976931348623157e308) return dm_sqrt_pos(x);
+    return __builtin_sqrt(x);
 #else
     return __builtin_sqrt(x);
 #endif
@@ -164,6 +200,17 @@ DM_FN double dm_exp_kernel(double r)
  * normal range takes dm_ldexp.                                                          */
 DM_FN double dm_exp(double x)
 {
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* x in [-708, 709]: ki = rint(x / ln2) lies in [-1021, 1023] and p 2^ki is normal, so the
+     * scaling below is exact and equals v_ldexp_f64; the special-value selects are not
+     * needed.  A branch: a wave runs the general path only when one of its lanes needs it. */
+    if (x >= -708.0 && x <= 709.0) {
+        const double kd = dm_rint_small(x * DM_INV_LN2);
+        const double hi = x - kd * DM_LN2_HI;
+        const double r = hi - kd * DM_LN2_LO;
+        return __builtin_amdgcn_ldexp(dm_exp_kernel(r), (int)kd);
+    }
+#endif
     const int nan_ = x != x, over = x > 709.782712893384, under = x < -745.1332191019412;
     const double xs = (nan_ | over | under) ? 0.0 : x;
     double kd = dm_rint_small(xs * DM_INV_LN2);
@@ -196,7 +243,8 @@ DM_FN double dm_log_core(double xs, int kadj)
     m = big ? m * 0.5 : m;
     k += big;
     double f = m - 1.0;                 /* exact (Sterbenz) */
-    double s = f / (2.0 + f);           /* (m-1)/(m+1), |s| <= 0.1716 */
+    /* (m-1)/(m+1), |s| <= 0.1716: f in [-0.293, 0.414], 2 + f in [1.70, 2.42] */
+    double s = dm_div_inrange(f, 2.0 + f);
     double z = s * s;
     /* R = z P(z) ~ 2 z/3 + 2 z^2/5 + ...  (the atanh series, minimax-fitted) */
     double R = DM_POLY(dm_c_log, 7, z);
@@ -408,21 +456,29 @@ DM_FN double dm_normal_pdf_cdf_ratio(double z, double s)
 /* ------------------------------------------------------------------------------------ */
 typedef struct { uint32_t v[4]; } dm_philox_ctr;
 
-#ifndef ESLAM_ABL_PHILOX_ROUNDS          /* ablation builds only (timing, wrong bits) */
-#define ESLAM_ABL_PHILOX_ROUNDS 10
+/* a ^ b ^ c: one v_bitop3_b32 on gfx950 (truth table 0x96) instead of two v_xor_b32 */
+DM_FN uint32_t dm_xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
 #endif
+}
+
 DM_FN dm_philox_ctr dm_philox4x32_10(dm_philox_ctr c, uint32_t k0, uint32_t k1)
 {
-    for (int r = 0; r < ESLAM_ABL_PHILOX_ROUNDS; ++r) {
+    DM_UNROLL
+    for (int r = 0; r < 10; ++r) {
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         uint64_t p0 = (uint64_t)0xD2511F53u * c.v[0];
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c.v[2];
         uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         dm_philox_ctr o;
-        o.v[0] = hi1 ^ c.v[1] ^ k0;
+        o.v[0] = dm_xor3(hi1, c.v[1], k0);
         o.v[1] = lo1;
-        o.v[2] = hi0 ^ c.v[3] ^ k1;
+        o.v[2] = dm_xor3(hi0, c.v[3], k1);
         o.v[3] = lo0;
         c = o;
     }

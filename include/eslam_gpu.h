@@ -265,6 +265,13 @@ int eslam_gpu_project(eslam_ctx* ctx, const eslam_step_input* in);
 int eslam_gpu_update(eslam_ctx* ctx, const eslam_step_input* in);
 /* wait for the stream; fetch the info of the last update (info may be NULL)               */
 int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info);
+/* The resample scan's blocks wait for each other (the fused finalize, the preceding tiles'
+ * totals).  A wait that gives up -- never expected: the blocks it waits for are dispatched
+ * first -- poisons the filter: nothing further is written, and every later call (step,
+ * update, sync, download, the ParticleFilter API) returns ESLAM_ERR_HIP until init_* or
+ * upload_particles starts over.  Testing only: polls before a wait gives up (default 2^18,
+ * about 60 ms; 0 gives up at once, which forces the poisoned path).                        */
+int eslam_gpu_debug_set_spin_limit(eslam_ctx* ctx, uint32_t polls);
 
 /* ---- ParticleFilter<T> API (src/ParticleFilter.hpp:34-173) ------------------------------ */
 int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum);          /* getWeightsSum :34-39     */

@@ -263,6 +263,9 @@ struct eslam_ctx {
     Shard* shards = nullptr;
     Ctl* ctl = nullptr;
     Ctl* ctl_host = nullptr;    // pinned
+    uint32_t* fault_host = nullptr;         // host-mapped: kFaultTimeout when a device wait gave up
+    bool poisoned = false;                  // the particle set is undefined until re-initialised
+    uint32_t spin_limit = kSpinLimit;       // polls of K3's cross-block waits (debug: 0 gives up at once)
     uint32_t* jump = nullptr;
     uint32_t jump_n = 1;                    // A^n_global, cached
     uint64_t jump_n_for = 0;
@@ -418,6 +421,19 @@ extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ?
 static int materialize(eslam_ctx* ctx);
 static int store_cow(eslam_ctx* ctx, uint32_t* ndup_out);
 
+static const char* kPoisonMsg =
+    "resample scan: a cross-block wait gave up (a preceding tile's total or the finalize never arrived); "
+    "the particle set is undefined until the filter is re-initialised";
+
+// a device wait that gave up poisons the filter (kFaultTimeout): seen here from the
+// host-mapped word without a synchronisation, so the next call after the faulting launch
+// fails instead of building on a corrupt particle set
+static int check_poisoned(eslam_ctx* ctx)
+{
+    if (!ctx->poisoned && (__atomic_load_n(ctx->fault_host, __ATOMIC_ACQUIRE) & kFaultTimeout)) ctx->poisoned = true;
+    return ctx->poisoned ? fail(ctx, ESLAM_ERR_HIP, kPoisonMsg) : ESLAM_OK;
+}
+
 static int read_ctl(eslam_ctx* ctx)
 {
     HIPCHK(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->stream));
@@ -451,12 +467,14 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
             hipHostMalloc(&ctx->ctl_host, sizeof(Ctl)) != hipSuccess ||
             hipMalloc(&ctx->jump, sizeof(uint32_t) * (2048 + 2048 + 1024)) != hipSuccess ||
             hipMalloc(&ctx->scratch, 4096) != hipSuccess ||
-            hipHostMalloc(&ctx->scratch_host, 4096) != hipSuccess) {
+            hipHostMalloc(&ctx->scratch_host, 4096) != hipSuccess ||
+            hipHostMalloc(&ctx->fault_host, 64) != hipSuccess) {
             rc = fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, "device allocation failed");
             break;
         }
         if (hipMemset(ctx->shards, 0, sizeof(Shard) * kNShard) != hipSuccess) { rc = fail(ctx, ESLAM_ERR_HIP, "shard reset"); break; }
         memset(ctx->ctl_host, 0, sizeof(Ctl));
+        memset(ctx->fault_host, 0, 64);
         ctx->ctl_host->minstd = dm_minstd_seed(cfg->seed);     // ParticleFilter(seed)
         dm_libc_srand(&ctx->libc, 1);                            // the reference never seeds rand()
         ctx->ctl_host->max_weight = 0.0;                         // PoseEstimator ctor
@@ -553,7 +571,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     free_particles(ctx);
     free_map(ctx);
     (void)hipFree(ctx->shards); (void)hipFree(ctx->ctl); (void)hipHostFree(ctx->ctl_host); (void)hipFree(ctx->jump);
-    (void)hipFree(ctx->scratch); (void)hipHostFree(ctx->scratch_host);
+    (void)hipFree(ctx->scratch); (void)hipHostFree(ctx->scratch_host); (void)hipHostFree(ctx->fault_host);
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
     (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay);
@@ -913,6 +931,13 @@ static int reset_ctl_for_new_particles(eslam_ctx* ctx, int wexp)
 {
     int rc = read_ctl(ctx);
     if (rc) return rc;
+    if (ctx->poisoned || (ctx->ctl_host->err & kFaultTimeout)) {
+        // a poisoned filter starts over: the fault cleared, no partial segment marks left
+        ctx->ctl_host->err &= ~(uint64_t)kFaultTimeout;
+        __atomic_store_n(ctx->fault_host, 0u, __ATOMIC_RELAXED);
+        HIPCHK(ctx, hipMemsetAsync(ctx->marks, 0, ctx->cap * 4, ctx->stream));
+        ctx->poisoned = false;
+    }
     ctx->ctl_host->base = 0;
     ctx->ctl_host->flip = 0;
     ctx->ctl_host->gather = 0;               // a pending gather of the old set is dropped
@@ -1157,6 +1182,7 @@ extern "C" int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const esla
 extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
 {
     if (!ctx || !p) return ESLAM_ERR_INVALID_ARG;
+    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     int rc = materialize(ctx);
     if (!rc) rc = read_ctl(ctx);
     if (rc) return rc;
@@ -1185,6 +1211,7 @@ extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64
                                           eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints)
 {
     if (!ctx || (!out && count)) return ESLAM_ERR_INVALID_ARG;
+    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     if (!count) return ESLAM_OK;
     if (!stride) stride = 1;
     if (first >= ctx->n || (count - 1) > (ctx->n - 1 - first) / stride)
@@ -1402,12 +1429,6 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
 // tile size never changes a result.
 static uint32_t scan_items(uint64_t n)
 {
-    static const int forced = [] {
-        const char* e = getenv("ESLAM_SCAN_ITEMS");
-        const int v = e ? atoi(e) : 0;
-        return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
-    }();
-    if (forced) return (uint32_t)forced;
     // measured (tools/ab_items.sh, bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
     // 64k and 256k (over 2 items, themselves +19 % over 8 at 256k), 2 or 4 items +4 % at 1M,
     // 8 items best from 4M on (fewer tiles_before re-sums)
@@ -1419,6 +1440,8 @@ static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normali
 {
     ScanParams sp;
     memset(&sp, 0, sizeof(sp));
+    sp.spin_limit = ctx->spin_limit;
+    sp.fault = ctx->fault_host;
     sp.n = ctx->n;
     sp.gbase = ctx->gbase;
     sp.n_global = ctx->n_global;
@@ -1469,19 +1492,10 @@ static int abort_pending_gather(eslam_ctx* ctx, hipError_t e, int rc = ESLAM_ERR
     return rc;
 }
 
-// host spin bound of the sharded step's wait for the slice totals (ESLAM_SPIN_US, microseconds;
-// measurements).  The wait starts while the step's weighting kernel still runs; a 2 ms bound
-// (which covers K1 + the exchanges of a 4M shard) measured the same as 200 us on one rank at
-// 2M and 4M (profiles/r02/ab_spin.log), so the shorter bound stays
-static long spin_bound_us()
-{
-    static const long us = [] {
-        const char* e = getenv("ESLAM_SPIN_US");
-        const long v = e ? atol(e) : 200;
-        return v < 0 ? 0 : v;
-    }();
-    return us;
-}
+// host spin bound of the sharded step's wait for the slice totals: the wait starts while the
+// step's weighting kernel still runs; a 2 ms bound (which covers K1 + the exchanges of a 4M
+// shard) measured the same as 200 us on one rank at 2M and 4M (profiles/r02/ab_spin.log)
+constexpr long kSpinBoundUs = 200;
 
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
@@ -1515,11 +1529,11 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     // wakes the thread tens of microseconds late, and the GPU runs dry before the next
     // step's launches if the host is late here (the segments kernel is all it has queued)
     {
-        // bounded (spin_bound_us): past it (a hung collective or kernel, or a late GPU) fall
+        // bounded (kSpinBoundUs): past it (a hung collective or kernel, or a late GPU) fall
         // back to a blocking wait instead of burning a host core next to the RCCL proxy threads
         hipError_t q;
         const auto t0 = std::chrono::steady_clock::now();
-        const auto bound = std::chrono::microseconds(spin_bound_us());
+        const auto bound = std::chrono::microseconds(kSpinBoundUs);
         while ((q = hipEventQuery(ctx->ev[0])) == hipErrorNotReady) {
             if (std::chrono::steady_clock::now() - t0 > bound) {
                 q = hipEventSynchronize(ctx->ev[0]);
@@ -1528,6 +1542,13 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
         }
         if (q != hipSuccess) return abort_pending_gather(ctx, q);
     }
+    // a rank whose slice-total wait gave up all-gathers ~0: every rank stops here
+    for (int r = 0; r < G; ++r)
+        if (h[mg::kTotals + r] == ~0ull) {
+            ctx->poisoned = true;
+            (void)abort_pending_gather(ctx, hipSuccess);
+            return fail(ctx, ESLAM_ERR_HIP, kPoisonMsg);
+        }
     const uint64_t c_resample = h[mg::kMirror];
     const uint32_t c_minstd_start = (uint32_t)h[mg::kMirror + 1];
     const int c_scan_shift = (int)(int64_t)h[mg::kMirror + 2];
@@ -1594,23 +1615,13 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     return ESLAM_OK;
 }
 
-// ESLAM_FUSED_FINALIZE=0 keeps the separate k_finalize launch (measurements; same results)
-static bool fused_finalize()
-{
-    static const bool on = [] {
-        const char* e = getenv("ESLAM_FUSED_FINALIZE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     if (ctx->sharded) return run_update_tail_multi(ctx, mode, timed);
     const FinParams fp = fin_params(ctx, mode);
     // an update step folds the finalize into K3's block 0 (one launch fewer per step); the
     // standalone normalise / resample / sum keep k_finalize
-    const bool fused = mode == FIN_UPDATE && fused_finalize();
+    const bool fused = mode == FIN_UPDATE;
     if (!fused) HIPCHK(ctx, eslam_launch_finalize(ctx->shards, kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, false);
@@ -1721,24 +1732,27 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
 }
 
 // the device's zero-measurement-variance flag (k_finalize aborted the update): clear it and
-// report the reference's exception text
+// report the reference's exception text.  A timeout fault stays set (poisoned filter).
 static int take_update_error(eslam_ctx* ctx)
 {
     int rc = read_ctl(ctx);
     if (rc) return rc;
     const uint64_t err = ctx->ctl_host->err;
-    if (!(err & 5ull)) return ESLAM_OK;
+    if (err & kFaultTimeout) {
+        ctx->poisoned = true;
+        return fail(ctx, ESLAM_ERR_HIP, kPoisonMsg);
+    }
+    if (!(err & 1ull)) return ESLAM_OK;
     ctx->ctl_host->err = 0;
     rc = write_ctl(ctx);
     if (rc) return rc;
-    if (err & 4ull)    // K3 waited in vain for a preceding tile's total (never expected: see k_normalize_segments)
-        return fail(ctx, ESLAM_ERR_HIP, "resample scan: a preceding tile's total was not published in time");
     return fail(ctx, ESLAM_ERR_ZERO_MEAS_VAR, "using a zero measurement variance leads to singularities");
 }
 
 static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project, bool weight)
 {
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     if (weight && !ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
     StepParams p;
     fill_step_params(ctx, in, p);
@@ -1846,6 +1860,13 @@ extern "C" int eslam_gpu_step(eslam_ctx* ctx, const eslam_step_input* in, int* u
     return ESLAM_OK;
 }
 
+extern "C" int eslam_gpu_debug_set_spin_limit(eslam_ctx* ctx, uint32_t polls)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    ctx->spin_limit = polls;
+    return ESLAM_OK;
+}
+
 extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
@@ -1890,6 +1911,7 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
 static int standalone(eslam_ctx* ctx, uint32_t mode)
 {
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     const int rc = materialize(ctx);
     if (rc) return rc;
     const uint32_t J = dm_chunk_rows(ctx->n_global);

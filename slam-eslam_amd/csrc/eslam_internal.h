@@ -250,8 +250,17 @@ struct ScanParams {
     uint32_t items;                      // particles per thread of K3: tile = kBlock * items
                                          // (2, 4 or kScanItems; sharded: kScanItems)
     uint32_t tag;                        // one GPU: this launch's tile-total tag (1..7, cycled per launch)
-    uint32_t pad;
+    uint32_t spin_limit;                 // polls of a cross-block wait before it gives up (kSpinLimit;
+                                         // 0: give up at once, eslam_gpu_debug_set_spin_limit)
+    uint32_t* fault;                     // host-mapped word: kFaultTimeout when a wait gave up
 };
+
+// A cross-block wait that gave up (a preceding tile's total or the fused finalize never
+// arrived) poisons the filter: the device ORs kFaultTimeout into ctl->err and into a
+// host-mapped word, writes nothing further, and every later launch that sees the bit in
+// ctl->err returns at once; the host refuses the filter until it is re-initialised.
+constexpr uint32_t kFaultTimeout = 4u;
+constexpr uint32_t kSpinLimit = 1u << 18;    // x s_sleep(8) (512 clocks): ~60 ms
 
 constexpr int kMaxRanks = 16;
 

@@ -209,38 +209,6 @@ template <class V> __device__ __forceinline__ double kd(const V& r, int k) { ret
 template <class T> using gmem = __attribute__((address_space(1))) T;
 template <class T, class V> __device__ __forceinline__ gmem<T>* kp(const V& r, int k) { return (gmem<T>*)(uintptr_t)kq(r, k); }
 
-// ESLAM_K1_PROF (diagnostic builds only): per-region shader-clock time of K1, summed by
-// lane 0 of every wave into k1_prof[] (LDS per block, one global atomic per region).
-#ifdef ESLAM_K1_PROF
-__device__ unsigned long long k1_prof[32];      // [0,16): K1 regions, [16,32): K3b regions
-#define PROF_INIT() __shared__ unsigned long long s_prof[16]; if (threadIdx.x < 16) s_prof[threadIdx.x] = 0; \
-    uint64_t prof_t = __builtin_readcyclecounter()
-#define PROF(k) do { const uint64_t t_ = __builtin_readcyclecounter(); \
-    if ((threadIdx.x & 63u) == 0) atomicAdd(&s_prof[k], (unsigned long long)(t_ - prof_t)); prof_t = t_; } while (0)
-#define PROF_FLUSH_AT(base) do { __syncthreads(); if (threadIdx.x < 16) atomicAdd(&k1_prof[(base) + threadIdx.x], s_prof[threadIdx.x]); } while (0)
-#define PROF_FLUSH() PROF_FLUSH_AT(0)
-#define PROF_PARAM , uint64_t& prof_t, unsigned long long* s_prof
-#define PROF_ARG , prof_t, s_prof
-#else
-#define PROF_PARAM
-#define PROF_ARG
-#define PROF_INIT() do {} while (0)
-#define PROF(k) do {} while (0)
-#define PROF_FLUSH() do {} while (0)
-#define PROF_FLUSH_AT(base) do {} while (0)
-#endif
-
-// ESLAM_K1_TL (diagnostic builds only): per-wave timeline of K1 in s_memrealtime ticks
-// (100 MHz): entry, window staged, exit (few stamps: each costs registers, and at 129
-// VGPRs the kernel drops to 3 waves per SIMD)
-#ifdef ESLAM_K1_TL
-__device__ unsigned long long k1_tl[8192 * 8];
-#define TL(k) do { const uint32_t gw_ = blockIdx.x * kWaves + (threadIdx.x >> 6); \
-    if ((threadIdx.x & 63u) == 0 && gw_ < 8192u) k1_tl[gw_ * 8u + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define TL(k) do {} while (0)
-#endif
-
 // the state pointers of buffer s[b] (offset KOFF(s[b]))
 struct StatePtrs {
     gmem<double> *x, *y, *th, *z, *zs, *w, *mprob;
@@ -532,11 +500,13 @@ __device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, 
     return s2 < 1600.0 && z * z < 31.36 * s2;
 }
 
-// MAXP: bound on the contact points found (group ends); BATCH: p.m <= MAXP contacts.
+// MAXP: bound on the contact points found (group ends); BATCH: p.m <= MAXP contacts;
+// UNG (with BATCH): every contact closes its group (groupId -1 or a group of one), so the
+// group logic reduces to the Q7 poisoning flag and a push per evaluated, found contact.
 // StepParams (p.*) and the contacts come from scalar loads of the kernel arguments.
-template <int MAXP, bool BATCH, bool DELTA = false>
+template <int MAXP, bool BATCH, bool DELTA = false, bool UNG = false>
 __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, double s, double r22, double x, double y,
-                                                  double z, double meas_var, uint32_t sid PROF_PARAM)
+                                                  double z, double meas_var, uint32_t sid)
 {
     CMResult r;
     // pushed contact points.  BATCH: slot = index of the contact that closed the group, so
@@ -584,15 +554,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
                     contact_ratio = 0;
                     return;
                 }
-#ifdef ESLAM_K1_PROF
-                if ((threadIdx.x & 63u) == __builtin_ctzll(__ballot(1))) atomicAdd(&k1_prof[14], 1ull);
-                atomicAdd(&k1_prof[15], 1ull);
-#endif
-#ifdef ESLAM_ABL_NO_RATIO
-                const double ratio = 1.0 + zdiff * 1e-3;
-#else
                 const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * corr);
-#endif
                 if (!valid) {
                     pzd = zdiff * ratio;
                     pzv = zvar * ratio;
@@ -636,12 +598,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
         wz = ((zz + r22 * pz) + z) - radius;
     };
     auto lookup = [&](double wx, double wy, double wz, double& mean, double& stdev) -> bool {
-#ifdef ESLAM_ABL_NO_MAP
-        mean = 0.0; stdev = 0.05;
-        return wx == wx;
-#else
         return get_patch<DELTA>(win, wx, wy, wz, qv, mean, stdev, sid);
-#endif
     };
 
     if constexpr (BATCH) {
@@ -658,13 +615,44 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
                 if ((eval_mask >> i) & 1u) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
             }
         }
-        PROF(6);
+        if constexpr (UNG) {
+            // contact() with c_end set for every contact: `valid` is false at the start of
+            // each one, a surely-significant point is pushed as it is, any other one through
+            // its ratio (pzd = (zdiff r) (1/r), ...), and a miss clears group_valid for good
+            // (Q7: it is only reset under `valid`, which a miss never sets)
+            bool alive = true;
 #pragma unroll
-        for (int i = 0; i < MAXP; ++i) {
-            if ((uint32_t)i >= m) break;
-            contact((uint32_t)i, fnd[i], mn[i], sd[i], wzs[i]);
+            for (int i = 0; i < MAXP; ++i) {
+                if ((uint32_t)i >= m) break;
+                if (!((eval_mask >> i) & 1u)) continue;
+                if (alive && fnd[i]) {
+                    const double zdiff = wzs[i] - mn[i];
+                    const double pose_var = sd[i] * sd[i];
+                    const double zvar = sd[i] * sd[i] + meas_var;
+                    double pzd_i = zdiff, pzv_i = zvar, pv_i = pose_var;
+                    bool take = true;
+                    if (!ratio_surely_significant(zdiff, zvar, corr)) {
+                        const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * corr);
+                        take = ratio > 1e-9;
+                        const double inv = 1.0 / ratio;
+                        pzd_i = (zdiff * ratio) * inv;
+                        pzv_i = (zvar * ratio) * inv;
+                        pv_i = (pose_var * ratio) * inv;
+                    }
+                    if (take) {
+                        posevar += pv_i;
+                        push((uint32_t)i, pzd_i, pzv_i);
+                    }
+                }
+                alive = alive && fnd[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < MAXP; ++i) {
+                if ((uint32_t)i >= m) break;
+                contact((uint32_t)i, fnd[i], mn[i], sd[i], wzs[i]);
+            }
         }
-        PROF(7);
     } else {
         for (uint32_t i = 0; i < m; ++i) {
             double wx, wy, wz, mean = 0.0, stdev = 0.0;
@@ -679,16 +667,23 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
     r.accepted = (uint64_t)ncp >= kq(wp, 3);
     r.weight = r.zdelta = r.zvar = r.s2 = 0.0;
     if (r.accepted) {
-        double d1 = 0, d2 = 0;
+        // every zvar lies in [meas_var, meas_var + 2^256] (a float stdev squared), and d2 in
+        // [2^-301, 4 / meas_var]: for meas_var in [2^-400, 2^300] the reciprocals need none of
+        // the division's scaling (dm_div_inrange: the same bits)
+        double d1 = 0, d2 = 0, inv_d2;
+        auto sums = [&](auto recip) {
 #pragma unroll
-        for (int k = 0; k < MAXP; ++k) {
-            if (BATCH ? ok[k] : (uint32_t)k < ncp) {
-                cv[k] = 1.0 / cv[k];            // cv now holds 1/zvar
-                d1 += cz[k] * cv[k];
-                d2 += cv[k];
+            for (int k = 0; k < MAXP; ++k) {
+                if (BATCH ? ok[k] : (uint32_t)k < ncp) {
+                    cv[k] = recip(cv[k]);       // cv now holds 1/zvar
+                    d1 += cz[k] * cv[k];
+                    d2 += cv[k];
+                }
             }
-        }
-        const double inv_d2 = 1.0 / d2;
+            inv_d2 = recip(d2);
+        };
+        if (meas_var >= 0x1p-400 && meas_var <= 0x1p300) sums([](double v) { return dm_div_inrange(1.0, v); });
+        else sums([](double v) { return 1.0 / v; });
         const double delta = d1 * inv_d2;
         double s2 = 0.0;
 #pragma unroll
@@ -700,11 +695,7 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
         }
         r.s2 = s2;
         const uint32_t use_shape = kl2(KOFF(p.use_shape))[0];
-#ifdef ESLAM_ABL_NO_EW
-        const double pz = use_shape ? 1.0 - 0.5 * s2 : 1.0;
-#else
         const double pz = use_shape ? dm_exp(-0.5 * s2) : 1.0;
-#endif
         r.weight = pz;
         r.zdelta = -delta;
         r.zvar = inv_d2;
@@ -732,54 +723,24 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
     return v;
 }
 
-#ifdef ESLAM_K1_WAVES
-#define K1_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ESLAM_K1_WAVES, ESLAM_K1_WAVES)))
-#else
-#define K1_OCCUPANCY
-#endif
-
-#ifdef ESLAM_ABL_NO_PHILOX       // ablation builds only (timing, wrong bits)
-__device__ __forceinline__ dm_philox_ctr k1_draw(uint64_t seed, uint32_t, uint64_t ev, uint64_t gi, uint32_t call)
-{
-    dm_philox_ctr c;
-    const uint32_t h = (uint32_t)gi * 0x9E3779B9u ^ (uint32_t)seed ^ (uint32_t)ev ^ call;
-    c.v[0] = h; c.v[1] = h ^ 0x85ebca6bu; c.v[2] = h + 0xc2b2ae35u; c.v[3] = h ^ 0x27d4eb2fu;
-    return c;
-}
-#define K1_DRAW k1_draw
-#else
-#define K1_DRAW dm_draw
-#endif
-
-#ifdef ESLAM_ABL_NO_BM           // ablation builds only (timing, wrong bits)
-#define K1_BOX_MULLER(a, b, z0, z1) (*(z0) = dm_u32(a) - 0.5, *(z1) = dm_u32(b) - 0.5)
-#else
-#define K1_BOX_MULLER dm_box_muller32
-#endif
-
 // The state written by K1 (and w by K3) is streamed: each value is read once, by the next
 // kernel, from another XCD.  Non-temporal stores (nt) leave fewer lines for the kernel-end L2
 // writeback (interleaved A/B on MI355X: 256k +3 %, 4M +0.7 %, 16M +1.6 % per step; plain
 // stores and agent-coherent sc1 stores measured beside them).  Same values, same bits.
 #define K1_ST(p, v) __builtin_nontemporal_store((v), (p))
-#ifdef ESLAM_NT_LOADS                    // experiment: streaming loads of the state as well
-#define K1_LD(p) __builtin_nontemporal_load(p)
-#else
-#define K1_LD(p) (*(p))
-#endif
 
-template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false>
-__global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a)
+template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false, bool UNG = false>
+__global__ void __launch_bounds__(kBlock) k_project_weight(K1Args a)
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
     // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
-    TL(0);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t n = a.p.n;
     const uint32_t J = a.p.J;
     const uint64_t csz = 64ull * J;
     const uint64_t nchunks = (n + csz - 1) / csz;
     Ctl* ctl = a.ctl;
+    if (ctl->err & kFaultTimeout) return;    // poisoned filter (a wait gave up): nothing is touched
     // a pending resample gather is fused here: read the ancestors from state[base],
     // write the updated particles to state[base ^ 1] (the latest buffer)
     const uint32_t gath = ctl->gather;
@@ -802,11 +763,7 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     Window win;
     win.on = 0;
     if (WEIGHT) win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds);
-#ifdef ESLAM_ABL_STAGE_TWICE            // ablation builds only: the staging cost
-    if (WEIGHT) { __syncthreads(); win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds); }
-#endif
 
-    TL(1);
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
@@ -817,8 +774,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
     const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
 
     // one canonical chunk (64 x J particles) per wave; its totals go to exact fixed point
-    PROF_INIT();
-    PROF(0);
     const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
     if (chunk < nchunks) {
     const uint64_t lbase = chunk * csz;
@@ -847,7 +802,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             src = decode_source(m - 1u, gf[1], kp<const Rec>(g, 3), &rc);
             rec_anc = gf[0];
         }
-        PROF(1);
         if (i >= n) continue;
         double x, y, th, z, zs, w, mp_in = 0.0;
         uint32_t fl_in = 0;
@@ -856,8 +810,8 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             mp_in = rc->mprob; fl_in = (uint8_t)rc->src;
         } else {
             const StatePtrs si = kstate(si_off);
-            x = K1_LD(si.x + src); y = K1_LD(si.y + src); th = K1_LD(si.th + src); z = K1_LD(si.z + src);
-            zs = K1_LD(si.zs + src); w = K1_LD(si.w + src);
+            x = si.x[src]; y = si.y[src]; th = si.th[src]; z = si.z[src];
+            zs = si.zs[src]; w = si.w[src];
             if (!WEIGHT && gath) { mp_in = si.mprob[src]; fl_in = si.flags[src]; }
         }
         if (gath && rec_anc) {
@@ -873,12 +827,11 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             const uint64_t gi = kq(key, 2) + i;
             // draw layout: call 0 -> two Box-Muller pairs (z0, z1), (z2, sn0);
             // call 1 -> slip test + slip factor, spread pair (sn1, sn2)
-            const dm_philox_ctr d0 = K1_DRAW(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 0);
-            const dm_philox_ctr d1 = K1_DRAW(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 1);
+            const dm_philox_ctr d0 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 0);
+            const dm_philox_ctr d1 = dm_draw(kq(key, 0), DM_STREAM_PROJECT, kq(key, 1), gi, 1);
             double z0, z1, z2, sn0;
-            K1_BOX_MULLER(d0.v[0], d0.v[1], &z0, &z1);
-            K1_BOX_MULLER(d0.v[2], d0.v[3], &z2, &sn0);
-            PROF(2);
+            dm_box_muller32(d0.v[0], d0.v[1], &z0, &z1);
+            dm_box_muller32(d0.v[2], d0.v[3], &z2, &sn0);
             // odometry.getPoseDeltaSample2D() = mu + L z
             const su16 P = kl16(KOFF(p.mu));         // mu0 mu1 mu2 L00 L10 L11 L20 L21
             const su8 Q = kl8(KOFF(p.L22));          // L22 slip_factor yaw max_yaw_dev
@@ -896,24 +849,18 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             }
             const su4 Z = kl4(KOFF(p.z_delta));      // z_delta z_var
             z += kd(Z, 0);
-            zs = dm_sqrt(zs * zs + kd(Z, 1));
+            zs = dm_sqrt_fast(zs * zs + kd(Z, 1));
             if (do_spread) {
                 double sn1, sn2;
-                K1_BOX_MULLER(d1.v[2], d1.v[3], &sn1, &sn2);
+                dm_box_muller32(d1.v[2], d1.v[3], &sn1, &sn2);
                 x += sn0 * tf + 0.0;
                 y += sn1 * tf + 0.0;
                 th += sn2 * rf + 0.0;
             }
-            PROF(3);
         }
         if (WEIGHT) {
             double s, co;
-#ifdef ESLAM_ABL_NO_SINCOS
-            s = th * 1e-3; co = 1.0 - s;
-#else
             dm_sincos(th, &s, &co);
-#endif
-            PROF(4);
             const double r22 = (1.0 - co) + co;
             const double meas_var = zs * zs + kd(kl2(KOFF(p.me2)), 0);
             uint32_t sid = 0;
@@ -922,23 +869,23 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
                 // is at i; its store name sits next to the state (DevState::sid)
                 sid = kp<const uint32_t>(kl2(st_off + (uint32_t)offsetof(DevState, sid)), 0)[i];
             }
-            CMResult r = evaluate_pose<MAXP, BATCH, DELTA>(win, co, s, r22, x, y, z, meas_var, sid PROF_ARG);
+            CMResult r = evaluate_pose<MAXP, BATCH, DELTA, UNG>(win, co, s, r22, x, y, z, meas_var, sid);
             if (meas_var == 0) {            // evaluatePose throws (src/ContactModel.cpp:122): no contact points
                 err = 1;
                 r.accepted = false;
                 r.ncp = 0;
             }
-            PROF(8);
             uint32_t floating;
             double sw = 0.0;
             if (r.accepted) {
                 // ContactModel::updateZPositionEstimate  src/ContactModel.cpp:319-340
                 double zvar = zs * zs;
-#ifdef ESLAM_ABL_NO_KALMAN
-                const double pose_var = r.posevar * 0.25;
-#else
-                const double pose_var = r.posevar / (double)r.ncp;
-#endif
+                // posevar / found: a power-of-two count divides exactly as a multiplication by
+                // its reciprocal (the same correctly rounded quotient)
+                const double inv_n = dm_recip_small(r.ncp);     // 1.0 / found, correctly rounded
+                double pose_var;
+                if (r.ncp != 0u && (r.ncp & (r.ncp - 1u)) == 0u) pose_var = r.posevar * inv_n;
+                else pose_var = r.posevar / (double)r.ncp;
                 const double av = zvar - pose_var;
                 double delta_var = (av < 1e-9) ? 1e-9 : av;
                 if (!(r.zdelta * r.zdelta > delta_var)) {
@@ -948,14 +895,13 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
                     delta_var = (1.0 - var_gain) * delta_var;
                     zvar = pose_var + delta_var;
                 }
-                zs = dm_sqrt(zvar);
+                zs = dm_sqrt_fast(zvar);
                 w *= r.weight;
                 mprob = r.weight;
                 floating = 0;
                 maxm = (maxm < r.weight) ? r.weight : maxm;
                 nD += 1;
                 // pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found))
-                const double inv_n = dm_recip_small(r.ncp);     // 1.0 / found, correctly rounded
                 const uint32_t use_shape = kl2(KOFF(p.use_shape))[0];
                 if (!use_shape || r.ncp == 0) sw = dm_pow(r.weight, inv_n);
                 else sw = r.weight == 0.0 ? 0.0 : dm_exp((-0.5 * r.s2) * inv_n);
@@ -990,7 +936,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             } while (todo);
             accSW = accSW + sw;
             flags = (r.ncp & 0x7fu) | (floating << 7);
-            PROF(9);
         } else {
             mprob = mp_in;
             flags = fl_in;
@@ -1019,7 +964,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             bb[2] = __builtin_fmaxf(bb[2], -yf);
             bb[3] = __builtin_fmaxf(bb[3], yf);
         }
-        PROF(10);
     }
 
     if (WEIGHT) {
@@ -1056,7 +1000,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
             if ((mi >> (4 * k)) & 1ull) flag |= 1u << (k + 16);
         }
     }
-        PROF(11);
     }
 
     // bounding box of the cloud for the next step's LDS window (maxima, any order)
@@ -1125,9 +1068,6 @@ __global__ void __launch_bounds__(kBlock) K1_OCCUPANCY k_project_weight(K1Args a
         if (f & 0x7fffffffu) atomicOr((unsigned long long*)&sh->flags, (unsigned long long)(f & 0x7fffffffu));
         if (f >> 31) atomicOr((unsigned long long*)&sh->err, 1ull);
     }
-    PROF(12);
-    PROF_FLUSH();
-    TL(5);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1864,15 +1804,15 @@ __device__ __forceinline__ void phase_b_load(const DevState& st, const ScanParam
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
-        v[r] = K1_LD(st.w + (i < sp.n ? i : last));
+        v[r] = st.w[(i < sp.n ? i : last)];
     }
     if (sp.phase_b) {
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
             const uint64_t i = t0 + (uint64_t)(r * kBlock + (int)tid);
             const uint64_t ic = i < sp.n ? i : last;
-            fl[r] = K1_LD(st.flags + ic);
-            mp[r] = K1_LD(st.mprob + ic);
+            fl[r] = st.flags[ic];
+            mp[r] = st.mprob[ic];
         }
     }
 }
@@ -1935,23 +1875,37 @@ __device__ __forceinline__ void phase_b_tile(const DevState& st, const ScanParam
 constexpr int kCtlWords = (int)(sizeof(Ctl) / 8);
 static_assert(sizeof(Ctl) % 8 == 0 && kCtlWords <= 64, "the control block is copied by one wave");
 
-__device__ __forceinline__ void fin_wait_copy(const Ctl* ctl, const uint64_t* fin_word, uint64_t epoch, uint64_t* s_img,
-                                              Ctl* ctl_err)
+// a cross-block wait gave up: poison the filter (kFaultTimeout in ctl->err, which every later
+// launch checks, and in the host-mapped word the host checks before it trusts anything)
+__device__ __forceinline__ void raise_timeout(Ctl* ctl, uint32_t* fault)
+{
+    atomicOr((unsigned long long*)&ctl->err, (unsigned long long)kFaultTimeout);
+    if (fault) __hip_atomic_fetch_or(fault, kFaultTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// true (block-uniform) when the wait gave up: s_img is then not valid
+__device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word, uint64_t epoch, uint64_t* s_img,
+                                              const ScanParams& sp, uint32_t* s_flag)
 {
     const uint32_t tid = threadIdx.x;
     if (tid < 64) {
-        bool timeout = false;
+        bool timeout = sp.spin_limit == 0;       // testing: give up at once
         if (tid == 0) {
             uint32_t spins = 0;
-            while (atomic_load_agent(fin_word) != epoch) {
-                if (++spins == (1u << 18)) { timeout = true; break; }      // x s_sleep(8): ~60 ms
+            while (!timeout && __hip_atomic_load(fin_word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+                if (spins++ >= sp.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(8);
             }
+            *s_flag = timeout ? 1u : 0u;
+            if (timeout) raise_timeout(ctl, sp.fault);
         }
+        // block 0's release store of the epoch pairs with the acquire load above: its ctl
+        // writes are visible to this wave's loads below
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (tid < (uint32_t)kCtlWords) s_img[tid] = atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + tid);
-        if (timeout) atomicOr((unsigned long long*)&ctl_err->err, 4ull);
     }
     __syncthreads();
+    return *s_flag != 0u;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2041,20 +1995,21 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
 }
 
 constexpr uint64_t kPubMask = (1ull << 61) - 1;
-constexpr uint32_t kPubSpinLimit = 1u << 18;       // x s_sleep(8) (512 clocks): ~60 ms
 
 // sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
 // them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
 // polls (light on the memory system the tiles it waits for are still streaming through);
 // the other waves wait at the barrier.
-__device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, uint32_t tag,
+// A wait that gives up (sp.spin_limit polls) poisons the filter and returns ~0.
+__device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, const ScanParams& sp,
                                                      uint64_t* s_red, Ctl* __restrict__ ctl)
 {
+    const uint32_t tag = sp.tag;
     const uint32_t tid = threadIdx.x;
     if (tid < 64) {
         uint64_t acc = 0;
-        bool timeout = false;
-        for (uint32_t b0 = 0; b0 < count; b0 += 8u * 64u) {
+        bool timeout = sp.spin_limit == 0 && count > 0;   // testing: give up at once
+        for (uint32_t b0 = 0; !timeout && b0 < count; b0 += 8u * 64u) {
             uint64_t v[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -2067,7 +2022,7 @@ __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict_
 #pragma unroll
                 for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
                 if (__ballot(!ready) == 0ull) break;
-                if (++spins == kPubSpinLimit) { timeout = true; break; }
+                if (spins++ >= sp.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(8);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -2078,9 +2033,9 @@ __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict_
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
         }
-        if (timeout && tid == 0) atomicOr((unsigned long long*)&ctl->err, 4ull);
         acc = wave_sum_u64(acc);
-        if (tid == 0) s_red[0] = acc;
+        if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
+        if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
     }
     __syncthreads();
     return s_red[0];
@@ -2116,8 +2071,9 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
-    if (ctl->aborted) {                  // the update threw (k_finalize): weights stay as phase A left them
+    if (ctl->aborted || (ctl->err & kFaultTimeout)) {   // the update threw (k_finalize), or the filter is poisoned
         if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+        if (total && tile + 1 == sp.ntiles && tid == 0 && (ctl->err & kFaultTimeout)) *total = ~0ull;
         return;
     }
     const bool resample = ctl->resample != 0;
@@ -2142,8 +2098,8 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
     if (tid == 0) atomic_store_agent(tile_sum + tile, tagw | (t & kPubMask));
     if (total && tile + 1 == sp.ntiles) {
-        const uint64_t before = tiles_before_pub(tile_sum, tile, sp.tag, s_red, ctl);
-        if (tid == 0) *total = before + t;
+        const uint64_t before = tiles_before_pub(tile_sum, tile, sp, s_red, ctl);
+        if (tid == 0) *total = before == ~0ull ? ~0ull : before + t;     // ~0: every rank sees the fault
     }
 }
 
@@ -2221,16 +2177,11 @@ __device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, 
 // order (per XCD), and a predecessor publishes before it waits on anything itself.  A
 // bounded spin turns a violated assumption into ctl->err bit 2 instead of a hang.
 // ---------------------------------------------------------------------------------------
-#ifdef ESLAM_K3_WAVES                    // experiment builds: waves per SIMD of the fused K3
-#define K3_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ESLAM_K3_WAVES, ESLAM_K3_WAVES)))
-#else
+
 // 8 items: the 6 waves per SIMD the unfused kernel reaches by itself (<= 80 VGPRs; the fused
 // one would take 86 and run at 5)
-#define K3_OCCUPANCY __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? 6 : 1)))
-#endif
-
 template <int ITEMS, bool FUSED>
-__global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? 6 : 1))) k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                                uint64_t* __restrict__ tile_pub, uint32_t* __restrict__ marks,
                                                                uint32_t* __restrict__ tile_first,
                                                                const uint32_t* __restrict__ jt, FusedFin ff)
@@ -2238,9 +2189,17 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
     __shared__ uint64_t s_wtot[kWaves], s_red[kWaves];
     __shared__ K3Lds<ITEMS> s_u;
     __shared__ uint64_t s_img[FUSED ? kCtlWords : 1];
+    __shared__ uint32_t s_flag;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
+    if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
+        if (tid == 0) {
+            atomic_store_agent(tile_pub + tile, tagw);
+            if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     if constexpr (FUSED) {
         if (tile == 0) {
             __shared__ FinLds s_fin;
@@ -2272,7 +2231,10 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
             double mp[ITEMS];
             uint32_t fl[ITEMS];
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
-            fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, ctl);
+            if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
+                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+                return;
+            }
             if (cv->aborted) {           // the update threw (k_finalize): weights stay as phase A left them
                 if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
                 return;
@@ -2285,17 +2247,14 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
-    PROF_INIT();
     if (!resample) {
         if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
         return;
     }
     __syncthreads();
-    PROF(0);
     const int shift = (int)sgpr_u32((uint32_t)cv->scan_shift);
     uint64_t c[ITEMS];
     const uint64_t run = blocked_fx(s_u.v, shift, c);
-    PROF(1);
     // in-tile exclusive prefix and the tile total (wave scans -> LDS)
     uint64_t tincl = run;
 #pragma unroll
@@ -2313,10 +2272,9 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
         agg += t;
     }
     if (tid == 0) atomic_store_agent(tile_pub + tile, tagw | (agg & kPubMask));
-    PROF(2);
-    const uint64_t tb = tiles_before_pub(tile_pub, tile, sp.tag, s_red, ctl);
+    const uint64_t tb = tiles_before_pub(tile_pub, tile, sp, s_red, ctl);
+    if (tb == ~0ull) return;             // gave up waiting: poisoned, no marks
     const uint64_t base = tb + wexcl + (tincl - run);
-    PROF(3);
 
     const uint64_t N = sp.n_global;
     const uint32_t xs = sgpr_u32(cv->minstd_start);
@@ -2380,7 +2338,6 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
         const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
         lo = lane == 0 ? K0 : prev;
     }
-    PROF(4);
     if (i0 == 0) lo = 0;
     uint64_t seg_lo[ITEMS], seg_hi[ITEMS];
     uint32_t val[ITEMS];
@@ -2400,11 +2357,7 @@ __global__ void __launch_bounds__(kBlock) K3_OCCUPANCY k_normalize_segments(DevS
             lo = hi;
         }
     }
-    PROF(5);
-    PROF(6);
     flush_marks(marks, tile_first, seg_lo, seg_hi, val);
-    PROF(7);
-    PROF_FLUSH_AT(16);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2806,28 +2759,38 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     args.shards = shards;
     memset(&args.store, 0, sizeof(args.store));
     if (store) args.store = *store;
-#define ESLAM_LAUNCH(P, W, M, B)                                                                      \
-    hipLaunchKernelGGL((k_project_weight<P, W, M, B>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
+#define ESLAM_LAUNCH(P, W, M, B, ...)                                                                   \
+    hipLaunchKernelGGL((k_project_weight<P, W, M, B, ##__VA_ARGS__>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
                        stream, args)
-#define ESLAM_LAUNCH_D(P, W, M, B)                                                                          \
-    hipLaunchKernelGGL((k_project_weight<P, W, M, B, true>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
-                       stream, args)
+    // every contact closes its group (groupId -1 or groups of one): the reduced group logic
+    const uint32_t all = p->m >= 32 ? 0xffffffffu : ((1u << p->m) - 1u);
+    const bool ung = (p->end_mask & all) == all;
     if (weight && store) {
         // per-particle maps: the lookups fall back to the particle's store (every pending
         // gather has been materialised by the host)
-        if (project) { if (p->m <= 4 && maxp <= 4) ESLAM_LAUNCH_D(true, true, 4, true); else ESLAM_LAUNCH_D(true, true, ESLAM_MAX_CONTACTS, false); }
-        else { if (p->m <= 4 && maxp <= 4) ESLAM_LAUNCH_D(false, true, 4, true); else ESLAM_LAUNCH_D(false, true, ESLAM_MAX_CONTACTS, false); }
+        if (p->m <= 4 && maxp <= 4) {
+            if (project) { if (ung) ESLAM_LAUNCH(true, true, 4, true, true, true); else ESLAM_LAUNCH(true, true, 4, true, true); }
+            else { if (ung) ESLAM_LAUNCH(false, true, 4, true, true, true); else ESLAM_LAUNCH(false, true, 4, true, true); }
+        } else {
+            if (project) ESLAM_LAUNCH(true, true, ESLAM_MAX_CONTACTS, false, true);
+            else ESLAM_LAUNCH(false, true, ESLAM_MAX_CONTACTS, false, true);
+        }
         return hipGetLastError();
     }
-#undef ESLAM_LAUNCH_D
     // batched contact lookups when every contact fits the MAXP-sized arrays
     if (project && !weight) ESLAM_LAUNCH(true, false, 4, false);
     else if (!project && weight) {
-        if (maxp <= 4) { if (p->m <= 4) ESLAM_LAUNCH(false, true, 4, true); else ESLAM_LAUNCH(false, true, 4, false); }
+        if (maxp <= 4) {
+            if (p->m <= 4) { if (ung) ESLAM_LAUNCH(false, true, 4, true, false, true); else ESLAM_LAUNCH(false, true, 4, true); }
+            else ESLAM_LAUNCH(false, true, 4, false);
+        }
         else if (maxp <= 8) { if (p->m <= 8) ESLAM_LAUNCH(false, true, 8, true); else ESLAM_LAUNCH(false, true, 8, false); }
         else ESLAM_LAUNCH(false, true, ESLAM_MAX_CONTACTS, false);
     } else {
-        if (maxp <= 4) { if (p->m <= 4) ESLAM_LAUNCH(true, true, 4, true); else ESLAM_LAUNCH(true, true, 4, false); }
+        if (maxp <= 4) {
+            if (p->m <= 4) { if (ung) ESLAM_LAUNCH(true, true, 4, true, false, true); else ESLAM_LAUNCH(true, true, 4, true); }
+            else ESLAM_LAUNCH(true, true, 4, false);
+        }
         else if (maxp <= 8) { if (p->m <= 8) ESLAM_LAUNCH(true, true, 8, true); else ESLAM_LAUNCH(true, true, 8, false); }
         else ESLAM_LAUNCH(true, true, ESLAM_MAX_CONTACTS, false);
     }
@@ -2981,7 +2944,6 @@ extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, 
     case 2: ESLAM_SEG(2); break;
     case 4: ESLAM_SEG(4); break;
     case 8: ESLAM_SEG(8); break;
-    case 16: ESLAM_SEG(16); break;
     default: return hipErrorInvalidValue;
     }
 #undef ESLAM_SEG
@@ -3129,18 +3091,3 @@ extern "C" int eslam_debug_k1_occupancy(int* blocks_per_cu, int lds)
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_project_weight<true, true, 4, true>, kBlock,
                                                         lds < 0 ? kStatsLds + kWindowLds : lds) == hipSuccess ? 0 : -1;
 }
-#ifdef ESLAM_K1_TL
-extern "C" int eslam_debug_k1_tl(unsigned long long* out)
-{
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(k1_tl), sizeof(unsigned long long) * 8192 * 8) == hipSuccess ? 0 : -1;
-}
-#endif
-#ifdef ESLAM_K1_PROF
-// diagnostic builds: read and clear the K1 region clocks
-extern "C" int eslam_debug_k1_prof(unsigned long long* out)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(k1_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
-    static const unsigned long long zero[32] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(k1_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-}
-#endif

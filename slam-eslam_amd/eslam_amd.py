@@ -73,6 +73,8 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_project.argtypes = [vp, C.POINTER(A.StepInput)]
     L.eslam_gpu_update.argtypes = [vp, C.POINTER(A.StepInput)]
     L.eslam_gpu_sync.argtypes = [vp, C.POINTER(A.UpdateInfo)]
+    if hasattr(L, "eslam_gpu_debug_set_spin_limit"):     # absent from older builds (A/B runs)
+        L.eslam_gpu_debug_set_spin_limit.argtypes = [vp, C.c_uint32]
     L.eslam_gpu_get_weights_sum.argtypes = [vp, dp]
     L.eslam_gpu_normalize_weights.argtypes = [vp, dp]
     L.eslam_gpu_resample.argtypes = [vp]
@@ -230,6 +232,10 @@ class GpuFilter:
         info = A.UpdateInfo()
         self._check(self.L.eslam_gpu_sync(self.h, C.byref(info)))
         return info
+
+    def debug_set_spin_limit(self, polls):
+        """Testing only: polls of K3's cross-block waits before they give up (0: at once)."""
+        self._check(self.L.eslam_gpu_debug_set_spin_limit(self.h, polls))
 
     # -- ParticleFilter API ----------------------------------------------------------------
     def weights_sum(self):
