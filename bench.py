@@ -30,6 +30,11 @@ BYTES_K1 = 113                # gathered read x, y, th, z, zs, w (48) + write x,
                               # + the 4-byte segment mark read and cleared (8)
 BYTES_K3 = 29                 # k_normalize_segments: read w, mprob, flags (17), write w (8), segment marks (4)
 BYTES_STEP = BYTES_K1 + BYTES_K3   # what the fused step moves per particle-update: the step roofline
+BYTES_K1_DELTA = BYTES_K1 + 4  # per-particle maps: + the store name (store lookups hit L2: the stores of
+                               # the cells under the feet, a few per particle and step)
+BYTES_MERGE_READ = 336        # k_map_merge per particle: store name 4, count 4, 24 keys + 24 {mean, stdev} 288,
+                              # pose x, y, theta, z, zsigma 40
+BYTES_MERGE_WRITE = 292       # per changed store: 24 keys + 24 values written back, count
 CONFIG3_GLOBAL = 16 * 1024 * 1024  # BASELINE configs[3]: 16M particles over 8 GPUs
 CONFIG4_GLOBAL = 64 * 1024 * 1024  # BASELINE configs[4]: 64M particles over 8 GPUs
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -195,8 +200,36 @@ def spawn_ranks(args):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].communicate()[0]
-    rcs = [p.wait() for p in procs]
+    # poll every rank: one that fails (RCCL init, out of memory) would leave the others waiting
+    # in a collective forever, so the rest are stopped and the run fails
+    import threading
+    box = {}
+    reader = threading.Thread(target=lambda: box.setdefault("out", procs[0].stdout.read()), daemon=True)
+    reader.start()
+    deadline = time.monotonic() + 3600
+    rcs = [None] * len(procs)
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        failed = [rc for rc in rcs if rc not in (None, 0)]
+        if failed or time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            if not failed:
+                sys.stderr.write("bench.py: ranks did not finish within the time limit\n")
+                sys.exit(124)
+            rcs = [p.returncode for p in procs]
+            break
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    out = box.get("out", b"")
     sys.stdout.write(out.decode())
     sys.stdout.flush()
     bad = [r for r in rcs if r]
@@ -321,12 +354,16 @@ def main():
     value = total_updates / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
-    # roofline of the dominant kernel (HIP events around every launch of the timed region)
-    per_kernel = {"k_project_weight": (kt["project_weight_ms"], BYTES_K1),
-                  "k_normalize_segments": (kt["normalize_scan_ms"], BYTES_K3)}
+    # roofline of the dominant kernel (HIP events around every launch of the timed region);
+    # per-particle maps: the map merge competes too (its write-back covers the changed stores)
+    per_kernel = {"k_project_weight": (kt["project_weight_ms"], (BYTES_K1_DELTA if args.local_maps else BYTES_K1) * n),
+                  "k_normalize_segments": (kt["normalize_scan_ms"], BYTES_K3 * n)}
+    if args.local_maps:
+        per_kernel["k_map_merge"] = (kt["map_merge_ms"], BYTES_MERGE_READ * n + BYTES_MERGE_WRITE * info.map_stores_changed)
     dom = max(per_kernel, key=lambda k: per_kernel[k][0])
-    dom_ms, dom_bytes = per_kernel[dom]
-    achieved = dom_bytes * n / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    dom_ms, dom_launch_bytes = per_kernel[dom]
+    dom_bytes = dom_launch_bytes / n
+    achieved = dom_launch_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     workload = "local-maps" if args.local_maps else ("rough" if args.rough else "flat")
     traffic = pmc_traffic(dom, n, args.map_cells, workload) if not sharded else None
     result = {
@@ -357,7 +394,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
-                     "algorithmic_bytes_per_particle": dom_bytes,
+                     "algorithmic_bytes_per_particle": round(dom_bytes, 2),
                      "avg_launch_ms": round(dom_ms, 5)},
         "kernel_ms": {k: round(v, 5) for k, v in kt.items()},
         "kernel_ms_note": "HIP events around every launch on the context stream, over a second pass of "
@@ -370,6 +407,12 @@ def main():
                               % (BYTES_STEP, BYTES_K1, BYTES_K3, BYTES_REFERENCE,
                                  BYTES_REFERENCE * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world)),
         "last_update": {"effective": info.effective, "resampled": info.resampled},
+        **({"map_update": {"patches_dropped": info.map_patches_dropped, "stores_copied": info.map_stores_copied,
+                           "stores_changed": info.map_stores_changed,
+                           "note": "the last step's map update: scan patches full stores could not take, stores "
+                                   "copied on write after the resample, stores the merge changed and wrote back; "
+                                   "kernel_ms.map_* time the update's phases (map_cow_ms includes the host read of "
+                                   "the copy count)"}} if args.local_maps else {}),
         "build_id": eslam_amd.build_id(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

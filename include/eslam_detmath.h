@@ -312,16 +312,40 @@ DM_FN void dm_quadrant(int q, double sr, double cr, double* s, double* c)
     *c = neg_c ? -cc : cc;
 }
 
+/* n mod 4 of the integer-valued n of dm_sincos, through a 32-bit conversion that saturates
+ * (v_cvt_i32_f64 on the device, the same clamp on the host): exact for |n| < 2^31, i.e.
+ * |x| < 3.3e9 rad; beyond, the quadrant of the clamped value (deterministic both sides)   */
+DM_FN int dm_quadrant_of(double n)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int q;
+    __asm__("v_cvt_i32_f64 %0, %1" : "=v"(q) : "v"(n));
+    return q & 3;
+#else
+    const int q = n >= 2147483647.0 ? 2147483647 : (n <= -2147483648.0 ? (-2147483647 - 1) : (int)n);
+    return q & 3;
+#endif
+}
+
 DM_FN void dm_sincos(double x, double* s, double* c)
 {
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* a wave whose angles are all finite takes the arithmetic without the special-value
+     * selects (the same values) */
+    if (__builtin_amdgcn_ballot_w64(!dm_isfinite(x)) == 0) {
+        const double n = dm_rint_small(x * DM_INV_PIO2);
+        const double r = ((x - n * DM_PIO2_1) - n * DM_PIO2_2) - n * DM_PIO2_3;
+        dm_quadrant(dm_quadrant_of(n), dm_sin_kernel(r), dm_cos_kernel(r), s, c);
+        return;
+    }
+#endif
     const int fin = dm_isfinite(x);
     const double xs = fin ? x : 0.0;
     /* |n| > 2^20 (|x| > 1.6e6 rad): the three-part reduction is inexact but deterministic */
     double n = dm_rint_small(xs * DM_INV_PIO2);
     double r = ((xs - n * DM_PIO2_1) - n * DM_PIO2_2) - n * DM_PIO2_3;
     double sr = dm_sin_kernel(r), cr = dm_cos_kernel(r);
-    int64_t q = (int64_t)(n - 4.0 * dm_floor(n * 0.25));  /* n mod 4 in [0,3] */
-    dm_quadrant((int)q, sr, cr, s, c);
+    dm_quadrant(dm_quadrant_of(n), sr, cr, s, c);
     if (!fin) { *s = x - x; *c = x - x; }
 }
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 2
+#define ESLAM_ABI_VERSION 3
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -88,7 +88,8 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_PARTICLE_MAPS 0x10u     /* useSharedMap = false: every particle its own local
                                               map (eslam_gpu_map_update)                      */
 #define ESLAM_FLAG_RECORD_CONTACTS 0x8u    /* keep every update's cpoints, meas_pos, meas_theta
-                                              (also on with log_debug); one GPU only          */
+                                              (also on with log_debug); one GPU only: the
+                                              set_comm calls return ESLAM_ERR_UNSUPPORTED    */
 
 void eslam_config_default(eslam_config* cfg);
 
@@ -159,6 +160,12 @@ typedef struct eslam_update_info {
     int32_t uniform_reset;                 /* sumWeights <= 0 branch taken                   */
     uint64_t resample_overruns;            /* draws beyond the cumulative sum (clamped, Q5)  */
     uint64_t update_count;
+    /* the last eslam_gpu_map_update (per-particle maps): scan patches a particle's map could
+     * not take because its store already held ESLAM_STORE_CAP patches (summed over the
+     * particles), and the stores copied on write before the merge                          */
+    uint64_t map_patches_dropped;
+    uint64_t map_stores_copied;
+    uint64_t map_stores_changed;           /* stores the merge changed (written back)        */
 } eslam_update_info;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */
@@ -190,6 +197,14 @@ int eslam_gpu_init_pose(eslam_ctx* ctx, const double position[3], const double o
 /* replace the particle set (getParticles() is a mutable reference in the reference)       */
 int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const eslam_particles* p);
 int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p);
+/* edit particles [first, first + count) in place, the way the reference's callers edit the
+ * vector getParticles() returns (processMap's weights, src/EmbodiedSlamFilter.cpp:183-220):
+ * every non-NULL field of p (arrays of count values) overwrites that field; the particle
+ * set, the per-particle maps, the RNG and the last update's records stay.  The weight scale
+ * of the next update is then set from the largest weight, as eslam_gpu_upload_particles does,
+ * so an edit through this call and a download / edit / upload of the whole set lead to the
+ * same particles bit for bit.                                                               */
+int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p);
 
 /* ---- per-particle local maps (useSharedMap = false) -----------------
  * EmbodiedSlamFilter::processMap(scanMap, match=false, update=true)
@@ -374,6 +389,13 @@ typedef struct eslam_kernel_times {
     float normalize_scan_ms;
     float resample_ms;
     float total_ms;
+    /* eslam_gpu_map_update (per-particle maps), averaged over the map updates of the timed
+     * region: the pending resample gather, the copy-on-write of shared stores (including its
+     * host read of the copy count), the merge kernel, and the whole call                   */
+    float map_gather_ms;
+    float map_cow_ms;
+    float map_merge_ms;
+    float map_total_ms;
 } eslam_kernel_times;
 int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable);
 int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t);

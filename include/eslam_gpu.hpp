@@ -218,6 +218,17 @@ struct UpdateThreshold {
     UpdateThreshold() {}
     UpdateThreshold(double distance, double angle) : distance(distance), angle(angle) {}
     bool test(double distance, double angle) const { return distance > this->distance || angle > this->angle; }
+    // test(const Eigen::Affine3d&)  src/Configuration.hpp:23-26: the rotation angle
+    // (Eigen::AngleAxisd(linear()).angle() = 2 atan2(|q.vec|, |q.w|)) goes in as the distance and
+    // the translation's norm as the angle (Q6, kept)
+    bool test(const Affine3d& pdelta) const
+    {
+        const Quaterniond q(pdelta.linear());
+        const double n = std::sqrt(q.x() * q.x() + q.y() * q.y() + q.z() * q.z());
+        const double a = n != 0.0 ? 2.0 * std::atan2(n, std::fabs(q.w())) : 0.0;
+        const Vector3d& t = pdelta.translation();
+        return test(a, std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]));
+    }
     double distance = 0;
     double angle = 0;
 };
@@ -585,6 +596,7 @@ public:
     // yaw-free body frame, placed at every particle's pose
     void updateMaps(const std::vector<ScanPatch>& scan)
     {
+        flush();
         std::vector<eslam_scan_patch> p(scan.size());
         for (size_t k = 0; k < scan.size(); ++k) {
             for (int i = 0; i < 3; ++i) p[k].position[i] = scan[k].position[i];
@@ -598,6 +610,7 @@ public:
     void init(int numParticles, SurfaceHash* hash)
     {
         if (!hash) throw std::runtime_error("could not sample from pose hash.");
+        discardView();
         check(ctx_, eslam_gpu_hash_create(ctx_));
         check(ctx_, eslam_gpu_init_hash(ctx_, (uint64_t)numParticles));
     }
@@ -606,6 +619,7 @@ public:
     {
         const double m[3] = {mu.position.x(), mu.position.y(), mu.orientation};
         const double s[3] = {sigma.position.x(), sigma.position.y(), sigma.orientation};
+        discardView();
         check(ctx_, eslam_gpu_init_gaussian(ctx_, (uint64_t)numParticles, m, s, zpos, zsigma));
     }
 
@@ -613,12 +627,16 @@ public:
     void project(const BodyContactState& state, const Quaterniond& orientation)
     {
         const eslam_step_input in = makeInput(state, orientation, Vector3d(), 0);
+        flush();
+        invalidate();
         check(ctx_, eslam_gpu_project(ctx_, &in));
     }
     // update(state, orientation, ltc)  src/PoseEstimator.cpp:244-255
     void update(const BodyContactState& state, const Quaterniond& orientation, const std::vector<TerrainClassification>& ltc)
     {
         const eslam_step_input in = makeInput(state, orientation, Vector3d(), ltc.size());
+        flush();
+        invalidate();
         check(ctx_, eslam_gpu_update(ctx_, &in));
         check(ctx_, eslam_gpu_sync(ctx_, &last_));
     }
@@ -626,6 +644,7 @@ public:
     // ParticleFilter<T>  src/ParticleFilter.hpp:34-173
     double getWeightsSum()
     {
+        flush();
         double s = 0;
         check(ctx_, eslam_gpu_get_weights_sum(ctx_, &s));
         return s;
@@ -633,13 +652,21 @@ public:
     double getWeightAvg() { return getWeightsSum() / (double)size(); }
     double normalizeWeights()
     {
+        flush();
+        invalidate();
         double e = 0;
         check(ctx_, eslam_gpu_normalize_weights(ctx_, &e));
         return e;
     }
-    void resample() { check(ctx_, eslam_gpu_resample(ctx_)); }
+    void resample()
+    {
+        flush();
+        invalidate();
+        check(ctx_, eslam_gpu_resample(ctx_));
+    }
     size_t getBestParticleIndex() const
     {
+        flush();
         uint64_t i = 0;
         check(ctx_, eslam_gpu_get_best_particle_index(ctx_, &i));
         return (size_t)i;
@@ -647,27 +674,46 @@ public:
     // getCentroid  src/PoseEstimator.cpp:354-383 (normalises in place, Q15)
     Pose getCentroid()
     {
+        flush();
+        invalidate();                     // normalises the weights
         double p[3], q[4];
         check(ctx_, eslam_gpu_get_centroid(ctx_, p, q));
         return Pose(Vector3d(p[0], p[1], p[2]), Quaterniond(q[0], q[1], q[2], q[3]));
     }
 
-    // getParticles(): a host copy of the particles (they live in HBM), refreshed on every
-    // call; with logDebug it carries cpoints / meas_pos / meas_theta of the last update.
-    // Edits reach the filter through setParticles().
-    std::vector<Particle>& getParticles() { return getParticles(0, 1, size()); }
-    // particles first, first + stride, ... (count): a device-side gather, for logging
-    std::vector<Particle>& getParticles(size_t first, size_t stride, size_t count)
+    // getParticles(): the particles as a vector the caller may edit, like the reference's
+    // std::vector<Particle>& (src/ParticleFilter.hpp:150-153; processMap edits weights through
+    // it, src/EmbodiedSlamFilter.cpp:183-220).  The particles live in HBM: the vector is
+    // downloaded on first use after the device changed them, and edits -- pose, zPos, zSigma,
+    // weight, mprob, floating, the number of cpoints, or the vector's size -- are written back
+    // (eslam_gpu_write_particles, or a whole new set when the size changed) before the next
+    // call that uses the particles on the device.  With logDebug it carries cpoints / meas_pos /
+    // meas_theta of the last update.  The reference stays valid; its contents are those of the
+    // last download.
+    std::vector<Particle>& getParticles()
     {
+        if (!view_valid_) {
+            view_ = getParticles(0, 1, size());
+            shadow_.resize(view_.size());
+            for (size_t i = 0; i < view_.size(); ++i) shadow_[i] = hot(view_[i]);
+            view_valid_ = true;
+        }
+        return view_;
+    }
+    // particles first, first + stride, ... (count): a device-side gather, for logging; a copy
+    // (edits to it are not written back)
+    std::vector<Particle> getParticles(size_t first, size_t stride, size_t count)
+    {
+        flush();
         std::vector<eslam_particle_record> rec(count);
         // contact points per particle: at most the contacts of the last step
         const uint32_t maxc = config_.logDebug || (config_.flags & ESLAM_FLAG_RECORD_CONTACTS) ? (last_m_ ? last_m_ : 1) : 0;
         std::vector<eslam_cpoint> cp(maxc ? count * maxc : 0);
         check(ctx_, eslam_gpu_download_records(ctx_, first, stride, count, rec.data(), maxc ? cp.data() : nullptr, maxc));
-        particles_.resize(count);
+        std::vector<Particle> particles(count);
         for (size_t k = 0; k < count; ++k) {
             const eslam_particle_record& r = rec[k];
-            Particle& p = particles_[k];
+            Particle& p = particles[k];
             p.position = Vector2d(r.position[0], r.position[1]);
             p.orientation = r.orientation;
             p.zPos = r.zpos;
@@ -694,9 +740,22 @@ public:
                 p.cpoints.resize(r.n_cpoints);        // the count (cpoints.size()) without the capture
             }
         }
-        return particles_;
+        return particles;
     }
     void setParticles(const std::vector<Particle>& in)
+    {
+        discardView();
+        replaceSet(in);
+    }
+    size_t size() const
+    {
+        uint64_t n = 0;
+        check(ctx_, eslam_gpu_particle_count(ctx_, &n));
+        return (size_t)n;
+    }
+
+private:
+    void replaceSet(const std::vector<Particle>& in) const
     {
         const size_t n = in.size();
         std::vector<double> x(n), y(n), th(n), z(n), zs(n), w(n), mp(n);
@@ -709,12 +768,8 @@ public:
         eslam_particles p = {x.data(), y.data(), th.data(), z.data(), zs.data(), w.data(), mp.data(), fl.data(), nc.data()};
         check(ctx_, eslam_gpu_upload_particles(ctx_, n, &p));
     }
-    size_t size() const
-    {
-        uint64_t n = 0;
-        check(ctx_, eslam_gpu_particle_count(ctx_, &n));
-        return (size_t)n;
-    }
+
+public:
 
     // multi-GPU (the reference has one CPU filter): this estimator becomes shard `rank` of
     // an nGlobal-particle filter over an RCCL communicator the library drives.  Rank 0 calls
@@ -733,6 +788,40 @@ public:
             throw std::runtime_error("setCommRccl: bad id or shard table");
         check(ctx_, eslam_gpu_set_comm_rccl(ctx_, nranks, rank, id.data(), nGlobal, shardGbase.data()));
     }
+
+    // write the edits made to the getParticles() vector back to the device (a no-op without
+    // any); every call above that uses the particles on the device runs it first
+    void flush() const
+    {
+        if (!view_valid_) return;
+        if (view_.size() != shadow_.size()) {          // the caller resized the set: replace it
+            view_valid_ = false;
+            replaceSet(view_);
+            return;
+        }
+        size_t lo = view_.size(), hi = 0;
+        for (size_t i = 0; i < view_.size(); ++i) {
+            const Hot h = hot(view_[i]);
+            if (std::memcmp(&h, &shadow_[i], sizeof(Hot)) != 0) {
+                if (i < lo) lo = i;
+                hi = i + 1;
+                shadow_[i] = h;
+            }
+        }
+        if (lo >= hi) return;
+        const size_t n = hi - lo;
+        std::vector<double> x(n), y(n), th(n), z(n), zs(n), w(n), mp(n);
+        std::vector<uint8_t> fl(n), nc(n);
+        for (size_t k = 0; k < n; ++k) {
+            const Hot& h = shadow_[lo + k];
+            x[k] = h.v[0]; y[k] = h.v[1]; th[k] = h.v[2]; z[k] = h.v[3]; zs[k] = h.v[4]; w[k] = h.v[5]; mp[k] = h.v[6];
+            fl[k] = h.floating; nc[k] = h.ncp;
+        }
+        eslam_particles p = {x.data(), y.data(), th.data(), z.data(), zs.data(), w.data(), mp.data(), fl.data(), nc.data()};
+        check(ctx_, eslam_gpu_write_particles(ctx_, lo, n, &p));
+    }
+    // the device is about to change the particles: the next getParticles() downloads again
+    void invalidate() { view_valid_ = false; }
 
     const eslam_update_info& lastUpdate() const { return last_; }
     eslam_ctx* handle() const { return ctx_; }
@@ -766,11 +855,31 @@ public:
     }
 
 private:
+    // the fields of a particle the device holds, as last downloaded or written back
+    struct Hot {
+        double v[7];                      // x, y, orientation, zPos, zSigma, weight, mprob
+        uint8_t floating, ncp, pad[6];
+    };
+    static Hot hot(const Particle& p)
+    {
+        Hot h;
+        std::memset(&h, 0, sizeof(h));
+        h.v[0] = p.position.x(); h.v[1] = p.position.y(); h.v[2] = p.orientation; h.v[3] = p.zPos;
+        h.v[4] = p.zSigma; h.v[5] = p.weight; h.v[6] = p.mprob;
+        h.floating = p.floating ? 1 : 0;
+        h.ncp = (uint8_t)(p.cpoints.size() & 0x7f);
+        return h;
+    }
+    // a new particle set replaces the view without writing it back
+    void discardView() const { view_valid_ = false; }
+
     FootContact& odometry_;
     Configuration config_;
     eslam_ctx* ctx_ = nullptr;
     eslam_update_info last_ = {};
-    std::vector<Particle> particles_;
+    mutable std::vector<Particle> view_;           // getParticles()
+    mutable std::vector<Hot> shadow_;              // view_ as the device holds it
+    mutable bool view_valid_ = false;
     mutable uint32_t last_m_ = 0;
 };
 
@@ -793,6 +902,7 @@ public:
     {
         filter_.reset(new PoseEstimator(odometry_, eslamConfig_, device_, hashConfig));
         filter_->setEnvironment(env, useSharedMap);
+        filter_->invalidate();
         sharedMap_ = useSharedMap;
         const double p[3] = {pose.position.x(), pose.position.y(), pose.position.z()};
         const double q[4] = {pose.orientation.w(), pose.orientation.x(), pose.orientation.y(), pose.orientation.z()};
@@ -810,6 +920,8 @@ public:
         odometry_.update(bs, orientation);
         const eslam_step_input in = f.makeInput(bs, orientation, body2odometry.translation(), ltc.size());
         int updated = 0;
+        f.flush();                        // edits made through getParticles()
+        f.invalidate();
         check(f.handle(), eslam_gpu_step(f.handle(), &in, &updated));
         if (updated) ++update_idx_;
         last_state_ = bs;

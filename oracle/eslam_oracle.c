@@ -585,6 +585,9 @@ struct or_filter {
     uint32_t* pm_key;                    /* n x 32 */
     float* pm_val;                       /* n x 32 x {mean, stdev} */
     uint32_t* pm_count;                  /* n */
+    uint64_t* pm_id;                     /* n: which map a particle holds (the resample copies the
+                                            id with the map); distinct ids at a map update =
+                                            the maps cloneMaps did not need to copy */
 };
 
 
@@ -646,7 +649,8 @@ static void or_free_particles(or_filter* f)
     free(f->anc);
     free(f->dbg_ncp); free(f->dbg_cp); free(f->dbg_zdelta); free(f->dbg_zvar);
     free(f->pm_key); free(f->pm_val); free(f->pm_count);
-    f->pm_key = NULL; f->pm_val = NULL; f->pm_count = NULL;
+    free(f->pm_id);
+    f->pm_key = NULL; f->pm_val = NULL; f->pm_count = NULL; f->pm_id = NULL;
     f->x = f->y = f->th = f->z = f->zs = f->w = f->mprob = NULL;
     f->floating = f->ncp = NULL;
     f->anc = NULL;
@@ -679,7 +683,9 @@ static int or_alloc_particles(or_filter* f, uint64_t n)
         f->pm_key = calloc(b * OR_STORE_SLOTS, 4);
         f->pm_val = calloc(b * OR_STORE_SLOTS * 2, 4);
         f->pm_count = calloc(b, 4);
-        if (!f->pm_key || !f->pm_val || !f->pm_count) return ESLAM_ERR_OUT_OF_MEMORY;
+        f->pm_id = malloc(b * 8);
+        if (!f->pm_key || !f->pm_val || !f->pm_count || !f->pm_id) return ESLAM_ERR_OUT_OF_MEMORY;
+        for (uint64_t i = 0; i < n; ++i) f->pm_id[i] = f->gbase + i;
     }
     f->has_anc = 0;
     return f->x ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
@@ -1427,14 +1433,16 @@ static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
         uint32_t* nk = malloc(samples * OR_STORE_SLOTS * 4);
         float* nv = malloc(samples * OR_STORE_SLOTS * 8);
         uint32_t* ncn = malloc(samples * 4);
+        uint64_t* nid = malloc(samples * 8);
         for (uint64_t k = 0; k < samples; ++k) {
             const uint32_t i = anc[k];
             memcpy(nk + k * OR_STORE_SLOTS, f->pm_key + (uint64_t)i * OR_STORE_SLOTS, OR_STORE_SLOTS * 4);
             memcpy(nv + k * OR_STORE_SLOTS * 2, f->pm_val + (uint64_t)i * OR_STORE_SLOTS * 2, OR_STORE_SLOTS * 8);
             ncn[k] = f->pm_count[i];
+            nid[k] = f->pm_id[i];
         }
-        free(f->pm_key); free(f->pm_val); free(f->pm_count);
-        f->pm_key = nk; f->pm_val = nv; f->pm_count = ncn;
+        free(f->pm_key); free(f->pm_val); free(f->pm_count); free(f->pm_id);
+        f->pm_key = nk; f->pm_val = nv; f->pm_count = ncn; f->pm_id = nid;
     }
 }
 
@@ -1489,6 +1497,7 @@ typedef struct {
     uint8_t floating, ncp, pad[6];
     /* per-particle maps: the source particle's own patches travel with it (a deep copy) */
     uint32_t pm_count, pm_pad;
+    uint64_t pm_id;
     uint32_t pm_key[OR_STORE_SLOTS];
     float pm_val[2 * OR_STORE_SLOTS];
 } or_mig;
@@ -1546,6 +1555,7 @@ static void resample_sharded(or_filter* f, int shift)
             m->lo = a; m->hi = b; m->src = f->gbase + i;
             if (f->pm_key) {
                 m->pm_count = f->pm_count[i];
+                m->pm_id = f->pm_id[i];
                 memcpy(m->pm_key, f->pm_key + i * OR_STORE_SLOTS, sizeof(m->pm_key));
                 memcpy(m->pm_val, f->pm_val + i * OR_STORE_SLOTS * 2, sizeof(m->pm_val));
             }
@@ -1577,6 +1587,7 @@ static void resample_sharded(or_filter* f, int shift)
         f->anc[o] = anc[o];
         if (f->pm_key) {
             f->pm_count[o] = m->pm_count;
+            f->pm_id[o] = m->pm_id;
             memcpy(f->pm_key + o * OR_STORE_SLOTS, m->pm_key, sizeof(m->pm_key));
             memcpy(f->pm_val + o * OR_STORE_SLOTS * 2, m->pm_val, sizeof(m->pm_val));
         }
@@ -1858,7 +1869,26 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     int is_id = 1;
     for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
-    for (uint64_t i = 0; i < f->n; ++i) {
+    /* the copies cloneMaps made since the last merge (one context: every particle beyond the
+     * first that holds a map), then every particle holds its own again */
+    {
+        const uint64_t ng = NG(f);
+        uint64_t* seen = calloc(ng / 64 + 1, 8);
+        uint64_t distinct = 0;
+        for (uint64_t i = 0; i < f->n; ++i) {
+            const uint64_t d = f->pm_id[i];
+            if (!(seen[d / 64] >> (d % 64) & 1ull)) { seen[d / 64] |= 1ull << (d % 64); ++distinct; }
+        }
+        free(seen);
+        f->info.map_stores_copied = f->n - distinct;
+        for (uint64_t i = 0; i < f->n; ++i) f->pm_id[i] = f->gbase + i;
+    }
+    uint64_t dropped = 0, changed = 0;
+    const int64_t n = (int64_t)f->n;
+    /* particles are independent: the OpenMP threads of or_set_threads (same results) */
+#pragma omp parallel for schedule(static) num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed)
+    for (int64_t i = 0; i < n; ++i) {
+        int dirty = 0;
         uint32_t* key = f->pm_key + i * OR_STORE_SLOTS;
         float* val = f->pm_val + i * OR_STORE_SLOTS * 2;
         uint32_t count = f->pm_count[i];
@@ -1890,6 +1920,7 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
                         const double vv = (v1 * var) / (v1 + var);
                         val[2 * h] = (float)mm;
                         val[2 * h + 1] = (float)dm_sqrt(vv);
+                        dirty = 1;
                     }
                     break;
                 }
@@ -1899,6 +1930,9 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
                         val[2 * h] = (float)wz;
                         val[2 * h + 1] = (float)dm_sqrt(var);
                         ++count;
+                        dirty = 1;
+                    } else {
+                        ++dropped;          /* the store is full: counted, not silent */
                     }
                     break;
                 }
@@ -1906,7 +1940,10 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
             }
         }
         f->pm_count[i] = count;
+        changed += (uint64_t)dirty;
     }
+    f->info.map_patches_dropped = dropped;
+    f->info.map_stores_changed = changed;
     return 0;
 }
 

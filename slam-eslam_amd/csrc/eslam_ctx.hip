@@ -26,11 +26,12 @@ using namespace eslam_dev;
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
                                                    const DebugRec* d, const MapStore* store, hipStream_t stream);
 extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
+extern "C" hipError_t eslam_launch_store_cow(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
                                              hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint64_t ndup,
-                                              const void* payloads, hipStream_t stream);
-extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const MapStore* ms,
+extern "C" hipError_t eslam_launch_store_copy(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch,
+                                              const uint32_t* ndup_dev, const void* payloads, uint64_t* copies_acc,
+                                              hipStream_t stream);
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
@@ -254,8 +255,9 @@ struct eslam_ctx {
     MapStore store = {};
     uint32_t* sid_mem = nullptr;             // 2 x cap: DevState::sid of both state buffers
     uint32_t* cow = nullptr;                 // owner, counts, free and sharing lists + the copy count
+    uint64_t* merge_cnt = nullptr;           // the map merge's statistics slots (2 x kMergeCounterSlots) and
+                                             // the copy-on-write copies since the last merge
     // logDebug records of the last update (ESLAM_FLAG_RECORD_CONTACTS / log_debug)
-    uint32_t last_map_copies = 0;            // stores copied by the last map update
     DebugRec dbg = {};
     uint64_t dbg_cap = 0;
     bool dbg_valid = false;
@@ -323,6 +325,8 @@ struct eslam_ctx {
     hipEvent_t ev[5] = {};                  // events of the step being recorded
     std::vector<hipEvent_t> ring;           // 5 events per recorded step (timing mode)
     uint32_t ring_steps = 0;
+    std::vector<hipEvent_t> mring;          // 4 events per recorded map update (timing mode)
+    uint32_t mring_steps = 0;
     eslam_kernel_times times = {};
 };
 
@@ -366,6 +370,19 @@ static void rec(eslam_ctx* ctx, int k)
     if (ctx->ring_steps >= kRingSteps) return;
     (void)hipEventRecord(ctx->ring[5 * ctx->ring_steps + k], ctx->stream);
     if (k == 4) ctx->ring_steps++;
+}
+
+// timing mode: event k (0..3) of the current map update (start, gather, copy on write, merge)
+static void mrec(eslam_ctx* ctx, int k)
+{
+    if (!ctx->timing) return;
+    if (ctx->mring.empty()) {
+        ctx->mring.resize(4 * kRingSteps);
+        for (auto& e : ctx->mring) (void)hipEventCreate(&e);
+    }
+    if (ctx->mring_steps >= kRingSteps) return;
+    (void)hipEventRecord(ctx->mring[4 * ctx->mring_steps + k], ctx->stream);
+    if (k == 3) ctx->mring_steps++;
 }
 
 static int fail(eslam_ctx* ctx, int code, const char* msg)
@@ -419,7 +436,7 @@ extern "C" void eslam_config_default(eslam_config* c)
 extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 static int materialize(eslam_ctx* ctx);
-static int store_cow(eslam_ctx* ctx, uint32_t* ndup_out);
+static int store_cow(eslam_ctx* ctx);
 
 static const char* kPoisonMsg =
     "resample scan: a cross-block wait gave up (a preceding tile's total or the finalize never arrived); "
@@ -539,7 +556,8 @@ static void free_particles(eslam_ctx* ctx)
 {
     free_debug(ctx);
     (void)hipFree(ctx->store.key); (void)hipFree(ctx->store.val); (void)hipFree(ctx->store.count);
-    (void)hipFree(ctx->sid_mem); (void)hipFree(ctx->cow);
+    (void)hipFree(ctx->sid_mem); (void)hipFree(ctx->cow); (void)hipFree(ctx->merge_cnt);
+    ctx->merge_cnt = nullptr;
     ctx->store = MapStore{};
     ctx->sid_mem = nullptr;
     ctx->cow = nullptr;
@@ -579,6 +597,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
+    for (auto& e : ctx->mring) if (e) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -634,6 +653,8 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
         HIPCHK(ctx, hipMalloc(&ctx->store.count, cap * 4));
         const uint64_t tiles = (cap + 2047) / 2048;
         HIPCHK(ctx, hipMalloc(&ctx->cow, (3 * cap + 2 * tiles + 2 + 1) * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->merge_cnt, (2 * kMergeCounterSlots + 1) * sizeof(uint64_t)));
+        HIPCHK(ctx, hipMemset(ctx->merge_cnt, 0, (2 * kMergeCounterSlots + 1) * sizeof(uint64_t)));
         HIPCHK(ctx, eslam_launch_store_init(ctx->st[0].sid, &ctx->store, cap, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     }
@@ -734,6 +755,13 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
         ctx->n_global = 0;
         return ESLAM_OK;
     }
+    // logDebug's per-particle contact records (cpoints, meas_pos) are indexed by the particle's
+    // position during the update and read through the resample's ancestors; on a sharded
+    // filter an ancestor may sit on another rank, so the records would have to travel with the
+    // migrating particles, which this build does not do: refused here rather than left empty
+    if (record_contacts(ctx))
+        return fail(ctx, ESLAM_ERR_UNSUPPORTED,
+                    "logDebug / ESLAM_FLAG_RECORD_CONTACTS is not supported on a sharded filter (one GPU only)");
     if (!shard_gbase || !comm->allgather || !comm->alltoallv || comm->nranks < 1 || comm->nranks > kMaxRanks ||
         comm->rank < 0 || comm->rank >= comm->nranks)
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: bad communicator (1 <= nranks <= 16)");
@@ -858,6 +886,9 @@ extern "C" int eslam_gpu_set_comm_rccl(eslam_ctx* ctx, int32_t nranks, int32_t r
                                        uint64_t n_global, const uint64_t* shard_gbase)
 {
     if (!ctx || !id) return ESLAM_ERR_INVALID_ARG;
+    if (record_contacts(ctx))             // see eslam_gpu_set_comm
+        return fail(ctx, ESLAM_ERR_UNSUPPORTED,
+                    "logDebug / ESLAM_FLAG_RECORD_CONTACTS is not supported on a sharded filter (one GPU only)");
     const RcclApi& a = rccl_api();
     if (!a.ok) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "eslam_gpu_set_comm_rccl: librccl.so.1 not found");
     if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
@@ -1207,6 +1238,57 @@ extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
     return ESLAM_OK;
 }
 
+extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p)
+{
+    if (!ctx || !p || first > ctx->n || count > ctx->n - first) return ESLAM_ERR_INVALID_ARG;
+    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
+    int rc = materialize(ctx);               // the particles the caller saw: any pending gather done
+    if (!rc) rc = read_ctl(ctx);
+    if (rc) return rc;
+    if (!count) return ESLAM_OK;
+    const DevState& s = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip];
+    const uint64_t b = count * 8;
+    const double* src[7] = {p->x, p->y, p->orientation, p->zpos, p->zsigma, p->weight, p->mprob};
+    double* dst[7] = {s.x, s.y, s.th, s.z, s.zs, s.w, s.mprob};
+    for (int k = 0; k < 7; ++k)
+        if (src[k]) HIPCHK(ctx, hipMemcpyAsync(dst[k] + first, src[k], b, hipMemcpyHostToDevice, ctx->stream));
+    if (p->floating || p->n_contact_points) {
+        std::vector<uint8_t> fl(count);
+        HIPCHK(ctx, hipMemcpyAsync(fl.data(), s.flags + first, count, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        for (uint64_t i = 0; i < count; ++i) {
+            uint8_t f = fl[i];
+            if (p->floating) f = (uint8_t)((f & 0x7f) | ((p->floating[i] ? 1 : 0) << 7));
+            if (p->n_contact_points) f = (uint8_t)((f & 0x80) | (p->n_contact_points[i] & 0x7f));
+            fl[i] = f;
+        }
+        HIPCHK(ctx, hipMemcpyAsync(s.flags + first, fl.data(), count, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (!p->weight) return ESLAM_OK;
+    // the weight scale of the next update, from the largest weight of the whole set exactly
+    // as eslam_gpu_upload_particles computes it (NaN and negative weights skipped)
+    std::vector<double> w(ctx->n);
+    HIPCHK(ctx, hipMemcpy(w.data(), s.w, ctx->n * 8, hipMemcpyDeviceToHost));
+    double mx = 0;
+    for (uint64_t i = 0; i < ctx->n; ++i) if (w[i] > mx) mx = w[i];
+    if (ctx->sharded) {
+        uint64_t* h = ctx->mg_host;
+        memcpy(&h[mg::kMaxW], &mx, 8);
+        HIPCHK(ctx, hipMemcpy(ctx->mg + mg::kMaxW, &h[mg::kMaxW], 8, hipMemcpyHostToDevice));
+        rc = comm_allgather(ctx, ctx->mg + mg::kMaxW, ctx->mg + mg::kMaxWAll, 8);
+        if (rc) return rc;
+        HIPCHK(ctx, hipMemcpy(&h[mg::kMaxWAll], ctx->mg + mg::kMaxWAll, 8 * ctx->comm.nranks, hipMemcpyDeviceToHost));
+        for (int r = 0; r < ctx->comm.nranks; ++r) {
+            double v;
+            memcpy(&v, &h[mg::kMaxWAll + r], 8);
+            if (v > mx) mx = v;
+        }
+    }
+    ctx->ctl_host->wexp = dm_weight_exp(mx);
+    return write_ctl(ctx);
+}
+
 extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64_t stride, uint64_t count,
                                           eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints)
 {
@@ -1250,19 +1332,22 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
     if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
-    int rc = materialize(ctx);
+    mrec(ctx, 0);
+    int rc = materialize(ctx);              // may run a copy-on-write pass for migrated stores
     if (rc) return rc;
-    uint32_t ndup = 0;
-    rc = store_cow(ctx, &ndup);
+    mrec(ctx, 1);
+    rc = store_cow(ctx);
     if (rc) return rc;
+    mrec(ctx, 2);
     MergeParams mp;
     memset(&mp, 0, sizeof(mp));
+    mp.cnt = ctx->merge_cnt;
     mp.n = ctx->n;
     mp.m = count;
     for (uint32_t k = 0; k < count; ++k)
         mp.sp[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
     HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->store, &mp, ctx->stream));
-    ctx->last_map_copies = ndup;
+    mrec(ctx, 3);
     return ESLAM_OK;
 }
 
@@ -1329,19 +1414,15 @@ static GatherView gather_view(eslam_ctx* ctx)
 // cloneMaps (src/PoseEstimator.cpp:31-47) as copy on write: particles that share a store get
 // private copies, and particles received from another rank (sid = kSidRecord | record) get a
 // free store filled from their record's payload.  *ndup: the copies made.
-static int store_cow(eslam_ctx* ctx, uint32_t* ndup_out)
+static int store_cow(eslam_ctx* ctx)
 {
-    int rc = read_ctl(ctx);                   // the current buffer (base ^ flip after the commit)
-    if (rc) return rc;
-    uint32_t* sid = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip].sid;
+    // the current buffer's store names (base ^ flip after the commit, read by the kernels)
+    const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
     uint32_t* ndup_dev = ctx->cow + 3 * ctx->cap + 2 * ((ctx->cap + 2047) / 2048) + 2;
-    HIPCHK(ctx, eslam_launch_store_cow(sid, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->stream));
-    uint32_t ndup = 0;
-    HIPCHK(ctx, hipMemcpyAsync(&ndup, ndup_dev, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    HIPCHK(ctx, eslam_launch_store_copy(sid, &ctx->store, ctx->n, ctx->cow, ndup, ctx->recvpay, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_cow(sr, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_copy(sr, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->recvpay,
+                                        ctx->merge_cnt + 2 * kMergeCounterSlots, ctx->stream));
     ctx->cow_pending = false;
-    if (ndup_out) *ndup_out = ndup;
     return ESLAM_OK;
 }
 
@@ -1353,7 +1434,7 @@ static int materialize(eslam_ctx* ctx)
     HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], ctx->n, ctx->gbase, ctx->ctl, &gv, aux, ctx->stream));
     // a sharded resample handed this rank particles whose stores are still in the received
     // payloads: they get local stores before anything reads a store
-    if (ctx->cow_pending) return store_cow(ctx, nullptr);
+    if (ctx->cow_pending) return store_cow(ctx);
     return ESLAM_OK;
 }
 
@@ -1772,7 +1853,7 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     }
     // logDebug records: the update's contact points are recorded on the projected state, so
     // the project runs as its own launch first (bit-identical to the fused kernel)
-    const bool records = weight && record_contacts(ctx) && !ctx->sharded;
+    const bool records = weight && record_contacts(ctx);   // one GPU only (eslam_gpu_set_comm refuses it)
     if (respawn || (records && project)) {
         const GatherView gv0 = gather_view(ctx);
         HIPCHK(ctx, eslam_launch_project_weight(1, 0, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
@@ -1884,6 +1965,9 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         info->uniform_reset = (int32_t)c.uniform;
         info->resample_overruns = c.overruns;
         info->update_count = c.update_count;
+        info->map_patches_dropped = c.map_dropped;
+        info->map_stores_copied = c.map_copied;
+        info->map_stores_changed = c.map_changed;
     }
     if (ctx->timing && ctx->ring_steps) {
         double acc[5] = {0, 0, 0, 0, 0};
@@ -1901,6 +1985,22 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         t.resample_ms = (float)(acc[3] * inv);
         t.total_ms = (float)(acc[4] * inv);
         ctx->ring_steps = 0;
+    }
+    if (ctx->timing && ctx->mring_steps) {
+        double acc[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < ctx->mring_steps; ++k) {
+            hipEvent_t* e = &ctx->mring[4 * k];
+            float ms;
+            for (int j = 0; j < 3; ++j) { ms = 0; (void)hipEventElapsedTime(&ms, e[j], e[j + 1]); acc[j] += ms; }
+            ms = 0; (void)hipEventElapsedTime(&ms, e[0], e[3]); acc[3] += ms;
+        }
+        eslam_kernel_times& t = ctx->times;
+        const double inv = 1.0 / ctx->mring_steps;
+        t.map_gather_ms = (float)(acc[0] * inv);
+        t.map_cow_ms = (float)(acc[1] * inv);
+        t.map_merge_ms = (float)(acc[2] * inv);
+        t.map_total_ms = (float)(acc[3] * inv);
+        ctx->mring_steps = 0;
     }
     return take_update_error(ctx);
 }
@@ -2094,6 +2194,7 @@ extern "C" int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable)
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->timing = enable != 0;
     ctx->ring_steps = 0;
+    ctx->mring_steps = 0;
     return ESLAM_OK;
 }
 

@@ -70,6 +70,9 @@ struct alignas(128) Ctl {
     uint64_t bbox[4];                    // particle bounding box of the last weighting (keys)
     uint32_t k3_base;                    // the buffer the last weighting kernel wrote (base ^ flip at
                                          // its start): the fused K3 reads it while block 0 commits
+    uint64_t map_dropped;                // scan patches the last map merge could not store (full stores)
+    uint64_t map_changed;                // stores the last map merge changed
+    uint64_t map_copied;                 // stores copied on write since the map merge before it
 };
 
 enum FinMode : uint32_t {
@@ -197,10 +200,20 @@ struct ScanPatch {
     double x, y, z, stdev;
 };
 constexpr int kMaxScanPatches = 64;
+constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
+
+// the store names of both state buffers; the copy-on-write kernels use the current one
+// (base ^ flip read on the device, so the host never waits for the commit)
+struct SidRef {
+    uint32_t* s0;
+    uint32_t* s1;
+    const Ctl* ctl;
+};
 struct MergeParams {
     uint64_t n;
     uint32_t m;                          // scan patches
     uint32_t pad;
+    uint64_t* cnt;                       // 2 x kMergeCounterSlots: dropped patches, changed stores (zeroed)
     ScanPatch sp[kMaxScanPatches];
 };
 

@@ -328,21 +328,20 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         ly = ((kd(a, 4) * px + kd(a, 5) * py) + kd(a, 6) * pz) + kd(a, 7);
         lz = ((kd(b, 0) * px + kd(b, 1) * py) + kd(b, 2) * pz) + kd(b, 3);
     }
-    double fm = floor((lx - kd(h, 4)) * kd(h, 2));
-    double fn = floor((ly - kd(h, 5)) * kd(h, 3));
+    const double ux = (lx - kd(h, 4)) * kd(h, 2);
+    const double uy = (ly - kd(h, 5)) * kd(h, 3);
     // fast path without branches: an in-window cell whose first patch passes the gate (the
     // window is only staged for maps without heights).  Everything else -- off the window,
     // heights, a failing first patch of a multi-patch cell -- takes the loop below.  The
-    // window lies inside the grid, so the window test alone decides the fast path: the
-    // conversions clamp out-of-range values (far outside the window) and only a NaN, which
-    // converts to 0, needs its own test.
+    // window lies inside the grid and starts at cell 1 in both directions, so the window test
+    // needs no floor: v_cvt_i32_f64 truncates (saturating; NaN -> 0), which equals the floor
+    // for every value >= 0, and maps every value < 1 -- negatives, NaN -- below the window.
     int im, in;                          // v_cvt_i32_f64 itself: defined for every input
-    asm("v_cvt_i32_f64 %0, %1" : "=v"(im) : "v"(fm));
-    asm("v_cvt_i32_f64 %0, %1" : "=v"(in) : "v"(fn));
-    const bool num = (fm + fn) == (fm + fn);
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(im) : "v"(ux));
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(in) : "v"(uy));
     const WinBounds wb = win_bounds();
     const uint32_t wm = (uint32_t)im - (uint32_t)wb.m0, wn = (uint32_t)in - (uint32_t)wb.n0;
-    const bool in_win = num & (wb.on != 0) & (wm < (uint32_t)wb.cols) & (wn < (uint32_t)(wb.n1 - wb.n0));
+    const bool in_win = (wb.on != 0) & (wm < (uint32_t)wb.cols) & (wn < (uint32_t)(wb.n1 - wb.n0));
     const WinCell wc = win.cells[in_win ? wn * (uint32_t)wb.cols + wm : 0u];
     const double pm = (double)wc.mean0, ps = (double)wc.stdev0;
     const double diff = dm_fabs(pm - lz);
@@ -350,6 +349,10 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     mean = pm;
     stdev = ps;
     if (gate0) return true;
+    // the cell by the floor (outside the window trunc and floor differ)
+    const double fm = floor(ux), fn = floor(uy);
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(im) : "v"(fm));
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(in) : "v"(fn));
     const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     if constexpr (DELTA) {
         if (!in_grid || (in_win && wc.count == 1)) return false;
@@ -420,11 +423,13 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
             const double fn0 = floor((ly0 - m.offset_y) * m.inv_scale_y) - 1.0;
             const double fn1 = floor((ly1 - m.offset_y) * m.inv_scale_y) + 2.0;
             if (dm_isfinite(fm0) && dm_isfinite(fm1) && dm_isfinite(fn0) && dm_isfinite(fn1)) {
+                // the window starts at cell 1 (get_patch's floor-free window test); cells of
+                // column / row 0 take the general path
                 const double W = (double)m.width, H = (double)m.height_cells;
-                const int m0 = (int)(fm0 < 0 ? 0 : (fm0 > W ? W : fm0));
-                const int m1 = (int)(fm1 < 0 ? 0 : (fm1 > W ? W : fm1));
-                const int n0 = (int)(fn0 < 0 ? 0 : (fn0 > H ? H : fn0));
-                const int n1 = (int)(fn1 < 0 ? 0 : (fn1 > H ? H : fn1));
+                const int m0 = (int)(fm0 < 1 ? 1 : (fm0 > W ? W : fm0));
+                const int m1 = (int)(fm1 < 1 ? 1 : (fm1 > W ? W : fm1));
+                const int n0 = (int)(fn0 < 1 ? 1 : (fn0 > H ? H : fn0));
+                const int n1 = (int)(fn1 < 1 ? 1 : (fn1 > H ? H : fn1));
                 const int rows = n1 - n0, cols = m1 - m0;
                 if (rows > 0 && cols > 0 && (int64_t)rows * cols * (int64_t)sizeof(WinCell) <= kWindowLds) {
                     on = 1;
@@ -1243,8 +1248,11 @@ __global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ si
 }
 
 // owner[s] = the lowest particle naming store s (~0: no particle does, the store is free)
-__global__ void __launch_bounds__(kBlock) k_store_owner(const uint32_t* __restrict__ sid, uint64_t n, uint32_t* __restrict__ owner)
+__device__ __forceinline__ uint32_t* cur_sid(const SidRef& r) { return (r.ctl->base ^ r.ctl->flip) ? r.s1 : r.s0; }
+
+__global__ void __launch_bounds__(kBlock) k_store_owner(SidRef sr, uint64_t n, uint32_t* __restrict__ owner)
 {
+    const uint32_t* sid = cur_sid(sr);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n && !(sid[i] & kSidRecord)) atomicMin(&owner[sid[i]], (uint32_t)i);
 }
@@ -1260,8 +1268,9 @@ constexpr int kCompactItems = 8;
 constexpr int kCompactTile = kBlock * kCompactItems;
 
 __global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, const uint32_t* __restrict__ owner,
-                                                          const uint32_t* __restrict__ sid, uint32_t* __restrict__ counts)
+                                                          SidRef sr, uint32_t* __restrict__ counts)
 {
+    const uint32_t* sid = cur_sid(sr);
     __shared__ uint32_t s_w[kWaves];
     const uint64_t base = (uint64_t)blockIdx.x * kCompactTile;
     uint32_t c = 0;
@@ -1277,9 +1286,10 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, 
 
 // offs: exclusive prefix of counts; each selected i goes to out[offs[b] + its rank in the tile]
 __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, const uint32_t* __restrict__ owner,
-                                                          const uint32_t* __restrict__ sid, const uint32_t* __restrict__ offs,
+                                                          SidRef sr, const uint32_t* __restrict__ offs,
                                                           uint32_t* __restrict__ out)
 {
+    const uint32_t* sid = cur_sid(sr);
     __shared__ uint32_t s_w[kWaves];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t base = (uint64_t)blockIdx.x * kCompactTile;
@@ -1300,34 +1310,44 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, 
 }
 
 // copy on write: the j-th sharing particle takes the j-th free store, a copy of the one it
-// shared (one thread per slot); a particle received from another rank, a copy of its record's
-// payload (pay: the received payloads, sharded filters)
+// shared (one thread per used slot: slots >= kStoreCap stay free in every store); a particle
+// received from another rank, a copy of its record's payload (pay: the received payloads,
+// sharded filters).  A fixed grid strides over the *ndup_dev copies, so the count never
+// travels to the host.
 __global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                       uint64_t ndup, uint32_t* __restrict__ sid, MapStore ms,
-                                                       const StorePayload* __restrict__ pay)
+                                                       const uint32_t* __restrict__ ndup_dev, SidRef sr,
+                                                       MapStore ms, const StorePayload* __restrict__ pay)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= ndup * kStoreSlots) return;
-    const uint64_t j = t / kStoreSlots;
-    const uint32_t slot = (uint32_t)(t - j * kStoreSlots);
-    const uint32_t p = dups[j], from = sid[p], to = frees[j];
-    if (from & kSidRecord) {
-        const StorePayload& q = pay[from & ~kSidRecord];
-        ms.key[(uint64_t)to * kStoreSlots + slot] = slot < kStoreCap ? q.key[slot] : kStoreFree;
-        ms.val[(uint64_t)to * kStoreSlots + slot] = slot < kStoreCap ? q.val[slot] : make_float2(0.0f, 0.0f);
-        if (slot == 0) ms.count[to] = q.count;
-        return;
+    const uint32_t* sid = cur_sid(sr);
+    const uint64_t total = (uint64_t)*ndup_dev * kStoreCap;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t j = t / kStoreCap;
+        const uint32_t slot = (uint32_t)(t - j * kStoreCap);
+        const uint32_t p = dups[j], from = sid[p], to = frees[j];
+        if (from & kSidRecord) {
+            const StorePayload& q = pay[from & ~kSidRecord];
+            ms.key[(uint64_t)to * kStoreSlots + slot] = q.key[slot];
+            ms.val[(uint64_t)to * kStoreSlots + slot] = q.val[slot];
+            if (slot == 0) ms.count[to] = q.count;
+            continue;
+        }
+        ms.key[(uint64_t)to * kStoreSlots + slot] = ms.key[(uint64_t)from * kStoreSlots + slot];
+        ms.val[(uint64_t)to * kStoreSlots + slot] = ms.val[(uint64_t)from * kStoreSlots + slot];
+        if (slot == 0) ms.count[to] = ms.count[from];
     }
-    ms.key[(uint64_t)to * kStoreSlots + slot] = ms.key[(uint64_t)from * kStoreSlots + slot];
-    ms.val[(uint64_t)to * kStoreSlots + slot] = ms.val[(uint64_t)from * kStoreSlots + slot];
-    if (slot == 0) ms.count[to] = ms.count[from];
 }
 
+// the sharing particles name their copies; the copies are counted for the next map update's
+// statistics (acc: the merge counter slots' copy accumulator)
 __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                         uint64_t ndup, uint32_t* __restrict__ sid)
+                                                         const uint32_t* __restrict__ ndup_dev, SidRef sr,
+                                                         uint64_t* __restrict__ acc)
 {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j < ndup) sid[dups[j]] = frees[j];
+    uint32_t* sid = cur_sid(sr);
+    const uint64_t ndup = *ndup_dev;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *acc += ndup;     // one thread; the kernels of a stream run in order
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < ndup; j += (uint64_t)gridDim.x * kBlock)
+        sid[dups[j]] = frees[j];
 }
 
 // processMap(scanMap, match = false, update = true) per particle: every scan patch, placed at
@@ -1345,7 +1365,7 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 // in-flight lane keeps a 384-B store hot).
 constexpr int kMergeBlock = 128;                 // 2 waves: 37 KB of LDS, 4 blocks per CU
 constexpr int kMergePad = 65;
-__global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+__global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
                                                            MapStore ms, MergeParams mp)
 {
     // only the kStoreCap slots that can be used are staged (the rest stay free in memory)
@@ -1388,6 +1408,8 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bool dirty = false;                  // a patch inserted or fused: the store is written back
+    uint32_t dropped = 0;                // patches a full store could not take
     if (valid) {
         const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
         uint32_t count = ms.count[sid];
@@ -1446,6 +1468,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                         const double m = (m1 * var + wz * v1) / (v1 + var);
                         const double v = (v1 * var) / (v1 + var);
                         s_val[w][pos][lane] = make_float2((float)m, (float)dm_sqrt(v));
+                        dirty = true;
                     }
                 } else if (count < kStoreCap) {
                     // insert at pos: shift the larger keys up one slot (count < kStoreCap < kStoreSlots)
@@ -1456,6 +1479,9 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     s_key[w][pos][lane] = target;
                     s_val[w][pos][lane] = make_float2((float)wz, (float)dm_sqrt(var));
                     ++count;
+                    dirty = true;
+                } else {
+                    ++dropped;
                 }
             }
         }
@@ -1464,15 +1490,41 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // write back (a fuse changes only values; written whole, like the staging)
+    dropped = wave_sum_u32(dropped);
+    // write back the changed stores (written whole, like the staging); once the stores are
+    // full and the scan repeats, most merges change nothing
+    const uint64_t dmask = __ballot(dirty);
+    if (lane == 0) {                     // one address per block slot: no single hot atomic
+        const uint32_t slot_c = blockIdx.x % kMergeCounterSlots;
+        if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
+        if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
+    }
+    if (dmask == 0ull) return;
 #pragma unroll 4
     for (uint32_t q = 0; q < 32; ++q) {
         const uint32_t pp = 2u * q + half;
         const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
-        if (i0 + pp < mp.n && slot < kStoreCap) {
+        if (((dmask >> pp) & 1ull) && slot < kStoreCap) {
             ms.key[(uint64_t)sp_ * kStoreSlots + slot] = s_key[w][slot][pp];
             ms.val[(uint64_t)sp_ * kStoreSlots + slot] = s_val[w][slot][pp];
         }
+    }
+}
+
+// the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads)
+__global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl)
+{
+    __shared__ uint64_t s[2][kMergeCounterSlots / 64];
+    const uint32_t t = threadIdx.x;
+    const uint64_t d = wave_sum_u64(cnt[t]), c = wave_sum_u64(cnt[kMergeCounterSlots + t]);
+    if ((t & 63u) == 0) { s[0][t >> 6] = d; s[1][t >> 6] = c; }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t sd = 0, sc = 0;
+        for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) { sd += s[0][w]; sc += s[1][w]; }
+        ctl->map_dropped = sd;
+        ctl->map_changed = sc;
+        ctl->map_copied = cnt[2 * kMergeCounterSlots];        // the copy-on-write copies since the last merge
     }
 }
 
@@ -1892,16 +1944,17 @@ __device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word
         bool timeout = sp.spin_limit == 0;       // testing: give up at once
         if (tid == 0) {
             uint32_t spins = 0;
-            while (!timeout && __hip_atomic_load(fin_word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            // relaxed agent-scope polls and copies: on gfx950 an agent-scope atomic load reads
+            // through this XCD's L2 to memory, where block 0's release store (a write-back of its
+            // L2) has put the ctl lines.  Acquire loads (or an acquire fence) here invalidate
+            // the L2 in every block: K3 53 -> 91 us at 4M, 18 -> 48 us at 256k (r03b).
+            while (!timeout && atomic_load_agent(fin_word) != epoch) {
                 if (spins++ >= sp.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(8);
             }
             *s_flag = timeout ? 1u : 0u;
             if (timeout) raise_timeout(ctl, sp.fault);
         }
-        // block 0's release store of the epoch pairs with the acquire load above: its ctl
-        // writes are visible to this wave's loads below
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (tid < (uint32_t)kCtlWords) s_img[tid] = atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + tid);
     }
     __syncthreads();
@@ -2842,7 +2895,7 @@ extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms,
 // copy on write of the map stores (before a merge): owner, the free-store and the sharing-
 // particle lists (compactions), the copies, the renames.  scratch: owner (n) + counts and
 // offsets (2 x tiles) + frees (n) + dups (n) words.  *ndup_dev: the number of copies (device).
-extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
+extern "C" hipError_t eslam_launch_store_cow(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
                                              hipStream_t stream)
 {
     if (!n) return hipSuccess;
@@ -2868,28 +2921,36 @@ extern "C" hipError_t eslam_launch_store_cow(uint32_t* sid, const MapStore* ms, 
     return e != hipSuccess ? e : hipGetLastError();
 }
 
-// the copies and renames for ndup sharing particles (host-read count)
-extern "C" hipError_t eslam_launch_store_copy(uint32_t* sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint64_t ndup,
-                                              const void* payloads, hipStream_t stream)
+// the copies and renames for the sharing particles, their count read on the device (ndup_dev,
+// written by eslam_launch_store_cow); copies_acc: where the copies are counted
+extern "C" hipError_t eslam_launch_store_copy(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch,
+                                              const uint32_t* ndup_dev, const void* payloads, uint64_t* copies_acc,
+                                              hipStream_t stream)
 {
-    if (!ndup) return hipSuccess;
+    if (!n) return hipSuccess;
     const uint32_t tiles = (uint32_t)((n + kCompactTile - 1) / kCompactTile);
     uint32_t* frees = scratch + n + 2ull * tiles + 2;
     uint32_t* dups = frees + n;
-    const uint64_t slots = ndup * kStoreSlots;
-    hipLaunchKernelGGL(k_store_copy, dim3((uint32_t)((slots + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, dups, frees, ndup,
-                       sid, *ms, (const StorePayload*)payloads);
-    hipLaunchKernelGGL(k_store_rename, dim3((uint32_t)((ndup + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, dups, frees, ndup,
-                       sid);
+    // grids for the worst case (every particle a copy), capped: the loops stride
+    const uint64_t want_c = (n * kStoreCap + kBlock - 1) / kBlock, want_r = (n + kBlock - 1) / kBlock;
+    const uint32_t gc = (uint32_t)(want_c < 8192 ? want_c : 8192), gr = (uint32_t)(want_r < 2048 ? want_r : 2048);
+    hipLaunchKernelGGL(k_store_copy, dim3(gc), dim3(kBlock), 0, stream, dups, frees, ndup_dev, sid, *ms,
+                       (const StorePayload*)payloads);
+    hipLaunchKernelGGL(k_store_rename, dim3(gr), dim3(kBlock), 0, stream, dups, frees, ndup_dev, sid, copies_acc);
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const MapStore* ms,
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream)
 {
+    hipError_t e = hipMemsetAsync(mp->cnt, 0, 2 * kMergeCounterSlots * sizeof(uint64_t), stream);
+    if (e != hipSuccess) return e;
     if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kMergeBlock - 1) / kMergeBlock)), dim3(kMergeBlock), 0,
                                   stream, s0, s1, ctl, *map, *ms, *mp);
-    return hipGetLastError();
+    hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
+    // the copy accumulator starts over for the next map update
+    e = hipMemsetAsync(mp->cnt + 2 * kMergeCounterSlots, 0, sizeof(uint64_t), stream);
+    return e != hipSuccess ? e : hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,

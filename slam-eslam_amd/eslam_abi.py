@@ -158,6 +158,9 @@ class UpdateInfo(C.Structure):
         ("uniform_reset", C.c_int32),
         ("resample_overruns", C.c_uint64),
         ("update_count", C.c_uint64),
+        ("map_patches_dropped", C.c_uint64),
+        ("map_stores_copied", C.c_uint64),
+        ("map_stores_changed", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -186,6 +189,10 @@ class KernelTimes(C.Structure):
         ("normalize_scan_ms", C.c_float),
         ("resample_ms", C.c_float),
         ("total_ms", C.c_float),
+        ("map_gather_ms", C.c_float),
+        ("map_cow_ms", C.c_float),
+        ("map_merge_ms", C.c_float),
+        ("map_total_ms", C.c_float),
     ]
 
 

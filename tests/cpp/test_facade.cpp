@@ -180,6 +180,73 @@ int main()
         EXPECT(raw.getBestParticleIndex() == best, "best particle");
     }
 
+    // ---- getParticles() is the filter's particles: an edit through the reference reaches the
+    // filter, as processMap's weighting (src/EmbodiedSlamFilter.cpp:183-220) relies on.  The
+    // same edits through the raw ABI (download, edit, upload) give the same particles. --------
+    {
+        eslam_ns::Configuration ec = eslamConfig;
+        ec.particleCount = 2000;
+        eslam_ns::EmbodiedSlamFilter ef(odometryConfig, ec);
+        ef.init(env, startPose, true);
+        eslam_ns::FootContact odo(odometryConfig);
+        eslam_ns::PoseEstimator raw(odo, ec);
+        const eslam_mls_grid g = env.toC();
+        EXPECT(eslam_gpu_set_map(raw.handle(), &g) == ESLAM_OK, "edit: raw set_map");
+        const double p0[3] = {0, 0, 0.18}, q0[4] = {1, 0, 0, 0};
+        EXPECT(eslam_gpu_init_pose(raw.handle(), p0, q0) == ESLAM_OK, "edit: raw init");
+        const size_t n = 2000;
+        std::vector<double> X(n), Y(n), TH(n), Z(n), ZS(n), W(n), M(n);
+        std::vector<uint8_t> FL(n), NC(n);
+        eslam_particles p = {X.data(), Y.data(), TH.data(), Z.data(), ZS.data(), W.data(), M.data(), FL.data(), NC.data()};
+        auto factor = [](size_t i) { return 1.0 + 0.5 * (double)((i * 2654435761u) % 7u) / 7.0; };
+        double ex = 0, eyaw = 0;
+        for (int s = 0; s < 6; ++s) {
+            eyaw += 0.002;
+            ex += 0.02;
+            const eslam_ns::Affine3d T = body_pose(ex, 0, eyaw);
+            const eslam_ns::BodyContactState bs = body_state(ex, 0, eyaw);
+            ef.update(T, bs, terrainClassification);
+            const eslam_ns::Quaterniond q(T.linear());
+            odo.update(bs, q);
+            const eslam_step_input in = raw.makeInput(bs, q, T.translation(), 0);
+            int u = 0;
+            EXPECT(eslam_gpu_step(raw.handle(), &in, &u) == ESLAM_OK, "edit: raw step");
+            if (s % 2 == 1) {
+                // a per-particle weighting through the vector (processMap(match): w *= weight^0.1)
+                std::vector<eslam_ns::PoseParticle>& ps = ef.getParticles();
+                for (size_t i = 0; i < ps.size(); ++i) ps[i].weight *= factor(i);
+                if (s == 3) ps[7].position = eslam_ns::Vector2d(ps[7].position.x() + 0.01, ps[7].position.y());
+                EXPECT(eslam_gpu_download_particles(raw.handle(), &p) == ESLAM_OK, "edit: raw download");
+                for (size_t i = 0; i < n; ++i) W[i] *= factor(i);
+                if (s == 3) X[7] += 0.01;
+                EXPECT(eslam_gpu_upload_particles(raw.handle(), n, &p) == ESLAM_OK, "edit: raw upload");
+            }
+        }
+        std::vector<eslam_ns::PoseParticle>& a = ef.getParticles();
+        EXPECT(eslam_gpu_download_particles(raw.handle(), &p) == ESLAM_OK, "edit: raw final download");
+        size_t diff = a.size() != n;
+        for (size_t i = 0; i < a.size() && i < n; ++i)
+            diff += std::memcmp(&a[i].position.v[0], &X[i], 8) || std::memcmp(&a[i].position.v[1], &Y[i], 8) ||
+                    std::memcmp(&a[i].orientation, &TH[i], 8) || std::memcmp(&a[i].zPos, &Z[i], 8) ||
+                    std::memcmp(&a[i].zSigma, &ZS[i], 8) || std::memcmp(&a[i].weight, &W[i], 8) ||
+                    std::memcmp(&a[i].mprob, &M[i], 8) || a[i].floating != (FL[i] != 0) || a[i].cpoints.size() != NC[i];
+        EXPECT(diff == 0, "edits through getParticles() == download / edit / upload, bit for bit");
+        EXPECT(&a == &ef.getParticles(), "getParticles() hands out the same vector");
+    }
+
+    // ---- UpdateThreshold::test(const Affine3d&) (src/Configuration.hpp:23-26, Q6 kept) -----
+    {
+        const eslam_ns::UpdateThreshold th(0.1, 10 * M_PI / 180.0);
+        eslam_ns::Affine3d turn = body_pose(0, 0, 0.15);
+        turn.translation() = eslam_ns::Vector3d(0, 0, 0);
+        eslam_ns::Affine3d small = eslam_ns::Affine3d::Identity(), big = eslam_ns::Affine3d::Identity();
+        small.translation() = eslam_ns::Vector3d(0.05, 0, 0);
+        big.translation() = eslam_ns::Vector3d(0.18, 0, 0);
+        EXPECT(th.test(turn), "a 0.15 rad turn exceeds the distance threshold 0.1 (angle and distance swapped)");
+        EXPECT(!th.test(small), "5 cm: neither 0 > 0.1 nor 0.05 > 10 deg");
+        EXPECT(th.test(big), "18 cm exceeds the angle threshold 10 deg = 0.1745 (swapped)");
+    }
+
     // ---- adapters from reference-shaped types ---------------------------------------------
     {
         ref::Configuration rc;

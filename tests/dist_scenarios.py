@@ -10,8 +10,9 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "maps")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps")
 CONFIG3_STEPS = 3
+MAP_SAMPLES = 64                                 # config4: particles whose maps are compared
 
 
 def scenario_config(name, n_global):
@@ -23,9 +24,9 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3", "maps"):
+    if name in ("forced", "config3", "config4", "maps"):
         S.bench_config(cfg, n_global)
-        if name == "maps":                       # useSharedMap = false: per-particle maps
+        if name in ("maps", "config4"):          # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
     else:
         cfg.particle_count = n_global
@@ -41,6 +42,8 @@ def scenario_grid(name):
         return hash_grid(cells=60)
     if name == "config3":
         return S.flat_map(cells=1000)             # the bench's 100 x 100 m map
+    if name == "config4":                         # bench.py --local-maps: rough, scans map x > 0.3 m
+        return S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
     if name == "maps":                            # the front feet stand on cells only the scans map
         return S.unmapped_beyond(S.rough_map(cells=120), 0.3)
     return S.rough_map(cells=120) if name != "forced" else S.rough_map(cells=120, multi=False)
@@ -51,17 +54,35 @@ def digest(a):
     return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8)).hexdigest()
 
 
-def run_config3(f, n_global, lo, hi, info_fn):
+def map_samples(n_global):
+    """global indices of the particles whose maps config4 compares"""
+    return sorted(set(np.linspace(0, n_global - 1, MAP_SAMPLES).astype(np.int64).tolist()))
+
+
+def run_config3(f, n_global, lo, hi, info_fn, name="config3"):
     """BASELINE configs[3]'s workload (bench map, forced update + resample, init as the bench)
     for CONFIG3_STEPS steps; records per-step info and, at the end, a SHA-256 of every field of
     this shard / slice [lo, hi) and of the last step's ancestors (a 16M-particle snapshot is
-    too large to ship between processes)."""
+    too large to ship between processes).  name="config4": configs[4]'s workload instead --
+    per-particle maps on the rough map unmapped beyond x = 0.3 m, tilted body, one scan merged
+    after every step -- plus the SHA-256 of the maps of map_samples() in [lo, hi)."""
     rec = {}
-    f.set_map(scenario_grid("config3"))
+    maps = name == "config4"
+    f.set_map(scenario_grid(name))
     f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
-    for k, st in enumerate(S.step_stream(CONFIG3_STEPS)):
+    scan = S.scan_patches() if maps else None
+    for k, st in enumerate(S.step_stream(CONFIG3_STEPS, tilt=maps)):
         f.step(st)
+        if maps:
+            f.map_update(scan)
         _info(rec, f"s{k}", info_fn(f))
+    if maps:
+        for g in map_samples(n_global):
+            if lo <= g < hi:
+                c, m, s = f.particle_map(g - lo)
+                o = np.argsort(c)
+                rec[f"map/{g}"] = np.array(digest(np.concatenate([c[o].view(np.uint8), m[o].view(np.uint8),
+                                                                  s[o].view(np.uint8)])))
     pa = f.download()
     anc = f.ancestors()
     best, rng = np.array([f.best_index()]), np.array([f.rng_state().minstd_x])

@@ -27,11 +27,14 @@ def main():
     import eslam_dist
     from dist_scenarios import run_scenario, scenario_config
     rank = int(os.environ["RANK"])
+    # rendezvous through a file the launcher names (no TCP port to race for); env:// otherwise
+    store = os.environ.get("ESLAM_DIST_STORE")
+    init = dict(init_method="file://" + store, rank=rank, world_size=int(os.environ["WORLD_SIZE"])) if store else {}
     if kind == "gpu" and mem in ("device", "rccl"):
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", **init)
     else:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", **init)
     comm = eslam_dist.TorchComm(device_memory=(mem in ("device", "rccl")))
     cfg = scenario_config(name, n_global)
     bounds = A.shard_bounds(n_global, comm.nranks)
@@ -47,9 +50,9 @@ def main():
             f = eslam_dist.RcclShardedGpuFilter(cfg, n_global, rank, comm.nranks, device=dev)
         else:
             f = eslam_dist.ShardedGpuFilter(cfg, n_global, comm, device=dev)
-        if name == "config3":
+        if name in ("config3", "config4"):
             from dist_scenarios import digest, run_config3
-            rec, fields, anc, best, rng = run_config3(f, n_global, lo, hi, info_fn=lambda g: g.sync())
+            rec, fields, anc, best, rng = run_config3(f, n_global, lo, hi, info_fn=lambda g: g.sync(), name=name)
             for fld, v in fields.items():
                 rec[f"sha/{fld}"] = np.array(digest(v))
             rec["sha/anc"] = np.array(digest(anc.astype(np.uint32)))

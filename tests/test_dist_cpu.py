@@ -3,7 +3,6 @@ multi-GPU decomposition) over gloo, world sizes 2 and 3, through the same eslam_
 callbacks (slam-eslam_amd/eslam_dist.TorchComm) the GPU library uses.  A sharded run
 concatenated over the ranks equals the one-process filter bit for bit."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -16,29 +15,16 @@ from dist_scenarios import run_scenario, scenario_config
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def launch(kind, name, n_global, world, tmp, mem="host", timeout=240):
-    """Run the ranks; a rendezvous port another process took between free_port() and the
-    bind (EADDRINUSE) is retried on a new port, at most twice (no GPU work has started)."""
-    for attempt in range(3):
-        res = _launch_once(kind, name, n_global, world, tmp, mem, timeout)
-        if res is not None:
-            return res
-    raise AssertionError("rendezvous port in use three times")
-
-
-def _launch_once(kind, name, n_global, world, tmp, mem, timeout):
-    port = free_port()
+    """Run the ranks; they meet through a FileStore in `tmp` (no rendezvous port to race for)."""
+    store = os.path.join(tmp, f"store_{kind}_{name}_{world}_{mem}")
+    if os.path.exists(store):
+        os.remove(store)
     procs, outs = [], []
     for r in range(world):
         out = os.path.join(tmp, f"{kind}_{name}_{world}_{r}.npz")
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), ESLAM_DIST_STORE=store,
+                   OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), kind, name, str(n_global),
                                        out, mem], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
         outs.append(out)
@@ -51,8 +37,6 @@ def _launch_once(kind, name, n_global, world, tmp, mem, timeout):
                 q.kill()
             raise
         logs.append(o.decode(errors="replace"))
-    if any(p.returncode != 0 for p in procs) and any("EADDRINUSE" in log for log in logs):
-        return None
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
     return [dict(np.load(o)) for o in outs]

@@ -80,3 +80,45 @@ def test_config3_eight_ranks_equal_single_context(oracle, tmp_path):
         getattr(after, fld)[:] = fields[fld]
     check_resample_properties(anc, after, n_global)
     f.close()
+
+
+@pytest.mark.timeout(1500)
+def test_config4_eight_ranks_equal_single_context(oracle, tmp_path):
+    """BASELINE configs[4]'s decomposition on one GPU: 64M particles with per-particle maps as
+    8 ranks x 8M (gloo, host staging; the ranks share the card), 3 steps of bench.py
+    --local-maps' workload (rough map unmapped beyond x = 0.3 m, a scan merged into every
+    particle's map after each step, forced resample).  Every rank's shard equals the same slice
+    of ONE 64M-particle context bit for bit (all fields, the last resample's ancestors as
+    global indices, the maps of 64 sampled particles -- a migrated particle carries its store),
+    every rank reports the single context's update info, best index and RNG state, and the
+    single context's last resample passes the stratified-resample properties."""
+    import eslam_abi as A
+    import eslam_amd
+    from dist_scenarios import CONFIG3_STEPS, FIELDS, digest, map_samples, run_config3, scenario_config
+    from parity_util import check_resample_properties
+    n_global, world = 64 * 1024 * 1024, 8
+    parts = launch("gpu", "config4", n_global, world, str(tmp_path), mem="host", timeout=1200)
+    f = eslam_amd.GpuFilter(scenario_config("config4", n_global))
+    rec, fields, anc, best, rng = run_config3(f, n_global, 0, n_global, info_fn=lambda g: g.sync(), name="config4")
+    bounds = A.shard_bounds(n_global, world)
+    seen = 0
+    for r, p in enumerate(parts):
+        lo, hi = bounds[r], bounds[r + 1]
+        assert tuple(p["range"]) == (lo, hi)
+        for fld in FIELDS:
+            assert str(p[f"sha/{fld}"]) == digest(fields[fld][lo:hi]), f"rank {r}: {fld} differs"
+        assert str(p["sha/anc"]) == digest(anc[lo:hi].astype(np.uint32)), f"rank {r}: ancestors differ"
+        for k in range(CONFIG3_STEPS):
+            assert np.array_equal(p[f"s{k}/info"].view(np.uint64), rec[f"s{k}/info"].view(np.uint64)), (r, k)
+        assert int(p["best"][0]) == int(best[0]) and int(p["rng"][0]) == int(rng[0])
+        for g in map_samples(n_global):
+            if lo <= g < hi:
+                assert str(p[f"map/{g}"]) == str(rec[f"map/{g}"]), f"rank {r}: map of particle {g} differs"
+                seen += 1
+    assert seen == len(map_samples(n_global))
+    assert rec[f"s{CONFIG3_STEPS - 1}/info"][6] == 1.0        # resampled
+    after = A.ParticleArrays(n_global)
+    for fld in FIELDS:
+        getattr(after, fld)[:] = fields[fld]
+    check_resample_properties(anc, after, n_global)
+    f.close()

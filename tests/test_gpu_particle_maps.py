@@ -20,6 +20,22 @@ def u32(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
 
+MAP_INFO = ("map_patches_dropped", "map_stores_copied", "map_stores_changed")
+
+
+def map_info(i):
+    return tuple(int(getattr(i, f)) for f in MAP_INFO)
+
+
+def assert_maps_equal(gpu, orc, idx, label):
+    for i in idx:
+        gc, gm, gs = gpu.particle_map(i)
+        oc, om, os_ = orc.particle_map(i)
+        go, oo = np.argsort(gc), np.argsort(oc)
+        assert np.array_equal(gc[go], oc[oo]), (label, i)
+        assert np.array_equal(u32(gm[go]), u32(om[oo])) and np.array_equal(u32(gs[go]), u32(os_[oo])), (label, i)
+
+
 @pytest.mark.parametrize("terrain,n,records", [("flat", 600, False), ("rough", 5003, False), ("rough", 2048, True)])
 def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
     cfg = S.bench_config(A.default_config(), n)
@@ -37,12 +53,17 @@ def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
         f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
     scan = S.scan_patches()
     stream = S.step_stream(24, tilt=(terrain == "rough"))
+    dropped = 0
     for k, st in enumerate(stream):
         assert gpu.step(st) == orc.step(st)
         gpu.map_update(scan)
         orc.map_update(scan)
-        gpu.sync()
+        gi = gpu.sync()
         assert_bit_identical(gpu.download(), orc.download(), f"{terrain} n={n} step {k}")
+        # a full store's dropped patches, the copy-on-write copies and the changed stores
+        # of every map update equal the oracle's (deep copies, open-addressing stores)
+        assert map_info(gi) == map_info(orc.info()), (k, map_info(gi), map_info(orc.info()))
+        dropped += gi.map_patches_dropped
         if k % 6 == 5:
             for i in list(range(0, n, max(n // 40, 1))) + [n - 1]:
                 gc, gm, gs = gpu.particle_map(i)
@@ -50,6 +71,7 @@ def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
                 go, oo = np.argsort(gc), np.argsort(oc)
                 assert np.array_equal(gc[go], oc[oo]), (k, i)
                 assert np.array_equal(u32(gm[go]), u32(om[oo])) and np.array_equal(u32(gs[go]), u32(os_[oo])), (k, i)
+    assert dropped > 0                   # the 48-patch scan overflows the 24-patch stores
     if records:
         rec, cps = gpu.download_records(max_cpoints=4)
         ncp, cp, _, _ = orc.debug()
@@ -90,12 +112,35 @@ def test_particle_maps_bench_workload(gpu_mod, oracle):
         assert gpu.step(st) == orc.step(st)
         gpu.map_update(scan)
         orc.map_update(scan)
-    gpu.sync()
+        assert map_info(gpu.sync()) == map_info(orc.info()), k
     assert_bit_identical(gpu.download(), orc.download(), "local maps 256k")
-    for i in [0, 1, 4097, n // 2, n - 1]:
-        gc, gm, gs = gpu.particle_map(i)
-        oc, om, os_ = orc.particle_map(i)
-        go, oo = np.argsort(gc), np.argsort(oc)
-        assert np.array_equal(gc[go], oc[oo]), i
-        assert np.array_equal(u32(gm[go]), u32(om[oo])) and np.array_equal(u32(gs[go]), u32(os_[oo])), i
+    assert_maps_equal(gpu, orc, [0, 1, 4097, n // 2, n - 1], "256k")
     assert np.mean(gpu.download().n_contact_points >= 2) > 0.1
+
+
+@pytest.mark.timeout(900)
+def test_particle_maps_config4_shard_size(gpu_mod, oracle):
+    """configs[4] at its per-GPU size: 8M particles (64M over 8 GPUs) with per-particle
+    maps on the bench workload, 3 steps, bit-exact against the oracle (16 threads): every
+    particle after the last step, the map-update counts of every step, and the maps of 40
+    sampled particles."""
+    n = 8 * 1024 * 1024
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS
+    grid = S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    orc.set_threads(16)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    scan = S.scan_patches()
+    for k, st in enumerate(S.step_stream(3, tilt=True)):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+        assert map_info(gpu.sync()) == map_info(orc.info()), k
+    assert_bit_identical(gpu.download(), orc.download(), "local maps 8M")
+    idx = sorted(set(np.linspace(0, n - 1, 38).astype(np.int64).tolist() + [1, n // 2 + 1]))
+    assert_maps_equal(gpu, orc, idx, "8M")
+    gpu.close()
