@@ -1996,6 +1996,11 @@ double or_dm(int fn, double x, double y)
     case 12: return dm_weighting_function(x, 0.0, y, 0.0);
     case 13: dm_sincos2pi(x, &s, &c); return s;
     case 14: dm_sincos2pi(x, &s, &c); return c;
+    case 15: return dm_log_bm(x);
+    case 16: dm_sincos2pi32((uint32_t)x, &s, &c); return s;
+    case 17: dm_sincos2pi32((uint32_t)x, &s, &c); return c;
+    case 18: dm_box_muller32((uint32_t)x, (uint32_t)y, &s, &c); return s;   /* z0 */
+    case 19: dm_box_muller32((uint32_t)x, (uint32_t)y, &s, &c); return c;   /* z1 */
     default: return NAN;
     }
 }

@@ -2761,21 +2761,27 @@ __global__ void k_selftest_math(int fn, const double* x, const double* y, double
     case 9: r = dm_from_bits(dm_fx61(x[i])); break;
     case 13: dm_sincos2pi(x[i], &s, &c); r = s; break;
     case 14: dm_sincos2pi(x[i], &s, &c); r = c; break;
+    case 15: r = dm_log_bm(x[i]); break;
+    case 16: dm_sincos2pi32((uint32_t)x[i], &s, &c); r = s; break;
+    case 17: dm_sincos2pi32((uint32_t)x[i], &s, &c); r = c; break;
+    case 18: dm_box_muller32((uint32_t)x[i], (uint32_t)y[i], &s, &c); r = s; break;
+    case 19: dm_box_muller32((uint32_t)x[i], (uint32_t)y[i], &s, &c); r = c; break;
     default: r = __builtin_nan("");
     }
     out[i] = r;
 }
 
-// every Box-Muller radius: the range-restricted log/sqrt against the general ones, for all
-// 2^32 uniform words (counts the words whose radius differs in any bit)
+// every Box-Muller radius: the range-restricted sqrt against the general one on -2 log u, for
+// all 2^32 uniform words (counts the words whose radius differs in any bit)
 __global__ void __launch_bounds__(kBlock) k_selftest_bm_radius(unsigned long long* bad)
 {
     uint32_t cnt = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x; a < (1ull << 32); a += stride) {
         const double u = dm_u32((uint32_t)a);
-        const double fast = dm_sqrt_pos(-2.0 * dm_log_pos(u));
-        const double ref = dm_sqrt(-2.0 * dm_log(u));
+        const double l = -2.0 * dm_log_bm(u);
+        const double fast = dm_sqrt_pos(l);
+        const double ref = dm_sqrt(l);
         cnt += dm_bits(fast) != dm_bits(ref) ? 1u : 0u;
     }
     cnt = wave_sum_u32(cnt);

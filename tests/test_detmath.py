@@ -202,3 +202,35 @@ def test_div_recip_equals_division(tmp_path_factory, mode, arg):
     out = subprocess.run([_check_div_bin(tmp_path_factory), mode, arg], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert " 0 mismatches" in out.stdout
+
+
+def test_log_bm(dm):
+    """the Box-Muller log (dm_log_bm: 128-interval table + log1p series) against mpmath over
+    the uniform words' range, both ends and the interval boundaries included"""
+    a = _rng().integers(0, 2 ** 32, 6000, dtype=np.uint64)
+    us = list((a.astype(np.float64) + 0.5) * 2.0 ** -32)
+    us += [2.0 ** -33, (2.0 ** 32 - 0.5) * 2.0 ** -32, 0.5, 0.75, 0.99609375, 1.0 - 2.0 ** -40]
+    us += [0.75 + i / 256 for i in range(64)] + [0.5 * (1 + i / 128) for i in range(64)]
+    worst = max(ulp_err(dm(15, float(u)), mp.log(mp.mpf(float(u)))) for u in us)
+    assert worst <= 2.0
+
+
+@pytest.mark.parametrize("fn,ref", [(16, mp.sin), (17, mp.cos)])
+def test_sincos2pi32(dm, fn, ref):
+    """sin/cos of the Box-Muller angle 2 pi (b + 1/2) 2^-32 from the 32-bit word (dm_sincos2pi32:
+    256-entry table + Taylor series + angle sums) against mpmath"""
+    b = list(_rng().integers(0, 2 ** 32, 6000, dtype=np.uint64)) + [0, 2 ** 32 - 1, 2 ** 30, 2 ** 31, 3 * 2 ** 30, 2 ** 24 - 1]
+    worst_abs = max(abs(dm(fn, float(x)) - float(ref(2 * mp.pi * (mp.mpf(int(x)) + mp.mpf(0.5)) / 2 ** 32))) for x in b)
+    assert worst_abs <= 3.5e-16
+
+
+def test_box_muller32_normals(dm):
+    """the contract's Box-Muller pair from two words against the same formula in mpmath"""
+    rng = _rng()
+    for a, b in zip(rng.integers(0, 2 ** 32, 2000), rng.integers(0, 2 ** 32, 2000)):
+        u = (mp.mpf(int(a)) + mp.mpf(0.5)) / 2 ** 32
+        t = 2 * mp.pi * (mp.mpf(int(b)) + mp.mpf(0.5)) / 2 ** 32
+        r = mp.sqrt(-2 * mp.log(u))
+        for fn, want in ((18, r * mp.cos(t)), (19, r * mp.sin(t))):
+            got = dm(fn, float(a), float(b))
+            assert abs(got - float(want)) <= 8e-16 * max(1.0, abs(float(want))), (a, b, fn)
