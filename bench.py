@@ -32,9 +32,10 @@ BYTES_K3 = 29                 # k_normalize_segments: read w, mprob, flags (17),
 BYTES_STEP = BYTES_K1 + BYTES_K3   # what the fused step moves per particle-update: the step roofline
 BYTES_K1_DELTA = BYTES_K1 + 4  # per-particle maps: + the store name (store lookups hit L2: the stores of
                                # the cells under the feet, a few per particle and step)
-BYTES_MERGE_READ = 336        # k_map_merge per particle: store name 4, count 4, 24 keys + 24 {mean, stdev} 288,
-                              # pose x, y, theta, z, zsigma 40
-BYTES_MERGE_WRITE = 292       # per changed store: 24 keys + 24 values written back, count
+BYTES_MERGE_READ = 148        # k_map_merge per particle: store name 4, class 4, count 4, 24 keys 96, pose x, y,
+                              # theta, z, zsigma 40 (the values are read only by a changing particle)
+BYTES_MERGE_WRITE = 488       # per changed store: 24 values read 192, 24 keys + 24 values written back 288,
+                              # count 4, the new name 4
 CONFIG3_GLOBAL = 16 * 1024 * 1024  # BASELINE configs[3]: 16M particles over 8 GPUs
 CONFIG4_GLOBAL = 64 * 1024 * 1024  # BASELINE configs[4]: 64M particles over 8 GPUs
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -409,10 +410,11 @@ def main():
         "last_update": {"effective": info.effective, "resampled": info.resampled},
         **({"map_update": {"patches_dropped": info.map_patches_dropped, "stores_copied": info.map_stores_copied,
                            "stores_changed": info.map_stores_changed,
-                           "note": "the last step's map update: scan patches full stores could not take, stores "
-                                   "copied on write after the resample, stores the merge changed and wrote back; "
-                                   "kernel_ms.map_* time the update's phases (map_cow_ms includes the host read of "
-                                   "the copy count)"}} if args.local_maps else {}),
+                           "note": "the last step's map update: scan patches full stores could not take, shared "
+                                   "stores a change copied on write, stores the merge changed and wrote back; "
+                                   "kernel_ms.map_* time the update's phases (map_cow_ms: the stores' sharing "
+                                   "classes and the free-store list); the timed steps include the stores' fill "
+                                   "phase unless --warmup covers it (DESIGN.md 5c)"}} if args.local_maps else {}),
         "build_id": eslam_amd.build_id(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

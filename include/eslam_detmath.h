@@ -1442,4 +1442,31 @@ DM_FN double dm_weighting_function(double x, double alpha, double beta, double g
     return 0.0;
 }
 
+/* int32 of a double, saturating (NaN -> 0): the device's v_cvt_i32_f64 */
+DM_FN int32_t dm_cvt_sat_i32(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t q;
+    __asm__("v_cvt_i32_f64 %0, %1" : "=v"(q) : "v"(x));
+    return q;
+#else
+    if (x != x) return 0;
+    return x >= 2147483647.0 ? 2147483647 : (x <= -2147483648.0 ? (-2147483647 - 1) : (int32_t)x);
+#endif
+}
+
+/* processMap's placement of a scan patch (sx, sy) at a particle, Translation(x, y, 0) * Rz(theta)
+ * (src/EmbodiedSlamFilter.cpp:186-189), and the grid cell it lands in, for an identity
+ * global2local: m = floor((co sx - sn sy + x - offset_x) / scale_x) evaluated as
+ * fma(co, sx, fma(-sn, sy, bx)) * inv_scale_x with bx = x - offset_x (per particle), n likewise.
+ * Returns the cell index, 0xffffffff off the grid.  The caller skips particles whose bx, by or
+ * theta are not finite (no NaN reaches the conversions).                                  */
+DM_FN uint32_t dm_merge_cell(double bx, double by, double co, double sn, double sx, double sy, double inv_x,
+                             double inv_y, uint32_t width, uint32_t height)
+{
+    const int32_t m = dm_cvt_sat_i32(dm_floor(dm_fma(co, sx, dm_fma(-sn, sy, bx)) * inv_x));
+    const int32_t n = dm_cvt_sat_i32(dm_floor(dm_fma(sn, sx, dm_fma(co, sy, by)) * inv_y));
+    return ((uint32_t)m < width && (uint32_t)n < height) ? (uint32_t)n * width + (uint32_t)m : 0xffffffffu;
+}
+
 #endif /* ESLAM_DETMATH_H */

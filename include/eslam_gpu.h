@@ -162,10 +162,11 @@ typedef struct eslam_update_info {
     uint64_t update_count;
     /* the last eslam_gpu_map_update (per-particle maps): scan patches a particle's map could
      * not take because its store already held ESLAM_STORE_CAP patches (summed over the
-     * particles), and the stores copied on write before the merge                          */
+     * particles); maps the merge changed while another particle shared them (copy on write:
+     * written to a free store the particle then names); maps the merge changed in all      */
     uint64_t map_patches_dropped;
     uint64_t map_stores_copied;
-    uint64_t map_stores_changed;           /* stores the merge changed (written back)        */
+    uint64_t map_stores_changed;
 } eslam_update_info;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */
@@ -390,8 +391,8 @@ typedef struct eslam_kernel_times {
     float resample_ms;
     float total_ms;
     /* eslam_gpu_map_update (per-particle maps), averaged over the map updates of the timed
-     * region: the pending resample gather, the copy-on-write of shared stores (including its
-     * host read of the copy count), the merge kernel, and the whole call                   */
+     * region: the pending resample gather, the stores' sharing classes and the free-store
+     * list (copy on write's bookkeeping), the merge kernel, and the whole call             */
     float map_gather_ms;
     float map_cow_ms;
     float map_merge_ms;

@@ -586,8 +586,11 @@ struct or_filter {
     float* pm_val;                       /* n x 32 x {mean, stdev} */
     uint32_t* pm_count;                  /* n */
     uint64_t* pm_id;                     /* n: which map a particle holds (the resample copies the
-                                            id with the map); distinct ids at a map update =
-                                            the maps cloneMaps did not need to copy */
+                                            id with the map; a particle that changes a map it
+                                            shares, or receives one from another rank, takes a
+                                            fresh id): the sharing that the GPU's copy on write
+                                            keeps (map_stores_copied) */
+    uint64_t pm_fresh;                   /* the next fresh id (bit 63 | gbase << 32 | counter) */
 };
 
 
@@ -686,6 +689,7 @@ static int or_alloc_particles(or_filter* f, uint64_t n)
         f->pm_id = malloc(b * 8);
         if (!f->pm_key || !f->pm_val || !f->pm_count || !f->pm_id) return ESLAM_ERR_OUT_OF_MEMORY;
         for (uint64_t i = 0; i < n; ++i) f->pm_id[i] = f->gbase + i;
+        f->pm_fresh = (1ull << 63) | ((uint64_t)f->gbase << 32);
     }
     f->has_anc = 0;
     return f->x ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
@@ -1587,7 +1591,8 @@ static void resample_sharded(or_filter* f, int shift)
         f->anc[o] = anc[o];
         if (f->pm_key) {
             f->pm_count[o] = m->pm_count;
-            f->pm_id[o] = m->pm_id;
+            /* a map from another rank arrives as a copy of its own (the GPU: a store per record) */
+            f->pm_id[o] = m->src - f->gbase < n ? m->pm_id : f->pm_fresh++;
             memcpy(f->pm_key + o * OR_STORE_SLOTS, m->pm_key, sizeof(m->pm_key));
             memcpy(f->pm_val + o * OR_STORE_SLOTS * 2, m->pm_val, sizeof(m->pm_val));
         }
@@ -1860,6 +1865,12 @@ void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
  * (variance-weighted) with the particle's patch there when within 3 sigma, ignored on the
  * shared grid's cells and when the particle already holds 24 patches.  (cloneMaps' copies
  * are the deep copies of gather().)                                                       */
+static int cmp_u64(const void* a, const void* b)
+{
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
 int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 {
     if (!f->pm_key) return ESLAM_ERR_INVALID_ARG;
@@ -1869,20 +1880,24 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     int is_id = 1;
     for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
-    /* the copies cloneMaps made since the last merge (one context: every particle beyond the
-     * first that holds a map), then every particle holds its own again */
-    {
-        const uint64_t ng = NG(f);
-        uint64_t* seen = calloc(ng / 64 + 1, 8);
-        uint64_t distinct = 0;
-        for (uint64_t i = 0; i < f->n; ++i) {
-            const uint64_t d = f->pm_id[i];
-            if (!(seen[d / 64] >> (d % 64) & 1ull)) { seen[d / 64] |= 1ull << (d % 64); ++distinct; }
+    /* which particles share their map with another (copies of one map the resample made and
+     * no map update has changed since): the ids sorted, a particle's id looked up */
+    uint64_t* sorted = malloc((f->n ? f->n : 1) * 8);
+    uint8_t* shared = calloc(f->n ? f->n : 1, 1);
+    uint8_t* dirt = calloc(f->n ? f->n : 1, 1);
+    if (!sorted || !shared || !dirt) { free(sorted); free(shared); free(dirt); return ESLAM_ERR_OUT_OF_MEMORY; }
+    memcpy(sorted, f->pm_id, f->n * 8);
+    qsort(sorted, f->n, 8, cmp_u64);
+    for (uint64_t i = 0; i < f->n; ++i) {
+        uint64_t lo = 0, hi = f->n;          /* first index with sorted[] >= id */
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if (sorted[mid] < f->pm_id[i]) lo = mid + 1;
+            else hi = mid;
         }
-        free(seen);
-        f->info.map_stores_copied = f->n - distinct;
-        for (uint64_t i = 0; i < f->n; ++i) f->pm_id[i] = f->gbase + i;
+        shared[i] = lo + 1 < f->n && sorted[lo + 1] == f->pm_id[i];
     }
+    free(sorted);
     uint64_t dropped = 0, changed = 0;
     const int64_t n = (int64_t)f->n;
     /* particles are independent: the OpenMP threads of or_set_threads (same results) */
@@ -1895,19 +1910,26 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
         double sn, co;
         dm_sincos(f->th[OD(i)], &sn, &co);
         const double zvar = f->zs[OD(i)] * f->zs[OD(i)];
+        const double bx = f->x[OD(i)] - g->offset_x, by = f->y[OD(i)] - g->offset_y;
+        const int placed = dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(f->th[OD(i)]);
         for (uint32_t k = 0; k < m; ++k) {
-            const double wx = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[OD(i)];
-            const double wy = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
             const double wz = sp[k].position[2] + f->z[OD(i)];
-            double lx = wx, ly = wy;
-            if (!is_id) {
-                lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-                ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+            uint32_t cell;
+            if (is_id) {
+                if (!placed) continue;
+                cell = dm_merge_cell(bx, by, co, sn, sp[k].position[0], sp[k].position[1], 1.0 / g->scale_x,
+                                     1.0 / g->scale_y, g->width, g->height);
+                if (cell == 0xffffffffu) continue;
+            } else {
+                const double wx = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[OD(i)];
+                const double wy = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
+                const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+                const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
+                const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
+                if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
+                cell = (uint32_t)fn * g->width + (uint32_t)fm;
             }
-            const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
-            const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
-            if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
-            const uint32_t cell = (uint32_t)fn * g->width + (uint32_t)fm;
             if (g->cell_start[cell] != g->cell_start[cell + 1]) continue;
             const double var = sp[k].stdev * sp[k].stdev + zvar;
             uint32_t h = dm_store_hash(cell);
@@ -1941,9 +1963,17 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
         }
         f->pm_count[i] = count;
         changed += (uint64_t)dirty;
+        dirt[i] = (uint8_t)dirty;
     }
+    /* a changed shared map becomes the particle's own (the GPU writes it to a free store) */
+    uint64_t copied = 0;
+    for (uint64_t i = 0; i < f->n; ++i)
+        if (dirt[i] && shared[i]) { f->pm_id[i] = f->pm_fresh++; ++copied; }
+    free(shared);
+    free(dirt);
     f->info.map_patches_dropped = dropped;
     f->info.map_stores_changed = changed;
+    f->info.map_stores_copied = copied;
     return 0;
 }
 

@@ -25,12 +25,10 @@ using namespace eslam_dev;
 
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
                                                    const DebugRec* d, const MapStore* store, hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_cow(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
-                                             hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_copy(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch,
-                                              const uint32_t* ndup_dev, const void* payloads, uint64_t* copies_acc,
-                                              hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, uint64_t pool, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_receive(SidRef sid, const MapStore* ms, uint64_t n, const CowScratch* cs,
+                                                 const void* payloads, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
@@ -279,6 +277,7 @@ struct eslam_ctx {
     uint32_t* d_cells = nullptr;
     float2* d_patch = nullptr;
     float* d_height = nullptr;
+    uint32_t* d_occ = nullptr;               // MapView::occ
     uint32_t maxp = 4;
     // host-side filter state
     uint64_t proj_event = 0, init_event = 0, hash_event = 0;
@@ -436,7 +435,7 @@ extern "C" void eslam_config_default(eslam_config* c)
 extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 static int materialize(eslam_ctx* ctx);
-static int store_cow(eslam_ctx* ctx);
+static int store_receive(eslam_ctx* ctx);
 
 static const char* kPoisonMsg =
     "resample scan: a cross-block wait gave up (a preceding tile's total or the finalize never arrived); "
@@ -574,8 +573,8 @@ static void free_particles(eslam_ctx* ctx)
 
 static void free_map(eslam_ctx* ctx)
 {
-    (void)hipFree(ctx->d_cells); (void)hipFree(ctx->d_patch); (void)hipFree(ctx->d_height);
-    ctx->d_cells = nullptr; ctx->d_patch = nullptr; ctx->d_height = nullptr;
+    (void)hipFree(ctx->d_cells); (void)hipFree(ctx->d_patch); (void)hipFree(ctx->d_height); (void)hipFree(ctx->d_occ);
+    ctx->d_cells = nullptr; ctx->d_patch = nullptr; ctx->d_height = nullptr; ctx->d_occ = nullptr;
     ctx->has_map = false;
 }
 
@@ -648,14 +647,16 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
         HIPCHK(ctx, hipMalloc(&ctx->sid_mem, 2 * cap * 4));
         ctx->st[0].sid = ctx->sid_mem;
         ctx->st[1].sid = ctx->sid_mem + cap;
-        HIPCHK(ctx, hipMalloc(&ctx->store.key, cap * kStoreSlots * 4));
-        HIPCHK(ctx, hipMalloc(&ctx->store.val, cap * kStoreSlots * sizeof(float2)));
-        HIPCHK(ctx, hipMalloc(&ctx->store.count, cap * 4));
-        const uint64_t tiles = (cap + 2047) / 2048;
-        HIPCHK(ctx, hipMalloc(&ctx->cow, (3 * cap + 2 * tiles + 2 + 1) * 4));
-        HIPCHK(ctx, hipMalloc(&ctx->merge_cnt, (2 * kMergeCounterSlots + 1) * sizeof(uint64_t)));
-        HIPCHK(ctx, hipMemset(ctx->merge_cnt, 0, (2 * kMergeCounterSlots + 1) * sizeof(uint64_t)));
-        HIPCHK(ctx, eslam_launch_store_init(ctx->st[0].sid, &ctx->store, cap, ctx->stream));
+        // the store pool: twice the particles, so a map update always finds a free store for
+        // every particle that changes a shared map (eslam_internal.h store_pool)
+        const uint64_t pool = store_pool(cap);
+        HIPCHK(ctx, hipMalloc(&ctx->store.key, pool * kStoreSlots * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->store.val, pool * kStoreSlots * sizeof(float2)));
+        HIPCHK(ctx, hipMalloc(&ctx->store.count, pool * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->cow, cow_words(cap) * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->merge_cnt, 3 * kMergeCounterSlots * sizeof(uint64_t)));
+        HIPCHK(ctx, hipMemset(ctx->merge_cnt, 0, 3 * kMergeCounterSlots * sizeof(uint64_t)));
+        HIPCHK(ctx, eslam_launch_store_init(ctx->st[0].sid, &ctx->store, cap, pool, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->n = n;
@@ -935,8 +936,18 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
         HIPCHK(ctx, hipMalloc(&ctx->d_height, np * 4));
         HIPCHK(ctx, hipMemcpy(ctx->d_height, g->patch_height, g->n_patches * 4, hipMemcpyHostToDevice));
     }
+    {
+        // one bit per cell: the shared grid holds patches there (the map merge's per-patch test
+        // is one 4-byte load instead of the cell's two range words)
+        std::vector<uint32_t> occ((ncell + 31) / 32, 0u);
+        for (uint64_t c = 0; c < ncell; ++c)
+            if (g->cell_start[c] != g->cell_start[c + 1]) occ[c >> 5] |= 1u << (c & 31);
+        HIPCHK(ctx, hipMalloc(&ctx->d_occ, occ.size() * 4));
+        HIPCHK(ctx, hipMemcpy(ctx->d_occ, occ.data(), occ.size() * 4, hipMemcpyHostToDevice));
+    }
     MapView& m = ctx->map;
     m.cell_start = ctx->d_cells;
+    m.occ = ctx->d_occ;
     m.patch = ctx->d_patch;
     m.height = ctx->d_height;
     m.has_height = ctx->d_height ? 1u : 0u;
@@ -1333,15 +1344,18 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
     mrec(ctx, 0);
-    int rc = materialize(ctx);              // may run a copy-on-write pass for migrated stores
+    int rc = materialize(ctx);              // may give received particles their stores
     if (rc) return rc;
     mrec(ctx, 1);
-    rc = store_cow(ctx);
-    if (rc) return rc;
+    const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
+    const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
+    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, ctx->stream));
     mrec(ctx, 2);
     MergeParams mp;
     memset(&mp, 0, sizeof(mp));
     mp.cnt = ctx->merge_cnt;
+    mp.ref = cs.ref;
+    mp.frees = cs.frees;
     mp.n = ctx->n;
     mp.m = count;
     for (uint32_t k = 0; k < count; ++k)
@@ -1411,17 +1425,16 @@ static GatherView gather_view(eslam_ctx* ctx)
 
 // before the particle state is read or replaced outside the hot path: run a pending
 // gather (device decides; a no-op otherwise) and commit the buffer flip
-// cloneMaps (src/PoseEstimator.cpp:31-47) as copy on write: particles that share a store get
-// private copies, and particles received from another rank (sid = kSidRecord | record) get a
-// free store filled from their record's payload.  *ndup: the copies made.
-static int store_cow(eslam_ctx* ctx)
+// cloneMaps (src/PoseEstimator.cpp:31-47) as copy on write: a resample's copies of a particle
+// share its store until a map update changes one of them (k_map_merge).  Particles received
+// from another rank (sid = kSidRecord | record) get free stores filled from their records'
+// payloads before anything reads a store.
+static int store_receive(eslam_ctx* ctx)
 {
-    // the current buffer's store names (base ^ flip after the commit, read by the kernels)
     const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
-    uint32_t* ndup_dev = ctx->cow + 3 * ctx->cap + 2 * ((ctx->cap + 2047) / 2048) + 2;
-    HIPCHK(ctx, eslam_launch_store_cow(sr, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->stream));
-    HIPCHK(ctx, eslam_launch_store_copy(sr, &ctx->store, ctx->n, ctx->cow, ndup_dev, ctx->recvpay,
-                                        ctx->merge_cnt + 2 * kMergeCounterSlots, ctx->stream));
+    const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
+    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_receive(sr, &ctx->store, ctx->n, &cs, ctx->recvpay, ctx->stream));
     ctx->cow_pending = false;
     return ESLAM_OK;
 }
@@ -1434,7 +1447,7 @@ static int materialize(eslam_ctx* ctx)
     HIPCHK(ctx, eslam_launch_resample_gather(ctx->st[0], ctx->st[1], ctx->n, ctx->gbase, ctx->ctl, &gv, aux, ctx->stream));
     // a sharded resample handed this rank particles whose stores are still in the received
     // payloads: they get local stores before anything reads a store
-    if (ctx->cow_pending) return store_cow(ctx);
+    if (ctx->cow_pending) return store_receive(ctx);
     return ESLAM_OK;
 }
 
@@ -1510,7 +1523,7 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
 // tile size never changes a result.
 static uint32_t scan_items(uint64_t n)
 {
-    // measured (tools/ab_items.sh, bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
+    // measured (round-2 A/B, profiles/r02/ab_items_256k_fused.log; bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
     // 64k and 256k (over 2 items, themselves +19 % over 8 at 256k), 2 or 4 items +4 % at 1M,
     // 8 items best from 4M on (fewer tiles_before re-sums)
     if (n <= (1ull << 18)) return 1u;

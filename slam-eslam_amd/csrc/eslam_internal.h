@@ -72,7 +72,7 @@ struct alignas(128) Ctl {
                                          // its start): the fused K3 reads it while block 0 commits
     uint64_t map_dropped;                // scan patches the last map merge could not store (full stores)
     uint64_t map_changed;                // stores the last map merge changed
-    uint64_t map_copied;                 // stores copied on write since the map merge before it
+    uint64_t map_copied;                 // shared stores the last map merge wrote to a free store
 };
 
 enum FinMode : uint32_t {
@@ -94,8 +94,10 @@ struct DevState {
 // sorted by key = cell + 1 (free slots, all after the used ones, hold kStoreFree): a lookup is
 // a 5-step binary search with no data-dependent trip count (the oracle's open-addressing
 // table holds the same set: membership and values do not depend on the layout).
-// Particles name their store (DevState::sid); the resample copies the name, and the next map
-// update gives every later copy of an ancestor a private copy of its store (copy on write).
+// Particles name their store (DevState::sid); the resample copies the name, so a store may be
+// named by several particles, and a map update that changes a shared store writes the result
+// to a free store that the particle then names (copy on write: a store is never written while
+// another particle names it; the unchanged copies keep sharing).
 constexpr uint32_t kStoreSlots = 32;
 constexpr uint32_t kStoreCap = 24;
 constexpr uint32_t kStoreFree = 0xffffffffu;
@@ -110,8 +112,8 @@ struct alignas(8) StorePayload {
 };
 static_assert(kStoreSlots == 32 && kStoreCap < kStoreSlots, "store search: 5 halving steps, a free slot at the end");
 struct MapStore {
-    uint32_t* key;                       // n stores x kStoreSlots
-    float2* val;                         // n stores x kStoreSlots: {mean, stdev}
+    uint32_t* key;                       // store_pool(cap) stores x kStoreSlots
+    float2* val;                         // store_pool(cap) stores x kStoreSlots: {mean, stdev}
     uint32_t* count;                     // patches per store
 };
 
@@ -125,6 +127,7 @@ struct MapView {
     uint32_t has_height;                 // height != nullptr
     const float* height;                 // nullable: all horizontal
     double g2l[12];
+    const uint32_t* occ;                 // bit c: the shared grid has patches in cell c (the map merge's test)
 };
 
 struct ContactC {
@@ -209,11 +212,48 @@ struct SidRef {
     uint32_t* s1;
     const Ctl* ctl;
 };
+// The store pool holds 2 x cap stores: at most n <= cap are named by a particle, so at least
+// cap are free whenever a map update starts, and particle i may take the i-th free store
+// (copy on write with a fixed, deterministic allocation and no allocation counter).
+inline uint64_t store_pool(uint64_t cap) { return 2 * cap; }
+// the copy-on-write scratch (u32 words): ref (pool), the two compactions' tile counts, the
+// free stores (pool), the received particles (cap), the received count, the free count
+struct CowScratch {
+    uint32_t* ref;                       // particles naming each store
+    uint32_t* counts;                    // 2 x (tiles + 1)
+    uint32_t* frees;                     // the stores no particle names, in store order
+    uint32_t* dups;                      // the particles received from another rank (sid = kSidRecord | record)
+    uint32_t* ndup;
+    uint32_t* nfree;
+    uint32_t tiles;                      // compaction tiles over the pool (>= the tiles over the particles)
+};
+constexpr int kCompactItems = 8;                // k_compact_*: items per thread
+constexpr int kCompactTileItems = kBlock * kCompactItems;
+inline uint64_t cow_words(uint64_t cap)
+{
+    const uint64_t pool = store_pool(cap), tiles = (pool + kCompactTileItems - 1) / kCompactTileItems;
+    return pool + 2 * (tiles + 1) + pool + cap + 2;
+}
+inline CowScratch cow_layout(uint32_t* base, uint64_t cap)
+{
+    const uint64_t pool = store_pool(cap), tiles = (pool + kCompactTileItems - 1) / kCompactTileItems;
+    CowScratch c;
+    c.ref = base;
+    c.counts = c.ref + pool;
+    c.frees = c.counts + 2 * (tiles + 1);
+    c.dups = c.frees + pool;
+    c.ndup = c.dups + cap;
+    c.nfree = c.ndup + 1;
+    c.tiles = (uint32_t)tiles;
+    return c;
+}
 struct MergeParams {
     uint64_t n;
     uint32_t m;                          // scan patches
     uint32_t pad;
-    uint64_t* cnt;                       // 2 x kMergeCounterSlots: dropped patches, changed stores (zeroed)
+    uint64_t* cnt;                       // 3 x kMergeCounterSlots: dropped patches, changed stores, copies (zeroed)
+    const uint32_t* ref;                 // CowScratch::ref of this update
+    const uint32_t* frees;               // CowScratch::frees: particle i's store if it writes a shared map
     ScanPatch sp[kMaxScanPatches];
 };
 

@@ -1237,37 +1237,54 @@ __global__ void __launch_bounds__(1024) k_scan_excl(uint32_t* __restrict__ a, ui
 // scan into every particle's map (src/EmbodiedSlamFilter.cpp:179-232) and cloneMaps' "no two
 // particles share a map" (src/PoseEstimator.cpp:31-47) as copy on write of the map stores.
 // ---------------------------------------------------------------------------------------
-// fresh maps: particle i names store i, every store empty
-__global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ sid, MapStore ms, uint64_t n)
+// fresh maps: particle i names store i, every store of the pool empty
+__global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ sid, MapStore ms, uint64_t n, uint64_t pool)
 {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    sid[i] = (uint32_t)i;
+    if (i >= pool) return;
+    if (i < n) sid[i] = (uint32_t)i;
     ms.count[i] = 0;
     for (uint32_t t = 0; t < kStoreSlots; ++t) ms.key[i * kStoreSlots + t] = kStoreFree;
 }
 
-// owner[s] = the lowest particle naming store s (~0: no particle does, the store is free)
 __device__ __forceinline__ uint32_t* cur_sid(const SidRef& r) { return (r.ctl->base ^ r.ctl->flip) ? r.s1 : r.s0; }
 
-__global__ void __launch_bounds__(kBlock) k_store_owner(SidRef sr, uint64_t n, uint32_t* __restrict__ owner)
+// ref[s]: 0, 1 or >= 2 particles name store s (received particles name none yet; the map merge
+// only asks "free", "own" or "shared").  A resample hands the copies of a particle out as
+// consecutive outputs, so equal names come in runs: the first lane of a run within the wave
+// raises ref to 2 with a plain store when the run is longer than one (no atomic: as sharing
+// grows, long runs span many waves and one hot atomic per wave serialised at 0.6 ms per 8M),
+// and adds 1 atomically otherwise.  Any interleaving ends at the right class.
+__global__ void __launch_bounds__(kBlock) k_store_ref(SidRef sr, uint64_t n, uint32_t* __restrict__ ref)
 {
     const uint32_t* sid = cur_sid(sr);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n && !(sid[i] & kSidRecord)) atomicMin(&owner[sid[i]], (uint32_t)i);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t s = i < n ? sid[i] : kStoreFree;
+    const uint32_t prev = (uint32_t)__shfl_up((int)s, 1, 64);
+    const bool head = lane == 0 || prev != s;
+    const uint64_t heads = __ballot(head);
+    const uint64_t above = lane == 63 ? 0ull : heads >> (lane + 1);
+    const uint32_t len = above ? (uint32_t)__builtin_ctzll(above) + 1u : 64u - lane;
+    if (head && !(s & kSidRecord)) {                               // kStoreFree has the record bit
+        if (len >= 2u) {
+            if (ref[s] < 2u) ref[s] = 2u;
+        } else {
+            atomicAdd(&ref[s], 1u);
+        }
+    }
 }
 
-// compaction, mode 0: free stores (no owner) in store order; mode 1: particles that share
-// their store with a lower particle, in particle order.  The two lists have equal length.
-__device__ __forceinline__ bool compact_pred(int mode, uint64_t i, const uint32_t* owner, const uint32_t* sid)
+// compaction, mode 0: the free stores (ref 0) in store order, over the pool; mode 1: the
+// particles received from another rank (sid = kSidRecord | record), in particle order
+__device__ __forceinline__ bool compact_pred(int mode, uint64_t i, const uint32_t* ref, const uint32_t* sid)
 {
-    return mode == 0 ? owner[i] == ~0u : ((sid[i] & kSidRecord) || owner[sid[i]] != (uint32_t)i);
+    return mode == 0 ? ref[i] == 0u : (sid[i] & kSidRecord) != 0u;
 }
 
-constexpr int kCompactItems = 8;
-constexpr int kCompactTile = kBlock * kCompactItems;
+constexpr int kCompactTile = kCompactTileItems;
 
-__global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, const uint32_t* __restrict__ owner,
+__global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, const uint32_t* __restrict__ ref,
                                                           SidRef sr, uint32_t* __restrict__ counts)
 {
     const uint32_t* sid = cur_sid(sr);
@@ -1276,7 +1293,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, 
     uint32_t c = 0;
     for (int r = 0; r < kCompactItems; ++r) {
         const uint64_t i = base + (uint64_t)r * kBlock + threadIdx.x;
-        if (i < n && compact_pred(mode, i, owner, sid)) ++c;
+        if (i < n && compact_pred(mode, i, ref, sid)) ++c;
     }
     c = wave_sum_u32(c);
     if ((threadIdx.x & 63u) == 0) s_w[threadIdx.x >> 6] = c;
@@ -1285,7 +1302,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, 
 }
 
 // offs: exclusive prefix of counts; each selected i goes to out[offs[b] + its rank in the tile]
-__global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, const uint32_t* __restrict__ owner,
+__global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, const uint32_t* __restrict__ ref,
                                                           SidRef sr, const uint32_t* __restrict__ offs,
                                                           uint32_t* __restrict__ out)
 {
@@ -1297,7 +1314,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, 
     uint32_t run = offs[blockIdx.x];
     for (int r = 0; r < kCompactItems; ++r) {       // rounds of 256 consecutive items, in order
         const uint64_t i = base + (uint64_t)r * kBlock + threadIdx.x;
-        const bool sel = i < n && compact_pred(mode, i, owner, sid);
+        const bool sel = i < n && compact_pred(mode, i, ref, sid);
         const uint64_t b = __ballot(sel);
         if (lane == 0) s_w[wave] = (uint32_t)__popcll(b);
         __syncthreads();
@@ -1309,11 +1326,9 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, 
     }
 }
 
-// copy on write: the j-th sharing particle takes the j-th free store, a copy of the one it
-// shared (one thread per used slot: slots >= kStoreCap stay free in every store); a particle
-// received from another rank, a copy of its record's payload (pay: the received payloads,
-// sharded filters).  A fixed grid strides over the *ndup_dev copies, so the count never
-// travels to the host.
+// a particle received from another rank gets the j-th free store, filled from its record's
+// payload (the migrated store; pay: the received payloads), one thread per usable slot.  A
+// fixed grid strides over the *ndup_dev received particles (the count stays on the device).
 __global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
                                                        const uint32_t* __restrict__ ndup_dev, SidRef sr,
                                                        MapStore ms, const StorePayload* __restrict__ pay)
@@ -1323,29 +1338,20 @@ __global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restric
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (uint64_t)gridDim.x * kBlock) {
         const uint64_t j = t / kStoreCap;
         const uint32_t slot = (uint32_t)(t - j * kStoreCap);
-        const uint32_t p = dups[j], from = sid[p], to = frees[j];
-        if (from & kSidRecord) {
-            const StorePayload& q = pay[from & ~kSidRecord];
-            ms.key[(uint64_t)to * kStoreSlots + slot] = q.key[slot];
-            ms.val[(uint64_t)to * kStoreSlots + slot] = q.val[slot];
-            if (slot == 0) ms.count[to] = q.count;
-            continue;
-        }
-        ms.key[(uint64_t)to * kStoreSlots + slot] = ms.key[(uint64_t)from * kStoreSlots + slot];
-        ms.val[(uint64_t)to * kStoreSlots + slot] = ms.val[(uint64_t)from * kStoreSlots + slot];
-        if (slot == 0) ms.count[to] = ms.count[from];
+        const uint32_t to = frees[j];
+        const StorePayload& q = pay[sid[dups[j]] & ~kSidRecord];
+        ms.key[(uint64_t)to * kStoreSlots + slot] = q.key[slot];
+        ms.val[(uint64_t)to * kStoreSlots + slot] = q.val[slot];
+        if (slot == 0) ms.count[to] = q.count;
     }
 }
 
-// the sharing particles name their copies; the copies are counted for the next map update's
-// statistics (acc: the merge counter slots' copy accumulator)
+// the received particles name their stores
 __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                         const uint32_t* __restrict__ ndup_dev, SidRef sr,
-                                                         uint64_t* __restrict__ acc)
+                                                         const uint32_t* __restrict__ ndup_dev, SidRef sr)
 {
     uint32_t* sid = cur_sid(sr);
     const uint64_t ndup = *ndup_dev;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *acc += ndup;     // one thread; the kernels of a stream run in order
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < ndup; j += (uint64_t)gridDim.x * kBlock)
         sid[dups[j]] = frees[j];
 }
@@ -1356,175 +1362,186 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 // shared grid's cells stay as they are; a cell it leaves empty gets the patch (the
 // insert-into-empty-cell rule of test/testMap.cpp:307-316) or, holding one already, fuses
 // with it when within 3 sigma (the MLS variance-weighted update; envire's merge is not in the
-// reference: parity unpinned).  A full store keeps its patches.
-// One wave merges the scan into the stores of its 64 particles.  The stores are staged in
-// LDS, transposed (slot-major, a padded row per slot: lane p's probes of any slots are
-// conflict-free), loaded and written back as whole contiguous stores (two 128-B key blocks /
-// two 256-B value blocks per wave instruction), so the 48-patch probe loop never touches
-// global memory for them; a thread-per-store loop over global memory thrashed L2 (each
-// in-flight lane keeps a 384-B store hot).
-constexpr int kMergeBlock = 128;                 // 2 waves: 37 KB of LDS, 4 blocks per CU
-constexpr int kMergePad = 65;
+// reference: parity unpinned).  A full store keeps its patches (the patch is counted dropped).
+// One thread per particle.  The store's keys live in 24 VGPRs: a patch that misses a full
+// store (the steady state: the scan keeps landing on new cells) costs 24 compares, and the
+// shared grid's test is one bit of MapView::occ.  The values are staged in LDS (transposed:
+// slot-major, lane-minor) at the particle's first change and shifted / fused there; a changed
+// map is written back whole at the end -- in place when no other particle names the store
+// (ref 1), else to the particle's reserved free store frees[i], which it then names.
+constexpr int kMergeBlock = 128;                 // 24 KB of LDS: 6 blocks (12 waves) per CU
+constexpr uint32_t kMergeGroup = 8;              // patches whose cells and occupancy words load together
+static_assert(kStoreCap == 24, "k_map_merge's membership min-tree covers 24 keys");
 __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
                                                            MapStore ms, MergeParams mp)
 {
-    // only the kStoreCap slots that can be used are staged (the rest stay free in memory)
-    __shared__ uint32_t s_key[kMergeBlock / 64][kStoreCap][kMergePad];
-    __shared__ float2 s_val[kMergeBlock / 64][kStoreCap][kMergePad];
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t i0 = (uint64_t)blockIdx.x * kMergeBlock + (uint64_t)w * 64u;
-    if (i0 >= mp.n) return;                       // wave-uniform
-    const uint64_t i = i0 + lane;
-    const bool valid = i < mp.n;
+    __shared__ float2 s_val[kStoreCap][kMergeBlock];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kMergeBlock + tid;
     const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
-    const uint32_t sid = valid ? st.sid[i] : 0u;
-    // stage: two particles per wave instruction (lanes 0-31: particle 2q, 32-63: 2q + 1)
-    const uint32_t slot = lane & 31u, half = lane >> 5;
-    // all 64 stores' loads in flight at once (96 VGPRs: LDS caps the kernel at 6 waves per CU,
-    // so a wave may hold up to 256)
-    for (uint32_t q0 = 0; q0 < 32; q0 += 32) {
-        uint32_t kv[32];
-        float2 vv[32];
+    bool dirty = false, moved = false;
+    uint32_t dropped = 0;
+    if (i < mp.n) {
+        const uint32_t sid = st.sid[i];
+        uint32_t key[kStoreCap];
+        {
+            const uint4* kp = reinterpret_cast<const uint4*>(ms.key + (uint64_t)sid * kStoreSlots);
 #pragma unroll
-        for (uint32_t q = 0; q < 32; ++q) {
-            const uint32_t pp = 2u * (q0 + q) + half;
-            const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
-            kv[q] = 0u;
-            vv[q] = make_float2(0.0f, 0.0f);
-            if (i0 + pp < mp.n) {
-                kv[q] = ms.key[(uint64_t)sp_ * kStoreSlots + slot];
-                vv[q] = ms.val[(uint64_t)sp_ * kStoreSlots + slot];
+            for (uint32_t q = 0; q < kStoreCap / 4; ++q) {
+                const uint4 v = kp[q];
+                key[4 * q] = v.x; key[4 * q + 1] = v.y; key[4 * q + 2] = v.z; key[4 * q + 3] = v.w;
             }
         }
-#pragma unroll
-        for (uint32_t q = 0; q < 32; ++q) {
-            const uint32_t pp = 2u * (q0 + q) + half;
-            if (slot < kStoreCap) {
-                s_key[w][slot][pp] = kv[q];
-                s_val[w][slot][pp] = vv[q];
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    bool dirty = false;                  // a patch inserted or fused: the store is written back
-    uint32_t dropped = 0;                // patches a full store could not take
-    if (valid) {
-        const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
         uint32_t count = ms.count[sid];
-        const uint32_t count0 = count;
+        const float2* sv = ms.val + (uint64_t)sid * kStoreSlots;
+        const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
         double sn, co;
         dm_sincos(th, &sn, &co);
         const double zvar = zs * zs;
-        // patches in groups of 24: the group's cells and their shared-grid ranges are loaded
-        // first (one memory latency per group, not per patch), then merged in patch order
-        constexpr uint32_t kGroup = 24;
-        for (uint32_t k0 = 0; k0 < mp.m; k0 += kGroup) {
-            uint32_t cellq[kGroup];
-            uint2 rng[kGroup];
+        const double bx = x - map.offset_x, by = y - map.offset_y;
+        const bool placed = dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(th);
+        // the first change: the values to LDS
+        auto take = [&]() {
+            if (dirty) return;
+            const uint4* from = reinterpret_cast<const uint4*>(sv);
+#pragma unroll 1
+            for (uint32_t h = 0; h < 3; ++h) {       // 4 loads at a time (VGPR pressure)
+                uint4 tmp[4];
 #pragma unroll
-            for (uint32_t q = 0; q < kGroup; ++q) {
-                cellq[q] = 0xffffffffu;
-                rng[q] = make_uint2(0u, 1u);
-                const uint32_t k = k0 + q;
-                if (k >= mp.m) continue;
-                const ScanPatch sp = mp.sp[k];
-                const double wx = (co * sp.x + (-sn) * sp.y) + x;
-                const double wy = (sn * sp.x + co * sp.y) + y;
-                const double wz = sp.z + z;
-                double lx = wx, ly = wy;
-                if (!map.g2l_identity) {
-                    const double* A = map.g2l;
-                    lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-                    ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                for (uint32_t q = 0; q < 4; ++q) tmp[q] = from[4 * h + q];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t t = 2 * (4 * h + q);
+                    s_val[t][tid] = make_float2(__uint_as_float(tmp[q].x), __uint_as_float(tmp[q].y));
+                    s_val[t + 1][tid] = make_float2(__uint_as_float(tmp[q].z), __uint_as_float(tmp[q].w));
                 }
-                const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
-                const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
-                if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
-                const uint32_t cell = (uint32_t)fn * map.width + (uint32_t)fm;
-                cellq[q] = cell;
-                rng[q] = make_uint2(map.cell_start[cell], map.cell_start[cell + 1]);
             }
+            dirty = true;
+        };
+        for (uint32_t k0 = 0; k0 < mp.m; k0 += kMergeGroup) {
+            uint32_t cellq[kMergeGroup], occw[kMergeGroup];
 #pragma unroll
-            for (uint32_t q = 0; q < kGroup; ++q) {
-                const uint32_t cell = cellq[q];
-                if (cell == 0xffffffffu || rng[q].x != rng[q].y) continue;   // off the grid / the shared grid has it
+            for (uint32_t q = 0; q < kMergeGroup; ++q) {
+                cellq[q] = 0xffffffffu;
+                occw[q] = 0xffffffffu;
+                const uint32_t k = k0 + q;
+                if (k >= mp.m) continue;         // uniform
+                const ScanPatch sp = mp.sp[k];
+                uint32_t cell;
+                if (map.g2l_identity) {
+                    cell = dm_merge_cell(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
+                                         map.height_cells);
+                    cell = placed ? cell : 0xffffffffu;
+                } else {
+                    const double wx = (co * sp.x + (-sn) * sp.y) + x;
+                    const double wy = (sn * sp.x + co * sp.y) + y;
+                    const double wz = sp.z + z;
+                    const double* A = map.g2l;
+                    const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+                    const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                    const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+                    const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+                    const bool in = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
+                    cell = in ? (uint32_t)fn * map.width + (uint32_t)fm : 0xffffffffu;
+                }
+                cellq[q] = cell;
+                occw[q] = map.occ[(cell == 0xffffffffu ? 0u : cell) >> 5];    // branch-free: always in range
+            }
+            uint32_t open = 0;               // bit q: patch k0 + q lands on a cell the shared grid leaves empty
+#pragma unroll
+            for (uint32_t q = 0; q < kMergeGroup; ++q)
+                open |= (cellq[q] != 0xffffffffu && !((occw[q] >> (cellq[q] & 31u)) & 1u)) ? (1u << q) : 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < kMergeGroup; ++q) {
+                if (!((open >> q) & 1u)) continue;
+                const uint32_t target = cellq[q] + 1u;
+                // membership as a min-tree of key ^ target (independent VALU ops; a compare
+                // chain through the scalar mask serialises on the VALU -> SALU latency)
+                uint32_t d[kStoreCap / 3];
+#pragma unroll
+                for (uint32_t t = 0; t < kStoreCap / 3; ++t)
+                    d[t] = min(min(key[3 * t] ^ target, key[3 * t + 1] ^ target), key[3 * t + 2] ^ target);
+                const uint32_t d0 = min(min(d[0], d[1]), d[2]), d1 = min(min(d[3], d[4]), d[5]);
+                const bool hit = min(min(d0, d1), min(d[6], d[7])) == 0u;
+                if (!hit && count >= kStoreCap) { ++dropped; continue; }
                 const ScanPatch sp = mp.sp[k0 + q];
                 const double wz = sp.z + z;
                 const double var = sp.stdev * sp.stdev + zvar;
-                const uint32_t target = cell + 1u;
-                uint32_t pos = 0;                      // lower bound in the sorted keys
+                uint32_t pos = 0;                      // lower bound of target in the sorted keys
 #pragma unroll
-                for (uint32_t step = kStoreSlots / 2; step; step >>= 1) {
-                    const uint32_t r = pos + step - 1;                // slots >= kStoreCap are free
-                    pos += (r < kStoreCap ? s_key[w][r < kStoreCap ? r : 0][lane] : kStoreFree) < target ? step : 0u;
-                }
-                if (pos < kStoreCap && s_key[w][pos][lane] == target) {
-                    const float2 pv = s_val[w][pos][lane];
+                for (uint32_t t = 0; t < kStoreCap; ++t) pos += key[t] < target ? 1u : 0u;
+                if (hit) {
+                    const float2 pv = dirty ? s_val[pos][tid] : sv[pos];
                     const double m1 = (double)pv.x, s1 = (double)pv.y;
                     const double v1 = s1 * s1, d = wz - m1;
                     if (d * d <= 9.0 * (v1 + var)) {
                         const double m = (m1 * var + wz * v1) / (v1 + var);
                         const double v = (v1 * var) / (v1 + var);
-                        s_val[w][pos][lane] = make_float2((float)m, (float)dm_sqrt(v));
-                        dirty = true;
+                        take();
+                        s_val[pos][tid] = make_float2((float)m, (float)dm_sqrt(v));
                     }
-                } else if (count < kStoreCap) {
-                    // insert at pos: shift the larger keys up one slot (count < kStoreCap < kStoreSlots)
-                    for (uint32_t t = count; t > pos; --t) {
-                        s_key[w][t][lane] = s_key[w][t - 1][lane];
-                        s_val[w][t][lane] = s_val[w][t - 1][lane];
-                    }
-                    s_key[w][pos][lane] = target;
-                    s_val[w][pos][lane] = make_float2((float)wz, (float)dm_sqrt(var));
-                    ++count;
-                    dirty = true;
                 } else {
-                    ++dropped;
+                    take();
+                    // insert at pos (count < kStoreCap): slots [pos, count) move up one (a loop
+                    // over LDS measured faster than three 8-slot chunks read whole, 0.86 vs 0.96 ms)
+                    for (uint32_t t = count; t > pos; --t) s_val[t][tid] = s_val[t - 1][tid];
+                    s_val[pos][tid] = make_float2((float)wz, (float)dm_sqrt(var));
+#pragma unroll
+                    for (uint32_t t = kStoreCap - 1; t >= 1; --t)
+                        key[t] = t > pos ? key[t - 1] : (t == pos ? target : key[t]);
+                    key[0] = pos == 0 ? target : key[0];
+                    ++count;
                 }
             }
         }
-        if (count != count0) ms.count[sid] = count;
+        if (dirty) {
+            uint32_t dst = sid;
+            if (mp.ref[sid] > 1u) {              // another particle names the store: a free one
+                dst = mp.frees[i];
+                st.sid[i] = dst;
+                moved = true;
+            }
+            uint4* kp = reinterpret_cast<uint4*>(ms.key + (uint64_t)dst * kStoreSlots);
+#pragma unroll
+            for (uint32_t q = 0; q < kStoreCap / 4; ++q)
+                kp[q] = make_uint4(key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]);
+            uint4* vp = reinterpret_cast<uint4*>(ms.val + (uint64_t)dst * kStoreSlots);
+#pragma unroll
+            for (uint32_t q = 0; q < kStoreCap / 2; ++q) {
+                const float2 a = s_val[2 * q][tid], b = s_val[2 * q + 1][tid];
+                vp[q] = make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y));
+            }
+            ms.count[dst] = count;
+        }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     dropped = wave_sum_u32(dropped);
-    // write back the changed stores (written whole, like the staging); once the stores are
-    // full and the scan repeats, most merges change nothing
-    const uint64_t dmask = __ballot(dirty);
-    if (lane == 0) {                     // one address per block slot: no single hot atomic
-        const uint32_t slot_c = blockIdx.x % kMergeCounterSlots;
+    const uint64_t dmask = __ballot(dirty), mmask = __ballot(moved);
+    if (lane == 0) {                     // one address per counter slot: no single hot atomic
+        const uint32_t slot_c = (uint32_t)((blockIdx.x * (kMergeBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
         if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
-    }
-    if (dmask == 0ull) return;
-#pragma unroll 4
-    for (uint32_t q = 0; q < 32; ++q) {
-        const uint32_t pp = 2u * q + half;
-        const uint32_t sp_ = (uint32_t)__shfl((int)sid, (int)pp, 64);
-        if (((dmask >> pp) & 1ull) && slot < kStoreCap) {
-            ms.key[(uint64_t)sp_ * kStoreSlots + slot] = s_key[w][slot][pp];
-            ms.val[(uint64_t)sp_ * kStoreSlots + slot] = s_val[w][slot][pp];
-        }
+        if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
     }
 }
 
 // the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads)
 __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl)
 {
-    __shared__ uint64_t s[2][kMergeCounterSlots / 64];
+    __shared__ uint64_t s[3][kMergeCounterSlots / 64];
     const uint32_t t = threadIdx.x;
-    const uint64_t d = wave_sum_u64(cnt[t]), c = wave_sum_u64(cnt[kMergeCounterSlots + t]);
-    if ((t & 63u) == 0) { s[0][t >> 6] = d; s[1][t >> 6] = c; }
+#pragma unroll
+    for (uint32_t g = 0; g < 3; ++g) {
+        const uint64_t v = wave_sum_u64(cnt[g * kMergeCounterSlots + t]);
+        if ((t & 63u) == 0) s[g][t >> 6] = v;
+    }
     __syncthreads();
     if (t == 0) {
-        uint64_t sd = 0, sc = 0;
-        for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) { sd += s[0][w]; sc += s[1][w]; }
-        ctl->map_dropped = sd;
-        ctl->map_changed = sc;
-        ctl->map_copied = cnt[2 * kMergeCounterSlots];        // the copy-on-write copies since the last merge
+        uint64_t r[3] = {0, 0, 0};
+        for (uint32_t g = 0; g < 3; ++g)
+            for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) r[g] += s[g][w];
+        ctl->map_dropped = r[0];
+        ctl->map_changed = r[1];
+        ctl->map_copied = r[2];
     }
 }
 
@@ -2021,11 +2038,17 @@ constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * wave_d
 // (at least 576)
 template <int ITEMS> constexpr int wave_draws() { return 64 * ITEMS + 64 > 576 ? 64 * ITEMS + 64 : 576; }
 
+// the LDS slot of a wave's draw x, one pad slot per 8: a lane's window reads sit near draw
+// 8 l + const (one target per particle, ITEMS = 8 particles per lane), and unpadded that stride
+// of 8 doubles put lanes l and l + 4 on one bank (8-way within each 32-lane ds_read_b64 group);
+// padded, the lanes' 8-byte reads cover the 64 banks once
+__device__ __forceinline__ uint32_t draw_slot(uint32_t x) { return x + (x >> 3); }
+
 // K3's LDS: the staged weights, then the wave's draws (the weights are dead before the
 // draws are written)
 template <int ITEMS> union K3Lds {
     double v[kBlock * ITEMS + kBlock * ITEMS / kSkew];
-    uint64_t T[kWaves][wave_draws<ITEMS>()];
+    uint64_t T[kWaves][wave_draws<ITEMS>() + wave_draws<ITEMS>() / 8];
 };
 
 // Write the marks of the tile's segment starts (relative to the slice) and the row carries
@@ -2202,7 +2225,7 @@ __device__ __forceinline__ uint32_t draws_le_chunk(uint32_t w, uint64_t c, const
     for (int d = 0; d < 3; ++d) {
         const uint32_t r = r0 + (uint32_t)d;
         const bool in = ((uint32_t)d < nd) & (r >= rq0) & (r < rq1);
-        const uint64_t t = sT[in ? r - rq0 : 0u];           // slot 0 is in LDS; used only when in
+        const uint64_t t = sT[draw_slot(in ? r - rq0 : 0u)];    // slot 0 is in LDS; used only when in
         w |= (in && t <= c) ? 1u << (19 + d) : 0u;
     }
     return w;
@@ -2363,7 +2386,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
                 uint32_t x = dm_mulmod31(dm_mulmod31(jump_pow(jt, q0 + 1), xs), a_lane);
 #pragma unroll 4
                 for (uint64_t k = q0 + lane; k < q1; k += 64) {
-                    sT[k - q0] = draw_fx(k, x, dN, inv_N, shift);
+                    sT[draw_slot((uint32_t)(k - q0))] = draw_fx(k, x, dN, inv_N, shift);
                     x = dm_mulmod31(x, a64);
                 }
             }
@@ -2892,71 +2915,63 @@ extern "C" hipError_t eslam_launch_scan_excl(uint32_t* a, uint64_t m, hipStream_
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, hipStream_t stream)
+extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, uint64_t pool, hipStream_t stream)
 {
-    if (n) hipLaunchKernelGGL(k_store_init, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, *ms, n);
+    if (pool) hipLaunchKernelGGL(k_store_init, dim3((uint32_t)((pool + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, *ms, n, pool);
     return hipGetLastError();
 }
 
-// copy on write of the map stores (before a merge): owner, the free-store and the sharing-
-// particle lists (compactions), the copies, the renames.  scratch: owner (n) + counts and
-// offsets (2 x tiles) + frees (n) + dups (n) words.  *ndup_dev: the number of copies (device).
-extern "C" hipError_t eslam_launch_store_cow(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch, uint32_t* ndup_dev,
-                                             hipStream_t stream)
+// one compaction (k_compact_count, the exclusive prefix over tiles + 1 entries -- entry tiles
+// becomes the total, copied to *total -- and k_compact_write) of the items [0, items)
+static hipError_t compact(int mode, uint64_t items, const uint32_t* ref, SidRef sid, uint32_t* counts, uint32_t* out,
+                          uint32_t* total, hipStream_t stream)
 {
-    if (!n) return hipSuccess;
-    const uint32_t tiles = (uint32_t)((n + kCompactTile - 1) / kCompactTile);
-    uint32_t* owner = scratch;
-    uint32_t* counts = owner + n;
-    uint32_t* frees = counts + 2ull * tiles + 2;
-    uint32_t* dups = frees + n;
-    const uint32_t nb = (uint32_t)((n + kBlock - 1) / kBlock);
-    hipError_t e = hipMemsetAsync(owner, 0xff, n * 4, stream);
+    const uint32_t tiles = (uint32_t)((items + kCompactTile - 1) / kCompactTile);
+    hipError_t e = hipMemsetAsync(counts + tiles, 0, 4, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_store_owner, dim3(nb), dim3(kBlock), 0, stream, sid, n, owner);
-    for (int mode = 0; mode < 2; ++mode) {
-        uint32_t* c = counts + (uint64_t)mode * (tiles + 1);
-        hipLaunchKernelGGL(k_compact_count, dim3(tiles), dim3(kBlock), 0, stream, mode, n, owner, sid, c);
-        // exclusive prefix over tiles + 1 entries: entry tiles becomes the total
-        e = hipMemsetAsync(c + tiles, 0, 4, stream);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, stream, c, (uint64_t)tiles + 1);
-        hipLaunchKernelGGL(k_compact_write, dim3(tiles), dim3(kBlock), 0, stream, mode, n, owner, sid, c, mode == 0 ? frees : dups);
-    }
-    e = hipMemcpyAsync(ndup_dev, counts + (tiles + 1) + tiles, 4, hipMemcpyDeviceToDevice, stream);
+    if (tiles) hipLaunchKernelGGL(k_compact_count, dim3(tiles), dim3(kBlock), 0, stream, mode, items, ref, sid, counts);
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, stream, counts, (uint64_t)tiles + 1);
+    if (tiles) hipLaunchKernelGGL(k_compact_write, dim3(tiles), dim3(kBlock), 0, stream, mode, items, ref, sid, counts, out);
+    return hipMemcpyAsync(total, counts + tiles, 4, hipMemcpyDeviceToDevice, stream);
+}
+
+// the stores' reference counts and the free-store list of the pool (before a map merge or a
+// copy on write): cs.ref, cs.frees, *cs.nfree
+extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(cs->ref, 0, pool * 4, stream);
+    if (e != hipSuccess) return e;
+    if (n) hipLaunchKernelGGL(k_store_ref, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, n, cs->ref);
+    e = compact(0, pool, cs->ref, sid, cs->counts, cs->frees, cs->nfree, stream);
     return e != hipSuccess ? e : hipGetLastError();
 }
 
-// the copies and renames for the sharing particles, their count read on the device (ndup_dev,
-// written by eslam_launch_store_cow); copies_acc: where the copies are counted
-extern "C" hipError_t eslam_launch_store_copy(SidRef sid, const MapStore* ms, uint64_t n, uint32_t* scratch,
-                                              const uint32_t* ndup_dev, const void* payloads, uint64_t* copies_acc,
-                                              hipStream_t stream)
+// the particles a sharded resample received (cs.dups, *cs.ndup) take the first free stores,
+// filled from their records' payloads (needs eslam_launch_store_refs first)
+extern "C" hipError_t eslam_launch_store_receive(SidRef sid, const MapStore* ms, uint64_t n, const CowScratch* cs,
+                                                 const void* payloads, hipStream_t stream)
 {
     if (!n) return hipSuccess;
-    const uint32_t tiles = (uint32_t)((n + kCompactTile - 1) / kCompactTile);
-    uint32_t* frees = scratch + n + 2ull * tiles + 2;
-    uint32_t* dups = frees + n;
-    // grids for the worst case (every particle a copy), capped: the loops stride
+    hipError_t e = compact(1, n, cs->ref, sid, cs->counts + cs->tiles + 1, cs->dups, cs->ndup, stream);
+    if (e != hipSuccess) return e;
+    // grids for the worst case (every particle received), capped: the loops stride
     const uint64_t want_c = (n * kStoreCap + kBlock - 1) / kBlock, want_r = (n + kBlock - 1) / kBlock;
     const uint32_t gc = (uint32_t)(want_c < 8192 ? want_c : 8192), gr = (uint32_t)(want_r < 2048 ? want_r : 2048);
-    hipLaunchKernelGGL(k_store_copy, dim3(gc), dim3(kBlock), 0, stream, dups, frees, ndup_dev, sid, *ms,
+    hipLaunchKernelGGL(k_store_copy, dim3(gc), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid, *ms,
                        (const StorePayload*)payloads);
-    hipLaunchKernelGGL(k_store_rename, dim3(gr), dim3(kBlock), 0, stream, dups, frees, ndup_dev, sid, copies_acc);
+    hipLaunchKernelGGL(k_store_rename, dim3(gr), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid);
     return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(mp->cnt, 0, 2 * kMergeCounterSlots * sizeof(uint64_t), stream);
+    hipError_t e = hipMemsetAsync(mp->cnt, 0, 3 * kMergeCounterSlots * sizeof(uint64_t), stream);
     if (e != hipSuccess) return e;
     if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kMergeBlock - 1) / kMergeBlock)), dim3(kMergeBlock), 0,
                                   stream, s0, s1, ctl, *map, *ms, *mp);
     hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
-    // the copy accumulator starts over for the next map update
-    e = hipMemsetAsync(mp->cnt + 2 * kMergeCounterSlots, 0, sizeof(uint64_t), stream);
-    return e != hipSuccess ? e : hipGetLastError();
+    return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
@@ -3152,7 +3167,7 @@ extern "C" hipError_t eslam_launch_centroid(DevState s0, DevState s1, uint64_t n
     return e;
 }
 
-// blocks per CU of the main K1 instantiation (diagnostics: tools/k1_timeline.py)
+// blocks per CU of the main K1 instantiation (diagnostics)
 extern "C" int eslam_debug_k1_occupancy(int* blocks_per_cu, int lds)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_project_weight<true, true, 4, true>, kBlock,

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of library builds on one GPU box, with one SQ instruction-count pass per
 # library:  bash tools/ab_libs.sh <tag> <reps> "<particle counts>" lib1.so lib2.so ...
+# (PMC="<counters>" replaces the SQ instruction counters; BENCH_ARGS adds bench.py flags)
 # Output: gpurun_out/<tag>/ab.log (value, ms/step, kernel ms per run) and pmc_<lib>.csv.
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -19,7 +20,7 @@ for n in $sizes; do
 done
 for lib in "$@"; do
   b=$(basename $lib .so)
-  ESLAM_GPU_LIB=$PWD/$lib timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU \
+  ESLAM_GPU_LIB=$PWD/$lib timeout -s KILL 90 rocprofv3 --pmc ${PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU} \
     --output-format csv -d $out/pmc_$b -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline $BENCH_ARGS > $out/pmc_$b.log 2>&1 || { echo "pmc $b failed"; exit 1; }
 done
 python3 - "$out" <<'PY'
