@@ -56,7 +56,7 @@ extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64
                                                 hipStream_t stream);
 extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, const FinParams* fp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* tile_sum,
-                                                  uint64_t* total, hipStream_t stream);
+                                                  uint64_t* total, const FusedFin* ff, hipStream_t stream);
 extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl,
                                                       uint64_t* tile_pub, uint32_t* marks, uint32_t* tile_first,
                                                       const uint32_t* jt, const FusedFin* ff, hipStream_t stream);
@@ -65,6 +65,7 @@ extern "C" hipError_t eslam_launch_resample_gather(DevState s0, DevState s1, uin
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
                                                   const uint64_t* tile_prefix, uint32_t* marks, uint32_t* tile_first,
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
+                                                  uint64_t* host_out, uint64_t* host_epoch, uint64_t epoch,
                                                   hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
                                         const uint64_t* first_last, uint64_t nsend, void* send, const MapStore* ms,
@@ -290,7 +291,8 @@ struct eslam_ctx {
     Shard* recs = nullptr;                  // gathered records of all ranks
     uint64_t* mg = nullptr;                 // MgBlock (device)
     void* rccl = nullptr;                   // ncclComm_t of eslam_gpu_set_comm_rccl (owned)
-    uint64_t* mg_host = nullptr;            // pinned
+    uint64_t* mg_host = nullptr;            // pinned, host-mapped (k_segments_multi writes the totals there)
+    uint64_t seg_epoch = 0;                 // the last k_segments_multi launch's epoch (mg_host[kHostEpoch])
     uint2* range = nullptr;                 // per particle: [lo, hi) of its global outputs
     void* sendbuf = nullptr; uint64_t send_cap = 0;
     void* recvbuf = nullptr; uint64_t recv_cap = 0;
@@ -354,7 +356,8 @@ constexpr int kBest = kFirstLast + 2 * kMaxRanks;           // [2] local best (k
 constexpr int kBestAll = kBest + 2;                         // [2 kMaxRanks]
 constexpr int kMaxW = kBestAll + 2 * kMaxRanks;             // local max weight (bits)
 constexpr int kMaxWAll = kMaxW + 1;                         // [kMaxRanks]
-constexpr int kWords = kMaxWAll + kMaxRanks;
+constexpr int kHostEpoch = kMaxWAll + kMaxRanks;           // (mg_host only) the segments kernel's epoch
+constexpr int kWords = kHostEpoch + 1;
 }  // namespace mg
 
 // timing mode: event k (0..4) of the current step, kept in a ring so a whole timed region
@@ -1599,42 +1602,47 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
     FinParams fp = fin_params(ctx, mode);
     fp.local_shards = ctx->shards;
     fp.mirror = ctx->mg + mg::kMirror;
-    HIPCHK(ctx, eslam_launch_finalize(ctx->recs, G * kNShard, ctx->ctl, &fp, ctx->stream));
+    // an update step folds the finalize (over every rank's shards) into K3a's block 0
+    const bool fused = mode == FIN_UPDATE;
+    if (!fused) HIPCHK(ctx, eslam_launch_finalize(ctx->recs, G * kNShard, ctx->ctl, &fp, ctx->stream));
     if (timed) rec(ctx, 2);
     if (mode == FIN_SUM) return ESLAM_OK;
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, true);
     sp.multi = 1;
     sp.tag = ctx->scan_tag = ctx->scan_tag % 7u + 1u;         // differs from the previous launch's
+    const FusedFin ff{ctx->recs, fp, ctx->fin_word, ++ctx->fin_epoch, G * kNShard};
     HIPCHK(ctx, eslam_launch_normalize_scan(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->mg + mg::kTotal,
-                                            ctx->stream));
+                                            fused ? &ff : nullptr, ctx->stream));
     rc = comm_allgather(ctx, ctx->mg + mg::kTotal, ctx->mg + mg::kTotals, 8);
     if (rc) return rc;
     uint64_t* h = ctx->mg_host;
-    // the gathered totals and the finalize mirror: one copy
-    HIPCHK(ctx, hipMemcpyAsync(h + mg::kTotals, ctx->mg + mg::kTotals, 8ull * (kMaxRanks + 3), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    // the gathered totals and the finalize mirror reach the host without a copy on the
+    // stream: the segments kernel's first thread writes them to the host-mapped mg_host and
+    // then the launch's epoch (system-scope release)
     PlanParams pp = plan_params(ctx);
+    const uint64_t epoch = ++ctx->seg_epoch;
     HIPCHK(ctx, eslam_launch_segments_multi(ctx->st[0], ctx->st[1], &sp, &pp, ctx->ctl, ctx->tile_sum, ctx->marks,
                                             ctx->tile_first, ctx->mg + mg::kTotals, ctx->jump, ctx->range,
-                                            ctx->mg + mg::kFirstLast, ctx->stream));
+                                            ctx->mg + mg::kFirstLast, h + mg::kTotals, h + mg::kHostEpoch, epoch,
+                                            ctx->stream));
     if (timed) rec(ctx, 3);
-    // the totals, not the segments kernel.  Spin on the event: a blocking synchronize
-    // wakes the thread tens of microseconds late, and the GPU runs dry before the next
-    // step's launches if the host is late here (the segments kernel is all it has queued)
     {
-        // bounded (kSpinBoundUs): past it (a hung collective or kernel, or a late GPU) fall
-        // back to a blocking wait instead of burning a host core next to the RCCL proxy threads
-        hipError_t q;
+        // spin on the epoch word: a blocking synchronize wakes the thread tens of microseconds
+        // late, and the GPU runs dry before the next step's launches if the host is late here
+        // (the segments kernel is all it has queued).  Bounded (kSpinBoundUs): past it (a hung
+        // collective or kernel, or a late GPU) fall back to a blocking wait instead of burning
+        // a host core next to the RCCL proxy threads.
         const auto t0 = std::chrono::steady_clock::now();
         const auto bound = std::chrono::microseconds(kSpinBoundUs);
-        while ((q = hipEventQuery(ctx->ev[0])) == hipErrorNotReady) {
+        while (__atomic_load_n(h + mg::kHostEpoch, __ATOMIC_ACQUIRE) != epoch) {
             if (std::chrono::steady_clock::now() - t0 > bound) {
-                q = hipEventSynchronize(ctx->ev[0]);
+                const hipError_t q = hipStreamSynchronize(ctx->stream);
+                if (q != hipSuccess) return abort_pending_gather(ctx, q);
                 break;
             }
         }
-        if (q != hipSuccess) return abort_pending_gather(ctx, q);
+        if (__atomic_load_n(h + mg::kHostEpoch, __ATOMIC_ACQUIRE) != epoch)
+            return abort_pending_gather(ctx, hipErrorUnknown);
     }
     // a rank whose slice-total wait gave up all-gathers ~0: every rank stops here
     for (int r = 0; r < G; ++r)
@@ -1720,7 +1728,7 @@ static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
     if (timed) rec(ctx, 2);
     ScanParams sp = scan_params(ctx, mode == FIN_UPDATE, mode == FIN_UPDATE || mode == FIN_NORMALIZE, false);
     sp.tag = ctx->scan_tag = ctx->scan_tag % 7u + 1u;         // differs from the previous launch's
-    FusedFin ff{ctx->shards, fp, ctx->fin_word, ++ctx->fin_epoch};
+    FusedFin ff{ctx->shards, fp, ctx->fin_word, ++ctx->fin_epoch, kNShard};
     HIPCHK(ctx, eslam_launch_normalize_segments(ctx->st[0], ctx->st[1], &sp, ctx->ctl, ctx->tile_sum, ctx->marks,
                                                 ctx->tile_first, ctx->jump, fused ? &ff : nullptr, ctx->stream));
     if (timed) rec(ctx, 3);

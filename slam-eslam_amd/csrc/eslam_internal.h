@@ -287,10 +287,11 @@ struct FinParams {
 // the finalize fused into the one-GPU K3 (k_normalize_segments<ITEMS, true>): block 0 runs
 // k_finalize's block over the local shards and publishes epoch in *fin_word
 struct FusedFin {
-    Shard* shards;
+    Shard* shards;                       // the statistics shards (all ranks' on a sharded filter)
     FinParams fp;
     uint64_t* fin_word;
     uint64_t epoch;
+    int nrec;                            // shards to reduce (kNShard, or kNShard x ranks)
 };
 
 

@@ -1820,39 +1820,6 @@ __device__ __forceinline__ uint64_t count_draws_le(uint64_t c, uint64_t N, uint3
     return cnt;
 }
 
-// Walks the stratified draws in order: k = number of draws <= the last target, x = minstd
-// state of draw k.  Consecutive targets of one thread are close, so stepping draw by draw
-// replaces a jump-ahead per particle; far targets (heavy particles) jump.
-struct DrawCursor {
-    uint64_t k, N;
-    uint32_t x, xs;
-    int shift;
-    double dN, inv_N;
-    const uint32_t* jt;
-    uint64_t T;                          // T_k of the current draw (valid when k < N)
-
-    __device__ __forceinline__ uint64_t draw_T() const { return draw_fx(k, x, dN, inv_N, shift); }
-    __device__ __forceinline__ void seek(uint64_t c)
-    {
-        k = count_draws_le(c, N, xs, shift, jt);
-        x = k < N ? dm_mulmod31(jump_pow(jt, k + 1), xs) : 0u;
-        if (k < N) T = draw_T();
-    }
-    // number of draws <= c (c >= the previous target): step, or jump after 16 steps.
-    // The draw a call stops at is kept for the next call (each draw is evaluated once).
-    __device__ __forceinline__ uint64_t advance(uint64_t c)
-    {
-        for (int steps = 0; k < N; ++steps) {
-            if (steps == 16) { seek(c); break; }
-            if (T > c) break;
-            ++k;
-            x = dm_minstd_next(x);
-            if (k < N) T = draw_T();
-        }
-        return k;
-    }
-};
-
 // phase B (updateWeights' second pass, src/PoseEstimator.cpp:332-344) + normalisation
 // (src/ParticleFilter.hpp:46-70) of one tile's items r * kBlock + tid, in place; v[r] is the
 // final weight (0 past the filter's end).  Every load of the tile is issued first (indices
@@ -2139,25 +2106,65 @@ __device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ ti
 // K3's words (every launch writes every word).  The last tile waits for the others' words
 // and writes this slice's total (the value all-gathered before K3b), so no separate kernel
 // sums the tiles; K3b re-sums the words before its own tile (any order: exact integers).
-template <int ITEMS>
+template <int ITEMS, bool FUSED>
 __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
-                                                           uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total)
+                                                           uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total,
+                                                           FusedFin ff)
 {
     __shared__ uint64_t s_wtot[kWaves], s_red[kWaves];
+    __shared__ uint64_t s_img[FUSED ? kCtlWords : 1];
+    __shared__ uint32_t s_flag;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
-    if (ctl->aborted || (ctl->err & kFaultTimeout)) {   // the update threw (k_finalize), or the filter is poisoned
-        if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
-        if (total && tile + 1 == sp.ntiles && tid == 0 && (ctl->err & kFaultTimeout)) *total = ~0ull;
+    const bool last_tile = total && tile + 1 == sp.ntiles;
+    if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
+        if (tid == 0) {
+            atomic_store_agent(tile_sum + tile, tagw);
+            if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (last_tile) *total = ~0ull;
+        }
         return;
     }
-    const bool resample = ctl->resample != 0;
-    const DevState st = ctl->base ? s1 : s0;
+    if constexpr (FUSED) {
+        // the update step's finalize over every rank's statistics (block 0; the sharded
+        // counterpart of k_normalize_segments' fused finalize)
+        if (tile == 0) {
+            __shared__ FinLds s_fin;
+            finalize_block(ff.shards, ff.nrec, ctl, ff.fp, s_fin);
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    const Ctl* cv = FUSED ? reinterpret_cast<const Ctl*>(s_img) : ctl;
+    const DevState st = (FUSED ? ctl->k3_base : ctl->base) ? s1 : s0;
     const uint64_t t0 = (uint64_t)tile * (kBlock * ITEMS);
-    const int shift = ctl->scan_shift;
     double v[ITEMS];
-    phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
+    if constexpr (FUSED) {
+        double mp[ITEMS];
+        uint32_t fl[ITEMS];
+        phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
+        if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
+            if (tid == 0) {
+                atomic_store_agent(tile_sum + tile, tagw);
+                if (last_tile) *total = ~0ull;               // every rank sees the fault
+            }
+            return;
+        }
+        if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
+            if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+            return;
+        }
+        phase_b_apply<ITEMS>(st, sp, cv, t0, tid, v, mp, fl);
+    } else {
+        if (ctl->aborted) {              // the update threw (k_finalize): weights stay as phase A left them
+            if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+            return;
+        }
+        phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
+    }
+    const bool resample = sgpr_u32(cv->resample) != 0;
+    const int shift = (int)sgpr_u32((uint32_t)cv->scan_shift);
     uint64_t fx_sum = 0;
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) fx_sum += fx_shift(v[r], shift);   // 0 past the end
@@ -2173,7 +2180,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
 #pragma unroll
     for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
     if (tid == 0) atomic_store_agent(tile_sum + tile, tagw | (t & kPubMask));
-    if (total && tile + 1 == sp.ntiles) {
+    if (last_tile) {
         const uint64_t before = tiles_before_pub(tile_sum, tile, sp, s_red, ctl);
         if (tid == 0) *total = before == ~0ull ? ~0ull : before + t;     // ~0: every rank sees the fault
     }
@@ -2241,6 +2248,73 @@ __device__ __forceinline__ uint64_t count_from_window(uint32_t w, uint64_t dlo, 
     return k0 + lead;
 }
 
+// The counts #{k : T_k <= base + c[r]} of one wave's targets (hi_r) and, for the lane's
+// first item, the count of its predecessor (lo: lane 0 #{T_k <= base}, the others the
+// previous lane's last count).  The wave's cumulative range [wlo, whi] needs only the draws
+// in [dlo, dhi) (the windows k* - 1 .. k* + 1 of wlo and whi, clamped to [0, N)): its lanes
+// evaluate them in parallel into LDS (sT, wave_draws at a time) and every target reads the
+// (at most three) draws of its window there.  Heavy weights (more than kWaveChunks chunks of
+// draws): each target's window evaluated directly.
+template <int ITEMS>
+__device__ __forceinline__ void wave_counts(uint64_t base, uint64_t run, const uint64_t (&c)[ITEMS], uint64_t N, int shift,
+                                            uint32_t xs, const uint32_t* __restrict__ jt, uint64_t* sT,
+                                            uint64_t (&hi_r)[ITEMS], uint64_t& lo)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const double dN = (double)N, inv_N = 1.0 / dN;
+    // wave-uniform by construction: moved to SGPRs, so the window bounds, the loop and the
+    // jump-ahead table reads of the first draw are scalar (readfirstlane returns int: each
+    // half is widened as unsigned)
+    auto rfl64 = [](uint64_t v) {
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        const uint32_t lo_ = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        return ((uint64_t)hi << 32) | (uint64_t)lo_;
+    };
+    const uint64_t wlo = rfl64(__shfl(base, 0, 64)), whi = rfl64(__shfl(base + run, 63, 64));
+    const uint64_t ks_lo = kstar_of(wlo, N, shift), ks_hi = kstar_of(whi, N, shift);
+    const uint64_t dlo = ks_lo >= 1 ? ks_lo - 1 : 0;
+    const uint64_t dhi = ks_hi + 2 < N ? ks_hi + 2 : N;
+    if (dlo >= dhi || dhi - dlo <= (uint64_t)kWaveChunks * wave_draws<ITEMS>()) {
+        // le[r] bit d: draw k0_r + d of target r (r = ITEMS: wlo) is <= its target
+        uint32_t win[ITEMS + 1];
+#pragma unroll
+        for (int r = 0; r <= ITEMS; ++r) win[r] = window_of(r < ITEMS ? base + c[r] : wlo, N, shift, dlo);
+        const uint32_t a64 = jt[64], a_lane = jt[lane];            // A^64, A^lane
+        for (uint64_t q0 = dlo; q0 < dhi; q0 += wave_draws<ITEMS>()) {
+            const uint64_t q1 = dhi - q0 < (uint64_t)wave_draws<ITEMS>() ? dhi : q0 + wave_draws<ITEMS>();
+            if (q0 + lane < q1) {
+                uint32_t x = dm_mulmod31(dm_mulmod31(jump_pow(jt, q0 + 1), xs), a_lane);
+#pragma unroll 4
+                for (uint64_t k = q0 + lane; k < q1; k += 64) {
+                    sT[draw_slot((uint32_t)(k - q0))] = draw_fx(k, x, dN, inv_N, shift);
+                    x = dm_mulmod31(x, a64);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r <= ITEMS; ++r)
+                win[r] = draws_le_chunk(win[r], r < ITEMS ? base + c[r] : wlo, sT, (uint32_t)(q0 - dlo),
+                                        (uint32_t)(q1 - dlo));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) hi_r[r] = count_from_window(win[r], dlo, N);
+        const uint64_t K0 = count_from_window(win[ITEMS], dlo, N);
+        const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
+        lo = lane == 0 ? K0 : prev;
+    } else {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) hi_r[r] = count_draws_le(base + c[r], N, xs, shift, jt);
+        const uint64_t K0 = count_draws_le(wlo, N, xs, shift, jt);
+        const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
+        lo = lane == 0 ? K0 : prev;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // K3 (one GPU): phase B + normalisation, the tile's exact fixed-point total, the prefix of
 // the preceding tiles and the segment marks, in one pass.  Each tile publishes its total as
@@ -2279,7 +2353,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     if constexpr (FUSED) {
         if (tile == 0) {
             __shared__ FinLds s_fin;
-            finalize_block(ff.shards, kNShard, ctl, ff.fp, s_fin);
+            finalize_block(ff.shards, ff.nrec, ctl, ff.fp, s_fin);
             __syncthreads();
             if (tid == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2354,66 +2428,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
 
     const uint64_t N = sp.n_global;
     const uint32_t xs = sgpr_u32(cv->minstd_start);
-    const double dN = (double)N, inv_N = 1.0 / dN;
     const uint64_t i0 = t0 + (uint64_t)tid * ITEMS;
-    // the wave's cumulative range [wlo, whi]: every count it needs reads only draws in
-    // [dlo, dhi) (the windows k* - 1 .. k* + 1 of wlo and whi, clamped to [0, N))
-    // wave-uniform by construction: moved to SGPRs, so the window bounds, the loop and the
-    // jump-ahead table reads of the first draw are scalar (readfirstlane returns int: each
-    // half is widened as unsigned)
-    auto rfl64 = [](uint64_t v) {
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-        return ((uint64_t)hi << 32) | (uint64_t)lo;
-    };
-    const uint64_t wlo = rfl64(__shfl(base, 0, 64)), whi = rfl64(__shfl(base + run, 63, 64));
-    const uint64_t ks_lo = kstar_of(wlo, N, shift), ks_hi = kstar_of(whi, N, shift);
-    const uint64_t dlo = ks_lo >= 1 ? ks_lo - 1 : 0;
-    const uint64_t dhi = ks_hi + 2 < N ? ks_hi + 2 : N;
     uint64_t hi_r[ITEMS];
     uint64_t lo;
-    if (dlo >= dhi || dhi - dlo <= (uint64_t)kWaveChunks * wave_draws<ITEMS>()) {
-        // draws in LDS, wave_draws at a time (one chunk unless the wave holds heavy weights);
-        // le[r] bit d: draw k0_r + d of target r (r = ITEMS: wlo) is <= its target
-        uint64_t* sT = s_u.T[wave];
-        uint32_t win[ITEMS + 1];
-#pragma unroll
-        for (int r = 0; r <= ITEMS; ++r) win[r] = window_of(r < ITEMS ? base + c[r] : wlo, N, shift, dlo);
-        const uint32_t a64 = jt[64], a_lane = jt[lane];            // A^64, A^lane
-        for (uint64_t q0 = dlo; q0 < dhi; q0 += wave_draws<ITEMS>()) {
-            const uint64_t q1 = dhi - q0 < (uint64_t)wave_draws<ITEMS>() ? dhi : q0 + wave_draws<ITEMS>();
-            if (q0 + lane < q1) {
-                uint32_t x = dm_mulmod31(dm_mulmod31(jump_pow(jt, q0 + 1), xs), a_lane);
-#pragma unroll 4
-                for (uint64_t k = q0 + lane; k < q1; k += 64) {
-                    sT[draw_slot((uint32_t)(k - q0))] = draw_fx(k, x, dN, inv_N, shift);
-                    x = dm_mulmod31(x, a64);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int r = 0; r <= ITEMS; ++r)
-                win[r] = draws_le_chunk(win[r], r < ITEMS ? base + c[r] : wlo, sT, (uint32_t)(q0 - dlo),
-                                        (uint32_t)(q1 - dlo));
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) hi_r[r] = count_from_window(win[r], dlo, N);
-        const uint64_t K0 = count_from_window(win[ITEMS], dlo, N);
-        const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
-        lo = lane == 0 ? K0 : prev;
-    } else {
-        // heavy weights: each target's window evaluated directly (jump + at most three draws)
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) hi_r[r] = count_draws_le(base + c[r], N, xs, shift, jt);
-        const uint64_t K0 = count_draws_le(wlo, N, xs, shift, jt);
-        const uint64_t prev = __shfl_up(hi_r[ITEMS - 1], 1, 64);
-        lo = lane == 0 ? K0 : prev;
-    }
+    wave_counts<ITEMS>(base, run, c, N, shift, xs, jt, s_u.T[wave], hi_r, lo);
     if (i0 == 0) lo = 0;
     uint64_t seg_lo[ITEMS], seg_hi[ITEMS];
     uint32_t val[ITEMS];
@@ -2457,11 +2475,20 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
                                                            Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
                                                            uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
                                                            const uint64_t* __restrict__ totals, const uint32_t* __restrict__ jt,
-                                                           uint2* __restrict__ range, uint64_t* __restrict__ first_last)
+                                                           uint2* __restrict__ range, uint64_t* __restrict__ first_last,
+                                                           uint64_t* host_out, uint64_t* host_epoch, uint64_t epoch)
 {
     __shared__ uint64_t s_wtot[kWaves];
     __shared__ K3Lds<kScanItems> s_u;
     double* s_v = s_u.v;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the gathered totals and the finalize mirror (they follow the totals) to the host-mapped
+        // buffer, then this launch's epoch: the host plans the exchange from them while the
+        // kernel runs (no copy on the stream)
+        for (int r = 0; r < pp.nranks; ++r) host_out[r] = totals[r];
+        for (int q = 0; q < 3; ++q) host_out[kMaxRanks + q] = totals[kMaxRanks + q];
+        __hip_atomic_store(host_epoch, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (!ctl->resample) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
@@ -2484,9 +2511,10 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     const uint64_t N = pp.n_global;
     const uint64_t W0 = pp.gbase[pp.rank], W1 = pp.gbase[pp.rank + 1];
     const uint64_t i0 = t0 + (uint64_t)tid * kScanItems;
-    DrawCursor cur{0, N, 0u, ctl->minstd_start, shift, (double)N, 1.0 / (double)N, jt, 0};
-    cur.seek(base);
-    uint64_t lo = i0 == 0 ? O0 : cur.k;
+    uint64_t hi_r[kScanItems];
+    uint64_t lo;
+    wave_counts<kScanItems>(base, run, c, N, shift, ctl->minstd_start, jt, s_u.T[tid >> 6], hi_r, lo);
+    if (i0 == 0) lo = O0;
     uint64_t seg_lo[kScanItems], seg_hi[kScanItems];
     uint32_t val[kScanItems];
 #pragma unroll
@@ -2495,7 +2523,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
         seg_lo[r] = seg_hi[r] = 0;
         val[r] = kMarkOwn + 1u + (uint32_t)i;
         if (i >= sp.n) continue;
-        uint64_t hi = cur.advance(base + c[r]);
+        uint64_t hi = hi_r[r];
         if (i + 1 == sp.n) {
             if (pp.rank == pp.nranks - 1 && hi < N)
                 atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
@@ -2991,19 +3019,29 @@ extern "C" hipError_t eslam_launch_finalize(Shard* recs, int nrec, Ctl* ctl, con
     return hipGetLastError();
 }
 
+// ff: the update step's finalize fused into block 0 (nullptr: k_finalize ran before)
 extern "C" hipError_t eslam_launch_normalize_scan(DevState s0, DevState s1, const ScanParams* sp, Ctl* ctl, uint64_t* tile_sum,
-                                                  uint64_t* total, hipStream_t stream)
+                                                  uint64_t* total, const FusedFin* ff, hipStream_t stream)
 {
     if (sp->ntiles == 0) return hipSuccess;
     if (sp->tag < 1 || sp->tag > 7) return hipErrorInvalidValue;
+    FusedFin none;
+    memset(&none, 0, sizeof(none));
+    const FusedFin& f = ff ? *ff : none;
+#define ESLAM_K3A(I)                                                                                                  \
+    do {                                                                                                              \
+        if (ff) hipLaunchKernelGGL((k_normalize_scan<I, true>), dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, \
+                                   ctl, tile_sum, total, f);                                                          \
+        else hipLaunchKernelGGL((k_normalize_scan<I, false>), dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp,   \
+                                ctl, tile_sum, total, f);                                                             \
+    } while (0)
     switch (sp->items) {
-    case 2: hipLaunchKernelGGL(k_normalize_scan<2>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total); break;
-    case 4: hipLaunchKernelGGL(k_normalize_scan<4>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total); break;
-    case kScanItems:
-        hipLaunchKernelGGL(k_normalize_scan<kScanItems>, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, ctl, tile_sum, total);
-        break;
+    case 2: ESLAM_K3A(2); break;
+    case 4: ESLAM_K3A(4); break;
+    case kScanItems: ESLAM_K3A(kScanItems); break;
     default: return hipErrorInvalidValue;
     }
+#undef ESLAM_K3A
     return hipGetLastError();
 }
 
@@ -3050,11 +3088,12 @@ extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream)
 extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, const ScanParams* sp, const PlanParams* pp, Ctl* ctl,
                                                   const uint64_t* tile_prefix, uint32_t* marks, uint32_t* tile_first,
                                                   const uint64_t* totals, const uint32_t* jt, uint2* range, uint64_t* first_last,
-                                                  hipStream_t stream)
+                                                  uint64_t* host_out, uint64_t* host_epoch, uint64_t epoch, hipStream_t stream)
 {
     if (sp->items != kScanItems) return hipErrorInvalidValue;       // the sharded scan uses full tiles
     if (sp->ntiles) hipLaunchKernelGGL(k_segments_multi, dim3(sp->ntiles), dim3(kBlock), 0, stream, s0, s1, *sp, *pp, ctl,
-                                       tile_prefix, marks, tile_first, totals, jt, range, first_last);
+                                       tile_prefix, marks, tile_first, totals, jt, range, first_last, host_out, host_epoch,
+                                       epoch);
     return hipGetLastError();
 }
 

@@ -94,6 +94,14 @@ def test_rough_forced_every_step_ragged(gpu_mod, rough_grid):
     run_pair(cfg, rough_grid, S.step_stream(6, tilt=True), n, gpu_factory=factory(gpu_mod), label="ragged")
 
 
+def test_two_item_scan_band(gpu_mod, rough_grid):
+    """n in (2^18, 2^19]: the 2-items-per-thread instantiation of k_normalize_segments
+    (eslam_ctx.hip scan_items), with a ragged last tile; every particle after every step."""
+    n = 400003
+    cfg = S.bench_config(A.default_config(), n)
+    run_pair(cfg, rough_grid, S.step_stream(3, tilt=True), n, gpu_factory=factory(gpu_mod), label="400k")
+
+
 def test_grouped_nan_contacts_and_misses(gpu_mod, rough_grid):
     # 8 contacts in 4 groups of 2 (asguard-like wheels), NaN = unknown contact probability
     feet = [(0.3, 0.1, -0.18), (0.3, -0.1, -0.2), (-0.3, 0.1, -0.18), (-0.3, -0.1, -0.22),
