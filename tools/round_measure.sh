@@ -3,6 +3,7 @@
 # instruction-mix passes, the bench line itself (with both CPU baselines), the other
 # workloads, smoke and the GPU test suite.  Usage (GPU box): bash tools/round_measure.sh <tag>
 cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
 tag=$1
 out=gpurun_out/round_$tag
 mkdir -p $out
@@ -21,7 +22,10 @@ step bench 600 python bench.py
 step bench_256k 300 python bench.py --particles 262144 --steps 50 --warmup 10 --no-cpu-baseline
 step bench_16m 300 python bench.py --particles 16777216 --steps 20 --warmup 5 --no-cpu-baseline
 step bench_rough 300 python bench.py --rough --steps 50 --warmup 10 --no-cpu-baseline
-step bench_local_maps 600 python bench.py --local-maps --steps 10 --warmup 3
-step bench_sharded 300 python bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline
+step bench_local_maps 600 python bench.py --local-maps --steps 20 --warmup 5
+step bench_local_maps_steady 600 python bench.py --local-maps --steps 20 --warmup 30 --no-cpu-baseline
+step prof_local_maps 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_local_maps -o run -- python3 bench.py --local-maps --steps 20 --warmup 30 --no-cpu-baseline
+step bench_sharded 300 python bench.py --sharded --particles 2097152 --steps 50 --warmup 10 --no-cpu-baseline
+step bench_2m 300 python bench.py --particles 2097152 --steps 50 --warmup 10 --no-cpu-baseline
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
