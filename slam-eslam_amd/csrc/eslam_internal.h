@@ -29,6 +29,9 @@ constexpr int kStatsLds = 2048;          // bytes of the statistics scratch at t
 #define ESLAM_WINDOW_LDS 38400
 #endif
 constexpr int kWindowLds = ESLAM_WINDOW_LDS;   // bytes of the MLS window after it (2400 cells: 40 KB per block with the stats, 4 blocks per CU)
+#ifndef ESLAM_K1_ATTR                    // experiment builds may set an occupancy attribute on K1
+#define ESLAM_K1_ATTR
+#endif
 
 // one statistics shard: exact sums as 4 limbs of 32-bit columns (uint64 each)
 struct alignas(128) Shard {

@@ -735,7 +735,7 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #define K1_ST(p, v) __builtin_nontemporal_store((v), (p))
 
 template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false, bool UNG = false>
-__global__ void __launch_bounds__(kBlock) k_project_weight(K1Args a)
+__global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args a)
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
     // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
