@@ -50,7 +50,8 @@ extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uin
                                              void* tmp, size_t* tmp_bytes, hipStream_t stream);
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  const GatherView* gv, const MapStore* store, hipStream_t stream);
+                                                  const GatherView* gv, const MapStore* store, hipStream_t stream,
+                                                  const ChunkSel* sel);
 extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
                                                 hipStream_t stream);
@@ -301,6 +302,14 @@ struct eslam_ctx {
     void* sendpay = nullptr; uint64_t sendpay_cap = 0;
     void* recvpay = nullptr; uint64_t recvpay_cap = 0;
     bool cow_pending = false;
+    // a sharded update's exchange left for the next call: the segments kernel's
+    // epoch and plan; the next step runs its own-output chunks before it completes it
+    bool xpend = false;
+    uint64_t xpend_epoch = 0;
+    PlanParams xpend_pp = {};
+    hipStream_t xstream = nullptr;           // the deferred exchange's stream (overlaps the own chunks)
+    hipEvent_t ev_seg = nullptr;             // recorded after the segments kernel
+    hipEvent_t ev_x = nullptr;               // recorded after the exchange's expand
     void* stage = nullptr; uint64_t stage_cap = 0;   // pinned staging (host-memory comm)
     // SurfaceHash (useHash)
     double map_scale[2] = {1, 1};
@@ -342,6 +351,8 @@ struct eslam_ctx {
 
 static constexpr uint32_t kRingSteps = 2048;
 
+static int settle(eslam_ctx* ctx);       // completes a deferred sharded exchange (run_update_tail_multi)
+
 // multi-GPU scratch block (uint64 words, device + pinned host mirror)
 namespace mg {
 constexpr int kTotal = 0;                                   // this rank's fixed-point weight total
@@ -357,7 +368,8 @@ constexpr int kBestAll = kBest + 2;                         // [2 kMaxRanks]
 constexpr int kMaxW = kBestAll + 2 * kMaxRanks;             // local max weight (bits)
 constexpr int kMaxWAll = kMaxW + 1;                         // [kMaxRanks]
 constexpr int kHostEpoch = kMaxWAll + kMaxRanks;           // (mg_host only) the segments kernel's epoch
-constexpr int kWords = kHostEpoch + 1;
+constexpr int kChunks = kHostEpoch + 1;                     // [2] own-output chunks of the slice (PlanParams::chunk_sel)
+constexpr int kWords = kChunks + 2;
 }  // namespace mg
 
 // timing mode: event k (0..4) of the current step, kept in a ring so a whole timed region
@@ -586,7 +598,11 @@ namespace { void rccl_release(eslam_ctx* ctx); }
 extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
 {
     if (!ctx) return;
+    ctx->xpend = false;                      // a deferred exchange is dropped (every rank drops it alike)
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->xstream) { (void)hipStreamSynchronize(ctx->xstream); (void)hipStreamDestroy(ctx->xstream); }
+    if (ctx->ev_seg) (void)hipEventDestroy(ctx->ev_seg);
+    if (ctx->ev_x) (void)hipEventDestroy(ctx->ev_x);
     rccl_release(ctx);
     free_particles(ctx);
     free_map(ctx);
@@ -607,6 +623,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
 extern "C" int eslam_gpu_set_stream(eslam_ctx* ctx, void* s)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (s) {
         if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
@@ -714,11 +731,13 @@ static int comm_allgather(eslam_ctx* ctx, const void* dsend, void* drecv, uint64
     return ESLAM_OK;
 }
 
-static int comm_alltoallv(eslam_ctx* ctx, const void* dsend, const uint64_t* sb, void* drecv, const uint64_t* rb)
+static int comm_alltoallv(eslam_ctx* ctx, const void* dsend, const uint64_t* sb, void* drecv, const uint64_t* rb,
+                          hipStream_t stream = nullptr)
 {
     const eslam_comm& c = ctx->comm;
+    if (!stream) stream = ctx->stream;
     if (c.device_memory) {
-        if (c.alltoallv(c.user, dsend, sb, drecv, rb, (void*)ctx->stream) != 0)
+        if (c.alltoallv(c.user, dsend, sb, drecv, rb, (void*)stream) != 0)
             return fail(ctx, ESLAM_ERR_COMM, "alltoallv callback failed");
         return ESLAM_OK;
     }
@@ -728,11 +747,11 @@ static int comm_alltoallv(eslam_ctx* ctx, const void* dsend, const uint64_t* sb,
     if (rc) return rc;
     char* h = (char*)ctx->stage;
     char* hr = h + ((ts + 63) & ~63ull);
-    if (ts) HIPCHK(ctx, hipMemcpyAsync(h, dsend, ts, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ts) HIPCHK(ctx, hipMemcpyAsync(h, dsend, ts, hipMemcpyDeviceToHost, stream));
+    HIPCHK(ctx, hipStreamSynchronize(stream));
     if (c.alltoallv(c.user, h, sb, hr, rb, nullptr) != 0) return fail(ctx, ESLAM_ERR_COMM, "alltoallv callback failed");
-    if (tr) HIPCHK(ctx, hipMemcpyAsync(drecv, hr, tr, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (tr) HIPCHK(ctx, hipMemcpyAsync(drecv, hr, tr, hipMemcpyHostToDevice, stream));
+    HIPCHK(ctx, hipStreamSynchronize(stream));
     return ESLAM_OK;
 }
 
@@ -744,12 +763,16 @@ static PlanParams plan_params(eslam_ctx* ctx)
     pp.rank = ctx->comm.rank;
     pp.nranks = ctx->comm.nranks;
     for (int r = 0; r <= ctx->comm.nranks; ++r) pp.gbase[r] = ctx->gall[r];
+    pp.chunk_sel = ctx->mg + mg::kChunks;
+    pp.n_local = ctx->n;
+    pp.J = dm_chunk_rows(ctx->n_global);
     return pp;
 }
 
 extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     free_particles(ctx);
     if (!comm) {
@@ -890,6 +913,7 @@ extern "C" int eslam_gpu_set_comm_rccl(eslam_ctx* ctx, int32_t nranks, int32_t r
                                        uint64_t n_global, const uint64_t* shard_gbase)
 {
     if (!ctx || !id) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (record_contacts(ctx))             // see eslam_gpu_set_comm
         return fail(ctx, ESLAM_ERR_UNSUPPORTED,
                     "logDebug / ESLAM_FLAG_RECORD_CONTACTS is not supported on a sharded filter (one GPU only)");
@@ -923,6 +947,7 @@ extern "C" int eslam_gpu_set_comm_rccl(eslam_ctx* ctx, int32_t nranks, int32_t r
 extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
 {
     if (!ctx || !g || !g->cell_start || !g->patch_mean || !g->patch_stdev) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (g->width == 0 || g->height == 0) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
     const uint64_t ncell = (uint64_t)g->width * g->height;
     if ((uint64_t)g->cell_start[ncell] != g->n_patches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "cell_start[width*height] != n_patches");
@@ -995,6 +1020,7 @@ extern "C" int eslam_gpu_init_gaussian(eslam_ctx* ctx, uint64_t n, const double 
                                        double zsigma)
 {
     if (!ctx || !mu || !sigma) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = alloc_particles(ctx, n);
     if (rc) return rc;
     rc = reset_ctl_for_new_particles(ctx, 1);
@@ -1008,6 +1034,7 @@ extern "C" int eslam_gpu_init_gaussian(eslam_ctx* ctx, uint64_t n, const double 
 extern "C" int eslam_gpu_init_pose(eslam_ctx* ctx, const double pos[3], const double q[4])
 {
     if (!ctx || !pos || !q) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
     double R[9];
     q_to_mat(q, R);
@@ -1058,6 +1085,7 @@ static dm_hash_grid hash_grid(eslam_ctx* ctx)
 extern "C" int eslam_gpu_hash_create(eslam_ctx* ctx)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
     const uint32_t steps = (uint32_t)ctx->cfg.hash_angular_steps, bins = (uint32_t)ctx->cfg.hash_slope_bins;
     if (steps == 0 || bins == 0 || bins > 4096) return fail(ctx, ESLAM_ERR_INVALID_ARG, "hash_angular_steps / hash_slope_bins");
@@ -1130,6 +1158,7 @@ static const double* hash_field(eslam_ctx* ctx, int f)
 extern "C" int eslam_gpu_init_hash(eslam_ctx* ctx, uint64_t n)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!ctx->has_hash || ctx->hash_n == 0) return fail(ctx, ESLAM_ERR_HASH_SAMPLE, "could not sample from pose hash.");
     int rc = alloc_particles(ctx, n);
     if (rc) return rc;
@@ -1166,6 +1195,7 @@ extern "C" int eslam_gpu_hash_info(eslam_ctx* ctx, uint64_t* n_poses, uint32_t* 
 extern "C" int eslam_gpu_hash_poses(eslam_ctx* ctx, double* x, double* y, double* theta, double* z, int32_t* bucket)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!ctx->has_hash) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no pose hash");
     const uint64_t n = ctx->hash_n;
     double* dst[4] = {x, y, theta, z};
@@ -1185,6 +1215,7 @@ extern "C" int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n)
 extern "C" int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const eslam_particles* p)
 {
     if (!ctx || !p || !p->x || !p->y || !p->orientation || !p->zpos || !p->zsigma || !p->weight) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = alloc_particles(ctx, n);
     if (rc) return rc;
     const DevState& s = ctx->st[0];
@@ -1227,6 +1258,7 @@ extern "C" int eslam_gpu_upload_particles(eslam_ctx* ctx, uint64_t n, const esla
 extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
 {
     if (!ctx || !p) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     int rc = materialize(ctx);
     if (!rc) rc = read_ctl(ctx);
@@ -1255,6 +1287,7 @@ extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
 extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p)
 {
     if (!ctx || !p || first > ctx->n || count > ctx->n - first) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     int rc = materialize(ctx);               // the particles the caller saw: any pending gather done
     if (!rc) rc = read_ctl(ctx);
@@ -1307,6 +1340,7 @@ extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64
                                           eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints)
 {
     if (!ctx || (!out && count)) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     if (!count) return ESLAM_OK;
     if (!stride) stride = 1;
@@ -1342,6 +1376,7 @@ extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64
 extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count)
 {
     if (!ctx || (!patches && count)) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update needs per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
     if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
@@ -1371,6 +1406,7 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
 extern "C" int eslam_gpu_set_particle_maps(eslam_ctx* ctx, int on)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     const bool cur = particle_maps(ctx);
     if ((on != 0) == cur) return ESLAM_OK;
     if (ctx->n) return fail(ctx, ESLAM_ERR_INVALID_ARG, "the map mode is chosen before the particles are initialised");
@@ -1383,6 +1419,7 @@ extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32
                                           uint32_t capacity, uint32_t* count)
 {
     if (!ctx || !count) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "no per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
     if (index >= ctx->n) return fail(ctx, ESLAM_ERR_INVALID_ARG, "particle index out of range");
     int rc = materialize(ctx);
@@ -1594,6 +1631,9 @@ static int abort_pending_gather(eslam_ctx* ctx, hipError_t e, int rc = ESLAM_ERR
 // shard) measured the same as 200 us on one rank at 2M and 4M (profiles/r02/ab_spin.log)
 constexpr long kSpinBoundUs = 200;
 
+static int exchange_tail(eslam_ctx* ctx, uint64_t epoch, PlanParams& pp, uint64_t* own_lo, uint64_t* own_hi,
+                         hipStream_t xs = nullptr, bool* queued = nullptr);
+
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
     const int G = ctx->comm.nranks, me = ctx->comm.rank;
@@ -1626,6 +1666,51 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
                                             ctx->mg + mg::kFirstLast, h + mg::kTotals, h + mg::kHostEpoch, epoch,
                                             ctx->stream));
     if (timed) rec(ctx, 3);
+    if (keep_ancestors(ctx)) ctx->has_anc = true;
+    // an update defers the exchange to the next call, which first runs the chunks of the rank's
+    // own outputs while the host waits for the totals (no particle maps: their stores travel
+    // with the records and are placed by the map update)
+    if (mode == FIN_UPDATE && !particle_maps(ctx)) {
+        if (G > 1) {                         // one rank exchanges nothing: no side stream
+            if (!ctx->xstream) {
+                HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking));
+                HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_seg, hipEventDisableTiming));
+                HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_x, hipEventDisableTiming));
+            }
+            HIPCHK(ctx, hipEventRecord(ctx->ev_seg, ctx->stream));
+        }
+        ctx->xpend = true;
+        ctx->xpend_epoch = epoch;
+        ctx->xpend_pp = pp;
+        if (timed) rec(ctx, 4);
+        return ESLAM_OK;
+    }
+    uint64_t own_lo = 0, own_hi = 0;
+    rc = exchange_tail(ctx, epoch, pp, &own_lo, &own_hi);
+    if (timed) rec(ctx, 4);
+    return rc;
+}
+
+// The exchange of a sharded resample, after k_segments_multi: wait for the gathered totals
+// (host-mapped words the segments kernel writes), derive every rank's output range (the
+// all_to_all_v sizes: one record per output that lands in another slice), pack, exchange,
+// expand.  own_lo / own_hi: the chunks of this slice holding only its own outputs (the
+// segments kernel's PlanParams::chunk_sel, computed alike).
+// xs: the stream of the pack / exchange / expand (the context's stream by default; the split
+// step's side stream, which waits for ev_seg, overlapping the own chunks' weighting launch)
+static int exchange_tail(eslam_ctx* ctx, uint64_t epoch, PlanParams& pp, uint64_t* own_lo, uint64_t* own_hi,
+                         hipStream_t xs, bool* queued)
+{
+    if (!xs) xs = ctx->stream;
+    if (queued) *queued = false;
+    const int G = ctx->comm.nranks, me = ctx->comm.rank;
+    int rc = ESLAM_OK;
+    uint64_t* h = ctx->mg_host;
+    {
+        const uint64_t csz = 64ull * pp.J;
+        *own_lo = 0;
+        *own_hi = (ctx->n + csz - 1) / csz;
+    }
     {
         // spin on the epoch word: a blocking synchronize wakes the thread tens of microseconds
         // late, and the GPU runs dry before the next step's launches if the host is late here
@@ -1636,7 +1721,7 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
         const auto bound = std::chrono::microseconds(kSpinBoundUs);
         while (__atomic_load_n(h + mg::kHostEpoch, __ATOMIC_ACQUIRE) != epoch) {
             if (std::chrono::steady_clock::now() - t0 > bound) {
-                const hipError_t q = hipStreamSynchronize(ctx->stream);
+                const hipError_t q = xs == ctx->stream ? hipStreamSynchronize(xs) : hipEventSynchronize(ctx->ev_seg);
                 if (q != hipSuccess) return abort_pending_gather(ctx, q);
                 break;
             }
@@ -1693,16 +1778,19 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
             if (!rc && maps) rc = grow(ctx, &ctx->sendpay, &ctx->sendpay_cap, nsend * P, false);
             if (!rc && maps) rc = grow(ctx, &ctx->recvpay, &ctx->recvpay_cap, nrecv * P, false);
             if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
+            // a side stream starts after the segments kernel (its records and ranges)
+            if (xs != ctx->stream) HIPCHK(ctx, hipStreamWaitEvent(xs, ctx->ev_seg, 0));
+            if (queued) *queued = true;
             const hipError_t e = eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
                                                    nsend, ctx->sendbuf, &ctx->store, maps ? ctx->sendpay : nullptr,
-                                                   ctx->stream);
+                                                   xs);
             if (e != hipSuccess) return abort_pending_gather(ctx, e);
-            rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb);
+            rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb, xs);
             if (!rc && maps) {
                 // the migrated stores, in the records' order (the same peers, P bytes per record)
                 uint64_t sp_[kMaxRanks], rp_[kMaxRanks];
                 for (int d = 0; d < G; ++d) { sp_[d] = sb[d] / R * P; rp_[d] = rb[d] / R * P; }
-                rc = comm_alltoallv(ctx, ctx->sendpay, sp_, ctx->recvpay, rp_);
+                rc = comm_alltoallv(ctx, ctx->sendpay, sp_, ctx->recvpay, rp_, xs);
                 ctx->cow_pending = !rc && nrecv > 0;
             }
             if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
@@ -1710,11 +1798,27 @@ static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
             nrecv = 0;
         }
     }
+    if (c_resample) {
+        // the own-output chunks (the same function of the same totals as on the device)
+        const uint64_t N = ctx->n_global;
+        uint64_t off = 0;
+        for (int r = 0; r < me; ++r) off += h[mg::kTotals + r];
+        const uint64_t O0 = me == 0 ? 0 : dm_count_draws_le(off, N, c_minstd_start, c_scan_shift);
+        const uint64_t O1 = me == G - 1 ? N : dm_count_draws_le(off + h[mg::kTotals + me], N, c_minstd_start, c_scan_shift);
+        own_chunks(O0, O1, ctx->gbase, ctx->n, pp.J, own_lo, own_hi);
+    }
     // marks of the migrated outputs; the gather is fused into the next k_project_weight
-    HIPCHK(ctx, eslam_launch_expand(ctx->recvbuf, nrecv, ctx->gbase, ctx->marks, ctx->tile_first, ctx->stream));
-    if (timed) rec(ctx, 4);
-    if (keep_ancestors(ctx)) ctx->has_anc = true;
+    HIPCHK(ctx, eslam_launch_expand(ctx->recvbuf, nrecv, ctx->gbase, ctx->marks, ctx->tile_first, xs));
     return ESLAM_OK;
+}
+
+// complete a deferred exchange before anything else reads the particles or the marks
+static int settle(eslam_ctx* ctx)
+{
+    if (!ctx->xpend) return ESLAM_OK;
+    ctx->xpend = false;
+    uint64_t lo = 0, hi = 0;
+    return exchange_tail(ctx, ctx->xpend_epoch, ctx->xpend_pp, &lo, &hi);
 }
 
 static int run_update_tail(eslam_ctx* ctx, uint32_t mode, bool timed)
@@ -1866,19 +1970,27 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
         const uint64_t period = ctx->cfg.hash_period ? ctx->cfg.hash_period : 1;
         respawn = (ctx->hash_event++ % period) == 0;
     }
+    // logDebug records: the update's contact points are recorded on the projected state
+    const bool records = weight && record_contacts(ctx);   // one GPU only (eslam_gpu_set_comm refuses it)
+    // a deferred sharded exchange: the weighting launch is split around it (own-output chunks,
+    // the exchange, the other chunks) unless the step takes another path first
+    const bool split = ctx->xpend && !respawn && !records && !particle_maps(ctx);
+    if (ctx->xpend && !split) {
+        const int rc = settle(ctx);
+        if (rc) return rc;
+    }
     // per-particle maps: the resample gather is materialised (it carries the store names), so
     // no k_project_weight consumes one
     if (particle_maps(ctx)) {
         const int rc = materialize(ctx);
         if (rc) return rc;
     }
-    // logDebug records: the update's contact points are recorded on the projected state, so
-    // the project runs as its own launch first (bit-identical to the fused kernel)
-    const bool records = weight && record_contacts(ctx);   // one GPU only (eslam_gpu_set_comm refuses it)
+    // logDebug records: the project runs as its own launch first (bit-identical to the fused
+    // kernel)
     if (respawn || (records && project)) {
         const GatherView gv0 = gather_view(ctx);
         HIPCHK(ctx, eslam_launch_project_weight(1, 0, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                                ctx->shards, &gv0, nullptr, ctx->stream));
+                                                ctx->shards, &gv0, nullptr, ctx->stream, nullptr));
         HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
         ctx->proj_event++;
         if (gv0.record) ctx->has_anc = true;
@@ -1905,8 +2017,46 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     }
     rec(ctx, 0);
     const GatherView gv = gather_view(ctx);
+    ChunkSel sel;
+    memset(&sel, 0, sizeof(sel));
+    if (split) {
+        sel.mode = 1;                         // the own-output chunks (the segments kernel's chunk_sel)
+        sel.cdev = ctx->mg + mg::kChunks;
+    }
     HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                            ctx->shards, &gv, store_of(ctx), ctx->stream));
+                                            ctx->shards, &gv, store_of(ctx), ctx->stream, split ? &sel : nullptr));
+    if (split) {
+        // the previous update's exchange (its host wait overlaps the launch above), then the
+        // chunks that needed its records.  A failure here leaves a half-weighted step: the
+        // filter is poisoned rather than continued.
+        ctx->xpend = false;
+        uint64_t own_lo = 0, own_hi = 0;
+        bool queued = false;
+        hipStream_t xs = ctx->comm.nranks > 1 ? ctx->xstream : ctx->stream;
+        const int rc = exchange_tail(ctx, ctx->xpend_epoch, ctx->xpend_pp, &own_lo, &own_hi, xs, &queued);
+        if (rc) {
+            ctx->poisoned = true;
+            if (xs != ctx->stream) (void)hipStreamSynchronize(xs);
+            return rc;
+        }
+        if (queued && xs != ctx->stream) {
+            // the main stream continues once the records and their marks are in place
+            HIPCHK(ctx, hipEventRecord(ctx->ev_x, xs));
+            HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_x, 0));
+        }
+        const uint64_t csz = 64ull * p.J, nch = (ctx->n + csz - 1) / csz;
+        if (own_lo > 0 || own_hi < nch) {
+            sel.mode = 2;
+            sel.c_lo = own_lo;
+            sel.c_hi = own_hi;
+            sel.cdev = nullptr;
+            // the exchange may have grown (reallocated) the receive buffer: the records are read
+            // through the gather view taken now, not the one of the first launch
+            const GatherView gve = gather_view(ctx);
+            HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p,
+                                                    ctx->ctl, ctx->shards, &gve, store_of(ctx), ctx->stream, &sel));
+        }
+    }
     rec(ctx, 1);
     if (project) ctx->proj_event++;
     if (gv.record) ctx->has_anc = true;
@@ -1972,6 +2122,7 @@ extern "C" int eslam_gpu_debug_set_spin_limit(eslam_ctx* ctx, uint32_t polls)
 extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = read_ctl(ctx);
     if (rc) return rc;
     const Ctl& c = *ctx->ctl_host;
@@ -2048,6 +2199,7 @@ static int standalone(eslam_ctx* ctx, uint32_t mode)
 extern "C" int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum)
 {
     if (!ctx || !sum) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = standalone(ctx, FIN_SUM);
     if (rc) return rc;
     rc = read_ctl(ctx);
@@ -2059,6 +2211,7 @@ extern "C" int eslam_gpu_get_weights_sum(eslam_ctx* ctx, double* sum)
 extern "C" int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = standalone(ctx, FIN_NORMALIZE);
     if (rc) return rc;
     rc = read_ctl(ctx);
@@ -2070,6 +2223,7 @@ extern "C" int eslam_gpu_normalize_weights(eslam_ctx* ctx, double* effective)
 extern "C" int eslam_gpu_resample(eslam_ctx* ctx)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     ctx->dbg_valid = false;                  // the records no longer follow the particles
     return standalone(ctx, FIN_RESAMPLE);
 }
@@ -2077,6 +2231,7 @@ extern "C" int eslam_gpu_resample(eslam_ctx* ctx)
 extern "C" int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index)
 {
     if (!ctx || !index) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!ctx->n) { *index = 0; return ESLAM_OK; }
     if (const int rc0 = materialize(ctx)) return rc0;
     uint64_t* out = reinterpret_cast<uint64_t*>(ctx->scratch);
@@ -2109,6 +2264,7 @@ extern "C" int eslam_gpu_get_best_particle_index(eslam_ctx* ctx, uint64_t* index
 extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double orientation[4])
 {
     if (!ctx || !position || !orientation) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = eslam_gpu_normalize_weights(ctx, nullptr);     // side effect, Q15
     if (rc) return rc;
     const uint32_t J = dm_chunk_rows(ctx->n_global);
@@ -2169,6 +2325,7 @@ extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double
 extern "C" int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st)
 {
     if (!ctx || !st) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = read_ctl(ctx);
     if (rc) return rc;
     memset(st, 0, sizeof(*st));
@@ -2186,6 +2343,7 @@ extern "C" int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st)
 extern "C" int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st)
 {
     if (!ctx || !st) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = read_ctl(ctx);
     if (rc) return rc;
     ctx->ctl_host->minstd = st->minstd_x;
@@ -2202,6 +2360,7 @@ extern "C" int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st
 extern "C" int eslam_gpu_get_ancestors(eslam_ctx* ctx, uint32_t* out, uint64_t n)
 {
     if (!ctx || !out) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!ctx->has_anc || !ctx->anc) return fail(ctx, ESLAM_ERR_INVALID_ARG, "no ancestors recorded (ESLAM_FLAG_RECORD_ANCESTORS)");
     if (const int rc = materialize(ctx)) return rc;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));

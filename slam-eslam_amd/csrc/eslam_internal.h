@@ -189,6 +189,15 @@ struct GatherView {
     uint32_t multi;                      // marks use the multi-GPU source encoding
 };
 
+// which chunks a k_project_weight launch processes: all (mode 0); the own chunks named by the
+// device words cdev[0..1] (mode 1); the others, [0, c_lo) and [c_hi, nchunks) (mode 2)
+struct ChunkSel {
+    uint32_t mode;
+    uint32_t pad;
+    uint64_t c_lo, c_hi;
+    const uint64_t* cdev;
+};
+
 // k_project_weight's single kernel argument: its fields are read with scalar loads from the
 // kernel-argument segment where they are used (offsetof), see k_project_weight
 struct K1Args {
@@ -199,6 +208,7 @@ struct K1Args {
     Ctl* ctl;
     Shard* shards;
     MapStore store;                      // per-particle maps (the DELTA instantiations only)
+    ChunkSel sel;                        // the chunks this launch processes
 };
 
 // one scan patch of a map update (the scan MLS of processMap, in the yaw-free body frame)
@@ -329,6 +339,28 @@ struct PlanParams {
     // outputs in d's slice [sd[d], ed[d]) and their offsets in the send buffer
     uint64_t sd[kMaxRanks], ed[kMaxRanks];
     uint64_t send_off[kMaxRanks + 1];
+    // the deferred exchange: the segments kernel writes the chunks of this rank's
+    // slice whose outputs all come from its own particles, [chunk_sel[0], chunk_sel[1])
+    uint64_t* chunk_sel;
+    uint64_t n_local;
+    uint32_t J;
 };
+
+// Chunks (64 J outputs each) of a rank's slice [W0, W0 + n) that hold only outputs of its own
+// particles, whose outputs are [O0, O1) globally: the rest -- a prefix filled from lower ranks,
+// a suffix from higher ranks -- needs the exchanged records.  Host and device compute it alike.
+__host__ __device__ inline void own_chunks(uint64_t O0, uint64_t O1, uint64_t W0, uint64_t n, uint32_t J, uint64_t* c_lo,
+                                           uint64_t* c_hi)
+{
+    const uint64_t csz = 64ull * J, nchunks = (n + csz - 1) / csz;
+    const uint64_t lo = O0 <= W0 ? 0 : (O0 - W0 < n ? O0 - W0 : n);
+    uint64_t hi = O1 <= W0 ? 0 : (O1 - W0 < n ? O1 - W0 : n);
+    hi = hi < lo ? lo : hi;
+    const uint64_t cl = (lo + csz - 1) / csz;
+    uint64_t ch = hi == n ? nchunks : hi / csz;
+    *c_lo = cl;
+    *c_hi = ch < cl ? cl : ch;
+}
+
 
 }  // namespace eslam_dev

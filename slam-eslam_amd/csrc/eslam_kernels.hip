@@ -87,7 +87,19 @@ template <class T, class Op> __device__ __forceinline__ T wave_butterfly(T v, Op
 // one stage of a transposed xor butterfly over 2H totals per lane (see K1's chunk flush):
 // the lane with bit O set keeps the upper H totals, its partner the lower H, and each adds
 // the partner's copy of the totals it keeps
-template <int O, int H> __device__ __forceinline__ void transpose_add(double (&v)[16], uint32_t lane)
+// transpose_add with another order-free operation (float maxima)
+template <int O, int H, int N, class Op> __device__ __forceinline__ void transpose_op(float (&v)[N], uint32_t lane, Op op)
+{
+    const bool up = (lane & (uint32_t)O) != 0u;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const float send = up ? v[j] : v[H + j];
+        const float keep = up ? v[H + j] : v[j];
+        v[j] = op(keep, xor_lane<O>(send));
+    }
+}
+
+template <int O, int H, int N> __device__ __forceinline__ void transpose_add(double (&v)[N], uint32_t lane)
 {
     const bool up = (lane & (uint32_t)O) != 0u;
 #pragma unroll
@@ -772,15 +784,26 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
+    uint32_t touched = 0;                // bit b: some row added to bucket b (wave-uniform)
     // -min x, max x, -min y, max y of the cloud, rounded to float (the window only needs a
     // box that holds the cloud; it is widened by the float rounding in bbox_keys)
     float bb[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     uint64_t limb = 0;                  // lane t < 52: column t & 3 of exact accumulator t >> 2
     const int sa = DM_FX_SCALE - wexp, sb = DM_FX_SCALE - 2 * wexp;
 
-    // one canonical chunk (64 x J particles) per wave; its totals go to exact fixed point
-    const uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
-    if (chunk < nchunks) {
+    // one canonical chunk (64 x J particles) per wave; its totals go to exact fixed point.
+    // A sharded step may split the launch (ChunkSel): the chunks of the rank's own outputs
+    // first, the chunks that need exchanged records after the exchange (exact sums: the
+    // statistics do not depend on the order in which chunks are processed)
+    uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave;
+    bool active = chunk < nchunks;
+    if (a.sel.mode == 1u) {
+        active = chunk >= a.sel.cdev[0] && chunk < a.sel.cdev[1];
+    } else if (a.sel.mode == 2u) {
+        chunk = chunk < a.sel.c_lo ? chunk : a.sel.c_hi + (chunk - a.sel.c_lo);
+        active = chunk < nchunks;
+    }
+    if (active) {
     const uint64_t lbase = chunk * csz;
     double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
 #pragma unroll
@@ -928,6 +951,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             do {
                 const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
                 const bool mine = bucket == b0;
+                touched |= 1u << b0;
                 const double a1 = mine ? am : 0.0, a2 = mine ? am2 : 0.0;
 #pragma unroll
                 for (int b = 0; b < kBuckets; ++b) {
@@ -980,18 +1004,51 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
         // finish it there, and each lane converts its total once and keeps limb lane & 3.
         constexpr int kQ = 2 * DM_NBUCKETS + 1;
         static_assert(kQ <= 16, "16 totals over the 64 lanes");
-        double v[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            v[q] = q < DM_NBUCKETS ? accA[q] : (q < 2 * DM_NBUCKETS ? accB[q - DM_NBUCKETS] : (q == kQ - 1 ? accSW : 0.0));
-        transpose_add<32, 8>(v, lane);
-        transpose_add<16, 4>(v, lane);
-        transpose_add<8, 2>(v, lane);
-        transpose_add<4, 1>(v, lane);
-        double t = v[0];
-        t = t + xor_lane<2>(t);
-        t = t + xor_lane<1>(t);
         const uint32_t q = lane >> 2;
+        double t;
+        // `touched` is only updated by the lanes active in a walk: lanes past n in the last row
+        // keep an older set.  Lane 0 takes part in every walk (a row runs only if row0 < n), so
+        // its set is complete, and read as a scalar the branch below is wave-uniform.
+        touched = (uint32_t)__builtin_amdgcn_readlane((int)touched, 0);
+        if (__builtin_popcount(touched) <= 1) {
+            // the usual wave: every row's particles in one bucket b0, so the totals of the
+            // other buckets are +0.0 (nothing was added to them).  The butterfly runs over
+            // A_b0, B_b0 and SW only (transposed at distances 32 and 16: total k ends in lanes
+            // 16k..16k+15), the same pairwise additions, and lane 4q + c picks total q.
+            const uint32_t b0 = touched ? (uint32_t)__builtin_ctz(touched) : 0u;
+            double w4[4] = {0.0, 0.0, accSW, 0.0};
+#pragma unroll
+            for (int b = 0; b < DM_NBUCKETS; ++b) {
+                if (b0 == (uint32_t)b) { w4[0] = accA[b]; w4[1] = accB[b]; }
+            }
+            transpose_add<32, 2>(w4, lane);
+            transpose_add<16, 1>(w4, lane);
+            double u = w4[0];
+            u = u + xor_lane<8>(u);
+            u = u + xor_lane<4>(u);
+            u = u + xor_lane<2>(u);
+            u = u + xor_lane<1>(u);
+            auto lane_value = [](double x, int l) {      // v_readlane of both halves
+                const uint64_t b = dm_bits(x);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+                return dm_from_bits(((uint64_t)hi << 32) | lo);
+            };
+            const double tA = lane_value(u, 0), tB = lane_value(u, 16), tS = lane_value(u, 32);
+            t = q == b0 ? tA : (q == DM_NBUCKETS + b0 ? tB : (q == kQ - 1 ? tS : 0.0));
+        } else {
+            double v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v[k] = k < DM_NBUCKETS ? accA[k] : (k < 2 * DM_NBUCKETS ? accB[k - DM_NBUCKETS] : (k == kQ - 1 ? accSW : 0.0));
+            transpose_add<32, 8>(v, lane);
+            transpose_add<16, 4>(v, lane);
+            transpose_add<8, 2>(v, lane);
+            transpose_add<4, 1>(v, lane);
+            t = v[0];
+            t = t + xor_lane<2>(t);
+            t = t + xor_lane<1>(t);
+        }
         const int scale = q < DM_NBUCKETS ? sa : (q < 2 * DM_NBUCKETS ? sb : DM_FX_SCALE);
         const bool nan_ = t != t, inf_ = !nan_ && !dm_isfinite(t);
         uint32_t l[4] = {0, 0, 0, 0};
@@ -1007,20 +1064,26 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     }
     }
 
-    // bounding box of the cloud for the next step's LDS window (maxima, any order)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        bb[q] = wave_butterfly(bb[q], [](float a, float b) { return __builtin_fmaxf(a, b); });
-    }
     Shard* shb = a.shards + (blockIdx.x % kNShard);
-    if (lane == 0 && bb[1] > -INFINITY) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
+    // bounding box of the cloud for the next step's LDS window (maxima, any order): the four
+    // maxima in one transposed butterfly (at distances 32 and 16 each lane pair keeps half of
+    // them), so value q ends in lanes 16q..16q+15 and lane 16q publishes it
+    {
+        transpose_op<32, 2>(bb, lane, [](float a, float b) { return __builtin_fmaxf(a, b); });
+        transpose_op<16, 1>(bb, lane, [](float a, float b) { return __builtin_fmaxf(a, b); });
+        float m = bb[0];
+        m = __builtin_fmaxf(m, xor_lane<8>(m));
+        m = __builtin_fmaxf(m, xor_lane<4>(m));
+        m = __builtin_fmaxf(m, xor_lane<2>(m));
+        m = __builtin_fmaxf(m, xor_lane<1>(m));
+        const float xmax = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(m), 16));
+        if ((lane & 15u) == 0u && xmax > -INFINITY) {
+            const uint32_t q = lane >> 4;
             // |x - (float)x| <= 2^-24 |x| + 2^-150: widen outward, then the order key
-            const double v = (double)bb[q];
+            const double v = (double)m;
             const double wv = v + (dm_fabs(v) * 0x1p-22 + 0x1p-140);
-            const uint64_t k = order_key((q & 1) ? wv : -wv);
-            atomicMax((unsigned long long*)&shb->bbox[q], (unsigned long long)((q & 1) ? k : ~k));
+            const uint64_t k = order_key((q & 1u) ? wv : -wv);
+            atomicMax((unsigned long long*)&shb->bbox[q], (unsigned long long)((q & 1u) ? k : ~k));
         }
     }
 
@@ -1036,7 +1099,10 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     static_assert(sizeof(StatsLds) <= kStatsLds, "stats scratch");
     StatsLds& sl = *reinterpret_cast<StatsLds*>(smem);
     const double wmax = wave_max_butterfly(maxm);
-    const uint32_t wD = wave_sum_u32(nD), wTP = wave_sum_u32(nTP);
+    // the two counts in one sum: nD <= 64 J and nTP <= ESLAM_MAX_CONTACTS nD per wave (16 bits each)
+    static_assert(64u * ESLAM_CHUNK_CAP * ESLAM_MAX_CONTACTS < 65536u, "packed wave counts");
+    const uint32_t wDTP = wave_sum_u32(nD | (nTP << 16));
+    const uint32_t wD = wDTP & 0xffffu, wTP = wDTP >> 16;
     const uint32_t werr = __ballot(err != 0) != 0ull ? 1u : 0u;
     if (lane < (2 * DM_NBUCKETS + 1) * 4) sl.limb[wave][lane] = limb;
     if (lane == 0) {
@@ -2488,6 +2554,16 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
         for (int r = 0; r < pp.nranks; ++r) host_out[r] = totals[r];
         for (int q = 0; q < 3; ++q) host_out[kMaxRanks + q] = totals[kMaxRanks + q];
         __hip_atomic_store(host_epoch, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the chunks the next weighting launch may process before the exchange: all of them
+        // without a resample (no gather pending), else those of the own outputs
+        uint64_t c_lo = 0, c_hi = (pp.n_local + 64ull * pp.J - 1) / (64ull * pp.J);
+        if (ctl->resample) {
+            uint64_t off, O0, O1;
+            plan_bounds(pp, ctl, totals, jt, off, O0, O1);
+            own_chunks(O0, O1, pp.gbase[pp.rank], pp.n_local, pp.J, &c_lo, &c_hi);
+        }
+        pp.chunk_sel[0] = c_lo;
+        pp.chunk_sel[1] = c_hi;
     }
     if (!ctl->resample) return;
     const uint32_t tid = threadIdx.x;
@@ -2853,10 +2929,12 @@ static uint32_t k1_grid(uint64_t chunks) { return (uint32_t)((chunks + kWaves - 
 
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  const GatherView* gv, const MapStore* store, hipStream_t stream)
+                                                  const GatherView* gv, const MapStore* store, hipStream_t stream,
+                                                  const ChunkSel* sel)
 {
     const uint64_t csz = 64ull * p->J;
-    const uint64_t chunks = (p->n + csz - 1) / csz;
+    uint64_t chunks = (p->n + csz - 1) / csz;
+    if (sel && sel->mode == 2u) chunks = sel->c_lo + (chunks > sel->c_hi ? chunks - sel->c_hi : 0);   // the edge chunks
     if (chunks == 0) return hipSuccess;
     const size_t lds = kStatsLds + (weight ? kWindowLds : 0);
     K1Args args;
@@ -2869,6 +2947,8 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     args.shards = shards;
     memset(&args.store, 0, sizeof(args.store));
     if (store) args.store = *store;
+    memset(&args.sel, 0, sizeof(args.sel));
+    if (sel) args.sel = *sel;
 #define ESLAM_LAUNCH(P, W, M, B, ...)                                                                   \
     hipLaunchKernelGGL((k_project_weight<P, W, M, B, ##__VA_ARGS__>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
                        stream, args)

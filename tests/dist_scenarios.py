@@ -24,7 +24,7 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3", "config4", "maps"):
+    if name in ("forced", "config3", "config4", "maps", "burst"):
         S.bench_config(cfg, n_global)
         if name in ("maps", "config4"):          # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
@@ -46,7 +46,7 @@ def scenario_grid(name):
         return S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
     if name == "maps":                            # the front feet stand on cells only the scans map
         return S.unmapped_beyond(S.rough_map(cells=120), 0.3)
-    return S.rough_map(cells=120) if name != "forced" else S.rough_map(cells=120, multi=False)
+    return S.rough_map(cells=120) if name not in ("forced", "burst") else S.rough_map(cells=120, multi=False)
 
 
 def digest(a):
@@ -146,6 +146,16 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     else:
         sigma = [0.1, 0.1, 0.1] if name == "forced" else [0.6, 0.6, 0.3]
         f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], sigma, 0.18, 1.001)
+    if name == "burst":
+        # forced updates back to back with nothing read between them: a sharded GPU filter
+        # defers each update's exchange into the next step (split weighting launch)
+        for st in S.step_stream(steps):
+            f.step(st)
+        _info(rec, "last", info_fn(f))
+        _snap(rec, "last", f, True)
+        rec["best"] = np.array([f.best_index()])
+        rec["rng"] = np.array([f.rng_state().minstd_x])
+        return rec
     _snap(rec, "init", f, False)
     if name == "hash":
         from hash_util import slope_stream

@@ -60,7 +60,12 @@ def main():
             rec["rng"] = rng
             rec["range"] = np.array([lo, hi])
         else:
-            rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.sync())
+            try:
+                rec = run_scenario(f, name, n_global, lo, hi, info_fn=lambda g: g.sync())
+            except Exception as e:
+                if comm.error is not None:       # the collective's own failure, not the library's report of it
+                    raise RuntimeError(f"rank {rank}: {e}") from comm.error
+                raise
         f.close()
     if comm.error is not None:
         raise comm.error

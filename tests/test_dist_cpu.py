@@ -37,8 +37,9 @@ def launch(kind, name, n_global, world, tmp, mem="host", timeout=240):
                 q.kill()
             raise
         logs.append(o.decode(errors="replace"))
-    for p, log in zip(procs, logs):
-        assert p.returncode == 0, log[-3000:]
+    bad = [f"--- rank {r} (exit {p.returncode}) ---\n{log[-2500:]}" for r, (p, log) in enumerate(zip(procs, logs))
+           if p.returncode != 0]
+    assert not bad, "\n".join(bad)
     return [dict(np.load(o)) for o in outs]
 
 
@@ -73,7 +74,8 @@ def single_oracle(name, n_global):
 
 @pytest.mark.parametrize("name,n_global,world", [("forced", 3000, 2), ("natural", 2500, 2), ("upload", 2000, 2),
                                                  ("forced", 1000, 3), ("upload", 700, 3), ("hash", 2000, 2),
-                                                 ("hash", 1500, 3), ("maps", 3000, 2), ("maps", 1500, 3)])
+                                                 ("hash", 1500, 3), ("maps", 3000, 2), ("maps", 1500, 3),
+                                                 ("burst", 3000, 2)])
 def test_sharded_oracle_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("oracle", name, n_global, world, str(tmp_path)))

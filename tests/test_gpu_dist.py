@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("name,n_global,world", [("forced", 5000, 2), ("natural", 2500, 2), ("upload", 2000, 2),
                                                  ("upload", 700, 3), ("hash", 3000, 2), ("hash", 1500, 3),
-                                                 ("maps", 3000, 2), ("maps", 1500, 3)])
+                                                 ("maps", 3000, 2), ("maps", 1500, 3),
+                                                 ("burst", 5000, 2), ("burst", 7001, 3)])
 def test_sharded_gpu_gloo_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, world, str(tmp_path), mem="host", timeout=400))
