@@ -817,15 +817,19 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
         uint32_t src = (uint32_t)i;
         const gmem<const Rec>* rc = nullptr;
         uint32_t rec_anc = 0;
+        bool clr = false;                        // this output's segment mark is set
         if (gath) {
             const su8 g = kl8(KOFF(gv));              // marks, row_first, anc, recs
             const su2 gf = kl2(KOFF(gv.record));      // record, multi
             gmem<uint32_t>* marks = kp<uint32_t>(g, 0);
-            // expand the segment marks of this row: inclusive max-scan + the row carry
-            uint32_t m = 0;
-            if (i < n) { m = marks[i]; if (m) marks[i] = 0; }
-            m = wave_incl_max_u32(m);
+            // expand the segment marks of this row: inclusive max-scan + the row carry.  Both
+            // loads are issued together; the mark is cleared with the row's other stores at its
+            // end (vmcnt counts stores too: a store here would add its round trip to the wait
+            // before the state loads)
             const uint32_t carry = kp<const uint32_t>(g, 1)[row0 / kRow] + 1u;
+            uint32_t m = 0;
+            if (i < n) { m = marks[i]; clr = m != 0; }
+            m = wave_incl_max_u32(m);
             m = m > carry ? m : carry;
             src = decode_source(m - 1u, gf[1], kp<const Rec>(g, 3), &rc);
             rec_anc = gf[0];
@@ -985,6 +989,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             K1_ST(st.zs + i, zs);
             if (gath || w != w_in || w != w) K1_ST(st.w + i, w);
         }
+        if (clr) kp<uint32_t>(kl2(KOFF(gv.marks)), 0)[i] = 0;
         {
             // v_max_f32 returns the other operand for a NaN: NaN coordinates are skipped
             const float xf = (float)x, yf = (float)y;
