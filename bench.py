@@ -295,9 +295,16 @@ def main():
         # one global filter of n * world particles, sharded over the ranks: RCCL all_gathers
         # of the statistics / totals / counts and an all_to_all_v of the migrating particles
         import eslam_dist
+        f = None
         if args.comm == "rccl":
-            f = eslam_dist.RcclShardedGpuFilter(cfg, n * world, rank, world, device=local_rank)
-        else:
+            try:
+                f = eslam_dist.RcclShardedGpuFilter(cfg, n * world, rank, world, device=local_rank)
+            except Exception as e:       # joining the library's communicator failed (on every rank:
+                # ncclCommInitRank is collective): the same exchanges through torch.distributed
+                sys.stderr.write(f"bench.py: the library's RCCL communicator failed ({e}); "
+                                 "using torch.distributed exchanges\n")
+                args.comm = "torch (library RCCL failed)"
+        if f is None:
             comm = eslam_dist.TorchComm(device_memory=True, device=local_rank)
             f = eslam_dist.ShardedGpuFilter(cfg, n * world, comm, device=local_rank)
         assert f.n_local == n, (f.n_local, n)
