@@ -47,8 +47,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--particles", type=int, default=None,
-                    help="particles per GPU (default: configs[2]'s 4M on one GPU; configs[3]'s 2M per GPU "
-                         "-- 16M global at 8 GPUs -- on several)")
+                    help="particles per GPU (default: configs[2]'s 4M on any number of GPUs -- weak scaling "
+                         "keeps the one-GPU line's per-GPU work; configs[3]'s 16M over 8 GPUs is 2097152)")
     ap.add_argument("--map-cells", type=int, default=1000)
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
     ap.add_argument("--local-maps", action="store_true",
@@ -113,7 +113,9 @@ def workload_name(n, world, rough, local_maps=False):
         return "configs[3]"
     if n == CONFIG3_GLOBAL // 8:
         return "configs[3]'s 2M-per-GPU shard, weak-scaled to %d GPUs" % world
-    return "configs[2] per GPU, weak-scaled" if n == 4 * 1024 * 1024 else "custom size, weak-scaled"
+    if n == 4 * 1024 * 1024:
+        return "configs[2]'s 4M per GPU, weak-scaled to %d GPUs (%dM global)" % (world, 4 * world)
+    return "custom size, weak-scaled"
 
 
 def host_cpu():
@@ -251,7 +253,7 @@ def main():
         if args.local_maps:
             args.particles = CONFIG4_GLOBAL // 8
         else:
-            args.particles = 4 * 1024 * 1024 if args.gpus == 1 else CONFIG3_GLOBAL // 8
+            args.particles = 4 * 1024 * 1024
     # stdout carries exactly one JSON line: native libraries (RCCL prints a version banner
     # when a communicator is created) write to stderr until the result is printed
     sys.stdout.flush()
