@@ -30,3 +30,14 @@ def test_world_size_mismatch_fails():
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert r.stdout.strip() == ""
     assert "--gpus 2 but WORLD_SIZE=3" in r.stderr
+
+
+def test_multi_gpu_default_is_weak_scaling():
+    """--gpus N keeps the one-GPU line's per-GPU work (configs[2]'s 4M particles per rank);
+    configs[3] (16M over 8 GPUs) is named when asked for explicitly."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert "weak-scaled to 8 GPUs (32M global)" in bench.workload_name(4 * 1024 * 1024, 8, False)
+    assert bench.workload_name(4 * 1024 * 1024, 1, False) == "configs[2]"
+    assert bench.workload_name(2 * 1024 * 1024, 8, False) == "configs[3]"
+    assert bench.workload_name(262144, 1, False) == "configs[1]"
