@@ -1636,7 +1636,7 @@ static int exchange_tail(eslam_ctx* ctx, uint64_t epoch, PlanParams& pp, uint64_
 
 static int run_update_tail_multi(eslam_ctx* ctx, uint32_t mode, bool timed)
 {
-    const int G = ctx->comm.nranks, me = ctx->comm.rank;
+    const int G = ctx->comm.nranks;
     int rc = comm_allgather(ctx, ctx->shards, ctx->recs, sizeof(Shard) * kNShard);
     if (rc) return rc;
     FinParams fp = fin_params(ctx, mode);
