@@ -204,7 +204,9 @@ int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p);
  * set, the per-particle maps, the RNG and the last update's records stay.  The weight scale
  * of the next update is then set from the largest weight, as eslam_gpu_upload_particles does,
  * so an edit through this call and a download / edit / upload of the whole set lead to the
- * same particles bit for bit.                                                               */
+ * same particles bit for bit.  On a sharded filter the call is collective, like the upload:
+ * every rank makes it at the same point (count may be 0, and any field may be NULL), and
+ * the ranks agree on the weight scale of the next update whichever of them wrote weights. */
 int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p);
 
 /* ---- per-particle local maps (useSharedMap = false) -----------------
@@ -363,7 +365,13 @@ typedef struct eslam_comm {
  * the hot path (step/project/update/sync), init, upload/download of the local shard,
  * weights sum / normalise / resample, the best particle (global index), the centroid, the
  * hash respawn and per-particle maps, each equal to one GPU bit for bit.  comm == NULL
- * returns the context to one GPU.                                                      */
+ * returns the context to one GPU.
+ * Calls on a sharded filter follow SPMD order: every rank makes the same sequence of
+ * calls that update, write, normalise, resample or reduce (they run collectives).  The
+ * rank-local getters (download, records, particle maps, RNG state, hash poses) may be
+ * called by any subset of ranks: the only collective they can run is the previous
+ * update's deferred exchange, which every rank completes exactly once -- in a getter, in
+ * its next collective call or in eslam_gpu_destroy -- so the ranks stay matched.       */
 int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase);
 
 /* ---- multi-GPU over RCCL, driven from the library (no callback into the host language) --

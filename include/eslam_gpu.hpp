@@ -787,10 +787,21 @@ public:
         if (id.size() != ESLAM_RCCL_ID_BYTES || shardGbase.size() != (size_t)nranks + 1)
             throw std::runtime_error("setCommRccl: bad id or shard table");
         check(ctx_, eslam_gpu_set_comm_rccl(ctx_, nranks, rank, id.data(), nGlobal, shardGbase.data()));
+        sharded_ = nranks > 0;
     }
+    // the same with caller-supplied collectives (eslam_gpu_set_comm); comm == nullptr: one GPU
+    void setComm(const eslam_comm* comm, uint64_t nGlobal, const std::vector<uint64_t>& shardGbase)
+    {
+        check(ctx_, eslam_gpu_set_comm(ctx_, comm, nGlobal, comm ? shardGbase.data() : nullptr));
+        sharded_ = comm != nullptr;
+    }
+    bool sharded() const { return sharded_; }
 
     // write the edits made to the getParticles() vector back to the device (a no-op without
-    // any); every call above that uses the particles on the device runs it first
+    // any); every call above that uses the particles on the device runs it first.  On a
+    // sharded filter the write-back is collective (eslam_gpu_write_particles): a rank holding
+    // a view writes back even without edits, so the ranks stay matched as long as they call
+    // getParticles() at the same points (SPMD order, include/eslam_gpu.h)
     void flush() const
     {
         if (!view_valid_) return;
@@ -808,7 +819,10 @@ public:
                 shadow_[i] = h;
             }
         }
-        if (lo >= hi) return;
+        if (lo >= hi) {
+            if (!sharded()) return;
+            lo = hi = 0;
+        }
         const size_t n = hi - lo;
         std::vector<double> x(n), y(n), th(n), z(n), zs(n), w(n), mp(n);
         std::vector<uint8_t> fl(n), nc(n);
@@ -881,6 +895,7 @@ private:
     mutable std::vector<Hot> shadow_;              // view_ as the device holds it
     mutable bool view_valid_ = false;
     mutable uint32_t last_m_ = 0;
+    bool sharded_ = false;
 };
 
 // ---------------------------------------------------------------------------------------

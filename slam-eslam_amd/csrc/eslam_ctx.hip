@@ -300,6 +300,7 @@ struct eslam_ctx {
     // per-particle maps on a sharded filter: the migrated particles' stores (StorePayload per
     // record, in the records' order) and whether a store copy on write is still owed to them
     void* sendpay = nullptr; uint64_t sendpay_cap = 0;
+    double* cent = nullptr; uint64_t cent_bytes = 0;   // sharded getCentroid's chunk records (set_comm)
     void* recvpay = nullptr; uint64_t recvpay_cap = 0;
     bool cow_pending = false;
     // a sharded update's exchange left for the next call: the segments kernel's
@@ -598,7 +599,10 @@ namespace { void rccl_release(eslam_ctx* ctx); }
 extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
 {
     if (!ctx) return;
-    ctx->xpend = false;                      // a deferred exchange is dropped (every rank drops it alike)
+    // a deferred exchange is completed first: a rank that settled it through a getter (its
+    // own all_to_all_v) is matched by the others here, so no rank is left waiting in it
+    if (ctx->xpend && !ctx->poisoned) (void)settle(ctx);
+    ctx->xpend = false;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->xstream) { (void)hipStreamSynchronize(ctx->xstream); (void)hipStreamDestroy(ctx->xstream); }
     if (ctx->ev_seg) (void)hipEventDestroy(ctx->ev_seg);
@@ -610,7 +614,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->scratch); (void)hipHostFree(ctx->scratch_host); (void)hipHostFree(ctx->fault_host);
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
-    (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay);
+    (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay); (void)hipFree(ctx->cent);
     (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
     (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -769,6 +773,20 @@ static PlanParams plan_params(eslam_ctx* ctx)
     return pp;
 }
 
+// sharded getCentroid: this rank's chunk records (padded to the largest shard), all ranks'
+// (G x that), and the tree's two ping-pong levels over the global chunks; 5 doubles a record
+static uint64_t centroid_bytes(const uint64_t* gall, int G, uint32_t J)
+{
+    const uint64_t csz = 64ull * J;
+    uint64_t maxch = 1, total = 0;
+    for (int r = 0; r < G; ++r) {
+        const uint64_t c = (gall[r + 1] - gall[r] + csz - 1) / csz;
+        maxch = c > maxch ? c : maxch;
+        total += c;
+    }
+    return (maxch + (uint64_t)G * maxch + 2 * (total ? total : 1)) * 5 * sizeof(double);
+}
+
 extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase)
 {
     if (!ctx) return ESLAM_ERR_INVALID_ARG;
@@ -809,6 +827,18 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
         HIPCHK(ctx, hipHostMalloc(&ctx->mg_host, mg::kWords * 8));
         HIPCHK(ctx, hipMemset(ctx->recs, 0, sizeof(Shard) * kNShard * kMaxRanks));
         HIPCHK(ctx, hipMemset(ctx->mg, 0, mg::kWords * 8));
+    }
+    {
+        // getCentroid's buffer (centroid_bytes): sized by the shard table, allocated here so
+        // the per-step getCentroid of a Rock task allocates nothing
+        const uint64_t need = centroid_bytes(shard_gbase, comm->nranks, dm_chunk_rows(n_global));
+        if (need > ctx->cent_bytes) {
+            (void)hipFree(ctx->cent);
+            ctx->cent = nullptr;
+            ctx->cent_bytes = 0;
+            HIPCHK(ctx, hipMalloc(&ctx->cent, need));
+            ctx->cent_bytes = need;
+        }
     }
     ctx->comm = *comm;
     ctx->sharded = true;
@@ -1292,7 +1322,9 @@ extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_
     int rc = materialize(ctx);               // the particles the caller saw: any pending gather done
     if (!rc) rc = read_ctl(ctx);
     if (rc) return rc;
-    if (!count) return ESLAM_OK;
+    // sharded: a collective (every rank calls it, count may be 0), whose weight-scale
+    // agreement runs whether or not this rank writes weights
+    if (!count && !ctx->sharded) return ESLAM_OK;
     const DevState& s = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip];
     const uint64_t b = count * 8;
     const double* src[7] = {p->x, p->y, p->orientation, p->zpos, p->zsigma, p->weight, p->mprob};
@@ -1312,7 +1344,7 @@ extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_
         HIPCHK(ctx, hipMemcpyAsync(s.flags + first, fl.data(), count, hipMemcpyHostToDevice, ctx->stream));
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if (!p->weight) return ESLAM_OK;
+    if (!p->weight && !ctx->sharded) return ESLAM_OK;
     // the weight scale of the next update, from the largest weight of the whole set exactly
     // as eslam_gpu_upload_particles computes it (NaN and negative weights skipped)
     std::vector<double> w(ctx->n);
@@ -1558,9 +1590,8 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
 }
 
 // particles per thread of the one-GPU K3: small filters take small tiles so the scan still
-// spreads over every CU (256k particles: 1024 blocks instead of 128); ESLAM_SCAN_ITEMS (1, 2,
-// 4, 8, 16) overrides, for measurements.  Exact integer tile totals: the
-// tile size never changes a result.
+// spreads over every CU (256k particles: 1024 blocks instead of 128).  Exact integer tile
+// totals: the tile size never changes a result.
 static uint32_t scan_items(uint64_t n)
 {
     // measured (round-2 A/B, profiles/r02/ab_items_256k_fused.log; bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
@@ -2286,17 +2317,17 @@ extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double
             total += nch[r];
         }
         const uint64_t rec = 5 * sizeof(double);
-        double* buf = nullptr;
-        HIPCHK(ctx, hipMalloc(&buf, (maxch + G * maxch + 2 * (total ? total : 1)) * rec));
-        double* mine = buf;
+        if (centroid_bytes(ctx->gall.data(), G, J) > ctx->cent_bytes)
+            return fail(ctx, ESLAM_ERR_HIP, "getCentroid: buffer not sized by set_comm");
+        double* mine = ctx->cent;
         double* all = mine + maxch * 5;
         double* a = all + G * maxch * 5;
         double* b = a + (total ? total : 1) * 5;
         hipError_t e = hipMemsetAsync(mine, 0, maxch * rec, ctx->stream);
         if (e == hipSuccess) e = eslam_launch_centroid_chunks(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, mine, ctx->stream);
-        if (e != hipSuccess) { (void)hipFree(buf); return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e)); }
+        if (e != hipSuccess) return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e));
         rc = comm_allgather(ctx, mine, all, maxch * rec);
-        if (rc) { (void)hipFree(buf); return rc; }
+        if (rc) return rc;
         uint64_t off = 0;
         for (int r = 0; r < G && e == hipSuccess; ++r) {
             if (nch[r]) e = hipMemcpyAsync(a + off * 5, all + (uint64_t)r * maxch * 5, nch[r] * rec, hipMemcpyDeviceToDevice,
@@ -2305,7 +2336,6 @@ extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double
         }
         if (e == hipSuccess) e = eslam_launch_centroid_tree(a, b, total, ctx->scratch, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        (void)hipFree(buf);
         if (e != hipSuccess) return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e));
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->scratch_host, ctx->scratch, 5 * 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -76,6 +76,8 @@ struct alignas(128) Ctl {
     uint64_t map_dropped;                // scan patches the last map merge could not store (full stores)
     uint64_t map_changed;                // stores the last map merge changed
     uint64_t map_copied;                 // shared stores the last map merge wrote to a free store
+    uint64_t fin_epoch;                  // fused finalize: the epoch of the launch whose finalize wrote
+                                         // this block (checked in every block's copy of it)
 };
 
 enum FinMode : uint32_t {

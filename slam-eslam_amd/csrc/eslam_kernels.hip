@@ -2010,7 +2010,24 @@ __device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word
             *s_flag = timeout ? 1u : 0u;
             if (timeout) raise_timeout(ctl, sp.fault);
         }
-        if (tid < (uint32_t)kCtlWords) s_img[tid] = atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + tid);
+        // the copy must carry this launch's epoch (ctl->fin_epoch, written by block 0 before its
+        // release): a stale line would show an older one.  The relaxed loads rely on gfx950's
+        // agent-scope loads missing this XCD's L2 for lines another XCD wrote back; should
+        // that ever not hold, the copy is retried and then reported (ESLAM_ERR_HIP), never used
+        constexpr uint32_t kEpochWord = (uint32_t)(offsetof(Ctl, fin_epoch) / 8);
+        if (!timeout) {
+            uint64_t word = 0;
+            for (int attempt = 0;; ++attempt) {
+                if (tid < (uint32_t)kCtlWords) word = atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + tid);
+                if (!__any(tid == kEpochWord && word != epoch)) break;
+                if (attempt == 64) {
+                    if (tid == 0) { *s_flag = 1u; raise_timeout(ctl, sp.fault); }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (tid < (uint32_t)kCtlWords) s_img[tid] = word;
+        }
     }
     __syncthreads();
     return *s_flag != 0u;
@@ -2204,7 +2221,10 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
             __shared__ FinLds s_fin;
             finalize_block(ff.shards, ff.nrec, ctl, ff.fp, s_fin);
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) {
+                ctl->fin_epoch = ff.epoch;       // ordered before the publication by the release
+                __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     const Ctl* cv = FUSED ? reinterpret_cast<const Ctl*>(s_img) : ctl;
@@ -2426,7 +2446,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             __shared__ FinLds s_fin;
             finalize_block(ff.shards, ff.nrec, ctl, ff.fp, s_fin);
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) {
+                ctl->fin_epoch = ff.epoch;       // ordered before the publication by the release
+                __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     // the finalize's outputs: ctl itself (k_finalize ran before this launch), or its copy in

@@ -62,6 +62,7 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_init_pose.argtypes = [vp, dp, dp]
     L.eslam_gpu_upload_particles.argtypes = [vp, C.c_uint64, C.POINTER(A.Particles)]
     L.eslam_gpu_download_particles.argtypes = [vp, C.POINTER(A.Particles)]
+    L.eslam_gpu_write_particles.argtypes = [vp, C.c_uint64, C.c_uint64, C.POINTER(A.Particles)]
     L.eslam_gpu_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
     L.eslam_gpu_set_particle_maps.argtypes = [vp, C.c_int]
     L.eslam_gpu_get_particle_map.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_float),
@@ -154,6 +155,12 @@ class GpuFilter:
         v = pa.view()
         self._check(self.L.eslam_gpu_download_particles(self.h, C.byref(v)))
         return pa
+
+    def write(self, first, pa):
+        """eslam_gpu_write_particles: particles [first, first + pa.n) take pa's fields (a
+        collective on a sharded filter: every rank calls it, pa.n may be 0)"""
+        v = pa.view()
+        self._check(self.L.eslam_gpu_write_particles(self.h, first, pa.n, C.byref(v)))
 
     def download_records(self, first=0, stride=1, count=None, max_cpoints=0):
         """eslam_gpu_download_records: particles first + k * stride as PoseParticle records

@@ -10,7 +10,8 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit")
+EDIT_GLOBAL = (0, 37)                            # edit: the particles one rank edits
 CONFIG3_STEPS = 3
 MAP_SAMPLES = 64                                 # config4: particles whose maps are compared
 
@@ -24,7 +25,7 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3", "config4", "maps", "burst"):
+    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0"):
         S.bench_config(cfg, n_global)
         if name in ("maps", "config4"):          # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
@@ -46,7 +47,7 @@ def scenario_grid(name):
         return S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
     if name == "maps":                            # the front feet stand on cells only the scans map
         return S.unmapped_beyond(S.rough_map(cells=120), 0.3)
-    return S.rough_map(cells=120) if name not in ("forced", "burst") else S.rough_map(cells=120, multi=False)
+    return S.rough_map(cells=120) if name not in ("forced", "burst", "edit", "getter0") else S.rough_map(cells=120, multi=False)
 
 
 def digest(a):
@@ -125,6 +126,28 @@ def _info(rec, key, i):
                                    float(i.uniform_reset)])
 
 
+def edit_particles(f, lo, hi):
+    """the caller edits particles through getParticles() (processMap's weights,
+    src/EmbodiedSlamFilter.cpp:183-220): global EDIT_GLOBAL, which lie on the first rank only.
+    A GPU filter writes them back with eslam_gpu_write_particles -- a collective on a sharded
+    filter, which every rank calls (the others with nothing to write); the oracle replaces its
+    shard (download, edit, upload: the same particles, documented in include/eslam_gpu.h)."""
+    g0, g1 = max(EDIT_GLOBAL[0], lo), min(EDIT_GLOBAL[1], hi)
+    pa = f.download()
+    if g1 > g0:
+        sl = slice(g0 - lo, g1 - lo)
+        pa.weight[sl] = pa.weight[sl] * 3.5 + 0.25       # above 1: the weight scale changes
+        pa.x[sl] = pa.x[sl] + 0.01
+    if hasattr(f, "write"):
+        part = A.ParticleArrays(max(g1 - g0, 0))
+        for fld in FIELDS:
+            if g1 > g0:
+                getattr(part, fld)[:] = getattr(pa, fld)[g0 - lo:g1 - lo]
+        f.write(g0 - lo if g1 > g0 else 0, part)
+    else:
+        f.upload(pa)
+
+
 def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     """f: OracleFilter or GpuFilter-like (set_map/init_gaussian/upload/step/...).
     info_fn(f) returns the eslam_update_info of the last update."""
@@ -146,6 +169,16 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     else:
         sigma = [0.1, 0.1, 0.1] if name == "forced" else [0.6, 0.6, 0.3]
         f.init_gaussian(hi - lo, [0.0, 0.0, 0.0], sigma, 0.18, 1.001)
+    if name == "getter0":
+        # forced updates back to back, then only the first rank reads its particles (a
+        # rank-local getter, which completes the last update's deferred exchange on a sharded
+        # GPU filter) and every rank closes its filter: destroy completes the exchange on the
+        # other ranks, so no rank is left waiting in it
+        for st in S.step_stream(steps):
+            f.step(st)
+        if lo == 0:
+            _snap(rec, "last", f, True)
+        return rec
     if name == "burst":
         # forced updates back to back with nothing read between them: a sharded GPU filter
         # defers each update's exchange into the next step (split weighting launch)
@@ -164,6 +197,9 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         stream = S.step_stream(steps, tilt=(name in ("natural", "maps")))
     scan = S.scan_patches() if name == "maps" else None
     for k, st in enumerate(stream):
+        if name == "edit" and k == 2:
+            edit_particles(f, lo, hi)
+            _snap(rec, "edit", f, False)
         f.step(st)
         info = info_fn(f)
         _info(rec, f"s{k}", info)

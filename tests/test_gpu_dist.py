@@ -15,11 +15,25 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("name,n_global,world", [("forced", 5000, 2), ("natural", 2500, 2), ("upload", 2000, 2),
                                                  ("upload", 700, 3), ("hash", 3000, 2), ("hash", 1500, 3),
                                                  ("maps", 3000, 2), ("maps", 1500, 3),
-                                                 ("burst", 5000, 2), ("burst", 7001, 3)])
+                                                 ("burst", 5000, 2), ("burst", 7001, 3), ("edit", 3000, 2),
+                                                 ("edit", 1500, 3)])
 def test_sharded_gpu_gloo_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, world, str(tmp_path), mem="host", timeout=400))
     assert_same(got, want, f"gpu {name} N={n_global} world={world}")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_getter_on_one_rank_then_destroy(oracle, tmp_path, world):
+    """A rank-local getter on rank 0 only after deferred updates, then every rank destroys its
+    context (include/eslam_gpu.h, SPMD order): no rank hangs in the deferred exchange, and
+    rank 0 holds the single filter's particles."""
+    want = single_oracle("getter0", 5000)
+    parts = launch("gpu", "getter0", 5000, world, str(tmp_path), mem="host", timeout=300)
+    hi = len(parts[0]["last/x"])
+    for key, v in parts[0].items():
+        assert np.array_equal(v.view(np.uint8), want[key][:hi].view(np.uint8)), key
+    assert all(not p for p in parts[1:])
 
 
 @pytest.mark.parametrize("name,n_global", [("forced", 5000), ("upload", 2000)])
