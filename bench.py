@@ -418,9 +418,11 @@ def main():
                                  BYTES_REFERENCE * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world)),
         "last_update": {"effective": info.effective, "resampled": info.resampled},
         **({"map_update": {"patches_dropped": info.map_patches_dropped, "stores_copied": info.map_stores_copied,
-                           "stores_changed": info.map_stores_changed,
+                           "stores_changed": info.map_stores_changed, "patches_covered": info.map_patches_covered,
+                           "patches_total": n * len(scan),
                            "note": "the last step's map update: scan patches full stores could not take, shared "
-                                   "stores a change copied on write, stores the merge changed and wrote back; "
+                                   "stores a change copied on write, stores the merge changed and wrote back, scan "
+                                   "patches on cells the shared grid covers (not merged, DESIGN.md 5c); "
                                    "kernel_ms.map_* time the update's phases (map_cow_ms: the stores' sharing "
                                    "classes and the free-store list); the timed steps include the stores' fill "
                                    "phase unless --warmup covers it (DESIGN.md 5c)"}} if args.local_maps else {}),

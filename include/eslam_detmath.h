@@ -1461,12 +1461,21 @@ DM_FN int32_t dm_cvt_sat_i32(double x)
  * fma(co, sx, fma(-sn, sy, bx)) * inv_scale_x with bx = x - offset_x (per particle), n likewise.
  * Returns the cell index, 0xffffffff off the grid.  The caller skips particles whose bx, by or
  * theta are not finite (no NaN reaches the conversions).                                  */
-DM_FN uint32_t dm_merge_cell(double bx, double by, double co, double sn, double sx, double sy, double inv_x,
-                             double inv_y, uint32_t width, uint32_t height)
+DM_FN uint32_t dm_merge_cell_mn(double bx, double by, double co, double sn, double sx, double sy, double inv_x,
+                                double inv_y, uint32_t width, uint32_t height, uint32_t* mo, uint32_t* no)
 {
     const int32_t m = dm_cvt_sat_i32(dm_floor(dm_fma(co, sx, dm_fma(-sn, sy, bx)) * inv_x));
     const int32_t n = dm_cvt_sat_i32(dm_floor(dm_fma(sn, sx, dm_fma(co, sy, by)) * inv_y));
+    *mo = (uint32_t)m;
+    *no = (uint32_t)n;
     return ((uint32_t)m < width && (uint32_t)n < height) ? (uint32_t)n * width + (uint32_t)m : 0xffffffffu;
+}
+/* the cell alone (the column m and row n of an on-grid cell: dm_merge_cell_mn) */
+DM_FN uint32_t dm_merge_cell(double bx, double by, double co, double sn, double sx, double sy, double inv_x,
+                             double inv_y, uint32_t width, uint32_t height)
+{
+    uint32_t m, n;
+    return dm_merge_cell_mn(bx, by, co, sn, sx, sy, inv_x, inv_y, width, height, &m, &n);
 }
 
 #endif /* ESLAM_DETMATH_H */

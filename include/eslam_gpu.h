@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 3
+#define ESLAM_ABI_VERSION 4
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -163,10 +163,13 @@ typedef struct eslam_update_info {
     /* the last eslam_gpu_map_update (per-particle maps): scan patches a particle's map could
      * not take because its store already held ESLAM_STORE_CAP patches (summed over the
      * particles); maps the merge changed while another particle shared them (copy on write:
-     * written to a free store the particle then names); maps the merge changed in all      */
+     * written to a free store the particle then names); maps the merge changed in all; scan
+     * patches that landed on cells the shared grid covers (not merged: the per-particle map
+     * holds only cells the shared grid leaves empty)                            */
     uint64_t map_patches_dropped;
     uint64_t map_stores_copied;
     uint64_t map_stores_changed;
+    uint64_t map_patches_covered;
 } eslam_update_info;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

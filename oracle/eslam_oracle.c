@@ -1898,10 +1898,10 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
         shared[i] = lo + 1 < f->n && sorted[lo + 1] == f->pm_id[i];
     }
     free(sorted);
-    uint64_t dropped = 0, changed = 0;
+    uint64_t dropped = 0, changed = 0, covered = 0;
     const int64_t n = (int64_t)f->n;
     /* particles are independent: the OpenMP threads of or_set_threads (same results) */
-#pragma omp parallel for schedule(static) num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed)
+#pragma omp parallel for schedule(static) num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed, covered)
     for (int64_t i = 0; i < n; ++i) {
         int dirty = 0;
         uint32_t* key = f->pm_key + i * OR_STORE_SLOTS;
@@ -1930,7 +1930,10 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
                 if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
                 cell = (uint32_t)fn * g->width + (uint32_t)fm;
             }
-            if (g->cell_start[cell] != g->cell_start[cell + 1]) continue;
+            if (g->cell_start[cell] != g->cell_start[cell + 1]) {
+                ++covered;          /* the shared grid covers the cell: not merged */
+                continue;
+            }
             const double var = sp[k].stdev * sp[k].stdev + zvar;
             uint32_t h = dm_store_hash(cell);
             for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
@@ -1974,6 +1977,7 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     f->info.map_patches_dropped = dropped;
     f->info.map_stores_changed = changed;
     f->info.map_stores_copied = copied;
+    f->info.map_patches_covered = covered;
     return 0;
 }
 

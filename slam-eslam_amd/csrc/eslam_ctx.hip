@@ -26,7 +26,8 @@ using namespace eslam_dev;
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
                                                    const DebugRec* d, const MapStore* store, hipStream_t stream);
 extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, uint64_t pool, hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, const GatherView* gv,
+                                              hipStream_t stream);
 extern "C" hipError_t eslam_launch_store_receive(SidRef sid, const MapStore* ms, uint64_t n, const CowScratch* cs,
                                                  const void* payloads, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
@@ -51,7 +52,7 @@ extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uin
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
                                                   const GatherView* gv, const MapStore* store, hipStream_t stream,
-                                                  const ChunkSel* sel);
+                                                  const ChunkSel* sel, double* bspill);
 extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
                                                 hipStream_t stream);
@@ -301,6 +302,7 @@ struct eslam_ctx {
     // record, in the records' order) and whether a store copy on write is still owed to them
     void* sendpay = nullptr; uint64_t sendpay_cap = 0;
     double* cent = nullptr; uint64_t cent_bytes = 0;   // sharded getCentroid's chunk records (set_comm)
+    double* bspill = nullptr; uint64_t bspill_cap = 0;  // K1's parked per-bucket sums (k1_bspill_bytes)
     void* recvpay = nullptr; uint64_t recvpay_cap = 0;
     bool cow_pending = false;
     // a sharded update's exchange left for the next call: the segments kernel's
@@ -452,6 +454,7 @@ extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ?
 
 static int materialize(eslam_ctx* ctx);
 static int store_receive(eslam_ctx* ctx);
+static GatherView gather_view(eslam_ctx* ctx);
 
 static const char* kPoisonMsg =
     "resample scan: a cross-block wait gave up (a preceding tile's total or the finalize never arrived); "
@@ -571,6 +574,7 @@ static void free_particles(eslam_ctx* ctx)
 {
     free_debug(ctx);
     (void)hipFree(ctx->store.key); (void)hipFree(ctx->store.val); (void)hipFree(ctx->store.count);
+    (void)hipFree(ctx->store.box);
     (void)hipFree(ctx->sid_mem); (void)hipFree(ctx->cow); (void)hipFree(ctx->merge_cnt);
     ctx->merge_cnt = nullptr;
     ctx->store = MapStore{};
@@ -614,7 +618,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->scratch); (void)hipHostFree(ctx->scratch_host); (void)hipHostFree(ctx->fault_host);
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
-    (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay); (void)hipFree(ctx->cent);
+    (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay); (void)hipFree(ctx->cent); (void)hipFree(ctx->bspill);
     (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
     (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -677,9 +681,10 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
         HIPCHK(ctx, hipMalloc(&ctx->store.key, pool * kStoreSlots * 4));
         HIPCHK(ctx, hipMalloc(&ctx->store.val, pool * kStoreSlots * sizeof(float2)));
         HIPCHK(ctx, hipMalloc(&ctx->store.count, pool * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->store.box, pool * sizeof(uint4)));
         HIPCHK(ctx, hipMalloc(&ctx->cow, cow_words(cap) * 4));
-        HIPCHK(ctx, hipMalloc(&ctx->merge_cnt, 3 * kMergeCounterSlots * sizeof(uint64_t)));
-        HIPCHK(ctx, hipMemset(ctx->merge_cnt, 0, 3 * kMergeCounterSlots * sizeof(uint64_t)));
+        HIPCHK(ctx, hipMalloc(&ctx->merge_cnt, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t)));
+        HIPCHK(ctx, hipMemset(ctx->merge_cnt, 0, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t)));
         HIPCHK(ctx, eslam_launch_store_init(ctx->st[0].sid, &ctx->store, cap, pool, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     }
@@ -1414,15 +1419,27 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
     mrec(ctx, 0);
-    int rc = materialize(ctx);              // may give received particles their stores
-    if (rc) return rc;
+    // one GPU: a pending resample gather runs inside the merge (MergeParams::fuse: the store
+    // classes and the merge read the particles through the marks), so the update reads and
+    // writes the particle state once.  Sharded: the gather may hand this rank particles whose
+    // stores are still in received payloads, which get local stores first (materialize).
+    const bool fuse = !ctx->sharded;
+    const GatherView gv = gather_view(ctx);
+    if (!fuse) {
+        const int rc = materialize(ctx);
+        if (rc) return rc;
+    }
     mrec(ctx, 1);
     const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
     const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
-    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, fuse ? &gv : nullptr, ctx->stream));
     mrec(ctx, 2);
     MergeParams mp;
     memset(&mp, 0, sizeof(mp));
+    mp.gv = gv;
+    mp.gbase = ctx->gbase;
+    mp.fuse = fuse ? 1u : 0u;
+    mp.aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
     mp.cnt = ctx->merge_cnt;
     mp.ref = cs.ref;
     mp.frees = cs.frees;
@@ -1431,6 +1448,9 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     for (uint32_t k = 0; k < count; ++k)
         mp.sp[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
     HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->store, &mp, ctx->stream));
+    if (fuse) {
+        HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));     // the gather's buffer flip, if one ran
+    }
     mrec(ctx, 3);
     return ESLAM_OK;
 }
@@ -1505,7 +1525,7 @@ static int store_receive(eslam_ctx* ctx)
 {
     const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
     const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
-    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, nullptr, ctx->stream));
     HIPCHK(ctx, eslam_launch_store_receive(sr, &ctx->store, ctx->n, &cs, ctx->recvpay, ctx->stream));
     ctx->cow_pending = false;
     return ESLAM_OK;
@@ -2021,7 +2041,7 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     if (respawn || (records && project)) {
         const GatherView gv0 = gather_view(ctx);
         HIPCHK(ctx, eslam_launch_project_weight(1, 0, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                                ctx->shards, &gv0, nullptr, ctx->stream, nullptr));
+                                                ctx->shards, &gv0, nullptr, ctx->stream, nullptr, nullptr));
         HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));
         ctx->proj_event++;
         if (gv0.record) ctx->has_anc = true;
@@ -2046,6 +2066,12 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
         HIPCHK(ctx, eslam_launch_contact_records(ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl, &ctx->dbg, store_of(ctx),
                                                  ctx->stream));
     }
+    if (weight) {
+        // K1's parked per-bucket sums (K1Args::bspill): one slot per chunk of this context
+        const uint64_t csz = 64ull * p.J;
+        const int rc = grow(ctx, (void**)&ctx->bspill, &ctx->bspill_cap, k1_bspill_bytes((ctx->n + csz - 1) / csz), false);
+        if (rc) return rc;
+    }
     rec(ctx, 0);
     const GatherView gv = gather_view(ctx);
     ChunkSel sel;
@@ -2055,7 +2081,7 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
         sel.cdev = ctx->mg + mg::kChunks;
     }
     HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p, ctx->ctl,
-                                            ctx->shards, &gv, store_of(ctx), ctx->stream, split ? &sel : nullptr));
+                                            ctx->shards, &gv, store_of(ctx), ctx->stream, split ? &sel : nullptr, ctx->bspill));
     if (split) {
         // the previous update's exchange (its host wait overlaps the launch above), then the
         // chunks that needed its records.  A failure here leaves a half-weighted step: the
@@ -2085,7 +2111,7 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
             // through the gather view taken now, not the one of the first launch
             const GatherView gve = gather_view(ctx);
             HIPCHK(ctx, eslam_launch_project_weight(project, weight, (int)ctx->maxp, ctx->st[0], ctx->st[1], &ctx->map, &p,
-                                                    ctx->ctl, ctx->shards, &gve, store_of(ctx), ctx->stream, &sel));
+                                                    ctx->ctl, ctx->shards, &gve, store_of(ctx), ctx->stream, &sel, ctx->bspill));
         }
     }
     rec(ctx, 1);
@@ -2170,6 +2196,7 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         info->update_count = c.update_count;
         info->map_patches_dropped = c.map_dropped;
         info->map_stores_copied = c.map_copied;
+        info->map_patches_covered = c.map_covered;
         info->map_stores_changed = c.map_changed;
     }
     if (ctx->timing && ctx->ring_steps) {

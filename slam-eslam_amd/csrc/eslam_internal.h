@@ -76,6 +76,7 @@ struct alignas(128) Ctl {
     uint64_t map_dropped;                // scan patches the last map merge could not store (full stores)
     uint64_t map_changed;                // stores the last map merge changed
     uint64_t map_copied;                 // shared stores the last map merge wrote to a free store
+    uint64_t map_covered;                // scan patches the last map merge saw on cells the shared grid covers
     uint64_t fin_epoch;                  // fused finalize: the epoch of the launch whose finalize wrote
                                          // this block (checked in every block's copy of it)
 };
@@ -112,6 +113,7 @@ constexpr uint32_t kStoreFree = 0xffffffffu;
 constexpr uint32_t kSidRecord = 0x80000000u;
 struct alignas(8) StorePayload {
     uint32_t count, pad;
+    uint32_t box[4];                     // MapStore::box
     uint32_t key[kStoreCap];
     float2 val[kStoreCap];
 };
@@ -120,7 +122,13 @@ struct MapStore {
     uint32_t* key;                       // store_pool(cap) stores x kStoreSlots
     float2* val;                         // store_pool(cap) stores x kStoreSlots: {mean, stdev}
     uint32_t* count;                     // patches per store
+    // per store: the bounding box {m0, m1, n0, n1} (inclusive cell columns m and rows n) of
+    // its cells, a superset kept by the inserts (empty: m0 > m1).  A cell outside it is not in
+    // the store, so the map merge and K1's lookups skip the keys (no membership test, no key
+    // fetch) for the cells a robot has moved past: acceleration only, no result depends on it
+    uint4* box;
 };
+constexpr uint32_t kBoxEmptyLo = 0xffffffffu;
 
 // K1 reads the first 64 bytes (the lookup header) with one scalar load per lookup
 struct MapView {
@@ -211,7 +219,12 @@ struct K1Args {
     Shard* shards;
     MapStore store;                      // per-particle maps (the DELTA instantiations only)
     ChunkSel sel;                        // the chunks this launch processes
+    double* bspill;                      // per chunk: the per-bucket sums a wave is not in (k1_bspill_bytes)
 };
+// K1 keeps the per-bucket sums of the bucket its wave is in in registers; a wave whose
+// particles fall into several buckets parks the others per lane in its chunk's slot here
+// (DM_NBUCKETS x {A, B} x 64 lanes), so the register file holds one pair instead of six
+inline uint64_t k1_bspill_bytes(uint64_t chunks) { return chunks * DM_NBUCKETS * 2 * 64 * sizeof(double); }
 
 // one scan patch of a map update (the scan MLS of processMap, in the yaw-free body frame)
 struct ScanPatch {
@@ -219,6 +232,7 @@ struct ScanPatch {
 };
 constexpr int kMaxScanPatches = 64;
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
+constexpr uint32_t kMergeCounters = 4;
 
 // the store names of both state buffers; the copy-on-write kernels use the current one
 // (base ^ flip read on the device, so the host never waits for the commit)
@@ -266,9 +280,13 @@ struct MergeParams {
     uint64_t n;
     uint32_t m;                          // scan patches
     uint32_t pad;
-    uint64_t* cnt;                       // 3 x kMergeCounterSlots: dropped patches, changed stores, copies (zeroed)
+    uint64_t* cnt;                       // kMergeCounters x kMergeCounterSlots: dropped patches, changed
+                                         // stores, copies, patches on covered cells (zeroed)
     const uint32_t* ref;                 // CowScratch::ref of this update
     const uint32_t* frees;               // CowScratch::frees: particle i's store if it writes a shared map
+    GatherView gv;                       // fuse: a pending resample gather runs in the merge (one GPU)
+    uint64_t gbase;
+    uint32_t fuse, aux;                  // aux: carry mprob / flags (ESLAM_FLAG_NO_AUX_GATHER unset)
     ScanPatch sp[kMaxScanPatches];
 };
 

@@ -297,9 +297,15 @@ __device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint
 
 // per-particle maps: the patch of a cell the shared grid leaves empty, from the particle's
 // store (K1Args::store), with the same 3-sigma gate as a grid patch
-__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double lz, double qv, double& mean, double& stdev)
+__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, uint32_t m, uint32_t n, double lz, double qv,
+                                            double& mean, double& stdev)
 {
-    const su8 st = kl8(KOFF(store));                  // key, val, count
+    const su8 st = kl8(KOFF(store));                  // key, val, count, box
+    // outside the store's bounding box (the cells a robot has moved past): not in the store,
+    // and none of its key lines is fetched
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4 bx = kp<const u4>(st, 3)[sid];
+    if (m < bx.x || m > bx.y || n < bx.z || n > bx.w) return false;
     const gmem<const uint32_t>* key = kp<const uint32_t>(st, 0) + (uint64_t)sid * kStoreSlots;
     const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
                                       (uint64_t)sid * kStoreSlots;
@@ -307,7 +313,6 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double 
     // lower bound in the sorted keys in two memory round trips: the middle key picks the half,
     // whose 16 keys come in four 16-byte loads
     const uint32_t h0 = key[kStoreSlots / 2 - 1] < target ? kStoreSlots / 2 : 0u;
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const gmem<const u4>* kv = reinterpret_cast<const gmem<const u4>*>(key + h0);
     uint32_t pos = h0, hit = 0;
 #pragma unroll
@@ -368,7 +373,7 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     if constexpr (DELTA) {
         if (!in_grid || (in_win && wc.count == 1)) return false;
-        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, lz, qv, mean, stdev);
+        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
     } else {
         if (!in_grid || (in_win && wc.count <= 1)) return false;
     }
@@ -384,7 +389,7 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         b = cell_start[cell];
         e = cell_start[cell + 1];
         if constexpr (DELTA) {
-            if (b == e) return store_patch(sid, (uint32_t)cell, lz, qv, mean, stdev);
+            if (b == e) return store_patch(sid, (uint32_t)cell, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
         }
     }
     for (uint32_t k = b; k < e; ++k) {
@@ -784,7 +789,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
-    uint32_t touched = 0;                // bit b: some row added to bucket b (wave-uniform)
+    uint32_t touched = 0;                // bit b: this lane took part in a walk over bucket b
     // -min x, max x, -min y, max y of the cloud, rounded to float (the window only needs a
     // box that holds the cloud; it is widened by the float rounding in bbox_keys)
     float bb[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -805,9 +810,13 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     }
     if (active) {
     const uint64_t lbase = chunk * csz;
-    double accA[DM_NBUCKETS], accB[DM_NBUCKETS];
-#pragma unroll
-    for (int b = 0; b < DM_NBUCKETS; ++b) { accA[b] = 0.0; accB[b] = 0.0; }
+    // the per-bucket sums A_b, B_b of the sum contract: the pair of the bucket the wave is in
+    // (cur_b; usually the chunk's only one) in registers, the others parked per lane in the
+    // chunk's slot of K1Args::bspill and reloaded when the wave returns to them.  Each lane's
+    // sum of bucket b sees the same additions in the same order as with a register per bucket.
+    constexpr uint32_t kNoBucket = 0xffu;
+    double curA = 0.0, curB = 0.0;
+    uint32_t cur_b = kNoBucket;
     double accSW = 0.0;
 
     for (uint32_t j = 0; j < J; ++j) {
@@ -950,21 +959,29 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             // wave walks its distinct buckets (usually one): each pass adds to one bucket's two
             // sums, chosen by a scalar branch, instead of selecting over every bucket per lane.
             // ncp <= MAXP: the buckets above MAXP stay empty
-            constexpr int kBuckets = MAXP + 1 < DM_NBUCKETS ? MAXP + 1 : DM_NBUCKETS;
             uint64_t todo = __ballot(1);
             do {
                 const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
                 const bool mine = bucket == b0;
-                touched |= 1u << b0;
-                const double a1 = mine ? am : 0.0, a2 = mine ? am2 : 0.0;
-#pragma unroll
-                for (int b = 0; b < kBuckets; ++b) {
-                    if (b0 == (uint32_t)b) {
-                        asm volatile("");           // a real scalar branch, not a select per bucket
-                        accA[b] = accA[b] + a1;
-                        accB[b] = accB[b] + a2;
+                if (b0 != cur_b) {
+                    // the wave moves to another bucket (active lanes share cur_b): park the
+                    // current pair, take b0's (a bucket this lane never entered starts at +0.0)
+                    asm volatile("");
+                    gmem<double>* sp = kp<double>(kl2(KOFF(bspill)), 0) + chunk * (DM_NBUCKETS * 128) + lane;
+                    if (cur_b != kNoBucket) {
+                        sp[cur_b * 128] = curA;
+                        sp[cur_b * 128 + 64] = curB;
                     }
+                    curA = curB = 0.0;
+                    if ((touched >> b0) & 1u) {
+                        curA = sp[b0 * 128];
+                        curB = sp[b0 * 128 + 64];
+                    }
+                    cur_b = b0;
                 }
+                touched |= 1u << b0;
+                curA = curA + (mine ? am : 0.0);
+                curB = curB + (mine ? am2 : 0.0);
                 todo &= ~__ballot(mine);
             } while (todo);
             accSW = accSW + sw;
@@ -1014,18 +1031,16 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
         // `touched` is only updated by the lanes active in a walk: lanes past n in the last row
         // keep an older set.  Lane 0 takes part in every walk (a row runs only if row0 < n), so
         // its set is complete, and read as a scalar the branch below is wave-uniform.
-        touched = (uint32_t)__builtin_amdgcn_readlane((int)touched, 0);
-        if (__builtin_popcount(touched) <= 1) {
+        const uint32_t touched0 = (uint32_t)__builtin_amdgcn_readlane((int)touched, 0);
+        if (__builtin_popcount(touched0) <= 1) {
             // the usual wave: every row's particles in one bucket b0, so the totals of the
-            // other buckets are +0.0 (nothing was added to them).  The butterfly runs over
-            // A_b0, B_b0 and SW only (transposed at distances 32 and 16: total k ends in lanes
-            // 16k..16k+15), the same pairwise additions, and lane 4q + c picks total q.
-            const uint32_t b0 = touched ? (uint32_t)__builtin_ctz(touched) : 0u;
-            double w4[4] = {0.0, 0.0, accSW, 0.0};
-#pragma unroll
-            for (int b = 0; b < DM_NBUCKETS; ++b) {
-                if (b0 == (uint32_t)b) { w4[0] = accA[b]; w4[1] = accB[b]; }
-            }
+            // other buckets are +0.0 (nothing was added to them) and every lane's register
+            // pair holds its sums of b0 (a lane that never took part holds +0.0).  The
+            // butterfly runs over A_b0, B_b0 and SW only (transposed at distances 32 and 16:
+            // total k ends in lanes 16k..16k+15), the same pairwise additions, and lane 4q + c
+            // picks total q.
+            const uint32_t b0 = touched0 ? (uint32_t)__builtin_ctz(touched0) : 0u;
+            double w4[4] = {curA, curB, accSW, 0.0};
             transpose_add<32, 2>(w4, lane);
             transpose_add<16, 1>(w4, lane);
             double u = w4[0];
@@ -1042,10 +1057,20 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             const double tA = lane_value(u, 0), tB = lane_value(u, 16), tS = lane_value(u, 32);
             t = q == b0 ? tA : (q == DM_NBUCKETS + b0 ? tB : (q == kQ - 1 ? tS : 0.0));
         } else {
+            // several buckets: each lane's sums of bucket k are its register pair (k == cur_b),
+            // its parked pair (a bucket it left), or +0.0 (a bucket it never entered: lanes
+            // past n in the chunk's last row miss that row's walks)
+            const gmem<const double>* sp = kp<const double>(kl2(KOFF(bspill)), 0) + chunk * (DM_NBUCKETS * 128) + lane;
             double v[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                v[k] = k < DM_NBUCKETS ? accA[k] : (k < 2 * DM_NBUCKETS ? accB[k - DM_NBUCKETS] : (k == kQ - 1 ? accSW : 0.0));
+            for (int k = 0; k < 16; ++k) {
+                v[k] = k == kQ - 1 ? accSW : 0.0;
+                if (k < 2 * DM_NBUCKETS) {
+                    const uint32_t b = (uint32_t)(k < DM_NBUCKETS ? k : k - DM_NBUCKETS);
+                    if (b == cur_b) v[k] = k < DM_NBUCKETS ? curA : curB;
+                    else if ((touched >> b) & 1u) v[k] = sp[b * 128 + (k < DM_NBUCKETS ? 0 : 64)];
+                }
+            }
             transpose_add<32, 8>(v, lane);
             transpose_add<16, 4>(v, lane);
             transpose_add<8, 2>(v, lane);
@@ -1315,6 +1340,7 @@ __global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ si
     if (i >= pool) return;
     if (i < n) sid[i] = (uint32_t)i;
     ms.count[i] = 0;
+    ms.box[i] = make_uint4(kBoxEmptyLo, 0u, kBoxEmptyLo, 0u);
     for (uint32_t t = 0; t < kStoreSlots; ++t) ms.key[i * kStoreSlots + t] = kStoreFree;
 }
 
@@ -1326,12 +1352,25 @@ __device__ __forceinline__ uint32_t* cur_sid(const SidRef& r) { return (r.ctl->b
 // raises ref to 2 with a plain store when the run is longer than one (no atomic: as sharing
 // grows, long runs span many waves and one hot atomic per wave serialised at 0.6 ms per 8M),
 // and adds 1 atomically otherwise.  Any interleaving ends at the right class.
-__global__ void __launch_bounds__(kBlock) k_store_ref(SidRef sr, uint64_t n, uint32_t* __restrict__ ref)
+__global__ void __launch_bounds__(kBlock) k_store_ref(SidRef sr, uint64_t n, uint32_t* __restrict__ ref, GatherView gv,
+                                                     uint32_t fuse)
 {
-    const uint32_t* sid = cur_sid(sr);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t s = i < n ? sid[i] : kStoreFree;
+    uint32_t s;
+    if (fuse && sr.ctl->gather) {
+        // a pending resample gather that the map merge runs (MergeParams::fuse): output i will
+        // name its ancestor's store (the marks expanded as in K1, state[base] read)
+        const uint32_t carry = gv.row_first[(i & ~(uint64_t)(kRow - 1)) / kRow] + 1u;
+        uint32_t mk = i < n ? gv.marks[i] : 0u;
+        mk = wave_incl_max_u32(mk);
+        const uint32_t src = (mk > carry ? mk : carry) - 1u;
+        const uint32_t* sin = sr.ctl->base ? sr.s1 : sr.s0;
+        s = i < n ? sin[src] : kStoreFree;
+    } else {
+        const uint32_t* sid = cur_sid(sr);
+        s = i < n ? sid[i] : kStoreFree;
+    }
     const uint32_t prev = (uint32_t)__shfl_up((int)s, 1, 64);
     const bool head = lane == 0 || prev != s;
     const uint64_t heads = __ballot(head);
@@ -1413,7 +1452,10 @@ __global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restric
         const StorePayload& q = pay[sid[dups[j]] & ~kSidRecord];
         ms.key[(uint64_t)to * kStoreSlots + slot] = q.key[slot];
         ms.val[(uint64_t)to * kStoreSlots + slot] = q.val[slot];
-        if (slot == 0) ms.count[to] = q.count;
+        if (slot == 0) {
+            ms.count[to] = q.count;
+            ms.box[to] = make_uint4(q.box[0], q.box[1], q.box[2], q.box[3]);
+        }
     }
 }
 
@@ -1450,10 +1492,32 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint64_t i = (uint64_t)blockIdx.x * kMergeBlock + tid;
     const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
+    // output i reads its ancestor src in state[base] (the marks expanded as in K1) and the
+    // merge writes the whole particle, its store name included, to st = state[base ^ 1]
+    const bool gath = mp.fuse && ctl->gather;
+    const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
+    uint32_t src = (uint32_t)i;
+    if (gath) {
+        const uint32_t carry = mp.gv.row_first[(i & ~(uint64_t)(kRow - 1)) / kRow] + 1u;
+        uint32_t mk = i < mp.n ? mp.gv.marks[i] : 0u;
+        const bool clr = mk != 0u;
+        mk = wave_incl_max_u32(mk);
+        src = (mk > carry ? mk : carry) - 1u;
+        if (i < mp.n) {
+            st.w[i] = in.w[src];
+            if (mp.aux) {
+                st.mprob[i] = in.mprob[src];
+                st.flags[i] = in.flags[src];
+            }
+            if (mp.gv.record) mp.gv.anc[i] = (uint32_t)(mp.gbase + src);
+            if (clr) mp.gv.marks[i] = 0u;
+        }
+    }
     bool dirty = false, moved = false;
-    uint32_t dropped = 0;
+    uint32_t dropped = 0, covered = 0;
     if (i < mp.n) {
-        const uint32_t sid = st.sid[i];
+        const uint32_t sid = in.sid[src];
         uint32_t key[kStoreCap];
         {
             const uint4* kp = reinterpret_cast<const uint4*>(ms.key + (uint64_t)sid * kStoreSlots);
@@ -1464,8 +1528,12 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
             }
         }
         uint32_t count = ms.count[sid];
+        uint4 box = ms.box[sid];             // the stored cells' bounding box (MapStore::box)
         const float2* sv = ms.val + (uint64_t)sid * kStoreSlots;
-        const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i];
+        const double x = in.x[src], y = in.y[src], th = in.th[src], z = in.z[src], zs = in.zs[src];
+        if (gath) {
+            st.x[i] = x; st.y[i] = y; st.th[i] = th; st.z[i] = z; st.zs[i] = zs;
+        }
         double sn, co;
         dm_sincos(th, &sn, &co);
         const double zvar = zs * zs;
@@ -1491,6 +1559,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
         };
         for (uint32_t k0 = 0; k0 < mp.m; k0 += kMergeGroup) {
             uint32_t cellq[kMergeGroup], occw[kMergeGroup];
+            uint32_t inbox = 0;              // bit q: the cell lies in the store's bounding box
 #pragma unroll
             for (uint32_t q = 0; q < kMergeGroup; ++q) {
                 cellq[q] = 0xffffffffu;
@@ -1498,10 +1567,10 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 const uint32_t k = k0 + q;
                 if (k >= mp.m) continue;         // uniform
                 const ScanPatch sp = mp.sp[k];
-                uint32_t cell;
+                uint32_t cell, cm, cn;
                 if (map.g2l_identity) {
-                    cell = dm_merge_cell(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
-                                         map.height_cells);
+                    cell = dm_merge_cell_mn(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
+                                            map.height_cells, &cm, &cn);
                     cell = placed ? cell : 0xffffffffu;
                 } else {
                     const double wx = (co * sp.x + (-sn) * sp.y) + x;
@@ -1514,26 +1583,39 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
                     const bool in = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
                     cell = in ? (uint32_t)fn * map.width + (uint32_t)fm : 0xffffffffu;
+                    cm = in ? (uint32_t)fm : 0u;
+                    cn = in ? (uint32_t)fn : 0u;
                 }
+                inbox |= (cm >= box.x && cm <= box.y && cn >= box.z && cn <= box.w) ? (1u << q) : 0u;
                 cellq[q] = cell;
                 occw[q] = map.occ[(cell == 0xffffffffu ? 0u : cell) >> 5];    // branch-free: always in range
             }
             uint32_t open = 0;               // bit q: patch k0 + q lands on a cell the shared grid leaves empty
+            uint32_t covd = 0;               // bit q: ... on a cell the shared grid covers (not merged)
 #pragma unroll
-            for (uint32_t q = 0; q < kMergeGroup; ++q)
-                open |= (cellq[q] != 0xffffffffu && !((occw[q] >> (cellq[q] & 31u)) & 1u)) ? (1u << q) : 0u;
+            for (uint32_t q = 0; q < kMergeGroup; ++q) {
+                const bool on = cellq[q] != 0xffffffffu, occ = (occw[q] >> (cellq[q] & 31u)) & 1u;
+                open |= (on && !occ) ? (1u << q) : 0u;
+                covd |= (on && occ) ? (1u << q) : 0u;
+            }
+            covered += (uint32_t)__builtin_popcount(covd);
 #pragma unroll
             for (uint32_t q = 0; q < kMergeGroup; ++q) {
                 if (!((open >> q) & 1u)) continue;
                 const uint32_t target = cellq[q] + 1u;
                 // membership as a min-tree of key ^ target (independent VALU ops; a compare
-                // chain through the scalar mask serialises on the VALU -> SALU latency)
-                uint32_t d[kStoreCap / 3];
+                // chain through the scalar mask serialises on the VALU -> SALU latency), only
+                // for cells inside the store's bounding box: a wave whose particles have all
+                // moved past their stored cells skips it
+                bool hit = false;
+                if ((inbox >> q) & 1u) {
+                    uint32_t d[kStoreCap / 3];
 #pragma unroll
-                for (uint32_t t = 0; t < kStoreCap / 3; ++t)
-                    d[t] = min(min(key[3 * t] ^ target, key[3 * t + 1] ^ target), key[3 * t + 2] ^ target);
-                const uint32_t d0 = min(min(d[0], d[1]), d[2]), d1 = min(min(d[3], d[4]), d[5]);
-                const bool hit = min(min(d0, d1), min(d[6], d[7])) == 0u;
+                    for (uint32_t t = 0; t < kStoreCap / 3; ++t)
+                        d[t] = min(min(key[3 * t] ^ target, key[3 * t + 1] ^ target), key[3 * t + 2] ^ target);
+                    const uint32_t d0 = min(min(d[0], d[1]), d[2]), d1 = min(min(d[3], d[4]), d[5]);
+                    hit = min(min(d0, d1), min(d[6], d[7])) == 0u;
+                }
                 if (!hit && count >= kStoreCap) { ++dropped; continue; }
                 const ScanPatch sp = mp.sp[k0 + q];
                 const double wz = sp.z + z;
@@ -1562,15 +1644,20 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                         key[t] = t > pos ? key[t - 1] : (t == pos ? target : key[t]);
                     key[0] = pos == 0 ? target : key[0];
                     ++count;
+                    const uint32_t cn = cellq[q] / map.width, cm = cellq[q] - cn * map.width;
+                    box.x = min(box.x, cm); box.y = max(box.y, cm);
+                    box.z = min(box.z, cn); box.w = max(box.w, cn);
                 }
             }
         }
+        uint32_t name = sid;                 // the store the particle names after the merge
         if (dirty) {
             uint32_t dst = sid;
             if (mp.ref[sid] > 1u) {              // another particle names the store: a free one
                 dst = mp.frees[i];
-                st.sid[i] = dst;
+                if (!gath) st.sid[i] = dst;
                 moved = true;
+                name = dst;
             }
             uint4* kp = reinterpret_cast<uint4*>(ms.key + (uint64_t)dst * kStoreSlots);
 #pragma unroll
@@ -1583,36 +1670,41 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 vp[q] = make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y));
             }
             ms.count[dst] = count;
+            ms.box[dst] = box;
         }
+        if (gath) st.sid[i] = name;
     }
     dropped = wave_sum_u32(dropped);
+    covered = wave_sum_u32(covered);
     const uint64_t dmask = __ballot(dirty), mmask = __ballot(moved);
     if (lane == 0) {                     // one address per counter slot: no single hot atomic
         const uint32_t slot_c = (uint32_t)((blockIdx.x * (kMergeBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
         if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
         if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
+        if (covered) atomicAdd((unsigned long long*)&mp.cnt[3 * kMergeCounterSlots + slot_c], (unsigned long long)covered);
     }
 }
 
 // the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads)
 __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl)
 {
-    __shared__ uint64_t s[3][kMergeCounterSlots / 64];
+    __shared__ uint64_t s[kMergeCounters][kMergeCounterSlots / 64];
     const uint32_t t = threadIdx.x;
 #pragma unroll
-    for (uint32_t g = 0; g < 3; ++g) {
+    for (uint32_t g = 0; g < kMergeCounters; ++g) {
         const uint64_t v = wave_sum_u64(cnt[g * kMergeCounterSlots + t]);
         if ((t & 63u) == 0) s[g][t >> 6] = v;
     }
     __syncthreads();
     if (t == 0) {
-        uint64_t r[3] = {0, 0, 0};
-        for (uint32_t g = 0; g < 3; ++g)
+        uint64_t r[kMergeCounters] = {0, 0, 0, 0};
+        for (uint32_t g = 0; g < kMergeCounters; ++g)
             for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) r[g] += s[g][w];
         ctl->map_dropped = r[0];
         ctl->map_changed = r[1];
         ctl->map_copied = r[2];
+        ctl->map_covered = r[3];
     }
 }
 
@@ -2685,6 +2777,8 @@ __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const
         StorePayload& q = pay[j];
         q.count = ms.count[s];
         q.pad = 0;
+        const uint4 bx = ms.box[s];
+        q.box[0] = bx.x; q.box[1] = bx.y; q.box[2] = bx.z; q.box[3] = bx.w;
         for (uint32_t t = 0; t < kStoreCap; ++t) {
             q.key[t] = ms.key[(uint64_t)s * kStoreSlots + t];
             q.val[t] = ms.val[(uint64_t)s * kStoreSlots + t];
@@ -2958,7 +3052,7 @@ static uint32_t k1_grid(uint64_t chunks) { return (uint32_t)((chunks + kWaves - 
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
                                                   const GatherView* gv, const MapStore* store, hipStream_t stream,
-                                                  const ChunkSel* sel)
+                                                  const ChunkSel* sel, double* bspill)
 {
     const uint64_t csz = 64ull * p->J;
     uint64_t chunks = (p->n + csz - 1) / csz;
@@ -2977,6 +3071,8 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
     if (store) args.store = *store;
     memset(&args.sel, 0, sizeof(args.sel));
     if (sel) args.sel = *sel;
+    args.bspill = bspill;
+    if (weight && !bspill) return hipErrorInvalidValue;
 #define ESLAM_LAUNCH(P, W, M, B, ...)                                                                   \
     hipLaunchKernelGGL((k_project_weight<P, W, M, B, ##__VA_ARGS__>), dim3(k1_grid(chunks)), dim3(kBlock), lds, \
                        stream, args)
@@ -3073,11 +3169,16 @@ static hipError_t compact(int mode, uint64_t items, const uint32_t* ref, SidRef 
 
 // the stores' reference counts and the free-store list of the pool (before a map merge or a
 // copy on write): cs.ref, cs.frees, *cs.nfree
-extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, hipStream_t stream)
+extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, const GatherView* gv,
+                                              hipStream_t stream)
 {
     hipError_t e = hipMemsetAsync(cs->ref, 0, pool * 4, stream);
     if (e != hipSuccess) return e;
-    if (n) hipLaunchKernelGGL(k_store_ref, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, n, cs->ref);
+    GatherView g;
+    memset(&g, 0, sizeof(g));
+    if (gv) g = *gv;
+    if (n) hipLaunchKernelGGL(k_store_ref, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, n, cs->ref,
+                              g, gv ? 1u : 0u);
     e = compact(0, pool, cs->ref, sid, cs->counts, cs->frees, cs->nfree, stream);
     return e != hipSuccess ? e : hipGetLastError();
 }
@@ -3102,7 +3203,7 @@ extern "C" hipError_t eslam_launch_store_receive(SidRef sid, const MapStore* ms,
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
                                              const MergeParams* mp, hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(mp->cnt, 0, 3 * kMergeCounterSlots * sizeof(uint64_t), stream);
+    hipError_t e = hipMemsetAsync(mp->cnt, 0, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t), stream);
     if (e != hipSuccess) return e;
     if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kMergeBlock - 1) / kMergeBlock)), dim3(kMergeBlock), 0,
                                   stream, s0, s1, ctl, *map, *ms, *mp);

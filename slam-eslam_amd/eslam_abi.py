@@ -161,6 +161,7 @@ class UpdateInfo(C.Structure):
         ("map_patches_dropped", C.c_uint64),
         ("map_stores_copied", C.c_uint64),
         ("map_stores_changed", C.c_uint64),
+        ("map_patches_covered", C.c_uint64),
     ]
 
     def as_dict(self):

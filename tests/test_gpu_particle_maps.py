@@ -20,7 +20,7 @@ def u32(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
 
-MAP_INFO = ("map_patches_dropped", "map_stores_copied", "map_stores_changed")
+MAP_INFO = ("map_patches_dropped", "map_stores_copied", "map_stores_changed", "map_patches_covered")
 
 
 def map_info(i):
