@@ -981,15 +981,317 @@ DM_FN void dm_sincos2pi32(uint32_t b, double* s, double* c)
     *c = dm_fma(e[1], cd, -(e[0] * sd));
 }
 
-/* Box-Muller from two 32-bit words (the project / init draw layout) */
+/* generated by tools/gen_bm_tables.py: fp32 {sin, cos} of 2 pi j / 256 (each rounded once) */
+DM_CONST float dm_bm_sc_tab32[256][2] = {
+    {0.0f, 1.0f},
+    {0.024541229009628296f, 0.99969881772995f},
+    {0.049067676067352295f, 0.9987954497337341f},
+    {0.0735645666718483f, 0.9972904324531555f},
+    {0.0980171412229538f, 0.9951847195625305f},
+    {0.12241067737340927f, 0.9924795627593994f},
+    {0.1467304676771164f, 0.9891765117645264f},
+    {0.1709618866443634f, 0.9852776527404785f},
+    {0.19509032368659973f, 0.9807852506637573f},
+    {0.21910123527050018f, 0.9757021069526672f},
+    {0.24298018217086792f, 0.9700312614440918f},
+    {0.2667127549648285f, 0.9637760519981384f},
+    {0.290284663438797f, 0.9569403529167175f},
+    {0.3136817514896393f, 0.949528157711029f},
+    {0.3368898630142212f, 0.9415440559387207f},
+    {0.3598950505256653f, 0.9329928159713745f},
+    {0.3826834261417389f, 0.9238795042037964f},
+    {0.40524131059646606f, 0.91420978307724f},
+    {0.4275550842285156f, 0.903989315032959f},
+    {0.4496113359928131f, 0.89322429895401f},
+    {0.4713967442512512f, 0.8819212913513184f},
+    {0.49289819598197937f, 0.8700869679450989f},
+    {0.5141027569770813f, 0.8577286005020142f},
+    {0.5349976420402527f, 0.8448535799980164f},
+    {0.5555702447891235f, 0.8314695954322815f},
+    {0.5758081674575806f, 0.8175848126411438f},
+    {0.5956993103027344f, 0.803207516670227f},
+    {0.6152315735816956f, 0.7883464097976685f},
+    {0.6343932747840881f, 0.7730104327201843f},
+    {0.6531728506088257f, 0.7572088241577148f},
+    {0.6715589761734009f, 0.7409511208534241f},
+    {0.6895405650138855f, 0.7242470979690552f},
+    {0.7071067690849304f, 0.7071067690849304f},
+    {0.7242470979690552f, 0.6895405650138855f},
+    {0.7409511208534241f, 0.6715589761734009f},
+    {0.7572088241577148f, 0.6531728506088257f},
+    {0.7730104327201843f, 0.6343932747840881f},
+    {0.7883464097976685f, 0.6152315735816956f},
+    {0.803207516670227f, 0.5956993103027344f},
+    {0.8175848126411438f, 0.5758081674575806f},
+    {0.8314695954322815f, 0.5555702447891235f},
+    {0.8448535799980164f, 0.5349976420402527f},
+    {0.8577286005020142f, 0.5141027569770813f},
+    {0.8700869679450989f, 0.49289819598197937f},
+    {0.8819212913513184f, 0.4713967442512512f},
+    {0.89322429895401f, 0.4496113359928131f},
+    {0.903989315032959f, 0.4275550842285156f},
+    {0.91420978307724f, 0.40524131059646606f},
+    {0.9238795042037964f, 0.3826834261417389f},
+    {0.9329928159713745f, 0.3598950505256653f},
+    {0.9415440559387207f, 0.3368898630142212f},
+    {0.949528157711029f, 0.3136817514896393f},
+    {0.9569403529167175f, 0.290284663438797f},
+    {0.9637760519981384f, 0.2667127549648285f},
+    {0.9700312614440918f, 0.24298018217086792f},
+    {0.9757021069526672f, 0.21910123527050018f},
+    {0.9807852506637573f, 0.19509032368659973f},
+    {0.9852776527404785f, 0.1709618866443634f},
+    {0.9891765117645264f, 0.1467304676771164f},
+    {0.9924795627593994f, 0.12241067737340927f},
+    {0.9951847195625305f, 0.0980171412229538f},
+    {0.9972904324531555f, 0.0735645666718483f},
+    {0.9987954497337341f, 0.049067676067352295f},
+    {0.99969881772995f, 0.024541229009628296f},
+    {1.0f, 0.0f},
+    {0.99969881772995f, -0.024541229009628296f},
+    {0.9987954497337341f, -0.049067676067352295f},
+    {0.9972904324531555f, -0.0735645666718483f},
+    {0.9951847195625305f, -0.0980171412229538f},
+    {0.9924795627593994f, -0.12241067737340927f},
+    {0.9891765117645264f, -0.1467304676771164f},
+    {0.9852776527404785f, -0.1709618866443634f},
+    {0.9807852506637573f, -0.19509032368659973f},
+    {0.9757021069526672f, -0.21910123527050018f},
+    {0.9700312614440918f, -0.24298018217086792f},
+    {0.9637760519981384f, -0.2667127549648285f},
+    {0.9569403529167175f, -0.290284663438797f},
+    {0.949528157711029f, -0.3136817514896393f},
+    {0.9415440559387207f, -0.3368898630142212f},
+    {0.9329928159713745f, -0.3598950505256653f},
+    {0.9238795042037964f, -0.3826834261417389f},
+    {0.91420978307724f, -0.40524131059646606f},
+    {0.903989315032959f, -0.4275550842285156f},
+    {0.89322429895401f, -0.4496113359928131f},
+    {0.8819212913513184f, -0.4713967442512512f},
+    {0.8700869679450989f, -0.49289819598197937f},
+    {0.8577286005020142f, -0.5141027569770813f},
+    {0.8448535799980164f, -0.5349976420402527f},
+    {0.8314695954322815f, -0.5555702447891235f},
+    {0.8175848126411438f, -0.5758081674575806f},
+    {0.803207516670227f, -0.5956993103027344f},
+    {0.7883464097976685f, -0.6152315735816956f},
+    {0.7730104327201843f, -0.6343932747840881f},
+    {0.7572088241577148f, -0.6531728506088257f},
+    {0.7409511208534241f, -0.6715589761734009f},
+    {0.7242470979690552f, -0.6895405650138855f},
+    {0.7071067690849304f, -0.7071067690849304f},
+    {0.6895405650138855f, -0.7242470979690552f},
+    {0.6715589761734009f, -0.7409511208534241f},
+    {0.6531728506088257f, -0.7572088241577148f},
+    {0.6343932747840881f, -0.7730104327201843f},
+    {0.6152315735816956f, -0.7883464097976685f},
+    {0.5956993103027344f, -0.803207516670227f},
+    {0.5758081674575806f, -0.8175848126411438f},
+    {0.5555702447891235f, -0.8314695954322815f},
+    {0.5349976420402527f, -0.8448535799980164f},
+    {0.5141027569770813f, -0.8577286005020142f},
+    {0.49289819598197937f, -0.8700869679450989f},
+    {0.4713967442512512f, -0.8819212913513184f},
+    {0.4496113359928131f, -0.89322429895401f},
+    {0.4275550842285156f, -0.903989315032959f},
+    {0.40524131059646606f, -0.91420978307724f},
+    {0.3826834261417389f, -0.9238795042037964f},
+    {0.3598950505256653f, -0.9329928159713745f},
+    {0.3368898630142212f, -0.9415440559387207f},
+    {0.3136817514896393f, -0.949528157711029f},
+    {0.290284663438797f, -0.9569403529167175f},
+    {0.2667127549648285f, -0.9637760519981384f},
+    {0.24298018217086792f, -0.9700312614440918f},
+    {0.21910123527050018f, -0.9757021069526672f},
+    {0.19509032368659973f, -0.9807852506637573f},
+    {0.1709618866443634f, -0.9852776527404785f},
+    {0.1467304676771164f, -0.9891765117645264f},
+    {0.12241067737340927f, -0.9924795627593994f},
+    {0.0980171412229538f, -0.9951847195625305f},
+    {0.0735645666718483f, -0.9972904324531555f},
+    {0.049067676067352295f, -0.9987954497337341f},
+    {0.024541229009628296f, -0.99969881772995f},
+    {0.0f, -1.0f},
+    {-0.024541229009628296f, -0.99969881772995f},
+    {-0.049067676067352295f, -0.9987954497337341f},
+    {-0.0735645666718483f, -0.9972904324531555f},
+    {-0.0980171412229538f, -0.9951847195625305f},
+    {-0.12241067737340927f, -0.9924795627593994f},
+    {-0.1467304676771164f, -0.9891765117645264f},
+    {-0.1709618866443634f, -0.9852776527404785f},
+    {-0.19509032368659973f, -0.9807852506637573f},
+    {-0.21910123527050018f, -0.9757021069526672f},
+    {-0.24298018217086792f, -0.9700312614440918f},
+    {-0.2667127549648285f, -0.9637760519981384f},
+    {-0.290284663438797f, -0.9569403529167175f},
+    {-0.3136817514896393f, -0.949528157711029f},
+    {-0.3368898630142212f, -0.9415440559387207f},
+    {-0.3598950505256653f, -0.9329928159713745f},
+    {-0.3826834261417389f, -0.9238795042037964f},
+    {-0.40524131059646606f, -0.91420978307724f},
+    {-0.4275550842285156f, -0.903989315032959f},
+    {-0.4496113359928131f, -0.89322429895401f},
+    {-0.4713967442512512f, -0.8819212913513184f},
+    {-0.49289819598197937f, -0.8700869679450989f},
+    {-0.5141027569770813f, -0.8577286005020142f},
+    {-0.5349976420402527f, -0.8448535799980164f},
+    {-0.5555702447891235f, -0.8314695954322815f},
+    {-0.5758081674575806f, -0.8175848126411438f},
+    {-0.5956993103027344f, -0.803207516670227f},
+    {-0.6152315735816956f, -0.7883464097976685f},
+    {-0.6343932747840881f, -0.7730104327201843f},
+    {-0.6531728506088257f, -0.7572088241577148f},
+    {-0.6715589761734009f, -0.7409511208534241f},
+    {-0.6895405650138855f, -0.7242470979690552f},
+    {-0.7071067690849304f, -0.7071067690849304f},
+    {-0.7242470979690552f, -0.6895405650138855f},
+    {-0.7409511208534241f, -0.6715589761734009f},
+    {-0.7572088241577148f, -0.6531728506088257f},
+    {-0.7730104327201843f, -0.6343932747840881f},
+    {-0.7883464097976685f, -0.6152315735816956f},
+    {-0.803207516670227f, -0.5956993103027344f},
+    {-0.8175848126411438f, -0.5758081674575806f},
+    {-0.8314695954322815f, -0.5555702447891235f},
+    {-0.8448535799980164f, -0.5349976420402527f},
+    {-0.8577286005020142f, -0.5141027569770813f},
+    {-0.8700869679450989f, -0.49289819598197937f},
+    {-0.8819212913513184f, -0.4713967442512512f},
+    {-0.89322429895401f, -0.4496113359928131f},
+    {-0.903989315032959f, -0.4275550842285156f},
+    {-0.91420978307724f, -0.40524131059646606f},
+    {-0.9238795042037964f, -0.3826834261417389f},
+    {-0.9329928159713745f, -0.3598950505256653f},
+    {-0.9415440559387207f, -0.3368898630142212f},
+    {-0.949528157711029f, -0.3136817514896393f},
+    {-0.9569403529167175f, -0.290284663438797f},
+    {-0.9637760519981384f, -0.2667127549648285f},
+    {-0.9700312614440918f, -0.24298018217086792f},
+    {-0.9757021069526672f, -0.21910123527050018f},
+    {-0.9807852506637573f, -0.19509032368659973f},
+    {-0.9852776527404785f, -0.1709618866443634f},
+    {-0.9891765117645264f, -0.1467304676771164f},
+    {-0.9924795627593994f, -0.12241067737340927f},
+    {-0.9951847195625305f, -0.0980171412229538f},
+    {-0.9972904324531555f, -0.0735645666718483f},
+    {-0.9987954497337341f, -0.049067676067352295f},
+    {-0.99969881772995f, -0.024541229009628296f},
+    {-1.0f, 0.0f},
+    {-0.99969881772995f, 0.024541229009628296f},
+    {-0.9987954497337341f, 0.049067676067352295f},
+    {-0.9972904324531555f, 0.0735645666718483f},
+    {-0.9951847195625305f, 0.0980171412229538f},
+    {-0.9924795627593994f, 0.12241067737340927f},
+    {-0.9891765117645264f, 0.1467304676771164f},
+    {-0.9852776527404785f, 0.1709618866443634f},
+    {-0.9807852506637573f, 0.19509032368659973f},
+    {-0.9757021069526672f, 0.21910123527050018f},
+    {-0.9700312614440918f, 0.24298018217086792f},
+    {-0.9637760519981384f, 0.2667127549648285f},
+    {-0.9569403529167175f, 0.290284663438797f},
+    {-0.949528157711029f, 0.3136817514896393f},
+    {-0.9415440559387207f, 0.3368898630142212f},
+    {-0.9329928159713745f, 0.3598950505256653f},
+    {-0.9238795042037964f, 0.3826834261417389f},
+    {-0.91420978307724f, 0.40524131059646606f},
+    {-0.903989315032959f, 0.4275550842285156f},
+    {-0.89322429895401f, 0.4496113359928131f},
+    {-0.8819212913513184f, 0.4713967442512512f},
+    {-0.8700869679450989f, 0.49289819598197937f},
+    {-0.8577286005020142f, 0.5141027569770813f},
+    {-0.8448535799980164f, 0.5349976420402527f},
+    {-0.8314695954322815f, 0.5555702447891235f},
+    {-0.8175848126411438f, 0.5758081674575806f},
+    {-0.803207516670227f, 0.5956993103027344f},
+    {-0.7883464097976685f, 0.6152315735816956f},
+    {-0.7730104327201843f, 0.6343932747840881f},
+    {-0.7572088241577148f, 0.6531728506088257f},
+    {-0.7409511208534241f, 0.6715589761734009f},
+    {-0.7242470979690552f, 0.6895405650138855f},
+    {-0.7071067690849304f, 0.7071067690849304f},
+    {-0.6895405650138855f, 0.7242470979690552f},
+    {-0.6715589761734009f, 0.7409511208534241f},
+    {-0.6531728506088257f, 0.7572088241577148f},
+    {-0.6343932747840881f, 0.7730104327201843f},
+    {-0.6152315735816956f, 0.7883464097976685f},
+    {-0.5956993103027344f, 0.803207516670227f},
+    {-0.5758081674575806f, 0.8175848126411438f},
+    {-0.5555702447891235f, 0.8314695954322815f},
+    {-0.5349976420402527f, 0.8448535799980164f},
+    {-0.5141027569770813f, 0.8577286005020142f},
+    {-0.49289819598197937f, 0.8700869679450989f},
+    {-0.4713967442512512f, 0.8819212913513184f},
+    {-0.4496113359928131f, 0.89322429895401f},
+    {-0.4275550842285156f, 0.903989315032959f},
+    {-0.40524131059646606f, 0.91420978307724f},
+    {-0.3826834261417389f, 0.9238795042037964f},
+    {-0.3598950505256653f, 0.9329928159713745f},
+    {-0.3368898630142212f, 0.9415440559387207f},
+    {-0.3136817514896393f, 0.949528157711029f},
+    {-0.290284663438797f, 0.9569403529167175f},
+    {-0.2667127549648285f, 0.9637760519981384f},
+    {-0.24298018217086792f, 0.9700312614440918f},
+    {-0.21910123527050018f, 0.9757021069526672f},
+    {-0.19509032368659973f, 0.9807852506637573f},
+    {-0.1709618866443634f, 0.9852776527404785f},
+    {-0.1467304676771164f, 0.9891765117645264f},
+    {-0.12241067737340927f, 0.9924795627593994f},
+    {-0.0980171412229538f, 0.9951847195625305f},
+    {-0.0735645666718483f, 0.9972904324531555f},
+    {-0.049067676067352295f, 0.9987954497337341f},
+    {-0.024541229009628296f, 0.99969881772995f},
+};
+#define DM_BM_DELTA_F 1.462918119976564e-09f   /* RN32(2 pi 2^-32) */
+
+DM_FN float dm_fmaf(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+/* sin and cos of 2 pi (b + 1/2) 2^-32 in fp32 (the Box-Muller angle): the angle of j = b >> 24
+ * from the fp32 table, the rest delta = (b mod 2^24 + 1/2) 2 pi 2^-32 < 2 pi / 256 by its
+ * Taylor series (sin to delta^3, cos to delta^4: remainders below 2^-33 relative), combined
+ * by the angle-sum formulas.  About 1 ulp of fp32; every operation is an IEEE fp32 add, mul or
+ * fma, so the host and the device agree bit for bit.                                       */
+DM_FN void dm_sincos2pi32f(uint32_t b, float* s, float* c)
+{
+    const float* e = dm_bm_sc_tab32[b >> 24];
+    const float d = dm_fmaf((float)(b & 0xffffffu), DM_BM_DELTA_F, 0.5f * DM_BM_DELTA_F);
+    const float z = d * d;
+    const float sd = dm_fmaf(d * z, -1.0f / 6.0f, d);
+    const float cd = dm_fmaf(z, dm_fmaf(z, 1.0f / 24.0f, -0.5f), 1.0f);
+    *s = dm_fmaf(e[0], cd, e[1] * sd);
+    *c = dm_fmaf(e[1], cd, -(e[0] * sd));
+}
+
+/* sqrt(x) correctly rounded in fp32 for a positive normal x: on the device the compiler's own
+ * correctly rounded sequence (v_sqrt_f32, then the neighbour whose square brackets x) without
+ * its tiny-argument scaling and zero/inf fix-up, which such an x never needs (the same bits:
+ * tests/test_gpu_parity.py compares it with sqrtf on the device for all 2^32 Box-Muller
+ * words); the host's sqrtf is correctly rounded.                                           */
+DM_FN float dm_sqrtf_pos(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_sqrtf(x);
+    const float dn = __uint_as_float(__float_as_uint(r) - 1u), up = __uint_as_float(__float_as_uint(r) + 1u);
+    float q = r;
+    if (__builtin_fmaf(-dn, r, x) <= 0.0f) q = dn;
+    if (__builtin_fmaf(-up, r, x) > 0.0f) q = up;
+    return q;
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+
+/* Box-Muller from two 32-bit words (the project / init draw layout): the radius
+ * sqrt(-2 log u) from the fp64 log rounded to fp32 and a correctly rounded fp32 sqrt, the
+ * angle's sin / cos in fp32; each normal is the exact fp64 product of the two fp32 factors
+ * (24 + 24 bits).  Noise draws need no more than fp32's 2^-24 relative resolution (the
+ * reference's own uniforms carry 31 bits), and fp32 arithmetic issues at twice the fp64 rate. */
 DM_FN void dm_box_muller32(uint32_t a, uint32_t b, double* z0, double* z1)
 {
-    /* u in [2^-33, 1): positive normal, so the range-restricted sqrt applies */
-    const double r = dm_sqrt_pos(-2.0 * dm_log_bm(dm_u32(a)));
-    double s, c;
-    dm_sincos2pi32(b, &s, &c);
-    *z0 = r * c;
-    *z1 = r * s;
+    /* -2 log u in [4.6e-10, 45.8] for u in [2^-33, 1): positive normal in fp32 */
+    const float r = dm_sqrtf_pos((float)(-2.0 * dm_log_bm(dm_u32(a))));
+    float s, c;
+    dm_sincos2pi32f(b, &s, &c);
+    *z0 = (double)r * (double)c;
+    *z1 = (double)r * (double)s;
 }
 
 /* RNG stream identifiers (Philox counter word 3, bits 24..31) */

@@ -2035,6 +2035,8 @@ double or_dm(int fn, double x, double y)
     case 17: dm_sincos2pi32((uint32_t)x, &s, &c); return c;
     case 18: dm_box_muller32((uint32_t)x, (uint32_t)y, &s, &c); return s;   /* z0 */
     case 19: dm_box_muller32((uint32_t)x, (uint32_t)y, &s, &c); return c;   /* z1 */
+    case 26: { float fs, fc; dm_sincos2pi32f((uint32_t)x, &fs, &fc); return fs; }
+    case 27: { float fs, fc; dm_sincos2pi32f((uint32_t)x, &fs, &fc); return fc; }
     default: return NAN;
     }
 }

@@ -3015,6 +3015,8 @@ __global__ void k_selftest_math(int fn, const double* x, const double* y, double
     case 17: dm_sincos2pi32((uint32_t)x[i], &s, &c); r = c; break;
     case 18: dm_box_muller32((uint32_t)x[i], (uint32_t)y[i], &s, &c); r = s; break;
     case 19: dm_box_muller32((uint32_t)x[i], (uint32_t)y[i], &s, &c); r = c; break;
+    case 26: { float fs, fc; dm_sincos2pi32f((uint32_t)x[i], &fs, &fc); r = fs; } break;
+    case 27: { float fs, fc; dm_sincos2pi32f((uint32_t)x[i], &fs, &fc); r = fc; } break;
     default: r = __builtin_nan("");
     }
     out[i] = r;
@@ -3027,11 +3029,8 @@ __global__ void __launch_bounds__(kBlock) k_selftest_bm_radius(unsigned long lon
     uint32_t cnt = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x; a < (1ull << 32); a += stride) {
-        const double u = dm_u32((uint32_t)a);
-        const double l = -2.0 * dm_log_bm(u);
-        const double fast = dm_sqrt_pos(l);
-        const double ref = dm_sqrt(l);
-        cnt += dm_bits(fast) != dm_bits(ref) ? 1u : 0u;
+        const float x = (float)(-2.0 * dm_log_bm(dm_u32((uint32_t)a)));
+        cnt += __float_as_uint(dm_sqrtf_pos(x)) != __float_as_uint(__builtin_sqrtf(x)) ? 1u : 0u;
     }
     cnt = wave_sum_u32(cnt);
     if ((threadIdx.x & 63u) == 0 && cnt) atomicAdd(bad, (unsigned long long)cnt);

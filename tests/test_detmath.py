@@ -224,8 +224,18 @@ def test_sincos2pi32(dm, fn, ref):
     assert worst_abs <= 3.5e-16
 
 
+@pytest.mark.parametrize("fn,ref", [(26, mp.sin), (27, mp.cos)])
+def test_sincos2pi32f(dm, fn, ref):
+    """the fp32 Box-Muller angle (dm_sincos2pi32f: fp32 table + Taylor series + angle sums)
+    against mpmath: within 1.5 fp32 ulps of 1 (the values lie in [-1, 1])"""
+    b = list(_rng().integers(0, 2 ** 32, 6000, dtype=np.uint64)) + [0, 2 ** 32 - 1, 2 ** 30, 2 ** 31, 3 * 2 ** 30, 2 ** 24 - 1]
+    worst_abs = max(abs(dm(fn, float(x)) - float(ref(2 * mp.pi * (mp.mpf(int(x)) + mp.mpf(0.5)) / 2 ** 32))) for x in b)
+    assert worst_abs <= 1.5 * 2.0 ** -24
+
+
 def test_box_muller32_normals(dm):
-    """the contract's Box-Muller pair from two words against the same formula in mpmath"""
+    """the contract's Box-Muller pair from two words against the same formula in mpmath: the
+    fp32 radius and angle (dm_box_muller32) keep each normal within 2^-22 of the radius"""
     rng = _rng()
     for a, b in zip(rng.integers(0, 2 ** 32, 2000), rng.integers(0, 2 ** 32, 2000)):
         u = (mp.mpf(int(a)) + mp.mpf(0.5)) / 2 ** 32
@@ -233,4 +243,4 @@ def test_box_muller32_normals(dm):
         r = mp.sqrt(-2 * mp.log(u))
         for fn, want in ((18, r * mp.cos(t)), (19, r * mp.sin(t))):
             got = dm(fn, float(a), float(b))
-            assert abs(got - float(want)) <= 8e-16 * max(1.0, abs(float(want))), (a, b, fn)
+            assert abs(got - float(want)) <= 2.0 ** -22 * max(1.0, float(r)), (a, b, fn)

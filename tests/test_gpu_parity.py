@@ -30,7 +30,7 @@ def factory(gpu_mod):
 @pytest.mark.parametrize("fn,lo,hi", [(0, -740, 700), (1, 1e-300, 1e300), (2, -50, 50), (3, -50, 50), (4, -8, 27),
                                       (5, 0, 1e10), (8, 0, 1.5), (9, 0, 1.9), (13, 0, 1), (14, 0, 1),
                                       (15, 2.0 ** -33, 1.0), (16, 0, 2.0 ** 32), (17, 0, 2.0 ** 32),
-                                      (18, 0, 2.0 ** 32), (19, 0, 2.0 ** 32)])
+                                      (18, 0, 2.0 ** 32), (19, 0, 2.0 ** 32), (26, 0, 2.0 ** 32), (27, 0, 2.0 ** 32)])
 def test_gpu_math_bit_identical(gpu_mod, oracle, fn, lo, hi):
     rng = np.random.default_rng(fn)
     x = rng.uniform(lo, hi, 20000) if fn != 1 else np.exp(rng.uniform(-690, 690, 20000))
@@ -46,9 +46,9 @@ def test_gpu_math_bit_identical(gpu_mod, oracle, fn, lo, hi):
 
 
 def test_box_muller_radius_all_words(gpu_mod):
-    """dm_sqrt_pos(-2 dm_log_bm(u)) == dm_sqrt(-2 dm_log_bm(u)) bit for bit on the device for
-    every one of the 2^32 uniform words: the range-restricted sqrt of the project kernel's
-    Box-Muller is correctly rounded there (the oracle uses the general one)."""
+    """dm_sqrtf_pos(x) == sqrtf(x), x = (float)(-2 dm_log_bm(u)), bit for bit on the device for
+    every one of the 2^32 uniform words: the range-restricted fp32 sqrt of the Box-Muller
+    radius is correctly rounded there (the oracle uses the C library's sqrtf)."""
     import ctypes as C
     L = gpu_mod.load_library()
     bad = C.c_uint64(1)
