@@ -83,6 +83,40 @@ def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
     assert np.mean(p.n_contact_points == 4) > (0.5 if terrain == "flat" else 0.1)
 
 
+def test_particle_maps_steady_state(gpu_mod, oracle):
+    """The bench workload run past the stores' fill phase: 45 steps move the robot 0.9 m, so
+    the scans land beyond the cells the full stores hold (the merge's bounding-box skip and
+    K1's skipped store fetches), with the call patterns around the merge's fused resample
+    gather: a step with no map update before the next step (the step gathers), two map updates
+    in a row (the second finds no gather pending), and no download in between.  Bit-exact
+    against the oracle: every step's map-update counts, then every particle and sampled maps."""
+    n = 65536
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
+    grid = S.unmapped_beyond(S.rough_map(cells=300), 0.3)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    orc.set_threads(16)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    scan = S.scan_patches()
+    for k, st in enumerate(S.step_stream(45, tilt=True)):
+        assert gpu.step(st) == orc.step(st)
+        if k % 10 == 7:
+            continue                      # no map update: the next step runs the gather
+        reps = 2 if k % 10 == 3 else 1    # a second update finds no gather pending
+        for _ in range(reps):
+            gpu.map_update(scan)
+            orc.map_update(scan)
+            assert map_info(gpu.sync()) == map_info(orc.info()), k
+    info = gpu.sync()
+    assert info.map_patches_dropped > 0 and info.map_stores_changed < n // 10   # the steady state
+    assert_bit_identical(gpu.download(), orc.download(), "local maps steady state")
+    assert np.array_equal(gpu.ancestors(), orc.ancestors())
+    assert_maps_equal(gpu, orc, [0, 1, 977, n // 3, n // 2 + 5, n - 1], "steady state")
+
+
 def test_map_update_needs_the_flag(gpu_mod):
     cfg = S.bench_config(A.default_config(), 100)
     gpu = gpu_mod.GpuFilter(cfg)
