@@ -789,7 +789,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
     uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
-    uint32_t touched = 0;                // bit b: this lane took part in a walk over bucket b
+    uint32_t touched = 0;                // bit b: the wave walked bucket b (wave-uniform)
     // -min x, max x, -min y, max y of the cloud, rounded to float (the window only needs a
     // box that holds the cloud; it is widened by the float rounding in bbox_keys)
     float bb[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -843,7 +843,11 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             src = decode_source(m - 1u, gf[1], kp<const Rec>(g, 3), &rc);
             rec_anc = gf[0];
         }
-        if (i >= n) continue;
+        // lanes past n (only in the last row of the last chunk) compute nothing but take part
+        // in the row's bucket walk, so the walk's state stays wave-uniform (scalar)
+        uint32_t bucket = kNoBucket;
+        double am = 0.0, am2 = 0.0;
+        if (i < n) {
         double x, y, th, z, zs, w, mp_in = 0.0;
         uint32_t fl_in = 0;
         if (rc) {
@@ -951,39 +955,9 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
                 floating = 1;
                 mprob = 1.0;
             }
-            const uint32_t bucket = r.ncp < DM_NBUCKETS - 1 ? r.ncp : DM_NBUCKETS - 1;
-            const double am = w * mprob;
-            const double am2 = am * am;
-            // per bucket b the lane adds am if it holds b, else +0.0 (the oracle's canonical
-            // per-bucket sums add +0.0 for the other buckets' particles: the same bits).  The
-            // wave walks its distinct buckets (usually one): each pass adds to one bucket's two
-            // sums, chosen by a scalar branch, instead of selecting over every bucket per lane.
-            // ncp <= MAXP: the buckets above MAXP stay empty
-            uint64_t todo = __ballot(1);
-            do {
-                const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
-                const bool mine = bucket == b0;
-                if (b0 != cur_b) {
-                    // the wave moves to another bucket (active lanes share cur_b): park the
-                    // current pair, take b0's (a bucket this lane never entered starts at +0.0)
-                    asm volatile("");
-                    gmem<double>* sp = kp<double>(kl2(KOFF(bspill)), 0) + chunk * (DM_NBUCKETS * 128) + lane;
-                    if (cur_b != kNoBucket) {
-                        sp[cur_b * 128] = curA;
-                        sp[cur_b * 128 + 64] = curB;
-                    }
-                    curA = curB = 0.0;
-                    if ((touched >> b0) & 1u) {
-                        curA = sp[b0 * 128];
-                        curB = sp[b0 * 128 + 64];
-                    }
-                    cur_b = b0;
-                }
-                touched |= 1u << b0;
-                curA = curA + (mine ? am : 0.0);
-                curB = curB + (mine ? am2 : 0.0);
-                todo &= ~__ballot(mine);
-            } while (todo);
+            bucket = r.ncp < DM_NBUCKETS - 1 ? r.ncp : DM_NBUCKETS - 1;
+            am = w * mprob;
+            am2 = am * am;
             accSW = accSW + sw;
             flags = (r.ncp & 0x7fu) | (floating << 7);
         } else {
@@ -1015,6 +989,39 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             bb[2] = __builtin_fmaxf(bb[2], -yf);
             bb[3] = __builtin_fmaxf(bb[3], yf);
         }
+        }
+        if (WEIGHT) {
+            // per bucket b the lane adds am if it holds b, else +0.0 (the oracle's canonical
+            // per-bucket sums add +0.0 for the other buckets' particles: the same bits).  The
+            // wave walks its distinct buckets (usually one): each pass adds to one bucket's two
+            // sums, chosen by a scalar branch, instead of selecting over every bucket per lane.
+            // ncp <= MAXP: the buckets above MAXP stay empty.  The whole wave walks (lanes
+            // without a particle add +0.0), so cur_b and touched are scalars.
+            uint64_t todo = __ballot(bucket != kNoBucket);
+            while (todo) {
+                const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
+                const bool mine = bucket == b0;
+                if (b0 != cur_b) {
+                    // the wave moves to another bucket: park the current pair, take b0's (a
+                    // bucket the wave never walked starts at +0.0)
+                    gmem<double>* sp = kp<double>(kl2(KOFF(bspill)), 0) + chunk * (DM_NBUCKETS * 128) + lane;
+                    if (cur_b != kNoBucket) {
+                        sp[cur_b * 128] = curA;
+                        sp[cur_b * 128 + 64] = curB;
+                    }
+                    curA = curB = 0.0;
+                    if ((touched >> b0) & 1u) {
+                        curA = sp[b0 * 128];
+                        curB = sp[b0 * 128 + 64];
+                    }
+                    cur_b = b0;
+                }
+                touched |= 1u << b0;
+                curA = curA + (mine ? am : 0.0);
+                curB = curB + (mine ? am2 : 0.0);
+                todo &= ~__ballot(mine);
+            }
+        }
     }
 
     if (WEIGHT) {
@@ -1031,11 +1038,11 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
         // `touched` is only updated by the lanes active in a walk: lanes past n in the last row
         // keep an older set.  Lane 0 takes part in every walk (a row runs only if row0 < n), so
         // its set is complete, and read as a scalar the branch below is wave-uniform.
-        const uint32_t touched0 = (uint32_t)__builtin_amdgcn_readlane((int)touched, 0);
+        const uint32_t touched0 = touched;
         if (__builtin_popcount(touched0) <= 1) {
             // the usual wave: every row's particles in one bucket b0, so the totals of the
-            // other buckets are +0.0 (nothing was added to them) and every lane's register
-            // pair holds its sums of b0 (a lane that never took part holds +0.0).  The
+            // other buckets are +0.0 (nothing was added to them) and the register pair holds
+            // the sums of b0.  The
             // butterfly runs over A_b0, B_b0 and SW only (transposed at distances 32 and 16:
             // total k ends in lanes 16k..16k+15), the same pairwise additions, and lane 4q + c
             // picks total q.
@@ -1057,9 +1064,8 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             const double tA = lane_value(u, 0), tB = lane_value(u, 16), tS = lane_value(u, 32);
             t = q == b0 ? tA : (q == DM_NBUCKETS + b0 ? tB : (q == kQ - 1 ? tS : 0.0));
         } else {
-            // several buckets: each lane's sums of bucket k are its register pair (k == cur_b),
-            // its parked pair (a bucket it left), or +0.0 (a bucket it never entered: lanes
-            // past n in the chunk's last row miss that row's walks)
+            // several buckets: the sums of bucket k are the register pair (k == cur_b), the
+            // parked pair (a bucket the wave left), or +0.0 (a bucket it never walked)
             const gmem<const double>* sp = kp<const double>(kl2(KOFF(bspill)), 0) + chunk * (DM_NBUCKETS * 128) + lane;
             double v[16];
 #pragma unroll
