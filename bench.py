@@ -340,6 +340,7 @@ def main():
     t0 = time.perf_counter()
     for st in stream[args.warmup:args.warmup + args.steps]:
         f_step(st)
+    t_enq = time.perf_counter()             # the host has queued every launch (nothing waits on the GPU)
     info = f.sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -407,6 +408,7 @@ def main():
                      "algorithmic_bytes_per_particle": round(dom_bytes, 2),
                      "avg_launch_ms": round(dom_ms, 5)},
         "kernel_ms": {k: round(v, 5) for k, v in kt.items()},
+        "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
         "kernel_ms_note": "HIP events around every launch on the context stream, over a second pass of "
                           "the same K steps (ms_per_step with events: %.4f); single-GPU update steps fold the finalize "
                           "into k_normalize_segments (block 0), so finalize_ms times an empty region there"

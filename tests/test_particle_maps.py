@@ -80,3 +80,29 @@ def test_fuse_and_capacity(oracle):
     f.map_update(big)
     c3, _, _ = f.particle_map(5)
     assert len(c3) == 24                                # at most 24 patches per particle
+
+
+def test_covered_cells_are_counted(oracle):
+    """Scan patches on cells the shared grid covers are not merged and are
+    counted (map_patches_covered): a scan reaching back over the mapped region x < 0.3."""
+    f, grid = setup(n=200)
+    back = S.scan_patches(nx=8, ny=6, x0=-0.6, x1=0.95)
+    f.map_update(back)
+    info = f.info()
+    p = f.download()
+    # recount on the host: every placed scan patch of every particle on a covered cell
+    cs = grid.cell_start.astype(np.int64)
+    covered = 0
+    for i in range(p.n):
+        c, s = math.cos(p.orientation[i]), math.sin(p.orientation[i])
+        for k in range(len(back)):
+            sx, sy = back[k].position[0], back[k].position[1]
+            m = math.floor((c * sx - s * sy + p.x[i] - grid.offset[0]) / grid.scale[0])
+            n_ = math.floor((s * sx + c * sy + p.y[i] - grid.offset[1]) / grid.scale[1])
+            if 0 <= m < grid.width and 0 <= n_ < grid.height:
+                cell = n_ * grid.width + m
+                covered += int(cs[cell + 1] != cs[cell])
+    assert info.map_patches_covered > 0
+    # the host recount uses plain double arithmetic: it may differ from the contract's cell
+    # placement (fma, 1/scale) on a handful of boundary patches
+    assert abs(int(info.map_patches_covered) - covered) <= max(3, covered // 500)

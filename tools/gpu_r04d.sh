@@ -20,10 +20,10 @@ tail -2 $out/pytest_gpu.log
 L=slam-eslam_amd/lib/ab
 for n in 4194304 262144; do
   for r in 1 2; do
-    for lib in base walk walk5; do
+    for lib in base walk walk5 walk6; do
       printf "n=%s %s " $n $lib >> $out/ab.log
       ESLAM_GPU_LIB=$PWD/$L/lib_$lib.so timeout -k 10 120 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --particles $n \
-        | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernel_ms'])" >> $out/ab.log \
+        | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('host_enqueue_ms_per_step'), d['kernel_ms'])" >> $out/ab.log \
         || { echo "bench $lib failed"; exit 1; }
     done
   done
