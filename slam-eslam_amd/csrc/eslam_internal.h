@@ -26,9 +26,9 @@ constexpr int kNShard = 16;              // statistics shards (blockIdx % kNShar
 constexpr int kJumpBits = 11;
 constexpr int kStatsLds = 2048;          // bytes of the statistics scratch at the LDS base
 #ifndef ESLAM_WINDOW_LDS                 // experiment builds may shrink it
-#define ESLAM_WINDOW_LDS 38400
+#define ESLAM_WINDOW_LDS 30656
 #endif
-constexpr int kWindowLds = ESLAM_WINDOW_LDS;   // bytes of the MLS window after it (2400 cells: 40 KB per block with the stats, 4 blocks per CU)
+constexpr int kWindowLds = ESLAM_WINDOW_LDS;   // bytes of the MLS window after it (1916 cells: 32 KB per block with the stats, 5 blocks per CU)
 #ifndef ESLAM_K1_ATTR                    // experiment builds may set an occupancy attribute on K1
 #define ESLAM_K1_ATTR
 #endif

@@ -788,7 +788,9 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
 
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
-    uint32_t nD = 0, nTP = 0, err = 0, flag = 0;
+    // data particles | total points << 16 per lane (nD <= J, nTP <= ESLAM_MAX_CONTACTS J);
+    // werr: some particle of the wave hit a zero measurement variance (wave-uniform)
+    uint32_t nDTP = 0, werr = 0, flag = 0;
     uint32_t touched = 0;                // bit b: the wave walked bucket b (wave-uniform)
     // -min x, max x, -min y, max y of the cloud, rounded to float (the window only needs a
     // box that holds the cloud; it is widened by the float rounding in bbox_keys)
@@ -847,6 +849,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
         // in the row's bucket walk, so the walk's state stays wave-uniform (scalar)
         uint32_t bucket = kNoBucket;
         double am = 0.0, am2 = 0.0;
+        bool rowerr = false;
         if (i < n) {
         double x, y, th, z, zs, w, mp_in = 0.0;
         uint32_t fl_in = 0;
@@ -916,7 +919,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             }
             CMResult r = evaluate_pose<MAXP, BATCH, DELTA, UNG>(win, co, s, r22, x, y, z, meas_var, sid);
             if (meas_var == 0) {            // evaluatePose throws (src/ContactModel.cpp:122): no contact points
-                err = 1;
+                rowerr = true;
                 r.accepted = false;
                 r.ncp = 0;
             }
@@ -945,12 +948,11 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
                 mprob = r.weight;
                 floating = 0;
                 maxm = (maxm < r.weight) ? r.weight : maxm;
-                nD += 1;
+                nDTP += 1u + (r.ncp << 16);
                 // pow(weight, 1.0/found) with weight = exp(-s2/2): exp(-s2/2 * (1/found))
                 const uint32_t use_shape = kl2(KOFF(p.use_shape))[0];
                 if (!use_shape || r.ncp == 0) sw = dm_pow(r.weight, inv_n);
                 else sw = r.weight == 0.0 ? 0.0 : dm_exp((-0.5 * r.s2) * inv_n);
-                nTP += r.ncp;
             } else {
                 floating = 1;
                 mprob = 1.0;
@@ -997,6 +999,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             // sums, chosen by a scalar branch, instead of selecting over every bucket per lane.
             // ncp <= MAXP: the buckets above MAXP stay empty.  The whole wave walks (lanes
             // without a particle add +0.0), so cur_b and touched are scalars.
+            werr |= __ballot(rowerr) != 0ull ? 1u : 0u;
             uint64_t todo = __ballot(bucket != kNoBucket);
             while (todo) {
                 const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
@@ -1137,9 +1140,8 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     const double wmax = wave_max_butterfly(maxm);
     // the two counts in one sum: nD <= 64 J and nTP <= ESLAM_MAX_CONTACTS nD per wave (16 bits each)
     static_assert(64u * ESLAM_CHUNK_CAP * ESLAM_MAX_CONTACTS < 65536u, "packed wave counts");
-    const uint32_t wDTP = wave_sum_u32(nD | (nTP << 16));
+    const uint32_t wDTP = wave_sum_u32(nDTP);
     const uint32_t wD = wDTP & 0xffffu, wTP = wDTP >> 16;
-    const uint32_t werr = __ballot(err != 0) != 0ull ? 1u : 0u;
     if (lane < (2 * DM_NBUCKETS + 1) * 4) sl.limb[wave][lane] = limb;
     if (lane == 0) {
         sl.flag[wave] = flag | (werr << 31);
