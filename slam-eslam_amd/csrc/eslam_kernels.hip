@@ -2377,6 +2377,71 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     }
 }
 
+// One GPU's K3: the sum of the totals of the tiles before `tile`, in two levels.  Tiles form
+// groups of kGroupTiles; the last tile of each group publishes the group's total (tag << 61 |
+// total) as soon as its group-mates have published theirs (it waits for them anyway), so a
+// tile reads at most kGroupTiles - 1 tile words of its own group and one word per earlier
+// group -- one load per lane for up to 64 groups -- instead of every earlier tile's word (up
+// to 32 loads per lane at 4M, 128 at 16M).  A group word depends only on its own group's
+// tiles, which were dispatched before any later tile: the waits terminate as the flat one
+// does.  Exact integer sums: the same value as summing every tile word.
+__device__ __forceinline__ uint64_t tiles_before_grouped(const uint64_t* __restrict__ pub, uint64_t* __restrict__ gpub,
+                                                         uint32_t tile, uint32_t ntiles, uint64_t own, const ScanParams& sp,
+                                                         uint64_t* s_red, Ctl* __restrict__ ctl)
+{
+    const uint32_t tag = sp.tag;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) {
+        const uint32_t g = tile / kGroupTiles, r = tile % kGroupTiles;
+        const bool last = r == kGroupTiles - 1;          // publishes the group word
+        const uint64_t tagw = (uint64_t)tag << 61;
+        bool timeout = sp.spin_limit == 0 && tile > 0;   // testing: give up at once
+        // the own group's earlier tiles: lane l < r holds tile 64 g + l
+        uint64_t vw = tid < r ? atomic_load_agent(pub + (uint64_t)g * kGroupTiles + tid) : tagw;
+        uint64_t acc_g = 0;
+        bool published = !last;
+        // earlier groups, 8 x 64 per batch (one batch up to 512 groups: 32768 tiles)
+        for (uint32_t b0 = 0; !timeout && (b0 < g || b0 == 0); b0 += 8u * 64u) {
+            uint64_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                v[q] = k < g ? atomic_load_agent(gpub + k) : tagw;
+            }
+            uint32_t spins = 0;
+            for (;;) {
+                const bool wready = __ballot((uint32_t)(vw >> 61) != tag) == 0ull;
+                if (wready && !published) {
+                    // the group's total: its earlier tiles + this one
+                    const uint64_t tot = wave_sum_u64(vw & kPubMask) + own;
+                    if (tid == 0) atomic_store_agent(gpub + g, tagw | (tot & kPubMask));
+                    published = true;
+                }
+                bool ready = wready;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
+                if (__ballot(!ready) == 0ull) break;
+                if (spins++ >= sp.spin_limit) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(8);
+                if ((uint32_t)(vw >> 61) != tag) vw = atomic_load_agent(pub + (uint64_t)g * kGroupTiles + tid);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                    if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(gpub + k);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc_g += v[q] & kPubMask;
+            if (b0 + 8u * 64u >= g) break;
+        }
+        uint64_t acc = wave_sum_u64(acc_g + (vw & kPubMask));
+        if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
+        if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
+    }
+    __syncthreads();
+    return s_red[0];
+}
+
 // Draw counting (#{k : T_k <= C}) for the particles of one wave: the counts of its targets
 // only read the draws [dlo, dhi) around floor(C N) of its first and last target.  Its lanes
 // evaluate those draws in parallel, wave_draws at a time (lane l: k = q0 + l + 64 j, one jump
@@ -2534,9 +2599,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
+    // a tile that leaves early still publishes (total 0) its word and, as its group's last
+    // tile, the group word: every launch writes every word, so none keeps an older tag
+    auto publish_nothing = [&]() {
+        atomic_store_agent(tile_pub + tile, tagw);
+        if (tile % kGroupTiles == kGroupTiles - 1) atomic_store_agent(sp.group_pub + tile / kGroupTiles, tagw);
+    };
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
-            atomic_store_agent(tile_pub + tile, tagw);
+            publish_nothing();
             if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
@@ -2561,7 +2632,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     bool resample = false;
     if constexpr (!FUSED) {
         if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+            if (tid == 0) publish_nothing();
             return;
         }
         resample = cv->resample != 0;
@@ -2576,11 +2647,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             uint32_t fl[ITEMS];
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
             if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
-                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+                if (tid == 0) publish_nothing();
                 return;
             }
             if (cv->aborted) {           // the update threw (k_finalize): weights stay as phase A left them
-                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+                if (tid == 0) publish_nothing();
                 return;
             }
             phase_b_apply<ITEMS>(st, sp, cv, t0, tid, v, mp, fl);
@@ -2592,7 +2663,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
     if (!resample) {
-        if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+        if (tid == 0) publish_nothing();
         return;
     }
     __syncthreads();
@@ -2616,7 +2687,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         agg += t;
     }
     if (tid == 0) atomic_store_agent(tile_pub + tile, tagw | (agg & kPubMask));
-    const uint64_t tb = tiles_before_pub(tile_pub, tile, sp, s_red, ctl);
+    const uint64_t tb = tiles_before_grouped(tile_pub, sp.group_pub, tile, sp.ntiles, agg & kPubMask, sp, s_red, ctl);
     if (tb == ~0ull) return;             // gave up waiting: poisoned, no marks
     const uint64_t base = tb + wexcl + (tincl - run);
 

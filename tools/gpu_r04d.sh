@@ -20,7 +20,7 @@ tail -2 $out/pytest_gpu.log
 L=slam-eslam_amd/lib/ab
 for n in 4194304 262144; do
   for r in 1 2; do
-    for lib in base walk walk5 cnt walk6; do
+    for lib in base walk5 cnt grp walk6; do
       printf "n=%s %s " $n $lib >> $out/ab.log
       ESLAM_GPU_LIB=$PWD/$L/lib_$lib.so timeout -k 10 120 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --particles $n \
         | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('host_enqueue_ms_per_step'), d['kernel_ms'])" >> $out/ab.log \
@@ -30,7 +30,7 @@ for n in 4194304 262144; do
 done
 cat $out/ab.log | cut -c1-160
 for r in 1 2; do
-  for lib in base cnt; do
+  for lib in base grp; do
     printf "lm %s " $lib >> $out/ab_lm.log
     ESLAM_GPU_LIB=$PWD/$L/lib_$lib.so timeout -k 10 200 python bench.py --local-maps --steps 20 --warmup 5 --no-cpu-baseline \
       | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernel_ms'], d.get('map_update'))" >> $out/ab_lm.log \
