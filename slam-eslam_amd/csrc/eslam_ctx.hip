@@ -1618,13 +1618,16 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
 // particles per thread of the one-GPU K3: small filters take small tiles so the scan still
 // spreads over every CU (256k particles: 1024 blocks instead of 128).  Exact integer tile
 // totals: the tile size never changes a result.
+#ifndef ESLAM_K3_ITEMS_LARGE               // experiment builds may set 4 (K3 <4> above 2M particles)
+#define ESLAM_K3_ITEMS_LARGE kScanItems
+#endif
 static uint32_t scan_items(uint64_t n)
 {
     // measured (round-2 A/B, profiles/r02/ab_items_256k_fused.log; bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
     // 64k and 256k (over 2 items, themselves +19 % over 8 at 256k), 2 or 4 items +4 % at 1M,
     // 8 items best from 4M on (fewer tiles_before re-sums)
     if (n <= (1ull << 18)) return 1u;
-    return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)kScanItems);
+    return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)ESLAM_K3_ITEMS_LARGE);
 }
 
 static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normalize, bool multi)

@@ -165,6 +165,27 @@ __device__ __forceinline__ uint32_t jump_pow(const uint32_t* __restrict__ jt, ui
 }
 
 // ---------------------------------------------------------------------------------------
+// Diagnostic builds only (-DESLAM_STAMPS, tools/stamps.py): per-block s_memrealtime stamps
+// (100 MHz, one clock for the whole device) at the phase boundaries of K1 and K3, written by
+// thread 0 to arrays of their own.  The product build compiles none of it.
+// ---------------------------------------------------------------------------------------
+#ifdef ESLAM_STAMPS
+constexpr uint32_t kStampBlocks = 32768, kStampSlots = 8;
+__device__ uint64_t g_stamps_k1[kStampBlocks][kStampSlots];
+__device__ uint64_t g_stamps_k3[kStampBlocks][kStampSlots];
+__device__ __forceinline__ uint64_t stamp_now()
+{
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define ESLAM_STAMP(arr, k) \
+    do { if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) arr[blockIdx.x][(k)] = stamp_now(); } while (0)
+#else
+#define ESLAM_STAMP(arr, k) do { } while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------
 // K1 kernel arguments by scalar load at the point of use.  K1 reads ~110 uniform values
 // (contacts, sampler, map header, state pointers).  Loaded once at kernel entry they exceed
 // the 102 SGPRs, and the compiler parks them in VGPR lanes and fetches them back with
@@ -756,6 +777,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
     // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
+    ESLAM_STAMP(g_stamps_k1, 0);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t n = a.p.n;
     const uint32_t J = a.p.J;
@@ -785,6 +807,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     Window win;
     win.on = 0;
     if (WEIGHT) win = stage_window(a.map, a.p, ctl, 6.0 * tf, smem + kStatsLds);
+    ESLAM_STAMP(g_stamps_k1, 1);
 
     // order-free per-lane state, kept across chunks
     double maxm = 0.0;
@@ -1103,6 +1126,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     }
     }
 
+    ESLAM_STAMP(g_stamps_k1, 2);
     Shard* shb = a.shards + (blockIdx.x % kNShard);
     // bounding box of the cloud for the next step's LDS window (maxima, any order): the four
     // maxima in one transposed butterfly (at distances 32 and 16 each lane pair keeps half of
@@ -1177,6 +1201,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
         if (f & 0x7fffffffu) atomicOr((unsigned long long*)&sh->flags, (unsigned long long)(f & 0x7fffffffu));
         if (f >> 31) atomicOr((unsigned long long*)&sh->err, 1ull);
     }
+    ESLAM_STAMP(g_stamps_k1, 3);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2598,6 +2623,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     __shared__ uint32_t s_flag;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
+    ESLAM_STAMP(g_stamps_k3, 0);
     const uint64_t tagw = (uint64_t)sp.tag << 61;
     // a tile that leaves early still publishes (total 0) its word and, as its group's last
     // tile, the group word: every launch writes every word, so none keeps an older tag
@@ -2646,6 +2672,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             double mp[ITEMS];
             uint32_t fl[ITEMS];
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
+            ESLAM_STAMP(g_stamps_k3, 1);
             if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
                 if (tid == 0) publish_nothing();
                 return;
@@ -2654,6 +2681,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
                 if (tid == 0) publish_nothing();
                 return;
             }
+            ESLAM_STAMP(g_stamps_k3, 2);
             phase_b_apply<ITEMS>(st, sp, cv, t0, tid, v, mp, fl);
             resample = sgpr_u32(cv->resample) != 0;
         } else {
@@ -2667,6 +2695,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         return;
     }
     __syncthreads();
+    ESLAM_STAMP(g_stamps_k3, 3);
     const int shift = (int)sgpr_u32((uint32_t)cv->scan_shift);
     uint64_t c[ITEMS];
     const uint64_t run = blocked_fx(s_u.v, shift, c);
@@ -2686,9 +2715,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         if ((uint32_t)wv < wave) wexcl += t;
         agg += t;
     }
+    ESLAM_STAMP(g_stamps_k3, 4);
     if (tid == 0) atomic_store_agent(tile_pub + tile, tagw | (agg & kPubMask));
     const uint64_t tb = tiles_before_grouped(tile_pub, sp.group_pub, tile, sp.ntiles, agg & kPubMask, sp, s_red, ctl);
     if (tb == ~0ull) return;             // gave up waiting: poisoned, no marks
+    ESLAM_STAMP(g_stamps_k3, 5);
     const uint64_t base = tb + wexcl + (tincl - run);
 
     const uint64_t N = sp.n_global;
@@ -2697,6 +2728,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     uint64_t hi_r[ITEMS];
     uint64_t lo;
     wave_counts<ITEMS>(base, run, c, N, shift, xs, jt, s_u.T[wave], hi_r, lo);
+    ESLAM_STAMP(g_stamps_k3, 6);
     if (i0 == 0) lo = 0;
     uint64_t seg_lo[ITEMS], seg_hi[ITEMS];
     uint32_t val[ITEMS];
@@ -2717,6 +2749,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         }
     }
     flush_marks(marks, tile_first, seg_lo, seg_hi, val);
+    ESLAM_STAMP(g_stamps_k3, 7);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3499,3 +3532,14 @@ extern "C" int eslam_debug_k1_occupancy(int* blocks_per_cu, int lds)
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_project_weight<true, true, 4, true>, kBlock,
                                                         lds < 0 ? kStatsLds + kWindowLds : lds) == hipSuccess ? 0 : -1;
 }
+
+#ifdef ESLAM_STAMPS
+// diagnostic builds: copy the stamps of the last K1 (which = 1) or K3 (which = 3) launch
+extern "C" int eslam_gpu_debug_stamps(int which, uint64_t* out, uint64_t blocks)
+{
+    if (blocks > kStampBlocks) blocks = kStampBlocks;
+    const hipError_t e = which == 1 ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k1), blocks * kStampSlots * 8)
+                                    : hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k3), blocks * kStampSlots * 8);
+    return e == hipSuccess ? 0 : -1;
+}
+#endif

@@ -20,7 +20,7 @@ tail -2 $out/pytest_gpu.log
 L=slam-eslam_amd/lib/ab
 for n in 4194304 262144; do
   for r in 1 2; do
-    for lib in base walk5 cnt grp walk6; do
+    for lib in base cnt grp grp4; do
       printf "n=%s %s " $n $lib >> $out/ab.log
       ESLAM_GPU_LIB=$PWD/$L/lib_$lib.so timeout -k 10 120 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --particles $n \
         | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('host_enqueue_ms_per_step'), d['kernel_ms'])" >> $out/ab.log \
@@ -38,3 +38,7 @@ for r in 1 2; do
   done
 done
 cat $out/ab_lm.log | cut -c1-400
+ESLAM_GPU_LIB=$PWD/$L/lib_stamps.so timeout -k 10 120 python tools/stamps.py 4194304 8 > $out/stamps_4m.log 2>&1 || { echo "stamps 4M failed"; tail -5 $out/stamps_4m.log; exit 1; }
+cat $out/stamps_4m.log
+ESLAM_GPU_LIB=$PWD/$L/lib_stamps.so timeout -k 10 120 python tools/stamps.py 262144 8 > $out/stamps_256k.log 2>&1 || { echo "stamps 256k failed"; exit 1; }
+cat $out/stamps_256k.log
