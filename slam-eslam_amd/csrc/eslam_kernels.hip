@@ -1394,7 +1394,8 @@ __global__ void __launch_bounds__(kBlock) k_store_ref(SidRef sr, uint64_t n, uin
     if (fuse && sr.ctl->gather) {
         // a pending resample gather that the map merge runs (MergeParams::fuse): output i will
         // name its ancestor's store (the marks expanded as in K1, state[base] read)
-        const uint32_t carry = gv.row_first[(i & ~(uint64_t)(kRow - 1)) / kRow] + 1u;
+        const uint64_t row0 = i & ~(uint64_t)(kRow - 1);          // a row past n has no row_first entry
+        const uint32_t carry = row0 < n ? gv.row_first[row0 / kRow] + 1u : 0u;
         uint32_t mk = i < n ? gv.marks[i] : 0u;
         mk = wave_incl_max_u32(mk);
         const uint32_t src = (mk > carry ? mk : carry) - 1u;
@@ -1532,7 +1533,8 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
     uint32_t src = (uint32_t)i;
     if (gath) {
-        const uint32_t carry = mp.gv.row_first[(i & ~(uint64_t)(kRow - 1)) / kRow] + 1u;
+        const uint64_t row0 = i & ~(uint64_t)(kRow - 1);          // a row past n has no row_first entry
+        const uint32_t carry = row0 < mp.n ? mp.gv.row_first[row0 / kRow] + 1u : 0u;
         uint32_t mk = i < mp.n ? mp.gv.marks[i] : 0u;
         const bool clr = mk != 0u;
         mk = wave_incl_max_u32(mk);
