@@ -331,13 +331,14 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, uint32_
     const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
                                       (uint64_t)sid * kStoreSlots;
     const uint32_t target = cell + 1u;
-    // lower bound in the sorted keys in two memory round trips: the middle key picks the half,
-    // whose 16 keys come in four 16-byte loads
-    const uint32_t h0 = key[kStoreSlots / 2 - 1] < target ? kStoreSlots / 2 : 0u;
-    const gmem<const u4>* kv = reinterpret_cast<const gmem<const u4>*>(key + h0);
-    uint32_t pos = h0, hit = 0;
+    // lower bound in the sorted keys in two memory round trips (one 128-byte line): the last
+    // keys of the first three quarters pick the quarter, whose 8 keys come in two 16-byte
+    // loads (8 registers in flight rather than 16: K1 DELTA stays at five waves per SIMD)
+    const uint32_t q0 = (key[7] < target ? 1u : 0u) + (key[15] < target ? 1u : 0u) + (key[23] < target ? 1u : 0u);
+    const gmem<const u4>* kv = reinterpret_cast<const gmem<const u4>*>(key + 8u * q0);
+    uint32_t pos = 8u * q0, hit = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 2; ++q) {
         const u4 k4 = kv[q];
         pos += (k4.x < target) + (k4.y < target) + (k4.z < target) + (k4.w < target);
         hit |= (k4.x == target) | (k4.y == target) | (k4.z == target) | (k4.w == target);
