@@ -325,8 +325,10 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, uint32_
     // outside the store's bounding box (the cells a robot has moved past): not in the store,
     // and none of its key lines is fetched
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+#ifndef ESLAM_NO_STORE_BOX               // diagnostic builds: every lookup searches the keys
     const u4 bx = kp<const u4>(st, 3)[sid];
     if (m < bx.x || m > bx.y || n < bx.z || n > bx.w) return false;
+#endif
     const gmem<const uint32_t>* key = kp<const uint32_t>(st, 0) + (uint64_t)sid * kStoreSlots;
     const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
                                       (uint64_t)sid * kStoreSlots;
@@ -1622,7 +1624,11 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     cm = in ? (uint32_t)fm : 0u;
                     cn = in ? (uint32_t)fn : 0u;
                 }
+#ifndef ESLAM_NO_STORE_BOX
                 inbox |= (cm >= box.x && cm <= box.y && cn >= box.z && cn <= box.w) ? (1u << q) : 0u;
+#else
+                inbox |= 1u << q;
+#endif
                 cellq[q] = cell;
                 occw[q] = map.occ[(cell == 0xffffffffu ? 0u : cell) >> 5];    // branch-free: always in range
             }
