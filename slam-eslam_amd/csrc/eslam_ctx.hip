@@ -246,8 +246,6 @@ struct eslam_ctx {
     uint32_t* marks = nullptr;
     uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
     uint64_t* fin_word = nullptr;           // the fused finalize's epoch word (after the tile words)
-    uint64_t* group_pub = nullptr;          // K3's group words (after the epoch word's line)
-    uint64_t tile_words = 0;                // words of the tile_sum allocation
     uint64_t fin_epoch = 0;                 // fused finalize launches so far
     uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total (sharded K3a), or
                                             // one GPU: tag << 61 | total published by K3 (zeroed at allocation)
@@ -666,13 +664,9 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
     // the tile words, then (in a line of its own) the fused finalize's epoch word
     const uint64_t fin_at = (ntiles + 15) & ~15ull;
-    // then the group words of K3's two-level look-back (kGroupTiles tiles a word)
-    const uint64_t groups = ((ntiles + kGroupTiles - 1) / kGroupTiles + 15) & ~15ull;
-    ctx->tile_words = fin_at + 16 + groups;
-    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, ctx->tile_words * 8));
-    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, ctx->tile_words * 8));        // tag / epoch 0: never published
+    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, (fin_at + 16) * 8));
+    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, (fin_at + 16) * 8));          // tag / epoch 0: never published
     ctx->fin_word = ctx->tile_sum + fin_at;
-    ctx->group_pub = ctx->fin_word + 16;
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
     if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     if (particle_maps(ctx)) {
@@ -1644,7 +1638,6 @@ static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normali
     sp.items = multi ? (uint32_t)kScanItems : scan_items(ctx->n);
     const uint64_t tile = (uint64_t)kBlock * sp.items;
     sp.ntiles = (uint32_t)((ctx->n + tile - 1) / tile);
-    sp.group_pub = ctx->group_pub;
     return sp;
 }
 

@@ -340,11 +340,7 @@ struct ScanParams {
     uint32_t spin_limit;                 // polls of a cross-block wait before it gives up (kSpinLimit;
                                          // 0: give up at once, eslam_gpu_debug_set_spin_limit)
     uint32_t* fault;                     // host-mapped word: kFaultTimeout when a wait gave up
-    uint64_t* group_pub;                 // one GPU: per complete group of kGroupTiles tiles, tag << 61 | its
-                                         // total (published by the group's last tile; zeroed at allocation
-                                         // and when the context changes between one and several GPUs)
 };
-constexpr uint32_t kGroupTiles = 64;
 
 // A cross-block wait that gave up (a preceding tile's total or the fused finalize never
 // arrived) poisons the filter: the device ORs kFaultTimeout into ctl->err and into a

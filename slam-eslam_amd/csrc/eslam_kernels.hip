@@ -2261,20 +2261,58 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
 
 constexpr uint64_t kPubMask = (1ull << 61) - 1;
 
+// sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
+// them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
+// polls (light on the memory system the tiles it waits for are still streaming through);
+// the other waves wait at the barrier.
+// A wait that gives up (sp.spin_limit polls) poisons the filter and returns ~0.
+__device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, const ScanParams& sp,
+                                                     uint64_t* s_red, Ctl* __restrict__ ctl)
+{
+    const uint32_t tag = sp.tag;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) {
+        uint64_t acc = 0;
+        bool timeout = sp.spin_limit == 0 && count > 0;   // testing: give up at once
+        for (uint32_t b0 = 0; !timeout && b0 < count; b0 += 8u * 64u) {
+            uint64_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                v[q] = k < count ? atomic_load_agent(pub + k) : ((uint64_t)tag << 61);
+            }
+            uint32_t spins = 0;
+            for (;;) {
+                bool ready = true;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
+                if (__ballot(!ready) == 0ull) break;
+                if (spins++ >= sp.spin_limit) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(8);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t k = b0 + (uint32_t)q * 64u + tid;
+                    if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
+        }
+        acc = wave_sum_u64(acc);
+        if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
+        if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
+    }
+    __syncthreads();
+    return s_red[0];
+}
 
 // sum of the first `count` tile totals of a finished K3a (one block, coalesced, any order:
 // exact integers; the words carry K3a's launch tag above bit 61)
-// the same sum once every tile and group word of the launch is published (the sharded
-// segments kernel, after K3a): the group words of the groups before `tile`'s and the tile
-// words of its own group, at most one of each per thread
-__device__ __forceinline__ uint64_t tiles_before_done(const uint64_t* __restrict__ tile_sum, const uint64_t* __restrict__ gpub,
-                                                      uint32_t tile, uint64_t* s_wtot)
+__device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ tile_sum, uint32_t count, uint64_t* s_wtot)
 {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t g = tile / kGroupTiles, r = tile % kGroupTiles;
     uint64_t acc = 0;
-    if (tid < r) acc += tile_sum[(uint64_t)g * kGroupTiles + tid] & kPubMask;
-    for (uint32_t k = tid; k < g; k += kBlock) acc += gpub[k] & kPubMask;
+    for (uint32_t k = tid; k < count; k += kBlock) acc += tile_sum[k] & kPubMask;
     acc = wave_sum_u64(acc);
     if (lane == 0) s_wtot[wave] = acc;
     __syncthreads();
@@ -2283,75 +2321,6 @@ __device__ __forceinline__ uint64_t tiles_before_done(const uint64_t* __restrict
     for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
     __syncthreads();                     // s_wtot is reused by the caller
     return t;
-}
-
-
-// One GPU's K3: the sum of the totals of the tiles before `tile`, in two levels.  Tiles form
-// groups of kGroupTiles; the last tile of each group publishes the group's total (tag << 61 |
-// total) as soon as its group-mates have published theirs (it waits for them anyway), so a
-// tile reads at most kGroupTiles - 1 tile words of its own group and one word per earlier
-// group -- one load per lane for up to 64 groups -- instead of every earlier tile's word (up
-// to 32 loads per lane at 4M, 128 at 16M).  A group word depends only on its own group's
-// tiles, which were dispatched before any later tile: the waits terminate as the flat one
-// does.  Exact integer sums: the same value as summing every tile word.
-// want_prefix = false (the sharded K3a's tiles other than its last): only the group's last
-// tile's part -- wait for the group-mates, publish the group word -- and 0 is returned.
-__device__ __forceinline__ uint64_t tiles_before_grouped(const uint64_t* __restrict__ pub, uint64_t* __restrict__ gpub,
-                                                         uint32_t tile, uint32_t ntiles, uint64_t own, const ScanParams& sp,
-                                                         uint64_t* s_red, Ctl* __restrict__ ctl, bool want_prefix = true)
-{
-    const uint32_t tag = sp.tag;
-    const uint32_t tid = threadIdx.x;
-    if (tid < 64) {
-        const uint32_t g0 = tile / kGroupTiles, r = tile % kGroupTiles;
-        const uint32_t g = want_prefix ? g0 : 0u;        // earlier groups read (none: publish only)
-        const bool last = r == kGroupTiles - 1;          // publishes the group word
-        const uint64_t tagw = (uint64_t)tag << 61;
-        bool timeout = sp.spin_limit == 0 && tile > 0;   // testing: give up at once
-        // the own group's earlier tiles: lane l < r holds tile 64 g + l
-        uint64_t vw = tid < r ? atomic_load_agent(pub + (uint64_t)g0 * kGroupTiles + tid) : tagw;
-        uint64_t acc_g = 0;
-        bool published = !last;
-        // earlier groups, 8 x 64 per batch (one batch up to 512 groups: 32768 tiles)
-        for (uint32_t b0 = 0; !timeout && (b0 < g || b0 == 0); b0 += 8u * 64u) {
-            uint64_t v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t k = b0 + (uint32_t)q * 64u + tid;
-                v[q] = k < g ? atomic_load_agent(gpub + k) : tagw;
-            }
-            uint32_t spins = 0;
-            for (;;) {
-                const bool wready = __ballot((uint32_t)(vw >> 61) != tag) == 0ull;
-                if (wready && !published) {
-                    // the group's total: its earlier tiles + this one
-                    const uint64_t tot = wave_sum_u64(vw & kPubMask) + own;
-                    if (tid == 0) atomic_store_agent(gpub + g0, tagw | (tot & kPubMask));
-                    published = true;
-                }
-                bool ready = wready;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
-                if (__ballot(!ready) == 0ull) break;
-                if (spins++ >= sp.spin_limit) { timeout = true; break; }
-                __builtin_amdgcn_s_sleep(8);
-                if ((uint32_t)(vw >> 61) != tag) vw = atomic_load_agent(pub + (uint64_t)g0 * kGroupTiles + tid);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t k = b0 + (uint32_t)q * 64u + tid;
-                    if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(gpub + k);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc_g += v[q] & kPubMask;
-            if (b0 + 8u * 64u >= g) break;
-        }
-        uint64_t acc = wave_sum_u64(acc_g + (vw & kPubMask));
-        if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
-        if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
-    }
-    __syncthreads();
-    return s_red[0];
 }
 
 // K3a (multi-GPU): phase B + normalisation (striped, coalesced) and, when resampling, the
@@ -2371,15 +2340,9 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     const uint32_t tile = blockIdx.x;
     const uint64_t tagw = (uint64_t)sp.tag << 61;
     const bool last_tile = total && tile + 1 == sp.ntiles;
-    // a tile that leaves early still publishes its word and, as its group's last tile, the
-    // group word (the segments kernel sums the group words)
-    auto publish_nothing = [&]() {
-        atomic_store_agent(tile_sum + tile, tagw);
-        if (tile % kGroupTiles == kGroupTiles - 1) atomic_store_agent(sp.group_pub + tile / kGroupTiles, tagw);
-    };
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
-            publish_nothing();
+            atomic_store_agent(tile_sum + tile, tagw);
             if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             if (last_tile) *total = ~0ull;
         }
@@ -2408,19 +2371,19 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
         phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
         if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
             if (tid == 0) {
-                publish_nothing();
+                atomic_store_agent(tile_sum + tile, tagw);
                 if (last_tile) *total = ~0ull;               // every rank sees the fault
             }
             return;
         }
         if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) publish_nothing();
+            if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
             return;
         }
         phase_b_apply<ITEMS>(st, sp, cv, t0, tid, v, mp, fl);
     } else {
         if (ctl->aborted) {              // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) publish_nothing();
+            if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
             return;
         }
         phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
@@ -2431,7 +2394,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) fx_sum += fx_shift(v[r], shift);   // 0 past the end
     if (!resample) {
-        if (tid == 0) publish_nothing();
+        if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
         return;
     }
 
@@ -2443,13 +2406,10 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
     if (tid == 0) atomic_store_agent(tile_sum + tile, tagw | (t & kPubMask));
     if (last_tile) {
-        const uint64_t before = tiles_before_grouped(tile_sum, sp.group_pub, tile, sp.ntiles, t & kPubMask, sp, s_red, ctl);
+        const uint64_t before = tiles_before_pub(tile_sum, tile, sp, s_red, ctl);
         if (tid == 0) *total = before == ~0ull ? ~0ull : before + t;     // ~0: every rank sees the fault
-    } else if (tile % kGroupTiles == kGroupTiles - 1) {
-        (void)tiles_before_grouped(tile_sum, sp.group_pub, tile, sp.ntiles, t & kPubMask, sp, s_red, ctl, false);
     }
 }
-
 
 // Draw counting (#{k : T_k <= C}) for the particles of one wave: the counts of its targets
 // only read the draws [dlo, dhi) around floor(C N) of its first and last target.  Its lanes
@@ -2609,15 +2569,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     const uint32_t tile = blockIdx.x;
     ESLAM_STAMP(g_stamps_k3, 0);
     const uint64_t tagw = (uint64_t)sp.tag << 61;
-    // a tile that leaves early still publishes (total 0) its word and, as its group's last
-    // tile, the group word: every launch writes every word, so none keeps an older tag
-    auto publish_nothing = [&]() {
-        atomic_store_agent(tile_pub + tile, tagw);
-        if (tile % kGroupTiles == kGroupTiles - 1) atomic_store_agent(sp.group_pub + tile / kGroupTiles, tagw);
-    };
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
-            publish_nothing();
+            atomic_store_agent(tile_pub + tile, tagw);
             if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
@@ -2642,7 +2596,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     bool resample = false;
     if constexpr (!FUSED) {
         if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) publish_nothing();
+            if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
             return;
         }
         resample = cv->resample != 0;
@@ -2658,11 +2612,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
             ESLAM_STAMP(g_stamps_k3, 1);
             if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
-                if (tid == 0) publish_nothing();
+                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
                 return;
             }
             if (cv->aborted) {           // the update threw (k_finalize): weights stay as phase A left them
-                if (tid == 0) publish_nothing();
+                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
                 return;
             }
             ESLAM_STAMP(g_stamps_k3, 2);
@@ -2675,7 +2629,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
     if (!resample) {
-        if (tid == 0) publish_nothing();
+        if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
         return;
     }
     __syncthreads();
@@ -2701,7 +2655,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     }
     ESLAM_STAMP(g_stamps_k3, 4);
     if (tid == 0) atomic_store_agent(tile_pub + tile, tagw | (agg & kPubMask));
-    const uint64_t tb = tiles_before_grouped(tile_pub, sp.group_pub, tile, sp.ntiles, agg & kPubMask, sp, s_red, ctl);
+    const uint64_t tb = tiles_before_pub(tile_pub, tile, sp, s_red, ctl);
     if (tb == ~0ull) return;             // gave up waiting: poisoned, no marks
     ESLAM_STAMP(g_stamps_k3, 5);
     const uint64_t base = tb + wexcl + (tincl - run);
@@ -2796,7 +2750,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
     const int shift = ctl->scan_shift;
     uint64_t c[kScanItems];
     const uint64_t run = blocked_fx<kScanItems>(s_v, shift, c);
-    const uint64_t tbase = tiles_before_done(tile_sum, sp.group_pub, tile, s_wtot) + block_excl(run, s_wtot);
+    const uint64_t tbase = tiles_before(tile_sum, tile, s_wtot) + block_excl(run, s_wtot);
     uint64_t off, O0, O1;
     plan_bounds(pp, ctl, totals, jt, off, O0, O1);
     const uint64_t base = off + tbase;
