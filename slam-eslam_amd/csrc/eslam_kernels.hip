@@ -1641,6 +1641,9 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 covd |= (on && occ) ? (1u << q) : 0u;
             }
             covered += (uint32_t)__builtin_popcount(covd);
+            // the box bits above predate this group's inserts: after one, a later patch of the
+            // group may land on the cell just inserted, so it searches the keys regardless
+            bool grew = false;
 #pragma unroll
             for (uint32_t q = 0; q < kMergeGroup; ++q) {
                 if (!((open >> q) & 1u)) continue;
@@ -1650,7 +1653,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 // for cells inside the store's bounding box: a wave whose particles have all
                 // moved past their stored cells skips it
                 bool hit = false;
-                if ((inbox >> q) & 1u) {
+                if (((inbox >> q) & 1u) || grew) {
                     uint32_t d[kStoreCap / 3];
 #pragma unroll
                     for (uint32_t t = 0; t < kStoreCap / 3; ++t)
@@ -1689,6 +1692,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     const uint32_t cn = cellq[q] / map.width, cm = cellq[q] - cn * map.width;
                     box.x = min(box.x, cm); box.y = max(box.y, cm);
                     box.z = min(box.z, cn); box.w = max(box.w, cn);
+                    grew = true;
                 }
             }
         }
