@@ -2235,7 +2235,19 @@ constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * wave_d
 
 // stratified draws one wave holds in LDS at a time: its particles' share plus a row of slack
 // (at least 576)
-template <int ITEMS> constexpr int wave_draws() { return 64 * ITEMS + 64 > 576 ? 64 * ITEMS + 64 : 576; }
+#ifndef ESLAM_K3_WAVES8                  // experiment builds: 8 (with ESLAM_K3_DRAW_SLACK 0: 19.5 KB of LDS)
+#define ESLAM_K3_WAVES8 6
+#endif
+#ifndef ESLAM_K3_DRAW_SLACK
+#define ESLAM_K3_DRAW_SLACK 64
+#endif
+#ifndef ESLAM_K3_DRAW_MIN
+#define ESLAM_K3_DRAW_MIN 576
+#endif
+template <int ITEMS> constexpr int wave_draws()
+{
+    return 64 * ITEMS + ESLAM_K3_DRAW_SLACK > ESLAM_K3_DRAW_MIN ? 64 * ITEMS + ESLAM_K3_DRAW_SLACK : ESLAM_K3_DRAW_MIN;
+}
 
 // the LDS slot of a wave's draw x, one pad slot per 8: a lane's window reads sit near draw
 // 8 l + const (one target per particle, ITEMS = 8 particles per lane), and unpadded that stride
@@ -2566,7 +2578,7 @@ __device__ __forceinline__ void wave_counts(uint64_t base, uint64_t run, const u
 // 8 items: the 6 waves per SIMD the unfused kernel reaches by itself (<= 80 VGPRs; the fused
 // one would take 86 and run at 5)
 template <int ITEMS, bool FUSED>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? 6 : 1))) k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? ESLAM_K3_WAVES8 : (ITEMS == 16 ? 4 : 1)))) k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                                uint64_t* __restrict__ tile_pub, uint32_t* __restrict__ marks,
                                                                uint32_t* __restrict__ tile_first,
                                                                const uint32_t* __restrict__ jt, FusedFin ff)
@@ -3332,6 +3344,9 @@ extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, 
     case 2: ESLAM_SEG(2); break;
     case 4: ESLAM_SEG(4); break;
     case 8: ESLAM_SEG(8); break;
+#if ESLAM_K3_ITEMS16
+    case 16: ESLAM_SEG(16); break;     // experiment builds (ESLAM_K3_ITEMS_LARGE=16)
+#endif
     default: return hipErrorInvalidValue;
     }
 #undef ESLAM_SEG
