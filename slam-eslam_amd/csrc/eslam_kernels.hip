@@ -2350,8 +2350,12 @@ __device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ ti
 // K3's words (every launch writes every word).  The last tile waits for the others' words
 // and writes this slice's total (the value all-gathered before K3b), so no separate kernel
 // sums the tiles; K3b re-sums the words before its own tile (any order: exact integers).
+#ifndef ESLAM_K3M_WAVES                  // experiment builds: waves per SIMD of the sharded K3a / segments kernel
+#define ESLAM_K3M_WAVES 1
+#endif
 template <int ITEMS, bool FUSED>
-__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ESLAM_K3M_WAVES)))
+k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                            uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total,
                                                            FusedFin ff)
 {
@@ -2729,7 +2733,8 @@ __device__ __forceinline__ void plan_bounds(const PlanParams& pp, const Ctl* ctl
     O1 = pp.rank == pp.nranks - 1 ? N : count_draws_le(off + totals[pp.rank], N, xs, shift, jt);
 }
 
-__global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState s1, ScanParams sp, PlanParams pp,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ESLAM_K3M_WAVES)))
+k_segments_multi(DevState s0, DevState s1, ScanParams sp, PlanParams pp,
                                                            Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
                                                            uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
                                                            const uint64_t* __restrict__ totals, const uint32_t* __restrict__ jt,

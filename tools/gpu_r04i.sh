@@ -9,8 +9,8 @@ out=gpurun_out/$tag
 mkdir -p $out
 L=slam-eslam_amd/lib/ab
 for v in "$@"; do
-  timeout -k 10 300 env ESLAM_GPU_LIB=$PWD/$L/lib_$v.so python -u -m pytest -q -x --timeout 240 --timeout-method thread \
-    tests/test_gpu_fullsize.py > $out/parity_$v.log 2>&1
+  timeout -k 10 400 env ESLAM_GPU_LIB=$PWD/$L/lib_$v.so python -u -m pytest -q -x --timeout 240 --timeout-method thread \
+    tests/test_gpu_fullsize.py tests/test_gpu_dist.py > $out/parity_$v.log 2>&1
   rc=$?
   echo "== parity $v rc=$rc" | tee -a $out/session.log
   [ $rc -eq 0 ] || { tail -20 $out/parity_$v.log; exit $rc; }
@@ -23,6 +23,14 @@ for n in 4194304 1048576 262144; do
         | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps(d['kernel_ms']))" >> $out/ab.log \
         || { echo "bench $v failed"; exit 1; }
     done
+  done
+done
+for r in 1 2; do
+  for v in "$@"; do
+    printf "sharded n=4194304 %s " $v >> $out/ab.log
+    timeout -k 10 120 env ESLAM_GPU_LIB=$PWD/$L/lib_$v.so python bench.py --sharded --steps 30 --warmup 5 --no-cpu-baseline --particles 4194304 \
+      | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps(d['kernel_ms']))" >> $out/ab.log \
+      || { echo "sharded bench $v failed"; exit 1; }
   done
 done
 cut -c1-260 $out/ab.log
