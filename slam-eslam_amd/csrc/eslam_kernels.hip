@@ -1525,6 +1525,11 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 // slot-major, lane-minor) at the particle's first change and shifted / fused there; a changed
 // map is written back whole at the end -- in place when no other particle names the store
 // (ref 1), else to the particle's reserved free store frees[i], which it then names.
+#ifndef ESLAM_MERGE_SIG
+#define ESLAM_MERGE_SIG 0
+#endif
+// the signature bit of a key (target = cell + 1; free slots hash too: a harmless extra bit)
+__device__ __forceinline__ uint32_t sig_bit(uint32_t key) { return (key * 0x9E3779B1u) >> 26; }
 constexpr int kMergeBlock = 128;                 // 24 KB of LDS: 6 blocks (12 waves) per CU
 constexpr uint32_t kMergeGroup = 8;              // patches whose cells and occupancy words load together
 static_assert(kStoreCap == 24, "k_map_merge's membership min-tree covers 24 keys");
@@ -1573,6 +1578,18 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
         }
         uint32_t count = ms.count[sid];
         uint4 box = ms.box[sid];             // the stored cells' bounding box (MapStore::box)
+#if ESLAM_MERGE_SIG
+        // a 64-bit signature of the stored keys (bit sig_bit(key)): a patch whose bit is clear
+        // is not in the store, so its 24-key membership test is skipped (the steady state's
+        // patches mostly miss full stores); the inserts below keep it current
+        uint32_t sig_lo = 0, sig_hi = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < kStoreCap; ++t) {
+            const uint32_t h = sig_bit(key[t]);
+            sig_lo |= h < 32u ? 1u << (h & 31u) : 0u;
+            sig_hi |= h >= 32u ? 1u << (h & 31u) : 0u;
+        }
+#endif
         const float2* sv = ms.val + (uint64_t)sid * kStoreSlots;
         const double x = in.x[src], y = in.y[src], th = in.th[src], z = in.z[src], zs = in.zs[src];
         if (gath) {
@@ -1659,7 +1676,13 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 // for cells inside the store's bounding box: a wave whose particles have all
                 // moved past their stored cells skips it
                 bool hit = false;
-                if (((inbox >> q) & 1u) || grew) {
+#if ESLAM_MERGE_SIG
+                const uint32_t hq = sig_bit(target);
+                const bool maybe = (((hq < 32u ? sig_lo : sig_hi) >> (hq & 31u)) & 1u) != 0u;
+#else
+                const bool maybe = true;
+#endif
+                if ((((inbox >> q) & 1u) || grew) && maybe) {
                     uint32_t d[kStoreCap / 3];
 #pragma unroll
                     for (uint32_t t = 0; t < kStoreCap / 3; ++t)
@@ -1699,6 +1722,10 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     box.x = min(box.x, cm); box.y = max(box.y, cm);
                     box.z = min(box.z, cn); box.w = max(box.w, cn);
                     grew = true;
+#if ESLAM_MERGE_SIG
+                    sig_lo |= hq < 32u ? 1u << (hq & 31u) : 0u;
+                    sig_hi |= hq >= 32u ? 1u << (hq & 31u) : 0u;
+#endif
                 }
             }
         }

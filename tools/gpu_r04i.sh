@@ -8,6 +8,20 @@ tag=$1; shift
 out=gpurun_out/$tag
 mkdir -p $out
 L=slam-eslam_amd/lib/ab
+# the map merge's key signature (lib_msig): per-particle-map parity, then configs[4] lines
+timeout -k 10 300 env ESLAM_GPU_LIB=$PWD/$L/lib_msig.so python -u -m pytest -q -x --timeout 240 --timeout-method thread \
+  tests/test_gpu_particle_maps.py tests/test_gpu_dist.py -k "maps or particle" > $out/parity_msig.log 2>&1
+rc=$?
+echo "== parity msig rc=$rc" | tee -a $out/session.log
+[ $rc -eq 0 ] || { tail -20 $out/parity_msig.log; exit $rc; }
+for r in 1 2; do
+  for v in main msig; do
+    printf "maps %s " $v >> $out/ab.log
+    timeout -k 10 200 env ESLAM_GPU_LIB=$PWD/$L/lib_$v.so python bench.py --local-maps --steps 20 --warmup 5 --no-cpu-baseline \
+      | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps(d['kernel_ms']))" >> $out/ab.log \
+      || { echo "maps bench $v failed"; exit 1; }
+  done
+done
 for v in "$@"; do
   timeout -k 10 400 env ESLAM_GPU_LIB=$PWD/$L/lib_$v.so python -u -m pytest -q -x --timeout 240 --timeout-method thread \
     tests/test_gpu_fullsize.py tests/test_gpu_dist.py > $out/parity_$v.log 2>&1
