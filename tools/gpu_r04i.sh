@@ -22,7 +22,7 @@ for r in 1 2; do
       || { echo "maps bench $v failed"; exit 1; }
   done
 done
-for v in "$@"; do
+for v in ${PARITY:-$@}; do
   timeout -k 10 400 env ESLAM_GPU_LIB=$PWD/$L/lib_$v.so python -u -m pytest -q -x --timeout 240 --timeout-method thread \
     tests/test_gpu_fullsize.py tests/test_gpu_dist.py > $out/parity_$v.log 2>&1
   rc=$?
