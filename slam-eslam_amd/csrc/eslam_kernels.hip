@@ -782,7 +782,7 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 #define K1_ST(p, v) __builtin_nontemporal_store((v), (p))
 
 template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false, bool UNG = false>
-__global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args a)
+__global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR __attribute__((amdgpu_waves_per_eu(DELTA ? 4 : 1))) k_project_weight(K1Args a)
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
     // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
@@ -851,6 +851,14 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
     constexpr uint32_t kNoBucket = 0xffu;
     double curA = 0.0, curB = 0.0;
     uint32_t cur_b = kNoBucket;
+    // DELTA (per-particle maps): a wave's particles find different numbers of contact points
+    // (cells only their stores hold), so its rows span several buckets and parking pairs in
+    // bspill costs a store and a load per switch (K1 DELTA 0.45 -> 0.51 ms at 8M, r04h).  Its
+    // kernel runs at four waves per SIMD anyway: every bucket's pair stays in registers.
+    constexpr bool kRegAcc = DELTA;
+    double accA[kRegAcc ? DM_NBUCKETS : 1], accB[kRegAcc ? DM_NBUCKETS : 1];
+#pragma unroll
+    for (int k = 0; k < (kRegAcc ? DM_NBUCKETS : 1); ++k) accA[k] = accB[k] = 0.0;
     double accSW = 0.0;
 
     for (uint32_t j = 0; j < J; ++j) {
@@ -1036,6 +1044,18 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             while (todo) {
                 const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bucket, (int)__builtin_ctzll(todo));
                 const bool mine = bucket == b0;
+                if constexpr (kRegAcc) {
+                    touched |= 1u << b0;
+#pragma unroll
+                    for (uint32_t k = 0; k < (uint32_t)DM_NBUCKETS; ++k) {
+                        if (k == b0) {                   // scalar branch (b0 is wave-uniform)
+                            accA[k] = accA[k] + (mine ? am : 0.0);
+                            accB[k] = accB[k] + (mine ? am2 : 0.0);
+                        }
+                    }
+                    todo &= ~__ballot(mine);
+                    continue;
+                }
                 if (b0 != cur_b) {
                     // the wave moves to another bucket: park the current pair, take b0's (a
                     // bucket the wave never walked starts at +0.0)
@@ -1082,6 +1102,11 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
             // total k ends in lanes 16k..16k+15), the same pairwise additions, and lane 4q + c
             // picks total q.
             const uint32_t b0 = touched0 ? (uint32_t)__builtin_ctz(touched0) : 0u;
+            if constexpr (kRegAcc) {
+#pragma unroll
+                for (uint32_t k = 0; k < (uint32_t)DM_NBUCKETS; ++k)
+                    if (k == b0) { curA = accA[k]; curB = accB[k]; }
+            }
             double w4[4] = {curA, curB, accSW, 0.0};
             transpose_add<32, 2>(w4, lane);
             transpose_add<16, 1>(w4, lane);
@@ -1108,7 +1133,8 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR k_project_weight(K1Args 
                 v[k] = k == kQ - 1 ? accSW : 0.0;
                 if (k < 2 * DM_NBUCKETS) {
                     const uint32_t b = (uint32_t)(k < DM_NBUCKETS ? k : k - DM_NBUCKETS);
-                    if (b == cur_b) v[k] = k < DM_NBUCKETS ? curA : curB;
+                    if constexpr (kRegAcc) v[k] = k < DM_NBUCKETS ? accA[b] : accB[b];
+                    else if (b == cur_b) v[k] = k < DM_NBUCKETS ? curA : curB;
                     else if ((touched >> b) & 1u) v[k] = sp[b * 128 + (k < DM_NBUCKETS ? 0 : 64)];
                 }
             }
