@@ -71,7 +71,7 @@ def parse():
     return ap.parse_args()
 
 
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r03", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r04", "summary.json")
 
 
 def pmc_traffic(kernel, n, map_cells, workload):
