@@ -1596,10 +1596,7 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
     const double motion = sqrt(p.mu[0] * p.mu[0] + p.mu[1] * p.mu[1]) +
                           6.0 * sqrt(in->sample_cov[0] + in->sample_cov[4]);
     p.win_margin = reach + motion + 0.05;
-#ifndef ESLAM_WINDOW_MIN_N               // experiment builds: no LDS window below this many particles
-#define ESLAM_WINDOW_MIN_N 0
-#endif
-    p.use_window = ((c.flags & ESLAM_FLAG_NO_MAP_LDS) || ctx->n < (uint64_t)ESLAM_WINDOW_MIN_N) ? 0u : 1u;
+    p.use_window = (c.flags & ESLAM_FLAG_NO_MAP_LDS) ? 0u : 1u;
     p.me2 = c.measurement_error * c.measurement_error;
     p.radius = c.contact_point_radius;
     p.corr = c.contact_likelihood_correction;
@@ -1615,16 +1612,13 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
 // particles per thread of the one-GPU K3: small filters take small tiles so the scan still
 // spreads over every CU (256k particles: 1024 blocks instead of 128).  Exact integer tile
 // totals: the tile size never changes a result.
-#ifndef ESLAM_K3_ITEMS_LARGE               // experiment builds may set 4 (K3 <4> above 2M particles)
-#define ESLAM_K3_ITEMS_LARGE kScanItems
-#endif
 static uint32_t scan_items(uint64_t n)
 {
     // measured (round-2 A/B, profiles/r02/ab_items_256k_fused.log; bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
     // 64k and 256k (over 2 items, themselves +19 % over 8 at 256k), 2 or 4 items +4 % at 1M,
     // 8 items best from 4M on (fewer tiles_before re-sums)
     if (n <= (1ull << 18)) return 1u;
-    return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)ESLAM_K3_ITEMS_LARGE);
+    return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)kScanItems);
 }
 
 static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normalize, bool multi)

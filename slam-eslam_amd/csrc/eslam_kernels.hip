@@ -318,12 +318,9 @@ __device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint
 
 // per-particle maps: the patch of a cell the shared grid leaves empty, from the particle's
 // store (K1Args::store), with the same 3-sigma gate as a grid patch
-__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, uint32_t m, uint32_t n, double lz, double qv,
-                                            double& mean, double& stdev)
+__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double lz, double qv, double& mean, double& stdev)
 {
     const su8 st = kl8(KOFF(store));                  // key, val, count, box
-    // outside the store's bounding box (the cells a robot has moved past): not in the store,
-    // and none of its key lines is fetched
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const gmem<const uint32_t>* key = kp<const uint32_t>(st, 0) + (uint64_t)sid * kStoreSlots;
     const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
@@ -331,17 +328,10 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, uint32_
     const uint32_t target = cell + 1u;
     // lower bound in the sorted keys in two memory round trips (one 128-byte line): the last
     // keys of the first three quarters pick the quarter, whose 8 keys come in two 16-byte
-    // loads (8 registers in flight rather than 16: K1 DELTA stays at five waves per SIMD).
-    // The box loads with the quarter keys (one round trip for both: checked first, it added
-    // a round trip to every lookup, K1 DELTA 0.44 -> 0.51 ms at 8M, r04g)
+    // loads (8 registers in flight rather than 16).  The store's bounding box is not consulted
+    // here: the quarter keys share the key line, so the box saves no fetch, only a test (K1
+    // DELTA with and without it: 0.516 / 0.516 ms at 8M, profiles/r04/ab_r04h_maps_box.log)
     const uint32_t k7 = key[7], k15 = key[15], k23 = key[23];
-#if !defined(ESLAM_NO_STORE_BOX) && !defined(ESLAM_NO_K1_BOX)   // diagnostic builds: every lookup searches the keys
-    const u4 bx = kp<const u4>(st, 3)[sid];
-    // both in flight before the box test (the compiler would otherwise sink the key loads
-    // below its branch)
-    asm volatile("" ::"v"(k7), "v"(k15), "v"(k23), "v"(bx));
-    if (m < bx.x || m > bx.y || n < bx.z || n > bx.w) return false;
-#endif
     const uint32_t q0 = (k7 < target ? 1u : 0u) + (k15 < target ? 1u : 0u) + (k23 < target ? 1u : 0u);
     const gmem<const u4>* kv = reinterpret_cast<const gmem<const u4>*>(key + 8u * q0);
     uint32_t pos = 8u * q0, hit = 0;
@@ -403,7 +393,7 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     if constexpr (DELTA) {
         if (!in_grid || (in_win && wc.count == 1)) return false;
-        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
+        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, lz, qv, mean, stdev);
     } else {
         if (!in_grid || (in_win && wc.count <= 1)) return false;
     }
@@ -419,7 +409,7 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         b = cell_start[cell];
         e = cell_start[cell + 1];
         if constexpr (DELTA) {
-            if (b == e) return store_patch(sid, (uint32_t)cell, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
+            if (b == e) return store_patch(sid, (uint32_t)cell, lz, qv, mean, stdev);
         }
     }
     for (uint32_t k = b; k < e; ++k) {
@@ -1551,11 +1541,6 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 // slot-major, lane-minor) at the particle's first change and shifted / fused there; a changed
 // map is written back whole at the end -- in place when no other particle names the store
 // (ref 1), else to the particle's reserved free store frees[i], which it then names.
-#ifndef ESLAM_MERGE_SIG
-#define ESLAM_MERGE_SIG 0
-#endif
-// the signature bit of a key (target = cell + 1; free slots hash too: a harmless extra bit)
-__device__ __forceinline__ uint32_t sig_bit(uint32_t key) { return (key * 0x9E3779B1u) >> 26; }
 constexpr int kMergeBlock = 128;                 // 24 KB of LDS: 6 blocks (12 waves) per CU
 constexpr uint32_t kMergeGroup = 8;              // patches whose cells and occupancy words load together
 static_assert(kStoreCap == 24, "k_map_merge's membership min-tree covers 24 keys");
@@ -1604,18 +1589,6 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
         }
         uint32_t count = ms.count[sid];
         uint4 box = ms.box[sid];             // the stored cells' bounding box (MapStore::box)
-#if ESLAM_MERGE_SIG
-        // a 64-bit signature of the stored keys (bit sig_bit(key)): a patch whose bit is clear
-        // is not in the store, so its 24-key membership test is skipped (the steady state's
-        // patches mostly miss full stores); the inserts below keep it current
-        uint32_t sig_lo = 0, sig_hi = 0;
-#pragma unroll
-        for (uint32_t t = 0; t < kStoreCap; ++t) {
-            const uint32_t h = sig_bit(key[t]);
-            sig_lo |= h < 32u ? 1u << (h & 31u) : 0u;
-            sig_hi |= h >= 32u ? 1u << (h & 31u) : 0u;
-        }
-#endif
         const float2* sv = ms.val + (uint64_t)sid * kStoreSlots;
         const double x = in.x[src], y = in.y[src], th = in.th[src], z = in.z[src], zs = in.zs[src];
         if (gath) {
@@ -1673,11 +1646,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     cm = in ? (uint32_t)fm : 0u;
                     cn = in ? (uint32_t)fn : 0u;
                 }
-#ifndef ESLAM_NO_STORE_BOX
                 inbox |= (cm >= box.x && cm <= box.y && cn >= box.z && cn <= box.w) ? (1u << q) : 0u;
-#else
-                inbox |= 1u << q;
-#endif
                 cellq[q] = cell;
                 occw[q] = map.occ[(cell == 0xffffffffu ? 0u : cell) >> 5];    // branch-free: always in range
             }
@@ -1702,13 +1671,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 // for cells inside the store's bounding box: a wave whose particles have all
                 // moved past their stored cells skips it
                 bool hit = false;
-#if ESLAM_MERGE_SIG
-                const uint32_t hq = sig_bit(target);
-                const bool maybe = (((hq < 32u ? sig_lo : sig_hi) >> (hq & 31u)) & 1u) != 0u;
-#else
-                const bool maybe = true;
-#endif
-                if ((((inbox >> q) & 1u) || grew) && maybe) {
+                if (((inbox >> q) & 1u) || grew) {
                     uint32_t d[kStoreCap / 3];
 #pragma unroll
                     for (uint32_t t = 0; t < kStoreCap / 3; ++t)
@@ -1748,10 +1711,6 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     box.x = min(box.x, cm); box.y = max(box.y, cm);
                     box.z = min(box.z, cn); box.w = max(box.w, cn);
                     grew = true;
-#if ESLAM_MERGE_SIG
-                    sig_lo |= hq < 32u ? 1u << (hq & 31u) : 0u;
-                    sig_hi |= hq >= 32u ? 1u << (hq & 31u) : 0u;
-#endif
                 }
             }
         }
@@ -2288,19 +2247,7 @@ constexpr int kWaveChunks = 2;           // more draws than kWaveChunks * wave_d
 
 // stratified draws one wave holds in LDS at a time: its particles' share plus a row of slack
 // (at least 576)
-#ifndef ESLAM_K3_WAVES8                  // experiment builds: 8 (with ESLAM_K3_DRAW_SLACK 0: 19.5 KB of LDS)
-#define ESLAM_K3_WAVES8 6
-#endif
-#ifndef ESLAM_K3_DRAW_SLACK
-#define ESLAM_K3_DRAW_SLACK 64
-#endif
-#ifndef ESLAM_K3_DRAW_MIN
-#define ESLAM_K3_DRAW_MIN 576
-#endif
-template <int ITEMS> constexpr int wave_draws()
-{
-    return 64 * ITEMS + ESLAM_K3_DRAW_SLACK > ESLAM_K3_DRAW_MIN ? 64 * ITEMS + ESLAM_K3_DRAW_SLACK : ESLAM_K3_DRAW_MIN;
-}
+template <int ITEMS> constexpr int wave_draws() { return 64 * ITEMS + 64 > 576 ? 64 * ITEMS + 64 : 576; }
 
 // the LDS slot of a wave's draw x, one pad slot per 8: a lane's window reads sit near draw
 // 8 l + const (one target per particle, ITEMS = 8 particles per lane), and unpadded that stride
@@ -2403,12 +2350,8 @@ __device__ __forceinline__ uint64_t tiles_before(const uint64_t* __restrict__ ti
 // K3's words (every launch writes every word).  The last tile waits for the others' words
 // and writes this slice's total (the value all-gathered before K3b), so no separate kernel
 // sums the tiles; K3b re-sums the words before its own tile (any order: exact integers).
-#ifndef ESLAM_K3M_WAVES                  // experiment builds: waves per SIMD of the sharded K3a / segments kernel
-#define ESLAM_K3M_WAVES 1
-#endif
 template <int ITEMS, bool FUSED>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ESLAM_K3M_WAVES)))
-k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+__global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                            uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ total,
                                                            FusedFin ff)
 {
@@ -2635,7 +2578,7 @@ __device__ __forceinline__ void wave_counts(uint64_t base, uint64_t run, const u
 // 8 items: the 6 waves per SIMD the unfused kernel reaches by itself (<= 80 VGPRs; the fused
 // one would take 86 and run at 5)
 template <int ITEMS, bool FUSED>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? ESLAM_K3_WAVES8 : (ITEMS == 16 ? 4 : 1)))) k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITEMS == 8 ? 6 : 1))) k_normalize_segments(DevState s0, DevState s1, ScanParams sp, Ctl* __restrict__ ctl,
                                                                uint64_t* __restrict__ tile_pub, uint32_t* __restrict__ marks,
                                                                uint32_t* __restrict__ tile_first,
                                                                const uint32_t* __restrict__ jt, FusedFin ff)
@@ -2786,8 +2729,7 @@ __device__ __forceinline__ void plan_bounds(const PlanParams& pp, const Ctl* ctl
     O1 = pp.rank == pp.nranks - 1 ? N : count_draws_le(off + totals[pp.rank], N, xs, shift, jt);
 }
 
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ESLAM_K3M_WAVES)))
-k_segments_multi(DevState s0, DevState s1, ScanParams sp, PlanParams pp,
+__global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState s1, ScanParams sp, PlanParams pp,
                                                            Ctl* __restrict__ ctl, const uint64_t* __restrict__ tile_sum,
                                                            uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first,
                                                            const uint64_t* __restrict__ totals, const uint32_t* __restrict__ jt,
@@ -3402,9 +3344,6 @@ extern "C" hipError_t eslam_launch_normalize_segments(DevState s0, DevState s1, 
     case 2: ESLAM_SEG(2); break;
     case 4: ESLAM_SEG(4); break;
     case 8: ESLAM_SEG(8); break;
-#if ESLAM_K3_ITEMS16
-    case 16: ESLAM_SEG(16); break;     // experiment builds (ESLAM_K3_ITEMS_LARGE=16)
-#endif
     default: return hipErrorInvalidValue;
     }
 #undef ESLAM_SEG
