@@ -281,6 +281,7 @@ struct eslam_ctx {
     float2* d_patch = nullptr;
     float* d_height = nullptr;
     uint32_t* d_occ = nullptr;               // MapView::occ
+    uint4* d_cell_tab = nullptr;             // MapView::cell_tab
     uint32_t maxp = 4;
     // host-side filter state
     uint64_t proj_event = 0, init_event = 0, hash_event = 0;
@@ -594,7 +595,9 @@ static void free_particles(eslam_ctx* ctx)
 static void free_map(eslam_ctx* ctx)
 {
     (void)hipFree(ctx->d_cells); (void)hipFree(ctx->d_patch); (void)hipFree(ctx->d_height); (void)hipFree(ctx->d_occ);
+    (void)hipFree(ctx->d_cell_tab);
     ctx->d_cells = nullptr; ctx->d_patch = nullptr; ctx->d_height = nullptr; ctx->d_occ = nullptr;
+    ctx->d_cell_tab = nullptr;
     ctx->has_map = false;
 }
 
@@ -1008,9 +1011,24 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
         HIPCHK(ctx, hipMalloc(&ctx->d_occ, occ.size() * 4));
         HIPCHK(ctx, hipMemcpy(ctx->d_occ, occ.data(), occ.size() * 4, hipMemcpyHostToDevice));
     }
+    {
+        // MapView::cell_tab: the cell's range and first patch in one 16-byte record
+        std::vector<uint4> tab(ncell);
+        for (uint64_t c = 0; c < ncell; ++c) {
+            const uint32_t b = g->cell_start[c], e = g->cell_start[c + 1];
+            const float2 f = e > b ? patch[b] : make_float2(0.0f, 0.0f);
+            uint32_t fm, fs;
+            memcpy(&fm, &f.x, 4);
+            memcpy(&fs, &f.y, 4);
+            tab[c] = make_uint4(fm, fs, b, e - b);
+        }
+        HIPCHK(ctx, hipMalloc(&ctx->d_cell_tab, ncell * sizeof(uint4)));
+        HIPCHK(ctx, hipMemcpy(ctx->d_cell_tab, tab.data(), ncell * sizeof(uint4), hipMemcpyHostToDevice));
+    }
     MapView& m = ctx->map;
     m.cell_start = ctx->d_cells;
     m.occ = ctx->d_occ;
+    m.cell_tab = ctx->d_cell_tab;
     m.patch = ctx->d_patch;
     m.height = ctx->d_height;
     m.has_height = ctx->d_height ? 1u : 0u;

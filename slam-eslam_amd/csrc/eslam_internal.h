@@ -144,6 +144,10 @@ struct MapView {
     const float* height;                 // nullable: all horizontal
     double g2l[12];
     const uint32_t* occ;                 // bit c: the shared grid has patches in cell c (the map merge's test)
+    // per cell {first patch mean, stdev (float bits), begin, count}: K1's window rows stage
+    // with one 16-byte load per cell, and a lookup off the window is one load for the cell and
+    // its first patch (the same values as cell_start / patch)
+    const uint4* cell_tab;
 };
 
 struct ContactC {

@@ -404,12 +404,19 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         b = wc.begin + 1;
         e = wc.begin + wc.count;
     } else {
-        const gmem<const uint32_t>* cell_start = kp<const uint32_t>(h, 0);
+        // the cell's record (MapView::cell_tab): its range and first patch in one load
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const gmem<const u4>* tab = kp<const u4>(kl2(KOFF(map.cell_tab)), 0);
         const uint64_t cell = (uint64_t)in * width + (uint64_t)im;
-        b = cell_start[cell];
-        e = cell_start[cell + 1];
+        const u4 ct = tab[cell];
+        b = ct.z;
+        e = ct.z + ct.w;
         if constexpr (DELTA) {
             if (b == e) return store_patch(sid, (uint32_t)cell, lz, qv, mean, stdev);
+        }
+        if (!has_height && b < e) {
+            if (patch_gate(nullptr, 0, __uint_as_float(ct.x), __uint_as_float(ct.y), lz, qv, mean, stdev)) return true;
+            ++b;
         }
     }
     for (uint32_t k = b; k < e; ++k) {
@@ -481,38 +488,30 @@ __device__ Window stage_window(const MapView& m, const StepParams& p, const Ctl*
     const int wm0 = s_w[1], wn0 = s_w[3], wn1 = s_w[4], wcols = s_w[5];
     WinCell* cells = reinterpret_cast<WinCell*>(lds);
     const int ncell = (wn1 - wn0) * wcols;
-    // two memory round trips per batch of kPer cells per thread: the batch's cell ranges
-    // first, then their first patches (a loop that waits per cell costs two round trips per
-    // cell); batches of 5 keep the prologue inside K1's register budget
-    constexpr int kPer = 5;
+    // one memory round trip per batch of kPer cells per thread: each cell's record in
+    // MapView::cell_tab is already the WinCell (range + first patch)
+    constexpr int kPer = 4;
+    const uint4* tab = m.cell_tab;
     for (int t0 = 0; t0 < ncell; t0 += kPer * kBlock) {
-        uint32_t b[kPer], e[kPer];
+        uint4 v[kPer];
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
             const int t = t0 + (int)threadIdx.x + q * kBlock;
-            b[q] = e[q] = 0;
+            v[q] = make_uint4(0u, 0u, 0u, 0u);
             if (t < ncell) {
                 const int r = t / wcols, c = t - r * wcols;
-                const uint64_t cell = (uint64_t)(wn0 + r) * m.width + (uint64_t)(wm0 + c);
-                b[q] = m.cell_start[cell];
-                e[q] = m.cell_start[cell + 1];
+                v[q] = tab[(uint64_t)(wn0 + r) * m.width + (uint64_t)(wm0 + c)];
             }
-        }
-        float2 pf[kPer];
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            pf[q] = make_float2(0.0f, 0.0f);
-            if (e[q] > b[q]) pf[q] = m.patch[b[q]];
         }
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
             const int t = t0 + (int)threadIdx.x + q * kBlock;
             if (t < ncell) {
                 WinCell wc;
-                wc.begin = b[q];
-                wc.count = e[q] - b[q];
-                wc.mean0 = pf[q].x;
-                wc.stdev0 = pf[q].y;
+                wc.mean0 = __uint_as_float(v[q].x);
+                wc.stdev0 = __uint_as_float(v[q].y);
+                wc.begin = v[q].z;
+                wc.count = v[q].w;
                 cells[t] = wc;
             }
         }
