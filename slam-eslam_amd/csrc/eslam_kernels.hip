@@ -1574,6 +1574,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
         }
     }
     bool dirty = false, moved = false;
+    bool grown = false;                  // a patch was inserted (the keys, count and box changed)
     uint32_t dropped = 0, covered = 0;
     if (i < mp.n) {
         const uint32_t sid = in.sid[src];
@@ -1710,6 +1711,7 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                     box.x = min(box.x, cm); box.y = max(box.y, cm);
                     box.z = min(box.z, cn); box.w = max(box.w, cn);
                     grew = true;
+                    grown = true;
                 }
             }
         }
@@ -1722,18 +1724,22 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
                 moved = true;
                 name = dst;
             }
-            uint4* kp = reinterpret_cast<uint4*>(ms.key + (uint64_t)dst * kStoreSlots);
+            // a store changed in place by fuses only keeps its keys, count and box: only the
+            // values go back (a copy on write writes the whole store)
+            if (moved || grown) {
+                uint4* kp = reinterpret_cast<uint4*>(ms.key + (uint64_t)dst * kStoreSlots);
 #pragma unroll
-            for (uint32_t q = 0; q < kStoreCap / 4; ++q)
-                kp[q] = make_uint4(key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]);
+                for (uint32_t q = 0; q < kStoreCap / 4; ++q)
+                    kp[q] = make_uint4(key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]);
+                ms.count[dst] = count;
+                ms.box[dst] = box;
+            }
             uint4* vp = reinterpret_cast<uint4*>(ms.val + (uint64_t)dst * kStoreSlots);
 #pragma unroll
             for (uint32_t q = 0; q < kStoreCap / 2; ++q) {
                 const float2 a = s_val[2 * q][tid], b = s_val[2 * q + 1][tid];
                 vp[q] = make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y));
             }
-            ms.count[dst] = count;
-            ms.box[dst] = box;
         }
         if (gath) st.sid[i] = name;
     }
