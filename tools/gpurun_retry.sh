@@ -4,7 +4,11 @@
 # repeated.  Waits as long as gpurun's back-off asks ("retry in Ns").
 # Usage: bash tools/gpurun_retry.sh <log> <timeout> '<command>' [attempts]
 log=$1; t=$2; cmd=$3; attempts=${4:-14}
+cd "$(dirname "$0")/.."
 for attempt in $(seq 1 $attempts); do
+  # every attempt snapshots the tree: the in-tree library must match the sources then (an
+  # edit since the last build would fail the library's build-id check on the box)
+  until timeout 900 python -c "import __graft_entry__ as g; g.build()" > /dev/null 2>&1; do sleep 60; done
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$cmd" > "$log" 2>&1
   rc=$?
   if grep -q "status=transient" "$log" && ! grep -q "run [1-9]" "$log"; then
