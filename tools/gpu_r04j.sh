@@ -33,6 +33,7 @@ tail -1 $out/smoke.log
 for r in 1 2; do
   line "4m_cur" "" --steps 30 --warmup 5
   line "4m_r04i" main --steps 30 --warmup 5
+  line "4m_k1w6" k1w6 --steps 30 --warmup 5
   line "sharded4m_cur" "" --sharded --steps 30 --warmup 5
   line "maps_cur" "" --local-maps --steps 20 --warmup 5
   line "maps_dreg" dreg --local-maps --steps 20 --warmup 5
