@@ -246,6 +246,7 @@ struct eslam_ctx {
     uint32_t* marks = nullptr;
     uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
     uint64_t* fin_word = nullptr;           // the fused finalize's epoch word (after the tile words)
+    uint32_t pub_stride = 0;                // ScanParams::pub_stride
     uint64_t fin_epoch = 0;                 // fused finalize launches so far
     uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total (sharded K3a), or
                                             // one GPU: tag << 61 | total published by K3 (zeroed at allocation)
@@ -666,7 +667,10 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     HIPCHK(ctx, hipMalloc(&ctx->marks, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->tile_first, ((cap + kRow - 1) / kRow) * 4));
     // the tile words, then (in a line of its own) the fused finalize's epoch word
-    const uint64_t fin_at = (ntiles + 15) & ~15ull;
+    // K3's kPubReplicas copies of the tile words (4 KB-aligned regions, 256 B apart beyond
+    // that, so the copies fall on different memory channels), then the epoch word's line
+    ctx->pub_stride = (uint32_t)(((ntiles + 511) & ~511ull) + 32);
+    const uint64_t fin_at = (uint64_t)kPubReplicas * ctx->pub_stride;
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, (fin_at + 16) * 8));
     HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, (fin_at + 16) * 8));          // tag / epoch 0: never published
     ctx->fin_word = ctx->tile_sum + fin_at;
@@ -1653,6 +1657,7 @@ static ScanParams scan_params(eslam_ctx* ctx, uint32_t phase_b, uint32_t normali
     sp.items = multi ? (uint32_t)kScanItems : scan_items(ctx->n);
     const uint64_t tile = (uint64_t)kBlock * sp.items;
     sp.ntiles = (uint32_t)((ctx->n + tile - 1) / tile);
+    sp.pub_stride = ctx->pub_stride;
     return sp;
 }
 

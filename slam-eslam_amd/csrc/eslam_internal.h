@@ -347,7 +347,12 @@ struct ScanParams {
     uint32_t spin_limit;                 // polls of a cross-block wait before it gives up (kSpinLimit;
                                          // 0: give up at once, eslam_gpu_debug_set_spin_limit)
     uint32_t* fault;                     // host-mapped word: kFaultTimeout when a wait gave up
+    uint32_t pub_stride;                 // one GPU: words between the replicas of K3's tile words
 };
+// K3 (one GPU) publishes each tile word in kPubReplicas copies, pub_stride words apart, and a
+// tile reads the copy of its XCD (tile % kPubReplicas): every tile reads every earlier word, so
+// one copy makes its few lines a hot spot of the memory system
+constexpr uint32_t kPubReplicas = 8;
 
 // A cross-block wait that gave up (a preceding tile's total or the fused finalize never
 // arrived) poisons the filter: the device ORs kFaultTimeout into ctl->err and into a

@@ -2288,6 +2288,19 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
 
 constexpr uint64_t kPubMask = (1ull << 61) - 1;
 
+// a tile's word into every replica (ScanParams::pub_stride), one lane each.  The sharded K3a
+// writes every replica too (one thread): the words of a launch tag never outlive a launch in
+// any copy, whichever kernel last wrote them
+__device__ __forceinline__ void publish_tile(uint64_t* pub, uint32_t stride, uint32_t tile, uint64_t w)
+{
+    if (threadIdx.x < kPubReplicas) atomic_store_agent(pub + (uint64_t)threadIdx.x * stride + tile, w);
+}
+__device__ __forceinline__ void publish_tile_1(uint64_t* pub, uint32_t stride, uint32_t tile, uint64_t w)
+{
+#pragma unroll
+    for (uint32_t r = 0; r < kPubReplicas; ++r) atomic_store_agent(pub + (uint64_t)r * stride + tile, w);
+}
+
 // sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
 // them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
 // polls (light on the memory system the tiles it waits for are still streaming through);
@@ -2369,7 +2382,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     const bool last_tile = total && tile + 1 == sp.ntiles;
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
-            atomic_store_agent(tile_sum + tile, tagw);
+            publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
             if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             if (last_tile) *total = ~0ull;
         }
@@ -2398,19 +2411,19 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
         phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
         if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
             if (tid == 0) {
-                atomic_store_agent(tile_sum + tile, tagw);
+                publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
                 if (last_tile) *total = ~0ull;               // every rank sees the fault
             }
             return;
         }
         if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+            if (tid == 0) publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
             return;
         }
         phase_b_apply<ITEMS>(st, sp, cv, t0, tid, v, mp, fl);
     } else {
         if (ctl->aborted) {              // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+            if (tid == 0) publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
             return;
         }
         phase_b_tile<ITEMS>(st, sp, ctl, t0, tid, v);
@@ -2421,7 +2434,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) fx_sum += fx_shift(v[r], shift);   // 0 past the end
     if (!resample) {
-        if (tid == 0) atomic_store_agent(tile_sum + tile, tagw);
+        if (tid == 0) publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
         return;
     }
 
@@ -2431,7 +2444,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     uint64_t t = 0;
 #pragma unroll
     for (int wv = 0; wv < kWaves; ++wv) t += s_wtot[wv];
-    if (tid == 0) atomic_store_agent(tile_sum + tile, tagw | (t & kPubMask));
+    if (tid == 0) publish_tile_1(tile_sum, sp.pub_stride, tile, tagw | (t & kPubMask));
     if (last_tile) {
         const uint64_t before = tiles_before_pub(tile_sum, tile, sp, s_red, ctl);
         if (tid == 0) *total = before == ~0ull ? ~0ull : before + t;     // ~0: every rank sees the fault
@@ -2598,9 +2611,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     const uint64_t tagw = (uint64_t)sp.tag << 61;
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
-            atomic_store_agent(tile_pub + tile, tagw);
             if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
+        publish_tile(tile_pub, sp.pub_stride, tile, tagw);
         return;
     }
     if constexpr (FUSED) {
@@ -2623,7 +2636,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     bool resample = false;
     if constexpr (!FUSED) {
         if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
-            if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+            publish_tile(tile_pub, sp.pub_stride, tile, tagw);
             return;
         }
         resample = cv->resample != 0;
@@ -2639,11 +2652,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
             ESLAM_STAMP(g_stamps_k3, 1);
             if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
-                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+                publish_tile(tile_pub, sp.pub_stride, tile, tagw);
                 return;
             }
             if (cv->aborted) {           // the update threw (k_finalize): weights stay as phase A left them
-                if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+                publish_tile(tile_pub, sp.pub_stride, tile, tagw);
                 return;
             }
             ESLAM_STAMP(g_stamps_k3, 2);
@@ -2656,7 +2669,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
     if (!resample) {
-        if (tid == 0) atomic_store_agent(tile_pub + tile, tagw);
+        publish_tile(tile_pub, sp.pub_stride, tile, tagw);
         return;
     }
     __syncthreads();
@@ -2681,8 +2694,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         agg += t;
     }
     ESLAM_STAMP(g_stamps_k3, 4);
-    if (tid == 0) atomic_store_agent(tile_pub + tile, tagw | (agg & kPubMask));
-    const uint64_t tb = tiles_before_pub(tile_pub, tile, sp, s_red, ctl);
+    publish_tile(tile_pub, sp.pub_stride, tile, tagw | (agg & kPubMask));
+    const uint64_t tb = tiles_before_pub(tile_pub + (uint64_t)(tile % kPubReplicas) * sp.pub_stride, tile, sp, s_red, ctl);
     if (tb == ~0ull) return;             // gave up waiting: poisoned, no marks
     ESLAM_STAMP(g_stamps_k3, 5);
     const uint64_t base = tb + wexcl + (tincl - run);
