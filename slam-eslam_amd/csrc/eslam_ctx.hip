@@ -245,7 +245,7 @@ struct eslam_ctx {
     void* state_mem = nullptr;
     uint32_t* marks = nullptr;
     uint32_t* tile_first = nullptr;         // row_first: source of every 64-output row's first output
-    uint64_t* fin_word = nullptr;           // the fused finalize's published copies (after the tile words)
+    uint64_t* fin_word = nullptr;           // the fused finalize's epoch word (after the tile words)
     uint32_t pub_stride = 0;                // ScanParams::pub_stride
     uint64_t fin_epoch = 0;                 // fused finalize launches so far
     uint64_t* tile_sum = nullptr;           // per scan tile: exact fixed-point weight total (sharded K3a), or
@@ -671,9 +671,8 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     // that, so the copies fall on different memory channels), then the epoch word's line
     ctx->pub_stride = (uint32_t)(((ntiles + 511) & ~511ull) + 32);
     const uint64_t fin_at = (uint64_t)kPubReplicas * ctx->pub_stride;
-    const uint64_t words = fin_at + (uint64_t)kPubReplicas * kFinImgStride;
-    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, words * 8));
-    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, words * 8));                  // tag / epoch 0: never published
+    HIPCHK(ctx, hipMalloc(&ctx->tile_sum, (fin_at + 16) * 8));
+    HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, (fin_at + 16) * 8));          // tag / epoch 0: never published
     ctx->fin_word = ctx->tile_sum + fin_at;
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
     if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));

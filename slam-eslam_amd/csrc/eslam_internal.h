@@ -353,11 +353,6 @@ struct ScanParams {
 // tile reads the copy of its XCD (tile % kPubReplicas): every tile reads every earlier word, so
 // one copy makes its few lines a hot spot of the memory system
 constexpr uint32_t kPubReplicas = 8;
-// The fused finalize publishes the control block in kPubReplicas copies as well: copy r at
-// FusedFin::fin_word + r * kFinImgStride holds the control block's words, then its epoch word
-// at kFinEpochAt (every block polls one epoch word and copies one image: one copy is a hot spot)
-constexpr uint32_t kFinImgStride = 160;
-constexpr uint32_t kFinEpochAt = 64;
 
 // A cross-block wait that gave up (a preceding tile's total or the fused finalize never
 // arrived) poisons the filter: the device ORs kFaultTimeout into ctl->err and into a

@@ -2151,41 +2151,7 @@ __device__ __forceinline__ void raise_timeout(Ctl* ctl, uint32_t* fault)
     if (fault) __hip_atomic_fetch_or(fault, kFaultTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Block 0 of a fused K3 / K3a after finalize_block (every thread): the control block goes to
-// memory (thread 0's release), every thread copies some of its words into the replicas, and
-// after the block's barrier each replica's epoch word is released (one lane each)
-__device__ __forceinline__ void publish_fin(Ctl* ctl, uint64_t* fin_word, uint64_t epoch)
-{
-    const uint32_t tid = threadIdx.x;
-    __syncthreads();                     // finalize_block's thread 0 is done with ctl
-    if (tid == 0) {
-        ctl->fin_epoch = epoch;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
-    __syncthreads();
-    for (uint32_t k = tid; k < kPubReplicas * (uint32_t)kCtlWords; k += kBlock) {
-        const uint32_t r = k / (uint32_t)kCtlWords, w = k - r * (uint32_t)kCtlWords;
-        atomic_store_agent(fin_word + (uint64_t)r * kFinImgStride + w,
-                           atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + w));
-    }
-    __syncthreads();
-    if (tid < kPubReplicas)
-        __hip_atomic_store(fin_word + (uint64_t)tid * kFinImgStride + kFinEpochAt, epoch, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// a poisoned launch's block 0 releases the epoch words without new images (the waiting blocks
-// then see an image without this epoch, retry, and report the fault)
-__device__ __forceinline__ void publish_fin_poisoned(uint64_t* fin_word, uint64_t epoch)
-{
-#pragma unroll
-    for (uint32_t r = 0; r < kPubReplicas; ++r)
-        __hip_atomic_store(fin_word + (uint64_t)r * kFinImgStride + kFinEpochAt, epoch, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// true (block-uniform) when the wait gave up: s_img is then not valid.  fin_word: the block's
-// replica (its epoch word at kFinEpochAt, the control block's image before it)
+// true (block-uniform) when the wait gave up: s_img is then not valid
 __device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word, uint64_t epoch, uint64_t* s_img,
                                               const ScanParams& sp, uint32_t* s_flag)
 {
@@ -2198,7 +2164,7 @@ __device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word
             // through this XCD's L2 to memory, where block 0's release store (a write-back of its
             // L2) has put the ctl lines.  Acquire loads (or an acquire fence) here invalidate
             // the L2 in every block: K3 53 -> 91 us at 4M, 18 -> 48 us at 256k (r03b).
-            while (!timeout && atomic_load_agent(fin_word + kFinEpochAt) != epoch) {
+            while (!timeout && atomic_load_agent(fin_word) != epoch) {
                 if (spins++ >= sp.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(8);
             }
@@ -2213,7 +2179,7 @@ __device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word
         if (!timeout) {
             uint64_t word = 0;
             for (int attempt = 0;; ++attempt) {
-                if (tid < (uint32_t)kCtlWords) word = atomic_load_agent(fin_word + tid);
+                if (tid < (uint32_t)kCtlWords) word = atomic_load_agent(reinterpret_cast<const uint64_t*>(ctl) + tid);
                 if (!__any(tid == kEpochWord && word != epoch)) break;
                 if (attempt == 64) {
                     if (tid == 0) { *s_flag = 1u; raise_timeout(ctl, sp.fault); }
@@ -2417,7 +2383,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
             publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
-            if (FUSED && tile == 0) publish_fin_poisoned(ff.fin_word, ff.epoch);
+            if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             if (last_tile) *total = ~0ull;
         }
         return;
@@ -2428,7 +2394,11 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
         if (tile == 0) {
             __shared__ FinLds s_fin;
             finalize_block(ff.shards, ff.nrec, ctl, ff.fp, s_fin);
-            publish_fin(ctl, ff.fin_word, ff.epoch);
+            __syncthreads();
+            if (tid == 0) {
+                ctl->fin_epoch = ff.epoch;       // ordered before the publication by the release
+                __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     const Ctl* cv = FUSED ? reinterpret_cast<const Ctl*>(s_img) : ctl;
@@ -2439,7 +2409,7 @@ __global__ void __launch_bounds__(kBlock) k_normalize_scan(DevState s0, DevState
         double mp[ITEMS];
         uint32_t fl[ITEMS];
         phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
-        if (fin_wait_copy(ctl, ff.fin_word + (uint64_t)(blockIdx.x % kPubReplicas) * kFinImgStride, ff.epoch, s_img, sp, &s_flag)) {
+        if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
             if (tid == 0) {
                 publish_tile_1(tile_sum, sp.pub_stride, tile, tagw);
                 if (last_tile) *total = ~0ull;               // every rank sees the fault
@@ -2641,7 +2611,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     const uint64_t tagw = (uint64_t)sp.tag << 61;
     if (ctl->err & kFaultTimeout) {      // poisoned: nothing is written (the waits of the other blocks end)
         if (tid == 0) {
-            if (FUSED && tile == 0) publish_fin_poisoned(ff.fin_word, ff.epoch);
+            if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         publish_tile(tile_pub, sp.pub_stride, tile, tagw);
         return;
@@ -2650,7 +2620,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         if (tile == 0) {
             __shared__ FinLds s_fin;
             finalize_block(ff.shards, ff.nrec, ctl, ff.fp, s_fin);
-            publish_fin(ctl, ff.fin_word, ff.epoch);
+            __syncthreads();
+            if (tid == 0) {
+                ctl->fin_epoch = ff.epoch;       // ordered before the publication by the release
+                __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     // the finalize's outputs: ctl itself (k_finalize ran before this launch), or its copy in
@@ -2677,7 +2651,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             uint32_t fl[ITEMS];
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
             ESLAM_STAMP(g_stamps_k3, 1);
-            if (fin_wait_copy(ctl, ff.fin_word + (uint64_t)(blockIdx.x % kPubReplicas) * kFinImgStride, ff.epoch, s_img, sp, &s_flag)) {
+            if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
                 publish_tile(tile_pub, sp.pub_stride, tile, tagw);
                 return;
             }
