@@ -2314,16 +2314,23 @@ __device__ __forceinline__ void publish_tile_1(uint64_t* pub, uint32_t stride, u
 // sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
 // them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
 // polls (light on the memory system the tiles it waits for are still streaming through);
-// the other waves wait at the barrier.
+// the other waves wait at the barrier.  incl (one GPU's K3): the inclusive prefixes tiles
+// publish after their own look-back; the word of tile count - 1, loaded with the first batch
+// and with every poll, replaces the whole sum once it carries this launch's tag (a tile of
+// the second round of blocks finds it at once; nothing ever waits for it).
 // A wait that gives up (sp.spin_limit polls) poisons the filter and returns ~0.
 __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, const ScanParams& sp,
-                                                     uint64_t* s_red, Ctl* __restrict__ ctl)
+                                                     uint64_t* s_red, Ctl* __restrict__ ctl,
+                                                     const uint64_t* __restrict__ incl = nullptr)
 {
     const uint32_t tag = sp.tag;
     const uint32_t tid = threadIdx.x;
     if (tid < 64) {
         uint64_t acc = 0;
         bool timeout = sp.spin_limit == 0 && count > 0;   // testing: give up at once
+        const bool with_inc = incl != nullptr && count > 0;
+        uint64_t inc = with_inc ? atomic_load_agent(incl + count - 1) : 0ull;   // one word, every lane
+        bool have_inc = false;
         for (uint32_t b0 = 0; !timeout && b0 < count; b0 += 8u * 64u) {
             uint64_t v[8];
 #pragma unroll
@@ -2333,89 +2340,26 @@ __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict_
             }
             uint32_t spins = 0;
             for (;;) {
+                have_inc = with_inc && (uint32_t)(inc >> 61) == tag;     // wave-uniform
+                if (have_inc) break;
                 bool ready = true;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
                 if (__ballot(!ready) == 0ull) break;
                 if (spins++ >= sp.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(ESLAM_LOOKBACK_SLEEP);
+                if (with_inc) inc = atomic_load_agent(incl + count - 1);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const uint32_t k = b0 + (uint32_t)q * 64u + tid;
                     if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
                 }
             }
+            if (have_inc) break;
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
         }
-        acc = wave_sum_u64(acc);
-        if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
-        if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
-    }
-    __syncthreads();
-    return s_red[0];
-}
-
-// One GPU's K3: the sum of the totals of tiles [0, count), walked backwards in windows of 512
-// tiles (8 per lane).  Each tile also publishes its inclusive prefix after its own look-back
-// (incl); the prefix words of a window's lowest 64 tiles are read with its totals (one per
-// lane: any prefix in the window serves), and the highest of them that carries the launch tag,
-// tile j, ends the walk: prefix(j) + the totals after j.  A window without one adds all its
-// totals and the walk moves to the previous window.  Only
-// totals are ever waited for (every tile publishes its total before its look-back), never a
-// prefix, so no chain of waits forms; a tile of the second round of blocks finds the prefix of
-// a first-round tile in its first window instead of reading every earlier total.
-__device__ __forceinline__ uint64_t tiles_before_lookback(const uint64_t* __restrict__ pub, const uint64_t* __restrict__ incl,
-                                                          uint32_t count, const ScanParams& sp, uint64_t* s_red,
-                                                          Ctl* __restrict__ ctl)
-{
-    const uint32_t tag = sp.tag;
-    const uint32_t tid = threadIdx.x;
-    if (tid < 64) {
-        uint64_t acc = 0;
-        bool timeout = sp.spin_limit == 0 && count > 0;   // testing: give up at once
-        uint32_t hi = count;
-        while (!timeout && hi > 0) {
-            const uint32_t lo = hi > 512u ? hi - 512u : 0u;
-            uint64_t v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t k = lo + (uint32_t)q * 64u + tid;
-                v[q] = k < hi ? atomic_load_agent(pub + k) : ((uint64_t)tag << 61);
-            }
-            const uint32_t ku = lo + tid;    // this lane's prefix word: tile lo + lane
-            uint64_t u = ku < hi ? atomic_load_agent(incl + ku) : 0ull;
-            uint32_t spins = 0;
-            uint32_t j1 = 0;                 // 1 + the highest tile of the window with a prefix (0: none)
-            for (;;) {
-                const uint32_t c = (ku < hi && (uint32_t)(u >> 61) == tag) ? ku + 1u : 0u;
-                j1 = wave_butterfly(c, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
-                bool ready = true;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t k = lo + (uint32_t)q * 64u + tid;
-                    ready &= k < j1 || (uint32_t)(v[q] >> 61) == tag;   // the totals after j
-                }
-                if (__ballot(!ready) == 0ull) break;
-                if (spins++ >= sp.spin_limit) { timeout = true; break; }
-                __builtin_amdgcn_s_sleep(ESLAM_LOOKBACK_SLEEP);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint32_t k = lo + (uint32_t)q * 64u + tid;
-                    if (k < hi && (uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
-                }
-                if (ku < hi && (uint32_t)(u >> 61) != tag) u = atomic_load_agent(incl + ku);
-            }
-            if (timeout) break;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t k = lo + (uint32_t)q * 64u + tid;
-                if (k < hi && k + 1u > j1) acc += v[q] & kPubMask;  // the totals after j
-            }
-            if (ku + 1u == j1) acc += u & kPubMask;                  // prefix(j) covers [0, j]
-            if (j1 != 0u) break;
-            hi = lo;
-        }
+        if (have_inc) acc = tid == 0 ? (inc & kPubMask) : 0ull;
         acc = wave_sum_u64(acc);
         if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
         if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
@@ -2775,7 +2719,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     publish_tile(tile_pub, sp.pub_stride, tile, tagw | (agg & kPubMask));
     uint64_t* const incl_pub = tile_pub + kPubReplicas * (uint64_t)sp.pub_stride;
     const uint64_t rep_off = (uint64_t)(tile % kPubReplicas) * sp.pub_stride;
-    const uint64_t tb = tiles_before_lookback(tile_pub + rep_off, incl_pub + rep_off, tile, sp, s_red, ctl);
+    const uint64_t tb = tiles_before_pub(tile_pub + rep_off, tile, sp, s_red, ctl, incl_pub + rep_off);
     if (tb == ~0ull) {                   // gave up waiting: poisoned, no marks
         publish_tile(incl_pub, sp.pub_stride, tile, tagw);
         return;
