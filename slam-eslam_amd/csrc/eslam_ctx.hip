@@ -670,8 +670,7 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     // K3's kPubReplicas copies of the tile words (4 KB-aligned regions, 256 B apart beyond
     // that, so the copies fall on different memory channels), then the epoch word's line
     ctx->pub_stride = (uint32_t)(((ntiles + 511) & ~511ull) + 32);
-    // (the aggregate words' replicas, then the inclusive prefixes' replicas)
-    const uint64_t fin_at = 2ull * kPubReplicas * ctx->pub_stride;
+    const uint64_t fin_at = (uint64_t)kPubReplicas * ctx->pub_stride;
     HIPCHK(ctx, hipMalloc(&ctx->tile_sum, (fin_at + 16) * 8));
     HIPCHK(ctx, hipMemset(ctx->tile_sum, 0, (fin_at + 16) * 8));          // tag / epoch 0: never published
     ctx->fin_word = ctx->tile_sum + fin_at;

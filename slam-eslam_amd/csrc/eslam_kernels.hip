@@ -2298,13 +2298,6 @@ __device__ __forceinline__ void publish_tile(uint64_t* pub, uint32_t stride, uin
 {
     if (threadIdx.x < kPubReplicas) atomic_store_agent(pub + (uint64_t)threadIdx.x * stride + tile, w);
 }
-// a one-GPU K3 tile that leaves before its look-back: its total and its inclusive prefix as
-// this launch's empty words (every launch writes every tile's words of both kinds)
-__device__ __forceinline__ void publish_exit(uint64_t* pub, uint32_t stride, uint32_t tile, uint64_t tagw)
-{
-    publish_tile(pub, stride, tile, tagw);
-    publish_tile(pub + kPubReplicas * (uint64_t)stride, stride, tile, tagw);
-}
 __device__ __forceinline__ void publish_tile_1(uint64_t* pub, uint32_t stride, uint32_t tile, uint64_t w)
 {
 #pragma unroll
@@ -2314,23 +2307,16 @@ __device__ __forceinline__ void publish_tile_1(uint64_t* pub, uint32_t stride, u
 // sum of the published totals of tiles [0, count) (any order: exact integers).  Wave 0 reads
 // them, 8 loads in flight per lane, and polls the unpublished ones with a sleep between
 // polls (light on the memory system the tiles it waits for are still streaming through);
-// the other waves wait at the barrier.  incl (one GPU's K3): the inclusive prefixes tiles
-// publish after their own look-back; the word of tile count - 1, loaded with the first batch
-// and with every poll, replaces the whole sum once it carries this launch's tag (a tile of
-// the second round of blocks finds it at once; nothing ever waits for it).
+// the other waves wait at the barrier.
 // A wait that gives up (sp.spin_limit polls) poisons the filter and returns ~0.
 __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict__ pub, uint32_t count, const ScanParams& sp,
-                                                     uint64_t* s_red, Ctl* __restrict__ ctl,
-                                                     const uint64_t* __restrict__ incl = nullptr)
+                                                     uint64_t* s_red, Ctl* __restrict__ ctl)
 {
     const uint32_t tag = sp.tag;
     const uint32_t tid = threadIdx.x;
     if (tid < 64) {
         uint64_t acc = 0;
         bool timeout = sp.spin_limit == 0 && count > 0;   // testing: give up at once
-        const bool with_inc = incl != nullptr && count > 0;
-        uint64_t inc = with_inc ? atomic_load_agent(incl + count - 1) : 0ull;   // one word, every lane
-        bool have_inc = false;
         for (uint32_t b0 = 0; !timeout && b0 < count; b0 += 8u * 64u) {
             uint64_t v[8];
 #pragma unroll
@@ -2340,26 +2326,21 @@ __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict_
             }
             uint32_t spins = 0;
             for (;;) {
-                have_inc = with_inc && (uint32_t)(inc >> 61) == tag;     // wave-uniform
-                if (have_inc) break;
                 bool ready = true;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
                 if (__ballot(!ready) == 0ull) break;
                 if (spins++ >= sp.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(ESLAM_LOOKBACK_SLEEP);
-                if (with_inc) inc = atomic_load_agent(incl + count - 1);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const uint32_t k = b0 + (uint32_t)q * 64u + tid;
                     if ((uint32_t)(v[q] >> 61) != tag) v[q] = atomic_load_agent(pub + k);
                 }
             }
-            if (have_inc) break;
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc += v[q] & kPubMask;
         }
-        if (have_inc) acc = tid == 0 ? (inc & kPubMask) : 0ull;
         acc = wave_sum_u64(acc);
         if (tid == 0) s_red[0] = timeout ? ~0ull : acc;
         if (timeout && tid == 0) raise_timeout(ctl, sp.fault);
@@ -2635,7 +2616,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         if (tid == 0) {
             if (FUSED && tile == 0) __hip_atomic_store(ff.fin_word, ff.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
-        publish_exit(tile_pub, sp.pub_stride, tile, tagw);
+        publish_tile(tile_pub, sp.pub_stride, tile, tagw);
         return;
     }
     if constexpr (FUSED) {
@@ -2658,7 +2639,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     bool resample = false;
     if constexpr (!FUSED) {
         if (cv->aborted) {               // the update threw (k_finalize): weights stay as phase A left them
-            publish_exit(tile_pub, sp.pub_stride, tile, tagw);
+            publish_tile(tile_pub, sp.pub_stride, tile, tagw);
             return;
         }
         resample = cv->resample != 0;
@@ -2674,11 +2655,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
             phase_b_load<ITEMS>(st, sp, t0, tid, v, mp, fl);
             ESLAM_STAMP(g_stamps_k3, 1);
             if (fin_wait_copy(ctl, ff.fin_word, ff.epoch, s_img, sp, &s_flag)) {
-                publish_exit(tile_pub, sp.pub_stride, tile, tagw);
+                publish_tile(tile_pub, sp.pub_stride, tile, tagw);
                 return;
             }
             if (cv->aborted) {           // the update threw (k_finalize): weights stay as phase A left them
-                publish_exit(tile_pub, sp.pub_stride, tile, tagw);
+                publish_tile(tile_pub, sp.pub_stride, tile, tagw);
                 return;
             }
             ESLAM_STAMP(g_stamps_k3, 2);
@@ -2691,7 +2672,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
         for (int r = 0; r < ITEMS; ++r) s_u.v[skew(r * kBlock + (int)tid)] = v[r];
     }
     if (!resample) {
-        publish_exit(tile_pub, sp.pub_stride, tile, tagw);
+        publish_tile(tile_pub, sp.pub_stride, tile, tagw);
         return;
     }
     __syncthreads();
@@ -2717,14 +2698,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     }
     ESLAM_STAMP(g_stamps_k3, 4);
     publish_tile(tile_pub, sp.pub_stride, tile, tagw | (agg & kPubMask));
-    uint64_t* const incl_pub = tile_pub + kPubReplicas * (uint64_t)sp.pub_stride;
-    const uint64_t rep_off = (uint64_t)(tile % kPubReplicas) * sp.pub_stride;
-    const uint64_t tb = tiles_before_pub(tile_pub + rep_off, tile, sp, s_red, ctl, incl_pub + rep_off);
-    if (tb == ~0ull) {                   // gave up waiting: poisoned, no marks
-        publish_tile(incl_pub, sp.pub_stride, tile, tagw);
-        return;
-    }
-    publish_tile(incl_pub, sp.pub_stride, tile, tagw | ((tb + agg) & kPubMask));
+    const uint64_t tb = tiles_before_pub(tile_pub + (uint64_t)(tile % kPubReplicas) * sp.pub_stride, tile, sp, s_red, ctl);
+    if (tb == ~0ull) return;             // gave up waiting: poisoned, no marks
     ESLAM_STAMP(g_stamps_k3, 5);
     const uint64_t base = tb + wexcl + (tincl - run);
 
