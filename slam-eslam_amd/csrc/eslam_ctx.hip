@@ -1639,10 +1639,7 @@ static uint32_t scan_items(uint64_t n)
     // measured (round-2 A/B, profiles/r02/ab_items_256k_fused.log; bench step at 64k / 256k / 1M / 4M / 16M): 1 item +5 % at
     // 64k and 256k (over 2 items, themselves +19 % over 8 at 256k), 2 or 4 items +4 % at 1M,
     // 8 items best from 4M on (fewer tiles_before re-sums)
-#ifndef ESLAM_K3_ONE_ITEM_MAX            // experiment builds
-#define ESLAM_K3_ONE_ITEM_MAX (1ull << 18)
-#endif
-    if (n <= (uint64_t)ESLAM_K3_ONE_ITEM_MAX) return 1u;
+    if (n <= (1ull << 18)) return 1u;
     return n <= (1ull << 19) ? 2u : (n <= (2ull << 20) ? 4u : (uint32_t)kScanItems);
 }
 

@@ -352,10 +352,7 @@ struct ScanParams {
 // K3 (one GPU) publishes each tile word in kPubReplicas copies, pub_stride words apart, and a
 // tile reads the copy of its XCD (tile % kPubReplicas): every tile reads every earlier word, so
 // one copy makes its few lines a hot spot of the memory system
-#ifndef ESLAM_PUB_REPLICAS                // experiment builds
-#define ESLAM_PUB_REPLICAS 8
-#endif
-constexpr uint32_t kPubReplicas = ESLAM_PUB_REPLICAS;
+constexpr uint32_t kPubReplicas = 8;
 
 // A cross-block wait that gave up (a preceding tile's total or the fused finalize never
 // arrived) poisons the filter: the device ORs kFaultTimeout into ctl->err and into a
