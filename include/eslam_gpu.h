@@ -187,7 +187,9 @@ const char* eslam_gpu_build_id(void);
 int eslam_gpu_set_stream(eslam_ctx* ctx, void* hip_stream);
 
 /* ---- environment: PoseEstimator::setEnvironment src/PoseEstimator.cpp:47-62 and
- * GridAccess::setMap src/PoseEstimator.hpp:68-95 (shared map, useShared = true)           */
+ * GridAccess::setMap src/PoseEstimator.hpp:68-95 (shared map, useShared = true).  Device
+ * memory: 8 bytes per patch (+4 with heights) and about 20.2 bytes per cell (range word,
+ * a 16-byte record of the cell's range and first patch, one occupancy bit)                 */
 int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* grid);
 
 /* ---- initialisation -------------------------------------------------------------------
