@@ -1618,10 +1618,7 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
     const double motion = sqrt(p.mu[0] * p.mu[0] + p.mu[1] * p.mu[1]) +
                           6.0 * sqrt(in->sample_cov[0] + in->sample_cov[4]);
     p.win_margin = reach + motion + 0.05;
-#ifndef ESLAM_WINDOW_MIN_N               // experiment builds: no LDS window below this many particles
-#define ESLAM_WINDOW_MIN_N 0
-#endif
-    p.use_window = ((c.flags & ESLAM_FLAG_NO_MAP_LDS) || ctx->n < (uint64_t)ESLAM_WINDOW_MIN_N) ? 0u : 1u;
+    p.use_window = (c.flags & ESLAM_FLAG_NO_MAP_LDS) ? 0u : 1u;
     p.me2 = c.measurement_error * c.measurement_error;
     p.radius = c.contact_point_radius;
     p.corr = c.contact_likelihood_correction;
