@@ -2287,9 +2287,6 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
 }
 
 constexpr uint64_t kPubMask = (1ull << 61) - 1;
-#ifndef ESLAM_LOOKBACK_SLEEP             // experiment builds: the look-back's poll interval (x 64 cycles)
-#define ESLAM_LOOKBACK_SLEEP 8
-#endif
 
 // a tile's word into every replica (ScanParams::pub_stride), one lane each.  The sharded K3a
 // writes every replica too (one thread): the words of a launch tag never outlive a launch in
@@ -2331,7 +2328,7 @@ __device__ __forceinline__ uint64_t tiles_before_pub(const uint64_t* __restrict_
                 for (int q = 0; q < 8; ++q) ready &= (uint32_t)(v[q] >> 61) == tag;
                 if (__ballot(!ready) == 0ull) break;
                 if (spins++ >= sp.spin_limit) { timeout = true; break; }
-                __builtin_amdgcn_s_sleep(ESLAM_LOOKBACK_SLEEP);
+                __builtin_amdgcn_s_sleep(8);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const uint32_t k = b0 + (uint32_t)q * 64u + tid;
