@@ -182,15 +182,35 @@ def cpu_baseline(args, grid, flags=0, scan=None):
     return out
 
 
+def visible_gpus():
+    """GPUs this process could open, counted without any HIP or torch.cuda call: the KFD
+    topology's GPU nodes (simd_count > 0), narrowed by a *_VISIBLE_DEVICES list if one is set.
+    The parent of a multi-rank run must not initialise the GPU (it forks the ranks)."""
+    import glob
+    n = 0
+    for prop in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(prop) as fh:
+                kv = dict(line.split()[:2] for line in fh if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(kv.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
 def spawn_ranks(args):
     """`bench.py --gpus N` without a launcher: start N ranks of this script as child processes
     (fresh interpreters, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), forward rank 0's JSON line
     and exit with the worst exit code.  The parent never touches the GPU: it counts devices
-    (no HIP initialisation on this image) and execs nothing."""
+    from the KFD topology in /sys (visible_gpus) and execs nothing."""
     import subprocess
     import socket
-    import torch
-    visible = torch.cuda.device_count()
+    visible = visible_gpus()
     if visible < args.gpus:
         sys.stderr.write(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible\n")
         sys.exit(2)

@@ -177,7 +177,14 @@ typedef struct eslam_ctx eslam_ctx;
 
 /* PoseEstimator(odometry, config) / EmbodiedSlamFilter(odoConfig, config): binds `device`. */
 int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx** out);
+/* Never collective: an exchange a sharded filter still owes (see eslam_gpu_set_comm) is
+ * dropped, so destroy is safe on one rank's error path and after the communicator is gone.
+ * SPMD code calls eslam_gpu_finish on every rank first.                                  */
 void eslam_gpu_destroy(eslam_ctx* ctx);
+/* Collective on a sharded filter (every rank, at the same point): completes the last
+ * update's deferred exchange if this rank still owes it, then waits for the stream; on one
+ * GPU it only waits for the stream.                                                       */
+int eslam_gpu_finish(eslam_ctx* ctx);
 const char* eslam_gpu_last_error(const eslam_ctx* ctx);
 int eslam_gpu_abi_version(void);
 /* SHA-256 (hex) of the sources, headers and compiler flags the library was built from
@@ -376,7 +383,7 @@ typedef struct eslam_comm {
  * rank-local getters (download, records, particle maps, RNG state, hash poses) may be
  * called by any subset of ranks: the only collective they can run is the previous
  * update's deferred exchange, which every rank completes exactly once -- in a getter, in
- * its next collective call or in eslam_gpu_destroy -- so the ranks stay matched.       */
+ * its next collective call or in eslam_gpu_finish -- so the ranks stay matched.         */
 int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64_t n_global, const uint64_t* shard_gbase);
 
 /* ---- multi-GPU over RCCL, driven from the library (no callback into the host language) --

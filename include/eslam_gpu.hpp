@@ -575,7 +575,10 @@ public:
         const eslam_config c = config.toC(hash);
         if (eslam_gpu_create(&c, device, &ctx_) != ESLAM_OK) throw std::runtime_error("eslam_gpu_create failed (no MI355X visible?)");
     }
-    ~PoseEstimator() { eslam_gpu_destroy(ctx_); }
+    ~PoseEstimator() { eslam_gpu_destroy(ctx_); }   // never collective (include/eslam_gpu.h)
+    // multi-GPU: the collective end of a sharded filter's life -- every rank calls it before
+    // the filter is destroyed, completing an exchange the rank may still owe
+    void finish() { check(ctx_, eslam_gpu_finish(ctx_)); }
     PoseEstimator(const PoseEstimator&) = delete;
     PoseEstimator& operator=(const PoseEstimator&) = delete;
 
@@ -801,7 +804,9 @@ public:
     // any); every call above that uses the particles on the device runs it first.  On a
     // sharded filter the write-back is collective (eslam_gpu_write_particles): a rank holding
     // a view writes back even without edits, so the ranks stay matched as long as they call
-    // getParticles() at the same points (SPMD order, include/eslam_gpu.h)
+    // getParticles() at the same points (SPMD order, include/eslam_gpu.h).  The contract is on
+    // the caller: a rank that never took a view (view_valid_ false) skips the write-back, so
+    // either every rank calls getParticles() at a point or none does
     void flush() const
     {
         if (!view_valid_) return;

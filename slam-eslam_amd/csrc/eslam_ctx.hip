@@ -607,9 +607,9 @@ namespace { void rccl_release(eslam_ctx* ctx); }
 extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
 {
     if (!ctx) return;
-    // a deferred exchange is completed first: a rank that settled it through a getter (its
-    // own all_to_all_v) is matched by the others here, so no rank is left waiting in it
-    if (ctx->xpend && !ctx->poisoned) (void)settle(ctx);
+    // never collective: a deferred exchange still pending is dropped (eslam_gpu_finish is the
+    // collective that completes it); destroy may run on an error path of one rank or after the
+    // caller's communicator is gone, so it must not wait for the other ranks
     ctx->xpend = false;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->xstream) { (void)hipStreamSynchronize(ctx->xstream); (void)hipStreamDestroy(ctx->xstream); }
@@ -630,6 +630,17 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     for (auto& e : ctx->mring) if (e) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+// collective on a sharded filter (every rank calls it at the same point): completes the last
+// update's deferred exchange if this rank still owes it; a no-op otherwise
+extern "C" int eslam_gpu_finish(eslam_ctx* ctx)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    if (ctx->poisoned) { ctx->xpend = false; return ESLAM_OK; }
+    if (const int rc_ = settle(ctx)) return rc_;
+    if (ctx->stream) HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return ESLAM_OK;
 }
 
 extern "C" int eslam_gpu_set_stream(eslam_ctx* ctx, void* s)
@@ -1341,17 +1352,23 @@ extern "C" int eslam_gpu_download_particles(eslam_ctx* ctx, eslam_particles* p)
     return ESLAM_OK;
 }
 
-extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p)
+// the largest weight of this context's particles (NaN and negative weights skipped), as
+// eslam_gpu_upload_particles computes the weight scale
+static int max_weight_local(eslam_ctx* ctx, double* out)
 {
-    if (!ctx || !p || first > ctx->n || count > ctx->n - first) return ESLAM_ERR_INVALID_ARG;
-    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
-    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
-    int rc = materialize(ctx);               // the particles the caller saw: any pending gather done
-    if (!rc) rc = read_ctl(ctx);
-    if (rc) return rc;
-    // sharded: a collective (every rank calls it, count may be 0), whose weight-scale
-    // agreement runs whether or not this rank writes weights
-    if (!count && !ctx->sharded) return ESLAM_OK;
+    const DevState& s = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip];
+    std::vector<double> w(ctx->n);
+    HIPCHK(ctx, hipMemcpy(w.data(), s.w, ctx->n * 8, hipMemcpyDeviceToHost));
+    double mx = 0;
+    for (uint64_t i = 0; i < ctx->n; ++i) if (w[i] > mx) mx = w[i];
+    *out = mx;
+    return ESLAM_OK;
+}
+
+// eslam_gpu_write_particles' rank-local part: the fields of p into [first, first + count)
+static int write_particles_local(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p)
+{
+    if (!count) return ESLAM_OK;
     const DevState& s = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip];
     const uint64_t b = count * 8;
     const double* src[7] = {p->x, p->y, p->orientation, p->zpos, p->zsigma, p->weight, p->mprob};
@@ -1371,26 +1388,50 @@ extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_
         HIPCHK(ctx, hipMemcpyAsync(s.flags + first, fl.data(), count, hipMemcpyHostToDevice, ctx->stream));
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if (!p->weight && !ctx->sharded) return ESLAM_OK;
     // the weight scale of the next update, from the largest weight of the whole set exactly
-    // as eslam_gpu_upload_particles computes it (NaN and negative weights skipped)
-    std::vector<double> w(ctx->n);
-    HIPCHK(ctx, hipMemcpy(w.data(), s.w, ctx->n * 8, hipMemcpyDeviceToHost));
-    double mx = 0;
-    for (uint64_t i = 0; i < ctx->n; ++i) if (w[i] > mx) mx = w[i];
-    if (ctx->sharded) {
-        uint64_t* h = ctx->mg_host;
-        memcpy(&h[mg::kMaxW], &mx, 8);
-        HIPCHK(ctx, hipMemcpy(ctx->mg + mg::kMaxW, &h[mg::kMaxW], 8, hipMemcpyHostToDevice));
-        rc = comm_allgather(ctx, ctx->mg + mg::kMaxW, ctx->mg + mg::kMaxWAll, 8);
+    // as eslam_gpu_upload_particles computes it (one GPU: only when weights were written)
+    if (p->weight && !ctx->sharded) {
+        double mx = 0;
+        const int rc = max_weight_local(ctx, &mx);
         if (rc) return rc;
-        HIPCHK(ctx, hipMemcpy(&h[mg::kMaxWAll], ctx->mg + mg::kMaxWAll, 8 * ctx->comm.nranks, hipMemcpyDeviceToHost));
-        for (int r = 0; r < ctx->comm.nranks; ++r) {
-            double v;
-            memcpy(&v, &h[mg::kMaxWAll + r], 8);
-            if (v > mx) mx = v;
-        }
+        ctx->ctl_host->wexp = dm_weight_exp(mx);
+        return write_ctl(ctx);
     }
+    return ESLAM_OK;
+}
+
+extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, const eslam_particles* p)
+{
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    // sharded: a collective (every rank calls it, count may be 0).  A rank whose own part fails
+    // still takes part in the weight-scale all_gather, with a NaN that tells the others to fail
+    // too, so no rank is left waiting in it (include/eslam_gpu.h)
+    int rc = (!p || first > ctx->n || count > ctx->n - first) ? fail(ctx, ESLAM_ERR_INVALID_ARG, "write_particles: bad range")
+                                                              : ESLAM_OK;
+    if (!rc) rc = settle(ctx);                          // a deferred sharded exchange first
+    if (!rc) rc = check_poisoned(ctx);
+    if (!rc) rc = materialize(ctx);                     // the particles the caller saw: any pending gather done
+    if (!rc) rc = read_ctl(ctx);
+    if (!rc) rc = write_particles_local(ctx, first, count, p);
+    if (!ctx->sharded) return rc;
+    double mx = 0;
+    if (!rc) rc = max_weight_local(ctx, &mx);
+    if (rc) mx = NAN;
+    uint64_t* h = ctx->mg_host;
+    memcpy(&h[mg::kMaxW], &mx, 8);
+    HIPCHK(ctx, hipMemcpy(ctx->mg + mg::kMaxW, &h[mg::kMaxW], 8, hipMemcpyHostToDevice));
+    const int crc = comm_allgather(ctx, ctx->mg + mg::kMaxW, ctx->mg + mg::kMaxWAll, 8);
+    if (crc) return rc ? rc : crc;
+    HIPCHK(ctx, hipMemcpy(&h[mg::kMaxWAll], ctx->mg + mg::kMaxWAll, 8 * ctx->comm.nranks, hipMemcpyDeviceToHost));
+    bool peer_failed = false;
+    for (int r = 0; r < ctx->comm.nranks; ++r) {
+        double v;
+        memcpy(&v, &h[mg::kMaxWAll + r], 8);
+        if (v != v) peer_failed = true;
+        else if (v > mx) mx = v;
+    }
+    if (rc) return rc;
+    if (peer_failed) return fail(ctx, ESLAM_ERR_COMM, "write_particles failed on another rank");
     ctx->ctl_host->wexp = dm_weight_exp(mx);
     return write_ctl(ctx);
 }

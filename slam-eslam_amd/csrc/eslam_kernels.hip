@@ -2171,10 +2171,14 @@ __device__ __forceinline__ bool fin_wait_copy(Ctl* ctl, const uint64_t* fin_word
             *s_flag = timeout ? 1u : 0u;
             if (timeout) raise_timeout(ctl, sp.fault);
         }
+        // lane 0's verdict for the whole wave (the other lanes skip the copy's retry loop)
+        timeout = __builtin_amdgcn_readfirstlane(timeout ? 1 : 0) != 0;
         // the copy must carry this launch's epoch (ctl->fin_epoch, written by block 0 before its
-        // release): a stale line would show an older one.  The relaxed loads rely on gfx950's
-        // agent-scope loads missing this XCD's L2 for lines another XCD wrote back; should
-        // that ever not hold, the copy is retried and then reported (ESLAM_ERR_HIP), never used
+        // release): a stale copy of the line holding it would show an older one.  The relaxed
+        // loads rely on gfx950's agent-scope loads missing this XCD's L2 for lines another XCD
+        // wrote back.  Only the epoch's own 128-byte line is validated: were that assumption to
+        // fail for another line of the block (resample, scan_shift, aborted sit in other lines),
+        // this check would not see it -- it guards the common failure, not every one
         constexpr uint32_t kEpochWord = (uint32_t)(offsetof(Ctl, fin_epoch) / 8);
         if (!timeout) {
             uint64_t word = 0;

@@ -54,6 +54,7 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_create.argtypes = [C.POINTER(A.Config), C.c_int, C.POINTER(vp)]
     L.eslam_gpu_destroy.argtypes = [vp]
     L.eslam_gpu_destroy.restype = None
+    L.eslam_gpu_finish.argtypes = [vp]
     L.eslam_gpu_last_error.argtypes = [vp]
     L.eslam_gpu_last_error.restype = C.c_char_p
     L.eslam_gpu_set_stream.argtypes = [vp, vp]
@@ -124,6 +125,11 @@ class GpuFilter:
         if getattr(self, "h", None):
             self.L.eslam_gpu_destroy(self.h)
             self.h = None
+
+    def finish(self):
+        """eslam_gpu_finish: collective on a sharded filter (completes an exchange still owed)."""
+        if getattr(self, "h", None):
+            self._check(self.L.eslam_gpu_finish(self.h))
 
     def __del__(self):
         self.close()

@@ -138,6 +138,9 @@ class ShardedGpuFilter:
         return getattr(self.f, name)
 
     def close(self):
+        """Collective: every rank completes the exchange it may still owe, then frees its context."""
+        if getattr(self.f, "h", None):
+            self.f.finish()
         self.f.close()
 
 
@@ -172,4 +175,7 @@ class RcclShardedGpuFilter:
         return getattr(self.f, name)
 
     def close(self):
+        """Collective: every rank completes the exchange it may still owe, then frees its context."""
+        if getattr(self.f, "h", None):
+            self.f.finish()
         self.f.close()

@@ -172,8 +172,9 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     if name == "getter0":
         # forced updates back to back, then only the first rank reads its particles (a
         # rank-local getter, which completes the last update's deferred exchange on a sharded
-        # GPU filter) and every rank closes its filter: destroy completes the exchange on the
-        # other ranks, so no rank is left waiting in it
+        # GPU filter) and every rank closes its filter: close() runs the collective
+        # eslam_gpu_finish, which completes the exchange on the other ranks, so no rank is
+        # left waiting in it (destroy itself never communicates)
         for st in S.step_stream(steps):
             f.step(st)
         if lo == 0:
