@@ -1780,4 +1780,64 @@ DM_FN uint32_t dm_merge_cell(double bx, double by, double co, double sn, double 
     return dm_merge_cell_mn(bx, by, co, sn, sx, sy, inv_x, inv_y, width, height, &m, &n);
 }
 
+
+/* ---- per-particle local maps: a window of tiles of 8 x 8 grid cells -----
+ * A particle's own map covers (2 hx + 1) x (2 hy + 1) tiles centred on the tile under the
+ * particle at its last map update; tile (a, b) (a = m >> 3, b = n >> 3) lives in slot
+ * (a mod wx) + wx (b mod wy), so a window that moves keeps every tile it still covers in
+ * place.  A page holds the tile's 64 cells (row-major, cell (m & 7) + 8 (n & 7)), each one
+ * patch {mean, stdev}; a cell holds a patch iff stdev >= 0 (an empty cell stores -1).    */
+#define DM_LM_TILE_BITS 3
+#define DM_LM_PAGE_CELLS 64u
+#define DM_LM_NONE 0xffffffffu               /* a slot with no page                           */
+#define DM_LM_UNSET ((int32_t)0x80000000)    /* a map that has never been centred (empty)     */
+#define DM_LM_MAX_HALF 15u                   /* at most 31 x 31 tiles per window              */
+/* half-width in tiles: every cell within r metres of any cell of the centre tile lies in the
+ * window (maxSensorRange, src/Configuration.hpp:107: 3 m at 0.1 m cells -> 4 tiles, 9 x 9)  */
+DM_FN uint32_t dm_lm_half(double r, double scale)
+{
+    const double q = r / (8.0 * scale);
+    if (!(q > 1.0)) return 1u;
+    if (q >= (double)DM_LM_MAX_HALF) return DM_LM_MAX_HALF;
+    const uint32_t h = (uint32_t)q;
+    return (double)h < q ? h + 1u : h;
+}
+/* the centre tile of a particle at grid-local l (one axis): the tile of the cell
+ * floor((l - offset) * inv_scale), saturated to int32 (callers skip non-finite positions)  */
+DM_FN int32_t dm_lm_centre(double l, double off, double inv)
+{
+    return dm_cvt_sat_i32(dm_floor((l - off) * inv)) >> DM_LM_TILE_BITS;
+}
+/* tile a (>= 0) inside the window [c - h, c + h] (wrapping uint32 arithmetic: an unset centre
+ * is never inside)                                                                           */
+DM_FN int dm_lm_inside(uint32_t a, int32_t c, uint32_t h, uint32_t w)
+{
+    return (uint32_t)(a - (uint32_t)c + h) < w;
+}
+/* the tile of slot column sa in the window [c - h, c + h] of width w = 2 h + 1 */
+DM_FN int64_t dm_lm_tile_of(uint32_t sa, int32_t c, uint32_t h, uint32_t w)
+{
+    const int64_t lo = (int64_t)c - (int64_t)h;
+    int64_t r = ((int64_t)sa - lo) % (int64_t)w;
+    if (r < 0) r += (int64_t)w;
+    return lo + r;
+}
+/* a page cell holds a patch */
+DM_FN int dm_lm_holds(float stdev) { return stdev >= 0.0f; }
+/* processMap's per-cell merge of a placed scan patch (wz, var) into a cell holding (m1, s1):
+ * the variance-weighted fusion when within 3 sigma (envire's MLSGrid::merge is not in the
+ * reference: this rule is the build's own, parity unpinned); returns 0 when it leaves the
+ * cell as it is                                                                            */
+DM_FN int dm_lm_fuse(float m1f, float s1f, double wz, double var, float* mo, float* so)
+{
+    const double m1 = (double)m1f, s1 = (double)s1f;
+    const double v1 = s1 * s1, d = wz - m1;
+    if (!(d * d <= 9.0 * (v1 + var))) return 0;
+    const double m = (m1 * var + wz * v1) / (v1 + var);
+    const double v = (v1 * var) / (v1 + var);
+    *mo = (float)m;
+    *so = (float)dm_sqrt(v);
+    return 1;
+}
+
 #endif /* ESLAM_DETMATH_H */

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 4
+#define ESLAM_ABI_VERSION 5
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -80,6 +80,13 @@ typedef struct eslam_config {
     int32_t log_debug;                     /* Configuration::logDebug (false)              */
     /* build-specific knobs (not in the reference) */
     uint32_t flags;                        /* ESLAM_FLAG_*                                 */
+    /* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): the device page pool, in pages of 8 x 8
+     * cells per particle (0: the default, 16); the pool is shared by all particles' maps and
+     * collected when a map update needs more (ESLAM_ERR_OUT_OF_MEMORY when even that fails) */
+    uint32_t local_map_pages;
+    /* Configuration::maxSensorRange (3.0, src/Configuration.hpp:107): a particle's own map keeps
+     * the tiles of 8 x 8 cells within this range of the particle             */
+    double max_sensor_range;
 } eslam_config;
 
 #define ESLAM_FLAG_RECORD_ANCESTORS 0x1u   /* keep the last resample's ancestor indices     */

@@ -278,6 +278,7 @@ struct Configuration {
     bool logDebug = false;
     unsigned int logParticlePeriod = 100;
     uint32_t flags = 0;                   // build-specific ESLAM_FLAG_* (not in the reference)
+    uint32_t localMapPages = 0;           // build-specific: per-particle map page pool per particle (0: 16)
 
     // the fields the MI355X path consumes, as the C ABI's POD (hash: the init() argument)
     eslam_config toC(const SurfaceHashConfig& hash = SurfaceHashConfig()) const
@@ -313,6 +314,8 @@ struct Configuration {
         c.hash_angular_steps = hash.angularSteps;
         c.log_debug = logDebug;
         c.flags = flags;
+        c.max_sensor_range = maxSensorRange;       // the reach of a particle's own map
+        c.local_map_pages = localMapPages;
         return c;
     }
 };

@@ -200,17 +200,31 @@ static int grid_map_fn(void* user, const double p[3], double q_mean, double q_va
     return or_mls_get_patch((const eslam_mls_grid*)user, p, q_mean, q_var, mean, stdev);
 }
 
-#define OR_STORE_SLOTS 32u            /* per-particle map store: slots, patches at most */
-#define OR_STORE_CAP 24u
+/* per-particle local maps: each particle's window of tiles (eslam_detmath.h
+ * DM_LM_*); a page holds one tile's 64 cells, {mean, stdev} each.  Pages live in blocks that
+ * never move (threads read them while others allocate) and are shared by the maps that a
+ * resample copied until a map update writes them (copy on write; page identity never shows
+ * in a result).                                                                            */
+#define OR_PAGE_BLOCK_BITS 16u
+#define OR_PAGE_BLOCKS (1u << 16)             /* at most 2^32 pages                            */
+typedef struct { float v[2 * DM_LM_PAGE_CELLS]; } or_page;
+
+/* the window of one particle's map: GridAccess::get on the particle's own map */
+typedef struct {
+    const eslam_mls_grid* g;
+    const int32_t* ctr;                  /* the particle's window centre (2 tiles)         */
+    const uint32_t* slot;                /* its slots (page or DM_LM_NONE)                  */
+    or_page* const* blk;                 /* page blocks                                     */
+    uint32_t hx, hy, wx, wy;
+} or_pmap;
+
+static const or_page* lm_page(or_page* const* blk, uint32_t p)
+{
+    return blk[p >> OR_PAGE_BLOCK_BITS] + (p & ((1u << OR_PAGE_BLOCK_BITS) - 1u));
+}
 
 /* per-particle maps: GridAccess::get on the particle's own map = the shared grid, and for a
  * cell the grid leaves empty the particle's patch there (same 3-sigma gate)               */
-typedef struct {
-    const eslam_mls_grid* g;
-    const uint32_t* key;                 /* the particle's 32 slots */
-    const float* val;
-} or_pmap;
-
 static int particle_map_fn(void* user, const double p[3], double q_mean, double q_var, double* mean, double* stdev)
 {
     const or_pmap* pm = (const or_pmap*)user;
@@ -229,19 +243,18 @@ static int particle_map_fn(void* user, const double p[3], double q_mean, double 
     const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
     const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
     if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) return 0;
-    const uint32_t cell = (uint32_t)fn * g->width + (uint32_t)fm;
+    const uint32_t m = (uint32_t)fm, n = (uint32_t)fn, cell = n * g->width + m;
     if (g->cell_start[cell] != g->cell_start[cell + 1]) return 0;       /* the grid's cell: no patch passed */
-    uint32_t h = dm_store_hash(cell);
-    for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
-        if (pm->key[h] == cell + 1u) {
-            const double m = (double)pm->val[2 * h], sd = (double)pm->val[2 * h + 1];
-            const double diff = fabs(m - lz);
-            if (diff * diff < 9.0 * (sd * sd + q_var)) { *mean = m; *stdev = sd; return 1; }
-            return 0;
-        }
-        if (pm->key[h] == 0) return 0;
-        h = (h + 1u) & (OR_STORE_SLOTS - 1u);
-    }
+    const uint32_t a = m >> DM_LM_TILE_BITS, b = n >> DM_LM_TILE_BITS;
+    if (!dm_lm_inside(a, pm->ctr[0], pm->hx, pm->wx) || !dm_lm_inside(b, pm->ctr[1], pm->hy, pm->wy)) return 0;
+    const uint32_t pg = pm->slot[(a % pm->wx) + pm->wx * (b % pm->wy)];
+    if (pg == DM_LM_NONE) return 0;
+    const uint32_t j = (m & 7u) + 8u * (n & 7u);
+    const float* v = lm_page(pm->blk, pg)->v;
+    if (!dm_lm_holds(v[2 * j + 1])) return 0;
+    const double mm = (double)v[2 * j], sd = (double)v[2 * j + 1];
+    const double diff = fabs(mm - lz);
+    if (diff * diff < 9.0 * (sd * sd + q_var)) { *mean = mm; *stdev = sd; return 1; }
     return 0;
 }
 
@@ -580,11 +593,17 @@ struct or_filter {
     int threads;
     int literal;                         /* or_set_literal */
     int debug;                           /* or_set_debug */
-    /* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): each particle's own patches in cells the
-     * shared grid leaves empty, 32 open-addressing slots (key = cell + 1), at most 24 */
-    uint32_t* pm_key;                    /* n x 32 */
-    float* pm_val;                       /* n x 32 x {mean, stdev} */
-    uint32_t* pm_count;                  /* n */
+    /* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): each particle's window of tiles in cells
+     * the shared grid leaves empty; sized from the map at set_map / init     */
+    int lm_on;                           /* pm_ctr / pm_slot allocated for the current map    */
+    uint32_t lm_hx, lm_hy, lm_wx, lm_wy, lm_S;
+    int32_t* pm_ctr;                     /* n x 2: window centre tile (DM_LM_UNSET: none)     */
+    uint32_t* pm_slot;                   /* n x S: page index or DM_LM_NONE                   */
+    or_page** pg_blk;                    /* OR_PAGE_BLOCKS block pointers                      */
+    uint32_t pg_nblk;                    /* blocks allocated                                   */
+    uint64_t pg_top;                     /* pages [0, pg_top) handed out at least once         */
+    uint32_t* pg_free;                   /* free pages (the last map update's collection)      */
+    uint64_t pg_nfree, pg_free_cap;
     uint64_t* pm_id;                     /* n: which map a particle holds (the resample copies the
                                             id with the map; a particle that changes a map it
                                             shares, or receives one from another rank, takes a
@@ -646,14 +665,72 @@ static void get_b(uint8_t* dst, const uint8_t* src, uint64_t n)
     for (uint64_t i = 0; i < n; ++i) dst[i] = src[OB(i)];
 }
 
+/* ---- per-particle local maps: storage ------------------------------------------------- */
+static void lm_free(or_filter* f)
+{
+    free(f->pm_ctr); free(f->pm_slot); free(f->pm_id);
+    f->pm_ctr = NULL; f->pm_slot = NULL; f->pm_id = NULL;
+    if (f->pg_blk) {
+        for (uint32_t k = 0; k < f->pg_nblk; ++k) free(f->pg_blk[k]);
+        free(f->pg_blk);
+    }
+    free(f->pg_free);
+    f->pg_blk = NULL; f->pg_nblk = 0; f->pg_top = 0;
+    f->pg_free = NULL; f->pg_nfree = f->pg_free_cap = 0;
+    f->lm_on = 0;
+}
+
+/* every particle's map empty, sized for the current map (none yet: nothing until set_map) */
+static int lm_reset(or_filter* f)
+{
+    lm_free(f);
+    if (!(f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS) || !f->has_map || !f->n) return 0;
+    f->lm_hx = dm_lm_half(f->cfg.max_sensor_range, f->map.scale_x);
+    f->lm_hy = dm_lm_half(f->cfg.max_sensor_range, f->map.scale_y);
+    f->lm_wx = 2 * f->lm_hx + 1;
+    f->lm_wy = 2 * f->lm_hy + 1;
+    f->lm_S = f->lm_wx * f->lm_wy;
+    const uint64_t n = f->n;
+    f->pm_ctr = malloc(n * 2 * sizeof(int32_t));
+    f->pm_slot = malloc(n * f->lm_S * sizeof(uint32_t));
+    f->pm_id = malloc(n * 8);
+    f->pg_blk = calloc(OR_PAGE_BLOCKS, sizeof(or_page*));
+    if (!f->pm_ctr || !f->pm_slot || !f->pm_id || !f->pg_blk) return ESLAM_ERR_OUT_OF_MEMORY;
+    for (uint64_t i = 0; i < 2 * n; ++i) f->pm_ctr[i] = DM_LM_UNSET;
+    memset(f->pm_slot, 0xff, n * f->lm_S * sizeof(uint32_t));
+    for (uint64_t i = 0; i < n; ++i) f->pm_id[i] = f->gbase + i;
+    f->pm_fresh = (1ull << 63) | ((uint64_t)f->gbase << 32);
+    f->lm_on = 1;
+    return 0;
+}
+
+/* a page for a map update's write: a free one, else a new one (called by one thread at a time) */
+static uint32_t lm_alloc(or_filter* f)
+{
+    if (f->pg_nfree) return f->pg_free[--f->pg_nfree];
+    const uint64_t p = f->pg_top;
+    const uint32_t blk = (uint32_t)(p >> OR_PAGE_BLOCK_BITS);
+    if (blk >= OR_PAGE_BLOCKS) return DM_LM_NONE;
+    if (blk >= f->pg_nblk) {
+        f->pg_blk[blk] = malloc(sizeof(or_page) << OR_PAGE_BLOCK_BITS);
+        if (!f->pg_blk[blk]) return DM_LM_NONE;
+        f->pg_nblk = blk + 1;
+    }
+    f->pg_top = p + 1;
+    return (uint32_t)p;
+}
+
+static or_page* lm_pg(or_filter* f, uint32_t p)
+{
+    return f->pg_blk[p >> OR_PAGE_BLOCK_BITS] + (p & ((1u << OR_PAGE_BLOCK_BITS) - 1u));
+}
+
 static void or_free_particles(or_filter* f)
 {
     free_state(f);
     free(f->anc);
     free(f->dbg_ncp); free(f->dbg_cp); free(f->dbg_zdelta); free(f->dbg_zvar);
-    free(f->pm_key); free(f->pm_val); free(f->pm_count);
-    free(f->pm_id);
-    f->pm_key = NULL; f->pm_val = NULL; f->pm_count = NULL; f->pm_id = NULL;
+    lm_free(f);
     f->x = f->y = f->th = f->z = f->zs = f->w = f->mprob = NULL;
     f->floating = f->ncp = NULL;
     f->anc = NULL;
@@ -682,15 +759,7 @@ static int or_alloc_particles(or_filter* f, uint64_t n)
         f->dbg_zdelta = calloc(b, 8); f->dbg_zvar = calloc(b, 8);
         if (!f->dbg_cp) return ESLAM_ERR_OUT_OF_MEMORY;
     }
-    if (f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS) {      /* every particle's map: still empty */
-        f->pm_key = calloc(b * OR_STORE_SLOTS, 4);
-        f->pm_val = calloc(b * OR_STORE_SLOTS * 2, 4);
-        f->pm_count = calloc(b, 4);
-        f->pm_id = malloc(b * 8);
-        if (!f->pm_key || !f->pm_val || !f->pm_count || !f->pm_id) return ESLAM_ERR_OUT_OF_MEMORY;
-        for (uint64_t i = 0; i < n; ++i) f->pm_id[i] = f->gbase + i;
-        f->pm_fresh = (1ull << 63) | ((uint64_t)f->gbase << 32);
-    }
+    if (lm_reset(f)) return ESLAM_ERR_OUT_OF_MEMORY;    /* every particle's map: still empty */
     f->has_anc = 0;
     return f->x ? 0 : ESLAM_ERR_OUT_OF_MEMORY;
 }
@@ -764,7 +833,8 @@ int or_set_map(or_filter* f, const eslam_mls_grid* g)
     f->map.patch_stdev = f->map_stdev;
     f->map.patch_height = f->map_height;
     f->has_map = 1;
-    return 0;
+    /* the particles' own maps name cells of the previous grid: they start over, empty */
+    return lm_reset(f);
 }
 
 uint64_t or_count(const or_filter* f) { return f->n; }
@@ -1245,9 +1315,10 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         /* Translation3d(x, y, zPos) * AngleAxisd(theta, UnitZ) */
         double T[12] = {co, -s, 0.0, f->x[OD(i)], s, co, 0.0, f->y[OD(i)], 0.0, 0.0, r22, f->z[OD(i)]};
         const double meas_var = f->literal ? pow(f->zs[OD(i)], 2) + pow(c->measurement_error, 2) : f->zs[OD(i)] * f->zs[OD(i)] + me2;
-        or_pmap pmc = {&f->map, f->pm_key ? f->pm_key + (uint64_t)i * OR_STORE_SLOTS : NULL,
-                       f->pm_val ? f->pm_val + (uint64_t)i * OR_STORE_SLOTS * 2 : NULL};
-        int acc = f->pm_key ? or_cm_evaluate_pose(&cm, T, meas_var, particle_map_fn, &pmc)
+        or_pmap pmc = {&f->map, f->lm_on ? f->pm_ctr + 2 * (uint64_t)i : NULL,
+                       f->lm_on ? f->pm_slot + (uint64_t)i * f->lm_S : NULL, f->pg_blk, f->lm_hx, f->lm_hy, f->lm_wx,
+                       f->lm_wy};
+        int acc = f->lm_on ? or_cm_evaluate_pose(&cm, T, meas_var, particle_map_fn, &pmc)
                             : or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
         if (acc < 0) { zero_var = 1; acc = 0; }
         sw_val[i] = 0.0;
@@ -1433,20 +1504,21 @@ static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
     free_state(f);
     f->x = nx; f->y = ny; f->th = nt; f->z = nz; f->zs = ns; f->w = nw; f->mprob = nm; f->floating = nf; f->ncp = nc;
 #endif
-    if (f->pm_key) {                      /* a copied particle carries its map (a deep copy) */
-        uint32_t* nk = malloc(samples * OR_STORE_SLOTS * 4);
-        float* nv = malloc(samples * OR_STORE_SLOTS * 8);
-        uint32_t* ncn = malloc(samples * 4);
+    if (f->lm_on) {                       /* a copied particle carries its map (cloneMaps: the
+                                             slots are copied, the pages shared until written) */
+        const uint64_t S = f->lm_S;
+        int32_t* nc = malloc(samples * 2 * sizeof(int32_t));
+        uint32_t* ns = malloc(samples * S * sizeof(uint32_t));
         uint64_t* nid = malloc(samples * 8);
         for (uint64_t k = 0; k < samples; ++k) {
             const uint32_t i = anc[k];
-            memcpy(nk + k * OR_STORE_SLOTS, f->pm_key + (uint64_t)i * OR_STORE_SLOTS, OR_STORE_SLOTS * 4);
-            memcpy(nv + k * OR_STORE_SLOTS * 2, f->pm_val + (uint64_t)i * OR_STORE_SLOTS * 2, OR_STORE_SLOTS * 8);
-            ncn[k] = f->pm_count[i];
+            nc[2 * k] = f->pm_ctr[2 * (uint64_t)i];
+            nc[2 * k + 1] = f->pm_ctr[2 * (uint64_t)i + 1];
+            memcpy(ns + k * S, f->pm_slot + (uint64_t)i * S, S * sizeof(uint32_t));
             nid[k] = f->pm_id[i];
         }
-        free(f->pm_key); free(f->pm_val); free(f->pm_count); free(f->pm_id);
-        f->pm_key = nk; f->pm_val = nv; f->pm_count = ncn; f->pm_id = nid;
+        free(f->pm_ctr); free(f->pm_slot); free(f->pm_id);
+        f->pm_ctr = nc; f->pm_slot = ns; f->pm_id = nid;
     }
 }
 
@@ -1499,12 +1571,16 @@ typedef struct {
     double x, y, th, z, zs, w, mprob;
     uint64_t lo, hi, src;          /* global output range, global source index */
     uint8_t floating, ncp, pad[6];
-    /* per-particle maps: the source particle's own patches travel with it (a deep copy) */
-    uint32_t pm_count, pm_pad;
+    /* per-particle maps: the source particle's map travels with it (a deep copy): its window
+     * centre here, its npg pages in the payload stream (or_mig_page each, in slot order)   */
+    int32_t pm_ctr[2];
+    uint32_t pm_npg, pm_pad;
     uint64_t pm_id;
-    uint32_t pm_key[OR_STORE_SLOTS];
-    float pm_val[2 * OR_STORE_SLOTS];
 } or_mig;
+typedef struct {
+    uint32_t slot, pad;
+    or_page page;
+} or_mig_page;
 
 static void resample_sharded(or_filter* f, int shift)
 {
@@ -1557,13 +1633,36 @@ static void resample_sharded(or_filter* f, int shift)
             m->w = f->w[OD(i)]; m->mprob = f->mprob[OD(i)];
             m->floating = f->floating[OB(i)]; m->ncp = f->ncp[OB(i)];
             m->lo = a; m->hi = b; m->src = f->gbase + i;
-            if (f->pm_key) {
-                m->pm_count = f->pm_count[i];
+            if (f->lm_on) {
                 m->pm_id = f->pm_id[i];
-                memcpy(m->pm_key, f->pm_key + i * OR_STORE_SLOTS, sizeof(m->pm_key));
-                memcpy(m->pm_val, f->pm_val + i * OR_STORE_SLOTS * 2, sizeof(m->pm_val));
+                m->pm_ctr[0] = f->pm_ctr[2 * i];
+                m->pm_ctr[1] = f->pm_ctr[2 * i + 1];
+                for (uint64_t q = 0; q < f->lm_S; ++q) m->pm_npg += f->pm_slot[i * f->lm_S + q] != DM_LM_NONE;
             }
         }
+    /* the maps' pages, in the records' order (one more all_to_all_v of byte counts the
+     * receivers learn from an all_gather) */
+    uint64_t pbytes[ESLAM_ORACLE_MAX_RANKS] = {0}, npay = 0;
+    or_mig_page* pay = NULL;
+    if (f->lm_on) {
+        uint64_t q = 0;
+        for (int d = 0; d < G; ++d)
+            for (uint64_t r = 0; r < cnt[d]; ++r) pbytes[d] += send[q++].pm_npg * sizeof(or_mig_page);
+        for (int d = 0; d < G; ++d) npay += pbytes[d] / sizeof(or_mig_page);
+        pay = malloc((npay ? npay : 1) * sizeof(or_mig_page));
+        uint64_t w = 0;
+        for (uint64_t r = 0; r < nsend; ++r) {
+            const uint64_t i = send[r].src - f->gbase;
+            for (uint32_t sl = 0; sl < f->lm_S; ++sl) {
+                const uint32_t pg = f->pm_slot[i * f->lm_S + sl];
+                if (pg == DM_LM_NONE) continue;
+                pay[w].slot = sl;
+                pay[w].pad = 0;
+                pay[w].page = *lm_pg(f, pg);
+                ++w;
+            }
+        }
+    }
     free(lo); free(hi);
     uint64_t all[ESLAM_ORACLE_MAX_RANKS * ESLAM_ORACLE_MAX_RANKS];
     comm_allgather(f, cnt, all, 8ull * G);
@@ -1576,26 +1675,76 @@ static void resample_sharded(or_filter* f, int shift)
     or_mig* recv = malloc(sizeof(or_mig) * (nrecv ? nrecv : 1));
     f->comm.alltoallv(f->comm.user, send, sb, recv, rb, NULL);
     free(send);
+    or_mig_page* rpay = NULL;
+    if (f->lm_on) {
+        uint64_t pall[ESLAM_ORACLE_MAX_RANKS * ESLAM_ORACLE_MAX_RANKS], prb[ESLAM_ORACLE_MAX_RANKS], nr = 0;
+        comm_allgather(f, pbytes, pall, 8ull * G);
+        for (int r = 0; r < G; ++r) {
+            prb[r] = pall[r * G + me];
+            nr += prb[r];
+        }
+        rpay = malloc(nr ? nr : 1);
+        f->comm.alltoallv(f->comm.user, pay, pbytes, rpay, prb, NULL);
+        free(pay);
+    }
+    /* the received maps: each record's pages become pages of this rank (first page index of
+     * record q: rfirst[q]); own records keep their maps' pages */
+    uint64_t* rfirst = calloc(nrecv ? nrecv : 1, 8);
+    uint32_t* rpg = NULL;
+    if (f->lm_on) {
+        uint64_t tot = 0;
+        for (uint64_t q = 0; q < nrecv; ++q) { rfirst[q] = tot; tot += recv[q].pm_npg; }
+        rpg = malloc((tot ? tot : 1) * 4);
+        for (uint64_t q = 0; q < tot; ++q) {
+            rpg[q] = lm_alloc(f);
+            *lm_pg(f, rpg[q]) = rpay[q].page;
+        }
+    }
     uint32_t* anc = calloc(n + 1, 4);
     or_mig* src = calloc(n ? n : 1, sizeof(or_mig));
+    uint64_t* srcq = calloc(n ? n : 1, 8);
     for (uint64_t q = 0; q < nrecv; ++q)
         for (uint64_t o = recv[q].lo; o < recv[q].hi; ++o) {
             src[o - f->gbase] = recv[q];
+            srcq[o - f->gbase] = q;
             anc[o - f->gbase] = (uint32_t)recv[q].src;
         }
     free(recv);
+    /* the new maps (slots of the sources this rank holds, the received pages for others) */
+    int32_t* nctr = NULL;
+    uint32_t* nslot = NULL;
+    if (f->lm_on) {
+        const uint64_t S = f->lm_S;
+        nctr = malloc(n * 2 * sizeof(int32_t));
+        nslot = malloc(n * S * 4);
+        for (uint64_t o = 0; o < n; ++o) {
+            const or_mig* m = &src[o];
+            nctr[2 * o] = m->pm_ctr[0];
+            nctr[2 * o + 1] = m->pm_ctr[1];
+            uint32_t* sl = nslot + o * S;
+            if (m->src - f->gbase < n) {
+                memcpy(sl, f->pm_slot + (m->src - f->gbase) * S, S * 4);
+            } else {
+                memset(sl, 0xff, S * 4);
+                const uint64_t q0 = rfirst[srcq[o]];
+                for (uint32_t k = 0; k < m->pm_npg; ++k) sl[rpay[q0 + k].slot] = rpg[q0 + k];
+            }
+        }
+    }
+    free(rfirst); free(rpg); free(rpay); free(srcq);
     for (uint64_t o = 0; o < n; ++o) {
         const or_mig* m = &src[o];
         f->x[OD(o)] = m->x; f->y[OD(o)] = m->y; f->th[OD(o)] = m->th; f->z[OD(o)] = m->z; f->zs[OD(o)] = m->zs;
         f->w[OD(o)] = m->w; f->mprob[OD(o)] = m->mprob; f->floating[OB(o)] = m->floating; f->ncp[OB(o)] = m->ncp;
         f->anc[o] = anc[o];
-        if (f->pm_key) {
-            f->pm_count[o] = m->pm_count;
-            /* a map from another rank arrives as a copy of its own (the GPU: a store per record) */
+        if (f->lm_on) {
+            /* a map from another rank arrives as a copy of its own (the GPU: a table per record) */
             f->pm_id[o] = m->src - f->gbase < n ? m->pm_id : f->pm_fresh++;
-            memcpy(f->pm_key + o * OR_STORE_SLOTS, m->pm_key, sizeof(m->pm_key));
-            memcpy(f->pm_val + o * OR_STORE_SLOTS * 2, m->pm_val, sizeof(m->pm_val));
         }
+    }
+    if (f->lm_on) {
+        free(f->pm_ctr); free(f->pm_slot);
+        f->pm_ctr = nctr; f->pm_slot = nslot;
     }
     free(src); free(anc);
     f->info.resample_overruns = overruns;
@@ -1858,13 +2007,16 @@ void or_set_rng_state(or_filter* f, const eslam_rng_state* st)
 }
 
 /* EmbodiedSlamFilter::processMap(scanMap, match = false, update = true)
- * (src/EmbodiedSlamFilter.cpp:179-232) on per-particle maps: every scan patch at the
- * particle's pose (scanFrame = Translation(x, y, 0) * Rz(theta), :186-189; the offset patch
- * adds zPos and zSigma^2, :213-214) into the cell it lands in -- inserted into a cell empty
- * in both the shared grid and the particle's map (test/testMap.cpp:307-316), fused
- * (variance-weighted) with the particle's patch there when within 3 sigma, ignored on the
- * shared grid's cells and when the particle already holds 24 patches.  (cloneMaps' copies
- * are the deep copies of gather().)                                                       */
+ * (src/EmbodiedSlamFilter.cpp:179-232) on per-particle maps.  Per particle: the map's window
+ * moves to the tile under the particle (the active-grid switch of :195-207, here a window of
+ * tiles reaching maxSensorRange around the particle: tiles that leave it are forgotten), then
+ * every scan patch at the particle's pose (scanFrame = Translation(x, y, 0) * Rz(theta),
+ * :186-189; the offset patch adds zPos and zSigma^2, :213-214) goes into the cell it lands in:
+ * inserted into a cell empty in both the shared grid and the particle's map
+ * (test/testMap.cpp:307-316), fused (variance-weighted) with the particle's patch there when
+ * within 3 sigma (dm_lm_fuse), ignored on the shared grid's cells; a patch outside the window
+ * (beyond maxSensorRange) is dropped.  A resample's copies share their pages until a write
+ * (cloneMaps, src/PoseEstimator.cpp:31-47: the copies are independent, by value).          */
 static int cmp_u64(const void* a, const void* b)
 {
     const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
@@ -1873,19 +2025,24 @@ static int cmp_u64(const void* a, const void* b)
 
 int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 {
-    if (!f->pm_key) return ESLAM_ERR_INVALID_ARG;
+    if (!(f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS)) return ESLAM_ERR_INVALID_ARG;
     if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
+    if (!f->n) return ESLAM_ERR_NOT_INITIALISED;
+    if (!f->lm_on) return ESLAM_ERR_OUT_OF_MEMORY;
     const eslam_mls_grid* g = &f->map;
     const double* A = g->global2local;
     static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     int is_id = 1;
     for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
+    const uint64_t S = f->lm_S;
+    const uint32_t hx = f->lm_hx, hy = f->lm_hy, wx = f->lm_wx, wy = f->lm_wy;
     /* which particles share their map with another (copies of one map the resample made and
      * no map update has changed since): the ids sorted, a particle's id looked up */
     uint64_t* sorted = malloc((f->n ? f->n : 1) * 8);
     uint8_t* shared = calloc(f->n ? f->n : 1, 1);
     uint8_t* dirt = calloc(f->n ? f->n : 1, 1);
-    if (!sorted || !shared || !dirt) { free(sorted); free(shared); free(dirt); return ESLAM_ERR_OUT_OF_MEMORY; }
+    uint32_t* ref = calloc(f->pg_top ? f->pg_top : 1, 4);
+    if (!sorted || !shared || !dirt || !ref) { free(sorted); free(shared); free(dirt); free(ref); return ESLAM_ERR_OUT_OF_MEMORY; }
     memcpy(sorted, f->pm_id, f->n * 8);
     qsort(sorted, f->n, 8, cmp_u64);
     for (uint64_t i = 0; i < f->n; ++i) {
@@ -1898,82 +2055,137 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
         shared[i] = lo + 1 < f->n && sorted[lo + 1] == f->pm_id[i];
     }
     free(sorted);
+    /* the names every map holds now: a page named once belongs to one particle's map and may
+     * be written in place, one named more often is copied first; one named by none is free */
+    for (uint64_t q = 0; q < f->n * S; ++q)
+        if (f->pm_slot[q] != DM_LM_NONE) ref[f->pm_slot[q]]++;
+    f->pg_nfree = 0;
+    if (f->pg_free_cap < f->pg_top) {
+        free(f->pg_free);
+        f->pg_free = malloc((f->pg_top ? f->pg_top : 1) * 4);
+        f->pg_free_cap = f->pg_top;
+        if (!f->pg_free) { free(shared); free(dirt); free(ref); f->pg_free_cap = 0; return ESLAM_ERR_OUT_OF_MEMORY; }
+    }
+    for (uint64_t q = f->pg_top; q-- > 0;)
+        if (!ref[q]) f->pg_free[f->pg_nfree++] = (uint32_t)q;
     uint64_t dropped = 0, changed = 0, covered = 0;
+    int oom = 0;
     const int64_t n = (int64_t)f->n;
     /* particles are independent: the OpenMP threads of or_set_threads (same results) */
-#pragma omp parallel for schedule(static) num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed, covered)
+#pragma omp parallel num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed, covered) reduction(| : oom)
+    {
+    uint8_t* mine = malloc(S);            /* slot's page made this particle's own in this update */
+#pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
         int dirty = 0;
-        uint32_t* key = f->pm_key + i * OR_STORE_SLOTS;
-        float* val = f->pm_val + i * OR_STORE_SLOTS * 2;
-        uint32_t count = f->pm_count[i];
+        int32_t* ctr = f->pm_ctr + 2 * i;
+        uint32_t* sl = f->pm_slot + (uint64_t)i * S;
         double sn, co;
         dm_sincos(f->th[OD(i)], &sn, &co);
         const double zvar = f->zs[OD(i)] * f->zs[OD(i)];
         const double bx = f->x[OD(i)] - g->offset_x, by = f->y[OD(i)] - g->offset_y;
         const int placed = dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(f->th[OD(i)]);
+        if (!placed) continue;
+        /* the window's centre: the tile under the particle */
+        int32_t na, nb;
+        if (is_id) {
+            na = dm_lm_centre(f->x[OD(i)], g->offset_x, 1.0 / g->scale_x);
+            nb = dm_lm_centre(f->y[OD(i)], g->offset_y, 1.0 / g->scale_y);
+        } else {
+            const double px = f->x[OD(i)], py = f->y[OD(i)], pz = f->z[OD(i)];
+            const double lx = ((A[0] * px + A[1] * py) + A[2] * pz) + A[3];
+            const double ly = ((A[4] * px + A[5] * py) + A[6] * pz) + A[7];
+            na = dm_lm_centre(lx, g->offset_x, 1.0 / g->scale_x);
+            nb = dm_lm_centre(ly, g->offset_y, 1.0 / g->scale_y);
+        }
+        if (ctr[0] != na || ctr[1] != nb) {
+            if (ctr[0] != DM_LM_UNSET) {          /* tiles leaving the window are forgotten */
+                for (uint32_t sb = 0; sb < wy; ++sb)
+                    for (uint32_t sa = 0; sa < wx; ++sa) {
+                        uint32_t* e = &sl[sa + wx * sb];
+                        if (*e == DM_LM_NONE) continue;
+                        const int64_t a = dm_lm_tile_of(sa, ctr[0], hx, wx), b = dm_lm_tile_of(sb, ctr[1], hy, wy);
+                        if (llabs(a - (int64_t)na) > (int64_t)hx || llabs(b - (int64_t)nb) > (int64_t)hy) *e = DM_LM_NONE;
+                    }
+            }
+            ctr[0] = na;
+            ctr[1] = nb;
+            dirty = 1;
+        }
+        memset(mine, 0, S);
         for (uint32_t k = 0; k < m; ++k) {
             const double wz = sp[k].position[2] + f->z[OD(i)];
-            uint32_t cell;
+            uint32_t cell, cm, cn;
             if (is_id) {
-                if (!placed) continue;
-                cell = dm_merge_cell(bx, by, co, sn, sp[k].position[0], sp[k].position[1], 1.0 / g->scale_x,
-                                     1.0 / g->scale_y, g->width, g->height);
+                cell = dm_merge_cell_mn(bx, by, co, sn, sp[k].position[0], sp[k].position[1], 1.0 / g->scale_x,
+                                        1.0 / g->scale_y, g->width, g->height, &cm, &cn);
                 if (cell == 0xffffffffu) continue;
             } else {
-                const double wx = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[OD(i)];
-                const double wy = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
-                const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-                const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                const double wx_ = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[OD(i)];
+                const double wy_ = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
+                const double lx = ((A[0] * wx_ + A[1] * wy_) + A[2] * wz) + A[3];
+                const double ly = ((A[4] * wx_ + A[5] * wy_) + A[6] * wz) + A[7];
                 const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
                 const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
                 if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
-                cell = (uint32_t)fn * g->width + (uint32_t)fm;
+                cm = (uint32_t)fm;
+                cn = (uint32_t)fn;
+                cell = cn * g->width + cm;
             }
             if (g->cell_start[cell] != g->cell_start[cell + 1]) {
                 ++covered;          /* the shared grid covers the cell: not merged */
                 continue;
             }
-            const double var = sp[k].stdev * sp[k].stdev + zvar;
-            uint32_t h = dm_store_hash(cell);
-            for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
-                if (key[h] == cell + 1u) {
-                    const double m1 = (double)val[2 * h], s1 = (double)val[2 * h + 1];
-                    const double v1 = s1 * s1, d = wz - m1;
-                    if (d * d <= 9.0 * (v1 + var)) {
-                        const double mm = (m1 * var + wz * v1) / (v1 + var);
-                        const double vv = (v1 * var) / (v1 + var);
-                        val[2 * h] = (float)mm;
-                        val[2 * h + 1] = (float)dm_sqrt(vv);
-                        dirty = 1;
-                    }
-                    break;
-                }
-                if (key[h] == 0) {
-                    if (count < OR_STORE_CAP) {
-                        key[h] = cell + 1u;
-                        val[2 * h] = (float)wz;
-                        val[2 * h + 1] = (float)dm_sqrt(var);
-                        ++count;
-                        dirty = 1;
-                    } else {
-                        ++dropped;          /* the store is full: counted, not silent */
-                    }
-                    break;
-                }
-                h = (h + 1u) & (OR_STORE_SLOTS - 1u);
+            const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+            if (!dm_lm_inside(a, ctr[0], hx, wx) || !dm_lm_inside(b, ctr[1], hy, wy)) {
+                ++dropped;          /* beyond maxSensorRange: outside the window */
+                continue;
             }
+            const uint32_t slot = (a % wx) + wx * (b % wy);
+            const uint32_t j = (cm & 7u) + 8u * (cn & 7u);
+            const double var = sp[k].stdev * sp[k].stdev + zvar;
+            uint32_t pg = sl[slot];
+            float mo, so;
+            if (pg != DM_LM_NONE && dm_lm_holds(lm_pg(f, pg)->v[2 * j + 1])) {
+                const float* v = lm_pg(f, pg)->v;
+                if (!dm_lm_fuse(v[2 * j], v[2 * j + 1], wz, var, &mo, &so)) continue;
+            } else {
+                mo = (float)wz;
+                so = (float)dm_sqrt(var);
+            }
+            if (!mine[slot] && (pg == DM_LM_NONE || ref[pg] > 1)) {
+                /* the first write to this tile: a page of the particle's own (copy on write) */
+                uint32_t np;
+#pragma omp critical(or_pages)
+                np = lm_alloc(f);
+                if (np == DM_LM_NONE) { oom = 1; break; }
+                or_page* d = lm_pg(f, np);
+                if (pg == DM_LM_NONE) {
+                    for (uint32_t q = 0; q < DM_LM_PAGE_CELLS; ++q) { d->v[2 * q] = 0.0f; d->v[2 * q + 1] = -1.0f; }
+                } else {
+                    *d = *lm_pg(f, pg);
+                }
+                sl[slot] = pg = np;
+            }
+            mine[slot] = 1;
+            or_page* d = lm_pg(f, pg);
+            d->v[2 * j] = mo;
+            d->v[2 * j + 1] = so;
+            dirty = 1;
         }
-        f->pm_count[i] = count;
         changed += (uint64_t)dirty;
         dirt[i] = (uint8_t)dirty;
     }
-    /* a changed shared map becomes the particle's own (the GPU writes it to a free store) */
+    free(mine);
+    }
+    free(ref);
+    /* a changed shared map becomes the particle's own (the GPU writes it to a free table) */
     uint64_t copied = 0;
     for (uint64_t i = 0; i < f->n; ++i)
         if (dirt[i] && shared[i]) { f->pm_id[i] = f->pm_fresh++; ++copied; }
     free(shared);
     free(dirt);
+    if (oom) return ESLAM_ERR_OUT_OF_MEMORY;
     f->info.map_patches_dropped = dropped;
     f->info.map_stores_changed = changed;
     f->info.map_stores_copied = copied;
@@ -1981,21 +2193,45 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     return 0;
 }
 
-/* particle i's own patches in slot order (cells, mean, stdev); returns how many it holds */
+/* particle i's own patches, tiles in slot order and each tile's cells in row order (cells
+ * n * width + m, mean, stdev); returns how many it holds                                 */
 uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* mean, float* stdev, uint32_t cap)
 {
-    if (!f->pm_key || i >= f->n) return 0;
+    if (!f->lm_on || i >= f->n) return 0;
+    const int32_t* ctr = f->pm_ctr + 2 * i;
+    const uint32_t* sl = f->pm_slot + i * f->lm_S;
     uint32_t c = 0;
-    for (uint32_t t = 0; t < OR_STORE_SLOTS; ++t) {
-        const uint32_t k = f->pm_key[i * OR_STORE_SLOTS + t];
-        if (!k) continue;
-        if (c < cap) {
-            cells[c] = k - 1u;
-            mean[c] = f->pm_val[(i * OR_STORE_SLOTS + t) * 2];
-            stdev[c] = f->pm_val[(i * OR_STORE_SLOTS + t) * 2 + 1];
+    for (uint32_t sb = 0; sb < f->lm_wy; ++sb)
+        for (uint32_t sa = 0; sa < f->lm_wx; ++sa) {
+            const uint32_t pg = sl[sa + f->lm_wx * sb];
+            if (pg == DM_LM_NONE) continue;
+            const int64_t a = dm_lm_tile_of(sa, ctr[0], f->lm_hx, f->lm_wx), b = dm_lm_tile_of(sb, ctr[1], f->lm_hy, f->lm_wy);
+            const float* v = lm_pg(f, pg)->v;
+            for (uint32_t j = 0; j < DM_LM_PAGE_CELLS; ++j) {
+                if (!dm_lm_holds(v[2 * j + 1])) continue;
+                const uint64_t mm = (uint64_t)(8 * a) + (j & 7u), nn = (uint64_t)(8 * b) + (j >> 3);
+                if (c < cap) {
+                    cells[c] = (uint32_t)(nn * f->map.width + mm);
+                    mean[c] = v[2 * j];
+                    stdev[c] = v[2 * j + 1];
+                }
+                ++c;
+            }
         }
-        ++c;
+    return c;
+}
+
+/* pages the particles' maps name (distinct), the pool's use */
+uint64_t or_pages_in_use(or_filter* f)
+{
+    if (!f->lm_on) return 0;
+    uint8_t* seen = calloc(f->pg_top ? f->pg_top : 1, 1);
+    uint64_t c = 0;
+    for (uint64_t q = 0; q < f->n * f->lm_S; ++q) {
+        const uint32_t p = f->pm_slot[q];
+        if (p != DM_LM_NONE && !seen[p]) { seen[p] = 1; ++c; }
     }
+    free(seen);
     return c;
 }
 

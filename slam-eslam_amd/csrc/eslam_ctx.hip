@@ -450,6 +450,8 @@ extern "C" void eslam_config_default(eslam_config* c)
     c->hash_angular_steps = 16;
     c->log_debug = 0;
     c->flags = 0;
+    c->local_map_pages = 0;
+    c->max_sensor_range = 3.0;
 }
 
 extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }

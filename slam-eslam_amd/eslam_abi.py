@@ -54,6 +54,8 @@ class Config(C.Structure):
         ("hash_angular_steps", C.c_uint64),
         ("log_debug", C.c_int32),
         ("flags", C.c_uint32),
+        ("local_map_pages", C.c_uint32),
+        ("max_sensor_range", C.c_double),
     ]
 
 
@@ -269,6 +271,8 @@ def default_config(lib=None):
     c.hash_angular_steps = 16
     c.log_debug = 0
     c.flags = 0
+    c.local_map_pages = 0
+    c.max_sensor_range = 3.0
     return c
 
 

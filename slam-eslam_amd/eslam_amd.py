@@ -190,17 +190,19 @@ class GpuFilter:
         """eslam_gpu_map_update: processMap's merge of a scan into every particle's map"""
         self._check(self.L.eslam_gpu_map_update(self.h, patches, len(patches)))
 
-    def particle_map(self, i, cap=64):
-        """particle i's own patches: (cells, mean, stdev) in slot order"""
-        cells = np.zeros(cap, np.uint32)
-        mean = np.zeros(cap, np.float32)
-        sd = np.zeros(cap, np.float32)
-        c = C.c_uint32()
-        self._check(self.L.eslam_gpu_get_particle_map(self.h, i, cells.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                                      mean.ctypes.data_as(C.POINTER(C.c_float)),
-                                                      sd.ctypes.data_as(C.POINTER(C.c_float)), cap, C.byref(c)))
-        k = min(c.value, cap)
-        return cells[:k], mean[:k], sd[:k]
+    def particle_map(self, i, cap=1024):
+        """particle i's own patches: (cells, mean, stdev), tiles in slot order, cells row by row"""
+        while True:
+            cells = np.zeros(cap, np.uint32)
+            mean = np.zeros(cap, np.float32)
+            sd = np.zeros(cap, np.float32)
+            c = C.c_uint32()
+            self._check(self.L.eslam_gpu_get_particle_map(self.h, i, cells.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                          mean.ctypes.data_as(C.POINTER(C.c_float)),
+                                                          sd.ctypes.data_as(C.POINTER(C.c_float)), cap, C.byref(c)))
+            if c.value <= cap:
+                return cells[:c.value], mean[:c.value], sd[:c.value]
+            cap = c.value
 
     def count(self):
         n = C.c_uint64()

@@ -209,14 +209,17 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
             f.map_update(scan)
     if scan is not None:                         # every particle's own patches, sorted by cell
         n = hi - lo
-        cells = np.full((n, 24), 0xffffffff, np.uint32)
-        mean = np.zeros((n, 24), np.float32)
-        sd = np.zeros((n, 24), np.float32)
+        count = np.zeros(n, np.uint32)
+        cells, mean, sd = [], [], []
         for i in range(n):
             c, m, s_ = f.particle_map(i)
             o = np.argsort(c)
-            cells[i, :len(c)], mean[i, :len(c)], sd[i, :len(c)] = c[o], m[o], s_[o]
-        rec["maps/cells"], rec["maps/mean"], rec["maps/stdev"] = cells, mean, sd
+            count[i] = len(c)
+            cells.append(c[o]); mean.append(m[o]); sd.append(s_[o])
+        rec["maps/count"] = count
+        rec["maps/cells"] = np.concatenate(cells) if cells else np.zeros(0, np.uint32)
+        rec["maps/mean"] = np.concatenate(mean) if mean else np.zeros(0, np.float32)
+        rec["maps/stdev"] = np.concatenate(sd) if sd else np.zeros(0, np.float32)
     rec["best"] = np.array([f.best_index()])
     rec["rng"] = np.array([f.rng_state().minstd_x])
     pos, quat = f.centroid()                 # getCentroid (normalises in place, Q15)

@@ -91,6 +91,8 @@ def lib(aos=False):
     L.or_set_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
     L.or_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
     L.or_get_particle_map.restype = C.c_uint32
+    L.or_pages_in_use.restype = C.c_uint64
+    L.or_pages_in_use.argtypes = [vp]
     L.or_get_particle_map.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                       C.c_uint32]
     L.or_get_debug.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(CPoint), C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -263,15 +265,20 @@ class OracleFilter:
     def map_update(self, patches):
         assert self.L.or_map_update(self.h, patches, len(patches)) == 0
 
-    def particle_map(self, i, cap=64):
-        cells = np.zeros(cap, np.uint32)
-        mean = np.zeros(cap, np.float32)
-        sd = np.zeros(cap, np.float32)
-        c = self.L.or_get_particle_map(self.h, i, cells.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                       mean.ctypes.data_as(C.POINTER(C.c_float)), sd.ctypes.data_as(C.POINTER(C.c_float)),
-                                       cap)
-        k = min(c, cap)
-        return cells[:k], mean[:k], sd[:k]
+    def particle_map(self, i, cap=1024):
+        while True:
+            cells = np.zeros(cap, np.uint32)
+            mean = np.zeros(cap, np.float32)
+            sd = np.zeros(cap, np.float32)
+            c = self.L.or_get_particle_map(self.h, i, cells.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                           mean.ctypes.data_as(C.POINTER(C.c_float)),
+                                           sd.ctypes.data_as(C.POINTER(C.c_float)), cap)
+            if c <= cap:
+                return cells[:c], mean[:c], sd[:c]
+            cap = c
+
+    def pages_in_use(self):
+        return int(self.L.or_pages_in_use(self.h))
 
     def debug(self):
         n = self.count()
