@@ -24,14 +24,19 @@
 using namespace eslam_dev;
 
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
-                                                   const DebugRec* d, const MapStore* store, hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, uint64_t pool, hipStream_t stream);
+                                                   const DebugRec* d, const LocalMaps* store, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const LocalMaps* lm, uint64_t n, uint64_t pool, hipStream_t stream);
 extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, const GatherView* gv,
-                                              hipStream_t stream);
-extern "C" hipError_t eslam_launch_store_receive(SidRef sid, const MapStore* ms, uint64_t n, const CowScratch* cs,
-                                                 const void* payloads, hipStream_t stream);
-extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
-                                             const MergeParams* mp, hipStream_t stream);
+                                              uint32_t* tgen, hipStream_t stream);
+extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint64_t n,
+                                                 const CowScratch* cs, const void* hdr, uint64_t nrecv, uint32_t* hoff,
+                                                 const void* pay, uint32_t* pgc, hipStream_t stream);
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                             const MergeParams* mp, uint32_t* pgc, hipStream_t stream);
+extern "C" hipError_t eslam_launch_pay_hdr(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
+                                           uint64_t gbase, const LocalMaps* lm, void* hdr, uint32_t* off, hipStream_t stream);
+extern "C" hipError_t eslam_launch_pay_pack(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
+                                            uint64_t gbase, const LocalMaps* lm, const uint32_t* off, void* pay, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
                                                 eslam_particle_record* out, eslam_cpoint* cps, uint32_t max_cp,
@@ -51,7 +56,7 @@ extern "C" hipError_t eslam_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uin
                                              void* tmp, size_t* tmp_bytes, hipStream_t stream);
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  const GatherView* gv, const MapStore* store, hipStream_t stream,
+                                                  const GatherView* gv, const LocalMaps* store, hipStream_t stream,
                                                   const ChunkSel* sel, double* bspill);
 extern "C" hipError_t eslam_launch_commit(Ctl* ctl, hipStream_t stream);
 extern "C" hipError_t eslam_launch_weight_stats(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl, Shard* shards,
@@ -70,8 +75,7 @@ extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, cons
                                                   uint64_t* host_out, uint64_t* host_epoch, uint64_t epoch,
                                                   hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
-                                        const uint64_t* first_last, uint64_t nsend, void* send, const MapStore* ms,
-                                        void* payloads, hipStream_t stream);
+                                        const uint64_t* first_last, uint64_t nsend, void* send, hipStream_t stream);
 extern "C" hipError_t eslam_launch_expand(const void* recv, uint64_t nrecv, uint64_t W0, uint32_t* marks, uint32_t* row_first,
                                           hipStream_t stream);
 extern "C" uint64_t eslam_record_bytes(void);
@@ -253,10 +257,14 @@ struct eslam_ctx {
     uint32_t scan_tag = 0;                  // the last K3 launch's tag (1..7)
     uint32_t* anc = nullptr;
     bool has_anc = false;
-    // per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): the map stores and the copy-on-write scratch
-    MapStore store = {};
+    // per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): the tables, pages and the copy-on-write scratch
+    LocalMaps lm = {};
+    bool lm_ready = false;                   // lm sized for the current map and particle count
     uint32_t* sid_mem = nullptr;             // 2 x cap: DevState::sid of both state buffers
     uint32_t* cow = nullptr;                 // owner, counts, free and sharing lists + the copy count
+    uint16_t* lm_need = nullptr;             // per particle: pages its merge may take (MergeParams::need)
+    uint32_t* lm_poff = nullptr;             // per merge block: page offsets (+ total)
+    uint32_t* lm_pgc = nullptr;              // the page collection's compaction counts
     uint64_t* merge_cnt = nullptr;           // the map merge's statistics slots (2 x kMergeCounterSlots) and
                                              // the copy-on-write copies since the last merge
     // logDebug records of the last update (ESLAM_FLAG_RECORD_CONTACTS / log_debug)
@@ -269,6 +277,7 @@ struct eslam_ctx {
     Ctl* ctl_host = nullptr;    // pinned
     uint32_t* fault_host = nullptr;         // host-mapped: kFaultTimeout when a device wait gave up
     bool poisoned = false;                  // the particle set is undefined until re-initialised
+    bool poison_pages = false;              // ... because the map pages ran out (kFaultPages)
     uint32_t spin_limit = kSpinLimit;       // polls of K3's cross-block waits (debug: 0 gives up at once)
     uint32_t* jump = nullptr;
     uint32_t jump_n = 1;                    // A^n_global, cached
@@ -300,9 +309,14 @@ struct eslam_ctx {
     uint2* range = nullptr;                 // per particle: [lo, hi) of its global outputs
     void* sendbuf = nullptr; uint64_t send_cap = 0;
     void* recvbuf = nullptr; uint64_t recv_cap = 0;
-    // per-particle maps on a sharded filter: the migrated particles' stores (StorePayload per
-    // record, in the records' order) and whether a store copy on write is still owed to them
+    // per-particle maps on a sharded filter: the migrated particles' maps (a MapPayHdr per
+    // record, then their pages as MapPayPage, in the records' order) and whether their tables
+    // are still owed to them
     void* sendpay = nullptr; uint64_t sendpay_cap = 0;
+    void* sendhdr = nullptr; uint64_t sendhdr_cap = 0;
+    void* recvhdr = nullptr; uint64_t recvhdr_cap = 0;
+    uint32_t* payoff = nullptr; uint64_t payoff_cap = 0;   // header prefix (send side, then receive side)
+    uint64_t nrecv_maps = 0;                 // records whose maps wait in recvhdr / recvpay
     double* cent = nullptr; uint64_t cent_bytes = 0;   // sharded getCentroid's chunk records (set_comm)
     double* bspill = nullptr; uint64_t bspill_cap = 0;  // K1's parked per-bucket sums (k1_bspill_bytes)
     void* recvpay = nullptr; uint64_t recvpay_cap = 0;
@@ -458,6 +472,7 @@ extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ?
 
 static int materialize(eslam_ctx* ctx);
 static int store_receive(eslam_ctx* ctx);
+static int local_maps_reset(eslam_ctx* ctx);
 static GatherView gather_view(eslam_ctx* ctx);
 
 static const char* kPoisonMsg =
@@ -467,10 +482,25 @@ static const char* kPoisonMsg =
 // a device wait that gave up poisons the filter (kFaultTimeout): seen here from the
 // host-mapped word without a synchronisation, so the next call after the faulting launch
 // fails instead of building on a corrupt particle set
+static const char* kPagesMsg =
+    "per-particle maps: the page pool cannot hold a map update's pages even after a collection "
+    "(raise eslam_config.local_map_pages); the particle set is undefined until the filter is re-initialised";
+
+static int poison_fail(eslam_ctx* ctx)
+{
+    return ctx->poison_pages ? fail(ctx, ESLAM_ERR_OUT_OF_MEMORY, kPagesMsg) : fail(ctx, ESLAM_ERR_HIP, kPoisonMsg);
+}
+
 static int check_poisoned(eslam_ctx* ctx)
 {
-    if (!ctx->poisoned && (__atomic_load_n(ctx->fault_host, __ATOMIC_ACQUIRE) & kFaultTimeout)) ctx->poisoned = true;
-    return ctx->poisoned ? fail(ctx, ESLAM_ERR_HIP, kPoisonMsg) : ESLAM_OK;
+    if (!ctx->poisoned) {
+        const uint32_t f = __atomic_load_n(ctx->fault_host, __ATOMIC_ACQUIRE);
+        if (f & (kFaultTimeout | kFaultPages)) {
+            ctx->poisoned = true;
+            ctx->poison_pages = (f & kFaultPages) != 0;
+        }
+    }
+    return ctx->poisoned ? poison_fail(ctx) : ESLAM_OK;
 }
 
 static int read_ctl(eslam_ctx* ctx)
@@ -572,16 +602,24 @@ static void free_debug(eslam_ctx* ctx)
 
 static bool particle_maps(const eslam_ctx* ctx) { return (ctx->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS) != 0; }
 
-static const MapStore* store_of(const eslam_ctx* ctx) { return particle_maps(ctx) ? &ctx->store : nullptr; }
+static const LocalMaps* store_of(const eslam_ctx* ctx) { return particle_maps(ctx) ? &ctx->lm : nullptr; }
+
+static void free_local_maps(eslam_ctx* ctx)
+{
+    (void)hipFree(ctx->lm.ctr); (void)hipFree(ctx->lm.slot); (void)hipFree(ctx->lm.page); (void)hipFree(ctx->lm.tgen);
+    (void)hipFree(ctx->lm.owner); (void)hipFree(ctx->lm.frees); (void)hipFree(ctx->lm.mark);
+    (void)hipFree(ctx->lm_need); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc);
+    ctx->lm = LocalMaps{};
+    ctx->lm_need = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr;
+    ctx->lm_ready = false;
+}
 
 static void free_particles(eslam_ctx* ctx)
 {
     free_debug(ctx);
-    (void)hipFree(ctx->store.key); (void)hipFree(ctx->store.val); (void)hipFree(ctx->store.count);
-    (void)hipFree(ctx->store.box);
+    free_local_maps(ctx);
     (void)hipFree(ctx->sid_mem); (void)hipFree(ctx->cow); (void)hipFree(ctx->merge_cnt);
     ctx->merge_cnt = nullptr;
-    ctx->store = MapStore{};
     ctx->sid_mem = nullptr;
     ctx->cow = nullptr;
     ctx->st[0].sid = ctx->st[1].sid = nullptr;
@@ -625,6 +663,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
     (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay); (void)hipFree(ctx->cent); (void)hipFree(ctx->bspill);
+    (void)hipFree(ctx->sendhdr); (void)hipFree(ctx->recvhdr); (void)hipFree(ctx->payoff);
     (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
     (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -690,23 +729,14 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
     HIPCHK(ctx, hipMemset(ctx->marks, 0, cap * 4));
     if (keep_ancestors(ctx)) HIPCHK(ctx, hipMalloc(&ctx->anc, cap * 4));
     if (particle_maps(ctx)) {
-        // one store per particle; particle i starts with store i, empty (cloneMaps of a fresh
-        // filter over the shared map: every particle its own, still empty, local patches)
+        // the table names of both state buffers; the tables and pages come with the map
+        // (local_maps_reset: their window size follows the map's cell size)
         HIPCHK(ctx, hipMalloc(&ctx->sid_mem, 2 * cap * 4));
         ctx->st[0].sid = ctx->sid_mem;
         ctx->st[1].sid = ctx->sid_mem + cap;
-        // the store pool: twice the particles, so a map update always finds a free store for
-        // every particle that changes a shared map (eslam_internal.h store_pool)
-        const uint64_t pool = store_pool(cap);
-        HIPCHK(ctx, hipMalloc(&ctx->store.key, pool * kStoreSlots * 4));
-        HIPCHK(ctx, hipMalloc(&ctx->store.val, pool * kStoreSlots * sizeof(float2)));
-        HIPCHK(ctx, hipMalloc(&ctx->store.count, pool * 4));
-        HIPCHK(ctx, hipMalloc(&ctx->store.box, pool * sizeof(uint4)));
         HIPCHK(ctx, hipMalloc(&ctx->cow, cow_words(cap) * 4));
         HIPCHK(ctx, hipMalloc(&ctx->merge_cnt, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t)));
         HIPCHK(ctx, hipMemset(ctx->merge_cnt, 0, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t)));
-        HIPCHK(ctx, eslam_launch_store_init(ctx->st[0].sid, &ctx->store, cap, pool, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->n = n;
     ctx->cap = cap;
@@ -716,6 +746,59 @@ static int alloc_particles(eslam_ctx* ctx, uint64_t n)
         ctx->n_global = n;
         ctx->gbase = 0;
     }
+    return local_maps_reset(ctx);
+}
+
+// Per-particle maps, sized for the current map and particle count: every
+// particle names its own empty table (cloneMaps of the reference's empty grid template,
+// src/EmbodiedSlamFilter.cpp:131-134), every page free.  A window of (2h + 1)^2 tiles reaching
+// maxSensorRange (dm_lm_half of the cell size); a pool of 2 x cap tables and local_map_pages
+// pages per particle.  Runs at particle allocation and at set_map (the tables name cells of
+// the map, so a new map starts them over).
+static int local_maps_reset(eslam_ctx* ctx)
+{
+    free_local_maps(ctx);
+    if (!particle_maps(ctx) || !ctx->has_map || !ctx->n) return ESLAM_OK;
+    const double r = ctx->cfg.max_sensor_range;
+    if (!(r == r) || r < 0.0 || r > 1e6) return fail(ctx, ESLAM_ERR_INVALID_ARG, "max_sensor_range must be finite and >= 0");
+    LocalMaps& lm = ctx->lm;
+    lm.hx = dm_lm_half(r, ctx->map_scale[0]);
+    lm.hy = dm_lm_half(r, ctx->map_scale[1]);
+    lm.wx = 2 * lm.hx + 1;
+    lm.wy = 2 * lm.hy + 1;
+    lm.S = lm.wx * lm.wy;
+    lm.mx = lm_magic(lm.wx);
+    lm.my = lm_magic(lm.wy);
+    lm.bx = lm.wx * (((1u << 29) + lm.wx - 1) / lm.wx);
+    lm.by = lm.wy * (((1u << 29) + lm.wy - 1) / lm.wy);
+    const uint64_t cap = ctx->cap, pool = store_pool(cap);
+    const uint64_t per = ctx->cfg.local_map_pages ? ctx->cfg.local_map_pages : kDefaultMapPages;
+    lm.ntables = pool;
+    lm.npages = cap * per;
+    if (lm.npages >= 0xffffffffull) return fail(ctx, ESLAM_ERR_INVALID_ARG, "per-particle map pool: at most 2^32 - 1 pages");
+    const uint64_t ptiles = (lm.npages + kCompactTileItems - 1) / kCompactTileItems;
+    HIPCHK(ctx, hipMalloc(&lm.ctr, pool * sizeof(int2)));
+    HIPCHK(ctx, hipMalloc(&lm.slot, pool * lm.S * 4));
+    HIPCHK(ctx, hipMalloc(&lm.tgen, pool * 4));
+    HIPCHK(ctx, hipMalloc(&lm.page, lm.npages * DM_LM_PAGE_CELLS * sizeof(float2)));
+    HIPCHK(ctx, hipMalloc(&lm.owner, lm.npages * 8));
+    HIPCHK(ctx, hipMalloc(&lm.frees, lm.npages * 4));
+    HIPCHK(ctx, hipMalloc(&lm.mark, ((lm.npages + 15) / 16) * 16));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_need, cap * 2));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_poff, ((cap + kLmBlock - 1) / kLmBlock + 1) * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_pgc, (ptiles + 1) * 4));
+    HIPCHK(ctx, eslam_launch_store_init(ctx->sid_mem, &lm, cap, pool, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    // the free list holds every page (k_store_init: frees[p] = p)
+    int rc = read_ctl(ctx);
+    if (rc) return rc;
+    ctx->ctl_host->pg_cursor = 0;
+    ctx->ctl_host->pg_nfree = lm.npages;
+    ctx->ctl_host->pg_total = 0;
+    ctx->ctl_host->pg_gc = 0;
+    rc = write_ctl(ctx);
+    if (rc) return rc;
+    ctx->lm_ready = true;
     return ESLAM_OK;
 }
 
@@ -1064,16 +1147,18 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
     for (int k = 0; k < 12; ++k)
         if (!(g->global2local[k] == kId[k])) m.g2l_identity = 0;
     ctx->has_map = true;
-    return ESLAM_OK;
+    // per-particle maps name cells of the previous grid: they start over, empty
+    return local_maps_reset(ctx);
 }
 
 static int reset_ctl_for_new_particles(eslam_ctx* ctx, int wexp)
 {
     int rc = read_ctl(ctx);
     if (rc) return rc;
-    if (ctx->poisoned || (ctx->ctl_host->err & kFaultTimeout)) {
+    if (ctx->poisoned || (ctx->ctl_host->err & (kFaultTimeout | kFaultPages))) {
         // a poisoned filter starts over: the fault cleared, no partial segment marks left
-        ctx->ctl_host->err &= ~(uint64_t)kFaultTimeout;
+        ctx->ctl_host->err &= ~(uint64_t)(kFaultTimeout | kFaultPages);
+        ctx->poison_pages = false;
         __atomic_store_n(ctx->fault_host, 0u, __ATOMIC_RELAXED);
         HIPCHK(ctx, hipMemsetAsync(ctx->marks, 0, ctx->cap * 4, ctx->stream));
         ctx->poisoned = false;
@@ -1475,6 +1560,21 @@ extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64
 // ---------------------------------------------------------------------------------------
 // per-particle local maps
 // ---------------------------------------------------------------------------------------
+// the map-update parameters every copy-on-write pass shares (the merge, a sharded receive)
+static MergeParams merge_params(eslam_ctx* ctx, const CowScratch& cs)
+{
+    MergeParams mp;
+    memset(&mp, 0, sizeof(mp));
+    mp.cnt = ctx->merge_cnt;
+    mp.ref = cs.ref;
+    mp.frees = cs.frees;
+    mp.need = ctx->lm_need;
+    mp.poff = ctx->lm_poff;
+    mp.fault = ctx->fault_host;
+    mp.n = ctx->n;
+    return mp;
+}
+
 extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count)
 {
     if (!ctx || (!patches && count)) return ESLAM_ERR_INVALID_ARG;
@@ -1483,6 +1583,12 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
     if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    if (const int rc_ = check_poisoned(ctx)) return rc_;
+    if (!ctx->lm_ready) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "per-particle maps not allocated");
+    for (uint32_t k = 0; k < count; ++k)
+        if (!dm_isfinite(patches[k].position[0]) || !dm_isfinite(patches[k].position[1]) ||
+            !dm_isfinite(patches[k].position[2]) || !dm_isfinite(patches[k].stdev))
+            return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: scan patches must be finite");
     mrec(ctx, 0);
     // one GPU: a pending resample gather runs inside the merge (MergeParams::fuse: the store
     // classes and the merge read the particles through the marks), so the update reads and
@@ -1497,22 +1603,18 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     mrec(ctx, 1);
     const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
     const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
-    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, fuse ? &gv : nullptr, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, fuse ? &gv : nullptr, ctx->lm.tgen, ctx->stream));
     mrec(ctx, 2);
-    MergeParams mp;
-    memset(&mp, 0, sizeof(mp));
+    MergeParams mp = merge_params(ctx, cs);
+    mp.is_id = ctx->map.g2l_identity;
     mp.gv = gv;
     mp.gbase = ctx->gbase;
     mp.fuse = fuse ? 1u : 0u;
     mp.aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
-    mp.cnt = ctx->merge_cnt;
-    mp.ref = cs.ref;
-    mp.frees = cs.frees;
-    mp.n = ctx->n;
     mp.m = count;
     for (uint32_t k = 0; k < count; ++k)
         mp.sp[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
-    HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->store, &mp, ctx->stream));
+    HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->lm_pgc, ctx->stream));
     if (fuse) {
         HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));     // the gather's buffer flip, if one ran
     }
@@ -1542,24 +1644,37 @@ extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32
     int rc = materialize(ctx);
     if (!rc) rc = read_ctl(ctx);
     if (rc) return rc;
+    *count = 0;
+    if (!ctx->lm_ready) return ESLAM_OK;
+    const LocalMaps& lm = ctx->lm;
     const uint32_t* sid = ctx->st[ctx->ctl_host->base ^ ctx->ctl_host->flip].sid;
-    uint32_t s = 0;
-    HIPCHK(ctx, hipMemcpy(&s, sid + index, 4, hipMemcpyDeviceToHost));
-    uint32_t key[kStoreSlots];
-    float2 val[kStoreSlots];
-    HIPCHK(ctx, hipMemcpy(key, ctx->store.key + (uint64_t)s * kStoreSlots, sizeof(key), hipMemcpyDeviceToHost));
-    HIPCHK(ctx, hipMemcpy(val, ctx->store.val + (uint64_t)s * kStoreSlots, sizeof(val), hipMemcpyDeviceToHost));
-    uint32_t c = 0;
-    for (uint32_t t = 0; t < kStoreSlots; ++t) {
-        if (key[t] == kStoreFree) continue;
-        if (c < capacity) {
-            if (cells) cells[c] = key[t] - 1u;
-            if (mean) mean[c] = val[t].x;
-            if (stdev) stdev[c] = val[t].y;
+    uint32_t X = 0;
+    HIPCHK(ctx, hipMemcpy(&X, sid + index, 4, hipMemcpyDeviceToHost));
+    int2 c;
+    std::vector<uint32_t> sl(lm.S);
+    HIPCHK(ctx, hipMemcpy(&c, lm.ctr + X, sizeof(int2), hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(sl.data(), lm.slot + (uint64_t)X * lm.S, lm.S * 4, hipMemcpyDeviceToHost));
+    // tiles in slot order, each tile's cells row by row (the oracle's or_get_particle_map)
+    uint32_t k = 0;
+    float2 cell[DM_LM_PAGE_CELLS];
+    for (uint32_t sb = 0; sb < lm.wy; ++sb)
+        for (uint32_t sa = 0; sa < lm.wx; ++sa) {
+            const uint32_t pg = sl[sa + lm.wx * sb];
+            if (pg == DM_LM_NONE) continue;
+            const int64_t a = dm_lm_tile_of(sa, c.x, lm.hx, lm.wx), b = dm_lm_tile_of(sb, c.y, lm.hy, lm.wy);
+            HIPCHK(ctx, hipMemcpy(cell, lm.page + (uint64_t)pg * DM_LM_PAGE_CELLS, sizeof(cell), hipMemcpyDeviceToHost));
+            for (uint32_t j = 0; j < DM_LM_PAGE_CELLS; ++j) {
+                if (!dm_lm_holds(cell[j].y)) continue;
+                if (k < capacity) {
+                    const uint64_t m = (uint64_t)(8 * a) + (j & 7u), n = (uint64_t)(8 * b) + (j >> 3);
+                    if (cells) cells[k] = (uint32_t)(n * ctx->map.width + m);
+                    if (mean) mean[k] = cell[j].x;
+                    if (stdev) stdev[k] = cell[j].y;
+                }
+                ++k;
+            }
         }
-        ++c;
-    }
-    *count = c;
+    *count = k;
     return ESLAM_OK;
 }
 
@@ -1590,8 +1705,12 @@ static int store_receive(eslam_ctx* ctx)
 {
     const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
     const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
-    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, nullptr, ctx->stream));
-    HIPCHK(ctx, eslam_launch_store_receive(sr, &ctx->store, ctx->n, &cs, ctx->recvpay, ctx->stream));
+    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, nullptr, ctx->lm.tgen, ctx->stream));
+    int rc = grow(ctx, (void**)&ctx->payoff, &ctx->payoff_cap, (ctx->nrecv_maps + 1) * 4, false);
+    if (rc) return rc;
+    const MergeParams mp = merge_params(ctx, cs);
+    HIPCHK(ctx, eslam_launch_store_receive(sr, ctx->ctl, &ctx->lm, &mp, ctx->n, &cs, ctx->recvhdr, ctx->nrecv_maps, ctx->payoff,
+                                           ctx->recvpay, ctx->lm_pgc, ctx->stream));
     ctx->cow_pending = false;
     return ESLAM_OK;
 }
@@ -1748,6 +1867,53 @@ static int abort_pending_gather(eslam_ctx* ctx, hipError_t e, int rc = ESLAM_ERR
 // shard) measured the same as 200 us on one rank at 2M and 4M (profiles/r02/ab_spin.log)
 constexpr long kSpinBoundUs = 200;
 
+// Per-particle maps on a sharded filter: every record's map travels with it:
+// a header per record (its source's table centre and page count), then the pages, each with
+// its slot.  The page counts per destination come from the headers' prefix; the receivers learn
+// theirs from an all_gather.  The received maps get local tables and pages in store_receive.
+static int exchange_maps(eslam_ctx* ctx, uint64_t nsend, uint64_t nrecv, const uint64_t* sb, const uint64_t* rb,
+                         const PlanParams& pp, hipStream_t xs)
+{
+    const int G = ctx->comm.nranks, me = ctx->comm.rank;
+    const uint64_t R = eslam_record_bytes(), H = sizeof(MapPayHdr), P = sizeof(MapPayPage);
+    int rc = grow(ctx, &ctx->sendhdr, &ctx->sendhdr_cap, (nsend ? nsend : 1) * H, false);
+    if (!rc) rc = grow(ctx, &ctx->recvhdr, &ctx->recvhdr_cap, (nrecv ? nrecv : 1) * H, false);
+    if (!rc) rc = grow(ctx, (void**)&ctx->payoff, &ctx->payoff_cap, (nsend + nrecv + 2) * 4, false);
+    if (rc) return rc;
+    HIPCHK(ctx, eslam_launch_pay_hdr(ctx->st[0], ctx->st[1], ctx->ctl, ctx->sendbuf, nsend, ctx->gbase, &ctx->lm, ctx->sendhdr,
+                                     ctx->payoff, xs));
+    // the page counts per destination (records [send_off[d], send_off[d + 1]) go to rank d)
+    std::vector<uint32_t> bound(G + 1);
+    for (int d = 0; d <= G; ++d)
+        HIPCHK(ctx, hipMemcpyAsync(&bound[d], ctx->payoff + pp.send_off[d], 4, hipMemcpyDeviceToHost, xs));
+    HIPCHK(ctx, hipStreamSynchronize(xs));
+    uint64_t* h = ctx->mg_host;
+    uint64_t spg[kMaxRanks], rpg[kMaxRanks], totr = 0;
+    for (int d = 0; d < G; ++d) h[mg::kCounts + d] = spg[d] = bound[d + 1] - bound[d];
+    HIPCHK(ctx, hipMemcpyAsync(ctx->mg + mg::kCounts, &h[mg::kCounts], 8 * G, hipMemcpyHostToDevice, xs));
+    HIPCHK(ctx, hipStreamSynchronize(xs));
+    rc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpy(&h[mg::kCountsAll], ctx->mg + mg::kCountsAll, 8ull * G * G, hipMemcpyDeviceToHost));
+    for (int r = 0; r < G; ++r) { rpg[r] = h[mg::kCountsAll + r * G + me]; totr += rpg[r]; }
+    rc = grow(ctx, &ctx->sendpay, &ctx->sendpay_cap, ((uint64_t)bound[G] + 1) * P, false);
+    if (!rc) rc = grow(ctx, &ctx->recvpay, &ctx->recvpay_cap, (totr + 1) * P, false);
+    if (rc) return rc;
+    HIPCHK(ctx, eslam_launch_pay_pack(ctx->st[0], ctx->st[1], ctx->ctl, ctx->sendbuf, nsend, ctx->gbase, &ctx->lm, ctx->payoff,
+                                      ctx->sendpay, xs));
+    uint64_t hs[kMaxRanks], hr[kMaxRanks], ps[kMaxRanks], pr[kMaxRanks];
+    for (int d = 0; d < G; ++d) {
+        hs[d] = sb[d] / R * H; hr[d] = rb[d] / R * H;
+        ps[d] = spg[d] * P; pr[d] = rpg[d] * P;
+    }
+    rc = comm_alltoallv(ctx, ctx->sendhdr, hs, ctx->recvhdr, hr, xs);
+    if (!rc) rc = comm_alltoallv(ctx, ctx->sendpay, ps, ctx->recvpay, pr, xs);
+    if (rc) return rc;
+    ctx->nrecv_maps = nrecv;
+    ctx->cow_pending = nrecv > 0;
+    return ESLAM_OK;
+}
+
 static int exchange_tail(eslam_ctx* ctx, uint64_t epoch, PlanParams& pp, uint64_t* own_lo, uint64_t* own_hi,
                          hipStream_t xs = nullptr, bool* queued = nullptr);
 
@@ -1889,27 +2055,17 @@ static int exchange_tail(eslam_ctx* ctx, uint64_t epoch, PlanParams& pp, uint64_
         }
         if (any) {
             const bool maps = particle_maps(ctx);
-            const uint64_t P = sizeof(StorePayload);
             rc = grow(ctx, &ctx->sendbuf, &ctx->send_cap, nsend * R, false);
             if (!rc) rc = grow(ctx, &ctx->recvbuf, &ctx->recv_cap, nrecv * R, false);
-            if (!rc && maps) rc = grow(ctx, &ctx->sendpay, &ctx->sendpay_cap, nsend * P, false);
-            if (!rc && maps) rc = grow(ctx, &ctx->recvpay, &ctx->recvpay_cap, nrecv * P, false);
             if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
             // a side stream starts after the segments kernel (its records and ranges)
             if (xs != ctx->stream) HIPCHK(ctx, hipStreamWaitEvent(xs, ctx->ev_seg, 0));
             if (queued) *queued = true;
             const hipError_t e = eslam_launch_pack(ctx->st[0], ctx->st[1], ctx->ctl, &pp, ctx->range, ctx->mg + mg::kFirstLast,
-                                                   nsend, ctx->sendbuf, &ctx->store, maps ? ctx->sendpay : nullptr,
-                                                   xs);
+                                                   nsend, ctx->sendbuf, xs);
             if (e != hipSuccess) return abort_pending_gather(ctx, e);
             rc = comm_alltoallv(ctx, ctx->sendbuf, sb, ctx->recvbuf, rb, xs);
-            if (!rc && maps) {
-                // the migrated stores, in the records' order (the same peers, P bytes per record)
-                uint64_t sp_[kMaxRanks], rp_[kMaxRanks];
-                for (int d = 0; d < G; ++d) { sp_[d] = sb[d] / R * P; rp_[d] = rb[d] / R * P; }
-                rc = comm_alltoallv(ctx, ctx->sendpay, sp_, ctx->recvpay, rp_, xs);
-                ctx->cow_pending = !rc && nrecv > 0;
-            }
+            if (!rc && maps) rc = exchange_maps(ctx, nsend, nrecv, sb, rb, pp, xs);
             if (rc) return abort_pending_gather(ctx, hipSuccess, rc);
         } else {
             nrecv = 0;
@@ -2061,9 +2217,10 @@ static int take_update_error(eslam_ctx* ctx)
     int rc = read_ctl(ctx);
     if (rc) return rc;
     const uint64_t err = ctx->ctl_host->err;
-    if (err & kFaultTimeout) {
+    if (err & (kFaultTimeout | kFaultPages)) {
         ctx->poisoned = true;
-        return fail(ctx, ESLAM_ERR_HIP, kPoisonMsg);
+        ctx->poison_pages = (err & kFaultPages) != 0;
+        return poison_fail(ctx);
     }
     if (!(err & 1ull)) return ESLAM_OK;
     ctx->ctl_host->err = 0;

@@ -80,6 +80,11 @@ struct alignas(128) Ctl {
     uint64_t map_changed;                // stores the last map merge changed
     uint64_t map_copied;                 // shared stores the last map merge wrote to a free store
     uint64_t map_covered;                // scan patches the last map merge saw on cells the shared grid covers
+    uint64_t pg_cursor;                  // per-particle maps: next unused entry of LocalMaps::frees
+    uint64_t pg_nfree;                   //   entries in LocalMaps::frees (the last collection)
+    uint64_t pg_total;                   //   pages the current map update may take (its plan)
+    uint32_t pg_gc;                      //   the current map update collects first
+    uint32_t pg_pad;
     uint64_t fin_epoch;                  // fused finalize: the epoch of the launch whose finalize wrote
                                          // this block (checked in every block's copy of it)
 };
@@ -97,41 +102,61 @@ struct DevState {
     uint32_t* sid;                       // per-particle maps only: the particle's map store
 };
 
-// Per-particle local maps (useSharedMap = false, ESLAM_FLAG_PARTICLE_MAPS): the shared grid
-// plus, per particle, a store of patches in cells the shared grid leaves empty.  A store is
-// kStoreSlots slots holding one patch {mean, stdev} each, at most kStoreCap of them, kept
-// sorted by key = cell + 1 (free slots, all after the used ones, hold kStoreFree): a lookup is
-// a 5-step binary search with no data-dependent trip count (the oracle's open-addressing
-// table holds the same set: membership and values do not depend on the layout).
-// Particles name their store (DevState::sid); the resample copies the name, so a store may be
-// named by several particles, and a map update that changes a shared store writes the result
-// to a free store that the particle then names (copy on write: a store is never written while
-// another particle names it; the unchanged copies keep sharing).
-constexpr uint32_t kStoreSlots = 32;
-constexpr uint32_t kStoreCap = 24;
-constexpr uint32_t kStoreFree = 0xffffffffu;
-// sharded filters: a particle that a resample received from another rank names no local store
-// yet; its sid is kSidRecord | the record index, and the store copy on write that follows the
-// gather gives it a free store filled from the record's payload (the migrated store)
+// Per-particle local maps (useSharedMap = false, ESLAM_FLAG_PARTICLE_MAPS): the
+// shared grid plus, per particle, a window of (2 hx + 1) x (2 hy + 1) tiles of 8 x 8 cells
+// around the particle (eslam_detmath.h DM_LM_*: the window reaches maxSensorRange and moves
+// with the particle at every map update; tiles it leaves are forgotten).
+//   table  what a particle names (DevState::sid): the window centre and S = wx * wy slots, the
+//          slot of tile (a, b) being (a mod wx) + wx (b mod wy), each a page id or DM_LM_NONE.
+//          The resample copies the name, so copies share a table; a map update that changes
+//          a table another particle also names writes the result to a free table the particle
+//          then names (copy on write: a shared table is never written).
+//   page   the 64 cells {mean, stdev} of one tile (stdev >= 0: the cell holds a patch).  Pages
+//          are shared by tables the same way; a page is written in place only by the table
+//          that owns it at the table's current generation (LocalMaps::owner == gen << 32 |
+//          table), and a table's generation moves on whenever it is shared, so every page it
+//          had is then frozen and copied on the next write.  Free pages come from a list the
+//          map update's collection rebuilds (mark the pages live tables name, compact the
+//          rest) when the list runs short.
+// K1 reads the first 64 bytes (LocalMaps up to my) with one scalar load per lookup.
+struct LocalMaps {
+    int2* ctr;                           // per table: window centre tile (DM_LM_UNSET: an empty table)
+    uint32_t* slot;                      // per table: S page ids
+    float2* page;                        // per page: 64 cells {mean, stdev}, row-major (m & 7) + 8 (n & 7)
+    uint32_t S, wx, wy, hx;
+    uint32_t hy, pad;
+    uint64_t mx, my;                     // lm_magic(wx), lm_magic(wy)
+    // --- the map update and the collection only
+    uint32_t bx, by;                     // multiples of wx, wy >= 2^29 (non-negative residues)
+    uint32_t* tgen;                      // per table: generation (bumped when a map update finds it shared)
+    uint64_t* owner;                     // per page: gen << 32 | the table that may write it in place
+    uint32_t* frees;                     // the free pages, in page order, from the last collection
+    uint8_t* mark;                       // per page: a live table names it (the collection's marks)
+    uint64_t npages, ntables;
+};
+static_assert(sizeof(int2) == 8, "centre");
+// sharded filters: a particle that a resample received from another rank names no local table
+// yet; its sid is kSidRecord | the record index, and the copy on write that follows the gather
+// gives it a free table (and pages) filled from the record's payload (the migrated map)
 constexpr uint32_t kSidRecord = 0x80000000u;
-struct alignas(8) StorePayload {
-    uint32_t count, pad;
-    uint32_t box[4];                     // MapStore::box
-    uint32_t key[kStoreCap];
-    float2 val[kStoreCap];
+// a migrated map: the header per record (its table's centre and page count), then the pages
+// of all records in the records' order, each with its slot
+struct alignas(8) MapPayHdr {
+    int2 ctr;
+    uint32_t npg, pad;
 };
-static_assert(kStoreSlots == 32 && kStoreCap < kStoreSlots, "store search: 5 halving steps, a free slot at the end");
-struct MapStore {
-    uint32_t* key;                       // store_pool(cap) stores x kStoreSlots
-    float2* val;                         // store_pool(cap) stores x kStoreSlots: {mean, stdev}
-    uint32_t* count;                     // patches per store
-    // per store: the bounding box {m0, m1, n0, n1} (inclusive cell columns m and rows n) of
-    // its cells, a superset kept by the inserts (empty: m0 > m1).  A cell outside it is not in
-    // the store, so the map merge skips the 24-key membership test for the cells a robot has
-    // moved past (merge 1.07 -> 0.87 ms at 8M): acceleration only, no result depends on it
-    uint4* box;
+struct alignas(8) MapPayPage {
+    uint32_t slot, pad;
+    float2 cell[DM_LM_PAGE_CELLS];
 };
-constexpr uint32_t kBoxEmptyLo = 0xffffffffu;
+static_assert(sizeof(MapPayPage) == 520, "payload page");
+// the tables' pool holds 2 x cap tables: at most n <= cap are named by a particle, so at least
+// cap are free whenever a map update starts, and particle i may take the i-th free one (copy
+// on write with a fixed, deterministic allocation of tables and no allocation counter)
+inline uint64_t store_pool(uint64_t cap) { return 2 * cap; }
+// a ceil(2^40 / w) multiplier: (a * m) >> 40 = floor(a / w) for a < 2^29, w < 2^11
+inline uint64_t lm_magic(uint32_t w) { return ((1ull << 40) + w - 1) / w; }
+constexpr uint32_t kDefaultMapPages = 16;       // pages per particle when the config says 0
 
 // K1 reads the first 64 bytes (the lookup header) with one scalar load per lookup
 struct MapView {
@@ -224,7 +249,7 @@ struct K1Args {
     DevState s[2];
     Ctl* ctl;
     Shard* shards;
-    MapStore store;                      // per-particle maps (the DELTA instantiations only)
+    LocalMaps store;                     // per-particle maps (the DELTA instantiations only)
     ChunkSel sel;                        // the chunks this launch processes
     double* bspill;                      // per chunk: the per-bucket sums a wave is not in (k1_bspill_bytes)
 };
@@ -238,6 +263,7 @@ struct ScanPatch {
     double x, y, z, stdev;
 };
 constexpr int kMaxScanPatches = 64;
+constexpr int kLmBlock = 128;                   // particles per block of k_map_plan / k_map_merge
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
 constexpr uint32_t kMergeCounters = 4;
 
@@ -248,10 +274,6 @@ struct SidRef {
     uint32_t* s1;
     const Ctl* ctl;
 };
-// The store pool holds 2 x cap stores: at most n <= cap are named by a particle, so at least
-// cap are free whenever a map update starts, and particle i may take the i-th free store
-// (copy on write with a fixed, deterministic allocation and no allocation counter).
-inline uint64_t store_pool(uint64_t cap) { return 2 * cap; }
 // the copy-on-write scratch (u32 words): ref (pool), the two compactions' tile counts, the
 // free stores (pool), the received particles (cap), the received count, the free count
 struct CowScratch {
@@ -286,11 +308,14 @@ inline CowScratch cow_layout(uint32_t* base, uint64_t cap)
 struct MergeParams {
     uint64_t n;
     uint32_t m;                          // scan patches
-    uint32_t pad;
+    uint32_t is_id;                      // the grid's global2local is the identity
     uint64_t* cnt;                       // kMergeCounters x kMergeCounterSlots: dropped patches, changed
                                          // stores, copies, patches on covered cells (zeroed)
     const uint32_t* ref;                 // CowScratch::ref of this update
-    const uint32_t* frees;               // CowScratch::frees: particle i's store if it writes a shared map
+    const uint32_t* frees;               // CowScratch::frees: particle i's table if it writes a shared map
+    uint16_t* need;                      // per particle: the pages its merge may take (k_map_plan)
+    uint32_t* poff;                      // per block of kLmBlock particles: first page offset (+ total)
+    uint32_t* fault;                     // host-mapped fault word (kFaultPages)
     GatherView gv;                       // fuse: a pending resample gather runs in the merge (one GPU)
     uint64_t gbase;
     uint32_t fuse, aux;                  // aux: carry mprob / flags (ESLAM_FLAG_NO_AUX_GATHER unset)
@@ -359,6 +384,9 @@ constexpr uint32_t kPubReplicas = 8;
 // host-mapped word, writes nothing further, and every later launch that sees the bit in
 // ctl->err returns at once; the host refuses the filter until it is re-initialised.
 constexpr uint32_t kFaultTimeout = 4u;
+// the per-particle maps' page pool could not hold a map update's pages even after a collection:
+// the update wrote nothing and the filter is poisoned like a timeout (ESLAM_ERR_OUT_OF_MEMORY)
+constexpr uint32_t kFaultPages = 8u;
 constexpr uint32_t kSpinLimit = 1u << 18;    // x s_sleep(8) (512 clocks): ~60 ms
 
 constexpr int kMaxRanks = 16;

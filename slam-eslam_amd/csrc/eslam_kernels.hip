@@ -259,6 +259,8 @@ static_assert(offsetof(StepParams, mu) == 24 && offsetof(StepParams, L22) == 88 
               "K1 scalar-load blocks");
 static_assert(offsetof(MapView, width) == 48 && offsetof(MapView, height) == 64, "map lookup header");
 static_assert(offsetof(ContactC, pz) == 32 && offsetof(GatherView, record) == 32, "K1 scalar-load blocks");
+static_assert(offsetof(LocalMaps, S) == 24 && offsetof(LocalMaps, hy) == 40 && offsetof(LocalMaps, mx) == 48 &&
+                  offsetof(LocalMaps, my) == 56, "K1 reads the local maps' first 64 bytes");
 
 // ---------------------------------------------------------------------------------------
 // GridAccess::get -> MLSMap::getPatch(C_global2local * p, patch, 3.0)  (src/PoseEstimator.hpp:97-105)
@@ -316,37 +318,28 @@ __device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint
     return false;
 }
 
-// per-particle maps: the patch of a cell the shared grid leaves empty, from the particle's
-// store (K1Args::store), with the same 3-sigma gate as a grid patch
-__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t cell, double lz, double qv, double& mean, double& stdev)
+// per-particle maps: the patch of cell (m, n), which the shared grid leaves empty, from the
+// particle's table (K1Args::store) with the same 3-sigma gate as a grid patch:
+// the table's centre and the tile's slot load together, then the page cell
+__device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t m, uint32_t n, double lz, double qv, double& mean,
+                                            double& stdev)
 {
-    const su8 st = kl8(KOFF(store));                  // key, val, count, box
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    const gmem<const uint32_t>* key = kp<const uint32_t>(st, 0) + (uint64_t)sid * kStoreSlots;
-    const gmem<const uint64_t>* val = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(st, 1)) +
-                                      (uint64_t)sid * kStoreSlots;
-    const uint32_t target = cell + 1u;
-    // lower bound in the sorted keys in two memory round trips (one 128-byte line): the last
-    // keys of the first three quarters pick the quarter, whose 8 keys come in two 16-byte
-    // loads (8 registers in flight rather than 16).  The store's bounding box is not consulted
-    // here: the quarter keys share the key line, so the box saves no fetch, only a test (K1
-    // DELTA with and without it: 0.516 / 0.516 ms at 8M, profiles/r04/ab_r04h_maps_box.log)
-    const uint32_t k7 = key[7], k15 = key[15], k23 = key[23];
-    const uint32_t q0 = (k7 < target ? 1u : 0u) + (k15 < target ? 1u : 0u) + (k23 < target ? 1u : 0u);
-    const gmem<const u4>* kv = reinterpret_cast<const gmem<const u4>*>(key + 8u * q0);
-    uint32_t pos = 8u * q0, hit = 0;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const u4 k4 = kv[q];
-        pos += (k4.x < target) + (k4.y < target) + (k4.z < target) + (k4.w < target);
-        hit |= (k4.x == target) | (k4.y == target) | (k4.z == target) | (k4.w == target);
-    }
-    if (hit) {
-        const uint64_t pf = val[pos];
-        return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), __uint_as_float((uint32_t)(pf >> 32)), lz, qv, mean,
-                          stdev);
-    }
-    return false;
+    const su8 h = kl8(KOFF(store));                  // ctr, slot, page, {S, wx}, {wy, hx}, {hy, -}, mx, my
+    const uint64_t w3 = kq(h, 3), w4 = kq(h, 4);
+    const uint32_t S = (uint32_t)w3, wx = (uint32_t)(w3 >> 32), wy = (uint32_t)w4, hx = (uint32_t)(w4 >> 32);
+    const uint32_t hy = (uint32_t)kq(h, 5);
+    const uint32_t a = m >> DM_LM_TILE_BITS, b = n >> DM_LM_TILE_BITS;
+    const uint32_t qa = (uint32_t)(((uint64_t)a * kq(h, 6)) >> 40), qb = (uint32_t)(((uint64_t)b * kq(h, 7)) >> 40);
+    const uint32_t s = (a - wx * qa) + wx * (b - wy * qb);
+    const uint64_t c = kp<const uint64_t>(h, 0)[sid];   // int2 {x, y}
+    const uint32_t pg = kp<const uint32_t>(h, 1)[(uint64_t)sid * S + s];
+    if (!dm_lm_inside(a, (int32_t)(uint32_t)c, hx, wx) || !dm_lm_inside(b, (int32_t)(uint32_t)(c >> 32), hy, wy) || pg == DM_LM_NONE)
+        return false;
+    const uint64_t pf = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(h, 2))
+        [(uint64_t)pg * DM_LM_PAGE_CELLS + (m & 7u) + 8u * (n & 7u)];
+    const float sd = __uint_as_float((uint32_t)(pf >> 32));
+    if (!dm_lm_holds(sd)) return false;
+    return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), sd, lz, qv, mean, stdev);
 }
 
 // the map is K1Args::map, read by scalar loads (header: 64 bytes per lookup).  DELTA: the
@@ -393,7 +386,7 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     if constexpr (DELTA) {
         if (!in_grid || (in_win && wc.count == 1)) return false;
-        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)in * width + (uint32_t)im, lz, qv, mean, stdev);
+        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
     } else {
         if (!in_grid || (in_win && wc.count <= 1)) return false;
     }
@@ -412,7 +405,7 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         b = ct.z;
         e = ct.z + ct.w;
         if constexpr (DELTA) {
-            if (b == e) return store_patch(sid, (uint32_t)cell, lz, qv, mean, stdev);
+            if (b == e) return store_patch(sid, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
         }
         if (!has_height && b < e) {
             if (patch_gate(nullptr, 0, __uint_as_float(ct.x), __uint_as_float(ct.y), lz, qv, mean, stdev)) return true;
@@ -1386,76 +1379,96 @@ __global__ void __launch_bounds__(1024) k_scan_excl(uint32_t* __restrict__ a, ui
 }
 
 // ---------------------------------------------------------------------------------------
-// Per-particle local maps (useSharedMap = false): processMap's merge of a
-// scan into every particle's map (src/EmbodiedSlamFilter.cpp:179-232) and cloneMaps' "no two
-// particles share a map" (src/PoseEstimator.cpp:31-47) as copy on write of the map stores.
+// Per-particle local maps (useSharedMap = false):
+// processMap's merge of a scan into every particle's map (src/EmbodiedSlamFilter.cpp:179-232)
+// and cloneMaps' independent copies (src/PoseEstimator.cpp:31-47) as copy on write of tables
+// and pages (eslam_internal.h LocalMaps).
 // ---------------------------------------------------------------------------------------
-// fresh maps: particle i names store i, every store of the pool empty
-__global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ sid, MapStore ms, uint64_t n, uint64_t pool)
+// fresh maps: particle i names table i (sid: both state buffers' names, 2 x n), every table
+// empty, every page free and unowned
+__global__ void __launch_bounds__(kBlock) k_store_init(uint32_t* __restrict__ sid, LocalMaps lm, uint64_t n, uint64_t pool,
+                                                      uint64_t items)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= pool) return;
-    if (i < n) sid[i] = (uint32_t)i;
-    ms.count[i] = 0;
-    ms.box[i] = make_uint4(kBoxEmptyLo, 0u, kBoxEmptyLo, 0u);
-    for (uint32_t t = 0; t < kStoreSlots; ++t) ms.key[i * kStoreSlots + t] = kStoreFree;
+    const uint64_t slots = pool * lm.S;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < items; i += (uint64_t)gridDim.x * kBlock) {
+        if (i < slots) lm.slot[i] = DM_LM_NONE;
+        if (i < pool) {
+            lm.ctr[i] = make_int2(DM_LM_UNSET, DM_LM_UNSET);
+            lm.tgen[i] = 0u;
+            if (i < n) {                     // both state buffers' names (n = cap here)
+                sid[i] = (uint32_t)i;
+                sid[n + i] = (uint32_t)i;
+            }
+        }
+        if (i < lm.npages) {
+            lm.frees[i] = (uint32_t)i;
+            lm.owner[i] = ~0ull;
+        }
+    }
 }
 
 __device__ __forceinline__ uint32_t* cur_sid(const SidRef& r) { return (r.ctl->base ^ r.ctl->flip) ? r.s1 : r.s0; }
 
-// ref[s]: 0, 1 or >= 2 particles name store s (received particles name none yet; the map merge
+// ref[s]: 0, 1 or >= 2 particles name table s (received particles name none yet; the map merge
 // only asks "free", "own" or "shared").  A resample hands the copies of a particle out as
 // consecutive outputs, so equal names come in runs: the first lane of a run within the wave
 // raises ref to 2 with a plain store when the run is longer than one (no atomic: as sharing
 // grows, long runs span many waves and one hot atomic per wave serialised at 0.6 ms per 8M),
-// and adds 1 atomically otherwise.  Any interleaving ends at the right class.
+// and adds 1 atomically otherwise.  Any interleaving ends at the right class.  A table found
+// shared moves to its next generation: its pages are frozen (the copies will name them too).
 __global__ void __launch_bounds__(kBlock) k_store_ref(SidRef sr, uint64_t n, uint32_t* __restrict__ ref, GatherView gv,
-                                                     uint32_t fuse)
+                                                     uint32_t fuse, uint32_t* __restrict__ tgen)
 {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t s;
     if (fuse && sr.ctl->gather) {
         // a pending resample gather that the map merge runs (MergeParams::fuse): output i will
-        // name its ancestor's store (the marks expanded as in K1, state[base] read)
+        // name its ancestor's table (the marks expanded as in K1, state[base] read)
         const uint64_t row0 = i & ~(uint64_t)(kRow - 1);          // a row past n has no row_first entry
         const uint32_t carry = row0 < n ? gv.row_first[row0 / kRow] + 1u : 0u;
         uint32_t mk = i < n ? gv.marks[i] : 0u;
         mk = wave_incl_max_u32(mk);
         const uint32_t src = (mk > carry ? mk : carry) - 1u;
         const uint32_t* sin = sr.ctl->base ? sr.s1 : sr.s0;
-        s = i < n ? sin[src] : kStoreFree;
+        s = i < n ? sin[src] : 0xffffffffu;
     } else {
         const uint32_t* sid = cur_sid(sr);
-        s = i < n ? sid[i] : kStoreFree;
+        s = i < n ? sid[i] : 0xffffffffu;
     }
     const uint32_t prev = (uint32_t)__shfl_up((int)s, 1, 64);
     const bool head = lane == 0 || prev != s;
     const uint64_t heads = __ballot(head);
     const uint64_t above = lane == 63 ? 0ull : heads >> (lane + 1);
     const uint32_t len = above ? (uint32_t)__builtin_ctzll(above) + 1u : 64u - lane;
-    if (head && !(s & kSidRecord)) {                               // kStoreFree has the record bit
+    if (head && !(s & kSidRecord)) {                               // 0xffffffff has the record bit
         if (len >= 2u) {
             if (ref[s] < 2u) ref[s] = 2u;
-        } else {
-            atomicAdd(&ref[s], 1u);
+            tgen[s] += 1u;                   // racing bumps of one table only move it further
+        } else if (atomicAdd(&ref[s], 1u) >= 1u) {
+            tgen[s] += 1u;
         }
     }
 }
 
-// compaction, mode 0: the free stores (ref 0) in store order, over the pool; mode 1: the
-// particles received from another rank (sid = kSidRecord | record), in particle order
+// compaction, mode 0: the free tables (ref 0) in table order, over the pool; mode 1: the
+// particles received from another rank (sid = kSidRecord | record), in particle order;
+// mode 2: the free pages (mark 0) in page order.  gate (device word, may be null): when 0
+// the launch does nothing (the collection runs only when a map update needs it)
 __device__ __forceinline__ bool compact_pred(int mode, uint64_t i, const uint32_t* ref, const uint32_t* sid)
 {
+    if (mode == 2) return reinterpret_cast<const uint8_t*>(ref)[i] == 0u;
     return mode == 0 ? ref[i] == 0u : (sid[i] & kSidRecord) != 0u;
 }
 
 constexpr int kCompactTile = kCompactTileItems;
 
 __global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, const uint32_t* __restrict__ ref,
-                                                          SidRef sr, uint32_t* __restrict__ counts)
+                                                          SidRef sr, uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ gate)
 {
-    const uint32_t* sid = cur_sid(sr);
+    if (gate && !*gate) return;
+    const uint32_t* sid = mode == 1 ? cur_sid(sr) : nullptr;
     __shared__ uint32_t s_w[kWaves];
     const uint64_t base = (uint64_t)blockIdx.x * kCompactTile;
     uint32_t c = 0;
@@ -1472,9 +1485,10 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(int mode, uint64_t n, 
 // offs: exclusive prefix of counts; each selected i goes to out[offs[b] + its rank in the tile]
 __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, const uint32_t* __restrict__ ref,
                                                           SidRef sr, const uint32_t* __restrict__ offs,
-                                                          uint32_t* __restrict__ out)
+                                                          uint32_t* __restrict__ out, const uint32_t* __restrict__ gate)
 {
-    const uint32_t* sid = cur_sid(sr);
+    if (gate && !*gate) return;
+    const uint32_t* sid = mode == 1 ? cur_sid(sr) : nullptr;
     __shared__ uint32_t s_w[kWaves];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t base = (uint64_t)blockIdx.x * kCompactTile;
@@ -1494,30 +1508,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, 
     }
 }
 
-// a particle received from another rank gets the j-th free store, filled from its record's
-// payload (the migrated store; pay: the received payloads), one thread per usable slot.  A
-// fixed grid strides over the *ndup_dev received particles (the count stays on the device).
-__global__ void __launch_bounds__(kBlock) k_store_copy(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                       const uint32_t* __restrict__ ndup_dev, SidRef sr,
-                                                       MapStore ms, const StorePayload* __restrict__ pay)
-{
-    const uint32_t* sid = cur_sid(sr);
-    const uint64_t total = (uint64_t)*ndup_dev * kStoreCap;
-    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t j = t / kStoreCap;
-        const uint32_t slot = (uint32_t)(t - j * kStoreCap);
-        const uint32_t to = frees[j];
-        const StorePayload& q = pay[sid[dups[j]] & ~kSidRecord];
-        ms.key[(uint64_t)to * kStoreSlots + slot] = q.key[slot];
-        ms.val[(uint64_t)to * kStoreSlots + slot] = q.val[slot];
-        if (slot == 0) {
-            ms.count[to] = q.count;
-            ms.box[to] = make_uint4(q.box[0], q.box[1], q.box[2], q.box[3]);
-        }
-    }
-}
-
-// the received particles name their stores
+// the received particles name their tables
 __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
                                                          const uint32_t* __restrict__ ndup_dev, SidRef sr)
 {
@@ -1527,227 +1518,457 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
         sid[dups[j]] = frees[j];
 }
 
-// processMap(scanMap, match = false, update = true) per particle: every scan patch, placed at
-// the particle's pose (Translation(x, y, 0) * Rz(theta); the offset patch adds zPos and
-// zSigma^2, src/EmbodiedSlamFilter.cpp:186-189, 213-214), merges into a cell of its map.  The
-// shared grid's cells stay as they are; a cell it leaves empty gets the patch (the
-// insert-into-empty-cell rule of test/testMap.cpp:307-316) or, holding one already, fuses
-// with it when within 3 sigma (the MLS variance-weighted update; envire's merge is not in the
-// reference: parity unpinned).  A full store keeps its patches (the patch is counted dropped).
-// One thread per particle.  The store's keys live in 24 VGPRs: a patch that misses a full
-// store (the steady state: the scan keeps landing on new cells) costs 24 compares, and the
-// shared grid's test is one bit of MapView::occ.  The values are staged in LDS (transposed:
-// slot-major, lane-minor) at the particle's first change and shifted / fused there; a changed
-// map is written back whole at the end -- in place when no other particle names the store
-// (ref 1), else to the particle's reserved free store frees[i], which it then names.
-constexpr int kMergeBlock = 128;                 // 24 KB of LDS: 6 blocks (12 waves) per CU
-constexpr uint32_t kMergeGroup = 8;              // patches whose cells and occupancy words load together
-static_assert(kStoreCap == 24, "k_map_merge's membership min-tree covers 24 keys");
-__global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
-                                                           MapStore ms, MergeParams mp)
+// ---- the window arithmetic (eslam_detmath.h DM_LM_*, the oracle's or_map_update) -------
+__device__ __forceinline__ uint32_t lm_div(uint32_t a, uint64_t m) { return (uint32_t)(((uint64_t)a * m) >> 40); }
+__device__ __forceinline__ uint32_t lm_mod(uint32_t a, uint32_t w, uint64_t m) { return a - w * lm_div(a, m); }
+// the tile of slot column s in the window [c - h, c + h] (= dm_lm_tile_of): lo + ((s - lo) mod w)
+// evaluated on s + (b - lo) with b a multiple of w >= 2^29, so the residue's argument is positive
+__device__ __forceinline__ int32_t lm_tile(uint32_t s, int32_t c, uint32_t h, uint32_t w, uint64_t m, uint32_t b)
 {
-    __shared__ float2 s_val[kStoreCap][kMergeBlock];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint64_t i = (uint64_t)blockIdx.x * kMergeBlock + tid;
-    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
-    // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
-    // output i reads its ancestor src in state[base] (the marks expanded as in K1) and the
-    // merge writes the whole particle, its store name included, to st = state[base ^ 1]
-    const bool gath = mp.fuse && ctl->gather;
-    const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
+    const int32_t lo = c - (int32_t)h;
+    return lo + (int32_t)lm_mod(s + (uint32_t)((int32_t)b - lo), w, m);
+}
+__device__ __forceinline__ bool lm_in(int32_t a, int32_t c, uint32_t h)
+{
+    const int32_t d = a - c;
+    return d <= (int32_t)h && -d <= (int32_t)h;
+}
+
+constexpr uint32_t kLmList = 8;                 // tiles one pass of the merge handles
+constexpr uint16_t kCodeSkip = 0xffffu;
+constexpr uint32_t kLmGroup = 8;                // patches whose cell values load together
+constexpr uint32_t kLmNoList = 0xffffffffu;
+
+// one particle as a map update sees it: its table, its pose, the window's new centre
+struct LmPart {
+    uint32_t X;                          // the table it names
+    bool shared;                         // another particle names X too
+    bool placed;                         // finite x, y, theta (else the update skips it)
+    double x, y, th, z, zs;
+    double sn, co;
+    int32_t na, nb;                      // the new centre
+};
+
+__device__ __forceinline__ void lm_centre(const MapView& map, const MergeParams& mp, const LmPart& q, int32_t& na, int32_t& nb)
+{
+    if (mp.is_id) {
+        na = dm_lm_centre(q.x, map.offset_x, map.inv_scale_x);
+        nb = dm_lm_centre(q.y, map.offset_y, map.inv_scale_y);
+    } else {
+        const double* A = map.g2l;
+        const double lx = ((A[0] * q.x + A[1] * q.y) + A[2] * q.z) + A[3];
+        const double ly = ((A[4] * q.x + A[5] * q.y) + A[6] * q.z) + A[7];
+        na = dm_lm_centre(lx, map.offset_x, map.inv_scale_x);
+        nb = dm_lm_centre(ly, map.offset_y, map.inv_scale_y);
+    }
+}
+
+// every scan patch's code for this particle: (slot << 6) | cell in the tile, or kCodeSkip
+// (off the grid, on a cell the shared grid covers, or outside the window); codes go to LDS
+// (patch-major, thread-minor).  Counts the covered and dropped patches.
+__device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
+                                         uint16_t* codes, uint32_t& covered, uint32_t& dropped)
+{
+    const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
+    for (uint32_t k = 0; k < mp.m; ++k) {
+        const ScanPatch sp = mp.sp[k];
+        uint32_t cell, cm, cn;
+        if (mp.is_id) {
+            cell = dm_merge_cell_mn(bx, by, q.co, q.sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
+                                    map.height_cells, &cm, &cn);
+        } else {
+            const double wx = (q.co * sp.x + (-q.sn) * sp.y) + q.x;
+            const double wy = (q.sn * sp.x + q.co * sp.y) + q.y;
+            const double wz = sp.z + q.z;
+            const double* A = map.g2l;
+            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+            const bool in = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
+            cm = in ? (uint32_t)fm : 0u;
+            cn = in ? (uint32_t)fn : 0u;
+            cell = in ? cn * map.width + cm : 0xffffffffu;
+        }
+        uint16_t code = kCodeSkip;
+        if (cell != 0xffffffffu) {
+            if ((map.occ[cell >> 5] >> (cell & 31u)) & 1u) {
+                ++covered;                   // the shared grid covers the cell: not merged
+            } else {
+                const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+                if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
+                    const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
+                    code = (uint16_t)((s << 6) | ((cm & 7u) + 8u * (cn & 7u)));
+                } else {
+                    ++dropped;               // beyond maxSensorRange: outside the window
+                }
+            }
+        }
+        codes[k * kLmBlock] = code;
+    }
+}
+
+// the up to kLmList smallest distinct slots above t (sorted; free entries kLmNoList)
+__device__ __forceinline__ void lm_collect(const uint16_t* codes, uint32_t m, uint32_t t, uint32_t (&L)[kLmList])
+{
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) L[r] = kLmNoList;
+    for (uint32_t k = 0; k < m; ++k) {
+        const uint16_t c = codes[k * kLmBlock];
+        if (c == kCodeSkip) continue;
+        const uint32_t s = (uint32_t)c >> 6;
+        if (t != kLmNoList && s <= t) continue;
+        bool dup = false;
+#pragma unroll
+        for (uint32_t r = 0; r < kLmList; ++r) dup |= L[r] == s;
+        if (dup) continue;
+#pragma unroll
+        for (uint32_t r = kLmList - 1; r >= 1; --r) L[r] = L[r - 1] > s ? L[r - 1] : (L[r] > s ? s : L[r]);
+        L[0] = L[0] > s ? s : L[0];
+    }
+}
+
+__device__ __forceinline__ uint32_t lm_find(const uint32_t (&L)[kLmList], uint32_t s)
+{
+    uint32_t idx = kLmNoList;
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) idx = L[r] == s ? r : idx;
+    return idx;
+}
+
+// the page slot s of table X holds for the new window: its page when the slot's tile under
+// the old centre oc is the same tile (the tile stays in the window), else none
+__device__ __forceinline__ uint32_t lm_page_of(const LocalMaps& lm, uint32_t X, int2 oc, const LmPart& q, uint32_t s)
+{
+    const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
+    const int32_t a = lm_tile(sa, q.na, lm.hx, lm.wx, lm.mx, lm.bx), b = lm_tile(sb, q.nb, lm.hy, lm.wy, lm.my, lm.by);
+    if (oc.x == DM_LM_UNSET || !lm_in(a, oc.x, lm.hx) || !lm_in(b, oc.y, lm.hy)) return DM_LM_NONE;
+    return lm.slot[(uint64_t)X * lm.S + s];
+}
+
+// the particle of a map update: output i reads its ancestor through the marks when the merge
+// runs the pending resample gather (fused), else itself
+__device__ __forceinline__ uint32_t lm_source(const MergeParams& mp, uint64_t i, bool gath)
+{
     uint32_t src = (uint32_t)i;
     if (gath) {
-        const uint64_t row0 = i & ~(uint64_t)(kRow - 1);          // a row past n has no row_first entry
+        const uint64_t row0 = i & ~(uint64_t)(kRow - 1);
         const uint32_t carry = row0 < mp.n ? mp.gv.row_first[row0 / kRow] + 1u : 0u;
         uint32_t mk = i < mp.n ? mp.gv.marks[i] : 0u;
-        const bool clr = mk != 0u;
         mk = wave_incl_max_u32(mk);
         src = (mk > carry ? mk : carry) - 1u;
-        if (i < mp.n) {
-            st.w[i] = in.w[src];
-            if (mp.aux) {
-                st.mprob[i] = in.mprob[src];
-                st.flags[i] = in.flags[src];
+    }
+    return src;
+}
+
+__device__ __forceinline__ void lm_load(const DevState& in, uint32_t src, const MapView& map, const MergeParams& mp,
+                                        const uint32_t* ref, LmPart& q)
+{
+    q.X = in.sid[src];
+    q.shared = ref[q.X] > 1u;
+    q.x = in.x[src]; q.y = in.y[src]; q.th = in.th[src]; q.z = in.z[src]; q.zs = in.zs[src];
+    dm_sincos(q.th, &q.sn, &q.co);
+    q.placed = dm_isfinite(q.x - map.offset_x) && dm_isfinite(q.y - map.offset_y) && dm_isfinite(q.th);
+    q.na = q.nb = 0;
+    if (q.placed) lm_centre(map, mp, q, q.na, q.nb);
+}
+
+// k_map_plan: the pages each particle's merge may take -- one per tile its scan patches
+// reach that its table cannot write in place (a new tile, or a page it does not own) -- and
+// the per-block sums (the allocation offsets after k_scan_excl).  The same decisions as
+// k_map_merge, without the values: a tile whose writes all turn out no-ops leaves its page
+// unused (free again at the next collection).
+__global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+                                                       LocalMaps lm, MergeParams mp)
+{
+    __shared__ uint16_t s_code[kMaxScanPatches * kLmBlock];
+    __shared__ uint32_t s_w[kLmBlock / 64];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kLmBlock + tid;
+    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    const bool gath = mp.fuse && ctl->gather;
+    const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
+    const uint32_t src = lm_source(mp, i, gath);
+    uint32_t need = 0;
+    if (i < mp.n) {
+        LmPart q;
+        lm_load(in, src, map, mp, mp.ref, q);
+        if (q.placed) {
+            uint32_t covered = 0, dropped = 0;
+            uint16_t* codes = s_code + tid;
+            lm_codes(map, lm, mp, q, codes, covered, dropped);
+            const int2 oc = lm.ctr[q.X];
+            const uint64_t gx = ((uint64_t)lm.tgen[q.X] << 32) | q.X;
+            uint32_t t = kLmNoList;
+            for (;;) {
+                uint32_t L[kLmList];
+                lm_collect(codes, mp.m, t, L);
+#pragma unroll
+                for (uint32_t r = 0; r < kLmList; ++r) {
+                    if (L[r] == kLmNoList) continue;
+                    const uint32_t P = lm_page_of(lm, q.X, oc, q, L[r]);
+                    const bool mine = !q.shared && P != DM_LM_NONE && lm.owner[P] == gx;
+                    need += mine ? 0u : 1u;
+                }
+                if (L[kLmList - 1] == kLmNoList) break;
+                t = L[kLmList - 1];
             }
-            if (mp.gv.record) mp.gv.anc[i] = (uint32_t)(mp.gbase + src);
-            if (clr) mp.gv.marks[i] = 0u;
+        }
+        mp.need[i] = (uint16_t)need;
+    }
+    const uint32_t w = wave_sum_u32(need);
+    if ((tid & 63u) == 0) s_w[tid >> 6] = w;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t b = 0;
+        for (int k = 0; k < kLmBlock / 64; ++k) b += s_w[k];
+        mp.poff[blockIdx.x] = b;
+    }
+}
+
+// after the scan of the plan's block sums: whether the free list holds this update's pages
+// (else the collection runs first)
+__global__ void k_page_budget(Ctl* __restrict__ ctl, const uint32_t* __restrict__ poff, uint32_t nblocks)
+{
+    const uint64_t total = poff[nblocks];
+    ctl->pg_total = total;
+    ctl->pg_gc = ctl->pg_cursor + total > ctl->pg_nfree ? 1u : 0u;
+}
+
+// the collection: clear the marks, mark every page a live table (ref >= 1) names, compact the
+// unmarked pages into LocalMaps::frees (k_compact_* mode 2), then k_page_budget2
+__global__ void __launch_bounds__(kBlock) k_pg_clear(uint8_t* __restrict__ mark, uint64_t npages, const uint32_t* __restrict__ gate)
+{
+    if (!*gate) return;
+    uint4* m4 = reinterpret_cast<uint4*>(mark);
+    const uint64_t n16 = (npages + 15) / 16;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * kBlock)
+        m4[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// one wave per table (grid-stride): its lanes walk the slots
+__global__ void __launch_bounds__(kBlock) k_pg_mark(LocalMaps lm, const uint32_t* __restrict__ ref, const uint32_t* __restrict__ gate)
+{
+    if (!*gate) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); t < lm.ntables; t += nw) {
+        if (ref[t] == 0u) continue;
+        const uint32_t* sl = lm.slot + t * lm.S;
+        for (uint32_t s = lane; s < lm.S; s += 64u) {
+            const uint32_t p = sl[s];
+            if (p != DM_LM_NONE) lm.mark[p] = 1u;
         }
     }
+}
+
+__global__ void k_page_budget2(Ctl* __restrict__ ctl, const uint32_t* __restrict__ counts, uint32_t tiles,
+                               uint32_t* fault)
+{
+    if (!ctl->pg_gc) return;
+    ctl->pg_nfree = counts[tiles];
+    ctl->pg_cursor = 0;
+    if (ctl->pg_total > ctl->pg_nfree) {
+        atomicOr((unsigned long long*)&ctl->err, (unsigned long long)kFaultPages);
+        if (fault) __hip_atomic_fetch_or(fault, kFaultPages, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// copy a page (512 bytes) or clear it, then give it to table gT
+__device__ __forceinline__ void lm_take_page(const LocalMaps& lm, uint32_t from, uint32_t to, uint64_t gT)
+{
+    uint4* d = reinterpret_cast<uint4*>(lm.page + (uint64_t)to * DM_LM_PAGE_CELLS);
+    if (from == DM_LM_NONE) {
+        const uint4 e = make_uint4(0u, __float_as_uint(-1.0f), 0u, __float_as_uint(-1.0f));
+#pragma unroll
+        for (uint32_t k = 0; k < 32; ++k) d[k] = e;
+    } else {
+        const uint4* s = reinterpret_cast<const uint4*>(lm.page + (uint64_t)from * DM_LM_PAGE_CELLS);
+#pragma unroll 1
+        for (uint32_t h = 0; h < 4; ++h) {
+            uint4 t[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) t[k] = s[8 * h + k];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) d[8 * h + k] = t[k];
+        }
+    }
+    lm.owner[to] = gT;
+}
+
+// processMap(scanMap, match = false, update = true) per particle (the oracle's or_map_update):
+// the window moves to the tile under the particle (tiles that leave it are forgotten), then
+// every scan patch, placed at the particle's pose (Translation(x, y, 0) * Rz(theta); the
+// offset patch adds zPos and zSigma^2, src/EmbodiedSlamFilter.cpp:186-189, 213-214), merges
+// into the cell it lands in: inserted into an empty cell (test/testMap.cpp:307-316) or fused
+// (dm_lm_fuse) with the patch there.  One thread per particle.  The table it writes is its own
+// (ref 1: in place) or, when shared, the free table frees[i] it then names (a copy of X made
+// first).  Patches go in passes of up to kLmList tiles (the smallest slots not yet done; the
+// bench's scan reaches <= 6 tiles: one pass) and in groups of kLmGroup whose cell values load
+// together; a tile's first write takes a page of the table's own (copy on write) from the
+// free list, at this particle's offset of the plan.
+__global__ void __launch_bounds__(kLmBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
+                                                        LocalMaps lm, MergeParams mp)
+{
+    __shared__ uint16_t s_code[kMaxScanPatches * kLmBlock];
+    __shared__ uint32_t s_w[kLmBlock / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint64_t i = (uint64_t)blockIdx.x * kLmBlock + tid;
+    if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
+    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
+    // output i reads its ancestor src in state[base] and the merge writes the whole particle,
+    // its table name included, to st = state[base ^ 1]
+    const bool gath = mp.fuse && ctl->gather;
+    const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
+    const uint32_t src = lm_source(mp, i, gath);
+    // this particle's first page of the plan: the block's offset plus the exclusive prefix of
+    // the needs in the block
+    const uint32_t need = i < mp.n ? (uint32_t)mp.need[i] : 0u;
+    uint32_t pfx = need;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)pfx, o, 64);
+        pfx += lane >= (uint32_t)o ? v : 0u;
+    }
+    if (lane == 63) s_w[tid >> 6] = pfx;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) wbase += s_w[w];
+    uint64_t alloc = ctl->pg_cursor + mp.poff[blockIdx.x] + wbase + (pfx - need);
+    if (gath && i < mp.n) {
+        st.w[i] = in.w[src];
+        if (mp.aux) {
+            st.mprob[i] = in.mprob[src];
+            st.flags[i] = in.flags[src];
+        }
+        if (mp.gv.record) mp.gv.anc[i] = (uint32_t)(mp.gbase + src);
+        if (mp.gv.marks[i]) mp.gv.marks[i] = 0u;
+    }
     bool dirty = false, moved = false;
-    bool grown = false;                  // a patch was inserted (the keys, count and box changed)
     uint32_t dropped = 0, covered = 0;
     if (i < mp.n) {
-        const uint32_t sid = in.sid[src];
-        uint32_t key[kStoreCap];
-        {
-            const uint4* kp = reinterpret_cast<const uint4*>(ms.key + (uint64_t)sid * kStoreSlots);
-#pragma unroll
-            for (uint32_t q = 0; q < kStoreCap / 4; ++q) {
-                const uint4 v = kp[q];
-                key[4 * q] = v.x; key[4 * q + 1] = v.y; key[4 * q + 2] = v.z; key[4 * q + 3] = v.w;
-            }
-        }
-        uint32_t count = ms.count[sid];
-        uint4 box = ms.box[sid];             // the stored cells' bounding box (MapStore::box)
-        const float2* sv = ms.val + (uint64_t)sid * kStoreSlots;
-        const double x = in.x[src], y = in.y[src], th = in.th[src], z = in.z[src], zs = in.zs[src];
+        LmPart q;
+        lm_load(in, src, map, mp, mp.ref, q);
         if (gath) {
-            st.x[i] = x; st.y[i] = y; st.th[i] = th; st.z[i] = z; st.zs[i] = zs;
+            st.x[i] = q.x; st.y[i] = q.y; st.th[i] = q.th; st.z[i] = q.z; st.zs[i] = q.zs;
         }
-        double sn, co;
-        dm_sincos(th, &sn, &co);
-        const double zvar = zs * zs;
-        const double bx = x - map.offset_x, by = y - map.offset_y;
-        const bool placed = dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(th);
-        // the first change: the values to LDS
-        auto take = [&]() {
-            if (dirty) return;
-            const uint4* from = reinterpret_cast<const uint4*>(sv);
-#pragma unroll 1
-            for (uint32_t h = 0; h < 3; ++h) {       // 4 loads at a time (VGPR pressure)
-                uint4 tmp[4];
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) tmp[q] = from[4 * h + q];
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) {
-                    const uint32_t t = 2 * (4 * h + q);
-                    s_val[t][tid] = make_float2(__uint_as_float(tmp[q].x), __uint_as_float(tmp[q].y));
-                    s_val[t + 1][tid] = make_float2(__uint_as_float(tmp[q].z), __uint_as_float(tmp[q].w));
-                }
-            }
-            dirty = true;
-        };
-        for (uint32_t k0 = 0; k0 < mp.m; k0 += kMergeGroup) {
-            uint32_t cellq[kMergeGroup], occw[kMergeGroup];
-            uint32_t inbox = 0;              // bit q: the cell lies in the store's bounding box
-#pragma unroll
-            for (uint32_t q = 0; q < kMergeGroup; ++q) {
-                cellq[q] = 0xffffffffu;
-                occw[q] = 0xffffffffu;
-                const uint32_t k = k0 + q;
-                if (k >= mp.m) continue;         // uniform
-                const ScanPatch sp = mp.sp[k];
-                uint32_t cell, cm, cn;
-                if (map.g2l_identity) {
-                    cell = dm_merge_cell_mn(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
-                                            map.height_cells, &cm, &cn);
-                    cell = placed ? cell : 0xffffffffu;
-                } else {
-                    const double wx = (co * sp.x + (-sn) * sp.y) + x;
-                    const double wy = (sn * sp.x + co * sp.y) + y;
-                    const double wz = sp.z + z;
-                    const double* A = map.g2l;
-                    const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-                    const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
-                    const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
-                    const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
-                    const bool in = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
-                    cell = in ? (uint32_t)fn * map.width + (uint32_t)fm : 0xffffffffu;
-                    cm = in ? (uint32_t)fm : 0u;
-                    cn = in ? (uint32_t)fn : 0u;
-                }
-                inbox |= (cm >= box.x && cm <= box.y && cn >= box.z && cn <= box.w) ? (1u << q) : 0u;
-                cellq[q] = cell;
-                occw[q] = map.occ[(cell == 0xffffffffu ? 0u : cell) >> 5];    // branch-free: always in range
-            }
-            uint32_t open = 0;               // bit q: patch k0 + q lands on a cell the shared grid leaves empty
-            uint32_t covd = 0;               // bit q: ... on a cell the shared grid covers (not merged)
-#pragma unroll
-            for (uint32_t q = 0; q < kMergeGroup; ++q) {
-                const bool on = cellq[q] != 0xffffffffu, occ = (occw[q] >> (cellq[q] & 31u)) & 1u;
-                open |= (on && !occ) ? (1u << q) : 0u;
-                covd |= (on && occ) ? (1u << q) : 0u;
-            }
-            covered += (uint32_t)__builtin_popcount(covd);
-            // the box bits above predate this group's inserts: after one, a later patch of the
-            // group may land on the cell just inserted, so it searches the keys regardless
-            bool grew = false;
-#pragma unroll
-            for (uint32_t q = 0; q < kMergeGroup; ++q) {
-                if (!((open >> q) & 1u)) continue;
-                const uint32_t target = cellq[q] + 1u;
-                // membership as a min-tree of key ^ target (independent VALU ops; a compare
-                // chain through the scalar mask serialises on the VALU -> SALU latency), only
-                // for cells inside the store's bounding box: a wave whose particles have all
-                // moved past their stored cells skips it
-                bool hit = false;
-                if (((inbox >> q) & 1u) || grew) {
-                    uint32_t d[kStoreCap / 3];
-#pragma unroll
-                    for (uint32_t t = 0; t < kStoreCap / 3; ++t)
-                        d[t] = min(min(key[3 * t] ^ target, key[3 * t + 1] ^ target), key[3 * t + 2] ^ target);
-                    const uint32_t d0 = min(min(d[0], d[1]), d[2]), d1 = min(min(d[3], d[4]), d[5]);
-                    hit = min(min(d0, d1), min(d[6], d[7])) == 0u;
-                }
-                if (!hit && count >= kStoreCap) { ++dropped; continue; }
-                const ScanPatch sp = mp.sp[k0 + q];
-                const double wz = sp.z + z;
-                const double var = sp.stdev * sp.stdev + zvar;
-                uint32_t pos = 0;                      // lower bound of target in the sorted keys
-#pragma unroll
-                for (uint32_t t = 0; t < kStoreCap; ++t) pos += key[t] < target ? 1u : 0u;
-                if (hit) {
-                    const float2 pv = dirty ? s_val[pos][tid] : sv[pos];
-                    const double m1 = (double)pv.x, s1 = (double)pv.y;
-                    const double v1 = s1 * s1, d = wz - m1;
-                    if (d * d <= 9.0 * (v1 + var)) {
-                        const double m = (m1 * var + wz * v1) / (v1 + var);
-                        const double v = (v1 * var) / (v1 + var);
-                        take();
-                        s_val[pos][tid] = make_float2((float)m, (float)dm_sqrt(v));
+        uint32_t name = q.X;                 // the table the particle names after the merge
+        if (q.placed) {
+            uint16_t* codes = s_code + tid;
+            lm_codes(map, lm, mp, q, codes, covered, dropped);
+            const int2 oc = lm.ctr[q.X];
+            const bool recentre = oc.x != q.na || oc.y != q.nb;
+            // the table this merge writes: X itself, or a fresh copy when others share X
+            const uint32_t T = q.shared ? mp.frees[i] : q.X;
+            const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
+            uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
+            const uint32_t* xsl = lm.slot + (uint64_t)q.X * lm.S;
+            if (q.shared || recentre) {
+                // the table under the new window: slots whose tile leaves it are cleared
+                for (uint32_t s = 0; s < lm.S; ++s) {
+                    uint32_t v = xsl[s];
+                    if (recentre && v != DM_LM_NONE) {
+                        const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
+                        const int32_t a = lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx);
+                        const int32_t b = lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by);
+                        if (!lm_in(a, q.na, lm.hx) || !lm_in(b, q.nb, lm.hy)) v = DM_LM_NONE;
                     }
-                } else {
-                    take();
-                    // insert at pos (count < kStoreCap): slots [pos, count) move up one (a loop
-                    // over LDS measured faster than three 8-slot chunks read whole, 0.86 vs 0.96 ms)
-                    for (uint32_t t = count; t > pos; --t) s_val[t][tid] = s_val[t - 1][tid];
-                    s_val[pos][tid] = make_float2((float)wz, (float)dm_sqrt(var));
-#pragma unroll
-                    for (uint32_t t = kStoreCap - 1; t >= 1; --t)
-                        key[t] = t > pos ? key[t - 1] : (t == pos ? target : key[t]);
-                    key[0] = pos == 0 ? target : key[0];
-                    ++count;
-                    const uint32_t cn = cellq[q] / map.width, cm = cellq[q] - cn * map.width;
-                    box.x = min(box.x, cm); box.y = max(box.y, cm);
-                    box.z = min(box.z, cn); box.w = max(box.w, cn);
-                    grew = true;
-                    grown = true;
+                    if (q.shared || v != xsl[s]) tsl[s] = v;
                 }
+                lm.ctr[T] = make_int2(q.na, q.nb);
             }
-        }
-        uint32_t name = sid;                 // the store the particle names after the merge
-        if (dirty) {
-            uint32_t dst = sid;
-            if (mp.ref[sid] > 1u) {              // another particle names the store: a free one
-                dst = mp.frees[i];
-                if (!gath) st.sid[i] = dst;
+            dirty = recentre;
+            const float2* pages = lm.page;
+            const double zvar = q.zs * q.zs;
+            uint32_t t = kLmNoList;
+            for (;;) {
+                uint32_t L[kLmList], P[kLmList];
+                bool own[kLmList];
+                lm_collect(codes, mp.m, t, L);
+#pragma unroll
+                for (uint32_t r = 0; r < kLmList; ++r) {
+                    P[r] = L[r] == kLmNoList ? DM_LM_NONE : tsl[L[r]];
+                    own[r] = P[r] != DM_LM_NONE && lm.owner[P[r]] == gT;
+                }
+                for (uint32_t k0 = 0; k0 < mp.m; k0 += kLmGroup) {
+                    uint32_t ci[kLmGroup], ri[kLmGroup];
+                    float2 cv[kLmGroup];
+#pragma unroll
+                    for (uint32_t g = 0; g < kLmGroup; ++g) {
+                        const uint32_t k = k0 + g;
+                        const uint16_t c = k < mp.m ? codes[k * kLmBlock] : kCodeSkip;
+                        ri[g] = c == kCodeSkip ? kLmNoList : lm_find(L, (uint32_t)c >> 6);
+                        ci[g] = (uint32_t)c & 63u;
+                        uint32_t pg = DM_LM_NONE;
+#pragma unroll
+                        for (uint32_t r = 0; r < kLmList; ++r) pg = ri[g] == r ? P[r] : pg;
+                        cv[g] = make_float2(0.0f, -1.0f);
+                        if (pg != DM_LM_NONE) cv[g] = pages[(uint64_t)pg * DM_LM_PAGE_CELLS + ci[g]];
+                    }
+#pragma unroll
+                    for (uint32_t g = 0; g < kLmGroup; ++g) {
+                        if (ri[g] == kLmNoList) continue;
+                        // an earlier patch of this group on the same cell already changed it
+#pragma unroll
+                        for (uint32_t e = 0; e < g; ++e)
+                            if (ri[e] == ri[g] && ci[e] == ci[g]) cv[g] = cv[e];
+                        const ScanPatch sp = mp.sp[k0 + g];
+                        const double wz = sp.z + q.z;
+                        const double var = sp.stdev * sp.stdev + zvar;
+                        float mo, so;
+                        if (dm_lm_holds(cv[g].y)) {
+                            if (!dm_lm_fuse(cv[g].x, cv[g].y, wz, var, &mo, &so)) { ri[g] = kLmNoList; continue; }
+                        } else {
+                            mo = (float)wz;
+                            so = (float)dm_sqrt(var);
+                        }
+                        cv[g] = make_float2(mo, so);
+                        // the tile's first write: a page of T's own
+                        uint32_t r0 = ri[g];
+                        bool mine = false;
+                        uint32_t pg = DM_LM_NONE;
+#pragma unroll
+                        for (uint32_t r = 0; r < kLmList; ++r) {
+                            mine = r0 == r ? own[r] : mine;
+                            pg = r0 == r ? P[r] : pg;
+                        }
+                        if (!mine) {
+                            const uint32_t np = lm.frees[alloc++];
+                            lm_take_page(lm, pg, np, gT);
+                            tsl[L[r0]] = np;
+#pragma unroll
+                            for (uint32_t r = 0; r < kLmList; ++r) {
+                                P[r] = r0 == r ? np : P[r];
+                                own[r] = r0 == r ? true : own[r];
+                            }
+                        }
+                        dirty = true;
+                    }
+#pragma unroll
+                    for (uint32_t g = 0; g < kLmGroup; ++g) {
+                        if (ri[g] == kLmNoList) continue;
+                        uint32_t pg = DM_LM_NONE;
+#pragma unroll
+                        for (uint32_t r = 0; r < kLmList; ++r) pg = ri[g] == r ? P[r] : pg;
+                        lm.page[(uint64_t)pg * DM_LM_PAGE_CELLS + ci[g]] = cv[g];
+                    }
+                }
+                if (L[kLmList - 1] == kLmNoList) break;
+                t = L[kLmList - 1];
+            }
+            if (q.shared && dirty) {
+                name = T;
                 moved = true;
-                name = dst;
-            }
-            // a store changed in place by fuses only keeps its keys, count and box: only the
-            // values go back (a copy on write writes the whole store)
-            if (moved || grown) {
-                uint4* kp = reinterpret_cast<uint4*>(ms.key + (uint64_t)dst * kStoreSlots);
-#pragma unroll
-                for (uint32_t q = 0; q < kStoreCap / 4; ++q)
-                    kp[q] = make_uint4(key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]);
-                ms.count[dst] = count;
-                ms.box[dst] = box;
-            }
-            uint4* vp = reinterpret_cast<uint4*>(ms.val + (uint64_t)dst * kStoreSlots);
-#pragma unroll
-            for (uint32_t q = 0; q < kStoreCap / 2; ++q) {
-                const float2 a = s_val[2 * q][tid], b = s_val[2 * q + 1][tid];
-                vp[q] = make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(b.x), __float_as_uint(b.y));
             }
         }
-        if (gath) st.sid[i] = name;
+        if (gath || moved) st.sid[i] = name;
     }
     dropped = wave_sum_u32(dropped);
     covered = wave_sum_u32(covered);
     const uint64_t dmask = __ballot(dirty), mmask = __ballot(moved);
     if (lane == 0) {                     // one address per counter slot: no single hot atomic
-        const uint32_t slot_c = (uint32_t)((blockIdx.x * (kMergeBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
+        const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
         if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
         if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
@@ -1755,7 +1976,8 @@ __global__ void __launch_bounds__(kMergeBlock) k_map_merge(DevState s0, DevState
     }
 }
 
-// the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads)
+// the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads); the free
+// list's cursor moves past this update's plan
 __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl)
 {
     __shared__ uint64_t s[kMergeCounters][kMergeCounterSlots / 64];
@@ -1774,7 +1996,14 @@ __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint6
         ctl->map_changed = r[1];
         ctl->map_copied = r[2];
         ctl->map_covered = r[3];
+        if (!(ctl->err & kFaultPages)) ctl->pg_cursor += ctl->pg_total;
     }
+}
+
+// the free list's cursor moves past a plan (the received maps' pages)
+__global__ void k_pg_advance(Ctl* __restrict__ ctl)
+{
+    if (!(ctl->err & kFaultPages)) ctl->pg_cursor += ctl->pg_total;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2846,7 +3075,7 @@ __global__ void __launch_bounds__(kBlock) k_segments_multi(DevState s0, DevState
 // [first, last] (d's run, from k_segments_multi) whose range [lo, hi) contains k
 __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const Ctl* __restrict__ ctl, PlanParams pp,
                                                  const uint2* __restrict__ range, const uint64_t* __restrict__ first_last,
-                                                 Rec* __restrict__ send, MapStore ms, StorePayload* __restrict__ pay)
+                                                 Rec* __restrict__ send)
 {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= pp.send_off[pp.nranks]) return;
@@ -2866,18 +3095,6 @@ __global__ void __launch_bounds__(kBlock) k_pack(DevState s0, DevState s1, const
     r.lohi = k | ((k + 1) << 32);
     r.src = (uint64_t)st.flags[i] | ((pp.gbase[pp.rank] + i) << 8);
     send[j] = r;
-    if (pay) {                           // per-particle maps: the source particle's store travels too
-        const uint32_t s = st.sid[i];
-        StorePayload& q = pay[j];
-        q.count = ms.count[s];
-        q.pad = 0;
-        const uint4 bx = ms.box[s];
-        q.box[0] = bx.x; q.box[1] = bx.y; q.box[2] = bx.z; q.box[3] = bx.w;
-        for (uint32_t t = 0; t < kStoreCap; ++t) {
-            q.key[t] = ms.key[(uint64_t)s * kStoreSlots + t];
-            q.val[t] = ms.val[(uint64_t)s * kStoreSlots + t];
-        }
-    }
 }
 
 // records -> marks (lower ranks: 1 + j, higher ranks: kMarkHigh + 1 + j)
@@ -3144,7 +3361,7 @@ static uint32_t k1_grid(uint64_t chunks) { return (uint32_t)((chunks + kWaves - 
 
 extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int maxp, DevState s0, DevState s1,
                                                   const MapView* map, const StepParams* p, Ctl* ctl, Shard* shards,
-                                                  const GatherView* gv, const MapStore* store, hipStream_t stream,
+                                                  const GatherView* gv, const LocalMaps* store, hipStream_t stream,
                                                   const ChunkSel* sel, double* bspill)
 {
     const uint64_t csz = 64ull * p->J;
@@ -3206,7 +3423,7 @@ extern "C" hipError_t eslam_launch_project_weight(int project, int weight, int m
 }
 
 extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, const MapView* map, const StepParams* p, Ctl* ctl,
-                                                   const DebugRec* d, const MapStore* store, hipStream_t stream)
+                                                   const DebugRec* d, const LocalMaps* store, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((p->n + kBlock - 1) / kBlock);
     if (!blocks) return hipSuccess;
@@ -3240,30 +3457,35 @@ extern "C" hipError_t eslam_launch_scan_excl(uint32_t* a, uint64_t m, hipStream_
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const MapStore* ms, uint64_t n, uint64_t pool, hipStream_t stream)
+extern "C" hipError_t eslam_launch_store_init(uint32_t* sid, const LocalMaps* lm, uint64_t n, uint64_t pool, hipStream_t stream)
 {
-    if (pool) hipLaunchKernelGGL(k_store_init, dim3((uint32_t)((pool + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, *ms, n, pool);
+    uint64_t items = pool * lm->S;
+    if (lm->npages > items) items = lm->npages;
+    const uint64_t want = (items + kBlock - 1) / kBlock;
+    if (items) hipLaunchKernelGGL(k_store_init, dim3((uint32_t)(want < 65536 ? want : 65536)), dim3(kBlock), 0, stream, sid, *lm, n,
+                                  pool, items);
     return hipGetLastError();
 }
 
 // one compaction (k_compact_count, the exclusive prefix over tiles + 1 entries -- entry tiles
-// becomes the total, copied to *total -- and k_compact_write) of the items [0, items)
+// becomes the total, copied to *total when total is not null -- and k_compact_write) of the
+// items [0, items); gate: see k_compact_count
 static hipError_t compact(int mode, uint64_t items, const uint32_t* ref, SidRef sid, uint32_t* counts, uint32_t* out,
-                          uint32_t* total, hipStream_t stream)
+                          uint32_t* total, hipStream_t stream, const uint32_t* gate = nullptr)
 {
     const uint32_t tiles = (uint32_t)((items + kCompactTile - 1) / kCompactTile);
     hipError_t e = hipMemsetAsync(counts + tiles, 0, 4, stream);
     if (e != hipSuccess) return e;
-    if (tiles) hipLaunchKernelGGL(k_compact_count, dim3(tiles), dim3(kBlock), 0, stream, mode, items, ref, sid, counts);
+    if (tiles) hipLaunchKernelGGL(k_compact_count, dim3(tiles), dim3(kBlock), 0, stream, mode, items, ref, sid, counts, gate);
     hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, stream, counts, (uint64_t)tiles + 1);
-    if (tiles) hipLaunchKernelGGL(k_compact_write, dim3(tiles), dim3(kBlock), 0, stream, mode, items, ref, sid, counts, out);
-    return hipMemcpyAsync(total, counts + tiles, 4, hipMemcpyDeviceToDevice, stream);
+    if (tiles) hipLaunchKernelGGL(k_compact_write, dim3(tiles), dim3(kBlock), 0, stream, mode, items, ref, sid, counts, out, gate);
+    return total ? hipMemcpyAsync(total, counts + tiles, 4, hipMemcpyDeviceToDevice, stream) : hipGetLastError();
 }
 
-// the stores' reference counts and the free-store list of the pool (before a map merge or a
-// copy on write): cs.ref, cs.frees, *cs.nfree
+// the tables' reference counts (and generations) and the free-table list of the pool (before a
+// map merge or a copy on write): cs.ref, cs.frees, *cs.nfree
 extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t pool, const CowScratch* cs, const GatherView* gv,
-                                              hipStream_t stream)
+                                              uint32_t* tgen, hipStream_t stream)
 {
     hipError_t e = hipMemsetAsync(cs->ref, 0, pool * 4, stream);
     if (e != hipSuccess) return e;
@@ -3271,36 +3493,230 @@ extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t p
     memset(&g, 0, sizeof(g));
     if (gv) g = *gv;
     if (n) hipLaunchKernelGGL(k_store_ref, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, sid, n, cs->ref,
-                              g, gv ? 1u : 0u);
+                              g, gv ? 1u : 0u, tgen);
     e = compact(0, pool, cs->ref, sid, cs->counts, cs->frees, cs->nfree, stream);
     return e != hipSuccess ? e : hipGetLastError();
 }
 
-// the particles a sharded resample received (cs.dups, *cs.ndup) take the first free stores,
-// filled from their records' payloads (needs eslam_launch_store_refs first)
-extern "C" hipError_t eslam_launch_store_receive(SidRef sid, const MapStore* ms, uint64_t n, const CowScratch* cs,
-                                                 const void* payloads, hipStream_t stream)
+// the page budget of a plan (mp->poff holds the block sums of mp->need over nblocks blocks):
+// the offsets, and a collection when the free list runs short (the gated kernels return at
+// once otherwise).  pgc: the collection's compaction counts (npages / kCompactTile + 1 words)
+static hipError_t page_budget(Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint32_t nblocks, uint32_t* pgc,
+                              hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, stream, mp->poff, (uint64_t)nblocks + 1);
+    hipLaunchKernelGGL(k_page_budget, dim3(1), dim3(1), 0, stream, ctl, mp->poff, nblocks);
+    const uint32_t* gate = &ctl->pg_gc;
+    const uint64_t n16 = (lm->npages + 15) / 16;
+    const uint64_t gcl = (n16 + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_pg_clear, dim3((uint32_t)(gcl < 8192 ? gcl : 8192)), dim3(kBlock), 0, stream, lm->mark, lm->npages, gate);
+    const uint64_t gm = (lm->ntables + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(k_pg_mark, dim3((uint32_t)(gm < 16384 ? gm : 16384)), dim3(kBlock), 0, stream, *lm, mp->ref, gate);
+    const SidRef none{nullptr, nullptr, nullptr};
+    hipError_t e = compact(2, lm->npages, reinterpret_cast<const uint32_t*>(lm->mark), none, pgc, lm->frees, nullptr, stream, gate);
+    if (e != hipSuccess) return e;
+    const uint32_t tiles = (uint32_t)((lm->npages + kCompactTile - 1) / kCompactTile);
+    hipLaunchKernelGGL(k_page_budget2, dim3(1), dim3(1), 0, stream, ctl, pgc, tiles, mp->fault);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                             const MergeParams* mp, uint32_t* pgc, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(mp->cnt, 0, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t nb = (uint32_t)((mp->n + kLmBlock - 1) / kLmBlock);
+    e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
+    if (e != hipSuccess) return e;
+    if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    e = page_budget(ctl, lm, mp, nb, pgc, stream);
+    if (e != hipSuccess) return e;
+    if (nb) hipLaunchKernelGGL(k_map_merge, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
+    return hipGetLastError();
+}
+
+// ---- sharded filters: the maps travel with the migrating particles -----------------------
+// k_pack's companion: each record's map header (its source's table centre and page count)
+__global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const DevState s1, const Ctl* __restrict__ ctl,
+                                                   const Rec* __restrict__ send, uint64_t nsend, uint64_t gbase, LocalMaps lm,
+                                                   MapPayHdr* __restrict__ hdr)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+    const DevState st = ctl->base ? s1 : s0;
+    for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
+        const uint64_t i = (send[j].src >> 8) - gbase;
+        const uint32_t X = st.sid[i];
+        uint32_t c = 0;
+        for (uint32_t s = lane; s < lm.S; s += 64u) c += lm.slot[(uint64_t)X * lm.S + s] != DM_LM_NONE ? 1u : 0u;
+        c = wave_sum_u32(c);
+        if (lane == 0) {
+            MapPayHdr h;
+            h.ctr = lm.ctr[X];
+            h.npg = c;
+            h.pad = 0;
+            hdr[j] = h;
+        }
+    }
+}
+
+// the records' pages in the records' order (off: exclusive prefix of the headers' npg), one
+// wave per record: its lanes copy each page's 64 cells
+__global__ void __launch_bounds__(kBlock) k_pay_pack(const DevState s0, const DevState s1, const Ctl* __restrict__ ctl,
+                                                    const Rec* __restrict__ send, uint64_t nsend, uint64_t gbase, LocalMaps lm,
+                                                    const uint32_t* __restrict__ off, MapPayPage* __restrict__ pay)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+    const DevState st = ctl->base ? s1 : s0;
+    for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
+        const uint64_t i = (send[j].src >> 8) - gbase;
+        const uint32_t X = st.sid[i];
+        uint64_t q = off[j];
+        for (uint32_t s = 0; s < lm.S; ++s) {
+            const uint32_t p = lm.slot[(uint64_t)X * lm.S + s];
+            if (p == DM_LM_NONE) continue;
+            if (lane == 0) { pay[q].slot = s; pay[q].pad = 0; }
+            pay[q].cell[lane] = lm.page[(uint64_t)p * DM_LM_PAGE_CELLS + lane];
+            ++q;
+        }
+    }
+}
+
+// exclusive prefix of the headers' page counts (one block; out: m + 1 words)
+__global__ void __launch_bounds__(1024) k_pay_prefix(const MapPayHdr* __restrict__ hdr, uint64_t m, uint32_t* __restrict__ out)
+{
+    __shared__ uint32_t s_sum[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    uint32_t t = 0;
+    for (uint64_t i = lo; i < hi; ++i) t += hdr[i].npg;
+    s_sum[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = threadIdx.x >= (uint32_t)o ? s_sum[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_sum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_sum[threadIdx.x] - t;
+    for (uint64_t i = lo; i < hi; ++i) {
+        out[i] = run;
+        run += hdr[i].npg;
+    }
+    if (threadIdx.x == 1023) out[m] = s_sum[1023];
+}
+
+// the received particles' page needs (their records' page counts), in dups order, and the
+// block sums (blocks of kLmBlock over the worst case n; past *ndup nothing)
+__global__ void __launch_bounds__(kLmBlock) k_recv_plan(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ ndup_dev,
+                                                        SidRef sr, const MapPayHdr* __restrict__ hdr, MergeParams mp)
+{
+    __shared__ uint32_t s_w[kLmBlock / 64];
+    const uint32_t* sid = cur_sid(sr);
+    const uint64_t j = (uint64_t)blockIdx.x * kLmBlock + threadIdx.x;
+    uint32_t need = 0;
+    if (j < *ndup_dev) need = hdr[sid[dups[j]] & ~kSidRecord].npg;
+    if (j < mp.n) mp.need[j] = (uint16_t)need;
+    const uint32_t w = wave_sum_u32(need);
+    if ((threadIdx.x & 63u) == 0) s_w[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t b = 0;
+        for (int k = 0; k < kLmBlock / 64; ++k) b += s_w[k];
+        mp.poff[blockIdx.x] = b;
+    }
+}
+
+// received particle j takes free table frees[j] and pages from the free list, filled from its
+// record's payload; one wave per particle: its lanes copy each page's cells, then each lane
+// writes its slots of the table
+__global__ void __launch_bounds__(kLmBlock) k_recv_maps(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
+                                                        const uint32_t* __restrict__ ndup_dev, SidRef sr, Ctl* __restrict__ ctl,
+                                                        const MapPayHdr* __restrict__ hdr, const uint32_t* __restrict__ hoff,
+                                                        const MapPayPage* __restrict__ pay, LocalMaps lm, MergeParams mp)
+{
+    __shared__ uint32_t s_need[kLmBlock];
+    if (ctl->err & kFaultPages) return;
+    const uint32_t* sid = cur_sid(sr);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint64_t ndup = *ndup_dev;
+    const uint64_t j0 = (uint64_t)blockIdx.x * kLmBlock;
+    s_need[tid] = j0 + tid < mp.n ? mp.need[j0 + tid] : 0u;
+    __syncthreads();
+    for (uint32_t k = tid >> 6; k < (uint32_t)kLmBlock; k += kLmBlock / 64) {
+        const uint64_t j = j0 + k;
+        if (j >= ndup) break;
+        uint64_t alloc = ctl->pg_cursor + mp.poff[blockIdx.x];
+        for (uint32_t e = 0; e < k; ++e) alloc += s_need[e];
+        const uint32_t rec = sid[dups[j]] & ~kSidRecord;
+        const uint32_t T = frees[j];
+        const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
+        const uint32_t npg = hdr[rec].npg;
+        const uint64_t q0 = hoff[rec];
+        for (uint32_t q = 0; q < npg; ++q) {
+            const uint32_t np = lm.frees[alloc + q];
+            lm.page[(uint64_t)np * DM_LM_PAGE_CELLS + lane] = pay[q0 + q].cell[lane];
+            if (lane == 0) lm.owner[np] = gT;
+        }
+        uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
+        for (uint32_t s = lane; s < lm.S; s += 64u) {
+            uint32_t v = DM_LM_NONE;
+            for (uint32_t q = 0; q < npg; ++q) v = pay[q0 + q].slot == s ? lm.frees[alloc + q] : v;
+            tsl[s] = v;
+        }
+        if (lane == 0) lm.ctr[T] = hdr[rec].ctr;
+    }
+}
+
+// the particles a sharded resample received (cs.dups, *cs.ndup) take the first free tables and
+// pages from the page pool, filled from their records' payloads (needs eslam_launch_store_refs
+// first): hdr / pay the received headers and pages, hoff (nrecv + 1 words) scratch
+extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint64_t n,
+                                                 const CowScratch* cs, const void* hdr, uint64_t nrecv, uint32_t* hoff,
+                                                 const void* pay, uint32_t* pgc, hipStream_t stream)
 {
     if (!n) return hipSuccess;
     hipError_t e = compact(1, n, cs->ref, sid, cs->counts + cs->tiles + 1, cs->dups, cs->ndup, stream);
     if (e != hipSuccess) return e;
-    // grids for the worst case (every particle received), capped: the loops stride
-    const uint64_t want_c = (n * kStoreCap + kBlock - 1) / kBlock, want_r = (n + kBlock - 1) / kBlock;
-    const uint32_t gc = (uint32_t)(want_c < 8192 ? want_c : 8192), gr = (uint32_t)(want_r < 2048 ? want_r : 2048);
-    hipLaunchKernelGGL(k_store_copy, dim3(gc), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid, *ms,
-                       (const StorePayload*)payloads);
+    const MapPayHdr* h = (const MapPayHdr*)hdr;
+    hipLaunchKernelGGL(k_pay_prefix, dim3(1), dim3(1024), 0, stream, h, nrecv, hoff);
+    const uint32_t nb = (uint32_t)((n + kLmBlock - 1) / kLmBlock);
+    e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_recv_plan, dim3(nb), dim3(kLmBlock), 0, stream, cs->dups, cs->ndup, sid, h, *mp);
+    e = page_budget(ctl, lm, mp, nb, pgc, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_recv_maps, dim3(nb), dim3(kLmBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid, ctl, h, hoff,
+                       (const MapPayPage*)pay, *lm, *mp);
+    hipLaunchKernelGGL(k_pg_advance, dim3(1), dim3(1), 0, stream, ctl);
+    const uint64_t want_r = (n + kBlock - 1) / kBlock;
+    const uint32_t gr = (uint32_t)(want_r < 2048 ? want_r : 2048);
     hipLaunchKernelGGL(k_store_rename, dim3(gr), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid);
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const MapStore* ms,
-                                             const MergeParams* mp, hipStream_t stream)
+// a sharded resample's map payloads (after k_pack): headers, their prefix (off: nsend + 1
+// words; the host reads the per-destination page counts from it), then the pages
+extern "C" hipError_t eslam_launch_pay_hdr(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
+                                           uint64_t gbase, const LocalMaps* lm, void* hdr, uint32_t* off, hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(mp->cnt, 0, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t), stream);
-    if (e != hipSuccess) return e;
-    if (mp->n) hipLaunchKernelGGL(k_map_merge, dim3((uint32_t)((mp->n + kMergeBlock - 1) / kMergeBlock)), dim3(kMergeBlock), 0,
-                                  stream, s0, s1, ctl, *map, *ms, *mp);
-    hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
+    if (!nsend) return hipMemsetAsync(off, 0, 4, stream);
+    const uint64_t g = (nsend + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(k_pay_hdr, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(kBlock), 0, stream, s0, s1, ctl, (const Rec*)send,
+                       nsend, gbase, *lm, (MapPayHdr*)hdr);
+    hipLaunchKernelGGL(k_pay_prefix, dim3(1), dim3(1024), 0, stream, (const MapPayHdr*)hdr, nsend, off);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_pay_pack(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
+                                            uint64_t gbase, const LocalMaps* lm, const uint32_t* off, void* pay, hipStream_t stream)
+{
+    if (!nsend) return hipSuccess;
+    const uint64_t g = (nsend + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(k_pay_pack, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(kBlock), 0, stream, s0, s1, ctl, (const Rec*)send,
+                       nsend, gbase, *lm, off, (MapPayPage*)pay);
     return hipGetLastError();
 }
 
@@ -3400,12 +3816,11 @@ extern "C" hipError_t eslam_launch_segments_multi(DevState s0, DevState s1, cons
 }
 
 extern "C" hipError_t eslam_launch_pack(DevState s0, DevState s1, Ctl* ctl, const PlanParams* pp, const uint2* range,
-                                        const uint64_t* first_last, uint64_t nsend, void* send, const MapStore* ms,
-                                        void* payloads, hipStream_t stream)
+                                        const uint64_t* first_last, uint64_t nsend, void* send, hipStream_t stream)
 {
-    if (!nsend) return hipSuccess;
-    hipLaunchKernelGGL(k_pack, dim3((uint32_t)((nsend + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, s0, s1, ctl, *pp,
-                       range, first_last, (Rec*)send, *ms, (StorePayload*)payloads);
+    const uint32_t blocks = (uint32_t)((nsend + kBlock - 1) / kBlock);
+    if (blocks)
+        hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, ctl, *pp, range, first_last, (Rec*)send);
     return hipGetLastError();
 }
 

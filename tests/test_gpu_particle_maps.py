@@ -1,10 +1,12 @@
 """Per-particle local maps on the GPU (useSharedMap = false): every
-particle's map is the shared grid plus its own patches (eslam_gpu_map_update = processMap's
-merge, src/EmbodiedSlamFilter.cpp:179-232), copied on write after a resample (cloneMaps,
-src/PoseEstimator.cpp:31-47), read by the contact update.  Bit-exact against the oracle,
-which deep-copies every map at every resample: particles after every step and every
-particle's own patches.  Parity with the reference is pinned only by the insert-into-
-empty-cell rule (test/testMap.cpp:307-316); the fuse rule is the build's own."""
+particle's map is the shared grid plus its own window of tiles reaching maxSensorRange
+(eslam_gpu_map_update = processMap's merge, src/EmbodiedSlamFilter.cpp:179-232; DESIGN.md
+5c), copied on write after a resample (cloneMaps, src/PoseEstimator.cpp:31-47), read by the
+contact update.  Bit-exact against the oracle, which copies every map at every resample:
+particles after every step and every particle's own patches.  The empty prior is the
+reference's own start with useSharedMap = false (every particle clones an empty grid
+template, src/EmbodiedSlamFilter.cpp:131-134).  Parity with the reference is pinned only by
+the insert-into-empty-cell rule (test/testMap.cpp:307-316); the fuse rule is the build's own."""
 import numpy as np
 import pytest
 
@@ -71,7 +73,7 @@ def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
                 go, oo = np.argsort(gc), np.argsort(oc)
                 assert np.array_equal(gc[go], oc[oo]), (k, i)
                 assert np.array_equal(u32(gm[go]), u32(om[oo])) and np.array_equal(u32(gs[go]), u32(os_[oo])), (k, i)
-    assert dropped > 0                   # the 48-patch scan overflows the 24-patch stores
+    assert dropped == 0                  # every scan patch lies within maxSensorRange
     if records:
         rec, cps = gpu.download_records(max_cpoints=4)
         ncp, cp, _, _ = orc.debug()
@@ -83,17 +85,23 @@ def test_particle_maps_bit_exact(gpu_mod, oracle, terrain, n, records):
     assert np.mean(p.n_contact_points == 4) > (0.5 if terrain == "flat" else 0.1)
 
 
-def test_particle_maps_steady_state(gpu_mod, oracle):
-    """The bench workload run past the stores' fill phase: 45 steps move the robot 0.9 m, so
-    the scans land beyond the cells the full stores hold (the merge's bounding-box skip and
-    K1's skipped store fetches), with the call patterns around the merge's fused resample
-    gather: a step with no map update before the next step (the step gathers), two map updates
-    in a row (the second finds no gather pending), and no download in between.  Bit-exact
-    against the oracle: every step's map-update counts, then every particle and sampled maps."""
+def prior(kind, cells):
+    base = S.rough_map(cells=cells)
+    return S.unmapped_beyond(base, 0.3 if kind == "current" else -1e9)
+
+
+@pytest.mark.parametrize("kind", ["current", "empty"])
+def test_particle_maps_steady_state(gpu_mod, oracle, kind):
+    """The bench workload run into the steady state: 45 steps move the robot 0.9 m (the window
+    moves and forgets tiles), with the call patterns around the merge's fused resample gather: a
+    step with no map update before the next step (the step gathers), two map updates in a row
+    (the second finds no gather pending), and no download in between.  Bit-exact against the
+    oracle: every step's map-update counts, then every particle and sampled maps.  In the steady
+    state no scan patch is dropped and the feet find the merged cells."""
     n = 65536
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
-    grid = S.unmapped_beyond(S.rough_map(cells=300), 0.3)
+    grid = prior(kind, 300)
     gpu = gpu_mod.GpuFilter(cfg)
     orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
     orc.set_threads(16)
@@ -111,10 +119,67 @@ def test_particle_maps_steady_state(gpu_mod, oracle):
             orc.map_update(scan)
             assert map_info(gpu.sync()) == map_info(orc.info()), k
     info = gpu.sync()
-    assert info.map_patches_dropped > 0 and info.map_stores_changed < n // 10   # the steady state
-    assert_bit_identical(gpu.download(), orc.download(), "local maps steady state")
+    assert info.map_patches_dropped == 0 and info.map_stores_changed == n
+    assert info.data_particles > 0.9 * n                     # the feet stand on merged cells
+    assert_bit_identical(gpu.download(), orc.download(), f"local maps steady state ({kind} prior)")
     assert np.array_equal(gpu.ancestors(), orc.ancestors())
     assert_maps_equal(gpu, orc, [0, 1, 977, n // 3, n // 2 + 5, n - 1], "steady state")
+
+
+def test_particle_maps_page_collection(gpu_mod, oracle):
+    """A page pool of 10 pages per particle (the steady state names about 5): the collection (mark the pages live tables name,
+    compact the rest) runs every few map updates; 60 steps stay bit-exact against the oracle,
+    which has no pool.  Then 1 page per particle: the pool cannot hold a map update, the update
+    writes nothing and the filter reports ESLAM_ERR_OUT_OF_MEMORY until it is re-initialised."""
+    n = 8192
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS
+    cfg.local_map_pages = 10
+    grid = prior("empty", 200)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    orc.set_threads(16)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    scan = S.scan_patches()
+    for k, st in enumerate(S.step_stream(60, tilt=True)):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+        assert map_info(gpu.sync()) == map_info(orc.info()), k
+    assert_bit_identical(gpu.download(), orc.download(), "page collection")
+    assert_maps_equal(gpu, orc, [0, 5, n // 2, n - 1], "page collection")
+    gpu.close()
+    cfg.local_map_pages = 1
+    g2 = gpu_mod.GpuFilter(cfg)
+    g2.set_map(grid)
+    g2.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    stream = S.step_stream(6, tilt=True)
+    with pytest.raises(gpu_mod.EslamError) as ei:
+        for st in stream:
+            g2.step(st)
+            g2.map_update(scan)
+            g2.sync()
+    assert ei.value.code == A.ERR_OUT_OF_MEMORY
+    g2.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)   # starts over
+    g2.step(stream[0])
+    g2.sync()
+
+
+def test_set_map_clears_particle_maps(gpu_mod):
+    n = 1000
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS
+    gpu = gpu_mod.GpuFilter(cfg)
+    grid = prior("empty", 100)
+    gpu.set_map(grid)
+    gpu.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.1], 0.18, 1.001)
+    gpu.step(S.step_stream(1)[0])
+    gpu.map_update(S.scan_patches())
+    assert len(gpu.particle_map(3)[0]) > 0
+    gpu.set_map(grid)
+    assert len(gpu.particle_map(3)[0]) == 0
 
 
 def test_map_update_needs_the_flag(gpu_mod):
@@ -126,15 +191,16 @@ def test_map_update_needs_the_flag(gpu_mod):
         gpu.map_update(S.scan_patches())
 
 
-def test_particle_maps_bench_workload(gpu_mod, oracle):
+@pytest.mark.parametrize("kind", ["current", "empty"])
+def test_particle_maps_bench_workload(gpu_mod, oracle, kind):
     """bench.py --local-maps' workload (configs[4]'s terrain: rough multi-patch map, unmapped
-    beyond x = 0.3 m, tilted body, one map update per step) at 256k particles on the 1000 x
-    1000 map: bit-exact against the oracle (16 threads) for 4 steps, and the maps of sampled
-    particles equal."""
+    beyond x = 0.3 m -- or the reference's empty start --, tilted body, one map update per
+    step) at 256k particles on the 1000 x 1000 map: bit-exact against the oracle (16 threads)
+    for 4 steps, and the maps of sampled particles equal."""
     n = 262144
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS
-    grid = S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
+    grid = prior(kind, 1000)
     gpu = gpu_mod.GpuFilter(cfg)
     orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
     orc.set_threads(16)
@@ -147,13 +213,15 @@ def test_particle_maps_bench_workload(gpu_mod, oracle):
         gpu.map_update(scan)
         orc.map_update(scan)
         assert map_info(gpu.sync()) == map_info(orc.info()), k
-    assert_bit_identical(gpu.download(), orc.download(), "local maps 256k")
+    assert_bit_identical(gpu.download(), orc.download(), f"local maps 256k ({kind} prior)")
     assert_maps_equal(gpu, orc, [0, 1, 4097, n // 2, n - 1], "256k")
-    assert np.mean(gpu.download().n_contact_points >= 2) > 0.1
+    if kind == "current":
+        assert np.mean(gpu.download().n_contact_points >= 2) > 0.1
 
 
-@pytest.mark.timeout(900)
-def test_particle_maps_config4_shard_size(gpu_mod, oracle):
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("kind", ["current", "empty"])
+def test_particle_maps_config4_shard_size(gpu_mod, oracle, kind):
     """configs[4] at its per-GPU size: 8M particles (64M over 8 GPUs) with per-particle
     maps on the bench workload, 3 steps, bit-exact against the oracle (16 threads): every
     particle after the last step, the map-update counts of every step, and the maps of 40
@@ -161,7 +229,7 @@ def test_particle_maps_config4_shard_size(gpu_mod, oracle):
     n = 8 * 1024 * 1024
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS
-    grid = S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
+    grid = prior(kind, 1000)
     gpu = gpu_mod.GpuFilter(cfg)
     orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
     orc.set_threads(16)
@@ -174,7 +242,7 @@ def test_particle_maps_config4_shard_size(gpu_mod, oracle):
         gpu.map_update(scan)
         orc.map_update(scan)
         assert map_info(gpu.sync()) == map_info(orc.info()), k
-    assert_bit_identical(gpu.download(), orc.download(), "local maps 8M")
+    assert_bit_identical(gpu.download(), orc.download(), f"local maps 8M ({kind} prior)")
     idx = sorted(set(np.linspace(0, n - 1, 38).astype(np.int64).tolist() + [1, n // 2 + 1]))
     assert_maps_equal(gpu, orc, idx, "8M")
     gpu.close()
