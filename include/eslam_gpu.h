@@ -167,16 +167,22 @@ typedef struct eslam_update_info {
     int32_t uniform_reset;                 /* sumWeights <= 0 branch taken                   */
     uint64_t resample_overruns;            /* draws beyond the cumulative sum (clamped, Q5)  */
     uint64_t update_count;
-    /* the last eslam_gpu_map_update (per-particle maps): scan patches a particle's map could
-     * not take because its store already held ESLAM_STORE_CAP patches (summed over the
-     * particles); maps the merge changed while another particle shared them (copy on write:
-     * written to a free store the particle then names); maps the merge changed in all; scan
+    /* the last eslam_gpu_map_update (per-particle maps): scan patches beyond a particle's
+     * window (farther than max_sensor_range; summed over the particles); maps the merge
+     * changed while another particle shared them (copy on write: written to a free table the
+     * particle then names); maps the merge changed in all (cells, or the window moved); scan
      * patches that landed on cells the shared grid covers (not merged: the per-particle map
      * holds only cells the shared grid leaves empty)                            */
     uint64_t map_patches_dropped;
     uint64_t map_stores_copied;
     uint64_t map_stores_changed;
     uint64_t map_patches_covered;
+    /* the device side of the same map update (not in the oracle: they depend on how the
+     * pages were shared): cell writes (inserts and fuses), pages taken from the pool (copies
+     * on write and new tiles), pages left in the pool's free list                           */
+    uint64_t map_cells_written;
+    uint64_t map_pages_taken;
+    uint64_t map_pages_free;
 } eslam_update_info;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */
@@ -232,14 +238,20 @@ int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_t count, co
  * EmbodiedSlamFilter::processMap(scanMap, match=false, update=true)
  * (src/EmbodiedSlamFilter.cpp:179-232) after PoseEstimator::cloneMaps (src/PoseEstimator.cpp:
  * 31-47): every particle's map is the shared grid plus its own patches in cells the grid
- * leaves empty.  A map update places the scan patches at each particle's pose
- * (Translation(x, y, 0) * Rz(theta); offset patch zPos, zSigma) and, per patch, inserts it
- * into an empty cell or fuses it (variance-weighted) with the particle's patch there when
- * within 3 sigma; cells of the shared grid are not changed, a particle holds at most 24
- * patches.  The contact update then reads each particle's own map.  Particles that a
- * resample copied share their patches until the next map update copies them (copy on
- * write).  Only the insert-into-empty-cell rule is pinned by the reference
- * (test/testMap.cpp:307-316); envire's MLSGrid::merge is not in the reference.            */
+ * leaves empty, kept in a window of tiles of 8 x 8 cells centred on the particle that reaches
+ * max_sensor_range (maxSensorRange, 3 m) in every direction.  A map update
+ * moves each particle's window to the tile under the particle (the active-grid switch of
+ * :195-207; tiles that leave the window are forgotten), places the scan patches at the
+ * particle's pose (Translation(x, y, 0) * Rz(theta); offset patch zPos, zSigma) and, per
+ * patch, inserts it into an empty cell or fuses it (variance-weighted) with the particle's
+ * patch there when within 3 sigma; cells of the shared grid are not changed, and a patch
+ * beyond the window is dropped (counted).  With an empty shared grid every particle starts
+ * from an empty map, as the reference's clones of its empty grid template
+ * (src/EmbodiedSlamFilter.cpp:131-134).  The contact update then reads each particle's own
+ * map.  Particles that a resample copied share their tables and pages until a map update
+ * writes them (copy on write).  set_map starts every particle's map over (empty).  Only the
+ * insert-into-empty-cell rule is pinned by the reference (test/testMap.cpp:307-316);
+ * envire's MLSGrid::merge is not in the reference.                                       */
 typedef struct eslam_scan_patch {
     double position[3];                    /* yaw-free body frame (the scan MLS's cells)    */
     double stdev;                          /* sensor sigma of the patch                      */
@@ -250,7 +262,8 @@ int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32
  * the particles are initialised (ESLAM_ERR_INVALID_ARG after).  On a sharded filter a
  * particle that a resample moves to another rank carries its own patches.                 */
 int eslam_gpu_set_particle_maps(eslam_ctx* ctx, int on);
-/* particle index's own patches (cell = n * width + m, mean, stdev); *count = how many it has */
+/* particle index's own patches (cell = n * width + m, mean, stdev), its window's tiles in slot
+ * order and each tile's cells row by row; *count = how many it has (up to capacity written) */
 int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32_t* cells, float* mean, float* stdev,
                                uint32_t capacity, uint32_t* count);
 

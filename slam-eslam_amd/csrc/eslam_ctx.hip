@@ -2421,6 +2421,9 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         info->map_stores_copied = c.map_copied;
         info->map_patches_covered = c.map_covered;
         info->map_stores_changed = c.map_changed;
+        info->map_cells_written = c.map_written;
+        info->map_pages_taken = c.map_taken;
+        info->map_pages_free = c.pg_nfree > c.pg_cursor ? c.pg_nfree - c.pg_cursor : 0;
     }
     if (ctx->timing && ctx->ring_steps) {
         double acc[5] = {0, 0, 0, 0, 0};

@@ -80,6 +80,8 @@ struct alignas(128) Ctl {
     uint64_t map_changed;                // stores the last map merge changed
     uint64_t map_copied;                 // shared stores the last map merge wrote to a free store
     uint64_t map_covered;                // scan patches the last map merge saw on cells the shared grid covers
+    uint64_t map_written;                // cell writes (inserts and fuses) of the last map merge
+    uint64_t map_taken;                  // pages the last map merge took from the free list
     uint64_t pg_cursor;                  // per-particle maps: next unused entry of LocalMaps::frees
     uint64_t pg_nfree;                   //   entries in LocalMaps::frees (the last collection)
     uint64_t pg_total;                   //   pages the current map update may take (its plan)
@@ -154,8 +156,10 @@ static_assert(sizeof(MapPayPage) == 520, "payload page");
 // cap are free whenever a map update starts, and particle i may take the i-th free one (copy
 // on write with a fixed, deterministic allocation of tables and no allocation counter)
 inline uint64_t store_pool(uint64_t cap) { return 2 * cap; }
-// a ceil(2^40 / w) multiplier: (a * m) >> 40 = floor(a / w) for a < 2^29, w < 2^11
-inline uint64_t lm_magic(uint32_t w) { return ((1ull << 40) + w - 1) / w; }
+// a ceil(2^35 / w) multiplier: (a * m) >> 35 = floor(a / w), exactly, for a < 2^30 and
+// 3 <= w <= 31 (a * m < 2^64; the rounding error a * (m w - 2^35) / (w 2^35) < 1 / w)
+constexpr uint32_t kLmMagicShift = 35;
+inline uint64_t lm_magic(uint32_t w) { return ((1ull << kLmMagicShift) + w - 1) / w; }
 constexpr uint32_t kDefaultMapPages = 16;       // pages per particle when the config says 0
 
 // K1 reads the first 64 bytes (the lookup header) with one scalar load per lookup
@@ -265,7 +269,7 @@ struct ScanPatch {
 constexpr int kMaxScanPatches = 64;
 constexpr int kLmBlock = 128;                   // particles per block of k_map_plan / k_map_merge
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
-constexpr uint32_t kMergeCounters = 4;
+constexpr uint32_t kMergeCounters = 6;
 
 // the store names of both state buffers; the copy-on-write kernels use the current one
 // (base ^ flip read on the device, so the host never waits for the commit)
@@ -310,7 +314,8 @@ struct MergeParams {
     uint32_t m;                          // scan patches
     uint32_t is_id;                      // the grid's global2local is the identity
     uint64_t* cnt;                       // kMergeCounters x kMergeCounterSlots: dropped patches, changed
-                                         // stores, copies, patches on covered cells (zeroed)
+                                         // tables, copies, patches on covered cells, cell writes, pages
+                                         // taken (zeroed)
     const uint32_t* ref;                 // CowScratch::ref of this update
     const uint32_t* frees;               // CowScratch::frees: particle i's table if it writes a shared map
     uint16_t* need;                      // per particle: the pages its merge may take (k_map_plan)

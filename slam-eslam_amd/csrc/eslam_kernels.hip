@@ -324,12 +324,13 @@ __device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint
 __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t m, uint32_t n, double lz, double qv, double& mean,
                                             double& stdev)
 {
-    const su8 h = kl8(KOFF(store));                  // ctr, slot, page, {S, wx}, {wy, hx}, {hy, -}, mx, my
+    const su16 h = kl16(KOFF(store));                // 64 bytes: ctr, slot, page, {S, wx}, {wy, hx}, {hy, -}, mx, my
     const uint64_t w3 = kq(h, 3), w4 = kq(h, 4);
     const uint32_t S = (uint32_t)w3, wx = (uint32_t)(w3 >> 32), wy = (uint32_t)w4, hx = (uint32_t)(w4 >> 32);
     const uint32_t hy = (uint32_t)kq(h, 5);
     const uint32_t a = m >> DM_LM_TILE_BITS, b = n >> DM_LM_TILE_BITS;
-    const uint32_t qa = (uint32_t)(((uint64_t)a * kq(h, 6)) >> 40), qb = (uint32_t)(((uint64_t)b * kq(h, 7)) >> 40);
+    const uint32_t qa = (uint32_t)(((uint64_t)a * kq(h, 6)) >> kLmMagicShift);
+    const uint32_t qb = (uint32_t)(((uint64_t)b * kq(h, 7)) >> kLmMagicShift);
     const uint32_t s = (a - wx * qa) + wx * (b - wy * qb);
     const uint64_t c = kp<const uint64_t>(h, 0)[sid];   // int2 {x, y}
     const uint32_t pg = kp<const uint32_t>(h, 1)[(uint64_t)sid * S + s];
@@ -1519,7 +1520,7 @@ __global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restr
 }
 
 // ---- the window arithmetic (eslam_detmath.h DM_LM_*, the oracle's or_map_update) -------
-__device__ __forceinline__ uint32_t lm_div(uint32_t a, uint64_t m) { return (uint32_t)(((uint64_t)a * m) >> 40); }
+__device__ __forceinline__ uint32_t lm_div(uint32_t a, uint64_t m) { return (uint32_t)(((uint64_t)a * m) >> kLmMagicShift); }
 __device__ __forceinline__ uint32_t lm_mod(uint32_t a, uint32_t w, uint64_t m) { return a - w * lm_div(a, m); }
 // the tile of slot column s in the window [c - h, c + h] (= dm_lm_tile_of): lo + ((s - lo) mod w)
 // evaluated on s + (b - lo) with b a multiple of w >= 2^29, so the residue's argument is positive
@@ -1846,7 +1847,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_merge(DevState s0, DevState s1
         if (mp.gv.marks[i]) mp.gv.marks[i] = 0u;
     }
     bool dirty = false, moved = false;
-    uint32_t dropped = 0, covered = 0;
+    uint32_t dropped = 0, covered = 0, written = 0, taken = 0;
     if (i < mp.n) {
         LmPart q;
         lm_load(in, src, map, mp, mp.ref, q);
@@ -1933,7 +1934,9 @@ __global__ void __launch_bounds__(kLmBlock) k_map_merge(DevState s0, DevState s1
                             mine = r0 == r ? own[r] : mine;
                             pg = r0 == r ? P[r] : pg;
                         }
+                        ++written;
                         if (!mine) {
+                            ++taken;
                             const uint32_t np = lm.frees[alloc++];
                             lm_take_page(lm, pg, np, gT);
                             tsl[L[r0]] = np;
@@ -1966,9 +1969,13 @@ __global__ void __launch_bounds__(kLmBlock) k_map_merge(DevState s0, DevState s1
     }
     dropped = wave_sum_u32(dropped);
     covered = wave_sum_u32(covered);
+    written = wave_sum_u32(written);
+    taken = wave_sum_u32(taken);
     const uint64_t dmask = __ballot(dirty), mmask = __ballot(moved);
     if (lane == 0) {                     // one address per counter slot: no single hot atomic
         const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
+        if (written) atomicAdd((unsigned long long*)&mp.cnt[4 * kMergeCounterSlots + slot_c], (unsigned long long)written);
+        if (taken) atomicAdd((unsigned long long*)&mp.cnt[5 * kMergeCounterSlots + slot_c], (unsigned long long)taken);
         if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
         if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
@@ -1989,13 +1996,15 @@ __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint6
     }
     __syncthreads();
     if (t == 0) {
-        uint64_t r[kMergeCounters] = {0, 0, 0, 0};
+        uint64_t r[kMergeCounters] = {0, 0, 0, 0, 0, 0};
         for (uint32_t g = 0; g < kMergeCounters; ++g)
             for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) r[g] += s[g][w];
         ctl->map_dropped = r[0];
         ctl->map_changed = r[1];
         ctl->map_copied = r[2];
         ctl->map_covered = r[3];
+        ctl->map_written = r[4];
+        ctl->map_taken = r[5];
         if (!(ctl->err & kFaultPages)) ctl->pg_cursor += ctl->pg_total;
     }
 }

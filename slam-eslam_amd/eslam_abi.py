@@ -164,6 +164,9 @@ class UpdateInfo(C.Structure):
         ("map_stores_copied", C.c_uint64),
         ("map_stores_changed", C.c_uint64),
         ("map_patches_covered", C.c_uint64),
+        ("map_cells_written", C.c_uint64),
+        ("map_pages_taken", C.c_uint64),
+        ("map_pages_free", C.c_uint64),
     ]
 
     def as_dict(self):
