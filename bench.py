@@ -30,12 +30,25 @@ BYTES_K1 = 113                # gathered read x, y, th, z, zs, w (48) + write x,
                               # + the 4-byte segment mark read and cleared (8)
 BYTES_K3 = 29                 # k_normalize_segments: read w, mprob, flags (17), write w (8), segment marks (4)
 BYTES_STEP = BYTES_K1 + BYTES_K3   # what the fused step moves per particle-update: the step roofline
-BYTES_K1_DELTA = BYTES_K1 + 4  # per-particle maps: + the store name (store lookups hit L2: the stores of
-                               # the cells under the feet, a few per particle and step)
-BYTES_MERGE_READ = 148        # k_map_merge per particle: store name 4, class 4, count 4, 24 keys 96, pose x, y,
-                              # theta, z, zsigma 40 (the values are read only by a changing particle)
-BYTES_MERGE_WRITE = 488       # per changed store: 24 values read 192, 24 keys + 24 values written back 288,
-                              # count 4, the new name 4
+BYTES_K1_DELTA = BYTES_K1 + 4  # per-particle maps: + the table name (the lookups of the cells under the
+                               # feet -- window centre, slot, page cell -- hit L2)
+# k_map_merge, per particle: pose x, y, theta, z, zsigma 40, table name read + written 8,
+# sharing class 4, plan need 2, window centre 8, table generation 4, and the fused resample gather's
+# w, mprob, flags read + written 34, x..zsigma written 40, marks 8 -> 148
+BYTES_MERGE_PARTICLE = 148
+BYTES_MERGE_CELL = 16         # per cell write (insert or fuse): the cell read and written
+BYTES_MERGE_PAGE = 1024       # per page taken: the tile's 64 cells read (copy on write) and written
+# per table copied on write: its S slots read and written (+ the centre)
+def merge_table_bytes(slots):
+    return 8 * slots + 8
+
+
+def window_slots(max_sensor_range, scale):
+    """eslam_detmath.h dm_lm_half: the per-particle map window's tiles per side, squared."""
+    import math
+    q = max_sensor_range / (8.0 * scale)
+    h = 1 if not q > 1.0 else min(15, math.ceil(q))
+    return (2 * h + 1) ** 2
 CONFIG3_GLOBAL = 16 * 1024 * 1024  # BASELINE configs[3]: 16M particles over 8 GPUs
 CONFIG4_GLOBAL = 64 * 1024 * 1024  # BASELINE configs[4]: 64M particles over 8 GPUs
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -180,6 +193,26 @@ def cpu_baseline(args, grid, flags=0, scan=None):
                       "sample": f"{n} particles x {ka} steps, the same oracle built -DOR_AOS (288-byte particle "
                                 f"records, whole-record resample copies), {da:.1f} s"}
     return out
+
+
+def gpu_clocks():
+    """The current shader and memory clock of every GPU as the driver reports them (sysfs
+    pp_dpm_sclk / pp_dpm_mclk, the line marked '*'): box-to-box clock differences show here."""
+    import glob
+    out = []
+    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+        rec = {}
+        for name in ("pp_dpm_sclk", "pp_dpm_mclk"):
+            try:
+                with open(os.path.join(dev, name)) as fh:
+                    cur = [ln.split(":", 1)[1].strip().rstrip("*").strip() for ln in fh if ln.rstrip().endswith("*")]
+                if cur:
+                    rec[name[7:]] = cur[0]
+            except OSError:
+                pass
+        if rec:
+            out.append(rec)
+    return out or None
 
 
 def visible_gpus():
@@ -390,7 +423,10 @@ def main():
     per_kernel = {"k_project_weight": (kt["project_weight_ms"], (BYTES_K1_DELTA if args.local_maps else BYTES_K1) * n),
                   "k_normalize_segments": (kt["normalize_scan_ms"], BYTES_K3 * n)}
     if args.local_maps:
-        per_kernel["k_map_merge"] = (kt["map_merge_ms"], BYTES_MERGE_READ * n + BYTES_MERGE_WRITE * info.map_stores_changed)
+        slots = window_slots(cfg.max_sensor_range, 0.1)
+        per_kernel["k_map_merge"] = (kt["map_merge_ms"], BYTES_MERGE_PARTICLE * n + BYTES_MERGE_CELL * info.map_cells_written
+                                     + BYTES_MERGE_PAGE * info.map_pages_taken
+                                     + merge_table_bytes(slots) * info.map_stores_copied)
     dom = max(per_kernel, key=lambda k: per_kernel[k][0])
     dom_ms, dom_launch_bytes = per_kernel[dom]
     dom_bytes = dom_launch_bytes / n
@@ -409,6 +445,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
+        "dtype_note": "all particle state, weights, sums and map values' arithmetic in fp64 (map cells stored as "
+                      "fp32); the project step's Box-Muller radius and angle are IEEE fp32 (DESIGN.md 2), the "
+                      "oracle computing the same fp32 operations",
+        "clocks": gpu_clocks(),
         "data": "synthetic (%s %gx%g m MLS map @0.1 m; odometry + 4 foot contacts per step%s)"
                 % ("rough multi-patch" if args.rough else "flat", args.map_cells / 10, args.map_cells / 10,
                    "; unmapped beyond x = 0.3 m, a %d-patch scan merged into every particle's map per step"
@@ -439,15 +479,19 @@ def main():
                               % (BYTES_STEP, BYTES_K1, BYTES_K3, BYTES_REFERENCE,
                                  BYTES_REFERENCE * n * world / (dt / args.steps) / 1e9 / (HBM_PEAK_GBS * world)),
         "last_update": {"effective": info.effective, "resampled": info.resampled},
-        **({"map_update": {"patches_dropped": info.map_patches_dropped, "stores_copied": info.map_stores_copied,
-                           "stores_changed": info.map_stores_changed, "patches_covered": info.map_patches_covered,
-                           "patches_total": n * len(scan),
-                           "note": "the last step's map update: scan patches full stores could not take, shared "
-                                   "stores a change copied on write, stores the merge changed and wrote back, scan "
-                                   "patches on cells the shared grid covers (not merged, DESIGN.md 5c); "
-                                   "kernel_ms.map_* time the update's phases (map_cow_ms: the stores' sharing "
-                                   "classes and the free-store list); the timed steps include the stores' fill "
-                                   "phase unless --warmup covers it (DESIGN.md 5c)"}} if args.local_maps else {}),
+        **({"map_update": {"patches_dropped": info.map_patches_dropped, "tables_copied": info.map_stores_copied,
+                           "maps_changed": info.map_stores_changed, "patches_covered": info.map_patches_covered,
+                           "cells_written": info.map_cells_written, "pages_taken": info.map_pages_taken,
+                           "pages_free": info.map_pages_free, "patches_total": n * len(scan),
+                           "data_particles": info.data_particles, "window_slots": window_slots(cfg.max_sensor_range, 0.1),
+                           "note": "the last step's map update: scan patches beyond a particle's window (farther "
+                                   "than maxSensorRange), shared tables a change copied on write, maps the merge "
+                                   "changed, scan patches on cells the shared grid covers (not merged, DESIGN.md "
+                                   "5c), cell writes, pages taken from the pool and left free; data_particles: "
+                                   "the last update's particles whose feet found patches; kernel_ms.map_* time "
+                                   "the update's phases (map_cow_ms: the tables' sharing classes and free list, "
+                                   "map_plan_ms: the page plan and any collection, map_merge_ms: the merge)"}}
+           if args.local_maps else {}),
         "build_id": eslam_amd.build_id(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -431,12 +431,15 @@ typedef struct eslam_kernel_times {
     float resample_ms;
     float total_ms;
     /* eslam_gpu_map_update (per-particle maps), averaged over the map updates of the timed
-     * region: the pending resample gather, the stores' sharing classes and the free-store
-     * list (copy on write's bookkeeping), the merge kernel, and the whole call             */
+     * region: the pending resample gather (sharded filters; one GPU fuses it into the merge),
+     * the tables' sharing classes and the free-table list (copy on write's bookkeeping), the
+     * plan (k_map_plan, the page budget and, when the free pages run short, the collection),
+     * the merge kernel with its counters, and the whole call                               */
     float map_gather_ms;
     float map_cow_ms;
     float map_merge_ms;
     float map_total_ms;
+    float map_plan_ms;
 } eslam_kernel_times;
 int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable);
 int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t);

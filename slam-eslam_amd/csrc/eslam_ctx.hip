@@ -31,8 +31,10 @@ extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t p
 extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint64_t n,
                                                  const CowScratch* cs, const void* hdr, uint64_t nrecv, uint32_t* hoff,
                                                  const void* pay, uint32_t* pgc, hipStream_t stream);
+extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                            const MergeParams* mp, uint32_t* pgc, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
-                                             const MergeParams* mp, uint32_t* pgc, hipStream_t stream);
+                                             const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pay_hdr(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
                                            uint64_t gbase, const LocalMaps* lm, void* hdr, uint32_t* off, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pay_pack(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
@@ -354,7 +356,7 @@ struct eslam_ctx {
     hipEvent_t ev[5] = {};                  // events of the step being recorded
     std::vector<hipEvent_t> ring;           // 5 events per recorded step (timing mode)
     uint32_t ring_steps = 0;
-    std::vector<hipEvent_t> mring;          // 4 events per recorded map update (timing mode)
+    std::vector<hipEvent_t> mring;          // 5 events per recorded map update (timing mode)
     uint32_t mring_steps = 0;
     eslam_kernel_times times = {};
 };
@@ -410,12 +412,12 @@ static void mrec(eslam_ctx* ctx, int k)
 {
     if (!ctx->timing) return;
     if (ctx->mring.empty()) {
-        ctx->mring.resize(4 * kRingSteps);
+        ctx->mring.resize(5 * kRingSteps);
         for (auto& e : ctx->mring) (void)hipEventCreate(&e);
     }
     if (ctx->mring_steps >= kRingSteps) return;
-    (void)hipEventRecord(ctx->mring[4 * ctx->mring_steps + k], ctx->stream);
-    if (k == 3) ctx->mring_steps++;
+    (void)hipEventRecord(ctx->mring[5 * ctx->mring_steps + k], ctx->stream);
+    if (k == 4) ctx->mring_steps++;
 }
 
 static int fail(eslam_ctx* ctx, int code, const char* msg)
@@ -1614,11 +1616,13 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     mp.m = count;
     for (uint32_t k = 0; k < count; ++k)
         mp.sp[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
-    HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->lm_pgc, ctx->stream));
+    HIPCHK(ctx, eslam_launch_map_plan(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->lm_pgc, ctx->stream));
+    mrec(ctx, 3);
+    HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
     if (fuse) {
         HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));     // the gather's buffer flip, if one ran
     }
-    mrec(ctx, 3);
+    mrec(ctx, 4);
     return ESLAM_OK;
 }
 
@@ -2443,19 +2447,20 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         ctx->ring_steps = 0;
     }
     if (ctx->timing && ctx->mring_steps) {
-        double acc[4] = {0, 0, 0, 0};
+        double acc[5] = {0, 0, 0, 0, 0};
         for (uint32_t k = 0; k < ctx->mring_steps; ++k) {
-            hipEvent_t* e = &ctx->mring[4 * k];
+            hipEvent_t* e = &ctx->mring[5 * k];
             float ms;
-            for (int j = 0; j < 3; ++j) { ms = 0; (void)hipEventElapsedTime(&ms, e[j], e[j + 1]); acc[j] += ms; }
-            ms = 0; (void)hipEventElapsedTime(&ms, e[0], e[3]); acc[3] += ms;
+            for (int j = 0; j < 4; ++j) { ms = 0; (void)hipEventElapsedTime(&ms, e[j], e[j + 1]); acc[j] += ms; }
+            ms = 0; (void)hipEventElapsedTime(&ms, e[0], e[4]); acc[4] += ms;
         }
         eslam_kernel_times& t = ctx->times;
         const double inv = 1.0 / ctx->mring_steps;
         t.map_gather_ms = (float)(acc[0] * inv);
         t.map_cow_ms = (float)(acc[1] * inv);
-        t.map_merge_ms = (float)(acc[2] * inv);
-        t.map_total_ms = (float)(acc[3] * inv);
+        t.map_plan_ms = (float)(acc[2] * inv);
+        t.map_merge_ms = (float)(acc[3] * inv);
+        t.map_total_ms = (float)(acc[4] * inv);
         ctx->mring_steps = 0;
     }
     return take_update_error(ctx);

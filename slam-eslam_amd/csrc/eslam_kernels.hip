@@ -3529,8 +3529,10 @@ static hipError_t page_budget(Ctl* ctl, const LocalMaps* lm, const MergeParams* 
     return hipGetLastError();
 }
 
-extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
-                                             const MergeParams* mp, uint32_t* pgc, hipStream_t stream)
+// a map update in two halves (timed apart): the plan (k_map_plan, the page budget and, when
+// the free list runs short, the collection), then the merge and its counters
+extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                            const MergeParams* mp, uint32_t* pgc, hipStream_t stream)
 {
     hipError_t e = hipMemsetAsync(mp->cnt, 0, kMergeCounters * kMergeCounterSlots * sizeof(uint64_t), stream);
     if (e != hipSuccess) return e;
@@ -3538,8 +3540,13 @@ extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl,
     e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
     if (e != hipSuccess) return e;
     if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
-    e = page_budget(ctl, lm, mp, nb, pgc, stream);
-    if (e != hipSuccess) return e;
+    return page_budget(ctl, lm, mp, nb, pgc, stream);
+}
+
+extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                             const MergeParams* mp, hipStream_t stream)
+{
+    const uint32_t nb = (uint32_t)((mp->n + kLmBlock - 1) / kLmBlock);
     if (nb) hipLaunchKernelGGL(k_map_merge, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
     return hipGetLastError();

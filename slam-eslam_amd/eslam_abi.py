@@ -199,6 +199,7 @@ class KernelTimes(C.Structure):
         ("map_cow_ms", C.c_float),
         ("map_merge_ms", C.c_float),
         ("map_total_ms", C.c_float),
+        ("map_plan_ms", C.c_float),
     ]
 
 

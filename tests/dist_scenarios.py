@@ -29,6 +29,11 @@ def scenario_config(name, n_global):
         S.bench_config(cfg, n_global)
         if name in ("maps", "config4"):          # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
+        if name == "config4":
+            # 8 ranks x 8M and then one 64M context share one GPU's 288 GB: a 5 x 5-tile window
+            # (1.5 m; the scan reaches 1.2 m) and 6 pages per particle (3 steps take ~5)
+            cfg.max_sensor_range = 1.5
+            cfg.local_map_pages = 6
     else:
         cfg.particle_count = n_global
         cfg.min_effective = (n_global * 9) // 10

@@ -52,6 +52,10 @@ def main():
             f = eslam_dist.ShardedGpuFilter(cfg, n_global, comm, device=dev)
         if name in ("config3", "config4"):
             from dist_scenarios import digest, run_config3
+            # the ranks share one GPU: a rank's waits between its own blocks may outlast another
+            # rank's long kernels (the 8M-particle map pools' initialisation), so they get
+            # seconds instead of the default ~60 ms before the filter is declared faulted
+            f.debug_set_spin_limit(1 << 24)
             rec, fields, anc, best, rng = run_config3(f, n_global, lo, hi, info_fn=lambda g: g.sync(), name=name)
             for fld, v in fields.items():
                 rec[f"sha/{fld}"] = np.array(digest(v))

