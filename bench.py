@@ -64,6 +64,8 @@ def parse():
                          "keeps the one-GPU line's per-GPU work; configs[3]'s 16M over 8 GPUs is 2097152)")
     ap.add_argument("--map-cells", type=int, default=1000)
     ap.add_argument("--rough", action="store_true", help="rough multi-patch terrain (config 5 map)")
+    ap.add_argument("--map-pages", type=int, default=0,
+                    help="per-particle maps: page pool per particle (eslam_config.local_map_pages; 0: the default)")
     ap.add_argument("--local-maps", action="store_true",
                     help="configs[4]'s per-particle local maps (useSharedMap = false): rough terrain, unmapped "
                          "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles per "
@@ -346,6 +348,7 @@ def main():
     cfg = S.bench_config(A.default_config(), n * world)
     if args.local_maps:
         cfg.flags |= A.FLAG_PARTICLE_MAPS
+        cfg.local_map_pages = args.map_pages
     if sharded:
         # one global filter of n * world particles, sharded over the ranks: RCCL all_gathers
         # of the statistics / totals / counts and an all_to_all_v of the migrating particles

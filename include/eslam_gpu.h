@@ -95,8 +95,8 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_PARTICLE_MAPS 0x10u     /* useSharedMap = false: every particle its own local
                                               map (eslam_gpu_map_update)                      */
 #define ESLAM_FLAG_RECORD_CONTACTS 0x8u    /* keep every update's cpoints, meas_pos, meas_theta
-                                              (also on with log_debug); one GPU only: the
-                                              set_comm calls return ESLAM_ERR_UNSUPPORTED    */
+                                              (also on with log_debug); on a sharded filter
+                                              download_records is then a collective          */
 
 void eslam_config_default(eslam_config* cfg);
 
@@ -293,7 +293,11 @@ typedef struct eslam_particle_record {
  * particles).  With ESLAM_FLAG_RECORD_CONTACTS (or log_debug) the meas_* fields and up to
  * max_cpoints contact points per particle (cpoints: count x max_cpoints, may be NULL) are
  * those of the last update, carried through its resample like the reference's vectors;
- * otherwise meas_* are 0 and n_cpoints = the count of the last update.                    */
+ * otherwise meas_* are 0 and n_cpoints = the count of the last update.
+ * Sharded with ESLAM_FLAG_RECORD_CONTACTS / log_debug: a collective (every rank calls it, in
+ * the same order, count may be 0): a particle whose ancestor at the last update sat on another
+ * rank gets that ancestor's records from it (two all_to_all_v); a rank whose own call fails
+ * still takes part and makes every rank return an error.                                    */
 int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64_t stride, uint64_t count,
                                eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints);
 int eslam_gpu_particle_count(const eslam_ctx* ctx, uint64_t* n);

@@ -17,6 +17,7 @@
 
 #include <string>
 #include <chrono>
+#include <algorithm>
 #include <vector>
 
 #include "eslam_internal.h"
@@ -42,7 +43,9 @@ extern "C" hipError_t eslam_launch_pay_pack(DevState s0, DevState s1, const Ctl*
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
                                                 eslam_particle_record* out, eslam_cpoint* cps, uint32_t max_cp,
-                                                hipStream_t stream);
+                                                const uint64_t* slot, const double* remote, hipStream_t stream);
+extern "C" hipError_t eslam_launch_gather_records(const uint32_t* req, uint64_t nreq, uint64_t gbase, const DebugRec* d,
+                                                  double* items, hipStream_t stream);
 extern "C" hipError_t eslam_launch_centroid_chunks(DevState s0, DevState s1, uint64_t n, uint32_t J, Ctl* ctl,
                                                    double* chunk_out, hipStream_t stream);
 extern "C" hipError_t eslam_launch_centroid_tree(double* a, double* b, uint64_t m, double* out, hipStream_t stream);
@@ -264,7 +267,8 @@ struct eslam_ctx {
     bool lm_ready = false;                   // lm sized for the current map and particle count
     uint32_t* sid_mem = nullptr;             // 2 x cap: DevState::sid of both state buffers
     uint32_t* cow = nullptr;                 // owner, counts, free and sharing lists + the copy count
-    uint16_t* lm_need = nullptr;             // per particle: pages its merge may take (MergeParams::need)
+    uint32_t* lm_off = nullptr;              // per particle: its first page in its plan block (MergeParams::off)
+    uint32_t* lm_srcv = nullptr;             // per particle: the particle its merge reads (MergeParams::srcv)
     uint32_t* lm_poff = nullptr;             // per merge block: page offsets (+ total)
     uint32_t* lm_pgc = nullptr;              // the page collection's compaction counts
     uint64_t* merge_cnt = nullptr;           // the map merge's statistics slots (2 x kMergeCounterSlots) and
@@ -610,9 +614,9 @@ static void free_local_maps(eslam_ctx* ctx)
 {
     (void)hipFree(ctx->lm.ctr); (void)hipFree(ctx->lm.slot); (void)hipFree(ctx->lm.page); (void)hipFree(ctx->lm.tgen);
     (void)hipFree(ctx->lm.owner); (void)hipFree(ctx->lm.frees); (void)hipFree(ctx->lm.mark);
-    (void)hipFree(ctx->lm_need); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc);
+    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_srcv); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc);
     ctx->lm = LocalMaps{};
-    ctx->lm_need = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr;
+    ctx->lm_off = nullptr; ctx->lm_srcv = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr;
     ctx->lm_ready = false;
 }
 
@@ -786,7 +790,8 @@ static int local_maps_reset(eslam_ctx* ctx)
     HIPCHK(ctx, hipMalloc(&lm.owner, lm.npages * 8));
     HIPCHK(ctx, hipMalloc(&lm.frees, lm.npages * 4));
     HIPCHK(ctx, hipMalloc(&lm.mark, ((lm.npages + 15) / 16) * 16));
-    HIPCHK(ctx, hipMalloc(&ctx->lm_need, cap * 2));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_off, cap * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_srcv, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->lm_poff, ((cap + kLmBlock - 1) / kLmBlock + 1) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->lm_pgc, (ptiles + 1) * 4));
     HIPCHK(ctx, eslam_launch_store_init(ctx->sid_mem, &lm, cap, pool, ctx->stream));
@@ -910,13 +915,6 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
         ctx->n_global = 0;
         return ESLAM_OK;
     }
-    // logDebug's per-particle contact records (cpoints, meas_pos) are indexed by the particle's
-    // position during the update and read through the resample's ancestors; on a sharded
-    // filter an ancestor may sit on another rank, so the records would have to travel with the
-    // migrating particles, which this build does not do: refused here rather than left empty
-    if (record_contacts(ctx))
-        return fail(ctx, ESLAM_ERR_UNSUPPORTED,
-                    "logDebug / ESLAM_FLAG_RECORD_CONTACTS is not supported on a sharded filter (one GPU only)");
     if (!shard_gbase || !comm->allgather || !comm->alltoallv || comm->nranks < 1 || comm->nranks > kMaxRanks ||
         comm->rank < 0 || comm->rank >= comm->nranks)
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: bad communicator (1 <= nranks <= 16)");
@@ -1054,9 +1052,6 @@ extern "C" int eslam_gpu_set_comm_rccl(eslam_ctx* ctx, int32_t nranks, int32_t r
 {
     if (!ctx || !id) return ESLAM_ERR_INVALID_ARG;
     if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
-    if (record_contacts(ctx))             // see eslam_gpu_set_comm
-        return fail(ctx, ESLAM_ERR_UNSUPPORTED,
-                    "logDebug / ESLAM_FLAG_RECORD_CONTACTS is not supported on a sharded filter (one GPU only)");
     const RcclApi& a = rccl_api();
     if (!a.ok) return fail(ctx, ESLAM_ERR_UNSUPPORTED, "eslam_gpu_set_comm_rccl: librccl.so.1 not found");
     if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
@@ -1525,36 +1520,155 @@ extern "C" int eslam_gpu_write_particles(eslam_ctx* ctx, uint64_t first, uint64_
     return write_ctl(ctx);
 }
 
+constexpr uint64_t kRecRemote = 1ull << 63;     // k_pack_records: a slot naming a fetched item
+
+// logDebug records on a sharded filter: particle i's records are those of its ancestor at the
+// last update's resample, which may have sat on another rank.  Those are fetched from their
+// ranks: the request counts all_gathered, then two all_to_all_v (the global indices asked for,
+// the items: meas 4, ncp, maxc x 6 contact-point doubles).  slot[k]: the record's position on
+// this rank, or kRecRemote | its item in *d_remote.  Every rank takes part; one whose own part
+// failed (rc) sends counts that make every rank fail, so no rank is left waiting.
+static int fetch_remote_records(eslam_ctx* ctx, int rc, uint64_t first, uint64_t stride, uint64_t count,
+                                std::vector<uint64_t>& slot, double** d_remote)
+{
+    const int G = ctx->comm.nranks, me = ctx->comm.rank;
+    const uint64_t gb = ctx->gbase, item = 8ull * (5 + 6ull * (ctx->dbg.maxc ? ctx->dbg.maxc : 1));
+    std::vector<std::vector<uint32_t>> req(G);
+    std::vector<uint32_t> owner_of;             // per remote slot: its owner
+    auto resolve = [&]() -> int {
+        if (!ctx->dbg_valid || !count) return ESLAM_OK;
+        uint32_t resampled = 0;
+        HIPCHK(ctx, hipMemcpy(&resampled, ctx->dbg.resampled, 4, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> anc;
+        if (resampled) {
+            anc.resize(ctx->n);
+            HIPCHK(ctx, hipMemcpy(anc.data(), ctx->anc, ctx->n * 4, hipMemcpyDeviceToHost));
+        }
+        slot.resize(count);
+        for (uint64_t k = 0; k < count; ++k) {
+            const uint64_t i = first + k * stride, g = resampled ? anc[i] : gb + i;
+            if (g >= gb && g < gb + ctx->n) {
+                slot[k] = g - gb;
+                continue;
+            }
+            const int o = (int)(std::upper_bound(ctx->gall.begin(), ctx->gall.end(), g) - ctx->gall.begin()) - 1;
+            if (o < 0 || o >= G || o == me) return fail(ctx, ESLAM_ERR_HIP, "download_records: ancestor outside the filter");
+            slot[k] = kRecRemote | req[o].size();
+            owner_of.push_back((uint32_t)o);
+            req[o].push_back((uint32_t)g);
+        }
+        return ESLAM_OK;
+    };
+    if (!rc) rc = resolve();
+    // the request counts: row r of the gathered matrix is what rank r asks of each rank
+    uint64_t* h = ctx->mg_host;
+    for (int d = 0; d < G; ++d) h[mg::kCounts + d] = rc ? ~0ull : (uint64_t)req[d].size();
+    HIPCHK(ctx, hipMemcpy(ctx->mg + mg::kCounts, &h[mg::kCounts], 8ull * G, hipMemcpyHostToDevice));
+    const int crc = comm_allgather(ctx, ctx->mg + mg::kCounts, ctx->mg + mg::kCountsAll, 8ull * G);
+    if (crc) return rc ? rc : crc;
+    HIPCHK(ctx, hipMemcpy(&h[mg::kCountsAll], ctx->mg + mg::kCountsAll, 8ull * G * G, hipMemcpyDeviceToHost));
+    bool peer_failed = false;
+    uint64_t nin[kMaxRanks], tin = 0, tout = 0, off[kMaxRanks + 1];
+    for (int r = 0; r < G; ++r) {
+        for (int d = 0; d < G; ++d) peer_failed |= h[mg::kCountsAll + r * G + d] == ~0ull;
+        nin[r] = h[mg::kCountsAll + r * G + me];
+    }
+    if (rc) return rc;
+    if (peer_failed) return fail(ctx, ESLAM_ERR_COMM, "download_records failed on another rank");
+    off[0] = 0;
+    for (int r = 0; r < G; ++r) {
+        tin += nin[r];
+        off[r + 1] = off[r] + req[r].size();
+    }
+    tout = off[G];
+    // the requests out, this rank's items for the others back
+    std::vector<uint32_t> hreq;
+    hreq.reserve(tout);
+    for (int d = 0; d < G; ++d) hreq.insert(hreq.end(), req[d].begin(), req[d].end());
+    uint32_t *d_out = nullptr, *d_in = nullptr;
+    double* d_items = nullptr;
+    int out = ESLAM_OK;
+    auto exchange = [&]() -> int {
+        HIPCHK(ctx, hipMalloc(&d_out, (tout + 1) * 4));
+        HIPCHK(ctx, hipMalloc(&d_in, (tin + 1) * 4));
+        HIPCHK(ctx, hipMalloc(&d_items, (tin + 1) * item));
+        HIPCHK(ctx, hipMalloc(d_remote, (tout + 1) * item));
+        if (tout) HIPCHK(ctx, hipMemcpy(d_out, hreq.data(), tout * 4, hipMemcpyHostToDevice));
+        uint64_t sb[kMaxRanks], rb[kMaxRanks];
+        for (int r = 0; r < G; ++r) { sb[r] = 4 * req[r].size(); rb[r] = 4 * nin[r]; }
+        int e = comm_alltoallv(ctx, d_out, sb, d_in, rb);
+        if (e) return e;
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (tin && ctx->dbg_valid) HIPCHK(ctx, eslam_launch_gather_records(d_in, tin, gb, &ctx->dbg, d_items, ctx->stream));
+        else if (tin) HIPCHK(ctx, hipMemsetAsync(d_items, 0, tin * item, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        for (int r = 0; r < G; ++r) { sb[r] = item * nin[r]; rb[r] = item * req[r].size(); }
+        e = comm_alltoallv(ctx, d_items, sb, *d_remote, rb);
+        if (e) return e;
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        return ESLAM_OK;
+    };
+    out = exchange();
+    (void)hipFree(d_out); (void)hipFree(d_in); (void)hipFree(d_items);
+    if (out) return out;
+    // the fetched items in rank order: rank o's start off[o]
+    uint64_t r = 0;
+    for (uint64_t k = 0; k < slot.size(); ++k)
+        if (slot[k] & kRecRemote) slot[k] = kRecRemote | (off[owner_of[r++]] + (slot[k] & ~kRecRemote));
+    return ESLAM_OK;
+}
+
 extern "C" int eslam_gpu_download_records(eslam_ctx* ctx, uint64_t first, uint64_t stride, uint64_t count,
                                           eslam_particle_record* out, eslam_cpoint* cpoints, uint32_t max_cpoints)
 {
-    if (!ctx || (!out && count)) return ESLAM_ERR_INVALID_ARG;
-    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
-    if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
-    if (!count) return ESLAM_OK;
+    if (!ctx) return ESLAM_ERR_INVALID_ARG;
+    // sharded with logDebug records: a collective (every rank calls it; count may be 0)
+    const bool coll = ctx->sharded && record_contacts(ctx);
     if (!stride) stride = 1;
-    if (first >= ctx->n || (count - 1) > (ctx->n - 1 - first) / stride)
-        return fail(ctx, ESLAM_ERR_INVALID_ARG, "download_records: range beyond the particles");
+    int rc = (!out && count) ? fail(ctx, ESLAM_ERR_INVALID_ARG, "download_records: no output") : ESLAM_OK;
+    if (!rc && count && (first >= ctx->n || (count - 1) > (ctx->n - 1 - first) / stride))
+        rc = fail(ctx, ESLAM_ERR_INVALID_ARG, "download_records: range beyond the particles");
+    if (!rc || coll) {
+        const int s = settle(ctx);                // a deferred sharded exchange first
+        if (!rc) rc = s;
+    }
+    if (!rc && check_poisoned(ctx)) rc = ESLAM_ERR_HIP;
+    if (!rc) rc = materialize(ctx);               // the pending gather writes the ancestors too
+    std::vector<uint64_t> slot;
+    double* d_remote = nullptr;
+    if (coll) {
+        const int frc = fetch_remote_records(ctx, rc, first, stride, count, slot, &d_remote);
+        if (!rc) rc = frc;
+    }
+    if (rc || !count) {
+        (void)hipFree(d_remote);
+        return rc;
+    }
     if (!cpoints) max_cpoints = 0;
-    int rc = materialize(ctx);                // the pending gather writes the ancestors too
-    if (rc) return rc;
     const DebugRec none = {};
     const DebugRec& d = ctx->dbg_valid ? ctx->dbg : none;
     eslam_particle_record* d_out = nullptr;
     eslam_cpoint* d_cp = nullptr;
-    HIPCHK(ctx, hipMalloc(&d_out, count * sizeof(eslam_particle_record)));
-    if (max_cpoints) {
-        hipError_t e = hipMalloc(&d_cp, count * max_cpoints * sizeof(eslam_cpoint));
+    uint64_t* d_slot = nullptr;
+    hipError_t e = hipMalloc(&d_out, count * sizeof(eslam_particle_record));
+    if (e == hipSuccess && max_cpoints) {
+        e = hipMalloc(&d_cp, count * max_cpoints * sizeof(eslam_cpoint));
         if (e == hipSuccess) e = hipMemsetAsync(d_cp, 0, count * max_cpoints * sizeof(eslam_cpoint), ctx->stream);
-        if (e != hipSuccess) { (void)hipFree(d_out); (void)hipFree(d_cp); return fail(ctx, ESLAM_ERR_HIP, hipGetErrorString(e)); }
     }
-    hipError_t e = eslam_launch_pack_records(ctx->st[0], ctx->st[1], ctx->ctl, first, stride, count, ctx->gbase, ctx->anc, &d,
-                                             d_out, d_cp, max_cpoints, ctx->stream);
+    if (e == hipSuccess && !slot.empty()) {
+        e = hipMalloc(&d_slot, count * 8);
+        if (e == hipSuccess) e = hipMemcpy(d_slot, slot.data(), count * 8, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess)
+        e = eslam_launch_pack_records(ctx->st[0], ctx->st[1], ctx->ctl, first, stride, count, ctx->gbase, ctx->anc, &d, d_out,
+                                      d_cp, max_cpoints, d_slot, d_remote, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess) e = hipMemcpy(out, d_out, count * sizeof(eslam_particle_record), hipMemcpyDeviceToHost);
     if (e == hipSuccess && max_cpoints) e = hipMemcpy(cpoints, d_cp, count * max_cpoints * sizeof(eslam_cpoint), hipMemcpyDeviceToHost);
     (void)hipFree(d_out);
     (void)hipFree(d_cp);
+    (void)hipFree(d_slot);
+    (void)hipFree(d_remote);
     if (e != hipSuccess) return fail(ctx, ESLAM_ERR_HIP, (std::string("download_records: ") + hipGetErrorString(e)).c_str());
     return ESLAM_OK;
 }
@@ -1570,7 +1684,8 @@ static MergeParams merge_params(eslam_ctx* ctx, const CowScratch& cs)
     mp.cnt = ctx->merge_cnt;
     mp.ref = cs.ref;
     mp.frees = cs.frees;
-    mp.need = ctx->lm_need;
+    mp.off = ctx->lm_off;
+    mp.srcv = ctx->lm_srcv;
     mp.poff = ctx->lm_poff;
     mp.fault = ctx->fault_host;
     mp.n = ctx->n;
@@ -2249,7 +2364,7 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
         respawn = (ctx->hash_event++ % period) == 0;
     }
     // logDebug records: the update's contact points are recorded on the projected state
-    const bool records = weight && record_contacts(ctx);   // one GPU only (eslam_gpu_set_comm refuses it)
+    const bool records = weight && record_contacts(ctx);
     // a deferred sharded exchange: the weighting launch is split around it (own-output chunks,
     // the exchange, the other chunks) unless the step takes another path first
     const bool split = ctx->xpend && !respawn && !records && !particle_maps(ctx);

@@ -267,7 +267,7 @@ struct ScanPatch {
     double x, y, z, stdev;
 };
 constexpr int kMaxScanPatches = 64;
-constexpr int kLmBlock = 128;                   // particles per block of k_map_plan / k_map_merge
+constexpr int kLmBlock = 128;                   // particles per block of the page plan (k_map_plan, k_recv_plan)
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
 constexpr uint32_t kMergeCounters = 6;
 
@@ -318,7 +318,10 @@ struct MergeParams {
                                          // taken (zeroed)
     const uint32_t* ref;                 // CowScratch::ref of this update
     const uint32_t* frees;               // CowScratch::frees: particle i's table if it writes a shared map
-    uint16_t* need;                      // per particle: the pages its merge may take (k_map_plan)
+    uint32_t* off;                       // per particle: its first page of the plan within its plan block
+                                         // (k_map_plan / k_recv_plan: the exclusive prefix of the needs)
+    uint32_t* srcv;                      // per particle: the particle the merge reads (its ancestor
+                                         // when the merge runs a pending resample gather; k_map_plan)
     uint32_t* poff;                      // per block of kLmBlock particles: first page offset (+ total)
     uint32_t* fault;                     // host-mapped fault word (kFaultPages)
     GatherView gv;                       // fuse: a pending resample gather runs in the merge (one GPU)

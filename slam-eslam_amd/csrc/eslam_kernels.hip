@@ -179,8 +179,12 @@ __device__ __forceinline__ uint64_t stamp_now()
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+__device__ uint32_t g_stamps_grid[2];    // gridDim.x of the last stamped K1 / K3 launch
 #define ESLAM_STAMP(arr, k) \
-    do { if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) arr[blockIdx.x][(k)] = stamp_now(); } while (0)
+    do { \
+        if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) arr[blockIdx.x][(k)] = stamp_now(); \
+        if ((k) == 0 && threadIdx.x == 0 && blockIdx.x == 0) g_stamps_grid[&arr == &g_stamps_k1 ? 0 : 1] = gridDim.x; \
+    } while (0)
 #else
 #define ESLAM_STAMP(arr, k) do { } while (0)
 #endif
@@ -1312,11 +1316,17 @@ __global__ void __launch_bounds__(kBlock) k_contact_records(K1Args a, DebugRec d
 // eslam_gpu_download_records: particles first + k * stride as PoseParticle records with their
 // debug fields.  Particle i's records are those of the particle it descends from at the last
 // update's resample (anc, global indices) -- the reference copies cpoints with the particle.
+// On a sharded filter the host resolves the descent first (slot[k]: the record's position on
+// this rank, or kRecRemote | its item in `remote`, fetched from the rank that held it).
+constexpr uint64_t kRecRemote = 1ull << 63;
+__device__ __forceinline__ uint32_t rec_items(uint32_t maxc) { return 5u + 6u * maxc; }    // doubles per item
+
 __global__ void __launch_bounds__(kBlock) k_pack_records(DevState s0, DevState s1, const Ctl* __restrict__ ctl, uint64_t first,
                                                          uint64_t stride, uint64_t count, uint64_t gbase,
                                                          const uint32_t* __restrict__ anc, DebugRec d,
                                                          eslam_particle_record* __restrict__ out,
-                                                         eslam_cpoint* __restrict__ cps, uint32_t max_cp)
+                                                         eslam_cpoint* __restrict__ cps, uint32_t max_cp,
+                                                         const uint64_t* __restrict__ slot, const double* __restrict__ remote)
 {
     const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
@@ -1335,13 +1345,23 @@ __global__ void __launch_bounds__(kBlock) k_pack_records(DevState s0, DevState s
     r.index = i + gbase;
     uint32_t n = 0;
     if (d.ncp) {
-        const uint64_t src = *d.resampled ? (uint64_t)anc[i] - gbase : i;
-        for (int q = 0; q < 3; ++q) r.meas_pos[q] = d.meas[4 * src + q];
-        r.meas_theta = d.meas[4 * src + 3];
-        n = d.ncp[src];
+        const uint64_t s = slot ? slot[k] : (*d.resampled ? (uint64_t)anc[i] - gbase : i);
+        const double *meas, *cp;
+        if (s & kRecRemote) {                 // an item fetched from another rank
+            const double* item = remote + (uint64_t)rec_items(d.maxc) * (s & ~kRecRemote);
+            meas = item;
+            n = (uint32_t)item[4];
+            cp = item + 5;
+        } else {
+            meas = d.meas + 4 * s;
+            n = d.ncp[s];
+            cp = d.cp + (uint64_t)6 * d.maxc * s;
+        }
+        for (int q = 0; q < 3; ++q) r.meas_pos[q] = meas[q];
+        r.meas_theta = meas[3];
         const uint32_t kept = n < d.maxc ? n : d.maxc;
         for (uint32_t q = 0; q < kept && q < max_cp; ++q) {
-            const double* c = d.cp + (uint64_t)6 * (d.maxc * src + q);
+            const double* c = cp + 6 * q;
             eslam_cpoint& o = cps[(uint64_t)max_cp * k + q];
             o.point[0] = c[0]; o.point[1] = c[1]; o.point[2] = c[2];
             o.zdiff = c[3]; o.zvar = c[4]; o.prob = c[5];
@@ -1353,6 +1373,21 @@ __global__ void __launch_bounds__(kBlock) k_pack_records(DevState s0, DevState s
     }
     r.n_cpoints = n;
     out[k] = r;
+}
+
+// the records other ranks asked for (sharded download_records): item j = the debug fields
+// of this rank's particle at global index req[j] during the last update (meas 4, ncp, cps)
+__global__ void __launch_bounds__(kBlock) k_gather_records(const uint32_t* __restrict__ req, uint64_t nreq, uint64_t gbase,
+                                                           DebugRec d, double* __restrict__ items)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= nreq) return;
+    const uint64_t s = (uint64_t)req[j] - gbase;
+    double* o = items + (uint64_t)rec_items(d.maxc) * j;
+    for (int q = 0; q < 4; ++q) o[q] = d.meas[4 * s + q];
+    o[4] = (double)d.ncp[s];
+    const double* c = d.cp + (uint64_t)6 * d.maxc * s;
+    for (uint32_t q = 0; q < 6 * d.maxc; ++q) o[5 + q] = c[q];
 }
 
 // exclusive prefix sum of m counts in place (one block: each thread a contiguous segment)
@@ -1537,7 +1572,6 @@ __device__ __forceinline__ bool lm_in(int32_t a, int32_t c, uint32_t h)
 
 constexpr uint32_t kLmList = 8;                 // tiles one pass of the merge handles
 constexpr uint16_t kCodeSkip = 0xffffu;
-constexpr uint32_t kLmGroup = 8;                // patches whose cell values load together
 constexpr uint32_t kLmNoList = 0xffffffffu;
 
 // one particle as a map update sees it: its table, its pose, the window's new centre
@@ -1562,79 +1596,6 @@ __device__ __forceinline__ void lm_centre(const MapView& map, const MergeParams&
         na = dm_lm_centre(lx, map.offset_x, map.inv_scale_x);
         nb = dm_lm_centre(ly, map.offset_y, map.inv_scale_y);
     }
-}
-
-// every scan patch's code for this particle: (slot << 6) | cell in the tile, or kCodeSkip
-// (off the grid, on a cell the shared grid covers, or outside the window); codes go to LDS
-// (patch-major, thread-minor).  Counts the covered and dropped patches.
-__device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
-                                         uint16_t* codes, uint32_t& covered, uint32_t& dropped)
-{
-    const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
-    for (uint32_t k = 0; k < mp.m; ++k) {
-        const ScanPatch sp = mp.sp[k];
-        uint32_t cell, cm, cn;
-        if (mp.is_id) {
-            cell = dm_merge_cell_mn(bx, by, q.co, q.sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
-                                    map.height_cells, &cm, &cn);
-        } else {
-            const double wx = (q.co * sp.x + (-q.sn) * sp.y) + q.x;
-            const double wy = (q.sn * sp.x + q.co * sp.y) + q.y;
-            const double wz = sp.z + q.z;
-            const double* A = map.g2l;
-            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
-            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
-            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
-            const bool in = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
-            cm = in ? (uint32_t)fm : 0u;
-            cn = in ? (uint32_t)fn : 0u;
-            cell = in ? cn * map.width + cm : 0xffffffffu;
-        }
-        uint16_t code = kCodeSkip;
-        if (cell != 0xffffffffu) {
-            if ((map.occ[cell >> 5] >> (cell & 31u)) & 1u) {
-                ++covered;                   // the shared grid covers the cell: not merged
-            } else {
-                const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
-                if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
-                    const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
-                    code = (uint16_t)((s << 6) | ((cm & 7u) + 8u * (cn & 7u)));
-                } else {
-                    ++dropped;               // beyond maxSensorRange: outside the window
-                }
-            }
-        }
-        codes[k * kLmBlock] = code;
-    }
-}
-
-// the up to kLmList smallest distinct slots above t (sorted; free entries kLmNoList)
-__device__ __forceinline__ void lm_collect(const uint16_t* codes, uint32_t m, uint32_t t, uint32_t (&L)[kLmList])
-{
-#pragma unroll
-    for (uint32_t r = 0; r < kLmList; ++r) L[r] = kLmNoList;
-    for (uint32_t k = 0; k < m; ++k) {
-        const uint16_t c = codes[k * kLmBlock];
-        if (c == kCodeSkip) continue;
-        const uint32_t s = (uint32_t)c >> 6;
-        if (t != kLmNoList && s <= t) continue;
-        bool dup = false;
-#pragma unroll
-        for (uint32_t r = 0; r < kLmList; ++r) dup |= L[r] == s;
-        if (dup) continue;
-#pragma unroll
-        for (uint32_t r = kLmList - 1; r >= 1; --r) L[r] = L[r - 1] > s ? L[r - 1] : (L[r] > s ? s : L[r]);
-        L[0] = L[0] > s ? s : L[0];
-    }
-}
-
-__device__ __forceinline__ uint32_t lm_find(const uint32_t (&L)[kLmList], uint32_t s)
-{
-    uint32_t idx = kLmNoList;
-#pragma unroll
-    for (uint32_t r = 0; r < kLmList; ++r) idx = L[r] == s ? r : idx;
-    return idx;
 }
 
 // the page slot s of table X holds for the new window: its page when the slot's tile under
@@ -1674,57 +1635,23 @@ __device__ __forceinline__ void lm_load(const DevState& in, uint32_t src, const 
     if (q.placed) lm_centre(map, mp, q, q.na, q.nb);
 }
 
-// k_map_plan: the pages each particle's merge may take -- one per tile its scan patches
-// reach that its table cannot write in place (a new tile, or a page it does not own) -- and
-// the per-block sums (the allocation offsets after k_scan_excl).  The same decisions as
-// k_map_merge, without the values: a tile whose writes all turn out no-ops leaves its page
-// unused (free again at the next collection).
-__global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
-                                                       LocalMaps lm, MergeParams mp)
+// the exclusive prefix of the blocks' per-thread needs (off[t], thread t of the block) and the
+// block's sum (*sum); s_w: kLmBlock / 64 words of LDS
+__device__ __forceinline__ void block_offsets(uint32_t need, bool valid, uint32_t* off, uint32_t* sum, uint32_t* s_w)
 {
-    __shared__ uint16_t s_code[kMaxScanPatches * kLmBlock];
-    __shared__ uint32_t s_w[kLmBlock / 64];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * kLmBlock + tid;
-    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
-    const bool gath = mp.fuse && ctl->gather;
-    const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
-    const uint32_t src = lm_source(mp, i, gath);
-    uint32_t need = 0;
-    if (i < mp.n) {
-        LmPart q;
-        lm_load(in, src, map, mp, mp.ref, q);
-        if (q.placed) {
-            uint32_t covered = 0, dropped = 0;
-            uint16_t* codes = s_code + tid;
-            lm_codes(map, lm, mp, q, codes, covered, dropped);
-            const int2 oc = lm.ctr[q.X];
-            const uint64_t gx = ((uint64_t)lm.tgen[q.X] << 32) | q.X;
-            uint32_t t = kLmNoList;
-            for (;;) {
-                uint32_t L[kLmList];
-                lm_collect(codes, mp.m, t, L);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    uint32_t pfx = need;
 #pragma unroll
-                for (uint32_t r = 0; r < kLmList; ++r) {
-                    if (L[r] == kLmNoList) continue;
-                    const uint32_t P = lm_page_of(lm, q.X, oc, q, L[r]);
-                    const bool mine = !q.shared && P != DM_LM_NONE && lm.owner[P] == gx;
-                    need += mine ? 0u : 1u;
-                }
-                if (L[kLmList - 1] == kLmNoList) break;
-                t = L[kLmList - 1];
-            }
-        }
-        mp.need[i] = (uint16_t)need;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)pfx, o, 64);
+        pfx += lane >= (uint32_t)o ? v : 0u;
     }
-    const uint32_t w = wave_sum_u32(need);
-    if ((tid & 63u) == 0) s_w[tid >> 6] = w;
+    if (lane == 63) s_w[tid >> 6] = pfx;
     __syncthreads();
-    if (tid == 0) {
-        uint32_t b = 0;
-        for (int k = 0; k < kLmBlock / 64; ++k) b += s_w[k];
-        mp.poff[blockIdx.x] = b;
-    }
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) base += s_w[w];
+    if (valid) off[tid] = base + pfx - need;
+    if (tid == kLmBlock - 1) *sum = base + pfx;
 }
 
 // after the scan of the plan's block sums: whether the free list holds this update's pages
@@ -1775,205 +1702,415 @@ __global__ void k_page_budget2(Ctl* __restrict__ ctl, const uint32_t* __restrict
     }
 }
 
-// copy a page (512 bytes) or clear it, then give it to table gT
-__device__ __forceinline__ void lm_take_page(const LocalMaps& lm, uint32_t from, uint32_t to, uint64_t gT)
-{
-    uint4* d = reinterpret_cast<uint4*>(lm.page + (uint64_t)to * DM_LM_PAGE_CELLS);
-    if (from == DM_LM_NONE) {
-        const uint4 e = make_uint4(0u, __float_as_uint(-1.0f), 0u, __float_as_uint(-1.0f));
-#pragma unroll
-        for (uint32_t k = 0; k < 32; ++k) d[k] = e;
-    } else {
-        const uint4* s = reinterpret_cast<const uint4*>(lm.page + (uint64_t)from * DM_LM_PAGE_CELLS);
-#pragma unroll 1
-        for (uint32_t h = 0; h < 4; ++h) {
-            uint4 t[8];
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) t[k] = s[8 * h + k];
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) d[8 * h + k] = t[k];
-        }
-    }
-    lm.owner[to] = gT;
-}
-
 // processMap(scanMap, match = false, update = true) per particle (the oracle's or_map_update):
 // the window moves to the tile under the particle (tiles that leave it are forgotten), then
 // every scan patch, placed at the particle's pose (Translation(x, y, 0) * Rz(theta); the
 // offset patch adds zPos and zSigma^2, src/EmbodiedSlamFilter.cpp:186-189, 213-214), merges
 // into the cell it lands in: inserted into an empty cell (test/testMap.cpp:307-316) or fused
-// (dm_lm_fuse) with the patch there.  One thread per particle.  The table it writes is its own
-// (ref 1: in place) or, when shared, the free table frees[i] it then names (a copy of X made
-// first).  Patches go in passes of up to kLmList tiles (the smallest slots not yet done; the
-// bench's scan reaches <= 6 tiles: one pass) and in groups of kLmGroup whose cell values load
-// together; a tile's first write takes a page of the table's own (copy on write) from the
-// free list, at this particle's offset of the plan.
-__global__ void __launch_bounds__(kLmBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
-                                                        LocalMaps lm, MergeParams mp)
+// (dm_lm_fuse) with the patch there.  The table the particle writes is its own (ref 1: in
+// place) or, when shared, the free table frees[i] it then names.
+// A group of kLmLanes lanes per particle (four particles a wave), so that every global access
+// of the maps is a whole table or page moved by the group together: a lane per particle
+// touching 8-byte cells scattered over 64 pages missed the caches on two of three accesses
+// (r05h: the merge moved ~2x the pages' bytes).  Per particle:
+//   1. the group places the scan patches (kLmPerLane a lane) into cell codes (slot, cell in
+//      the tile; LDS) and ranks each patch among the earlier patches on its cell;
+//   2. passes over its tiles, the kLmList smallest slots not done yet (the bench's scan reaches
+//      <= 6 tiles: one pass); lane r of the group takes tile r: the page the table holds for
+//      it and, when the table does not own that page, a new one from the free list (the
+//      plan's offsets; the plan counted the same tiles);
+//   3. a table copied on write or whose window moved is rewritten by the group (with the
+//      first pass's new pages folded in);
+//   4. kLmStage pages at a time are staged in LDS (loaded whole, or cleared), the patches
+//      applied there rank by rank (scan order on every cell), and the pages stored whole.
+// A tile whose patches all turn out no-ops keeps the copy it got: the same values.
+constexpr uint32_t kLmLanes = 16;
+constexpr uint32_t kLmMergeBlock = 128;
+constexpr uint32_t kLmPpb = kLmMergeBlock / kLmLanes;               // particles per block
+constexpr uint32_t kLmStage = 4;                                     // pages in LDS per particle
+constexpr uint32_t kLmPerLane = (uint32_t)kMaxScanPatches / kLmLanes;
+static_assert(kLmList <= kLmLanes && kLmStage * 2 * kLmLanes == kLmStage * DM_LM_PAGE_CELLS / 2,
+              "a lane per tile of a pass; two 16-byte words of a page per lane");
+
+// the lanes of a wave see each other's LDS writes (in-order LDS; no code motion across)
+__device__ __forceinline__ void wave_sync()
 {
-    __shared__ uint16_t s_code[kMaxScanPatches * kLmBlock];
-    __shared__ uint32_t s_w[kLmBlock / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint64_t i = (uint64_t)blockIdx.x * kLmBlock + tid;
-    if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t grp_min(uint32_t v)
+{
+#pragma unroll
+    for (int o = kLmLanes / 2; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, kLmLanes));
+    return v;
+}
+__device__ __forceinline__ uint32_t grp_max(uint32_t v)
+{
+#pragma unroll
+    for (int o = kLmLanes / 2; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kLmLanes));
+    return v;
+}
+__device__ __forceinline__ uint32_t grp_or(uint32_t v)
+{
+#pragma unroll
+    for (int o = kLmLanes / 2; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, kLmLanes);
+    return v;
+}
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v)
+{
+#pragma unroll
+    for (int o = kLmLanes / 2; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, kLmLanes);
+    return v;
+}
+__device__ __forceinline__ uint32_t grp_get(uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)l, kLmLanes); }
+
+// the smallest slot of the lane's codes above lo (-1: any), over the group
+__device__ __forceinline__ uint32_t lm_next_slot(const uint16_t (&code)[kLmPerLane], int32_t lo)
+{
+    uint32_t mn = kLmNoList;
+#pragma unroll
+    for (uint32_t u = 0; u < kLmPerLane; ++u) {
+        const uint32_t s = (uint32_t)code[u] >> 6;
+        if (code[u] != kCodeSkip && (int32_t)s > lo) mn = min(mn, s);
+    }
+    return grp_min(mn);
+}
+
+// the group's share of a particle's scan patches (k = l + kLmLanes u): their cell codes
+// (slot << 6 | cell in the tile, or kCodeSkip: off the grid, on a cell the shared grid covers,
+// or outside the window), counting the covered and dropped patches
+__device__ __forceinline__ void lm_group_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
+                                               uint32_t l, uint16_t (&code)[kLmPerLane], uint32_t& covered, uint32_t& dropped)
+{
+    const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
+    uint32_t cell[kLmPerLane], cmg[kLmPerLane], cng[kLmPerLane], occw[kLmPerLane];
+#pragma unroll
+    for (uint32_t u = 0; u < kLmPerLane; ++u) {
+        const uint32_t k = l + kLmLanes * u;
+        cell[u] = 0xffffffffu;
+        cmg[u] = cng[u] = 0;
+        if (k >= mp.m) continue;
+        const ScanPatch sp = mp.sp[k];
+        uint32_t cm, cn;
+        if (mp.is_id) {
+            cell[u] = dm_merge_cell_mn(bx, by, q.co, q.sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
+                                       map.height_cells, &cm, &cn);
+        } else {
+            const double wx = (q.co * sp.x + (-q.sn) * sp.y) + q.x;
+            const double wy = (q.sn * sp.x + q.co * sp.y) + q.y;
+            const double wz = sp.z + q.z;
+            const double* A = map.g2l;
+            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+            const bool inn = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
+            cm = inn ? (uint32_t)fm : 0u;
+            cn = inn ? (uint32_t)fn : 0u;
+            cell[u] = inn ? cn * map.width + cm : 0xffffffffu;
+        }
+        cmg[u] = cm;
+        cng[u] = cn;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kLmPerLane; ++u) occw[u] = map.occ[(cell[u] == 0xffffffffu ? 0u : cell[u]) >> 5];
+#pragma unroll
+    for (uint32_t u = 0; u < kLmPerLane; ++u) {
+        code[u] = kCodeSkip;
+        if (cell[u] == 0xffffffffu) continue;
+        if ((occw[u] >> (cell[u] & 31u)) & 1u) {
+            ++covered;                // the shared grid covers the cell: not merged
+            continue;
+        }
+        const uint32_t a = cmg[u] >> DM_LM_TILE_BITS, b = cng[u] >> DM_LM_TILE_BITS;
+        if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
+            const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
+            code[u] = (uint16_t)((s << 6) | ((cmg[u] & 7u) + 8u * (cng[u] & 7u)));
+        } else {
+            ++dropped;                // beyond maxSensorRange: outside the window
+        }
+    }
+}
+
+// k_map_plan: the pages each particle's merge may take -- one per tile its scan patches
+// reach that its table cannot write in place (a new tile, or a page it does not own) -- and
+// the per-block sums (the allocation offsets after k_scan_excl).  The same decisions as
+// k_map_merge, without the values: a tile whose writes all turn out no-ops leaves its page
+// unused (free again at the next collection).  A block of kLmPlanBlock threads plans kLmBlock
+// particles, a group of kLmLanes lanes per particle as in the merge.
+constexpr uint32_t kLmPlanBlock = 256;
+__global__ void __launch_bounds__(kLmPlanBlock) k_map_plan(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+                                                           LocalMaps lm, MergeParams mp)
+{
+    __shared__ uint32_t s_src[kLmBlock], s_need[kLmBlock];
+    __shared__ uint32_t s_w[kLmPlanBlock / 64];
+    const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), g = tid / kLmLanes;
+    const uint64_t base = (uint64_t)blockIdx.x * kLmBlock;
     const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
-    // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
-    // output i reads its ancestor src in state[base] and the merge writes the whole particle,
-    // its table name included, to st = state[base ^ 1]
     const bool gath = mp.fuse && ctl->gather;
     const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
-    const uint32_t src = lm_source(mp, i, gath);
-    // this particle's first page of the plan: the block's offset plus the exclusive prefix of
-    // the needs in the block
-    const uint32_t need = i < mp.n ? (uint32_t)mp.need[i] : 0u;
-    uint32_t pfx = need;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_up((int)pfx, o, 64);
-        pfx += lane >= (uint32_t)o ? v : 0u;
+    if (tid < kLmBlock) {                     // whole waves: the source scan is wave-wide
+        const uint64_t i = base + tid;
+        const uint32_t src = lm_source(mp, i, gath);
+        s_src[tid] = src;
+        if (i < mp.n) mp.srcv[i] = src;
     }
-    if (lane == 63) s_w[tid >> 6] = pfx;
     __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) wbase += s_w[w];
-    uint64_t alloc = ctl->pg_cursor + mp.poff[blockIdx.x] + wbase + (pfx - need);
-    if (gath && i < mp.n) {
-        st.w[i] = in.w[src];
-        if (mp.aux) {
-            st.mprob[i] = in.mprob[src];
-            st.flags[i] = in.flags[src];
+    for (uint32_t j = g; j < kLmBlock; j += kLmPlanBlock / kLmLanes) {
+        const uint64_t i = base + j;
+        uint32_t need = 0;
+        if (i < mp.n) {                       // group-uniform
+            LmPart q;
+            lm_load(in, s_src[j], map, mp, mp.ref, q);
+            if (q.placed) {
+                uint32_t covered = 0, dropped = 0;
+                uint16_t code[kLmPerLane];
+                lm_group_codes(map, lm, mp, q, l, code, covered, dropped);
+                const int2 oc = lm.ctr[q.X];
+                const uint64_t gx = ((uint64_t)lm.tgen[q.X] << 32) | q.X;
+                int32_t lo = -1;
+                for (;;) {
+                    uint32_t cnt = 0, Lr = kLmNoList;
+                    for (; cnt < kLmList; ++cnt) {
+                        const uint32_t mn = lm_next_slot(code, lo);
+                        if (mn == kLmNoList) break;
+                        if (l == cnt) Lr = mn;
+                        lo = (int32_t)mn;
+                    }
+                    bool mine = true;
+                    if (l < cnt) {
+                        const uint32_t P = lm_page_of(lm, q.X, oc, q, Lr);
+                        mine = !q.shared && P != DM_LM_NONE && lm.owner[P] == gx;
+                    }
+                    need += grp_sum(mine ? 0u : 1u);
+                    if (cnt < kLmList || lm_next_slot(code, lo) == kLmNoList) break;
+                }
+            }
         }
-        if (mp.gv.record) mp.gv.anc[i] = (uint32_t)(mp.gbase + src);
-        if (mp.gv.marks[i]) mp.gv.marks[i] = 0u;
+        if (l == 0) s_need[j] = need;
+    }
+    __syncthreads();
+    const uint32_t need = tid < kLmBlock ? s_need[tid] : 0u;
+    block_offsets(need, tid < kLmBlock && base + tid < mp.n, mp.off + base, mp.poff + blockIdx.x, s_w);
+}
+
+__global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
+                                                             LocalMaps lm, MergeParams mp)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][kMaxScanPatches];
+    __shared__ uint4 s_page[kLmPpb][kLmStage][DM_LM_PAGE_CELLS / 2];                  // 16 KB
+    __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
+    const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes;
+    const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
+    if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
+    const bool valid = i < mp.n;
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;      // by value: no private copy of the arguments
+    // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
+    // output i reads its ancestor (srcv: k_map_plan found it) in state[base] and the merge
+    // writes the whole particle, its table name included, to st = state[base ^ 1]
+    const bool gath = mp.fuse && ctl->gather;
+    const DevState in = gath ? (ctl->base ? s1 : s0) : st;
+    const uint32_t src = valid ? (gath ? mp.srcv[i] : (uint32_t)i) : 0u;
+    if (gath && valid) {                      // the gather's copies: a field a lane
+        switch (l) {
+        case 0: st.w[i] = in.w[src]; break;
+        case 1: if (mp.aux) st.mprob[i] = in.mprob[src]; break;
+        case 2: if (mp.aux) st.flags[i] = in.flags[src]; break;
+        case 3: if (mp.gv.record) mp.gv.anc[i] = (uint32_t)(mp.gbase + src); break;
+        case 4: if (mp.gv.marks[i]) mp.gv.marks[i] = 0u; break;
+        case 5: st.x[i] = in.x[src]; break;
+        case 6: st.y[i] = in.y[src]; break;
+        case 7: st.th[i] = in.th[src]; break;
+        case 8: st.z[i] = in.z[src]; break;
+        case 9: st.zs[i] = in.zs[src]; break;
+        default: break;
+        }
     }
     bool dirty = false, moved = false;
     uint32_t dropped = 0, covered = 0, written = 0, taken = 0;
-    if (i < mp.n) {
-        LmPart q;
-        lm_load(in, src, map, mp, mp.ref, q);
-        if (gath) {
-            st.x[i] = q.x; st.y[i] = q.y; st.th[i] = q.th; st.z[i] = q.z; st.zs[i] = q.zs;
-        }
-        uint32_t name = q.X;                 // the table the particle names after the merge
-        if (q.placed) {
-            uint16_t* codes = s_code + tid;
-            lm_codes(map, lm, mp, q, codes, covered, dropped);
-            const int2 oc = lm.ctr[q.X];
-            const bool recentre = oc.x != q.na || oc.y != q.nb;
-            // the table this merge writes: X itself, or a fresh copy when others share X
-            const uint32_t T = q.shared ? mp.frees[i] : q.X;
-            const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
-            uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
-            const uint32_t* xsl = lm.slot + (uint64_t)q.X * lm.S;
-            if (q.shared || recentre) {
-                // the table under the new window: slots whose tile leaves it are cleared
-                for (uint32_t s = 0; s < lm.S; ++s) {
-                    uint32_t v = xsl[s];
-                    if (recentre && v != DM_LM_NONE) {
-                        const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
-                        const int32_t a = lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx);
-                        const int32_t b = lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by);
-                        if (!lm_in(a, q.na, lm.hx) || !lm_in(b, q.nb, lm.hy)) v = DM_LM_NONE;
-                    }
-                    if (q.shared || v != xsl[s]) tsl[s] = v;
+    LmPart q;
+    q.X = 0;
+    q.placed = false;
+    if (valid) lm_load(in, src, map, mp, mp.ref, q);
+    if (valid && q.placed) {                  // group-uniform from here on
+        // ---- 1. the cell codes of the lane's patches (k = l + kLmLanes u)
+        uint16_t code[kLmPerLane];
+        lm_group_codes(map, lm, mp, q, l, code, covered, dropped);
+#pragma unroll
+        for (uint32_t u = 0; u < kLmPerLane; ++u) s_code[pl][l + kLmLanes * u] = code[u];
+        wave_sync();
+        // each patch's rank: the earlier patches on its cell (eight codes a load, broadcast)
+        uint32_t rank[kLmPerLane] = {0, 0, 0, 0};
+        {
+            const uint4* c8 = reinterpret_cast<const uint4*>(&s_code[pl][0]);
+            for (uint32_t e0 = 0; e0 < mp.m; e0 += 8) {
+                const uint4 w = c8[e0 / 8];
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) {
+                    const uint32_t c = (ws[j / 2] >> (16 * (j & 1))) & 0xffffu;
+                    const uint32_t e = e0 + j;
+#pragma unroll
+                    for (uint32_t u = 0; u < kLmPerLane; ++u)
+                        rank[u] += (c == code[u] && e < l + kLmLanes * u) ? 1u : 0u;
                 }
-                lm.ctr[T] = make_int2(q.na, q.nb);
             }
-            dirty = recentre;
-            const float2* pages = lm.page;
-            const double zvar = q.zs * q.zs;
-            uint32_t t = kLmNoList;
-            for (;;) {
-                uint32_t L[kLmList], P[kLmList];
-                bool own[kLmList];
-                lm_collect(codes, mp.m, t, L);
+        }
+        uint32_t maxrank = 0;
 #pragma unroll
-                for (uint32_t r = 0; r < kLmList; ++r) {
-                    P[r] = L[r] == kLmNoList ? DM_LM_NONE : tsl[L[r]];
-                    own[r] = P[r] != DM_LM_NONE && lm.owner[P[r]] == gT;
-                }
-                for (uint32_t k0 = 0; k0 < mp.m; k0 += kLmGroup) {
-                    uint32_t ci[kLmGroup], ri[kLmGroup];
-                    float2 cv[kLmGroup];
-#pragma unroll
-                    for (uint32_t g = 0; g < kLmGroup; ++g) {
-                        const uint32_t k = k0 + g;
-                        const uint16_t c = k < mp.m ? codes[k * kLmBlock] : kCodeSkip;
-                        ri[g] = c == kCodeSkip ? kLmNoList : lm_find(L, (uint32_t)c >> 6);
-                        ci[g] = (uint32_t)c & 63u;
-                        uint32_t pg = DM_LM_NONE;
-#pragma unroll
-                        for (uint32_t r = 0; r < kLmList; ++r) pg = ri[g] == r ? P[r] : pg;
-                        cv[g] = make_float2(0.0f, -1.0f);
-                        if (pg != DM_LM_NONE) cv[g] = pages[(uint64_t)pg * DM_LM_PAGE_CELLS + ci[g]];
+        for (uint32_t u = 0; u < kLmPerLane; ++u) maxrank = code[u] != kCodeSkip ? max(maxrank, rank[u]) : maxrank;
+        maxrank = grp_max(maxrank);
+        // ---- 2. the first pass's tiles: lane r holds L[r], its page P and new page NP
+        const int2 oc = lm.ctr[q.X];
+        const bool recentre = oc.x != q.na || oc.y != q.nb;
+        const uint32_t T = q.shared ? mp.frees[i] : q.X;
+        const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
+        uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
+        const uint32_t* xsl = lm.slot + (uint64_t)q.X * lm.S;
+        uint64_t alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
+        const uint32_t gshift = (tid & 63u) & ~(kLmLanes - 1u);
+        const double zvar = q.zs * q.zs;
+        const bool rewrite = q.shared || (recentre && oc.x != DM_LM_UNSET);
+        int32_t lo = -1;
+        for (uint32_t pass = 0;; ++pass) {
+            uint32_t Lr = kLmNoList, cnt = 0;
+            for (; cnt < kLmList; ++cnt) {
+                const uint32_t mn = lm_next_slot(code, lo);
+                if (mn == kLmNoList) break;
+                if (l == cnt) Lr = mn;
+                lo = (int32_t)mn;
+            }
+            const bool more = cnt == kLmList && lm_next_slot(code, lo) != kLmNoList;
+            uint32_t P = DM_LM_NONE, NP = DM_LM_NONE;
+            bool need = false;
+            if (l < cnt) {
+                P = lm_page_of(lm, q.X, oc, q, Lr);
+                need = !(!q.shared && P != DM_LM_NONE && lm.owner[P] == gT);
+            }
+            const uint32_t gmask = (uint32_t)(__ballot(need) >> gshift) & ((1u << kLmLanes) - 1u);
+            if (need) {
+                NP = lm.frees[alloc + __builtin_popcount(gmask & ((1u << l) - 1u))];
+                lm.owner[NP] = gT;
+                ++taken;
+            }
+            alloc += __builtin_popcount(gmask);
+            if (pass == 0) {
+                // ---- 3. the table: X's slots rewritten into T (evictions; a copy when shared)
+                // with this pass's new pages, else the new pages alone
+                if (rewrite) {
+                    if (l < kLmList) {
+                        s_np[pl][2 * l] = Lr;
+                        s_np[pl][2 * l + 1] = NP;
                     }
+                    wave_sync();
+                    for (uint32_t s = l; s < lm.S; s += kLmLanes) {
+                        const uint32_t v0 = xsl[s];
+                        uint32_t v = v0;
+                        if (recentre && v != DM_LM_NONE) {
+                            const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
+                            const int32_t a = lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx);
+                            const int32_t b = lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by);
+                            if (!lm_in(a, q.na, lm.hx) || !lm_in(b, q.nb, lm.hy)) v = DM_LM_NONE;
+                        }
 #pragma unroll
-                    for (uint32_t g = 0; g < kLmGroup; ++g) {
-                        if (ri[g] == kLmNoList) continue;
-                        // an earlier patch of this group on the same cell already changed it
+                        for (uint32_t r = 0; r < kLmList; ++r)
+                            if (r < cnt && s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) v = s_np[pl][2 * r + 1];
+                        if (q.shared || v != v0) tsl[s] = v;
+                    }
+                } else if (need) {
+                    tsl[Lr] = NP;
+                }
+                if ((q.shared || recentre) && l == 0) lm.ctr[T] = make_int2(q.na, q.nb);
+                dirty = recentre;
+            } else if (need) {
+                // a later pass: T's slot may have been rewritten above (same wave; in order)
+                __builtin_amdgcn_s_waitcnt(0);
+                tsl[Lr] = NP;
+            }
+            // ---- 4. the pass's pages, kLmStage at a time through LDS
+            for (uint32_t r0 = 0; r0 < cnt; r0 += kLmStage) {
+                uint32_t Ls[kLmStage], Ps[kLmStage], Ds[kLmStage];
 #pragma unroll
-                        for (uint32_t e = 0; e < g; ++e)
-                            if (ri[e] == ri[g] && ci[e] == ci[g]) cv[g] = cv[e];
-                        const ScanPatch sp = mp.sp[k0 + g];
+                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
+                    Ls[rr] = grp_get(Lr, r0 + rr);                 // kLmNoList beyond cnt
+                    Ps[rr] = grp_get(P, r0 + rr);
+                    const uint32_t npr = grp_get(NP, r0 + rr);
+                    Ds[rr] = npr != DM_LM_NONE ? npr : Ps[rr];
+                }
+                uint4 v[kLmStage][2];
+#pragma unroll
+                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
+                    const uint4 e = make_uint4(0u, __float_as_uint(-1.0f), 0u, __float_as_uint(-1.0f));
+                    v[rr][0] = v[rr][1] = e;
+                    if (Ls[rr] != kLmNoList && Ps[rr] != DM_LM_NONE) {
+                        const uint4* pp = reinterpret_cast<const uint4*>(lm.page + (uint64_t)Ps[rr] * DM_LM_PAGE_CELLS);
+                        v[rr][0] = pp[2 * l];
+                        v[rr][1] = pp[2 * l + 1];
+                    }
+                }
+                wave_sync();                  // the previous stage's stores read LDS before this one lands
+#pragma unroll
+                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
+                    s_page[pl][rr][2 * l] = v[rr][0];
+                    s_page[pl][rr][2 * l + 1] = v[rr][1];
+                }
+                float2* cells = reinterpret_cast<float2*>(&s_page[pl][0][0]);
+                uint32_t wbits = 0;           // bit rr: this lane wrote page rr
+                for (uint32_t rk = 0; rk <= maxrank; ++rk) {
+                    wave_sync();
+#pragma unroll
+                    for (uint32_t u = 0; u < kLmPerLane; ++u) {
+                        if (code[u] == kCodeSkip || rank[u] != rk) continue;
+                        const uint32_t sl = (uint32_t)code[u] >> 6, ci = (uint32_t)code[u] & 63u;
+                        uint32_t rr = kLmNoList;
+#pragma unroll
+                        for (uint32_t w = 0; w < kLmStage; ++w) rr = Ls[w] == sl ? w : rr;
+                        if (rr == kLmNoList) continue;
+                        const float2 cv = cells[rr * DM_LM_PAGE_CELLS + ci];
+                        const ScanPatch sp = mp.sp[l + kLmLanes * u];
                         const double wz = sp.z + q.z;
                         const double var = sp.stdev * sp.stdev + zvar;
                         float mo, so;
-                        if (dm_lm_holds(cv[g].y)) {
-                            if (!dm_lm_fuse(cv[g].x, cv[g].y, wz, var, &mo, &so)) { ri[g] = kLmNoList; continue; }
+                        if (dm_lm_holds(cv.y)) {
+                            if (!dm_lm_fuse(cv.x, cv.y, wz, var, &mo, &so)) continue;
                         } else {
                             mo = (float)wz;
                             so = (float)dm_sqrt(var);
                         }
-                        cv[g] = make_float2(mo, so);
-                        // the tile's first write: a page of T's own
-                        uint32_t r0 = ri[g];
-                        bool mine = false;
-                        uint32_t pg = DM_LM_NONE;
-#pragma unroll
-                        for (uint32_t r = 0; r < kLmList; ++r) {
-                            mine = r0 == r ? own[r] : mine;
-                            pg = r0 == r ? P[r] : pg;
-                        }
+                        cells[rr * DM_LM_PAGE_CELLS + ci] = make_float2(mo, so);
+                        wbits |= 1u << rr;
                         ++written;
-                        if (!mine) {
-                            ++taken;
-                            const uint32_t np = lm.frees[alloc++];
-                            lm_take_page(lm, pg, np, gT);
-                            tsl[L[r0]] = np;
-#pragma unroll
-                            for (uint32_t r = 0; r < kLmList; ++r) {
-                                P[r] = r0 == r ? np : P[r];
-                                own[r] = r0 == r ? true : own[r];
-                            }
-                        }
-                        dirty = true;
-                    }
-#pragma unroll
-                    for (uint32_t g = 0; g < kLmGroup; ++g) {
-                        if (ri[g] == kLmNoList) continue;
-                        uint32_t pg = DM_LM_NONE;
-#pragma unroll
-                        for (uint32_t r = 0; r < kLmList; ++r) pg = ri[g] == r ? P[r] : pg;
-                        lm.page[(uint64_t)pg * DM_LM_PAGE_CELLS + ci[g]] = cv[g];
                     }
                 }
-                if (L[kLmList - 1] == kLmNoList) break;
-                t = L[kLmList - 1];
+                wbits = grp_or(wbits);
+                wave_sync();
+                // a page goes back whole when the patches changed it, or when it is new
+#pragma unroll
+                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
+                    if (Ls[rr] == kLmNoList || (Ds[rr] == Ps[rr] && !((wbits >> rr) & 1u))) continue;
+                    uint4* dp = reinterpret_cast<uint4*>(lm.page + (uint64_t)Ds[rr] * DM_LM_PAGE_CELLS);
+                    dp[2 * l] = s_page[pl][rr][2 * l];
+                    dp[2 * l + 1] = s_page[pl][rr][2 * l + 1];
+                }
+                dirty = dirty || wbits != 0;
             }
-            if (q.shared && dirty) {
-                name = T;
-                moved = true;
-            }
+            if (!more) break;
         }
-        if (gath || moved) st.sid[i] = name;
+        if (q.shared && dirty) moved = true;
+        if ((gath || moved) && l == 0) st.sid[i] = moved ? T : q.X;
+    } else if (valid && gath && l == 0) {
+        st.sid[i] = q.X;
     }
+    // the counters: particles once (the group's lane 0), patches from every lane
+    const bool lead = l == 0;
     dropped = wave_sum_u32(dropped);
     covered = wave_sum_u32(covered);
     written = wave_sum_u32(written);
     taken = wave_sum_u32(taken);
-    const uint64_t dmask = __ballot(dirty), mmask = __ballot(moved);
-    if (lane == 0) {                     // one address per counter slot: no single hot atomic
-        const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
+    const uint64_t dmask = __ballot(lead && dirty), mmask = __ballot(lead && moved);
+    if ((tid & 63u) == 0) {                   // one address per counter slot: no single hot atomic
+        const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmMergeBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
         if (written) atomicAdd((unsigned long long*)&mp.cnt[4 * kMergeCounterSlots + slot_c], (unsigned long long)written);
         if (taken) atomicAdd((unsigned long long*)&mp.cnt[5 * kMergeCounterSlots + slot_c], (unsigned long long)taken);
         if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
@@ -3451,12 +3588,20 @@ extern "C" hipError_t eslam_launch_contact_records(DevState s0, DevState s1, con
 
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d, eslam_particle_record* out, eslam_cpoint* cps,
-                                                uint32_t max_cp, hipStream_t stream)
+                                                uint32_t max_cp, const uint64_t* slot, const double* remote, hipStream_t stream)
 {
     const uint32_t blocks = (uint32_t)((count + kBlock - 1) / kBlock);
     if (!blocks) return hipSuccess;
     hipLaunchKernelGGL(k_pack_records, dim3(blocks), dim3(kBlock), 0, stream, s0, s1, ctl, first, stride, count, gbase, anc,
-                       *d, out, cps, max_cp);
+                       *d, out, cps, max_cp, slot, remote);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t eslam_launch_gather_records(const uint32_t* req, uint64_t nreq, uint64_t gbase, const DebugRec* d,
+                                                  double* items, hipStream_t stream)
+{
+    const uint64_t blocks = (nreq + kBlock - 1) / kBlock;
+    if (blocks) hipLaunchKernelGGL(k_gather_records, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, req, nreq, gbase, *d, items);
     return hipGetLastError();
 }
 
@@ -3539,15 +3684,15 @@ extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, 
     const uint32_t nb = (uint32_t)((mp->n + kLmBlock - 1) / kLmBlock);
     e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
     if (e != hipSuccess) return e;
-    if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmPlanBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     return page_budget(ctl, lm, mp, nb, pgc, stream);
 }
 
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
                                              const MergeParams* mp, hipStream_t stream)
 {
-    const uint32_t nb = (uint32_t)((mp->n + kLmBlock - 1) / kLmBlock);
-    if (nb) hipLaunchKernelGGL(k_map_merge, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    const uint32_t nb = (uint32_t)((mp->n + kLmPpb - 1) / kLmPpb);
+    if (nb) hipLaunchKernelGGL(k_map_merge, dim3(nb), dim3(kLmMergeBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
     return hipGetLastError();
 }
@@ -3634,15 +3779,7 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_plan(const uint32_t* __restri
     const uint64_t j = (uint64_t)blockIdx.x * kLmBlock + threadIdx.x;
     uint32_t need = 0;
     if (j < *ndup_dev) need = hdr[sid[dups[j]] & ~kSidRecord].npg;
-    if (j < mp.n) mp.need[j] = (uint16_t)need;
-    const uint32_t w = wave_sum_u32(need);
-    if ((threadIdx.x & 63u) == 0) s_w[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t b = 0;
-        for (int k = 0; k < kLmBlock / 64; ++k) b += s_w[k];
-        mp.poff[blockIdx.x] = b;
-    }
+    block_offsets(need, j < mp.n, mp.off + (j - threadIdx.x), mp.poff + blockIdx.x, s_w);
 }
 
 // received particle j takes free table frees[j] and pages from the free list, filled from its
@@ -3653,19 +3790,15 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(const uint32_t* __restri
                                                         const MapPayHdr* __restrict__ hdr, const uint32_t* __restrict__ hoff,
                                                         const MapPayPage* __restrict__ pay, LocalMaps lm, MergeParams mp)
 {
-    __shared__ uint32_t s_need[kLmBlock];
     if (ctl->err & kFaultPages) return;
     const uint32_t* sid = cur_sid(sr);
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint64_t ndup = *ndup_dev;
     const uint64_t j0 = (uint64_t)blockIdx.x * kLmBlock;
-    s_need[tid] = j0 + tid < mp.n ? mp.need[j0 + tid] : 0u;
-    __syncthreads();
     for (uint32_t k = tid >> 6; k < (uint32_t)kLmBlock; k += kLmBlock / 64) {
         const uint64_t j = j0 + k;
         if (j >= ndup) break;
-        uint64_t alloc = ctl->pg_cursor + mp.poff[blockIdx.x];
-        for (uint32_t e = 0; e < k; ++e) alloc += s_need[e];
+        const uint64_t alloc = ctl->pg_cursor + mp.poff[blockIdx.x] + mp.off[j];
         const uint32_t rec = sid[dups[j]] & ~kSidRecord;
         const uint32_t T = frees[j];
         const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
@@ -3947,12 +4080,28 @@ extern "C" int eslam_debug_k1_occupancy(int* blocks_per_cu, int lds)
 }
 
 #ifdef ESLAM_STAMPS
-// diagnostic builds: copy the stamps of the last K1 (which = 1) or K3 (which = 3) launch
-extern "C" int eslam_gpu_debug_stamps(int which, uint64_t* out, uint64_t blocks)
+// diagnostic builds: zero the stamps (before the launch to be measured: a block that returns
+// early then leaves zeros, not an older launch's stamps)
+extern "C" int eslam_gpu_debug_stamps_clear(void)
+{
+    void *a = nullptr, *b = nullptr, *g = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_stamps_k1)) != hipSuccess || hipGetSymbolAddress(&b, HIP_SYMBOL(g_stamps_k3)) != hipSuccess ||
+        hipGetSymbolAddress(&g, HIP_SYMBOL(g_stamps_grid)) != hipSuccess)
+        return -1;
+    const size_t bytes = sizeof(uint64_t) * kStampBlocks * kStampSlots;
+    if (hipMemset(a, 0, bytes) != hipSuccess || hipMemset(b, 0, bytes) != hipSuccess || hipMemset(g, 0, 8) != hipSuccess) return -1;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+// copy the stamps of the last K1 (which = 1) or K3 (which = 3) launch; returns that launch's
+// block count (its grid; blocks past kStampBlocks are not stamped), or -1
+extern "C" int64_t eslam_gpu_debug_stamps(int which, uint64_t* out, uint64_t blocks)
 {
     if (blocks > kStampBlocks) blocks = kStampBlocks;
+    uint32_t grid[2] = {0, 0};
     const hipError_t e = which == 1 ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k1), blocks * kStampSlots * 8)
                                     : hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k3), blocks * kStampSlots * 8);
-    return e == hipSuccess ? 0 : -1;
+    if (e != hipSuccess || hipMemcpyFromSymbol(grid, HIP_SYMBOL(g_stamps_grid), sizeof(grid)) != hipSuccess) return -1;
+    return (int64_t)grid[which == 1 ? 0 : 1];
 }
 #endif

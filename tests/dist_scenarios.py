@@ -10,10 +10,11 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit", "records")
 EDIT_GLOBAL = (0, 37)                            # edit: the particles one rank edits
 CONFIG3_STEPS = 3
 MAP_SAMPLES = 64                                 # config4: particles whose maps are compared
+RECORD_CPOINTS = 8                               # records: contact points per particle compared
 
 
 def scenario_config(name, n_global):
@@ -25,8 +26,10 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0"):
+    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0", "records"):
         S.bench_config(cfg, n_global)
+        if name == "records":                    # logDebug: every update's contact points
+            cfg.flags |= A.FLAG_RECORD_CONTACTS
         if name in ("maps", "config4"):          # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
         if name == "config4":
@@ -52,7 +55,7 @@ def scenario_grid(name):
         return S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
     if name == "maps":                            # the front feet stand on cells only the scans map
         return S.unmapped_beyond(S.rough_map(cells=120), 0.3)
-    return S.rough_map(cells=120) if name not in ("forced", "burst", "edit", "getter0") else S.rough_map(cells=120, multi=False)
+    return S.rough_map(cells=120) if name not in ("forced", "burst", "edit", "getter0", "records") else S.rough_map(cells=120, multi=False)
 
 
 def digest(a):
@@ -153,6 +156,17 @@ def edit_particles(f, lo, hi):
         f.upload(pa)
 
 
+def _records(rec, key, f):
+    """logDebug's PoseParticle records (eslam_gpu_download_records: cpoints, meas_pos,
+    meas_theta of each particle's ancestor at the last update; a collective on a sharded
+    filter, so every rank calls it)"""
+    r, cps = f.download_records(max_cpoints=RECORD_CPOINTS)
+    for fld in ("index", "n_cpoints", "meas_pos", "meas_theta", "position", "weight"):
+        rec[f"{key}/rec_{fld}"] = np.ascontiguousarray(r[fld])
+    for fld in ("point", "zdiff", "zvar", "prob"):
+        rec[f"{key}/cp_{fld}"] = np.ascontiguousarray(cps[fld])
+
+
 def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     """f: OracleFilter or GpuFilter-like (set_map/init_gaussian/upload/step/...).
     info_fn(f) returns the eslam_update_info of the last update."""
@@ -210,6 +224,8 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         info = info_fn(f)
         _info(rec, f"s{k}", info)
         _snap(rec, f"s{k}", f, bool(info.resampled))
+        if name == "records":
+            _records(rec, f"s{k}", f)
         if scan is not None:                     # processMap(scan, false, true)
             f.map_update(scan)
     if scan is not None:                         # every particle's own patches, sorted by cell

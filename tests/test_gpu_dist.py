@@ -24,6 +24,30 @@ def test_sharded_gpu_gloo_equals_single(oracle, tmp_path, name, n_global, world)
 
 
 @pytest.mark.parametrize("world", [2, 3])
+def test_sharded_records_equal_single_context(gpu_mod, tmp_path, world):
+    """logDebug on a sharded filter (src/PoseEstimator.cpp:285-287,322-325): the PoseParticle
+    records with their cpoints, meas_pos and meas_theta, downloaded after every update by every
+    rank (a collective: records of ancestors that sat on another rank are fetched from it),
+    concatenated over 2 / 3 gloo ranks, equal the one-context filter's records bit for bit --
+    and particles did descend from ancestors on other ranks.  The one-context records equal the
+    oracle's capture (test_gpu_records.py)."""
+    import eslam_abi as A
+    from dist_scenarios import run_scenario, scenario_config
+    n_global = 6000
+    cfg = scenario_config("records", n_global)
+    f = gpu_mod.GpuFilter(cfg)
+    want = run_scenario(f, "records", n_global, 0, n_global, info_fn=lambda g: g.sync())
+    f.close()
+    got = merge(launch("gpu", "records", n_global, world, str(tmp_path), mem="host", timeout=400))
+    assert_same(got, want, f"gpu records N={n_global} world={world}")
+    g = A.shard_bounds(n_global, world)
+    owner = np.searchsorted(g, np.arange(n_global), side="right") - 1
+    moved = sum(int(np.count_nonzero(owner[want[k].astype(np.int64)] != owner)) for k in want if k.endswith("/anc"))
+    assert moved > 0
+    assert any(want[k].any() for k in want if k.endswith("/rec_n_cpoints"))
+
+
+@pytest.mark.parametrize("world", [2, 3])
 def test_sharded_getter_on_one_rank_then_destroy(oracle, tmp_path, world):
     """A rank-local getter on rank 0 only after deferred updates, then every rank destroys its
     context (include/eslam_gpu.h, SPMD order): no rank hangs in the deferred exchange, and

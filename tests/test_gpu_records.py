@@ -89,22 +89,3 @@ def test_records_strided_without_capture(gpu_mod):
     assert not rec["meas_pos"].any()
     with pytest.raises(gpu_mod.EslamError):
         gpu.download_records(first=n - 1, stride=1, count=2)
-
-
-def test_records_refused_on_a_sharded_filter(gpu_mod, tmp_path):
-    """logDebug's records are one-GPU only: making a logDebug filter a shard fails loudly
-    (ESLAM_ERR_UNSUPPORTED) instead of stepping without records."""
-    import torch.distributed as dist
-    import eslam_dist
-    dist.init_process_group("gloo", init_method="file://" + str(tmp_path / "store"), rank=0, world_size=1)
-    try:
-        comm = eslam_dist.TorchComm(device_memory=False)
-        for flags, debug in ((A.FLAG_RECORD_CONTACTS, 0), (0, 1)):
-            cfg = S.bench_config(A.default_config(), 1024)
-            cfg.flags |= flags
-            cfg.log_debug = debug
-            with pytest.raises(gpu_mod.EslamError, match="not supported on a sharded filter") as e:
-                eslam_dist.ShardedGpuFilter(cfg, 1024, comm)
-            assert e.value.code == -8            # ESLAM_ERR_UNSUPPORTED
-    finally:
-        dist.destroy_process_group()
