@@ -268,7 +268,8 @@ struct eslam_ctx {
     uint32_t* sid_mem = nullptr;             // 2 x cap: DevState::sid of both state buffers
     uint32_t* cow = nullptr;                 // owner, counts, free and sharing lists + the copy count
     uint32_t* lm_off = nullptr;              // per particle: its first page in its plan block (MergeParams::off)
-    uint32_t* lm_srcv = nullptr;             // per particle: the particle its merge reads (MergeParams::srcv)
+    void* lm_job = nullptr;                  // per particle: the plan's record (MergeParams::job)
+    uint16_t* lm_codes = nullptr;            // per particle: the plan's cell codes (MergeParams::codes)
     uint32_t* lm_poff = nullptr;             // per merge block: page offsets (+ total)
     uint32_t* lm_pgc = nullptr;              // the page collection's compaction counts
     uint64_t* merge_cnt = nullptr;           // the map merge's statistics slots (2 x kMergeCounterSlots) and
@@ -614,9 +615,9 @@ static void free_local_maps(eslam_ctx* ctx)
 {
     (void)hipFree(ctx->lm.ctr); (void)hipFree(ctx->lm.slot); (void)hipFree(ctx->lm.page); (void)hipFree(ctx->lm.tgen);
     (void)hipFree(ctx->lm.owner); (void)hipFree(ctx->lm.frees); (void)hipFree(ctx->lm.mark);
-    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_srcv); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc);
+    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_job); (void)hipFree(ctx->lm_codes); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc);
     ctx->lm = LocalMaps{};
-    ctx->lm_off = nullptr; ctx->lm_srcv = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr;
+    ctx->lm_off = nullptr; ctx->lm_job = nullptr; ctx->lm_codes = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr;
     ctx->lm_ready = false;
 }
 
@@ -791,7 +792,8 @@ static int local_maps_reset(eslam_ctx* ctx)
     HIPCHK(ctx, hipMalloc(&lm.frees, lm.npages * 4));
     HIPCHK(ctx, hipMalloc(&lm.mark, ((lm.npages + 15) / 16) * 16));
     HIPCHK(ctx, hipMalloc(&ctx->lm_off, cap * 4));
-    HIPCHK(ctx, hipMalloc(&ctx->lm_srcv, cap * 4));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_job, cap * sizeof(MergeJob)));
+    HIPCHK(ctx, hipMalloc(&ctx->lm_codes, cap * 2 * kMaxScanPatches));
     HIPCHK(ctx, hipMalloc(&ctx->lm_poff, ((cap + kLmBlock - 1) / kLmBlock + 1) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->lm_pgc, (ptiles + 1) * 4));
     HIPCHK(ctx, eslam_launch_store_init(ctx->sid_mem, &lm, cap, pool, ctx->stream));
@@ -1685,7 +1687,8 @@ static MergeParams merge_params(eslam_ctx* ctx, const CowScratch& cs)
     mp.ref = cs.ref;
     mp.frees = cs.frees;
     mp.off = ctx->lm_off;
-    mp.srcv = ctx->lm_srcv;
+    mp.job = (MergeJob*)ctx->lm_job;
+    mp.codes = ctx->lm_codes;
     mp.poff = ctx->lm_poff;
     mp.fault = ctx->fault_host;
     mp.n = ctx->n;

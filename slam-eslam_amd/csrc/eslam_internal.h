@@ -309,6 +309,23 @@ inline CowScratch cow_layout(uint32_t* base, uint64_t cap)
     c.tiles = (uint32_t)tiles;
     return c;
 }
+// k_map_plan -> k_map_merge, per particle (one 128-byte record): what the plan decided, so
+// the merge's first memory round trip brings everything its page moves need
+constexpr uint32_t kJobPlaced = 1u, kJobShared = 2u, kJobMore = 4u;    // flags; tiles of pass 1 << 8
+struct alignas(16) MergeJob {
+    uint32_t X, T;                       // the table the particle names; the table its merge writes
+    uint64_t gT;                         // tgen[T] << 32 | T: the owner word of T's pages
+    int32_t na, nb;                      // the window's new centre
+    int32_t ox, oy;                      // its old centre (ctr[X])
+    uint32_t flags;
+    uint32_t need;                       // bit r: tile r of pass 1 takes a new page
+    uint16_t L[8];                       // pass 1's tiles (slots, ascending)
+    uint32_t P[8];                       // their pages in X (DM_LM_NONE: none)
+    double z, zs;                        // zPos, zSigma (the offset patch)
+    uint32_t src, pad[5];                // the particle the merge reads (gather); pad to 128 B
+};
+static_assert(sizeof(MergeJob) == 128, "merge job");
+
 struct MergeParams {
     uint64_t n;
     uint32_t m;                          // scan patches
@@ -320,9 +337,9 @@ struct MergeParams {
     const uint32_t* frees;               // CowScratch::frees: particle i's table if it writes a shared map
     uint32_t* off;                       // per particle: its first page of the plan within its plan block
                                          // (k_map_plan / k_recv_plan: the exclusive prefix of the needs)
-    uint32_t* srcv;                      // per particle: the particle the merge reads (its ancestor
-                                         // when the merge runs a pending resample gather; k_map_plan)
     uint32_t* poff;                      // per block of kLmBlock particles: first page offset (+ total)
+    MergeJob* job;                       // per particle: k_map_plan's record for the merge
+    uint16_t* codes;                     // per particle: kMaxScanPatches scan-patch cell codes (plan)
     uint32_t* fault;                     // host-mapped fault word (kFaultPages)
     GatherView gv;                       // fuse: a pending resample gather runs in the merge (one GPU)
     uint64_t gbase;

@@ -26,6 +26,7 @@
 // lanes, ballots as 64-bit masks.  All arithmetic goes through include/eslam_detmath.h and
 // the file is compiled with -ffp-contract=off, so results equal the CPU oracle bit for bit.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <string.h>
 
 #include "eslam_internal.h"
@@ -1572,6 +1573,7 @@ __device__ __forceinline__ bool lm_in(int32_t a, int32_t c, uint32_t h)
 
 constexpr uint32_t kLmList = 8;                 // tiles one pass of the merge handles
 constexpr uint16_t kCodeSkip = 0xffffu;
+constexpr uint32_t kLmGroup = 8;                // patches whose cell values load together
 constexpr uint32_t kLmNoList = 0xffffffffu;
 
 // one particle as a map update sees it: its table, its pose, the window's new centre
@@ -1596,6 +1598,79 @@ __device__ __forceinline__ void lm_centre(const MapView& map, const MergeParams&
         na = dm_lm_centre(lx, map.offset_x, map.inv_scale_x);
         nb = dm_lm_centre(ly, map.offset_y, map.inv_scale_y);
     }
+}
+
+// every scan patch's code for this particle: (slot << 6) | cell in the tile, or kCodeSkip
+// (off the grid, on a cell the shared grid covers, or outside the window); codes go to LDS
+// (patch-major, thread-minor).  Counts the covered and dropped patches.
+__device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
+                                         uint16_t* codes, uint32_t& covered, uint32_t& dropped)
+{
+    const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
+    for (uint32_t k = 0; k < mp.m; ++k) {
+        const ScanPatch sp = mp.sp[k];
+        uint32_t cell, cm, cn;
+        if (mp.is_id) {
+            cell = dm_merge_cell_mn(bx, by, q.co, q.sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
+                                    map.height_cells, &cm, &cn);
+        } else {
+            const double wx = (q.co * sp.x + (-q.sn) * sp.y) + q.x;
+            const double wy = (q.sn * sp.x + q.co * sp.y) + q.y;
+            const double wz = sp.z + q.z;
+            const double* A = map.g2l;
+            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+            const bool in = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
+            cm = in ? (uint32_t)fm : 0u;
+            cn = in ? (uint32_t)fn : 0u;
+            cell = in ? cn * map.width + cm : 0xffffffffu;
+        }
+        uint16_t code = kCodeSkip;
+        if (cell != 0xffffffffu) {
+            if ((map.occ[cell >> 5] >> (cell & 31u)) & 1u) {
+                ++covered;                   // the shared grid covers the cell: not merged
+            } else {
+                const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+                if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
+                    const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
+                    code = (uint16_t)((s << 6) | ((cm & 7u) + 8u * (cn & 7u)));
+                } else {
+                    ++dropped;               // beyond maxSensorRange: outside the window
+                }
+            }
+        }
+        codes[k * kLmBlock] = code;
+    }
+}
+
+// the up to kLmList smallest distinct slots above t (sorted; free entries kLmNoList)
+__device__ __forceinline__ void lm_collect(const uint16_t* codes, uint32_t m, uint32_t t, uint32_t (&L)[kLmList])
+{
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) L[r] = kLmNoList;
+    for (uint32_t k = 0; k < m; ++k) {
+        const uint16_t c = codes[k * kLmBlock];
+        if (c == kCodeSkip) continue;
+        const uint32_t s = (uint32_t)c >> 6;
+        if (t != kLmNoList && s <= t) continue;
+        bool dup = false;
+#pragma unroll
+        for (uint32_t r = 0; r < kLmList; ++r) dup |= L[r] == s;
+        if (dup) continue;
+#pragma unroll
+        for (uint32_t r = kLmList - 1; r >= 1; --r) L[r] = L[r - 1] > s ? L[r - 1] : (L[r] > s ? s : L[r]);
+        L[0] = L[0] > s ? s : L[0];
+    }
+}
+
+__device__ __forceinline__ uint32_t lm_find(const uint32_t (&L)[kLmList], uint32_t s)
+{
+    uint32_t idx = kLmNoList;
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) idx = L[r] == s ? r : idx;
+    return idx;
 }
 
 // the page slot s of table X holds for the new window: its page when the slot's tile under
@@ -1709,28 +1784,41 @@ __global__ void k_page_budget2(Ctl* __restrict__ ctl, const uint32_t* __restrict
 // into the cell it lands in: inserted into an empty cell (test/testMap.cpp:307-316) or fused
 // (dm_lm_fuse) with the patch there.  The table the particle writes is its own (ref 1: in
 // place) or, when shared, the free table frees[i] it then names.
-// A group of kLmLanes lanes per particle (four particles a wave), so that every global access
-// of the maps is a whole table or page moved by the group together: a lane per particle
-// touching 8-byte cells scattered over 64 pages missed the caches on two of three accesses
-// (r05h: the merge moved ~2x the pages' bytes).  Per particle:
-//   1. the group places the scan patches (kLmPerLane a lane) into cell codes (slot, cell in
-//      the tile; LDS) and ranks each patch among the earlier patches on its cell;
-//   2. passes over its tiles, the kLmList smallest slots not done yet (the bench's scan reaches
-//      <= 6 tiles: one pass); lane r of the group takes tile r: the page the table holds for
-//      it and, when the table does not own that page, a new one from the free list (the
-//      plan's offsets; the plan counted the same tiles);
-//   3. a table copied on write or whose window moved is rewritten by the group (with the
-//      first pass's new pages folded in);
-//   4. kLmStage pages at a time are staged in LDS (loaded whole, or cleared), the patches
-//      applied there rank by rank (scan order on every cell), and the pages stored whole.
+// Two kernels.  k_map_plan (a lane per particle) does the lookups: the codes of the scan's
+// cells, the tiles, their pages, whether the table owns them.  k_map_merge moves the data, a
+// group of kLmLanes lanes per particle (four particles a wave), so that every access of the
+// maps is a whole table or page moved by the group together (a lane per particle touching
+// 8-byte cells scattered over 64 pages missed the caches on two of three accesses: r05h).
+// Per particle:
+//   1. the plan's record, the codes (kLmPerLane a lane) and the allocation offset arrive in one
+//      round trip; each patch is ranked among the earlier patches on its cell;
+//   2. lane r of the group takes tile r of the first pass: a new page when the plan says the
+//      table does not own it; a table copied on write or whose window moved is rewritten by
+//      the group (evictions, the pass's new pages folded in);
+//   3. kLmStage pages at a time are staged in LDS (each lane loads 32 B: whole 512-B pages),
+//      the patches applied there rank by rank (scan order on every cell), and the changed or
+//      new pages stored whole.  Tiles beyond kLmList (a later pass) are looked up by the group.
 // A tile whose patches all turn out no-ops keeps the copy it got: the same values.
-constexpr uint32_t kLmLanes = 16;
+// 8 lanes per particle, 2 staged pages each, at most 128 VGPRs: 11.8 ms per merge at 8M against
+// 12.4 for 16 lanes with 4 pages (r05 A/B, profiles/r05/ab_merge_lanes.log)
+#ifndef ESLAM_LM_LANES
+#define ESLAM_LM_LANES 8
+#endif
+#ifndef ESLAM_LM_STAGE
+#define ESLAM_LM_STAGE 2
+#endif
+#ifndef ESLAM_LM_WPE
+#define ESLAM_LM_WPE 4
+#endif
+constexpr uint32_t kLmLanes = ESLAM_LM_LANES;                       // lanes per particle: 8 or 16
 constexpr uint32_t kLmMergeBlock = 128;
 constexpr uint32_t kLmPpb = kLmMergeBlock / kLmLanes;               // particles per block
-constexpr uint32_t kLmStage = 4;                                     // pages in LDS per particle
+constexpr uint32_t kLmStage = ESLAM_LM_STAGE;                        // pages in LDS per particle
 constexpr uint32_t kLmPerLane = (uint32_t)kMaxScanPatches / kLmLanes;
-static_assert(kLmList <= kLmLanes && kLmStage * 2 * kLmLanes == kLmStage * DM_LM_PAGE_CELLS / 2,
-              "a lane per tile of a pass; two 16-byte words of a page per lane");
+static_assert(kLmList <= kLmLanes && (kLmLanes == 8 || kLmLanes == 16) && kLmStage <= 4,
+              "a lane per tile of a pass; 8 or 16 lanes; row masks of 8 bits per staged page in a word");
+constexpr uint32_t kLmChunk = kLmLanes * 16;                         // bytes of a page a group moves per instruction
+constexpr uint32_t kLmNq = DM_LM_PAGE_CELLS * 8 / kLmChunk;           // such chunks per page
 
 // the lanes of a wave see each other's LDS writes (in-order LDS; no code motion across)
 __device__ __forceinline__ void wave_sync()
@@ -1757,12 +1845,6 @@ __device__ __forceinline__ uint32_t grp_or(uint32_t v)
     for (int o = kLmLanes / 2; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, kLmLanes);
     return v;
 }
-__device__ __forceinline__ uint32_t grp_sum(uint32_t v)
-{
-#pragma unroll
-    for (int o = kLmLanes / 2; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, kLmLanes);
-    return v;
-}
 __device__ __forceinline__ uint32_t grp_get(uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)l, kLmLanes); }
 
 // the smallest slot of the lane's codes above lo (-1: any), over the group
@@ -1777,143 +1859,194 @@ __device__ __forceinline__ uint32_t lm_next_slot(const uint16_t (&code)[kLmPerLa
     return grp_min(mn);
 }
 
-// the group's share of a particle's scan patches (k = l + kLmLanes u): their cell codes
-// (slot << 6 | cell in the tile, or kCodeSkip: off the grid, on a cell the shared grid covers,
-// or outside the window), counting the covered and dropped patches
-__device__ __forceinline__ void lm_group_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
-                                               uint32_t l, uint16_t (&code)[kLmPerLane], uint32_t& covered, uint32_t& dropped)
+// k_map_plan: per particle (a lane each: kLmBlock particles a block, so the latency of its
+// chain of lookups -- state, table, page, owner -- overlaps across many particles) the cell
+// codes of its scan (MergeParams::codes), the first pass's tiles with their pages and whether
+// the table owns them (the MergeJob record), and the pages its merge takes: one per tile its
+// scan reaches that its table cannot write in place (a new tile, or a page it does not own).
+// The block sums give the allocation offsets (k_scan_excl).  A tile whose writes all turn out
+// no-ops leaves its page unused (free again at the next collection).
+__global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+                                                       LocalMaps lm, MergeParams mp)
 {
-    const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
-    uint32_t cell[kLmPerLane], cmg[kLmPerLane], cng[kLmPerLane], occw[kLmPerLane];
-#pragma unroll
-    for (uint32_t u = 0; u < kLmPerLane; ++u) {
-        const uint32_t k = l + kLmLanes * u;
-        cell[u] = 0xffffffffu;
-        cmg[u] = cng[u] = 0;
-        if (k >= mp.m) continue;
-        const ScanPatch sp = mp.sp[k];
-        uint32_t cm, cn;
-        if (mp.is_id) {
-            cell[u] = dm_merge_cell_mn(bx, by, q.co, q.sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
-                                       map.height_cells, &cm, &cn);
-        } else {
-            const double wx = (q.co * sp.x + (-q.sn) * sp.y) + q.x;
-            const double wy = (q.sn * sp.x + q.co * sp.y) + q.y;
-            const double wz = sp.z + q.z;
-            const double* A = map.g2l;
-            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
-            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
-            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
-            const bool inn = (fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells);
-            cm = inn ? (uint32_t)fm : 0u;
-            cn = inn ? (uint32_t)fn : 0u;
-            cell[u] = inn ? cn * map.width + cm : 0xffffffffu;
-        }
-        cmg[u] = cm;
-        cng[u] = cn;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kLmPerLane; ++u) occw[u] = map.occ[(cell[u] == 0xffffffffu ? 0u : cell[u]) >> 5];
-#pragma unroll
-    for (uint32_t u = 0; u < kLmPerLane; ++u) {
-        code[u] = kCodeSkip;
-        if (cell[u] == 0xffffffffu) continue;
-        if ((occw[u] >> (cell[u] & 31u)) & 1u) {
-            ++covered;                // the shared grid covers the cell: not merged
-            continue;
-        }
-        const uint32_t a = cmg[u] >> DM_LM_TILE_BITS, b = cng[u] >> DM_LM_TILE_BITS;
-        if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
-            const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
-            code[u] = (uint16_t)((s << 6) | ((cmg[u] & 7u) + 8u * (cng[u] & 7u)));
-        } else {
-            ++dropped;                // beyond maxSensorRange: outside the window
-        }
-    }
-}
-
-// k_map_plan: the pages each particle's merge may take -- one per tile its scan patches
-// reach that its table cannot write in place (a new tile, or a page it does not own) -- and
-// the per-block sums (the allocation offsets after k_scan_excl).  The same decisions as
-// k_map_merge, without the values: a tile whose writes all turn out no-ops leaves its page
-// unused (free again at the next collection).  A block of kLmPlanBlock threads plans kLmBlock
-// particles, a group of kLmLanes lanes per particle as in the merge.
-constexpr uint32_t kLmPlanBlock = 256;
-__global__ void __launch_bounds__(kLmPlanBlock) k_map_plan(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
-                                                           LocalMaps lm, MergeParams mp)
-{
-    __shared__ uint32_t s_src[kLmBlock], s_need[kLmBlock];
-    __shared__ uint32_t s_w[kLmPlanBlock / 64];
-    const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), g = tid / kLmLanes;
-    const uint64_t base = (uint64_t)blockIdx.x * kLmBlock;
-    const DevState& st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    __shared__ __attribute__((aligned(16))) uint16_t s_code[kMaxScanPatches * kLmBlock];   // then the records
+    __shared__ uint32_t s_w[kLmBlock / 64];
+    static_assert(sizeof(MergeJob) * kLmBlock <= sizeof(uint16_t) * kMaxScanPatches * kLmBlock, "records in s_code");
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * kLmBlock, i = base + tid;
+    const uint32_t nb = (uint32_t)(mp.n - base < kLmBlock ? mp.n - base : kLmBlock);     // particles of the block
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
     const bool gath = mp.fuse && ctl->gather;
-    const DevState& in = gath ? (ctl->base ? s1 : s0) : st;
-    if (tid < kLmBlock) {                     // whole waves: the source scan is wave-wide
-        const uint64_t i = base + tid;
-        const uint32_t src = lm_source(mp, i, gath);
-        s_src[tid] = src;
-        if (i < mp.n) mp.srcv[i] = src;
-    }
-    __syncthreads();
-    for (uint32_t j = g; j < kLmBlock; j += kLmPlanBlock / kLmLanes) {
-        const uint64_t i = base + j;
-        uint32_t need = 0;
-        if (i < mp.n) {                       // group-uniform
-            LmPart q;
-            lm_load(in, s_src[j], map, mp, mp.ref, q);
-            if (q.placed) {
-                uint32_t covered = 0, dropped = 0;
-                uint16_t code[kLmPerLane];
-                lm_group_codes(map, lm, mp, q, l, code, covered, dropped);
-                const int2 oc = lm.ctr[q.X];
-                const uint64_t gx = ((uint64_t)lm.tgen[q.X] << 32) | q.X;
-                int32_t lo = -1;
-                for (;;) {
-                    uint32_t cnt = 0, Lr = kLmNoList;
-                    for (; cnt < kLmList; ++cnt) {
-                        const uint32_t mn = lm_next_slot(code, lo);
-                        if (mn == kLmNoList) break;
-                        if (l == cnt) Lr = mn;
-                        lo = (int32_t)mn;
-                    }
-                    bool mine = true;
-                    if (l < cnt) {
-                        const uint32_t P = lm_page_of(lm, q.X, oc, q, Lr);
-                        mine = !q.shared && P != DM_LM_NONE && lm.owner[P] == gx;
-                    }
-                    need += grp_sum(mine ? 0u : 1u);
-                    if (cnt < kLmList || lm_next_slot(code, lo) == kLmNoList) break;
+    const DevState in = gath ? (ctl->base ? s1 : s0) : st;
+    const uint32_t src = lm_source(mp, i, gath);
+    uint32_t need = 0, covered = 0, dropped = 0;
+    MergeJob jb;
+    if (i < mp.n) {
+        LmPart q;
+        lm_load(in, src, map, mp, mp.ref, q);
+        jb.X = q.X;
+        jb.T = q.X;
+        jb.gT = 0;
+        jb.na = q.na;
+        jb.nb = q.nb;
+        jb.ox = jb.oy = DM_LM_UNSET;
+        jb.flags = 0;
+        jb.need = 0;
+        jb.z = q.z;
+        jb.zs = q.zs;
+        jb.src = src;
+#pragma unroll
+        for (uint32_t r = 0; r < kLmList; ++r) { jb.L[r] = 0; jb.P[r] = DM_LM_NONE; }
+        if (q.placed) {
+            uint16_t* codes = s_code + tid;
+            lm_codes(map, lm, mp, q, codes, covered, dropped);
+            const int2 oc = lm.ctr[q.X];
+            const uint32_t T = q.shared ? mp.frees[i] : q.X;
+            const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
+            uint32_t L[kLmList];
+            lm_collect(codes, mp.m, kLmNoList, L);
+            uint32_t nt = 0, bits = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < kLmList; ++r) {
+                if (L[r] == kLmNoList) continue;
+                const uint32_t P = lm_page_of(lm, q.X, oc, q, L[r]);
+                const bool mine = !q.shared && P != DM_LM_NONE && lm.owner[P] == gT;
+                bits |= mine ? 0u : 1u << r;
+                jb.L[r] = (uint16_t)L[r];
+                jb.P[r] = P;
+                ++nt;
+            }
+            need = __builtin_popcount(bits);
+            // later passes (a scan reaching more than kLmList tiles): counted here, resolved by the merge
+            bool more = false;
+            for (uint32_t t = L[kLmList - 1]; t != kLmNoList; t = L[kLmList - 1]) {
+                lm_collect(codes, mp.m, t, L);
+                if (L[0] == kLmNoList) break;
+                more = true;
+#pragma unroll
+                for (uint32_t r = 0; r < kLmList; ++r) {
+                    if (L[r] == kLmNoList) continue;
+                    const uint32_t P = lm_page_of(lm, q.X, oc, q, L[r]);
+                    need += (!q.shared && P != DM_LM_NONE && lm.owner[P] == gT) ? 0u : 1u;
                 }
             }
+            jb.T = T;
+            jb.gT = gT;
+            jb.ox = oc.x;
+            jb.oy = oc.y;
+            jb.need = bits;
+            jb.flags = kJobPlaced | (q.shared ? kJobShared : 0u) | (more ? kJobMore : 0u) | (nt << 8);
         }
-        if (l == 0) s_need[j] = need;
+    }
+    // the codes rows and the records leave through LDS, so every store is a whole 1-KiB line of
+    // the wave (a lane per particle storing its own 128-byte record wrote 64 lines partially)
+    __syncthreads();
+    uint4* rows = reinterpret_cast<uint4*>(mp.codes + base * kMaxScanPatches);
+    for (uint32_t c = tid; c < nb * (kMaxScanPatches / 8); c += kLmBlock) {
+        const uint32_t p = c / (kMaxScanPatches / 8), k0 = (c % (kMaxScanPatches / 8)) * 8;
+        if (k0 >= mp.m) continue;
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t a = k0 + 2 * j < mp.m ? s_code[(k0 + 2 * j) * kLmBlock + p] : kCodeSkip;
+            const uint32_t b = k0 + 2 * j + 1 < mp.m ? s_code[(k0 + 2 * j + 1) * kLmBlock + p] : kCodeSkip;
+            w[j] = a | (b << 16);
+        }
+        rows[c] = make_uint4(w[0], w[1], w[2], w[3]);
     }
     __syncthreads();
-    const uint32_t need = tid < kLmBlock ? s_need[tid] : 0u;
-    block_offsets(need, tid < kLmBlock && base + tid < mp.n, mp.off + base, mp.poff + blockIdx.x, s_w);
+    uint4* srec = reinterpret_cast<uint4*>(s_code);
+    if (i < mp.n) {
+        const uint4* r = reinterpret_cast<const uint4*>(&jb);
+#pragma unroll
+        for (uint32_t k = 0; k < sizeof(MergeJob) / 16; ++k) srec[tid * (sizeof(MergeJob) / 16) + k] = r[k];
+    }
+    __syncthreads();
+    uint4* jobs = reinterpret_cast<uint4*>(mp.job + base);
+    for (uint32_t c = tid; c < nb * (sizeof(MergeJob) / 16); c += kLmBlock) jobs[c] = srec[c];
+    covered = wave_sum_u32(covered);
+    dropped = wave_sum_u32(dropped);
+    if ((tid & 63u) == 0) {                   // the update's dropped / covered patches (k_merge_counts)
+        const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
+        if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
+        if (covered) atomicAdd((unsigned long long*)&mp.cnt[3 * kMergeCounterSlots + slot_c], (unsigned long long)covered);
+    }
+    block_offsets(need, i < mp.n, mp.off + (i - tid), mp.poff + blockIdx.x, s_w);
 }
 
-__global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
+// the page slot s of table X holds for the window centred at (na, nb) (lm_page_of)
+__device__ __forceinline__ uint32_t lm_page_at(const LocalMaps& lm, uint32_t X, int2 oc, int32_t na, int32_t nb, uint32_t s)
+{
+    const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
+    const int32_t a = lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx), b = lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by);
+    if (oc.x == DM_LM_UNSET || !lm_in(a, oc.x, lm.hx) || !lm_in(b, oc.y, lm.hy)) return DM_LM_NONE;
+    return lm.slot[(uint64_t)X * lm.S + s];
+}
+
+// the number of lower lanes of the 16-lane row holding the same code (c == 0xffffffff never
+// matches): DPP row shifts, the group's lanes all active
+template <int D>
+__device__ __forceinline__ uint32_t row_same(uint32_t c, uint32_t l)
+{
+    if constexpr (D >= (int)kLmLanes) {
+        return 0u;
+    } else {
+        const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)c, 0x110 + D, 0xf, 0xf, false);
+        return (o == c && l >= (uint32_t)D) ? 1u : 0u;     // l >= D: the lane D lower is in the group
+    }
+}
+__device__ __forceinline__ uint32_t row_rank(uint32_t c, uint32_t l)
+{
+    return row_same<1>(c, l) + row_same<2>(c, l) + row_same<3>(c, l) + row_same<4>(c, l) + row_same<5>(c, l) +
+           row_same<6>(c, l) + row_same<7>(c, l) + row_same<8>(c, l) + row_same<9>(c, l) + row_same<10>(c, l) +
+           row_same<11>(c, l) + row_same<12>(c, l) + row_same<13>(c, l) + row_same<14>(c, l) + row_same<15>(c, l);
+}
+
+// the staged pages of a wave: for stage page rr, chunk q (kLmChunk bytes) the groups' chunks
+// lie side by side (one 16-byte LDS-DMA per lane fills [rr][q] for the whole wave: 1 KiB)
+constexpr uint32_t kLmWaveStage = kLmStage * kLmNq * 1024;          // bytes per wave
+__device__ __forceinline__ uint32_t lm_stage_off(uint32_t rr, uint32_t ci, uint32_t g)
+{
+    constexpr uint32_t cpc = kLmChunk / 8;                           // cells per chunk
+    return (rr * kLmNq + ci / cpc) * 1024 + g * kLmChunk + (ci % cpc) * 8;
+}
+using lm_codes_t = typename std::conditional<kLmLanes == 16, uint2, uint4>::type;   // a lane's codes
+
+#define LM_MERGE_ATTR __attribute__((amdgpu_waves_per_eu(ESLAM_LM_WPE)))
+__global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
                                                              LocalMaps lm, MergeParams mp)
 {
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][kMaxScanPatches];
-    __shared__ uint4 s_page[kLmPpb][kLmStage][DM_LM_PAGE_CELLS / 2];                  // 16 KB
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
     __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
-    const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes;
+    const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
     const bool valid = i < mp.n;
     const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;      // by value: no private copy of the arguments
     // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
-    // output i reads its ancestor (srcv: k_map_plan found it) in state[base] and the merge
-    // writes the whole particle, its table name included, to st = state[base ^ 1]
+    // output i reads its ancestor (the plan's src) in state[base] and the merge writes the
+    // whole particle, its table name included, to st = state[base ^ 1]
     const bool gath = mp.fuse && ctl->gather;
     const DevState in = gath ? (ctl->base ? s1 : s0) : st;
-    const uint32_t src = valid ? (gath ? mp.srcv[i] : (uint32_t)i) : 0u;
+    // the plan's record, the codes and this particle's first page: one round trip
+    uint32_t X = 0, T = 0, flags = 0, needb = 0, src = 0, Lr = kLmNoList, Pr = DM_LM_NONE;
+    uint64_t gT = 0, alloc = 0;
+    int32_t na = 0, nb = 0, ox = 0, oy = 0;
+    double z = 0.0, zs = 0.0;
+    lm_codes_t c4 = {};
+    if (valid) {
+        const MergeJob* J = mp.job + i;
+        X = J->X; T = J->T; gT = J->gT;
+        na = J->na; nb = J->nb; ox = J->ox; oy = J->oy;
+        flags = J->flags; needb = J->need;
+        z = J->z; zs = J->zs; src = J->src;
+        if (l < kLmList) { Lr = J->L[l]; Pr = J->P[l]; }
+        c4 = reinterpret_cast<const lm_codes_t*>(mp.codes + i * kMaxScanPatches)[l];
+        alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
+    }
     if (gath && valid) {                      // the gather's copies: a field a lane
-        switch (l) {
+        for (uint32_t f = l; f < 10; f += kLmLanes) switch (f) {
         case 0: st.w[i] = in.w[src]; break;
         case 1: if (mp.aux) st.mprob[i] = in.mprob[src]; break;
         case 2: if (mp.aux) st.flags[i] = in.flags[src]; break;
@@ -1928,65 +2061,94 @@ __global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevSta
         }
     }
     bool dirty = false, moved = false;
-    uint32_t dropped = 0, covered = 0, written = 0, taken = 0;
-    LmPart q;
-    q.X = 0;
-    q.placed = false;
-    if (valid) lm_load(in, src, map, mp, mp.ref, q);
-    if (valid && q.placed) {                  // group-uniform from here on
-        // ---- 1. the cell codes of the lane's patches (k = l + kLmLanes u)
-        uint16_t code[kLmPerLane];
-        lm_group_codes(map, lm, mp, q, l, code, covered, dropped);
-#pragma unroll
-        for (uint32_t u = 0; u < kLmPerLane; ++u) s_code[pl][l + kLmLanes * u] = code[u];
+    uint32_t written = 0, taken = 0;
+    const bool shared = (flags & kJobShared) != 0;
+    if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
+        // ---- 1. the codes: patch k = l + kLmLanes u in lane l (round u precedes round u + 1 in
+        // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
+        reinterpret_cast<lm_codes_t*>(&s_code[pl][0])[l] = c4;
         wave_sync();
-        // each patch's rank: the earlier patches on its cell (eight codes a load, broadcast)
-        uint32_t rank[kLmPerLane] = {0, 0, 0, 0};
-        {
-            const uint4* c8 = reinterpret_cast<const uint4*>(&s_code[pl][0]);
-            for (uint32_t e0 = 0; e0 < mp.m; e0 += 8) {
-                const uint4 w = c8[e0 / 8];
-                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        uint32_t code[kLmPerLane], rank[kLmPerLane], maxr[kLmPerLane];
 #pragma unroll
-                for (uint32_t j = 0; j < 8; ++j) {
-                    const uint32_t c = (ws[j / 2] >> (16 * (j & 1))) & 0xffffu;
-                    const uint32_t e = e0 + j;
+        for (uint32_t u = 0; u < kLmPerLane; ++u) {
+            const uint32_t k = l + kLmLanes * u;
+            code[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
+            const uint32_t c = code[u] == kCodeSkip ? 0xfffffffeu - l : code[u];   // skips never match
+            rank[u] = row_rank(c, l);
+            maxr[u] = grp_max(code[u] == kCodeSkip ? 0u : rank[u]);
+        }
+        const int2 oc = make_int2(ox, oy);
+        const bool recentre = ox != na || oy != nb;
+        const bool rewrite = shared || (recentre && ox != DM_LM_UNSET);
+        uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
+        const uint32_t* xsl = lm.slot + (uint64_t)X * lm.S;
+        const uint32_t gshift = (tid & 63u) & ~(kLmLanes - 1u);
+        const double zvar = zs * zs;
+        uint8_t* stage = &s_stage[wv][0];
+        // stage: lane l moves bytes [16 l, 16 l + 16) of each chunk of the pages, straight into LDS
+        auto stage_pages = [&](const uint32_t (&Ls)[kLmStage], const uint32_t (&Ps)[kLmStage]) {
 #pragma unroll
-                    for (uint32_t u = 0; u < kLmPerLane; ++u)
-                        rank[u] += (c == code[u] && e < l + kLmLanes * u) ? 1u : 0u;
+            for (uint32_t rr = 0; rr < kLmStage; ++rr) {
+#pragma unroll
+                for (uint32_t h = 0; h < kLmNq; ++h) {
+                    uint8_t* dst = stage + (rr * kLmNq + h) * 1024;
+                    if (Ls[rr] != kLmNoList && Ps[rr] != DM_LM_NONE) {
+                        const uint8_t* srcp = reinterpret_cast<const uint8_t*>(lm.page + (uint64_t)Ps[rr] * DM_LM_PAGE_CELLS) +
+                                              h * kLmChunk + l * 16;
+                        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)srcp,
+                                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+                    } else {
+                        *reinterpret_cast<uint4*>(dst + (tid & 63u) * 16) =
+                            make_uint4(0u, __float_as_uint(-1.0f), 0u, __float_as_uint(-1.0f));
+                    }
                 }
             }
-        }
-        uint32_t maxrank = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < kLmPerLane; ++u) maxrank = code[u] != kCodeSkip ? max(maxrank, rank[u]) : maxrank;
-        maxrank = grp_max(maxrank);
-        // ---- 2. the first pass's tiles: lane r holds L[r], its page P and new page NP
-        const int2 oc = lm.ctr[q.X];
-        const bool recentre = oc.x != q.na || oc.y != q.nb;
-        const uint32_t T = q.shared ? mp.frees[i] : q.X;
-        const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
-        uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
-        const uint32_t* xsl = lm.slot + (uint64_t)q.X * lm.S;
-        uint64_t alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
-        const uint32_t gshift = (tid & 63u) & ~(kLmLanes - 1u);
-        const double zvar = q.zs * q.zs;
-        const bool rewrite = q.shared || (recentre && oc.x != DM_LM_UNSET);
+        };
+        uint32_t cnt = (flags >> 8) & 0xffu;
         int32_t lo = -1;
         for (uint32_t pass = 0;; ++pass) {
-            uint32_t Lr = kLmNoList, cnt = 0;
-            for (; cnt < kLmList; ++cnt) {
-                const uint32_t mn = lm_next_slot(code, lo);
-                if (mn == kLmNoList) break;
-                if (l == cnt) Lr = mn;
-                lo = (int32_t)mn;
-            }
-            const bool more = cnt == kLmList && lm_next_slot(code, lo) != kLmNoList;
-            uint32_t P = DM_LM_NONE, NP = DM_LM_NONE;
+            // lane r: tile r of the pass, its page P, whether it takes a new page NP
             bool need = false;
-            if (l < cnt) {
-                P = lm_page_of(lm, q.X, oc, q, Lr);
-                need = !(!q.shared && P != DM_LM_NONE && lm.owner[P] == gT);
+            uint32_t P = DM_LM_NONE, NP = DM_LM_NONE;
+            bool more;
+            if (pass == 0) {
+                if (l >= cnt) Lr = kLmNoList;
+                P = Pr;
+                need = l < cnt && ((needb >> l) & 1u);
+                more = (flags & kJobMore) != 0;
+                lo = cnt ? (int32_t)grp_get(Lr, cnt - 1) : -1;
+                // the first stage's pages are known from the record: their loads overlap the
+                // allocation and the table rewrite below
+                uint32_t Ls0[kLmStage], Ps0[kLmStage];
+#pragma unroll
+                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
+                    Ls0[rr] = grp_get(Lr, rr);
+                    Ps0[rr] = grp_get(P, rr);
+                }
+                stage_pages(Ls0, Ps0);
+            } else {
+                Lr = kLmNoList;
+                for (cnt = 0; cnt < kLmList; ++cnt) {
+                    uint32_t mn = kLmNoList;
+#pragma unroll
+                    for (uint32_t u = 0; u < kLmPerLane; ++u) {
+                        const uint32_t s = code[u] >> 6;
+                        if (code[u] != kCodeSkip && (int32_t)s > lo) mn = min(mn, s);
+                    }
+                    mn = grp_min(mn);
+                    if (mn == kLmNoList) break;
+                    if (l == cnt) Lr = mn;
+                    lo = (int32_t)mn;
+                }
+                uint32_t nx = kLmNoList;
+#pragma unroll
+                for (uint32_t u = 0; u < kLmPerLane; ++u)
+                    if (code[u] != kCodeSkip && (int32_t)(code[u] >> 6) > lo) nx = min(nx, code[u] >> 6);
+                more = cnt == kLmList && grp_min(nx) != kLmNoList;
+                if (l < cnt) {
+                    P = lm_page_at(lm, X, oc, na, nb, Lr);
+                    need = !(!shared && P != DM_LM_NONE && lm.owner[P] == gT);
+                }
             }
             const uint32_t gmask = (uint32_t)(__ballot(need) >> gshift) & ((1u << kLmLanes) - 1u);
             if (need) {
@@ -1996,7 +2158,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevSta
             }
             alloc += __builtin_popcount(gmask);
             if (pass == 0) {
-                // ---- 3. the table: X's slots rewritten into T (evictions; a copy when shared)
+                // ---- 2. the table: X's slots rewritten into T (evictions; a copy when shared)
                 // with this pass's new pages, else the new pages alone
                 if (rewrite) {
                     if (l < kLmList) {
@@ -2009,26 +2171,25 @@ __global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevSta
                         uint32_t v = v0;
                         if (recentre && v != DM_LM_NONE) {
                             const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
-                            const int32_t a = lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx);
-                            const int32_t b = lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by);
-                            if (!lm_in(a, q.na, lm.hx) || !lm_in(b, q.nb, lm.hy)) v = DM_LM_NONE;
+                            const int32_t a = lm_tile(sa, ox, lm.hx, lm.wx, lm.mx, lm.bx);
+                            const int32_t b = lm_tile(sb, oy, lm.hy, lm.wy, lm.my, lm.by);
+                            if (!lm_in(a, na, lm.hx) || !lm_in(b, nb, lm.hy)) v = DM_LM_NONE;
                         }
-#pragma unroll
-                        for (uint32_t r = 0; r < kLmList; ++r)
-                            if (r < cnt && s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) v = s_np[pl][2 * r + 1];
-                        if (q.shared || v != v0) tsl[s] = v;
+                        for (uint32_t r = 0; r < cnt; ++r)
+                            if (s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) v = s_np[pl][2 * r + 1];
+                        if (shared || v != v0) tsl[s] = v;
                     }
                 } else if (need) {
                     tsl[Lr] = NP;
                 }
-                if ((q.shared || recentre) && l == 0) lm.ctr[T] = make_int2(q.na, q.nb);
+                if ((shared || recentre) && l == 0) lm.ctr[T] = make_int2(na, nb);
                 dirty = recentre;
             } else if (need) {
                 // a later pass: T's slot may have been rewritten above (same wave; in order)
                 __builtin_amdgcn_s_waitcnt(0);
                 tsl[Lr] = NP;
             }
-            // ---- 4. the pass's pages, kLmStage at a time through LDS
+            // ---- 3. the pass's pages, kLmStage at a time through LDS
             for (uint32_t r0 = 0; r0 < cnt; r0 += kLmStage) {
                 uint32_t Ls[kLmStage], Ps[kLmStage], Ds[kLmStage];
 #pragma unroll
@@ -2038,74 +2199,61 @@ __global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevSta
                     const uint32_t npr = grp_get(NP, r0 + rr);
                     Ds[rr] = npr != DM_LM_NONE ? npr : Ps[rr];
                 }
-                uint4 v[kLmStage][2];
-#pragma unroll
-                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
-                    const uint4 e = make_uint4(0u, __float_as_uint(-1.0f), 0u, __float_as_uint(-1.0f));
-                    v[rr][0] = v[rr][1] = e;
-                    if (Ls[rr] != kLmNoList && Ps[rr] != DM_LM_NONE) {
-                        const uint4* pp = reinterpret_cast<const uint4*>(lm.page + (uint64_t)Ps[rr] * DM_LM_PAGE_CELLS);
-                        v[rr][0] = pp[2 * l];
-                        v[rr][1] = pp[2 * l + 1];
-                    }
+                if (pass != 0 || r0 != 0) {   // (pass 0's first stage was issued with the record)
+                    wave_sync();              // the previous stage's stores have read LDS
+                    stage_pages(Ls, Ps);
                 }
-                wave_sync();                  // the previous stage's stores read LDS before this one lands
-#pragma unroll
-                for (uint32_t rr = 0; rr < kLmStage; ++rr) {
-                    s_page[pl][rr][2 * l] = v[rr][0];
-                    s_page[pl][rr][2 * l + 1] = v[rr][1];
-                }
-                float2* cells = reinterpret_cast<float2*>(&s_page[pl][0][0]);
+                __builtin_amdgcn_s_waitcnt(0);
+                wave_sync();
                 uint32_t wbits = 0;           // bit rr: this lane wrote page rr
-                for (uint32_t rk = 0; rk <= maxrank; ++rk) {
-                    wave_sync();
 #pragma unroll
-                    for (uint32_t u = 0; u < kLmPerLane; ++u) {
-                        if (code[u] == kCodeSkip || rank[u] != rk) continue;
-                        const uint32_t sl = (uint32_t)code[u] >> 6, ci = (uint32_t)code[u] & 63u;
-                        uint32_t rr = kLmNoList;
+                for (uint32_t u = 0; u < kLmPerLane; ++u) {
+                    const uint32_t sl = code[u] >> 6, ci = code[u] & 63u;
+                    uint32_t rr = kLmNoList;
 #pragma unroll
-                        for (uint32_t w = 0; w < kLmStage; ++w) rr = Ls[w] == sl ? w : rr;
-                        if (rr == kLmNoList) continue;
-                        const float2 cv = cells[rr * DM_LM_PAGE_CELLS + ci];
-                        const ScanPatch sp = mp.sp[l + kLmLanes * u];
-                        const double wz = sp.z + q.z;
-                        const double var = sp.stdev * sp.stdev + zvar;
-                        float mo, so;
-                        if (dm_lm_holds(cv.y)) {
-                            if (!dm_lm_fuse(cv.x, cv.y, wz, var, &mo, &so)) continue;
-                        } else {
-                            mo = (float)wz;
-                            so = (float)dm_sqrt(var);
+                    for (uint32_t w = 0; w < kLmStage; ++w) rr = (code[u] != kCodeSkip && Ls[w] == sl) ? w : rr;
+                    for (uint32_t rk = 0; rk <= maxr[u]; ++rk) {
+                        if (rr != kLmNoList && rank[u] == rk) {
+                            float2* cp = reinterpret_cast<float2*>(stage + lm_stage_off(rr, ci, g));
+                            const float2 cv = *cp;
+                            const ScanPatch sp = mp.sp[l + kLmLanes * u];
+                            const double wz = sp.z + z;
+                            const double var = sp.stdev * sp.stdev + zvar;
+                            float mo = cv.x, so = cv.y;
+                            bool w = true;
+                            if (dm_lm_holds(cv.y)) w = dm_lm_fuse(cv.x, cv.y, wz, var, &mo, &so);
+                            else { mo = (float)wz; so = (float)dm_sqrt(var); }
+                            if (w) {
+                                *cp = make_float2(mo, so);
+                                wbits |= 1u << rr;
+                                ++written;
+                            }
                         }
-                        cells[rr * DM_LM_PAGE_CELLS + ci] = make_float2(mo, so);
-                        wbits |= 1u << rr;
-                        ++written;
+                        wave_sync();
                     }
                 }
                 wbits = grp_or(wbits);
-                wave_sync();
                 // a page goes back whole when the patches changed it, or when it is new
 #pragma unroll
                 for (uint32_t rr = 0; rr < kLmStage; ++rr) {
                     if (Ls[rr] == kLmNoList || (Ds[rr] == Ps[rr] && !((wbits >> rr) & 1u))) continue;
                     uint4* dp = reinterpret_cast<uint4*>(lm.page + (uint64_t)Ds[rr] * DM_LM_PAGE_CELLS);
-                    dp[2 * l] = s_page[pl][rr][2 * l];
-                    dp[2 * l + 1] = s_page[pl][rr][2 * l + 1];
+#pragma unroll
+                    for (uint32_t h = 0; h < kLmNq; ++h)
+                        dp[kLmLanes * h + l] = *reinterpret_cast<const uint4*>(stage + (rr * kLmNq + h) * 1024 + (tid & 63u) * 16);
                 }
                 dirty = dirty || wbits != 0;
             }
             if (!more) break;
         }
-        if (q.shared && dirty) moved = true;
-        if ((gath || moved) && l == 0) st.sid[i] = moved ? T : q.X;
+        if (shared && dirty) moved = true;
+        if ((gath || moved) && l == 0) st.sid[i] = moved ? T : X;
     } else if (valid && gath && l == 0) {
-        st.sid[i] = q.X;
+        st.sid[i] = X;
     }
-    // the counters: particles once (the group's lane 0), patches from every lane
+    // the counters: particles once (the group's lane 0), cell writes and pages from every lane
+    // (the plan counted the dropped and covered patches)
     const bool lead = l == 0;
-    dropped = wave_sum_u32(dropped);
-    covered = wave_sum_u32(covered);
     written = wave_sum_u32(written);
     taken = wave_sum_u32(taken);
     const uint64_t dmask = __ballot(lead && dirty), mmask = __ballot(lead && moved);
@@ -2113,10 +2261,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) k_map_merge(DevState s0, DevSta
         const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmMergeBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
         if (written) atomicAdd((unsigned long long*)&mp.cnt[4 * kMergeCounterSlots + slot_c], (unsigned long long)written);
         if (taken) atomicAdd((unsigned long long*)&mp.cnt[5 * kMergeCounterSlots + slot_c], (unsigned long long)taken);
-        if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
         if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
-        if (covered) atomicAdd((unsigned long long*)&mp.cnt[3 * kMergeCounterSlots + slot_c], (unsigned long long)covered);
     }
 }
 
@@ -3684,7 +3830,7 @@ extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, 
     const uint32_t nb = (uint32_t)((mp->n + kLmBlock - 1) / kLmBlock);
     e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
     if (e != hipSuccess) return e;
-    if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmPlanBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     return page_budget(ctl, lm, mp, nb, pgc, stream);
 }
 
