@@ -197,24 +197,77 @@ def cpu_baseline(args, grid, flags=0, scan=None):
     return out
 
 
-def gpu_clocks():
-    """The current shader and memory clock of every GPU as the driver reports them (sysfs
-    pp_dpm_sclk / pp_dpm_mclk, the line marked '*'): box-to-box clock differences show here."""
+def gpu_card(device):
+    """The sysfs node of the GPU this process runs on, matched by the PCI address the HIP
+    runtime (the one libeslam_gpu already loaded) reports for it; None if not found."""
+    import ctypes as C
     import glob
-    out = []
+    try:
+        hip = C.CDLL("libamdhip64.so", mode=C.RTLD_GLOBAL)
+        buf = C.create_string_buffer(64)
+        rc = hip.hipDeviceGetPCIBusId(buf, 64, int(device))
+        if rc != 0:
+            raise RuntimeError(f"hipDeviceGetPCIBusId returned {rc}")
+        want = buf.value.decode().lower()
+    except Exception as e:                 # noqa: BLE001 -- a report field, never fatal
+        sys.stderr.write(f"bench.py: no PCI address for the clock report ({e})\n")
+        return None
     for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
-        rec = {}
-        for name in ("pp_dpm_sclk", "pp_dpm_mclk"):
-            try:
-                with open(os.path.join(dev, name)) as fh:
-                    cur = [ln.split(":", 1)[1].strip().rstrip("*").strip() for ln in fh if ln.rstrip().endswith("*")]
-                if cur:
-                    rec[name[7:]] = cur[0]
-            except OSError:
-                pass
-        if rec:
-            out.append(rec)
-    return out or None
+        if os.path.basename(os.path.realpath(dev)).lower() == want:
+            return dev
+    sys.stderr.write(f"bench.py: no sysfs card at PCI {want} for the clock report\n")
+    return None
+
+
+def _dpm_mhz(dev, name):
+    """the level marked '*' in sysfs pp_dpm_sclk / pp_dpm_mclk, in MHz (None if unreadable)"""
+    try:
+        with open(os.path.join(dev, name)) as fh:
+            for ln in fh:
+                if ln.rstrip().endswith("*"):
+                    return int("".join(c for c in ln.split(":", 1)[1] if c.isdigit()))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+class ClockSampler:
+    """The shader clock of this process's GPU sampled every 2 ms while the timed region runs
+    (sysfs, no HIP call): a box whose card ran below its peak clock shows it here."""
+
+    def __init__(self, device):
+        import threading
+        self.dev = gpu_card(device)
+        self.sclk = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True) if self.dev else None
+
+    def _run(self):
+        while not self._stop.is_set():
+            v = _dpm_mhz(self.dev, "pp_dpm_sclk")
+            if v is not None:
+                self.sclk.append(v)
+            self._stop.wait(0.002)
+
+    def __enter__(self):
+        if self._t:
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t:
+            self._t.join()
+
+    def report(self):
+        if not self.dev:
+            return None
+        s = sorted(self.sclk)
+        return {"card": os.path.basename(os.path.dirname(self.dev)) if self.dev.endswith("/device") else self.dev,
+                "pci": os.path.basename(os.path.realpath(self.dev)),
+                "sclk_mhz_timed": {"samples": len(s), "min": s[0] if s else None, "median": s[len(s) // 2] if s else None,
+                                   "max": s[-1] if s else None},
+                "mclk_mhz": _dpm_mhz(self.dev, "pp_dpm_mclk")}
 
 
 def visible_gpus():
@@ -393,13 +446,15 @@ def main():
     barrier()
     # timed region: K steps back to back, no per-kernel events (HIP event records between
     # the launches cost ~10 % of a step here)
-    t0 = time.perf_counter()
-    for st in stream[args.warmup:args.warmup + args.steps]:
-        f_step(st)
-    t_enq = time.perf_counter()             # the host has queued every launch (nothing waits on the GPU)
-    info = f.sync()
-    barrier()
-    dt = time.perf_counter() - t0
+    clocks = ClockSampler(local_rank if dist is not None else 0)
+    with clocks:
+        t0 = time.perf_counter()
+        for st in stream[args.warmup:args.warmup + args.steps]:
+            f_step(st)
+        t_enq = time.perf_counter()         # the host has queued every launch (nothing waits on the GPU)
+        info = f.sync()
+        barrier()
+        dt = time.perf_counter() - t0
     # kernel breakdown: the next K steps of the same stream with HIP events around every
     # launch, on the context's stream (eslam_gpu_enable_timing)
     f.enable_timing(True)
@@ -451,7 +506,7 @@ def main():
         "dtype_note": "all particle state, weights, sums and map values' arithmetic in fp64 (map cells stored as "
                       "fp32); the project step's Box-Muller radius and angle are IEEE fp32 (DESIGN.md 2), the "
                       "oracle computing the same fp32 operations",
-        "clocks": gpu_clocks(),
+        "clocks": clocks.report(),
         "data": "synthetic (%s %gx%g m MLS map @0.1 m; odometry + 4 foot contacts per step%s)"
                 % ("rough multi-patch" if args.rough else "flat", args.map_cells / 10, args.map_cells / 10,
                    "; unmapped beyond x = 0.3 m, a %d-patch scan merged into every particle's map per step"
