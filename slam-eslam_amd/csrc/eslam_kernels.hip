@@ -2022,6 +2022,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][kMaxScanPatches];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
     __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
+    __shared__ uint8_t s_list[kLmPpb][kMaxScanPatches];                                // a stage's patches, in scan order
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
@@ -2071,14 +2072,11 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
         reinterpret_cast<lm_codes_t*>(&s_code[pl][0])[l] = c4;
         wave_sync();
-        uint32_t code[kLmPerLane], rank[kLmPerLane], maxr[kLmPerLane];
+        uint32_t code[kLmPerLane];
 #pragma unroll
         for (uint32_t u = 0; u < kLmPerLane; ++u) {
             const uint32_t k = l + kLmLanes * u;
             code[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
-            const uint32_t c = code[u] == kCodeSkip ? 0xfffffffeu - l : code[u];   // skips never match
-            rank[u] = row_rank(c, l);
-            maxr[u] = grp_max(code[u] == kCodeSkip ? 0u : rank[u]);
         }
         const int2 oc = make_int2(ox, oy);
         const bool recentre = ox != na || oy != nb;
@@ -2168,19 +2166,30 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                         s_np[pl][2 * l] = Lr;
                         s_np[pl][2 * l + 1] = NP;
                     }
+                    // the window's columns and rows whose tiles leave it (bit sa / sb), the pass's
+                    // slot range (only slots inside it can take a new page)
+                    uint32_t colx = 0, rowx = 0;
+                    if (recentre && ox != DM_LM_UNSET) {
+                        for (uint32_t s = l; s < lm.wx; s += kLmLanes)
+                            colx |= lm_in(lm_tile(s, ox, lm.hx, lm.wx, lm.mx, lm.bx), na, lm.hx) ? 0u : 1u << s;
+                        for (uint32_t s = l; s < lm.wy; s += kLmLanes)
+                            rowx |= lm_in(lm_tile(s, oy, lm.hy, lm.wy, lm.my, lm.by), nb, lm.hy) ? 0u : 1u << s;
+                        colx = grp_or(colx);
+                        rowx = grp_or(rowx);
+                    }
+                    const uint32_t lmin = cnt ? grp_get(Lr, 0) : 1u, lmax = cnt ? grp_get(Lr, cnt - 1) : 0u;
                     wave_sync();
+                    uint32_t sb = lm_div(l, lm.mx), sa = l - lm.wx * sb;
                     for (uint32_t s = l; s < lm.S; s += kLmLanes) {
                         const uint32_t v0 = xsl[s];
                         uint32_t v = v0;
-                        if (recentre && v != DM_LM_NONE) {
-                            const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
-                            const int32_t a = lm_tile(sa, ox, lm.hx, lm.wx, lm.mx, lm.bx);
-                            const int32_t b = lm_tile(sb, oy, lm.hy, lm.wy, lm.my, lm.by);
-                            if (!lm_in(a, na, lm.hx) || !lm_in(b, nb, lm.hy)) v = DM_LM_NONE;
-                        }
-                        for (uint32_t r = 0; r < cnt; ++r)
-                            if (s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) v = s_np[pl][2 * r + 1];
+                        if (((colx >> sa) | (rowx >> sb)) & 1u) v = DM_LM_NONE;
+                        if (s >= lmin && s <= lmax)
+                            for (uint32_t r = 0; r < cnt; ++r)
+                                if (s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) v = s_np[pl][2 * r + 1];
                         if (shared || v != v0) tsl[s] = v;
+                        sa += kLmLanes;               // the next slot's column and row
+                        while (sa >= lm.wx) { sa -= lm.wx; ++sb; }
                     }
                 } else if (need) {
                     tsl[Lr] = NP;
@@ -2209,17 +2218,35 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 __builtin_amdgcn_s_waitcnt(0);
                 wave_sync();
                 uint32_t wbits = 0;           // bit rr: this lane wrote page rr
+                // the stage's patches listed in scan order (k = l + kLmLanes u is u-major), then
+                // applied kLmLanes at a time: a round's lanes on one cell go by rank (DPP row
+                // compare), rounds in order -- every cell sees its patches in scan order
+                uint32_t nst = 0;
 #pragma unroll
                 for (uint32_t u = 0; u < kLmPerLane; ++u) {
-                    const uint32_t sl = code[u] >> 6, ci = code[u] & 63u;
-                    uint32_t rr = kLmNoList;
+                    bool in = false;
 #pragma unroll
-                    for (uint32_t w = 0; w < kLmStage; ++w) rr = (code[u] != kCodeSkip && Ls[w] == sl) ? w : rr;
-                    for (uint32_t rk = 0; rk <= maxr[u]; ++rk) {
-                        if (rr != kLmNoList && rank[u] == rk) {
+                    for (uint32_t w = 0; w < kLmStage; ++w) in |= code[u] != kCodeSkip && Ls[w] == (code[u] >> 6);
+                    const uint32_t gm = (uint32_t)(__ballot(in) >> gshift) & ((1u << kLmLanes) - 1u);
+                    if (in) s_list[pl][nst + __builtin_popcount(gm & ((1u << l) - 1u))] = (uint8_t)(l + kLmLanes * u);
+                    nst += __builtin_popcount(gm);
+                }
+                wave_sync();
+                for (uint32_t j0 = 0; j0 < nst; j0 += kLmLanes) {
+                    const bool act = j0 + l < nst;
+                    const uint32_t k = act ? s_list[pl][j0 + l] : 0u;
+                    const uint32_t c = act ? (uint32_t)s_code[pl][k] : 0xfffffffeu - l;   // idle lanes never match
+                    const uint32_t rank = row_rank(c, l);
+                    const uint32_t maxr = grp_max(act ? rank : 0u);
+                    uint32_t rr = 0;
+#pragma unroll
+                    for (uint32_t w = 0; w < kLmStage; ++w) rr = Ls[w] == (c >> 6) ? w : rr;
+                    const uint32_t ci = c & 63u;
+                    for (uint32_t rk = 0; rk <= maxr; ++rk) {
+                        if (act && rank == rk) {
                             float2* cp = reinterpret_cast<float2*>(stage + lm_stage_off(rr, ci, g));
                             const float2 cv = *cp;
-                            const ScanPatch sp = mp.sp[l + kLmLanes * u];
+                            const ScanPatch sp = mp.sp[k];
                             const double wz = sp.z + z;
                             const double var = sp.stdev * sp.stdev + zvar;
                             float mo = cv.x, so = cv.y;
