@@ -1703,24 +1703,27 @@ DM_FN uint32_t dm_store_hash(uint32_t cell) { return (cell * 2654435761u) >> 27;
 
 #define DM_NBUCKETS 6            /* cpoints.size() buckets 0,1,2,3,4,>=5 (phase B)     */
 
-/* J = the largest power of two <= min(8, n_global / 2^18): from 256k particles on there are
- * ~4096 chunks of 64 x J up to 2M, and 8 rows per chunk beyond (the weighting kernel runs one
- * chunk per wave; 4096 waves fill the 256 CUs x 4 waves per SIMD once).  Measured on MI355X
- * (interleaved A/B against 2^19 and a cap of 16): 1M +6.5 %, 2M +3 %, 4M unchanged per step;
- * the cap of 8 keeps a sharded rank at 4096 waves per GPU (configs[3]: 16M over 8 GPUs, 2M
- * per GPU), where 16 rows would leave 2 waves per SIMD.                                   */
-#ifndef ESLAM_CHUNK_UNIT                 /* experiment builds only (changes the sum order) */
-#define ESLAM_CHUNK_UNIT 262144u
+/* J: rows of 64 particles per canonical summation chunk (the weighting kernel runs one chunk
+ * per wave).  The chunks are sized to whole generations of the kernel's resident waves on an
+ * MI355X (256 CUs x 4 SIMDs x 5 waves = ESLAM_CHUNK_WAVES): G = the generations needed at
+ * <= ESLAM_CHUNK_CAP rows, J = ceil(rows / (G x waves)).  4M particles: 13 rows, 5042 chunks
+ * in one generation (power-of-two rows left 8192 chunks, 1.6 generations: the second 60 %
+ * full); 2M: 7 rows; up to 327 680 particles one row.  Measured (interleaved A/B,
+ * profiles/r05/ab_chunk_rows.log): K1 167 -> 160 us at 4M, 96 -> 91 us at 2M.  Part of the sum
+ * contract (the oracle uses the same function); ESLAM_CHUNK_CAP also bounds the packed wave
+ * counts (64 J ESLAM_MAX_CONTACTS < 2^16).                                                 */
+#ifndef ESLAM_CHUNK_WAVES                /* experiment builds only (changes the sum order) */
+#define ESLAM_CHUNK_WAVES 5120u
 #endif
 #ifndef ESLAM_CHUNK_CAP
-#define ESLAM_CHUNK_CAP 8u
+#define ESLAM_CHUNK_CAP 13u
 #endif
 DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
 {
-    uint64_t q = n_global / ESLAM_CHUNK_UNIT;
-    uint32_t j = 1;
-    while (j < ESLAM_CHUNK_CAP && (uint64_t)(j * 2u) <= q) j *= 2u;
-    return j;
+    const uint64_t rows = (n_global + 63) / 64, per = (uint64_t)ESLAM_CHUNK_WAVES * ESLAM_CHUNK_CAP;
+    const uint64_t slots = (rows <= per ? 1 : (rows + per - 1) / per) * (uint64_t)ESLAM_CHUNK_WAVES;
+    const uint64_t j = (rows + slots - 1) / slots;
+    return j < 1 ? 1u : (uint32_t)j;
 }
 
 /* exponent e >= 1 with max_w < 2^e (weight scale of the A_n / B_n accumulators) */

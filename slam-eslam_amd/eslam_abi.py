@@ -222,13 +222,16 @@ class Comm(C.Structure):
 MAX_RANKS = 16
 
 
+CHUNK_WAVES, CHUNK_CAP = 5120, 13
+
+
 def chunk_rows(n_global):
-    """dm_chunk_rows (include/eslam_detmath.h): rows of 64 lanes per canonical summation chunk."""
-    q = n_global // 262144
-    j = 1
-    while j < 8 and j * 2 <= q:
-        j *= 2
-    return j
+    """dm_chunk_rows (include/eslam_detmath.h): rows of 64 lanes per canonical summation chunk,
+    sized to whole generations of the weighting kernel's resident waves."""
+    rows = (n_global + 63) // 64
+    per = CHUNK_WAVES * CHUNK_CAP
+    slots = (1 if rows <= per else -(-rows // per)) * CHUNK_WAVES
+    return max(1, -(-rows // slots))
 
 
 def shard_bounds(n_global, nranks):
