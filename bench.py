@@ -86,15 +86,17 @@ def parse():
     return ap.parse_args()
 
 
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r04", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r05", "summary.json")
+PROFILE_SUMMARIES = {"local-maps": os.path.join(ROOT, "profiles", "r05", "summary_local_maps.json")}
 
 
 def pmc_traffic(kernel, n, map_cells, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (tools/profile.sh -> profiles/<round>/summary.json: FETCH_SIZE x2 + WRITE_SIZE, the
     gfx950 correction of MI355X_MICROARCH.md), when they were taken on this workload."""
+    path = PROFILE_SUMMARIES.get(workload, PROFILE_SUMMARY)
     try:
-        with open(PROFILE_SUMMARY) as fh:
+        with open(path) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
         return None
@@ -103,7 +105,7 @@ def pmc_traffic(kernel, n, map_cells, workload):
     for name, e in d.get("kernels", {}).items():
         if name.startswith(kernel) and "hbm_bytes_per_dispatch" in e:
             out = {"bytes_per_launch": round(e["hbm_bytes_per_dispatch"]), "fetch_bytes": round(e["fetch_size_bytes"]),
-                   "write_bytes": round(e["write_size_bytes"]), "source": os.path.relpath(PROFILE_SUMMARY, ROOT)}
+                   "write_bytes": round(e["write_size_bytes"]), "source": os.path.relpath(path, ROOT)}
             # what actually bounds the kernel: the VALU (rocprofv3 derived metrics, same run)
             if "valubusy_pct" in e:
                 out["valu_busy_pct"] = round(e["valubusy_pct"], 1)
