@@ -256,7 +256,10 @@ typedef struct eslam_scan_patch {
     double position[3];                    /* yaw-free body frame (the scan MLS's cells)    */
     double stdev;                          /* sensor sigma of the patch                      */
 } eslam_scan_patch;
-int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);   /* count <= 64 */
+/* Any count: a scan of more than 64 patches merges 64 at a time, in order (every cell sees
+ * its patches in the scan's order); the update's counters add up over the parts
+ * (map_stores_changed counts a map once per part that changed it).                          */
+int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);
 /* PoseEstimator::setEnvironment(env, map, useShared)  src/PoseEstimator.cpp:49-62: on = 1
  * gives every particle its own map (ESLAM_FLAG_PARTICLE_MAPS), 0 the shared map only.  Before
  * the particles are initialised (ESLAM_ERR_INVALID_ARG after).  On a sharded filter a

@@ -2023,7 +2023,7 @@ static int cmp_u64(const void* a, const void* b)
     return x < y ? -1 : x > y;
 }
 
-int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
+static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 {
     if (!(f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS)) return ESLAM_ERR_INVALID_ARG;
     if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
@@ -2186,10 +2186,24 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     free(shared);
     free(dirt);
     if (oom) return ESLAM_ERR_OUT_OF_MEMORY;
-    f->info.map_patches_dropped = dropped;
-    f->info.map_stores_changed = changed;
-    f->info.map_stores_copied = copied;
-    f->info.map_patches_covered = covered;
+    f->info.map_patches_dropped += dropped;
+    f->info.map_stores_changed += changed;
+    f->info.map_stores_copied += copied;
+    f->info.map_patches_covered += covered;
+    return 0;
+}
+
+/* processMap's merge of a whole scan: 64 patches at a time, in order (the GPU's parts,
+ * eslam_gpu_map_update); every cell sees its patches in the scan's order, the counters add up */
+#define OR_SCAN_PART 64u
+int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
+{
+    f->info.map_patches_dropped = f->info.map_stores_changed = 0;
+    f->info.map_stores_copied = f->info.map_patches_covered = 0;
+    for (uint32_t c0 = 0; c0 == 0 || c0 < m; c0 += OR_SCAN_PART) {
+        const int rc = or_map_update_part(f, sp + c0, m - c0 < OR_SCAN_PART ? m - c0 : OR_SCAN_PART);
+        if (rc) return rc;
+    }
     return 0;
 }
 

@@ -1701,7 +1701,6 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
     if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update needs per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
-    if (count > (uint32_t)kMaxScanPatches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_update: more than 64 scan patches");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
     if (const int rc_ = check_poisoned(ctx)) return rc_;
     if (!ctx->lm_ready) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "per-particle maps not allocated");
@@ -1721,24 +1720,34 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
         if (rc) return rc;
     }
     mrec(ctx, 1);
-    const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
-    const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
-    HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, fuse ? &gv : nullptr, ctx->lm.tgen, ctx->stream));
-    mrec(ctx, 2);
-    MergeParams mp = merge_params(ctx, cs);
-    mp.is_id = ctx->map.g2l_identity;
-    mp.gv = gv;
-    mp.gbase = ctx->gbase;
-    mp.fuse = fuse ? 1u : 0u;
-    mp.aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
-    mp.m = count;
-    for (uint32_t k = 0; k < count; ++k)
-        mp.sp[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
-    HIPCHK(ctx, eslam_launch_map_plan(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->lm_pgc, ctx->stream));
-    mrec(ctx, 3);
-    HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
-    if (fuse) {
-        HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));     // the gather's buffer flip, if one ran
+    // a scan of more than kMaxScanPatches patches merges kMaxScanPatches at a time, in order:
+    // every cell sees its patches in the scan's order; the parts' counters add up
+    // (map_stores_changed counts a map once per part that changed it)
+    for (uint32_t c0 = 0; c0 == 0 || c0 < count; c0 += (uint32_t)kMaxScanPatches) {
+        const uint32_t cm = count - c0 < (uint32_t)kMaxScanPatches ? count - c0 : (uint32_t)kMaxScanPatches;
+        const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
+        const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
+        HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, fuse ? &gv : nullptr, ctx->lm.tgen,
+                                            ctx->stream));
+        if (!c0) mrec(ctx, 2);
+        MergeParams mp = merge_params(ctx, cs);
+        mp.is_id = ctx->map.g2l_identity;
+        mp.gv = gv;                           // (the first part runs a pending gather; the device knows)
+        mp.gbase = ctx->gbase;
+        mp.fuse = fuse ? 1u : 0u;
+        mp.aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
+        mp.acc = c0 ? 1u : 0u;
+        mp.m = cm;
+        for (uint32_t k = 0; k < cm; ++k) {
+            const eslam_scan_patch& s = patches[c0 + k];
+            mp.sp[k] = ScanPatch{s.position[0], s.position[1], s.position[2], s.stdev};
+        }
+        HIPCHK(ctx, eslam_launch_map_plan(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->lm_pgc, ctx->stream));
+        if (!c0) mrec(ctx, 3);
+        HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
+        if (fuse) {
+            HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));     // the gather's buffer flip, if one ran
+        }
     }
     mrec(ctx, 4);
     return ESLAM_OK;

@@ -344,6 +344,7 @@ struct MergeParams {
     GatherView gv;                       // fuse: a pending resample gather runs in the merge (one GPU)
     uint64_t gbase;
     uint32_t fuse, aux;                  // aux: carry mprob / flags (ESLAM_FLAG_NO_AUX_GATHER unset)
+    uint32_t acc, pad2;                  // acc: add this merge's counters to the update's (a later 64-patch part)
     ScanPatch sp[kMaxScanPatches];
 };
 

@@ -2298,7 +2298,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 
 // the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads); the free
 // list's cursor moves past this update's plan
-__global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl)
+__global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl,
+                                                                      uint32_t acc)
 {
     __shared__ uint64_t s[kMergeCounters][kMergeCounterSlots / 64];
     const uint32_t t = threadIdx.x;
@@ -2312,12 +2313,14 @@ __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint6
         uint64_t r[kMergeCounters] = {0, 0, 0, 0, 0, 0};
         for (uint32_t g = 0; g < kMergeCounters; ++g)
             for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) r[g] += s[g][w];
-        ctl->map_dropped = r[0];
-        ctl->map_changed = r[1];
-        ctl->map_copied = r[2];
-        ctl->map_covered = r[3];
-        ctl->map_written = r[4];
-        ctl->map_taken = r[5];
+        // acc: a later part of a scan merged 64 patches at a time (eslam_gpu_map_update) adds
+        if (acc) {
+            ctl->map_dropped += r[0]; ctl->map_changed += r[1]; ctl->map_copied += r[2];
+            ctl->map_covered += r[3]; ctl->map_written += r[4]; ctl->map_taken += r[5];
+        } else {
+            ctl->map_dropped = r[0]; ctl->map_changed = r[1]; ctl->map_copied = r[2];
+            ctl->map_covered = r[3]; ctl->map_written = r[4]; ctl->map_taken = r[5];
+        }
         if (!(ctl->err & kFaultPages)) ctl->pg_cursor += ctl->pg_total;
     }
 }
@@ -3869,7 +3872,7 @@ extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl,
 {
     const uint32_t nb = (uint32_t)((mp->n + kLmPpb - 1) / kLmPpb);
     if (nb) hipLaunchKernelGGL(k_map_merge, dim3(nb), dim3(kLmMergeBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
-    hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl);
+    hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl, mp->acc);
     return hipGetLastError();
 }
 

@@ -246,3 +246,58 @@ def test_particle_maps_config4_shard_size(gpu_mod, oracle, kind):
     idx = sorted(set(np.linspace(0, n - 1, 38).astype(np.int64).tolist() + [1, n // 2 + 1]))
     assert_maps_equal(gpu, orc, idx, "8M")
     gpu.close()
+
+
+def rotated(grid, yaw=0.3, tx=0.4, ty=-0.25):
+    """the grid in a local frame rotated by yaw and shifted: global2local = Rz(-yaw) (p - t)"""
+    import math
+    c, s = math.cos(yaw), math.sin(yaw)
+    grid.g2l = [c, s, 0.0, -(c * tx + s * ty), -s, c, 0.0, -(-s * tx + c * ty), 0.0, 0.0, 1.0, 0.0]
+    return grid
+
+
+@pytest.mark.parametrize("case", ["wide_scan", "rotated_grid", "small_window", "large_window"])
+def test_particle_maps_shapes(gpu_mod, oracle, case):
+    """The window's other shapes against the oracle, bit for bit: a scan reaching more tiles than
+    one merge pass holds (kLmList = 8: the plan's and the merge's later passes) and past the
+    window (dropped patches); a grid whose global2local is not the identity (every cell placed
+    through the transform, in the plan, the merge and K1's lookups); a 5 x 5-tile window
+    (maxSensorRange 1 m) and a 27 x 27-tile one (10 m, reaching past the grid's edges)."""
+    n = 1500
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
+    grid = S.unmapped_beyond(S.rough_map(cells=120), 0.3)
+    scan = S.scan_patches()
+    if case == "wide_scan":
+        scan = S.scan_patches(nx=16, ny=12, x0=-2.6, x1=4.6, y0=-2.5, y1=2.4)   # 192 patches: three parts of 64
+        cfg.local_map_pages = 128            # ~50 tiles a particle and its copies' pages
+    elif case == "rotated_grid":
+        grid = rotated(grid)
+    elif case == "small_window":
+        cfg.max_sensor_range = 1.0
+        scan = S.scan_patches(nx=10, ny=8, x0=-0.8, x1=1.9, y0=-1.2, y1=1.0)
+    else:
+        cfg.max_sensor_range = 10.0
+        scan = S.scan_patches(nx=12, ny=10, x0=-5.0, x1=5.5, y0=-4.0, y1=4.0)
+        cfg.local_map_pages = 256            # up to 120 tiles a particle
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.05], 0.18, 0.05)
+    dropped = written = 0
+    for k, st in enumerate(S.step_stream(12, tilt=True)):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+        gi = gpu.sync()
+        assert_bit_identical(gpu.download(), orc.download(), f"{case} step {k}")
+        assert map_info(gi) == map_info(orc.info()), (case, k, map_info(gi), map_info(orc.info()))
+        dropped += gi.map_patches_dropped
+        written += gi.map_cells_written
+    assert_maps_equal(gpu, orc, list(range(0, n, 97)) + [n - 1], case)
+    assert written > 0
+    if case in ("wide_scan", "small_window"):
+        assert dropped > 0                   # the scan reaches past the window
+    else:
+        assert dropped == 0

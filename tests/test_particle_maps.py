@@ -10,6 +10,7 @@ from fractions import Fraction
 import math
 
 import numpy as np
+import pytest
 
 import eslam_abi as A
 import oracle_ffi as O
@@ -168,10 +169,12 @@ def _model_update(maps, p, scan, grid, sincos):
     return drop
 
 
-def test_window_model(oracle):
-    """The oracle's map update against the Python window model, cell for cell, over 40 steps
-    of the bench stream (with its resample copies) on the empty prior and with a scan wide
-    enough to reach past the window."""
+@pytest.mark.parametrize("nx,ny,steps", [(10, 5, 40), (13, 10, 16)])
+def test_window_model(oracle, nx, ny, steps):
+    """The oracle's map update against the Python window model, cell for cell, over the bench
+    stream (with its resample copies) on the empty prior and with a scan wide enough to reach
+    past the window; the 130-patch scan is merged in parts of 64 (eslam_gpu_map_update), the
+    model takes it whole."""
     n = 12
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
@@ -179,10 +182,10 @@ def test_window_model(oracle):
     f = O.OracleFilter(cfg, O.SUM_CONTRACT)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.3, 0.3, 0.2], 0.18, 0.05)
-    scan = S.scan_patches(nx=10, ny=5, x0=-0.5, x1=4.2, y0=-1.5, y1=1.0)
+    scan = S.scan_patches(nx=nx, ny=ny, x0=-0.5, x1=4.2, y0=-1.5, y1=1.0)
     sincos = lambda th: (O.dm(2, th), O.dm(3, th))
     maps = [(None, {}) for _ in range(n)]
-    for k, st in enumerate(S.step_stream(40, dx=0.05)):
+    for k, st in enumerate(S.step_stream(steps, dx=0.05)):
         f.step(st)
         anc = f.ancestors().astype(np.int64) if f.info().resampled else np.arange(n)
         maps = [maps[a] for a in anc]
