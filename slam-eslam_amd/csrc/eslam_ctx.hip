@@ -773,7 +773,7 @@ static int local_maps_reset(eslam_ctx* ctx)
     lm.hy = dm_lm_half(r, ctx->map_scale[1]);
     lm.wx = 2 * lm.hx + 1;
     lm.wy = 2 * lm.hy + 1;
-    lm.S = lm.wx * lm.wy;
+    lm.S = (lm.wx * lm.wy + 3u) & ~3u;        // slots per table, padded (NONE) to whole 16-byte words
     lm.mx = lm_magic(lm.wx);
     lm.my = lm_magic(lm.wy);
     lm.bx = lm.wx * (((1u << 29) + lm.wx - 1) / lm.wx);

@@ -108,7 +108,8 @@ struct DevState {
 // shared grid plus, per particle, a window of (2 hx + 1) x (2 hy + 1) tiles of 8 x 8 cells
 // around the particle (eslam_detmath.h DM_LM_*: the window reaches maxSensorRange and moves
 // with the particle at every map update; tiles it leaves are forgotten).
-//   table  what a particle names (DevState::sid): the window centre and S = wx * wy slots, the
+//   table  what a particle names (DevState::sid): the window centre and S slots (wx * wy, padded
+//          with DM_LM_NONE to a multiple of 4), the
 //          slot of tile (a, b) being (a mod wx) + wx (b mod wy), each a page id or DM_LM_NONE.
 //          The resample copies the name, so copies share a table; a map update that changes
 //          a table another particle also names writes the result to a free table the particle

@@ -2179,17 +2179,24 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     }
                     const uint32_t lmin = cnt ? grp_get(Lr, 0) : 1u, lmax = cnt ? grp_get(Lr, cnt - 1) : 0u;
                     wave_sync();
-                    uint32_t sb = lm_div(l, lm.mx), sa = l - lm.wx * sb;
-                    for (uint32_t s = l; s < lm.S; s += kLmLanes) {
-                        const uint32_t v0 = xsl[s];
-                        uint32_t v = v0;
-                        if (((colx >> sa) | (rowx >> sb)) & 1u) v = DM_LM_NONE;
-                        if (s >= lmin && s <= lmax)
-                            for (uint32_t r = 0; r < cnt; ++r)
-                                if (s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) v = s_np[pl][2 * r + 1];
-                        if (shared || v != v0) tsl[s] = v;
-                        sa += kLmLanes;               // the next slot's column and row
-                        while (sa >= lm.wx) { sa -= lm.wx; ++sb; }
+                    // four slots a lane (tables are padded to whole 16-byte words): each group
+                    // instruction moves 128 contiguous bytes of the table
+                    for (uint32_t q = l; q < lm.S / 4; q += kLmLanes) {
+                        const uint4 w4 = reinterpret_cast<const uint4*>(xsl)[q];
+                        uint32_t v[4] = {w4.x, w4.y, w4.z, w4.w};
+                        bool ch = false;
+#pragma unroll
+                        for (uint32_t e = 0; e < 4; ++e) {
+                            const uint32_t s = 4 * q + e, sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
+                            uint32_t w = v[e];
+                            if (((colx >> sa) | (rowx >> sb)) & 1u) w = DM_LM_NONE;
+                            if (s >= lmin && s <= lmax)
+                                for (uint32_t r = 0; r < cnt; ++r)
+                                    if (s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) w = s_np[pl][2 * r + 1];
+                            ch |= w != v[e];
+                            v[e] = w;
+                        }
+                        if (shared || ch) reinterpret_cast<uint4*>(tsl)[q] = make_uint4(v[0], v[1], v[2], v[3]);
                     }
                 } else if (need) {
                     tsl[Lr] = NP;
