@@ -260,6 +260,16 @@ typedef struct eslam_scan_patch {
  * its patches in the scan's order); the update's counters add up over the parts
  * (map_stores_changed counts a map once per part that changed it).                          */
 int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);
+/* processMap(scanMap, match = true, ...)  src/EmbodiedSlamFilter.cpp:214-221: the visual
+ * weighting w *= pow(weight, 0.1f) of every particle against its own map (per-particle maps).
+ * envire's MLSGrid::match is not in the reference, so the rule is this build's (DESIGN.md 5c,
+ * parity unpinned): every 10th scan patch (sampling 10), placed like the merge, that lands on
+ * a cell the particle's own map holds -- a tile inside both its window and the window the
+ * next update centres on the particle -- scores exp(-d^2 / (2 sigma^2)), sigma 0.2f, d = the
+ * patch's height + zPos - the cell's mean; weight = the mean score as a float (1 without a
+ * matched cell).  Call it before eslam_gpu_map_update, as processMap does; weights are not
+ * normalised.                                                                              */
+int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count);
 /* PoseEstimator::setEnvironment(env, map, useShared)  src/PoseEstimator.cpp:49-62: on = 1
  * gives every particle its own map (ESLAM_FLAG_PARTICLE_MAPS), 0 the shared map only.  Before
  * the particles are initialised (ESLAM_ERR_INVALID_ARG after).  On a sharded filter a

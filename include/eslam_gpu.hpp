@@ -597,6 +597,19 @@ public:
     // patches until the next map update gives each a private copy (copy on write), so there is
     // nothing to do here
     void cloneMaps() {}
+    // the match half of EmbodiedSlamFilter::processMap(scanMap, match, update)
+    // (src/EmbodiedSlamFilter.cpp:214-221): every particle's weight *= pow(weight, 0.1f)
+    void matchMaps(const std::vector<ScanPatch>& scan)
+    {
+        flush();
+        invalidate();
+        std::vector<eslam_scan_patch> p(scan.size());
+        for (size_t k = 0; k < scan.size(); ++k) {
+            for (int i = 0; i < 3; ++i) p[k].position[i] = scan[k].position[i];
+            p[k].stdev = scan[k].stdev;
+        }
+        check(ctx_, eslam_gpu_map_match(ctx_, p.data(), (uint32_t)p.size()));
+    }
     // the merge half of EmbodiedSlamFilter::processMap(scanMap, match, update)
     // (src/EmbodiedSlamFilter.cpp:179-232) for per-particle maps: the scan's patches in the
     // yaw-free body frame, placed at every particle's pose
@@ -954,11 +967,12 @@ public:
 
     // processMap(scanMap, match, update)  src/EmbodiedSlamFilter.cpp:179-232 with the scan's
     // MLS as patches: update merges them into every particle's own map (useSharedMap = false;
-    // the reference's update-only call, src/EmbodiedSlamFilter.cpp:340-342); the visual match
-    // weighting (match = true, envire's MLSGrid::match) is not built
+    // the reference's update-only call, src/EmbodiedSlamFilter.cpp:340-342); match weights every
+    // particle against its own map first (the build's match rule, eslam_gpu_map_match)
     void processMap(const std::vector<ScanPatch>& scanMap, bool match, bool update)
     {
-        if (match) throw std::runtime_error("processMap: the visual match update is not supported by the MI355X filter");
+        if (match && sharedMap_) throw std::runtime_error("processMap: match needs per-particle maps (useSharedMap = false)");
+        if (match) estimator().matchMaps(scanMap);
         if (update && !sharedMap_) estimator().updateMaps(scanMap);
     }
 

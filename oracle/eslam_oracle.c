@@ -2196,6 +2196,8 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
 /* processMap's merge of a whole scan: 64 patches at a time, in order (the GPU's parts,
  * eslam_gpu_map_update); every cell sees its patches in the scan's order, the counters add up */
 #define OR_SCAN_PART 64u
+#define OR_MATCH_SAMPLING 10u       /* src/EmbodiedSlamFilter.cpp:216 */
+#define OR_MATCH_SIGMA ((double)0.2f) /* :217, a float there */
 int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 {
     f->info.map_patches_dropped = f->info.map_stores_changed = 0;
@@ -2203,6 +2205,83 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     for (uint32_t c0 = 0; c0 == 0 || c0 < m; c0 += OR_SCAN_PART) {
         const int rc = or_map_update_part(f, sp + c0, m - c0 < OR_SCAN_PART ? m - c0 : OR_SCAN_PART);
         if (rc) return rc;
+    }
+    return 0;
+}
+
+/* processMap(scanMap, match = true): the visual weighting p.weight *= pow(weight, 0.1) of
+ * src/EmbodiedSlamFilter.cpp:214-221 (sampling 10, sigma 0.2).  envire's MLSGrid::match is
+ * not in the reference tree, so this rule is the build's own (parity unpinned):
+ * every 10th scan patch, placed like the merge, that lands on a cell of the particle's own
+ * map (a tile inside both its current window and the window the update centres on the
+ * particle: the reference selects the active grid before matching, :195-207) scores
+ * exp(-d^2 / (2 sigma^2)), d = patch height + zPos - the cell's mean; weight = the mean score
+ * (1 without a matched cell), a float as in the reference; weight *= pow(weight, 0.1f).     */
+int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
+{
+    if (!(f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS)) return ESLAM_ERR_INVALID_ARG;
+    if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
+    if (!f->n) return ESLAM_ERR_NOT_INITIALISED;
+    if (!f->lm_on) return ESLAM_ERR_OUT_OF_MEMORY;
+    const eslam_mls_grid* g = &f->map;
+    const double* A = g->global2local;
+    static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    int is_id = 1;
+    for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
+    const uint64_t S = f->lm_S;
+    const uint32_t hx = f->lm_hx, hy = f->lm_hy, wx = f->lm_wx, wy = f->lm_wy;
+    const int64_t n = (int64_t)f->n;
+#pragma omp parallel for num_threads(f->threads) if (f->threads > 1) schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t* ctr = f->pm_ctr + 2 * i;
+        const uint32_t* sl = f->pm_slot + (uint64_t)i * S;
+        double sn, co;
+        dm_sincos(f->th[OD(i)], &sn, &co);
+        const double bx = f->x[OD(i)] - g->offset_x, by = f->y[OD(i)] - g->offset_y;
+        if (!(dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(f->th[OD(i)]))) continue;
+        int32_t na, nb;
+        if (is_id) {
+            na = dm_lm_centre(f->x[OD(i)], g->offset_x, 1.0 / g->scale_x);
+            nb = dm_lm_centre(f->y[OD(i)], g->offset_y, 1.0 / g->scale_y);
+        } else {
+            const double px = f->x[OD(i)], py = f->y[OD(i)], pz = f->z[OD(i)];
+            na = dm_lm_centre(((A[0] * px + A[1] * py) + A[2] * pz) + A[3], g->offset_x, 1.0 / g->scale_x);
+            nb = dm_lm_centre(((A[4] * px + A[5] * py) + A[6] * pz) + A[7], g->offset_y, 1.0 / g->scale_y);
+        }
+        double sum = 0.0;
+        uint32_t cnt = 0;
+        for (uint32_t k = 0; k < m; k += OR_MATCH_SAMPLING) {
+            const double wz = sp[k].position[2] + f->z[OD(i)];
+            uint32_t cm, cn;
+            if (is_id) {
+                if (dm_merge_cell_mn(bx, by, co, sn, sp[k].position[0], sp[k].position[1], 1.0 / g->scale_x,
+                                     1.0 / g->scale_y, g->width, g->height, &cm, &cn) == 0xffffffffu)
+                    continue;
+            } else {
+                const double wx_ = (co * sp[k].position[0] + (-sn) * sp[k].position[1]) + f->x[OD(i)];
+                const double wy_ = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
+                const double lx = ((A[0] * wx_ + A[1] * wy_) + A[2] * wz) + A[3];
+                const double ly = ((A[4] * wx_ + A[5] * wy_) + A[6] * wz) + A[7];
+                const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
+                const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
+                if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
+                cm = (uint32_t)fm;
+                cn = (uint32_t)fn;
+            }
+            const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+            if (!dm_lm_inside(a, na, hx, wx) || !dm_lm_inside(b, nb, hy, wy)) continue;
+            if (!dm_lm_inside(a, ctr[0], hx, wx) || !dm_lm_inside(b, ctr[1], hy, wy)) continue;
+            const uint32_t pg = sl[(a % wx) + wx * (b % wy)];
+            if (pg == DM_LM_NONE) continue;
+            const float* v = lm_pg(f, pg)->v;
+            const uint32_t j = (cm & 7u) + 8u * (cn & 7u);
+            if (!dm_lm_holds(v[2 * j + 1])) continue;
+            const double d = wz - (double)v[2 * j];
+            sum += dm_exp(-(d * d) / (2.0 * OR_MATCH_SIGMA * OR_MATCH_SIGMA));
+            ++cnt;
+        }
+        const float wf = cnt ? (float)(sum / (double)cnt) : 1.0f;
+        f->w[OD(i)] *= dm_pow((double)wf, (double)0.1f);
     }
     return 0;
 }

@@ -144,6 +144,7 @@ void or_dm_fx128(double v, int scale, uint32_t limbs[4]);
 
 /* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): processMap's merge, and a particle's patches */
 int or_map_update(or_filter* f, const eslam_scan_patch* patches, uint32_t count);
+int or_map_match(or_filter* f, const eslam_scan_patch* patches, uint32_t count);
 uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* mean, float* stdev, uint32_t cap);
 uint64_t or_pages_in_use(or_filter* f);
 

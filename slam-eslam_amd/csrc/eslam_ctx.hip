@@ -34,6 +34,8 @@ extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const Loc
                                                  const void* pay, uint32_t* pgc, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
                                             const MergeParams* mp, uint32_t* pgc, hipStream_t stream);
+extern "C" hipError_t eslam_launch_map_match(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                             const MatchParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
                                              const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pay_hdr(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
@@ -272,6 +274,8 @@ struct eslam_ctx {
     uint16_t* lm_codes = nullptr;            // per particle: the plan's cell codes (MergeParams::codes)
     uint32_t* lm_poff = nullptr;             // per merge block: page offsets (+ total)
     uint32_t* lm_pgc = nullptr;              // the page collection's compaction counts
+    void* match_sp = nullptr;                // processMap match: the sampled scan patches (device)
+    uint64_t match_cap = 0;
     uint64_t* merge_cnt = nullptr;           // the map merge's statistics slots (2 x kMergeCounterSlots) and
                                              // the copy-on-write copies since the last merge
     // logDebug records of the last update (ESLAM_FLAG_RECORD_CONTACTS / log_debug)
@@ -615,9 +619,9 @@ static void free_local_maps(eslam_ctx* ctx)
 {
     (void)hipFree(ctx->lm.ctr); (void)hipFree(ctx->lm.slot); (void)hipFree(ctx->lm.page); (void)hipFree(ctx->lm.tgen);
     (void)hipFree(ctx->lm.owner); (void)hipFree(ctx->lm.frees); (void)hipFree(ctx->lm.mark);
-    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_job); (void)hipFree(ctx->lm_codes); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc);
+    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_job); (void)hipFree(ctx->lm_codes); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc); (void)hipFree(ctx->match_sp);
     ctx->lm = LocalMaps{};
-    ctx->lm_off = nullptr; ctx->lm_job = nullptr; ctx->lm_codes = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr;
+    ctx->lm_off = nullptr; ctx->lm_job = nullptr; ctx->lm_codes = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr; ctx->match_sp = nullptr; ctx->match_cap = 0;
     ctx->lm_ready = false;
 }
 
@@ -1750,6 +1754,39 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
         }
     }
     mrec(ctx, 4);
+    return ESLAM_OK;
+}
+
+// processMap(scanMap, match = true, ...)  src/EmbodiedSlamFilter.cpp:214-221 (k_map_match)
+extern "C" int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patches, uint32_t count)
+{
+    if (!ctx || (!patches && count)) return ESLAM_ERR_INVALID_ARG;
+    if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
+    if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_match needs per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
+    if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
+    if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
+    if (const int rc_ = check_poisoned(ctx)) return rc_;
+    if (!ctx->lm_ready) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "per-particle maps not allocated");
+    for (uint32_t k = 0; k < count; ++k)
+        if (!dm_isfinite(patches[k].position[0]) || !dm_isfinite(patches[k].position[1]) ||
+            !dm_isfinite(patches[k].position[2]) || !dm_isfinite(patches[k].stdev))
+            return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_match: scan patches must be finite");
+    int rc = materialize(ctx);                // the weights of the particles as they stand
+    if (rc) return rc;
+    std::vector<ScanPatch> s;
+    for (uint32_t k = 0; k < count; k += kMatchSampling)
+        s.push_back(ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev});
+    rc = grow(ctx, &ctx->match_sp, &ctx->match_cap, (s.size() + 1) * sizeof(ScanPatch), false);
+    if (rc) return rc;
+    if (!s.empty()) HIPCHK(ctx, hipMemcpyAsync(ctx->match_sp, s.data(), s.size() * sizeof(ScanPatch), hipMemcpyHostToDevice, ctx->stream));
+    MatchParams mp;
+    mp.n = ctx->n;
+    mp.m = (uint32_t)s.size();
+    mp.is_id = ctx->map.g2l_identity;
+    mp.sp = (const ScanPatch*)ctx->match_sp;
+    HIPCHK(ctx, eslam_launch_map_match(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
+    // the host's copy of the patches may go away when this returns
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return ESLAM_OK;
 }
 

@@ -268,6 +268,15 @@ struct ScanPatch {
     double x, y, z, stdev;
 };
 constexpr int kMaxScanPatches = 64;
+// processMap(scanMap, match = true) (k_map_match): every kMatchSampling-th scan patch
+constexpr uint32_t kMatchSampling = 10;          // src/EmbodiedSlamFilter.cpp:216
+constexpr double kMatchSigma = (double)0.2f;     // :217 (a float there)
+struct MatchParams {
+    uint64_t n;
+    uint32_t m;                          // the sampled patches in sp
+    uint32_t is_id;                      // the grid's global2local is the identity
+    const ScanPatch* sp;                 // device copy of the sampled patches
+};
 constexpr int kLmBlock = 128;                   // particles per block of the page plan (k_map_plan, k_recv_plan)
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
 constexpr uint32_t kMergeCounters = 6;

@@ -2303,6 +2303,71 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     }
 }
 
+// processMap(scanMap, match = true) per particle (the oracle's or_map_match; the rule is the
+// build's own, envire's MLSGrid::match not being in the reference): every 10th scan patch,
+// placed like the merge, that lands on a cell of the particle's own map -- a tile inside both
+// its window and the window the update centres on the particle -- scores
+// exp(-d^2 / (2 sigma^2)), sigma 0.2f (src/EmbodiedSlamFilter.cpp:217); the particle's weight
+// is multiplied by pow(weight, 0.1f), weight the float mean score (1 without a matched cell).
+// A lane per particle: a handful of lookups each (the sampled patches, scalar loads).
+__global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
+                                                      LocalMaps lm, MatchParams mp)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= mp.n) return;
+    const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
+    const uint32_t X = st.sid[i];
+    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i];
+    const double bx = x - map.offset_x, by = y - map.offset_y;
+    if (!(dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(th))) return;
+    double sn, co;
+    dm_sincos(th, &sn, &co);
+    const double* A = map.g2l;
+    int32_t na, nb;
+    if (mp.is_id) {
+        na = dm_lm_centre(x, map.offset_x, map.inv_scale_x);
+        nb = dm_lm_centre(y, map.offset_y, map.inv_scale_y);
+    } else {
+        na = dm_lm_centre(((A[0] * x + A[1] * y) + A[2] * z) + A[3], map.offset_x, map.inv_scale_x);
+        nb = dm_lm_centre(((A[4] * x + A[5] * y) + A[6] * z) + A[7], map.offset_y, map.inv_scale_y);
+    }
+    const int2 c = lm.ctr[X];
+    double sum = 0.0;
+    uint32_t cnt = 0;
+    for (uint32_t k = 0; k < mp.m; ++k) {
+        const ScanPatch sp = mp.sp[k];
+        const double wz = sp.z + z;
+        uint32_t cm, cn;
+        if (mp.is_id) {
+            if (dm_merge_cell_mn(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width, map.height_cells,
+                                 &cm, &cn) == 0xffffffffu)
+                continue;
+        } else {
+            const double wx = (co * sp.x + (-sn) * sp.y) + x;
+            const double wy = (sn * sp.x + co * sp.y) + y;
+            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+            if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
+            cm = (uint32_t)fm;
+            cn = (uint32_t)fn;
+        }
+        const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+        if (!dm_lm_inside(a, na, lm.hx, lm.wx) || !dm_lm_inside(b, nb, lm.hy, lm.wy)) continue;
+        if (!dm_lm_inside(a, c.x, lm.hx, lm.wx) || !dm_lm_inside(b, c.y, lm.hy, lm.wy)) continue;
+        const uint32_t pg = lm.slot[(uint64_t)X * lm.S + lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my)];
+        if (pg == DM_LM_NONE) continue;
+        const float2 cv = lm.page[(uint64_t)pg * DM_LM_PAGE_CELLS + (cm & 7u) + 8u * (cn & 7u)];
+        if (!dm_lm_holds(cv.y)) continue;
+        const double d = wz - (double)cv.x;
+        sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
+        ++cnt;
+    }
+    const float wf = cnt ? (float)(sum / (double)cnt) : 1.0f;
+    st.w[i] = st.w[i] * dm_pow((double)wf, (double)0.1f);
+}
+
 // the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads); the free
 // list's cursor moves past this update's plan
 __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint64_t* __restrict__ cnt, Ctl* __restrict__ ctl,
@@ -3872,6 +3937,14 @@ extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, 
     if (e != hipSuccess) return e;
     if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     return page_budget(ctl, lm, mp, nb, pgc, stream);
+}
+
+extern "C" hipError_t eslam_launch_map_match(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const LocalMaps* lm,
+                                             const MatchParams* mp, hipStream_t stream)
+{
+    const uint64_t blocks = (mp->n + kBlock - 1) / kBlock;
+    if (blocks) hipLaunchKernelGGL(k_map_match, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,

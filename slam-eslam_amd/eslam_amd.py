@@ -65,6 +65,8 @@ def load_library(path=LIB_PATH):
     L.eslam_gpu_download_particles.argtypes = [vp, C.POINTER(A.Particles)]
     L.eslam_gpu_write_particles.argtypes = [vp, C.c_uint64, C.c_uint64, C.POINTER(A.Particles)]
     L.eslam_gpu_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
+    if hasattr(L, "eslam_gpu_map_match"):                 # absent from older builds (A/B runs)
+        L.eslam_gpu_map_match.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
     L.eslam_gpu_set_particle_maps.argtypes = [vp, C.c_int]
     L.eslam_gpu_get_particle_map.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_float),
                                              C.POINTER(C.c_float), C.c_uint32, C.POINTER(C.c_uint32)]
@@ -189,6 +191,10 @@ class GpuFilter:
     def map_update(self, patches):
         """eslam_gpu_map_update: processMap's merge of a scan into every particle's map"""
         self._check(self.L.eslam_gpu_map_update(self.h, patches, len(patches)))
+
+    def map_match(self, patches):
+        """eslam_gpu_map_match: processMap's visual weighting (match = true) against each own map"""
+        self._check(self.L.eslam_gpu_map_match(self.h, patches, len(patches)))
 
     def particle_map(self, i, cap=1024):
         """particle i's own patches: (cells, mean, stdev), tiles in slot order, cells row by row"""

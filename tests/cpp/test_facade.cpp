@@ -373,9 +373,23 @@ int main()
         float mean[64], sd[64];
         EXPECT(eslam_gpu_get_particle_map(mf.estimator().handle(), 0, cells, mean, sd, 64, &cnt) == ESLAM_OK && cnt > 0,
                "particle 0 holds patches from the scans");
-        bool threw = false;
-        try { mf.processMap(scan, true, false); } catch (const std::runtime_error&) { threw = true; }
-        EXPECT(threw, "processMap(match = true) is not built: throws");
+        // processMap(scanMap, true, true): the match weighting (eslam_gpu_map_match) before the
+        // merge, against the raw ABI; a scan 5 cm higher scores below 1 on the matched cells
+        std::vector<eslam_ns::ScanPatch> hi = scan;
+        for (auto& sp : hi) sp.position = eslam_ns::Vector3d(sp.position.x(), sp.position.y(), sp.position.z() + 0.05);
+        std::vector<eslam_scan_patch> rh(rs);
+        for (auto& sp : rh) sp.position[2] += 0.05;
+        const double w0 = mf.getParticles()[0].weight;
+        mf.processMap(hi, true, true);
+        EXPECT(eslam_gpu_map_match(raw.handle(), rh.data(), (uint32_t)rh.size()) == ESLAM_OK &&
+                   eslam_gpu_map_update(raw.handle(), rh.data(), (uint32_t)rh.size()) == ESLAM_OK,
+               "raw match + update");
+        std::vector<eslam_ns::PoseParticle>& a2 = mf.getParticles();
+        std::vector<eslam_ns::PoseParticle>& b2 = raw.getParticles();
+        diff = a2.size() != b2.size();
+        for (size_t i = 0; i < a2.size() && i < b2.size(); ++i) diff += std::memcmp(&a2[i].weight, &b2[i].weight, 8) != 0;
+        EXPECT(diff == 0, "processMap(match = true): façade == raw ABI, bit for bit");
+        EXPECT(a2[0].weight < w0, "the higher scan lowers particle 0's weight");
     }
 
     // ---- one shard of a 3000-particle filter over the library's own RCCL communicator ----

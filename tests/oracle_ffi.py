@@ -90,6 +90,7 @@ def lib(aos=False):
     L.or_get_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
     L.or_set_rng_state.argtypes = [vp, C.POINTER(A.RngState)]
     L.or_map_update.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
+    L.or_map_match.argtypes = [vp, C.POINTER(A.ScanPatch), C.c_uint32]
     L.or_get_particle_map.restype = C.c_uint32
     L.or_pages_in_use.restype = C.c_uint64
     L.or_pages_in_use.argtypes = [vp]
@@ -264,6 +265,9 @@ class OracleFilter:
 
     def map_update(self, patches):
         assert self.L.or_map_update(self.h, patches, len(patches)) == 0
+
+    def map_match(self, patches):
+        assert self.L.or_map_match(self.h, patches, len(patches)) == 0
 
     def particle_map(self, i, cap=1024):
         while True:

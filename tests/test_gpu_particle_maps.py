@@ -301,3 +301,41 @@ def test_particle_maps_shapes(gpu_mod, oracle, case):
         assert dropped > 0                   # the scan reaches past the window
     else:
         assert dropped == 0
+
+
+@pytest.mark.parametrize("case", ["identity", "rotated_grid"])
+def test_particle_maps_match_bit_exact(gpu_mod, oracle, case):
+    """processMap(scanMap, match, update) (src/EmbodiedSlamFilter.cpp:179-232): the match
+    weighting (eslam_gpu_map_match: every 10th patch scored against the particle's own map,
+    w *= pow(weight, 0.1f); the rule is the build's own) before the merge, with
+    match-only and update-only calls mixed in and the weights feeding the next step's resample;
+    a match against empty maps first.  Bit-exact against the oracle after every call."""
+    n = 5003
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
+    grid = S.unmapped_beyond(S.rough_map(cells=120), 0.3)
+    if case == "rotated_grid":
+        grid = rotated(grid)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.05], 0.18, 0.05)
+    scan = S.scan_patches(nx=12, ny=9)                # 108 patches: 11 sampled
+    probe = S.scan_patches(nx=12, ny=9, z=-0.15)
+    lowered = 0
+    for k, st in enumerate(S.step_stream(14, tilt=True)):
+        assert gpu.step(st) == orc.step(st)
+        w0 = gpu.download().weight.copy()
+        if k % 4 != 2:                                # processMap(scan, true, ...)
+            gpu.map_match(probe)
+            orc.map_match(probe)
+            assert_bit_identical(gpu.download(), orc.download(), f"{case} match step {k}")
+            lowered += int(np.sum(gpu.download().weight < w0))
+        if k % 4 != 1:                                # processMap(scan, ..., true)
+            gpu.map_update(scan)
+            orc.map_update(scan)
+            assert map_info(gpu.sync()) == map_info(orc.info()), (case, k)
+        assert_bit_identical(gpu.download(), orc.download(), f"{case} step {k}")
+    assert np.array_equal(gpu.ancestors(), orc.ancestors())
+    assert lowered > n                                # the probe scan sits 3 cm above the maps

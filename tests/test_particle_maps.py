@@ -229,3 +229,45 @@ def test_covered_cells_are_counted(oracle):
     # the host recount uses plain double arithmetic: it may differ from the contract's cell
     # placement (fma, 1/scale) on a handful of boundary patches
     assert abs(int(info.map_patches_covered) - covered) <= max(3, covered // 500)
+
+
+def flat_scan(dz=0.0, **kw):
+    scan = S.scan_patches(**kw)
+    for k in range(len(scan)):
+        scan[k].position[2] = -0.18 + dz
+    return scan
+
+
+def test_match_weights_against_own_map(oracle):
+    """processMap(scanMap, match = true) (src/EmbodiedSlamFilter.cpp:214-221; the match rule is
+    the build's own, envire's MLSGrid::match not being in the reference -- parity unpinned):
+    against maps holding a flat scan, the same scan scores 1 on every cell (weights unchanged,
+    bit for bit), a scan dz higher multiplies each matched particle's weight by
+    float(exp(-dz^2 / (2 * 0.2f^2)))^0.1f and leaves the unmatched ones as they are, and only
+    every 10th patch counts (sampling 10)."""
+    f, _ = setup()
+    f.step(S.step_stream(1)[0])                          # the weights of an update (init leaves 0)
+    w_empty = f.download().weight.copy()
+    assert np.all(w_empty > 0)
+    f.map_match(flat_scan(0.1))                          # empty maps: nothing to match
+    assert np.array_equal(f.download().weight, w_empty)
+    scan = flat_scan()
+    f.map_update(scan)
+    w0 = f.download().weight.copy()
+    f.map_match(scan)
+    assert np.array_equal(f.download().weight, w0)
+    odd = flat_scan()
+    for k in range(len(odd)):
+        if k % 10:
+            odd[k].position[2] += 5.0                    # never sampled
+    f.map_match(odd)
+    assert np.array_equal(f.download().weight, w0)
+    dz = 0.1
+    f.map_match(flat_scan(dz))
+    r = f.download().weight / w0
+    sig = float(np.float32(0.2))
+    score = float(np.float32(math.exp(-dz * dz / (2.0 * sig * sig))))
+    expect = score ** float(np.float32(0.1))
+    matched = np.abs(r - expect) < 1e-6
+    assert np.all(matched | (r == 1.0))
+    assert matched.mean() > 0.9
