@@ -97,6 +97,10 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_RECORD_CONTACTS 0x8u    /* keep every update's cpoints, meas_pos, meas_theta
                                               (also on with log_debug); on a sharded filter
                                               download_records is then a collective          */
+#define ESLAM_FLAG_PROCESS_STATICS 0x20u  /* Q11: the hash-respawn counter (the function static
+                                              of src/PoseEstimator.cpp:239) and rand() are the
+                                              process's, shared by every context that sets this
+                                              flag (default: each context its own)           */
 
 void eslam_config_default(eslam_config* cfg);
 

@@ -244,6 +244,20 @@ void set_translation_pose(double ud[12], double x, double y, double z)
 // ---------------------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------------------
+// ESLAM_FLAG_PROCESS_STATICS: the reference's function-static hash-respawn counter
+// (src/PoseEstimator.cpp:239) and the C library's rand() (SurfaceHash::sample), shared by every
+// context of the process that sets the flag -- Q11.  Not locked, like the reference's statics.
+struct ProcessStatics {
+    uint64_t hash_event = 0;
+    dm_libc_rand_state libc;
+    ProcessStatics() { dm_libc_srand(&libc, 1); }
+};
+static ProcessStatics& process_statics()
+{
+    static ProcessStatics ps;
+    return ps;
+}
+
 struct eslam_ctx {
     eslam_config cfg;
     int device = 0;
@@ -350,6 +364,10 @@ struct eslam_ctx {
     std::vector<uint32_t> hash_bstart;       // bins^2 + 1
     std::vector<int32_t> hash_bucket;        // per pose (sweep order)
     dm_libc_rand_state libc;                 // rand() of SurfaceHash::sample (glibc, seed 1)
+    // the hash-respawn counter and rand() in use: this context's own, or the process's
+    // (ESLAM_FLAG_PROCESS_STATICS: the reference's function statics, Q11)
+    uint64_t* hash_ev = nullptr;
+    dm_libc_rand_state* libcp = nullptr;
     void* hsend = nullptr; uint64_t hsend_cap = 0;   // sharded respawn: candidate pairs out / in
     void* hrecv = nullptr; uint64_t hrecv_cap = 0;
     void* hsort = nullptr; uint64_t hsort_cap = 0;   // their keys, vals, sorted keys, order + sort scratch
@@ -557,6 +575,14 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
         memset(ctx->fault_host, 0, 64);
         ctx->ctl_host->minstd = dm_minstd_seed(cfg->seed);     // ParticleFilter(seed)
         dm_libc_srand(&ctx->libc, 1);                            // the reference never seeds rand()
+        if (cfg->flags & ESLAM_FLAG_PROCESS_STATICS) {
+            ProcessStatics& ps = process_statics();
+            ctx->hash_ev = &ps.hash_event;
+            ctx->libcp = &ps.libc;
+        } else {
+            ctx->hash_ev = &ctx->hash_event;
+            ctx->libcp = &ctx->libc;
+        }
         ctx->ctl_host->max_weight = 0.0;                         // PoseEstimator ctor
         ctx->ctl_host->wexp = 1;
         ctx->ctl_host->scan_shift = 60;
@@ -1326,7 +1352,7 @@ extern "C" int eslam_gpu_init_hash(eslam_ctx* ctx, uint64_t n)
     const uint64_t total = ctx->sharded ? ctx->n_global : n, skip = ctx->gbase;
     std::vector<uint32_t> idx(n ? n : 1);
     for (uint64_t gi = 0; gi < total; ++gi) {
-        const uint32_t v = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&ctx->libc) % ctx->hash_n);
+        const uint32_t v = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(ctx->libcp) % ctx->hash_n);
         if (gi >= skip && gi < skip + n) idx[gi - skip] = v;
     }
     uint32_t* d_idx = nullptr;
@@ -2358,7 +2384,7 @@ static int sample_from_hash(eslam_ctx* ctx, const eslam_step_input* in, const St
         gorder = so;
     }
     std::vector<uint32_t> draws(k);
-    for (uint64_t j = 0; j < k; ++j) draws[j] = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(&ctx->libc) % bsize);
+    for (uint64_t j = 0; j < k; ++j) draws[j] = (uint32_t)((uint64_t)(uint32_t)dm_libc_rand(ctx->libcp) % bsize);
     if (ctx->draws_cap < k) {
         (void)hipFree(ctx->d_draws); ctx->d_draws = nullptr; ctx->draws_cap = 0;
         HIPCHK(ctx, hipMalloc(&ctx->d_draws, sizeof(uint32_t) * k));
@@ -2410,7 +2436,7 @@ static int launch_step(eslam_ctx* ctx, const eslam_step_input* in, bool project,
     bool respawn = false;
     if (project && ctx->cfg.hash_use && ctx->has_hash) {
         const uint64_t period = ctx->cfg.hash_period ? ctx->cfg.hash_period : 1;
-        respawn = (ctx->hash_event++ % period) == 0;
+        respawn = ((*ctx->hash_ev)++ % period) == 0;
     }
     // logDebug records: the update's contact points are recorded on the projected state
     const bool records = weight && record_contacts(ctx);
@@ -2784,11 +2810,11 @@ extern "C" int eslam_gpu_get_rng_state(eslam_ctx* ctx, eslam_rng_state* st)
     st->minstd_x = ctx->ctl_host->minstd;
     st->project_count = ctx->proj_event;
     st->init_count = ctx->init_event;
-    st->hash_count = ctx->hash_event;
+    st->hash_count = *ctx->hash_ev;
     st->max_weight = ctx->ctl_host->max_weight;
     memcpy(st->ud_pose, ctx->ud_pose, sizeof(ctx->ud_pose));
-    memcpy(st->libc_rand, ctx->libc.r, sizeof(st->libc_rand));
-    st->libc_rand_pos = ctx->libc.i;
+    memcpy(st->libc_rand, ctx->libcp->r, sizeof(st->libc_rand));
+    st->libc_rand_pos = ctx->libcp->i;
     return ESLAM_OK;
 }
 
@@ -2801,11 +2827,11 @@ extern "C" int eslam_gpu_set_rng_state(eslam_ctx* ctx, const eslam_rng_state* st
     ctx->ctl_host->minstd = st->minstd_x;
     ctx->proj_event = st->project_count;
     ctx->init_event = st->init_count;
-    ctx->hash_event = st->hash_count;
+    *ctx->hash_ev = st->hash_count;
     ctx->ctl_host->max_weight = st->max_weight;
     memcpy(ctx->ud_pose, st->ud_pose, sizeof(ctx->ud_pose));
-    memcpy(ctx->libc.r, st->libc_rand, sizeof(st->libc_rand));
-    ctx->libc.i = st->libc_rand_pos % 34u;
+    memcpy(ctx->libcp->r, st->libc_rand, sizeof(st->libc_rand));
+    ctx->libcp->i = st->libc_rand_pos % 34u;
     return write_ctl(ctx);
 }
 

@@ -1573,10 +1573,6 @@ __device__ __forceinline__ bool lm_in(int32_t a, int32_t c, uint32_t h)
 
 constexpr uint32_t kLmList = 8;                 // tiles one pass of the merge handles
 constexpr uint16_t kCodeSkip = 0xffffu;
-#ifndef ESLAM_LM_GROUP
-#define ESLAM_LM_GROUP 8
-#endif
-constexpr uint32_t kLmGroup = ESLAM_LM_GROUP;   // patches whose occupancy words load together
 constexpr uint32_t kLmNoList = 0xffffffffu;
 
 // one particle as a map update sees it: its table, its pose, the window's new centre

@@ -23,6 +23,7 @@ FLAG_NO_MAP_LDS = 0x2
 FLAG_NO_AUX_GATHER = 0x4
 FLAG_RECORD_CONTACTS = 0x8
 FLAG_PARTICLE_MAPS = 0x10
+FLAG_PROCESS_STATICS = 0x20
 
 
 class Config(C.Structure):

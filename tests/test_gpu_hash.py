@@ -74,3 +74,49 @@ def test_radix_sort_stable(gpu_mod, n, distinct):
     assert L.eslam_gpu_selftest_sort(0, p(keys), p(vals), n, p(ko), p(vo)) == 0
     order = np.argsort(keys, kind="stable")
     assert np.array_equal(vo, vals[order]) and np.array_equal(ko, keys[order])
+
+
+def _share(src, dst):
+    """the process-wide statics of src (hash counter, rand()) handed to dst's oracle"""
+    s, t = dst.rng_state(), src.rng_state()
+    s.hash_count = t.hash_count
+    s.libc_rand[:] = t.libc_rand[:]
+    s.libc_rand_pos = t.libc_rand_pos
+    dst.set_rng_state(s)
+
+
+def test_process_statics_shared_between_contexts(gpu_mod):
+    """Q11 (ESLAM_FLAG_PROCESS_STATICS): two filters of one process share the function-static
+    hash-respawn counter (src/PoseEstimator.cpp:239) and rand(), as the reference's do.  Two
+    flagged contexts stepped in turn equal two oracle filters that hand the counter and the
+    rand() state to each other before every call, bit for bit; the counter then counts both."""
+    import eslam_abi as A
+    n = 2000
+    cfg = hash_config(n, steps=8, bins=20, period=3)
+    cfg.flags |= A.FLAG_PROCESS_STATICS
+    grid = hash_grid(cells=60)
+    ga, gb = gpu_mod.GpuFilter(cfg), gpu_mod.GpuFilter(cfg)
+    oa, ob = O.OracleFilter(cfg, O.SUM_CONTRACT), O.OracleFilter(cfg, O.SUM_CONTRACT)
+    for f in (ga, gb, oa, ob):
+        f.set_map(grid)
+    h0 = ga.rng_state().hash_count
+    ga.init_pose([0.0, 0.0, 0.0], [1.0, 0.0, 0.0, 0.0])
+    oa.init_pose([0.0, 0.0, 0.0], [1.0, 0.0, 0.0, 0.0])
+    _share(oa, ob)
+    gb.init_pose([0.0, 0.0, 0.0], [1.0, 0.0, 0.0, 0.0])
+    ob.init_pose([0.0, 0.0, 0.0], [1.0, 0.0, 0.0, 0.0])
+    steps = slope_stream(5)
+    for k, st in enumerate(steps):
+        _share(ob, oa)
+        ga.step(st)
+        oa.step(st)
+        _share(oa, ob)
+        gb.step(st)
+        ob.step(st)
+        assert_bit_identical(ga.download(), oa.download(), f"A step {k}")
+        assert_bit_identical(gb.download(), ob.download(), f"B step {k}")
+    sa, sb = ga.rng_state(), gb.rng_state()
+    assert sa.hash_count == sb.hash_count == h0 + 2 * len(steps)
+    assert sa.libc_rand_pos == sb.libc_rand_pos == ob.rng_state().libc_rand_pos
+    ga.close()
+    gb.close()
