@@ -385,6 +385,7 @@ int main()
                    eslam_gpu_map_update(raw.handle(), rh.data(), (uint32_t)rh.size()) == ESLAM_OK,
                "raw match + update");
         std::vector<eslam_ns::PoseParticle>& a2 = mf.getParticles();
+        raw.invalidate();                 // the raw ABI calls changed the particles behind the view
         std::vector<eslam_ns::PoseParticle>& b2 = raw.getParticles();
         diff = a2.size() != b2.size();
         for (size_t i = 0; i < a2.size() && i < b2.size(); ++i) diff += std::memcmp(&a2[i].weight, &b2[i].weight, 8) != 0;
