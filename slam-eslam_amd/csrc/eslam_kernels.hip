@@ -544,6 +544,13 @@ __device__ __forceinline__ bool ratio_surely_significant(double z, double zvar, 
 // UNG (with BATCH): every contact closes its group (groupId -1 or a group of one), so the
 // group logic reduces to the Q7 poisoning flag and a push per evaluated, found contact.
 // StepParams (p.*) and the contacts come from scalar loads of the kernel arguments.
+// lookups in flight per particle in the reduced group logic (BATCH && UNG): all MAXP by
+// default; an experiment knob (fewer live registers)
+#ifndef ESLAM_K1_LB
+#define ESLAM_K1_LB 4
+#endif
+constexpr int kK1LookupBatch = ESLAM_K1_LB;
+
 template <int MAXP, bool BATCH, bool DELTA = false, bool UNG = false>
 __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, double s, double r22, double x, double y,
                                                   double z, double meas_var, uint32_t sid)
@@ -641,7 +648,51 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
         return get_patch<DELTA>(win, wx, wy, wz, qv, mean, stdev, sid);
     };
 
-    if constexpr (BATCH) {
+    if constexpr (BATCH && UNG && kK1LookupBatch < MAXP) {
+        // the reduced group logic (below) with kK1LookupBatch lookups in flight at a time
+        bool alive = true;
+#pragma unroll
+        for (int g = 0; g < MAXP; g += kK1LookupBatch) {
+            bool fnd[kK1LookupBatch];
+            double mn[kK1LookupBatch], sd[kK1LookupBatch], wzs[kK1LookupBatch];
+#pragma unroll
+            for (int q = 0; q < kK1LookupBatch; ++q) {
+                const int i = g + q;
+                fnd[q] = false; mn[q] = 0.0; sd[q] = 0.0; wzs[q] = 0.0;
+                if ((uint32_t)i < m) {
+                    double wx, wy;
+                    world((uint32_t)i, wx, wy, wzs[q]);
+                    if ((eval_mask >> i) & 1u) fnd[q] = lookup(wx, wy, wzs[q], mn[q], sd[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kK1LookupBatch; ++q) {
+                const int i = g + q;
+                if ((uint32_t)i >= m) break;
+                if (!((eval_mask >> i) & 1u)) continue;
+                if (alive && fnd[q]) {
+                    const double zdiff = wzs[q] - mn[q];
+                    const double pose_var = sd[q] * sd[q];
+                    const double zvar = sd[q] * sd[q] + meas_var;
+                    double pzd_i = zdiff, pzv_i = zvar, pv_i = pose_var;
+                    bool take = true;
+                    if (!ratio_surely_significant(zdiff, zvar, corr)) {
+                        const double ratio = dm_normal_pdf_cdf_ratio(zdiff, dm_sqrt(zvar) * corr);
+                        take = ratio > 1e-9;
+                        const double inv = 1.0 / ratio;
+                        pzd_i = (zdiff * ratio) * inv;
+                        pzv_i = (zvar * ratio) * inv;
+                        pv_i = (pose_var * ratio) * inv;
+                    }
+                    if (take) {
+                        posevar += pv_i;
+                        push((uint32_t)i, pzd_i, pzv_i);
+                    }
+                }
+                alive = alive && fnd[q];
+            }
+        }
+    } else if constexpr (BATCH) {
         // all m <= MAXP contacts' lookups first: independent, so their memory latencies
         // overlap (a lookup the group logic then skips is harmless: pure function)
         bool fnd[MAXP];
