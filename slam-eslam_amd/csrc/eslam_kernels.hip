@@ -1442,27 +1442,62 @@ __global__ void __launch_bounds__(kBlock) k_gather_records(const uint32_t* __res
     for (uint32_t q = 0; q < 6 * d.maxc; ++q) o[5 + q] = c[q];
 }
 
-// exclusive prefix sum of m counts in place (one block: each thread a contiguous segment)
+// exclusive prefix sum of m counts in place, one block: chunks of 8192 counts are loaded and
+// stored striped (coalesced, every load of a chunk in flight together) through LDS, where each
+// thread scans 8 consecutive counts; the wave scans and a carry join the threads and chunks.
+// (A thread per contiguous segment of m / 1024 counts read and wrote them one dependent load
+// at a time: 73 us per call at 8M particles' 32k block sums.)
+constexpr uint32_t kScanPer = 8, kScanChunk = 1024 * kScanPer;
 __global__ void __launch_bounds__(1024) k_scan_excl(uint32_t* __restrict__ a, uint64_t m)
 {
-    __shared__ uint32_t s_sum[1024];
-    const uint64_t per = (m + 1023) / 1024;
-    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
-    uint32_t t = 0;
-    for (uint64_t i = lo; i < hi; ++i) t += a[i];
-    s_sum[threadIdx.x] = t;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {             // Hillis-Steele inclusive scan of the segment sums
-        const uint32_t v = threadIdx.x >= (uint32_t)o ? s_sum[threadIdx.x - o] : 0u;
+    __shared__ __attribute__((aligned(16))) uint32_t s_v[kScanChunk];
+    __shared__ uint32_t s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint32_t carry = 0;
+    for (uint64_t base = 0; base < m; base += kScanChunk) {
+        const uint32_t cnt = m - base < kScanChunk ? (uint32_t)(m - base) : kScanChunk;
+        uint32_t v[kScanPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kScanPer; ++q) {
+            const uint32_t k = q * 1024u + tid;
+            v[q] = k < cnt ? a[base + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kScanPer; ++q) s_v[q * 1024u + tid] = v[q];
         __syncthreads();
-        s_sum[threadIdx.x] += v;
+        const uint4 lo = reinterpret_cast<const uint4*>(s_v)[2 * tid], hi = reinterpret_cast<const uint4*>(s_v)[2 * tid + 1];
+        const uint32_t u[kScanPer] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kScanPer; ++q) tot += u[q];
+        uint32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t x = (uint32_t)__shfl_up((int)incl, o, 64);
+            incl += lane >= (uint32_t)o ? x : 0u;
+        }
+        if (lane == 63) s_w[wave] = incl;
         __syncthreads();
-    }
-    uint32_t run = s_sum[threadIdx.x] - t;
-    for (uint64_t i = lo; i < hi; ++i) {
-        const uint32_t v = a[i];
-        a[i] = run;
-        run += v;
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16; ++w) {
+            before += w < wave ? s_w[w] : 0u;
+            all += s_w[w];
+        }
+        uint32_t run = carry + before + (incl - tot);
+        uint32_t r[kScanPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kScanPer; ++q) { r[q] = run; run += u[q]; }
+        reinterpret_cast<uint4*>(s_v)[2 * tid] = make_uint4(r[0], r[1], r[2], r[3]);
+        reinterpret_cast<uint4*>(s_v)[2 * tid + 1] = make_uint4(r[4], r[5], r[6], r[7]);
+        carry += all;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kScanPer; ++q) {
+            const uint32_t k = q * 1024u + tid;
+            if (k < cnt) a[base + k] = s_v[k];
+        }
+        __syncthreads();                 // s_v and s_w are reused by the next chunk
     }
 }
 
