@@ -216,6 +216,7 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     else:
         stream = S.step_stream(steps, tilt=(name in ("natural", "maps")))
     scan = S.scan_patches() if name == "maps" else None
+    probe = S.scan_patches(z=-0.15) if name == "maps" else None
     for k, st in enumerate(stream):
         if name == "edit" and k == 2:
             edit_particles(f, lo, hi)
@@ -226,6 +227,9 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         _snap(rec, f"s{k}", f, bool(info.resampled))
         if name == "records":
             _records(rec, f"s{k}", f)
+        if scan is not None and k % 2 == 1:      # processMap(probe, true, ...): the match weighting
+            f.map_match(probe)
+            _snap(rec, f"m{k}", f, False)
         if scan is not None:                     # processMap(scan, false, true)
             f.map_update(scan)
     if scan is not None:                         # every particle's own patches, sorted by cell
