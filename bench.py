@@ -70,6 +70,9 @@ def parse():
                     help="configs[4]'s per-particle local maps (useSharedMap = false): rough terrain, unmapped "
                          "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles per "
                          "GPU (64M over 8 GPUs with --gpus 8)")
+    ap.add_argument("--match", action="store_true",
+                    help="with --local-maps: processMap(scan, match = true, update = true), the match "
+                         "weighting (eslam_gpu_map_match) before every merge")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-aos", action="store_true",
                     help="skip cpu_baseline.aos, the oracle with the reference's 288-byte particle records")
@@ -401,6 +404,8 @@ def main():
         scan = S.scan_patches()
     stream = S.step_stream(args.warmup + 2 * args.steps + 1, tilt=args.local_maps)
     cfg = S.bench_config(A.default_config(), n * world)
+    if args.match and not args.local_maps:
+        raise SystemExit("bench.py: --match needs --local-maps (the match reads per-particle maps)")
     if args.local_maps:
         cfg.flags |= A.FLAG_PARTICLE_MAPS
         cfg.local_map_pages = args.map_pages
@@ -428,8 +433,10 @@ def main():
     if scan is not None:
         step_one = f.step
 
-        def step_and_map(st):                  # EmbodiedSlamFilter::update + processMap(scan, update)
+        def step_and_map(st):                  # EmbodiedSlamFilter::update + processMap(scan, match, update)
             r = step_one(st)
+            if args.match:
+                f.map_match(scan)
             f.map_update(scan)
             return r
         f_step = step_and_map
@@ -517,7 +524,8 @@ def main():
                                "resample forced every step%s" % (workload_name(n, world, args.rough, args.local_maps), n,
                                                                  "rough " if args.rough else "", args.map_cells,
                                                                  args.map_cells,
-                                                                 ", per-particle local maps + map update per step"
+                                                                 (", per-particle local maps + map %supdate per step"
+                                                                  % ("match + " if args.match else ""))
                                                                  if args.local_maps else ""),
                    "particles_per_gpu": n, "global_particles": n * world,
                    "parallelism": "dp%d (particle shards%s)" % (world, (", sharded path, %s exchanges" % args.comm)

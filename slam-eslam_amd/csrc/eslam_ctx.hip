@@ -1802,17 +1802,23 @@ extern "C" int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patch
     std::vector<ScanPatch> s;
     for (uint32_t k = 0; k < count; k += kMatchSampling)
         s.push_back(ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev});
-    rc = grow(ctx, &ctx->match_sp, &ctx->match_cap, (s.size() + 1) * sizeof(ScanPatch), false);
-    if (rc) return rc;
-    if (!s.empty()) HIPCHK(ctx, hipMemcpyAsync(ctx->match_sp, s.data(), s.size() * sizeof(ScanPatch), hipMemcpyHostToDevice, ctx->stream));
     MatchParams mp;
     mp.n = ctx->n;
     mp.m = (uint32_t)s.size();
     mp.is_id = ctx->map.g2l_identity;
-    mp.sp = (const ScanPatch*)ctx->match_sp;
+    mp.sp = nullptr;
+    const bool inline_sp = s.size() <= (size_t)kMaxScanPatches;   // the kernel arguments carry them
+    if (inline_sp) {
+        for (size_t k = 0; k < s.size(); ++k) mp.spi[k] = s[k];
+    } else {
+        rc = grow(ctx, &ctx->match_sp, &ctx->match_cap, s.size() * sizeof(ScanPatch), false);
+        if (rc) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->match_sp, s.data(), s.size() * sizeof(ScanPatch), hipMemcpyHostToDevice, ctx->stream));
+        mp.sp = (const ScanPatch*)ctx->match_sp;
+    }
     HIPCHK(ctx, eslam_launch_map_match(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
-    // the host's copy of the patches may go away when this returns
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    // a scan of more than 640 patches: the host's copy of the sampled ones goes away on return
+    if (!inline_sp) HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return ESLAM_OK;
 }
 

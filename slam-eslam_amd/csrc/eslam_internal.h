@@ -275,7 +275,8 @@ struct MatchParams {
     uint64_t n;
     uint32_t m;                          // the sampled patches in sp
     uint32_t is_id;                      // the grid's global2local is the identity
-    const ScanPatch* sp;                 // device copy of the sampled patches
+    const ScanPatch* sp;                 // device copy of the sampled patches (more than kMaxScanPatches)
+    ScanPatch spi[kMaxScanPatches];      // else the sampled patches themselves (sp null)
 };
 constexpr int kLmBlock = 128;                   // particles per block of the page plan (k_map_plan, k_recv_plan)
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots

@@ -2417,7 +2417,7 @@ __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, 
     double sum = 0.0;
     uint32_t cnt = 0;
     for (uint32_t k = 0; k < mp.m; ++k) {
-        const ScanPatch sp = mp.sp[k];
+        const ScanPatch sp = mp.sp ? mp.sp[k] : mp.spi[k];
         const double wz = sp.z + z;
         uint32_t cm, cn;
         if (mp.is_id) {

@@ -339,3 +339,44 @@ def test_particle_maps_match_bit_exact(gpu_mod, oracle, case):
         assert_bit_identical(gpu.download(), orc.download(), f"{case} step {k}")
     assert np.array_equal(gpu.ancestors(), orc.ancestors())
     assert lowered > n                                # the probe scan sits 3 cm above the maps
+
+
+def test_particle_maps_match_edges(gpu_mod, oracle):
+    """eslam_gpu_map_match's edges: an empty scan (weight 1: weights unchanged, bit for bit), a
+    scan of fewer than 10 patches (only patch 0 sampled), non-finite patches and a filter with
+    the shared map only (ESLAM_ERR_INVALID_ARG, nothing changed)."""
+    n = 700
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS
+    grid = S.unmapped_beyond(S.flat_map(cells=80), 0.3)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    scan = S.scan_patches()
+    for st in S.step_stream(3):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+    w0 = gpu.download().weight.copy()
+    empty = (A.ScanPatch * 0)()
+    gpu.map_match(empty)
+    orc.map_match(empty)
+    assert np.array_equal(gpu.download().weight, w0)
+    few = S.scan_patches(nx=3, ny=3, z=-0.12)           # 9 patches: patch 0 alone is sampled
+    gpu.map_match(few)
+    orc.map_match(few)
+    assert_bit_identical(gpu.download(), orc.download(), "9-patch match")
+    bad = S.scan_patches(nx=2, ny=2)
+    bad[1].position[2] = float("nan")
+    w1 = gpu.download().weight.copy()
+    with pytest.raises(gpu_mod.EslamError):
+        gpu.map_match(bad)
+    assert np.array_equal(gpu.download().weight, w1)
+    shared = gpu_mod.GpuFilter(S.bench_config(A.default_config(), n))
+    shared.set_map(grid)
+    shared.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    with pytest.raises(gpu_mod.EslamError):
+        shared.map_match(scan)
+    shared.close()
