@@ -2391,7 +2391,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 // its window and the window the update centres on the particle -- scores
 // exp(-d^2 / (2 sigma^2)), sigma 0.2f (src/EmbodiedSlamFilter.cpp:217); the particle's weight
 // is multiplied by pow(weight, 0.1f), weight the float mean score (1 without a matched cell).
-// A lane per particle: a handful of lookups each (the sampled patches, scalar loads).
+// A lane per particle: a handful of lookups each (the sampled patches from the kernel
+// arguments, scalar loads).
 __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
                                                       LocalMaps lm, MatchParams mp)
 {
@@ -2399,7 +2400,7 @@ __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, 
     if (i >= mp.n) return;
     const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
     const uint32_t X = st.sid[i];
-    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i];
+    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], w = st.w[i];
     const double bx = x - map.offset_x, by = y - map.offset_y;
     if (!(dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(th))) return;
     double sn, co;
@@ -2416,38 +2417,59 @@ __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, 
     const int2 c = lm.ctr[X];
     double sum = 0.0;
     uint32_t cnt = 0;
-    for (uint32_t k = 0; k < mp.m; ++k) {
-        const ScanPatch sp = mp.sp ? mp.sp[k] : mp.spi[k];
-        const double wz = sp.z + z;
-        uint32_t cm, cn;
-        if (mp.is_id) {
-            if (dm_merge_cell_mn(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width, map.height_cells,
-                                 &cm, &cn) == 0xffffffffu)
-                continue;
-        } else {
-            const double wx = (co * sp.x + (-sn) * sp.y) + x;
-            const double wy = (sn * sp.x + co * sp.y) + y;
-            const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
-            const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
-            const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
-            const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
-            if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
-            cm = (uint32_t)fm;
-            cn = (uint32_t)fn;
+    // kMatchBatch patches at a time: their table slots, then their cells, each batch of loads
+    // in flight together (one patch after another was two dependent round trips per patch);
+    // the scores are added in patch order
+    constexpr uint32_t kMatchBatch = 8;
+    for (uint32_t k0 = 0; k0 < mp.m; k0 += kMatchBatch) {
+        uint32_t pg[kMatchBatch], cj[kMatchBatch];
+        double wzs[kMatchBatch];
+#pragma unroll
+        for (uint32_t q = 0; q < kMatchBatch; ++q) {
+            const uint32_t k = k0 + q;
+            pg[q] = DM_LM_NONE;
+            cj[q] = 0;
+            wzs[q] = 0.0;
+            if (k >= mp.m) continue;
+            const ScanPatch sp = mp.sp ? mp.sp[k] : mp.spi[k];
+            const double wz = sp.z + z;
+            wzs[q] = wz;
+            uint32_t cm, cn;
+            if (mp.is_id) {
+                if (dm_merge_cell_mn(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
+                                     map.height_cells, &cm, &cn) == 0xffffffffu)
+                    continue;
+            } else {
+                const double wx = (co * sp.x + (-sn) * sp.y) + x;
+                const double wy = (sn * sp.x + co * sp.y) + y;
+                const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
+                const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
+                const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
+                if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
+                cm = (uint32_t)fm;
+                cn = (uint32_t)fn;
+            }
+            const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+            if (!dm_lm_inside(a, na, lm.hx, lm.wx) || !dm_lm_inside(b, nb, lm.hy, lm.wy)) continue;
+            if (!dm_lm_inside(a, c.x, lm.hx, lm.wx) || !dm_lm_inside(b, c.y, lm.hy, lm.wy)) continue;
+            pg[q] = lm.slot[(uint64_t)X * lm.S + lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my)];
+            cj[q] = (cm & 7u) + 8u * (cn & 7u);
         }
-        const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
-        if (!dm_lm_inside(a, na, lm.hx, lm.wx) || !dm_lm_inside(b, nb, lm.hy, lm.wy)) continue;
-        if (!dm_lm_inside(a, c.x, lm.hx, lm.wx) || !dm_lm_inside(b, c.y, lm.hy, lm.wy)) continue;
-        const uint32_t pg = lm.slot[(uint64_t)X * lm.S + lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my)];
-        if (pg == DM_LM_NONE) continue;
-        const float2 cv = lm.page[(uint64_t)pg * DM_LM_PAGE_CELLS + (cm & 7u) + 8u * (cn & 7u)];
-        if (!dm_lm_holds(cv.y)) continue;
-        const double d = wz - (double)cv.x;
-        sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
-        ++cnt;
+        float2 cv[kMatchBatch];
+#pragma unroll
+        for (uint32_t q = 0; q < kMatchBatch; ++q)
+            cv[q] = pg[q] != DM_LM_NONE ? lm.page[(uint64_t)pg[q] * DM_LM_PAGE_CELLS + cj[q]] : make_float2(0.0f, -1.0f);
+#pragma unroll
+        for (uint32_t q = 0; q < kMatchBatch; ++q) {
+            if (pg[q] == DM_LM_NONE || !dm_lm_holds(cv[q].y)) continue;
+            const double d = wzs[q] - (double)cv[q].x;
+            sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
+            ++cnt;
+        }
     }
     const float wf = cnt ? (float)(sum / (double)cnt) : 1.0f;
-    st.w[i] = st.w[i] * dm_pow((double)wf, (double)0.1f);
+    st.w[i] = w * dm_pow((double)wf, (double)0.1f);
 }
 
 // the merge's statistics slots -> ctl (one block of kMergeCounterSlots threads); the free
