@@ -191,12 +191,13 @@ def test_map_update_needs_the_flag(gpu_mod):
         gpu.map_update(S.scan_patches())
 
 
-@pytest.mark.parametrize("kind", ["current", "empty"])
-def test_particle_maps_bench_workload(gpu_mod, oracle, kind):
+@pytest.mark.parametrize("kind,match", [("current", False), ("empty", False), ("current", True)])
+def test_particle_maps_bench_workload(gpu_mod, oracle, kind, match):
     """bench.py --local-maps' workload (configs[4]'s terrain: rough multi-patch map, unmapped
     beyond x = 0.3 m -- or the reference's empty start --, tilted body, one map update per
-    step) at 256k particles on the 1000 x 1000 map: bit-exact against the oracle (16 threads)
-    for 4 steps, and the maps of sampled particles equal."""
+    step; with match, `--local-maps --match`: the match weighting before every merge) at 256k
+    particles on the 1000 x 1000 map: bit-exact against the oracle (16 threads) for 4 steps,
+    and the maps of sampled particles equal."""
     n = 262144
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS
@@ -210,10 +211,13 @@ def test_particle_maps_bench_workload(gpu_mod, oracle, kind):
     scan = S.scan_patches()
     for k, st in enumerate(S.step_stream(4, tilt=True)):
         assert gpu.step(st) == orc.step(st)
+        if match:
+            gpu.map_match(scan)
+            orc.map_match(scan)
         gpu.map_update(scan)
         orc.map_update(scan)
         assert map_info(gpu.sync()) == map_info(orc.info()), k
-    assert_bit_identical(gpu.download(), orc.download(), f"local maps 256k ({kind} prior)")
+    assert_bit_identical(gpu.download(), orc.download(), f"local maps 256k ({kind} prior, match {match})")
     assert_maps_equal(gpu, orc, [0, 1, 4097, n // 2, n - 1], "256k")
     if kind == "current":
         assert np.mean(gpu.download().n_contact_points >= 2) > 0.1
