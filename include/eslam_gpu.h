@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 5
+#define ESLAM_ABI_VERSION 6
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -461,6 +461,9 @@ typedef struct eslam_kernel_times {
     float map_merge_ms;
     float map_total_ms;
     float map_plan_ms;
+    /* eslam_gpu_map_match (ABI 6): the call's gather and k_map_match, averaged over the
+     * matches of the timed region                                                         */
+    float map_match_ms;
 } eslam_kernel_times;
 int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable);
 int eslam_gpu_get_kernel_times(eslam_ctx* ctx, eslam_kernel_times* t);

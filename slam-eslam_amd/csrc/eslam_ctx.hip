@@ -385,6 +385,8 @@ struct eslam_ctx {
     uint32_t ring_steps = 0;
     std::vector<hipEvent_t> mring;          // 5 events per recorded map update (timing mode)
     uint32_t mring_steps = 0;
+    std::vector<hipEvent_t> xring;          // 2 events per recorded map match (timing mode)
+    uint32_t xring_steps = 0;
     eslam_kernel_times times = {};
 };
 
@@ -445,6 +447,19 @@ static void mrec(eslam_ctx* ctx, int k)
     if (ctx->mring_steps >= kRingSteps) return;
     (void)hipEventRecord(ctx->mring[5 * ctx->mring_steps + k], ctx->stream);
     if (k == 4) ctx->mring_steps++;
+}
+
+// timing mode: event k (0: start, 1: end) of the current map match
+static void xrec(eslam_ctx* ctx, int k)
+{
+    if (!ctx->timing) return;
+    if (ctx->xring.empty()) {
+        ctx->xring.resize(2 * kRingSteps);
+        for (auto& e : ctx->xring) (void)hipEventCreate(&e);
+    }
+    if (ctx->xring_steps >= kRingSteps) return;
+    (void)hipEventRecord(ctx->xring[2 * ctx->xring_steps + k], ctx->stream);
+    if (k == 1) ctx->xring_steps++;
 }
 
 static int fail(eslam_ctx* ctx, int code, const char* msg)
@@ -706,6 +721,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->mring) if (e) (void)hipEventDestroy(e);
+    for (auto& e : ctx->xring) if (e) (void)hipEventDestroy(e);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1797,6 +1813,7 @@ extern "C" int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patch
         if (!dm_isfinite(patches[k].position[0]) || !dm_isfinite(patches[k].position[1]) ||
             !dm_isfinite(patches[k].position[2]) || !dm_isfinite(patches[k].stdev))
             return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_match: scan patches must be finite");
+    xrec(ctx, 0);
     int rc = materialize(ctx);                // the weights of the particles as they stand
     if (rc) return rc;
     std::vector<ScanPatch> s;
@@ -1817,6 +1834,7 @@ extern "C" int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patch
         mp.sp = (const ScanPatch*)ctx->match_sp;
     }
     HIPCHK(ctx, eslam_launch_map_match(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
+    xrec(ctx, 1);
     // a scan of more than 640 patches: the host's copy of the sampled ones goes away on return
     if (!inline_sp) HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return ESLAM_OK;
@@ -2659,6 +2677,16 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         t.map_total_ms = (float)(acc[4] * inv);
         ctx->mring_steps = 0;
     }
+    if (ctx->timing && ctx->xring_steps) {
+        double acc = 0;
+        for (uint32_t k = 0; k < ctx->xring_steps; ++k) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ctx->xring[2 * k], ctx->xring[2 * k + 1]);
+            acc += ms;
+        }
+        ctx->times.map_match_ms = (float)(acc / ctx->xring_steps);
+        ctx->xring_steps = 0;
+    }
     return take_update_error(ctx);
 }
 
@@ -2859,6 +2887,7 @@ extern "C" int eslam_gpu_enable_timing(eslam_ctx* ctx, int enable)
     ctx->timing = enable != 0;
     ctx->ring_steps = 0;
     ctx->mring_steps = 0;
+    ctx->xring_steps = 0;
     return ESLAM_OK;
 }
 

@@ -201,6 +201,7 @@ class KernelTimes(C.Structure):
         ("map_merge_ms", C.c_float),
         ("map_total_ms", C.c_float),
         ("map_plan_ms", C.c_float),
+        ("map_match_ms", C.c_float),
     ]
 
 
