@@ -238,14 +238,26 @@ def flat_scan(dz=0.0, **kw):
     return scan
 
 
-def test_match_weights_against_own_map(oracle):
+@pytest.mark.parametrize("rotated", [False, True])
+def test_match_weights_against_own_map(oracle, rotated):
     """processMap(scanMap, match = true) (src/EmbodiedSlamFilter.cpp:214-221; the match rule is
     the build's own, envire's MLSGrid::match not being in the reference -- parity unpinned):
     against maps holding a flat scan, the same scan scores 1 on every cell (weights unchanged,
     bit for bit), a scan dz higher multiplies each matched particle's weight by
     float(exp(-dz^2 / (2 * 0.2f^2)))^0.1f and leaves the unmatched ones as they are, and only
-    every 10th patch counts (sampling 10)."""
-    f, _ = setup()
+    every 10th patch counts (sampling 10).  rotated: a grid whose global2local is a rotation and
+    a shift (every cell placed through the transform)."""
+    if rotated:
+        cfg = S.bench_config(A.default_config(), 600)
+        cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
+        grid = S.unmapped_beyond(S.flat_map(cells=60), 0.3)
+        c, s = math.cos(0.3), math.sin(0.3)
+        grid.g2l = [c, s, 0.0, -(c * 0.4 + s * -0.25), -s, c, 0.0, -(-s * 0.4 + c * -0.25), 0.0, 0.0, 1.0, 0.0]
+        f = O.OracleFilter(cfg, O.SUM_CONTRACT)
+        f.set_map(grid)
+        f.init_gaussian(600, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    else:
+        f, _ = setup()
     f.step(S.step_stream(1)[0])                          # the weights of an update (init leaves 0)
     w_empty = f.download().weight.copy()
     assert np.all(w_empty > 0)
