@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 6
+#define ESLAM_ABI_VERSION 7
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -87,6 +87,12 @@ typedef struct eslam_config {
     /* Configuration::maxSensorRange (3.0, src/Configuration.hpp:107): a particle's own map keeps
      * the tiles of 8 x 8 cells within this range of the particle             */
     double max_sensor_range;
+    /* per-particle maps (ABI 7): tiles a map keeps after its window has left them (the trail;
+     * the reference's MLSMap keeps every grid it made, src/EmbodiedSlamFilter.cpp:195-207), up
+     * to this many per map (default 16; 0: tiles leaving the window are forgotten).  Their
+     * pages come from the same pool (local_map_pages).                                       */
+    uint32_t local_map_trail;
+    uint32_t pad_trail;
 } eslam_config;
 
 #define ESLAM_FLAG_RECORD_ANCESTORS 0x1u   /* keep the last resample's ancestor indices     */
@@ -187,6 +193,9 @@ typedef struct eslam_update_info {
     uint64_t map_cells_written;
     uint64_t map_pages_taken;
     uint64_t map_pages_free;
+    /* (ABI 7) tiles the last map update's windows left that a full trail could not keep
+     * (forgotten; summed over the particles; in the oracle too)                              */
+    uint64_t map_tiles_evicted;
 } eslam_update_info;
 
 /* ---- lifecycle ------------------------------------------------------------------------ */

@@ -279,6 +279,7 @@ struct Configuration {
     unsigned int logParticlePeriod = 100;
     uint32_t flags = 0;                   // build-specific ESLAM_FLAG_* (not in the reference)
     uint32_t localMapPages = 0;           // build-specific: per-particle map page pool per particle (0: 16)
+    uint32_t localMapTrail = 16;          // build-specific: tiles a particle's map keeps behind its window
 
     // the fields the MI355X path consumes, as the C ABI's POD (hash: the init() argument)
     eslam_config toC(const SurfaceHashConfig& hash = SurfaceHashConfig()) const
@@ -316,6 +317,7 @@ struct Configuration {
         c.flags = flags;
         c.max_sensor_range = maxSensorRange;       // the reach of a particle's own map
         c.local_map_pages = localMapPages;
+        c.local_map_trail = localMapTrail;
         return c;
     }
 };
@@ -968,10 +970,10 @@ public:
     // processMap(scanMap, match, update)  src/EmbodiedSlamFilter.cpp:179-232 with the scan's
     // MLS as patches: update merges them into every particle's own map (useSharedMap = false;
     // the reference's update-only call, src/EmbodiedSlamFilter.cpp:340-342); match weights every
-    // particle against its own map first (the build's match rule, eslam_gpu_map_match)
+    // particle against its map first -- the shared grid (useSharedMap = true: the laser path's
+    // match-only call, :342-344) or its own map (the build's match rule, eslam_gpu_map_match)
     void processMap(const std::vector<ScanPatch>& scanMap, bool match, bool update)
     {
-        if (match && sharedMap_) throw std::runtime_error("processMap: match needs per-particle maps (useSharedMap = false)");
         if (match) estimator().matchMaps(scanMap);
         if (update && !sharedMap_) estimator().updateMaps(scanMap);
     }

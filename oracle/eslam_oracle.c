@@ -176,7 +176,12 @@ int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean_w
     double fm = floor((lx - g->offset_x) * inv_x);
     double fn = floor((ly - g->offset_y) * inv_y);
     if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) return 0;
-    uint64_t cell = (uint64_t)fn * g->width + (uint64_t)fm;
+    return or_mls_cell_patch(g, (uint64_t)fn * g->width + (uint64_t)fm, q_mean, q_var, mean, stdev);
+}
+
+/* the first patch of grid cell `cell` passing the 3-sigma gate against the local height q_mean */
+int or_mls_cell_patch(const eslam_mls_grid* g, uint64_t cell, double q_mean, double q_var, double* mean, double* stdev)
+{
     uint32_t b = g->cell_start[cell], e = g->cell_start[cell + 1];
     for (uint32_t k = b; k < e; ++k) {
         double pm = (double)g->patch_mean[k];
@@ -213,14 +218,105 @@ typedef struct { float v[2 * DM_LM_PAGE_CELLS]; } or_page;
 typedef struct {
     const eslam_mls_grid* g;
     const int32_t* ctr;                  /* the particle's window centre (2 tiles)         */
-    const uint32_t* slot;                /* its slots (page or DM_LM_NONE)                  */
+    const uint32_t* slot;                /* its row: slots (page or DM_LM_NONE), then trail */
     or_page* const* blk;                 /* page blocks                                     */
     uint32_t hx, hy, wx, wy;
+    uint32_t V;                          /* trail entries after the wx * wy slots           */
 } or_pmap;
 
 static const or_page* lm_page(or_page* const* blk, uint32_t p)
 {
     return blk[p >> OR_PAGE_BLOCK_BITS] + (p & ((1u << OR_PAGE_BLOCK_BITS) - 1u));
+}
+
+/* ---- the trail: a map's tiles outside its window ------------------------
+ * The reference's per-particle MLSMap keeps every grid it has made; selectActiveGrid only
+ * changes which one is active (src/EmbodiedSlamFilter.cpp:195-207).  Here the window holds the
+ * tiles around the particle and the trail the tiles it left: V entries {a, b, page} after the
+ * row's S slots (page DM_LM_NONE: an empty entry).  A tile is never in both.  When the window
+ * moves, (1) the tiles leaving it go to the trail in slot order, each into the first empty
+ * entry, or -- the trail full -- in place of the entry farthest from the new centre (Chebyshev
+ * distance in tiles; the first such entry) when that one is farther than the tile itself,
+ * which is otherwise the one forgotten; (2) every trail entry whose tile lies inside the new
+ * window goes back to its slot.  A returning tile is never the one forgotten: it lies within
+ * the window's reach of the new centre, every leaving tile beyond it.  Forgotten tiles are
+ * counted (map_tiles_evicted).                                                              */
+static int lm_trail_find(const uint32_t* trail, uint32_t V, int64_t a, int64_t b)
+{
+    for (uint32_t e = 0; e < V; ++e) {
+        const uint32_t* t = trail + 3 * e;
+        if (t[2] != DM_LM_NONE && (int64_t)(int32_t)t[0] == a && (int64_t)(int32_t)t[1] == b) return (int)e;
+    }
+    return -1;
+}
+
+static int64_t lm_cheb(int64_t a, int64_t b, int64_t na, int64_t nb)
+{
+    const int64_t da = llabs(a - na), db = llabs(b - nb);
+    return da > db ? da : db;
+}
+
+/* one tile into the trail; returns 1 when a tile was forgotten */
+static uint32_t lm_trail_push(uint32_t* trail, uint32_t V, int32_t na, int32_t nb, int64_t a, int64_t b, uint32_t pg)
+{
+    int64_t far = -1;
+    uint32_t fe = 0;
+    for (uint32_t e = 0; e < V; ++e) {
+        uint32_t* t = trail + 3 * e;
+        if (t[2] == DM_LM_NONE) {
+            t[0] = (uint32_t)(int32_t)a; t[1] = (uint32_t)(int32_t)b; t[2] = pg;
+            return 0;
+        }
+        const int64_t d = lm_cheb((int32_t)t[0], (int32_t)t[1], na, nb);
+        if (d > far) { far = d; fe = e; }
+    }
+    if (V && far > lm_cheb(a, b, na, nb)) {
+        uint32_t* t = trail + 3 * fe;
+        t[0] = (uint32_t)(int32_t)a; t[1] = (uint32_t)(int32_t)b; t[2] = pg;
+    }
+    return 1;
+}
+
+/* the window of row (S = wx * wy slots, then the trail) moves from ctr to (na, nb); returns
+ * the tiles forgotten */
+static uint32_t lm_recentre(uint32_t* row, int32_t* ctr, int32_t na, int32_t nb, uint32_t hx, uint32_t hy,
+                            uint32_t wx, uint32_t wy, uint32_t V)
+{
+    const uint32_t S = wx * wy;
+    uint32_t* trail = row + S;
+    uint32_t forgot = 0;
+    if (ctr[0] != DM_LM_UNSET) {
+        for (uint32_t sb = 0; sb < wy; ++sb)           /* (1) the leaving tiles, slot order */
+            for (uint32_t sa = 0; sa < wx; ++sa) {
+                const int64_t a = dm_lm_tile_of(sa, ctr[0], hx, wx), b = dm_lm_tile_of(sb, ctr[1], hy, wy);
+                if (llabs(a - (int64_t)na) <= (int64_t)hx && llabs(b - (int64_t)nb) <= (int64_t)hy) continue;
+                uint32_t* e = &row[sa + wx * sb];
+                if (*e == DM_LM_NONE) continue;
+                forgot += lm_trail_push(trail, V, na, nb, a, b, *e);
+                *e = DM_LM_NONE;
+            }
+        for (uint32_t e = 0; e < V; ++e) {              /* (2) the returning tiles */
+            uint32_t* t = trail + 3 * e;
+            const int64_t a = (int32_t)t[0], b = (int32_t)t[1];
+            if (t[2] == DM_LM_NONE || llabs(a - (int64_t)na) > (int64_t)hx || llabs(b - (int64_t)nb) > (int64_t)hy) continue;
+            row[(uint32_t)(a % wx) + wx * (uint32_t)(b % wy)] = t[2];
+            t[2] = DM_LM_NONE;
+        }
+    }
+    ctr[0] = na;
+    ctr[1] = nb;
+    return forgot;
+}
+
+/* the page of tile (a, b) in a particle's map: its slot when the tile is inside the window
+ * centred at ctr, else its trail entry (DM_LM_NONE: the map does not hold it)              */
+static uint32_t lm_tile_page(const uint32_t* row, const int32_t* ctr, uint32_t hx, uint32_t hy, uint32_t wx, uint32_t wy,
+                             uint32_t V, uint32_t a, uint32_t b)
+{
+    if (ctr[0] == DM_LM_UNSET) return DM_LM_NONE;
+    if (dm_lm_inside(a, ctr[0], hx, wx) && dm_lm_inside(b, ctr[1], hy, wy)) return row[(a % wx) + wx * (b % wy)];
+    const int k = lm_trail_find(row + wx * wy, V, a, b);
+    return k >= 0 ? row[wx * wy + 3 * k + 2] : DM_LM_NONE;
 }
 
 /* per-particle maps: GridAccess::get on the particle's own map = the shared grid, and for a
@@ -246,8 +342,7 @@ static int particle_map_fn(void* user, const double p[3], double q_mean, double 
     const uint32_t m = (uint32_t)fm, n = (uint32_t)fn, cell = n * g->width + m;
     if (g->cell_start[cell] != g->cell_start[cell + 1]) return 0;       /* the grid's cell: no patch passed */
     const uint32_t a = m >> DM_LM_TILE_BITS, b = n >> DM_LM_TILE_BITS;
-    if (!dm_lm_inside(a, pm->ctr[0], pm->hx, pm->wx) || !dm_lm_inside(b, pm->ctr[1], pm->hy, pm->wy)) return 0;
-    const uint32_t pg = pm->slot[(a % pm->wx) + pm->wx * (b % pm->wy)];
+    const uint32_t pg = lm_tile_page(pm->slot, pm->ctr, pm->hx, pm->hy, pm->wx, pm->wy, pm->V, a, b);
     if (pg == DM_LM_NONE) return 0;
     const uint32_t j = (m & 7u) + 8u * (n & 7u);
     const float* v = lm_page(pm->blk, pg)->v;
@@ -597,8 +692,12 @@ struct or_filter {
      * the shared grid leaves empty; sized from the map at set_map / init     */
     int lm_on;                           /* pm_ctr / pm_slot allocated for the current map    */
     uint32_t lm_hx, lm_hy, lm_wx, lm_wy, lm_S;
+    uint32_t lm_V;                       /* trail entries per map (eslam_config::local_map_trail) */
+    uint64_t lm_R;                       /* words per particle's row: S slots + V trail entries
+                                            {a, b, page} (lm_row)                               */
     int32_t* pm_ctr;                     /* n x 2: window centre tile (DM_LM_UNSET: none)     */
-    uint32_t* pm_slot;                   /* n x S: page index or DM_LM_NONE                   */
+    uint32_t* pm_slot;                   /* n rows of lm_R words: the S window slots (page index
+                                            or DM_LM_NONE), then the trail       */
     or_page** pg_blk;                    /* OR_PAGE_BLOCKS block pointers                      */
     uint32_t pg_nblk;                    /* blocks allocated                                   */
     uint64_t pg_top;                     /* pages [0, pg_top) handed out at least once         */
@@ -690,14 +789,16 @@ static int lm_reset(or_filter* f)
     f->lm_wx = 2 * f->lm_hx + 1;
     f->lm_wy = 2 * f->lm_hy + 1;
     f->lm_S = f->lm_wx * f->lm_wy;
+    f->lm_V = f->cfg.local_map_trail;
+    f->lm_R = (uint64_t)f->lm_S + 3ull * f->lm_V;
     const uint64_t n = f->n;
     f->pm_ctr = malloc(n * 2 * sizeof(int32_t));
-    f->pm_slot = malloc(n * f->lm_S * sizeof(uint32_t));
+    f->pm_slot = malloc(n * f->lm_R * sizeof(uint32_t));
     f->pm_id = malloc(n * 8);
     f->pg_blk = calloc(OR_PAGE_BLOCKS, sizeof(or_page*));
     if (!f->pm_ctr || !f->pm_slot || !f->pm_id || !f->pg_blk) return ESLAM_ERR_OUT_OF_MEMORY;
     for (uint64_t i = 0; i < 2 * n; ++i) f->pm_ctr[i] = DM_LM_UNSET;
-    memset(f->pm_slot, 0xff, n * f->lm_S * sizeof(uint32_t));
+    memset(f->pm_slot, 0xff, n * f->lm_R * sizeof(uint32_t));
     for (uint64_t i = 0; i < n; ++i) f->pm_id[i] = f->gbase + i;
     f->pm_fresh = (1ull << 63) | ((uint64_t)f->gbase << 32);
     f->lm_on = 1;
@@ -1316,8 +1417,8 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
         double T[12] = {co, -s, 0.0, f->x[OD(i)], s, co, 0.0, f->y[OD(i)], 0.0, 0.0, r22, f->z[OD(i)]};
         const double meas_var = f->literal ? pow(f->zs[OD(i)], 2) + pow(c->measurement_error, 2) : f->zs[OD(i)] * f->zs[OD(i)] + me2;
         or_pmap pmc = {&f->map, f->lm_on ? f->pm_ctr + 2 * (uint64_t)i : NULL,
-                       f->lm_on ? f->pm_slot + (uint64_t)i * f->lm_S : NULL, f->pg_blk, f->lm_hx, f->lm_hy, f->lm_wx,
-                       f->lm_wy};
+                       f->lm_on ? f->pm_slot + (uint64_t)i * f->lm_R : NULL, f->pg_blk, f->lm_hx, f->lm_hy, f->lm_wx,
+                       f->lm_wy, f->lm_V};
         int acc = f->lm_on ? or_cm_evaluate_pose(&cm, T, meas_var, particle_map_fn, &pmc)
                             : or_cm_evaluate_pose(&cm, T, meas_var, grid_map_fn, &f->map);
         if (acc < 0) { zero_var = 1; acc = 0; }
@@ -1506,7 +1607,7 @@ static void gather(or_filter* f, const uint32_t* anc, uint64_t samples)
 #endif
     if (f->lm_on) {                       /* a copied particle carries its map (cloneMaps: the
                                              slots are copied, the pages shared until written) */
-        const uint64_t S = f->lm_S;
+        const uint64_t S = f->lm_R;          /* the slots and the trail */
         int32_t* nc = malloc(samples * 2 * sizeof(int32_t));
         uint32_t* ns = malloc(samples * S * sizeof(uint32_t));
         uint64_t* nid = malloc(samples * 8);
@@ -1572,13 +1673,16 @@ typedef struct {
     uint64_t lo, hi, src;          /* global output range, global source index */
     uint8_t floating, ncp, pad[6];
     /* per-particle maps: the source particle's map travels with it (a deep copy): its window
-     * centre here, its npg pages in the payload stream (or_mig_page each, in slot order)   */
+     * centre here, its npg pages in the payload stream (or_mig_page each: the window's in slot
+     * order, then the trail's in entry order)                                             */
     int32_t pm_ctr[2];
     uint32_t pm_npg, pm_pad;
     uint64_t pm_id;
 } or_mig;
 typedef struct {
-    uint32_t slot, pad;
+    uint32_t slot;                 /* < S: a window slot; S + e: trail entry e of tile (a, b) */
+    int32_t a, b;
+    uint32_t pad;
     or_page page;
 } or_mig_page;
 
@@ -1637,7 +1741,9 @@ static void resample_sharded(or_filter* f, int shift)
                 m->pm_id = f->pm_id[i];
                 m->pm_ctr[0] = f->pm_ctr[2 * i];
                 m->pm_ctr[1] = f->pm_ctr[2 * i + 1];
-                for (uint64_t q = 0; q < f->lm_S; ++q) m->pm_npg += f->pm_slot[i * f->lm_S + q] != DM_LM_NONE;
+                const uint32_t* row = f->pm_slot + i * f->lm_R;
+                for (uint64_t q = 0; q < f->lm_S; ++q) m->pm_npg += row[q] != DM_LM_NONE;
+                for (uint32_t e = 0; e < f->lm_V; ++e) m->pm_npg += row[f->lm_S + 3 * e + 2] != DM_LM_NONE;
             }
         }
     /* the maps' pages, in the records' order (one more all_to_all_v of byte counts the
@@ -1653,10 +1759,13 @@ static void resample_sharded(or_filter* f, int shift)
         uint64_t w = 0;
         for (uint64_t r = 0; r < nsend; ++r) {
             const uint64_t i = send[r].src - f->gbase;
-            for (uint32_t sl = 0; sl < f->lm_S; ++sl) {
-                const uint32_t pg = f->pm_slot[i * f->lm_S + sl];
+            const uint32_t* row = f->pm_slot + i * f->lm_R;
+            for (uint32_t sl = 0; sl < f->lm_S + f->lm_V; ++sl) {
+                const uint32_t pg = sl < f->lm_S ? row[sl] : row[f->lm_S + 3 * (sl - f->lm_S) + 2];
                 if (pg == DM_LM_NONE) continue;
                 pay[w].slot = sl;
+                pay[w].a = sl < f->lm_S ? 0 : (int32_t)row[f->lm_S + 3 * (sl - f->lm_S)];
+                pay[w].b = sl < f->lm_S ? 0 : (int32_t)row[f->lm_S + 3 * (sl - f->lm_S) + 1];
                 pay[w].pad = 0;
                 pay[w].page = *lm_pg(f, pg);
                 ++w;
@@ -1714,34 +1823,44 @@ static void resample_sharded(or_filter* f, int shift)
     int32_t* nctr = NULL;
     uint32_t* nslot = NULL;
     if (f->lm_on) {
-        const uint64_t S = f->lm_S;
+        const uint64_t R = f->lm_R, S = f->lm_S;
         nctr = malloc(n * 2 * sizeof(int32_t));
-        nslot = malloc(n * S * 4);
+        nslot = malloc(n * R * 4);
         for (uint64_t o = 0; o < n; ++o) {
             const or_mig* m = &src[o];
             nctr[2 * o] = m->pm_ctr[0];
             nctr[2 * o + 1] = m->pm_ctr[1];
-            uint32_t* sl = nslot + o * S;
+            uint32_t* sl = nslot + o * R;
             if (m->src - f->gbase < n) {
-                memcpy(sl, f->pm_slot + (m->src - f->gbase) * S, S * 4);
+                memcpy(sl, f->pm_slot + (m->src - f->gbase) * R, R * 4);
             } else {
-                memset(sl, 0xff, S * 4);
+                memset(sl, 0xff, R * 4);
                 const uint64_t q0 = rfirst[srcq[o]];
-                for (uint32_t k = 0; k < m->pm_npg; ++k) sl[rpay[q0 + k].slot] = rpg[q0 + k];
+                for (uint32_t k = 0; k < m->pm_npg; ++k) {
+                    const or_mig_page* pp = &rpay[q0 + k];
+                    if (pp->slot < S) {
+                        sl[pp->slot] = rpg[q0 + k];
+                    } else {
+                        uint32_t* t = sl + S + 3 * (pp->slot - S);
+                        t[0] = (uint32_t)pp->a; t[1] = (uint32_t)pp->b; t[2] = rpg[q0 + k];
+                    }
+                }
             }
         }
     }
-    free(rfirst); free(rpg); free(rpay); free(srcq);
     for (uint64_t o = 0; o < n; ++o) {
         const or_mig* m = &src[o];
         f->x[OD(o)] = m->x; f->y[OD(o)] = m->y; f->th[OD(o)] = m->th; f->z[OD(o)] = m->z; f->zs[OD(o)] = m->zs;
         f->w[OD(o)] = m->w; f->mprob[OD(o)] = m->mprob; f->floating[OB(o)] = m->floating; f->ncp[OB(o)] = m->ncp;
         f->anc[o] = anc[o];
         if (f->lm_on) {
-            /* a map from another rank arrives as a copy of its own (the GPU: a table per record) */
-            f->pm_id[o] = m->src - f->gbase < n ? m->pm_id : f->pm_fresh++;
+            /* a map from another rank arrives as a copy of its own, one per record, which the
+             * record's outputs share (the GPU: a table per record that they all name) */
+            f->pm_id[o] = m->src - f->gbase < n ? m->pm_id : f->pm_fresh + srcq[o];
         }
     }
+    if (f->lm_on) f->pm_fresh += nrecv;
+    free(rfirst); free(rpg); free(rpay); free(srcq);
     if (f->lm_on) {
         free(f->pm_ctr); free(f->pm_slot);
         f->pm_ctr = nctr; f->pm_slot = nslot;
@@ -2034,8 +2153,8 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
     static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     int is_id = 1;
     for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
-    const uint64_t S = f->lm_S;
-    const uint32_t hx = f->lm_hx, hy = f->lm_hy, wx = f->lm_wx, wy = f->lm_wy;
+    const uint64_t S = f->lm_S, R = f->lm_R;
+    const uint32_t hx = f->lm_hx, hy = f->lm_hy, wx = f->lm_wx, wy = f->lm_wy, V = f->lm_V;
     /* which particles share their map with another (copies of one map the resample made and
      * no map update has changed since): the ids sorted, a particle's id looked up */
     uint64_t* sorted = malloc((f->n ? f->n : 1) * 8);
@@ -2057,8 +2176,13 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
     free(sorted);
     /* the names every map holds now: a page named once belongs to one particle's map and may
      * be written in place, one named more often is copied first; one named by none is free */
-    for (uint64_t q = 0; q < f->n * S; ++q)
-        if (f->pm_slot[q] != DM_LM_NONE) ref[f->pm_slot[q]]++;
+    for (uint64_t i = 0; i < f->n; ++i) {
+        const uint32_t* row = f->pm_slot + i * R;
+        for (uint64_t q = 0; q < S; ++q)
+            if (row[q] != DM_LM_NONE) ref[row[q]]++;
+        for (uint32_t e = 0; e < V; ++e)
+            if (row[S + 3 * e + 2] != DM_LM_NONE) ref[row[S + 3 * e + 2]]++;
+    }
     f->pg_nfree = 0;
     if (f->pg_free_cap < f->pg_top) {
         free(f->pg_free);
@@ -2068,18 +2192,18 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
     }
     for (uint64_t q = f->pg_top; q-- > 0;)
         if (!ref[q]) f->pg_free[f->pg_nfree++] = (uint32_t)q;
-    uint64_t dropped = 0, changed = 0, covered = 0;
+    uint64_t dropped = 0, changed = 0, covered = 0, evicted = 0;
     int oom = 0;
     const int64_t n = (int64_t)f->n;
     /* particles are independent: the OpenMP threads of or_set_threads (same results) */
-#pragma omp parallel num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed, covered) reduction(| : oom)
+#pragma omp parallel num_threads(f->threads) if (f->threads > 1) reduction(+ : dropped, changed, covered, evicted) reduction(| : oom)
     {
     uint8_t* mine = malloc(S);            /* slot's page made this particle's own in this update */
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
         int dirty = 0;
         int32_t* ctr = f->pm_ctr + 2 * i;
-        uint32_t* sl = f->pm_slot + (uint64_t)i * S;
+        uint32_t* sl = f->pm_slot + (uint64_t)i * R;
         double sn, co;
         dm_sincos(f->th[OD(i)], &sn, &co);
         const double zvar = f->zs[OD(i)] * f->zs[OD(i)];
@@ -2098,18 +2222,8 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
             na = dm_lm_centre(lx, g->offset_x, 1.0 / g->scale_x);
             nb = dm_lm_centre(ly, g->offset_y, 1.0 / g->scale_y);
         }
-        if (ctr[0] != na || ctr[1] != nb) {
-            if (ctr[0] != DM_LM_UNSET) {          /* tiles leaving the window are forgotten */
-                for (uint32_t sb = 0; sb < wy; ++sb)
-                    for (uint32_t sa = 0; sa < wx; ++sa) {
-                        uint32_t* e = &sl[sa + wx * sb];
-                        if (*e == DM_LM_NONE) continue;
-                        const int64_t a = dm_lm_tile_of(sa, ctr[0], hx, wx), b = dm_lm_tile_of(sb, ctr[1], hy, wy);
-                        if (llabs(a - (int64_t)na) > (int64_t)hx || llabs(b - (int64_t)nb) > (int64_t)hy) *e = DM_LM_NONE;
-                    }
-            }
-            ctr[0] = na;
-            ctr[1] = nb;
+        if (ctr[0] != na || ctr[1] != nb) {        /* tiles leaving the window go to the trail */
+            evicted += lm_recentre(sl, ctr, na, nb, hx, hy, wx, wy, V);
             dirty = 1;
         }
         memset(mine, 0, S);
@@ -2190,6 +2304,7 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
     f->info.map_stores_changed += changed;
     f->info.map_stores_copied += copied;
     f->info.map_patches_covered += covered;
+    f->info.map_tiles_evicted += evicted;
     return 0;
 }
 
@@ -2202,6 +2317,7 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 {
     f->info.map_patches_dropped = f->info.map_stores_changed = 0;
     f->info.map_stores_copied = f->info.map_patches_covered = 0;
+    f->info.map_tiles_evicted = 0;
     for (uint32_t c0 = 0; c0 == 0 || c0 < m; c0 += OR_SCAN_PART) {
         const int rc = or_map_update_part(f, sp + c0, m - c0 < OR_SCAN_PART ? m - c0 : OR_SCAN_PART);
         if (rc) return rc;
@@ -2210,36 +2326,42 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 }
 
 /* processMap(scanMap, match = true): the visual weighting p.weight *= pow(weight, 0.1) of
- * src/EmbodiedSlamFilter.cpp:214-221 (sampling 10, sigma 0.2).  envire's MLSGrid::match is
- * not in the reference tree, so this rule is the build's own (parity unpinned):
- * every 10th scan patch, placed like the merge, that lands on a cell of the particle's own
- * map (a tile inside both its current window and the window the update centres on the
- * particle: the reference selects the active grid before matching, :195-207) scores
- * exp(-d^2 / (2 sigma^2)), d = patch height + zPos - the cell's mean; weight = the mean score
- * (1 without a matched cell), a float as in the reference; weight *= pow(weight, 0.1f).     */
+ * src/EmbodiedSlamFilter.cpp:214-221 (sampling 10, sigma 0.2), against the particle's map: the
+ * shared grid (useSharedMap = true, the match-only call of :342-344), or its own map -- the
+ * grid's cells, and its own patches in the cells the grid leaves empty (per-particle maps, the
+ * clone the reference merges into).  envire's MLSGrid::match is not in the reference tree, so
+ * this rule is the build's own (parity unpinned): every 10th scan patch, placed
+ * like the merge (offset patch zPos, zSigma), scores on the cell it lands in --
+ *   a cell of the shared grid: exp(-d^2 / (2 sigma^2)) for the patch getPatch's 3-sigma gate
+ *     picks against the placed patch (d = its local height - the patch's mean), 0 when none
+ *     passes;
+ *   an empty grid cell the particle's own map holds, in a tile inside the window the update
+ *     centres on the particle (the reference selects the active grid before matching,
+ *     :195-207; the tile comes from the window or the trail): exp(-d^2 / (2 sigma^2)),
+ *     d = the patch's height + zPos - the cell's mean;
+ * other patches do not count.  weight = the mean score as a float (1 when none counts);
+ * p.weight *= pow(weight, 0.1f).                                                            */
 int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
 {
-    if (!(f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS)) return ESLAM_ERR_INVALID_ARG;
+    const int pmaps = (f->cfg.flags & ESLAM_FLAG_PARTICLE_MAPS) != 0;
     if (!f->has_map) return ESLAM_ERR_NO_ENVIRONMENT;
     if (!f->n) return ESLAM_ERR_NOT_INITIALISED;
-    if (!f->lm_on) return ESLAM_ERR_OUT_OF_MEMORY;
+    if (pmaps && !f->lm_on) return ESLAM_ERR_OUT_OF_MEMORY;
     const eslam_mls_grid* g = &f->map;
     const double* A = g->global2local;
     static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     int is_id = 1;
     for (int k = 0; k < 12; ++k) is_id &= A[k] == id[k];
-    const uint64_t S = f->lm_S;
-    const uint32_t hx = f->lm_hx, hy = f->lm_hy, wx = f->lm_wx, wy = f->lm_wy;
+    const uint32_t hx = f->lm_hx, hy = f->lm_hy, wx = f->lm_wx, wy = f->lm_wy, V = f->lm_V;
     const int64_t n = (int64_t)f->n;
 #pragma omp parallel for num_threads(f->threads) if (f->threads > 1) schedule(static)
     for (int64_t i = 0; i < n; ++i) {
-        const int32_t* ctr = f->pm_ctr + 2 * i;
-        const uint32_t* sl = f->pm_slot + (uint64_t)i * S;
         double sn, co;
         dm_sincos(f->th[OD(i)], &sn, &co);
         const double bx = f->x[OD(i)] - g->offset_x, by = f->y[OD(i)] - g->offset_y;
         if (!(dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(f->th[OD(i)]))) continue;
-        int32_t na, nb;
+        const double zvar = f->zs[OD(i)] * f->zs[OD(i)];
+        int32_t na = 0, nb = 0;
         if (is_id) {
             na = dm_lm_centre(f->x[OD(i)], g->offset_x, 1.0 / g->scale_x);
             nb = dm_lm_centre(f->y[OD(i)], g->offset_y, 1.0 / g->scale_y);
@@ -2252,6 +2374,7 @@ int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
         uint32_t cnt = 0;
         for (uint32_t k = 0; k < m; k += OR_MATCH_SAMPLING) {
             const double wz = sp[k].position[2] + f->z[OD(i)];
+            double lz = wz;
             uint32_t cm, cn;
             if (is_id) {
                 if (dm_merge_cell_mn(bx, by, co, sn, sp[k].position[0], sp[k].position[1], 1.0 / g->scale_x,
@@ -2262,16 +2385,28 @@ int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
                 const double wy_ = (sn * sp[k].position[0] + co * sp[k].position[1]) + f->y[OD(i)];
                 const double lx = ((A[0] * wx_ + A[1] * wy_) + A[2] * wz) + A[3];
                 const double ly = ((A[4] * wx_ + A[5] * wy_) + A[6] * wz) + A[7];
+                lz = ((A[8] * wx_ + A[9] * wy_) + A[10] * wz) + A[11];
                 const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
                 const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
                 if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) continue;
                 cm = (uint32_t)fm;
                 cn = (uint32_t)fn;
             }
+            const uint64_t cell = (uint64_t)cn * g->width + cm;
+            if (g->cell_start[cell] != g->cell_start[cell + 1]) {        /* a cell of the shared grid */
+                double mean, sd;
+                const double var = sp[k].stdev * sp[k].stdev + zvar;
+                if (or_mls_cell_patch(g, cell, lz, var, &mean, &sd)) {
+                    const double d = lz - mean;
+                    sum += dm_exp(-(d * d) / (2.0 * OR_MATCH_SIGMA * OR_MATCH_SIGMA));
+                }
+                ++cnt;
+                continue;
+            }
+            if (!pmaps) continue;
             const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
             if (!dm_lm_inside(a, na, hx, wx) || !dm_lm_inside(b, nb, hy, wy)) continue;
-            if (!dm_lm_inside(a, ctr[0], hx, wx) || !dm_lm_inside(b, ctr[1], hy, wy)) continue;
-            const uint32_t pg = sl[(a % wx) + wx * (b % wy)];
+            const uint32_t pg = lm_tile_page(f->pm_slot + (uint64_t)i * f->lm_R, f->pm_ctr + 2 * i, hx, hy, wx, wy, V, a, b);
             if (pg == DM_LM_NONE) continue;
             const float* v = lm_pg(f, pg)->v;
             const uint32_t j = (cm & 7u) + 8u * (cn & 7u);
@@ -2286,19 +2421,21 @@ int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     return 0;
 }
 
-/* particle i's own patches, tiles in slot order and each tile's cells in row order (cells
- * n * width + m, mean, stdev); returns how many it holds                                 */
+/* particle i's own patches: the window's tiles in slot order, then the trail's in entry order,
+ * each tile's cells in row order (cells n * width + m, mean, stdev); returns how many it holds */
 uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* mean, float* stdev, uint32_t cap)
 {
     if (!f->lm_on || i >= f->n) return 0;
     const int32_t* ctr = f->pm_ctr + 2 * i;
-    const uint32_t* sl = f->pm_slot + i * f->lm_S;
+    const uint32_t* sl = f->pm_slot + i * f->lm_R;
+    const uint32_t S = f->lm_S;
     uint32_t c = 0;
-    for (uint32_t sb = 0; sb < f->lm_wy; ++sb)
-        for (uint32_t sa = 0; sa < f->lm_wx; ++sa) {
-            const uint32_t pg = sl[sa + f->lm_wx * sb];
+    for (uint32_t s = 0; s < S + f->lm_V; ++s) {
+            const uint32_t pg = s < S ? sl[s] : sl[S + 3 * (s - S) + 2];
             if (pg == DM_LM_NONE) continue;
-            const int64_t a = dm_lm_tile_of(sa, ctr[0], f->lm_hx, f->lm_wx), b = dm_lm_tile_of(sb, ctr[1], f->lm_hy, f->lm_wy);
+            const uint32_t sa = s % f->lm_wx, sb = s / f->lm_wx;
+            const int64_t a = s < S ? dm_lm_tile_of(sa, ctr[0], f->lm_hx, f->lm_wx) : (int32_t)sl[S + 3 * (s - S)];
+            const int64_t b = s < S ? dm_lm_tile_of(sb, ctr[1], f->lm_hy, f->lm_wy) : (int32_t)sl[S + 3 * (s - S) + 1];
             const float* v = lm_pg(f, pg)->v;
             for (uint32_t j = 0; j < DM_LM_PAGE_CELLS; ++j) {
                 if (!dm_lm_holds(v[2 * j + 1])) continue;
@@ -2310,7 +2447,7 @@ uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* m
                 }
                 ++c;
             }
-        }
+    }
     return c;
 }
 
@@ -2320,9 +2457,12 @@ uint64_t or_pages_in_use(or_filter* f)
     if (!f->lm_on) return 0;
     uint8_t* seen = calloc(f->pg_top ? f->pg_top : 1, 1);
     uint64_t c = 0;
-    for (uint64_t q = 0; q < f->n * f->lm_S; ++q) {
-        const uint32_t p = f->pm_slot[q];
-        if (p != DM_LM_NONE && !seen[p]) { seen[p] = 1; ++c; }
+    for (uint64_t i = 0; i < f->n; ++i) {
+        const uint32_t* row = f->pm_slot + i * f->lm_R;
+        for (uint32_t s = 0; s < f->lm_S + f->lm_V; ++s) {
+            const uint32_t p = s < f->lm_S ? row[s] : row[f->lm_S + 3 * (s - f->lm_S) + 2];
+            if (p != DM_LM_NONE && !seen[p]) { seen[p] = 1; ++c; }
+        }
     }
     free(seen);
     return c;

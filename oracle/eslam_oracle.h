@@ -82,6 +82,9 @@ int or_bucket_index(int count, double min_val, double max_val, double value);
 /* ---- MLS grid (envire::MLSGrid::getPatch semantics, see eslam_gpu.h) --------------------- */
 int or_mls_get_patch(const eslam_mls_grid* g, const double p[3], double q_mean, double q_var,
                      double* mean, double* stdev);
+/* the first patch of one grid cell passing the 3-sigma gate against the local height q_mean */
+int or_mls_cell_patch(const eslam_mls_grid* g, uint64_t cell, double q_mean, double q_var, double* mean,
+                      double* stdev);
 
 /* ---- the filter (PoseEstimator + EmbodiedSlamFilter) -------------------------------------- */
 typedef struct or_filter or_filter;
@@ -142,7 +145,8 @@ void or_dm_libc_rand(uint32_t seed, uint32_t n, int32_t* out);     /* glibc rand
 double or_dm_limbs_to_double(const uint64_t L[4], int scale);
 void or_dm_fx128(double v, int scale, uint32_t limbs[4]);
 
-/* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): processMap's merge, and a particle's patches */
+/* per-particle maps (ESLAM_FLAG_PARTICLE_MAPS): processMap's merge, and a particle's patches;
+ * processMap's match weighting on either map (the shared grid, or each particle's own) */
 int or_map_update(or_filter* f, const eslam_scan_patch* patches, uint32_t count);
 int or_map_match(or_filter* f, const eslam_scan_patch* patches, uint32_t count);
 uint32_t or_get_particle_map(or_filter* f, uint64_t i, uint32_t* cells, float* mean, float* stdev, uint32_t cap);

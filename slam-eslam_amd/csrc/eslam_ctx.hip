@@ -510,6 +510,7 @@ extern "C" void eslam_config_default(eslam_config* c)
     c->flags = 0;
     c->local_map_pages = 0;
     c->max_sensor_range = 3.0;
+    c->local_map_trail = 16;
 }
 
 extern "C" const char* eslam_gpu_last_error(const eslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -819,7 +820,11 @@ static int local_maps_reset(eslam_ctx* ctx)
     lm.hy = dm_lm_half(r, ctx->map_scale[1]);
     lm.wx = 2 * lm.hx + 1;
     lm.wy = 2 * lm.hy + 1;
-    lm.S = (lm.wx * lm.wy + 3u) & ~3u;        // slots per table, padded (NONE) to whole 16-byte words
+    if (ctx->cfg.local_map_trail > 4096) return fail(ctx, ESLAM_ERR_INVALID_ARG, "local_map_trail: at most 4096 tiles");
+    lm.V = ctx->cfg.local_map_trail;
+    // a table's row: the window's slots, padded (NONE) to whole 16-byte words, then the trail's
+    // V 16-byte entries
+    lm.S = ((lm.wx * lm.wy + 3u) & ~3u) + 4u * lm.V;
     lm.mx = lm_magic(lm.wx);
     lm.my = lm_magic(lm.wy);
     lm.bx = lm.wx * (((1u << 29) + lm.wx - 1) / lm.wx);
@@ -1134,6 +1139,9 @@ extern "C" int eslam_gpu_set_map(eslam_ctx* ctx, const eslam_mls_grid* g)
     if (g->width == 0 || g->height == 0) return fail(ctx, ESLAM_ERR_NO_MLS_GRID, "The provided environment does not contain an mls grid.");
     const uint64_t ncell = (uint64_t)g->width * g->height;
     if ((uint64_t)g->cell_start[ncell] != g->n_patches) return fail(ctx, ESLAM_ERR_INVALID_ARG, "cell_start[width*height] != n_patches");
+    // a pending resample gather, and on a sharded filter the received maps it names, land in
+    // the old pool first; local_maps_reset below then starts every map over, empty
+    if (const int rc_ = materialize(ctx)) return rc_;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     free_map(ctx);
     const uint64_t np = g->n_patches ? g->n_patches : 1;
@@ -1804,11 +1812,10 @@ extern "C" int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patch
 {
     if (!ctx || (!patches && count)) return ESLAM_ERR_INVALID_ARG;
     if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
-    if (!particle_maps(ctx)) return fail(ctx, ESLAM_ERR_INVALID_ARG, "map_match needs per-particle maps (ESLAM_FLAG_PARTICLE_MAPS)");
     if (!ctx->has_map) return fail(ctx, ESLAM_ERR_NO_ENVIRONMENT, "No environment attached.");
     if (!ctx->n) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "no particles");
     if (const int rc_ = check_poisoned(ctx)) return rc_;
-    if (!ctx->lm_ready) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "per-particle maps not allocated");
+    if (particle_maps(ctx) && !ctx->lm_ready) return fail(ctx, ESLAM_ERR_NOT_INITIALISED, "per-particle maps not allocated");
     for (uint32_t k = 0; k < count; ++k)
         if (!dm_isfinite(patches[k].position[0]) || !dm_isfinite(patches[k].position[1]) ||
             !dm_isfinite(patches[k].position[2]) || !dm_isfinite(patches[k].stdev))
@@ -1833,7 +1840,7 @@ extern "C" int eslam_gpu_map_match(eslam_ctx* ctx, const eslam_scan_patch* patch
         HIPCHK(ctx, hipMemcpyAsync(ctx->match_sp, s.data(), s.size() * sizeof(ScanPatch), hipMemcpyHostToDevice, ctx->stream));
         mp.sp = (const ScanPatch*)ctx->match_sp;
     }
-    HIPCHK(ctx, eslam_launch_map_match(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
+    HIPCHK(ctx, eslam_launch_map_match(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, store_of(ctx), &mp, ctx->stream));
     xrec(ctx, 1);
     // a scan of more than 640 patches: the host's copy of the sampled ones goes away on return
     if (!inline_sp) HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1872,14 +1879,17 @@ extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32
     std::vector<uint32_t> sl(lm.S);
     HIPCHK(ctx, hipMemcpy(&c, lm.ctr + X, sizeof(int2), hipMemcpyDeviceToHost));
     HIPCHK(ctx, hipMemcpy(sl.data(), lm.slot + (uint64_t)X * lm.S, lm.S * 4, hipMemcpyDeviceToHost));
-    // tiles in slot order, each tile's cells row by row (the oracle's or_get_particle_map)
+    // the window's tiles in slot order, then the trail's in entry order, each tile's cells row
+    // by row (the oracle's or_get_particle_map)
     uint32_t k = 0;
     float2 cell[DM_LM_PAGE_CELLS];
-    for (uint32_t sb = 0; sb < lm.wy; ++sb)
-        for (uint32_t sa = 0; sa < lm.wx; ++sa) {
-            const uint32_t pg = sl[sa + lm.wx * sb];
+    const uint32_t W = lm.wx * lm.wy, toff = lm.S - 4u * lm.V;
+    for (uint32_t s = 0; s < W + lm.V; ++s) {
+            const bool tr = s >= W;
+            const uint32_t pg = tr ? sl[toff + 4u * (s - W) + 2u] : sl[s];
             if (pg == DM_LM_NONE) continue;
-            const int64_t a = dm_lm_tile_of(sa, c.x, lm.hx, lm.wx), b = dm_lm_tile_of(sb, c.y, lm.hy, lm.wy);
+            const int64_t a = tr ? (int64_t)(int32_t)sl[toff + 4u * (s - W)] : dm_lm_tile_of(s % lm.wx, c.x, lm.hx, lm.wx);
+            const int64_t b = tr ? (int64_t)(int32_t)sl[toff + 4u * (s - W) + 1u] : dm_lm_tile_of(s / lm.wx, c.y, lm.hy, lm.wy);
             HIPCHK(ctx, hipMemcpy(cell, lm.page + (uint64_t)pg * DM_LM_PAGE_CELLS, sizeof(cell), hipMemcpyDeviceToHost));
             for (uint32_t j = 0; j < DM_LM_PAGE_CELLS; ++j) {
                 if (!dm_lm_holds(cell[j].y)) continue;
@@ -1891,7 +1901,7 @@ extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32
                 }
                 ++k;
             }
-        }
+    }
     *count = k;
     return ESLAM_OK;
 }
@@ -2641,6 +2651,7 @@ extern "C" int eslam_gpu_sync(eslam_ctx* ctx, eslam_update_info* info)
         info->map_stores_changed = c.map_changed;
         info->map_cells_written = c.map_written;
         info->map_pages_taken = c.map_taken;
+        info->map_tiles_evicted = c.map_evicted;
         info->map_pages_free = c.pg_nfree > c.pg_cursor ? c.pg_nfree - c.pg_cursor : 0;
     }
     if (ctx->timing && ctx->ring_steps) {

@@ -82,6 +82,7 @@ struct alignas(128) Ctl {
     uint64_t map_covered;                // scan patches the last map merge saw on cells the shared grid covers
     uint64_t map_written;                // cell writes (inserts and fuses) of the last map merge
     uint64_t map_taken;                  // pages the last map merge took from the free list
+    uint64_t map_evicted;                // tiles the last map update's full trails forgot
     uint64_t pg_cursor;                  // per-particle maps: next unused entry of LocalMaps::frees
     uint64_t pg_nfree;                   //   entries in LocalMaps::frees (the last collection)
     uint64_t pg_total;                   //   pages the current map update may take (its plan)
@@ -107,10 +108,11 @@ struct DevState {
 // Per-particle local maps (useSharedMap = false, ESLAM_FLAG_PARTICLE_MAPS): the
 // shared grid plus, per particle, a window of (2 hx + 1) x (2 hy + 1) tiles of 8 x 8 cells
 // around the particle (eslam_detmath.h DM_LM_*: the window reaches maxSensorRange and moves
-// with the particle at every map update; tiles it leaves are forgotten).
-//   table  what a particle names (DevState::sid): the window centre and S slots (wx * wy, padded
-//          with DM_LM_NONE to a multiple of 4), the
-//          slot of tile (a, b) being (a mod wx) + wx (b mod wy), each a page id or DM_LM_NONE.
+// with the particle at every map update) and a trail of up to V tiles the window has left.
+//   table  what a particle names (DevState::sid): the window centre and a row of S words: the
+//          window's slots (wx * wy, padded with DM_LM_NONE to a multiple of 4; the slot of tile
+//          (a, b) being (a mod wx) + wx (b mod wy), each a page id or DM_LM_NONE), then the
+//          trail's V entries {a, b, page, -} (page DM_LM_NONE: empty; lm_trail_* below).
 //          The resample copies the name, so copies share a table; a map update that changes
 //          a table another particle also names writes the result to a free table the particle
 //          then names (copy on write: a shared table is never written).
@@ -126,8 +128,8 @@ struct LocalMaps {
     int2* ctr;                           // per table: window centre tile (DM_LM_UNSET: an empty table)
     uint32_t* slot;                      // per table: S page ids
     float2* page;                        // per page: 64 cells {mean, stdev}, row-major (m & 7) + 8 (n & 7)
-    uint32_t S, wx, wy, hx;
-    uint32_t hy, pad;
+    uint32_t S, wx, wy, hx;              // S: words per table row (window slots + 4 V)
+    uint32_t hy, V;                      // V: trail entries per table (the last 4 V words of a row)
     uint64_t mx, my;                     // lm_magic(wx), lm_magic(wy)
     // --- the map update and the collection only
     uint32_t bx, by;                     // multiples of wx, wy >= 2^29 (non-negative residues)
@@ -149,10 +151,13 @@ struct alignas(8) MapPayHdr {
     uint32_t npg, pad;
 };
 struct alignas(8) MapPayPage {
-    uint32_t slot, pad;
+    uint32_t slot;                       // a window slot, or kPayTrail | trail entry e of tile (a, b)
+    int32_t a, b;
+    uint32_t pad;
     float2 cell[DM_LM_PAGE_CELLS];
 };
-static_assert(sizeof(MapPayPage) == 520, "payload page");
+static_assert(sizeof(MapPayPage) == 528, "payload page");
+constexpr uint32_t kPayTrail = 0x80000000u;
 // the tables' pool holds 2 x cap tables: at most n <= cap are named by a particle, so at least
 // cap are free whenever a map update starts, and particle i may take the i-th free one (copy
 // on write with a fixed, deterministic allocation of tables and no allocation counter)
@@ -280,7 +285,7 @@ struct MatchParams {
 };
 constexpr int kLmBlock = 128;                   // particles per block of the page plan (k_map_plan, k_recv_plan)
 constexpr uint32_t kMergeCounterSlots = 256;   // the merge's statistics, spread over slots
-constexpr uint32_t kMergeCounters = 6;
+constexpr uint32_t kMergeCounters = 7;
 
 // the store names of both state buffers; the copy-on-write kernels use the current one
 // (base ^ flip read on the device, so the host never waits for the commit)
@@ -322,12 +327,12 @@ inline CowScratch cow_layout(uint32_t* base, uint64_t cap)
 }
 // k_map_plan -> k_map_merge, per particle (one 128-byte record): what the plan decided, so
 // the merge's first memory round trip brings everything its page moves need
-constexpr uint32_t kJobPlaced = 1u, kJobShared = 2u, kJobMore = 4u;    // flags; tiles of pass 1 << 8
+constexpr uint32_t kJobPlaced = 1u, kJobShared = 2u, kJobMore = 4u, kJobMoved = 8u;   // flags; tiles of pass 1 << 8
 struct alignas(16) MergeJob {
     uint32_t X, T;                       // the table the particle names; the table its merge writes
     uint64_t gT;                         // tgen[T] << 32 | T: the owner word of T's pages
     int32_t na, nb;                      // the window's new centre
-    int32_t ox, oy;                      // its old centre (ctr[X])
+    int32_t ox, oy;                      // its old centre (ctr[X]; the plan has moved T's window)
     uint32_t flags;
     uint32_t need;                       // bit r: tile r of pass 1 takes a new page
     uint16_t L[8];                       // pass 1's tiles (slots, ascending)
@@ -343,7 +348,7 @@ struct MergeParams {
     uint32_t is_id;                      // the grid's global2local is the identity
     uint64_t* cnt;                       // kMergeCounters x kMergeCounterSlots: dropped patches, changed
                                          // tables, copies, patches on covered cells, cell writes, pages
-                                         // taken (zeroed)
+                                         // taken, tiles the trail forgot (zeroed)
     const uint32_t* ref;                 // CowScratch::ref of this update
     const uint32_t* frees;               // CowScratch::frees: particle i's table if it writes a shared map
     uint32_t* off;                       // per particle: its first page of the plan within its plan block

@@ -325,22 +325,32 @@ __device__ __forceinline__ bool patch_gate(const gmem<const float>* height, uint
 
 // per-particle maps: the patch of cell (m, n), which the shared grid leaves empty, from the
 // particle's table (K1Args::store) with the same 3-sigma gate as a grid patch:
-// the table's centre and the tile's slot load together, then the page cell
+// the table's centre and the tile's slot load together, then the page cell.  A tile outside
+// the window comes from the table's trail (rare: the window follows the particle).
 __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t m, uint32_t n, double lz, double qv, double& mean,
                                             double& stdev)
 {
-    const su16 h = kl16(KOFF(store));                // 64 bytes: ctr, slot, page, {S, wx}, {wy, hx}, {hy, -}, mx, my
-    const uint64_t w3 = kq(h, 3), w4 = kq(h, 4);
+    const su16 h = kl16(KOFF(store));                // 64 bytes: ctr, slot, page, {S, wx}, {wy, hx}, {hy, V}, mx, my
+    const uint64_t w3 = kq(h, 3), w4 = kq(h, 4), w5 = kq(h, 5);
     const uint32_t S = (uint32_t)w3, wx = (uint32_t)(w3 >> 32), wy = (uint32_t)w4, hx = (uint32_t)(w4 >> 32);
-    const uint32_t hy = (uint32_t)kq(h, 5);
+    const uint32_t hy = (uint32_t)w5, V = (uint32_t)(w5 >> 32);
     const uint32_t a = m >> DM_LM_TILE_BITS, b = n >> DM_LM_TILE_BITS;
     const uint32_t qa = (uint32_t)(((uint64_t)a * kq(h, 6)) >> kLmMagicShift);
     const uint32_t qb = (uint32_t)(((uint64_t)b * kq(h, 7)) >> kLmMagicShift);
     const uint32_t s = (a - wx * qa) + wx * (b - wy * qb);
     const uint64_t c = kp<const uint64_t>(h, 0)[sid];   // int2 {x, y}
-    const uint32_t pg = kp<const uint32_t>(h, 1)[(uint64_t)sid * S + s];
-    if (!dm_lm_inside(a, (int32_t)(uint32_t)c, hx, wx) || !dm_lm_inside(b, (int32_t)(uint32_t)(c >> 32), hy, wy) || pg == DM_LM_NONE)
-        return false;
+    const gmem<const uint32_t>* row = kp<const uint32_t>(h, 1) + (uint64_t)sid * S;
+    uint32_t pg = row[s];
+    if (!dm_lm_inside(a, (int32_t)(uint32_t)c, hx, wx) || !dm_lm_inside(b, (int32_t)(uint32_t)(c >> 32), hy, wy)) {
+        pg = DM_LM_NONE;
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const gmem<const u4>* t = reinterpret_cast<const gmem<const u4>*>(row + (S - 4u * V));
+        for (uint32_t e = 0; e < V; ++e) {
+            const u4 v = t[e];
+            if (v.z != DM_LM_NONE && v.x == a && v.y == b) pg = v.z;
+        }
+    }
+    if (pg == DM_LM_NONE) return false;
     const uint64_t pf = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(h, 2))
         [(uint64_t)pg * DM_LM_PAGE_CELLS + (m & 7u) + 8u * (n & 7u)];
     const float sd = __uint_as_float((uint32_t)(pf >> 32));
@@ -1631,16 +1641,6 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(int mode, uint64_t n, 
     }
 }
 
-// the received particles name their tables
-__global__ void __launch_bounds__(kBlock) k_store_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                         const uint32_t* __restrict__ ndup_dev, SidRef sr)
-{
-    uint32_t* sid = cur_sid(sr);
-    const uint64_t ndup = *ndup_dev;
-    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < ndup; j += (uint64_t)gridDim.x * kBlock)
-        sid[dups[j]] = frees[j];
-}
-
 // ---- the window arithmetic (eslam_detmath.h DM_LM_*, the oracle's or_map_update) -------
 __device__ __forceinline__ uint32_t lm_div(uint32_t a, uint64_t m) { return (uint32_t)(((uint64_t)a * m) >> kLmMagicShift); }
 __device__ __forceinline__ uint32_t lm_mod(uint32_t a, uint32_t w, uint64_t m) { return a - w * lm_div(a, m); }
@@ -1655,6 +1655,35 @@ __device__ __forceinline__ bool lm_in(int32_t a, int32_t c, uint32_t h)
 {
     const int32_t d = a - c;
     return d <= (int32_t)h && -d <= (int32_t)h;
+}
+
+// ---- the trail (eslam_internal.h LocalMaps; the oracle's lm_trail_* and lm_recentre): a
+// table's tiles outside its window, V entries {a, b, page, -} closing its row
+__device__ __forceinline__ uint32_t lm_trail_off(const LocalMaps& lm) { return lm.S - 4u * lm.V; }
+__device__ __forceinline__ int32_t lm_cheb(int32_t a, int32_t b, int32_t na, int32_t nb)
+{
+    const int32_t da = a > na ? a - na : na - a, db = b > nb ? b - nb : nb - b;
+    return da > db ? da : db;
+}
+// tile (a, b) into the trail of row: the first empty entry, else in place of the entry farthest
+// from (na, nb) (the first such) when that one is farther than the tile; 1 when a tile was forgotten
+__device__ __forceinline__ uint32_t lm_trail_push(const LocalMaps& lm, uint32_t* row, int32_t na, int32_t nb, int32_t a, int32_t b,
+                                                  uint32_t pg)
+{
+    uint4* t = reinterpret_cast<uint4*>(row + lm_trail_off(lm));
+    int32_t far = -1;
+    uint32_t fe = 0;
+    for (uint32_t e = 0; e < lm.V; ++e) {
+        const uint4 v = t[e];
+        if (v.z == DM_LM_NONE) {
+            t[e] = make_uint4((uint32_t)a, (uint32_t)b, pg, DM_LM_NONE);
+            return 0u;
+        }
+        const int32_t d = lm_cheb((int32_t)v.x, (int32_t)v.y, na, nb);
+        if (d > far) { far = d; fe = e; }
+    }
+    if (lm.V && far > lm_cheb(a, b, na, nb)) t[fe] = make_uint4((uint32_t)a, (uint32_t)b, pg, DM_LM_NONE);
+    return 1u;
 }
 
 constexpr uint32_t kLmList = 8;                 // tiles one pass of the merge handles
@@ -1758,14 +1787,42 @@ __device__ __forceinline__ uint32_t lm_find(const uint32_t (&L)[kLmList], uint32
     return idx;
 }
 
-// the page slot s of table X holds for the new window: its page when the slot's tile under
-// the old centre oc is the same tile (the tile stays in the window), else none
-__device__ __forceinline__ uint32_t lm_page_of(const LocalMaps& lm, uint32_t X, int2 oc, const LmPart& q, uint32_t s)
+// the plan's table step (the oracle's lm_recentre; copy on write): table T's row and centre
+// from X's, the window moved to (na, nb): (1) the tiles leaving it go to the trail in slot
+// order, (2) the trail's tiles inside the new window go back to their slots.  T != X: X is
+// shared, T a free table written whole.  A lane per particle; returns the tiles forgotten.
+__device__ uint32_t lm_rewrite(const LocalMaps& lm, uint32_t X, uint32_t T, int2 oc, int32_t na, int32_t nb)
 {
-    const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
-    const int32_t a = lm_tile(sa, q.na, lm.hx, lm.wx, lm.mx, lm.bx), b = lm_tile(sb, q.nb, lm.hy, lm.wy, lm.my, lm.by);
-    if (oc.x == DM_LM_UNSET || !lm_in(a, oc.x, lm.hx) || !lm_in(b, oc.y, lm.hy)) return DM_LM_NONE;
-    return lm.slot[(uint64_t)X * lm.S + s];
+    uint32_t* row = lm.slot + (uint64_t)T * lm.S;
+    if (X != T) {
+        const uint4* src = reinterpret_cast<const uint4*>(lm.slot + (uint64_t)X * lm.S);
+        uint4* dst = reinterpret_cast<uint4*>(row);
+        for (uint32_t q = 0; q < lm.S / 4; ++q) dst[q] = src[q];
+    }
+    uint32_t forgot = 0;
+    if (oc.x != DM_LM_UNSET && (oc.x != na || oc.y != nb)) {
+        for (uint32_t sb = 0; sb < lm.wy; ++sb) {
+            const int32_t b = lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by);
+            const bool row_leaves = !lm_in(b, nb, lm.hy);
+            for (uint32_t sa = 0; sa < lm.wx; ++sa) {
+                const int32_t a = lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx);
+                if (!row_leaves && lm_in(a, na, lm.hx)) continue;
+                const uint32_t s = sa + lm.wx * sb, p = row[s];
+                if (p == DM_LM_NONE) continue;
+                forgot += lm_trail_push(lm, row, na, nb, a, b, p);
+                row[s] = DM_LM_NONE;
+            }
+        }
+        uint4* t = reinterpret_cast<uint4*>(row + lm_trail_off(lm));
+        for (uint32_t e = 0; e < lm.V; ++e) {
+            const uint4 v = t[e];
+            if (v.z == DM_LM_NONE || !lm_in((int32_t)v.x, na, lm.hx) || !lm_in((int32_t)v.y, nb, lm.hy)) continue;
+            row[lm_mod(v.x, lm.wx, lm.mx) + lm.wx * lm_mod(v.y, lm.wy, lm.my)] = v.z;
+            t[e] = make_uint4(v.x, v.y, DM_LM_NONE, DM_LM_NONE);
+        }
+    }
+    lm.ctr[T] = make_int2(na, nb);
+    return forgot;
 }
 
 // the particle of a map update: output i reads its ancestor through the marks when the merge
@@ -1834,17 +1891,22 @@ __global__ void __launch_bounds__(kBlock) k_pg_clear(uint8_t* __restrict__ mark,
         m4[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
-// one wave per table (grid-stride): its lanes walk the slots
+// one wave per table (grid-stride): its lanes walk the slots, then the trail's pages
 __global__ void __launch_bounds__(kBlock) k_pg_mark(LocalMaps lm, const uint32_t* __restrict__ ref, const uint32_t* __restrict__ gate)
 {
     if (!*gate) return;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+    const uint32_t toff = lm.S - 4u * lm.V;
     for (uint64_t t = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); t < lm.ntables; t += nw) {
         if (ref[t] == 0u) continue;
         const uint32_t* sl = lm.slot + t * lm.S;
-        for (uint32_t s = lane; s < lm.S; s += 64u) {
+        for (uint32_t s = lane; s < toff; s += 64u) {
             const uint32_t p = sl[s];
+            if (p != DM_LM_NONE) lm.mark[p] = 1u;
+        }
+        for (uint32_t e = lane; e < lm.V; e += 64u) {
+            const uint32_t p = sl[toff + 4u * e + 2u];
             if (p != DM_LM_NONE) lm.mark[p] = 1u;
         }
     }
@@ -1964,7 +2026,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
     const bool gath = mp.fuse && ctl->gather;
     const DevState in = gath ? (ctl->base ? s1 : s0) : st;
     const uint32_t src = lm_source(mp, i, gath);
-    uint32_t need = 0, covered = 0, dropped = 0;
+    uint32_t need = 0, covered = 0, dropped = 0, forgot = 0;
     MergeJob jb;
     if (i < mp.n) {
         LmPart q;
@@ -1987,6 +2049,11 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             lm_codes(map, lm, mp, q, codes, covered, dropped);
             const int2 oc = lm.ctr[q.X];
             const uint32_t T = q.shared ? mp.frees[i] : q.X;
+            // the window moves to the particle (and a shared table is copied to T): from here
+            // on every tile the scan reaches is in T's slots
+            const bool moved = oc.x != q.na || oc.y != q.nb;
+            if (q.shared || moved) forgot = lm_rewrite(lm, q.X, T, oc, q.na, q.nb);
+            const uint32_t* trow = lm.slot + (uint64_t)T * lm.S;
             const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
             uint32_t L[kLmList];
             lm_collect(codes, mp.m, kLmNoList, L);
@@ -1994,7 +2061,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
 #pragma unroll
             for (uint32_t r = 0; r < kLmList; ++r) {
                 if (L[r] == kLmNoList) continue;
-                const uint32_t P = lm_page_of(lm, q.X, oc, q, L[r]);
+                const uint32_t P = trow[L[r]];
                 const bool mine = !q.shared && P != DM_LM_NONE && lm.owner[P] == gT;
                 bits |= mine ? 0u : 1u << r;
                 jb.L[r] = (uint16_t)L[r];
@@ -2011,7 +2078,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
 #pragma unroll
                 for (uint32_t r = 0; r < kLmList; ++r) {
                     if (L[r] == kLmNoList) continue;
-                    const uint32_t P = lm_page_of(lm, q.X, oc, q, L[r]);
+                    const uint32_t P = trow[L[r]];
                     need += (!q.shared && P != DM_LM_NONE && lm.owner[P] == gT) ? 0u : 1u;
                 }
             }
@@ -2020,7 +2087,8 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             jb.ox = oc.x;
             jb.oy = oc.y;
             jb.need = bits;
-            jb.flags = kJobPlaced | (q.shared ? kJobShared : 0u) | (more ? kJobMore : 0u) | (nt << 8);
+            jb.flags = kJobPlaced | (q.shared ? kJobShared : 0u) | (more ? kJobMore : 0u) | (moved ? kJobMoved : 0u) |
+                       (nt << 8);
         }
     }
     // the codes rows and the records leave through LDS, so every store is a whole 1-KiB line of
@@ -2051,21 +2119,14 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
     for (uint32_t c = tid; c < nb * (sizeof(MergeJob) / 16); c += kLmBlock) jobs[c] = srec[c];
     covered = wave_sum_u32(covered);
     dropped = wave_sum_u32(dropped);
-    if ((tid & 63u) == 0) {                   // the update's dropped / covered patches (k_merge_counts)
+    forgot = wave_sum_u32(forgot);
+    if ((tid & 63u) == 0) {                   // the update's dropped / covered patches, forgotten tiles (k_merge_counts)
         const uint32_t slot_c = (uint32_t)((blockIdx.x * (kLmBlock / 64) + (tid >> 6)) % kMergeCounterSlots);
         if (dropped) atomicAdd((unsigned long long*)&mp.cnt[slot_c], (unsigned long long)dropped);
         if (covered) atomicAdd((unsigned long long*)&mp.cnt[3 * kMergeCounterSlots + slot_c], (unsigned long long)covered);
+        if (forgot) atomicAdd((unsigned long long*)&mp.cnt[6 * kMergeCounterSlots + slot_c], (unsigned long long)forgot);
     }
     block_offsets(need, i < mp.n, mp.off + (i - tid), mp.poff + blockIdx.x, s_w);
-}
-
-// the page slot s of table X holds for the window centred at (na, nb) (lm_page_of)
-__device__ __forceinline__ uint32_t lm_page_at(const LocalMaps& lm, uint32_t X, int2 oc, int32_t na, int32_t nb, uint32_t s)
-{
-    const uint32_t sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
-    const int32_t a = lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx), b = lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by);
-    if (oc.x == DM_LM_UNSET || !lm_in(a, oc.x, lm.hx) || !lm_in(b, oc.y, lm.hy)) return DM_LM_NONE;
-    return lm.slot[(uint64_t)X * lm.S + s];
 }
 
 // the number of lower lanes of the 16-lane row holding the same code (c == 0xffffffff never
@@ -2103,7 +2164,6 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 {
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][kMaxScanPatches];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
-    __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
     __shared__ uint8_t s_list[kLmPpb][kMaxScanPatches];                                // a stage's patches, in scan order
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
@@ -2118,13 +2178,11 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     // the plan's record, the codes and this particle's first page: one round trip
     uint32_t X = 0, T = 0, flags = 0, needb = 0, src = 0, Lr = kLmNoList, Pr = DM_LM_NONE;
     uint64_t gT = 0, alloc = 0;
-    int32_t na = 0, nb = 0, ox = 0, oy = 0;
     double z = 0.0, zs = 0.0;
     lm_codes_t c4 = {};
     if (valid) {
         const MergeJob* J = mp.job + i;
         X = J->X; T = J->T; gT = J->gT;
-        na = J->na; nb = J->nb; ox = J->ox; oy = J->oy;
         flags = J->flags; needb = J->need;
         z = J->z; zs = J->zs; src = J->src;
         if (l < kLmList) { Lr = J->L[l]; Pr = J->P[l]; }
@@ -2160,11 +2218,9 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
             const uint32_t k = l + kLmLanes * u;
             code[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
         }
-        const int2 oc = make_int2(ox, oy);
-        const bool recentre = ox != na || oy != nb;
-        const bool rewrite = shared || (recentre && ox != DM_LM_UNSET);
+        // the plan has moved T's window (and copied a shared X to T): every tile of the scan is
+        // in T's slots, and the merge only adds the new pages
         uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
-        const uint32_t* xsl = lm.slot + (uint64_t)X * lm.S;
         const uint32_t gshift = (tid & 63u) & ~(kLmLanes - 1u);
         const double zvar = zs * zs;
         uint8_t* stage = &s_stage[wv][0];
@@ -2229,7 +2285,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     if (code[u] != kCodeSkip && (int32_t)(code[u] >> 6) > lo) nx = min(nx, code[u] >> 6);
                 more = cnt == kLmList && grp_min(nx) != kLmNoList;
                 if (l < cnt) {
-                    P = lm_page_at(lm, X, oc, na, nb, Lr);
+                    P = tsl[Lr];
                     need = !(!shared && P != DM_LM_NONE && lm.owner[P] == gT);
                 }
             }
@@ -2240,56 +2296,13 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 ++taken;
             }
             alloc += __builtin_popcount(gmask);
-            if (pass == 0) {
-                // ---- 2. the table: X's slots rewritten into T (evictions; a copy when shared)
-                // with this pass's new pages, else the new pages alone
-                if (rewrite) {
-                    if (l < kLmList) {
-                        s_np[pl][2 * l] = Lr;
-                        s_np[pl][2 * l + 1] = NP;
-                    }
-                    // the window's columns and rows whose tiles leave it (bit sa / sb), the pass's
-                    // slot range (only slots inside it can take a new page)
-                    uint32_t colx = 0, rowx = 0;
-                    if (recentre && ox != DM_LM_UNSET) {
-                        for (uint32_t s = l; s < lm.wx; s += kLmLanes)
-                            colx |= lm_in(lm_tile(s, ox, lm.hx, lm.wx, lm.mx, lm.bx), na, lm.hx) ? 0u : 1u << s;
-                        for (uint32_t s = l; s < lm.wy; s += kLmLanes)
-                            rowx |= lm_in(lm_tile(s, oy, lm.hy, lm.wy, lm.my, lm.by), nb, lm.hy) ? 0u : 1u << s;
-                        colx = grp_or(colx);
-                        rowx = grp_or(rowx);
-                    }
-                    const uint32_t lmin = cnt ? grp_get(Lr, 0) : 1u, lmax = cnt ? grp_get(Lr, cnt - 1) : 0u;
-                    wave_sync();
-                    // four slots a lane (tables are padded to whole 16-byte words): each group
-                    // instruction moves 128 contiguous bytes of the table
-                    for (uint32_t q = l; q < lm.S / 4; q += kLmLanes) {
-                        const uint4 w4 = reinterpret_cast<const uint4*>(xsl)[q];
-                        uint32_t v[4] = {w4.x, w4.y, w4.z, w4.w};
-                        bool ch = false;
-#pragma unroll
-                        for (uint32_t e = 0; e < 4; ++e) {
-                            const uint32_t s = 4 * q + e, sb = lm_div(s, lm.mx), sa = s - lm.wx * sb;
-                            uint32_t w = v[e];
-                            if (((colx >> sa) | (rowx >> sb)) & 1u) w = DM_LM_NONE;
-                            if (s >= lmin && s <= lmax)
-                                for (uint32_t r = 0; r < cnt; ++r)
-                                    if (s_np[pl][2 * r] == s && s_np[pl][2 * r + 1] != DM_LM_NONE) w = s_np[pl][2 * r + 1];
-                            ch |= w != v[e];
-                            v[e] = w;
-                        }
-                        if (shared || ch) reinterpret_cast<uint4*>(tsl)[q] = make_uint4(v[0], v[1], v[2], v[3]);
-                    }
-                } else if (need) {
-                    tsl[Lr] = NP;
-                }
-                if ((shared || recentre) && l == 0) lm.ctr[T] = make_int2(na, nb);
-                dirty = recentre;
-            } else if (need) {
-                // a later pass: T's slot may have been rewritten above (same wave; in order)
-                __builtin_amdgcn_s_waitcnt(0);
+            // ---- 2. the table: the new pages into T's slots (a later pass: T's slot may have
+            // been written by this group above -- the same wave, in order)
+            if (need) {
+                if (pass != 0) __builtin_amdgcn_s_waitcnt(0);
                 tsl[Lr] = NP;
             }
+            if (pass == 0) dirty = (flags & kJobMoved) != 0;
             // ---- 3. the pass's pages, kLmStage at a time through LDS
             for (uint32_t r0 = 0; r0 < cnt; r0 += kLmStage) {
                 uint32_t Ls[kLmStage], Ps[kLmStage], Ds[kLmStage];
@@ -2385,55 +2398,86 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     }
 }
 
+// the first patch of shared-grid cell ct (its MapView::cell_tab record) passing getPatch's
+// 3-sigma gate against the local height lz (the oracle's or_mls_cell_patch)
+__device__ __forceinline__ bool grid_cell_patch(const MapView& map, uint4 ct, double lz, double qv, double& mean)
+{
+    for (uint32_t k = ct.z; k < ct.z + ct.w; ++k) {
+        const float2 pf = k == ct.z ? make_float2(__uint_as_float(ct.x), __uint_as_float(ct.y)) : map.patch[k];
+        const double pm = (double)pf.x, ps = (double)pf.y;
+        const double ph = map.height ? (double)map.height[k] : 0.0;
+        double diff;
+        if (ph > 0.0) {
+            if (lz > pm) diff = lz - pm;
+            else if (lz < pm - ph) diff = (pm - ph) - lz;
+            else diff = 0.0;
+        } else {
+            diff = dm_fabs(pm - lz);
+        }
+        if (diff * diff < 9.0 * (ps * ps + qv)) { mean = pm; return true; }
+    }
+    return false;
+}
+
 // processMap(scanMap, match = true) per particle (the oracle's or_map_match; the rule is the
 // build's own, envire's MLSGrid::match not being in the reference): every 10th scan patch,
-// placed like the merge, that lands on a cell of the particle's own map -- a tile inside both
-// its window and the window the update centres on the particle -- scores
-// exp(-d^2 / (2 sigma^2)), sigma 0.2f (src/EmbodiedSlamFilter.cpp:217); the particle's weight
-// is multiplied by pow(weight, 0.1f), weight the float mean score (1 without a matched cell).
-// A lane per particle: a handful of lookups each (the sampled patches from the kernel
-// arguments, scalar loads).
+// placed like the merge, scores on the cell it lands in -- a cell of the shared grid: the
+// patch getPatch's 3-sigma gate picks (0 when none passes); with per-particle maps (PMAPS) an
+// empty grid cell of the particle's own map, in a tile inside the window the update centres on
+// the particle (from the window or the trail): its cell -- exp(-d^2 / (2 sigma^2)), sigma 0.2f
+// (src/EmbodiedSlamFilter.cpp:217); the particle's weight is multiplied by pow(weight, 0.1f),
+// weight the float mean score (1 when no patch counts).  A lane per particle; the sampled
+// patches from the kernel arguments (scalar loads), kMatchBatch at a time: their grid records
+// and table slots in one round trip, then the cells.
+template <bool PMAPS>
 __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
                                                       LocalMaps lm, MatchParams mp)
 {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= mp.n) return;
     const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;
-    const uint32_t X = st.sid[i];
-    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], w = st.w[i];
+    const uint32_t X = PMAPS ? st.sid[i] : 0u;
+    const double x = st.x[i], y = st.y[i], th = st.th[i], z = st.z[i], zs = st.zs[i], w = st.w[i];
     const double bx = x - map.offset_x, by = y - map.offset_y;
     if (!(dm_isfinite(bx) && dm_isfinite(by) && dm_isfinite(th))) return;
     double sn, co;
     dm_sincos(th, &sn, &co);
+    const double zvar = zs * zs;
     const double* A = map.g2l;
-    int32_t na, nb;
-    if (mp.is_id) {
-        na = dm_lm_centre(x, map.offset_x, map.inv_scale_x);
-        nb = dm_lm_centre(y, map.offset_y, map.inv_scale_y);
-    } else {
-        na = dm_lm_centre(((A[0] * x + A[1] * y) + A[2] * z) + A[3], map.offset_x, map.inv_scale_x);
-        nb = dm_lm_centre(((A[4] * x + A[5] * y) + A[6] * z) + A[7], map.offset_y, map.inv_scale_y);
+    int32_t na = 0, nb = 0;
+    int2 c = make_int2(0, 0);
+    const uint32_t* row = nullptr;
+    if constexpr (PMAPS) {
+        if (mp.is_id) {
+            na = dm_lm_centre(x, map.offset_x, map.inv_scale_x);
+            nb = dm_lm_centre(y, map.offset_y, map.inv_scale_y);
+        } else {
+            na = dm_lm_centre(((A[0] * x + A[1] * y) + A[2] * z) + A[3], map.offset_x, map.inv_scale_x);
+            nb = dm_lm_centre(((A[4] * x + A[5] * y) + A[6] * z) + A[7], map.offset_y, map.inv_scale_y);
+        }
+        c = lm.ctr[X];
+        row = lm.slot + (uint64_t)X * lm.S;
     }
-    const int2 c = lm.ctr[X];
     double sum = 0.0;
     uint32_t cnt = 0;
-    // kMatchBatch patches at a time: their table slots, then their cells, each batch of loads
-    // in flight together (one patch after another was two dependent round trips per patch);
-    // the scores are added in patch order
     constexpr uint32_t kMatchBatch = 8;
     for (uint32_t k0 = 0; k0 < mp.m; k0 += kMatchBatch) {
-        uint32_t pg[kMatchBatch], cj[kMatchBatch];
-        double wzs[kMatchBatch];
+        uint4 ct[kMatchBatch];
+        uint32_t pg[kMatchBatch], cj[kMatchBatch], sl[kMatchBatch];
+        double wzs[kMatchBatch], lzs[kMatchBatch], var[kMatchBatch];
+        bool on[kMatchBatch], own[kMatchBatch];
 #pragma unroll
         for (uint32_t q = 0; q < kMatchBatch; ++q) {
             const uint32_t k = k0 + q;
+            on[q] = own[q] = false;
+            ct[q] = make_uint4(0u, 0u, 0u, 0u);
             pg[q] = DM_LM_NONE;
-            cj[q] = 0;
-            wzs[q] = 0.0;
+            cj[q] = sl[q] = 0;
+            wzs[q] = lzs[q] = var[q] = 0.0;
             if (k >= mp.m) continue;
             const ScanPatch sp = mp.sp ? mp.sp[k] : mp.spi[k];
             const double wz = sp.z + z;
-            wzs[q] = wz;
+            double lz = wz;
             uint32_t cm, cn;
             if (mp.is_id) {
                 if (dm_merge_cell_mn(bx, by, co, sn, sp.x, sp.y, map.inv_scale_x, map.inv_scale_y, map.width,
@@ -2444,24 +2488,53 @@ __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, 
                 const double wy = (sn * sp.x + co * sp.y) + y;
                 const double lx = ((A[0] * wx + A[1] * wy) + A[2] * wz) + A[3];
                 const double ly = ((A[4] * wx + A[5] * wy) + A[6] * wz) + A[7];
+                lz = ((A[8] * wx + A[9] * wy) + A[10] * wz) + A[11];
                 const double fm = floor((lx - map.offset_x) * map.inv_scale_x);
                 const double fn = floor((ly - map.offset_y) * map.inv_scale_y);
                 if (!((fm >= 0.0) & (fm < (double)map.width) & (fn >= 0.0) & (fn < (double)map.height_cells))) continue;
                 cm = (uint32_t)fm;
                 cn = (uint32_t)fn;
             }
-            const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
-            if (!dm_lm_inside(a, na, lm.hx, lm.wx) || !dm_lm_inside(b, nb, lm.hy, lm.wy)) continue;
-            if (!dm_lm_inside(a, c.x, lm.hx, lm.wx) || !dm_lm_inside(b, c.y, lm.hy, lm.wy)) continue;
-            pg[q] = lm.slot[(uint64_t)X * lm.S + lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my)];
-            cj[q] = (cm & 7u) + 8u * (cn & 7u);
+            on[q] = true;
+            wzs[q] = wz;
+            lzs[q] = lz;
+            var[q] = sp.stdev * sp.stdev + zvar;
+            ct[q] = map.cell_tab[(uint64_t)cn * map.width + cm];
+            if constexpr (PMAPS) {
+                const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+                if (dm_lm_inside(a, na, lm.hx, lm.wx) && dm_lm_inside(b, nb, lm.hy, lm.wy)) {
+                    own[q] = true;
+                    cj[q] = (cm & 7u) + 8u * (cn & 7u);
+                    const bool inw = dm_lm_inside(a, c.x, lm.hx, lm.wx) && dm_lm_inside(b, c.y, lm.hy, lm.wy);
+                    sl[q] = inw ? row[lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my)] : DM_LM_NONE;
+                    if (!inw) {                  // a tile the window has left: the trail (rare)
+                        const uint4* t = reinterpret_cast<const uint4*>(row + lm_trail_off(lm));
+                        for (uint32_t e = 0; e < lm.V; ++e) {
+                            const uint4 v = t[e];
+                            if (v.z != DM_LM_NONE && v.x == a && v.y == b) sl[q] = v.z;
+                        }
+                    }
+                }
+            }
         }
         float2 cv[kMatchBatch];
 #pragma unroll
-        for (uint32_t q = 0; q < kMatchBatch; ++q)
+        for (uint32_t q = 0; q < kMatchBatch; ++q) {
+            pg[q] = (PMAPS && own[q] && ct[q].w == 0u) ? sl[q] : DM_LM_NONE;
             cv[q] = pg[q] != DM_LM_NONE ? lm.page[(uint64_t)pg[q] * DM_LM_PAGE_CELLS + cj[q]] : make_float2(0.0f, -1.0f);
+        }
 #pragma unroll
         for (uint32_t q = 0; q < kMatchBatch; ++q) {
+            if (!on[q]) continue;
+            if (ct[q].w != 0u) {                 // a cell of the shared grid
+                double mean;
+                if (grid_cell_patch(map, ct[q], lzs[q], var[q], mean)) {
+                    const double d = lzs[q] - mean;
+                    sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
+                }
+                ++cnt;
+                continue;
+            }
             if (pg[q] == DM_LM_NONE || !dm_lm_holds(cv[q].y)) continue;
             const double d = wzs[q] - (double)cv[q].x;
             sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
@@ -2486,16 +2559,18 @@ __global__ void __launch_bounds__(kMergeCounterSlots) k_merge_counts(const uint6
     }
     __syncthreads();
     if (t == 0) {
-        uint64_t r[kMergeCounters] = {0, 0, 0, 0, 0, 0};
+        uint64_t r[kMergeCounters] = {0, 0, 0, 0, 0, 0, 0};
         for (uint32_t g = 0; g < kMergeCounters; ++g)
             for (uint32_t w = 0; w < kMergeCounterSlots / 64; ++w) r[g] += s[g][w];
         // acc: a later part of a scan merged 64 patches at a time (eslam_gpu_map_update) adds
         if (acc) {
             ctl->map_dropped += r[0]; ctl->map_changed += r[1]; ctl->map_copied += r[2];
             ctl->map_covered += r[3]; ctl->map_written += r[4]; ctl->map_taken += r[5];
+            ctl->map_evicted += r[6];
         } else {
             ctl->map_dropped = r[0]; ctl->map_changed = r[1]; ctl->map_copied = r[2];
             ctl->map_covered = r[3]; ctl->map_written = r[4]; ctl->map_taken = r[5];
+            ctl->map_evicted = r[6];
         }
         if (!(ctl->err & kFaultPages)) ctl->pg_cursor += ctl->pg_total;
     }
@@ -4047,7 +4122,12 @@ extern "C" hipError_t eslam_launch_map_match(DevState s0, DevState s1, const Ctl
                                              const MatchParams* mp, hipStream_t stream)
 {
     const uint64_t blocks = (mp->n + kBlock - 1) / kBlock;
-    if (blocks) hipLaunchKernelGGL(k_map_match, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    if (blocks && lm) hipLaunchKernelGGL(k_map_match<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    if (blocks && !lm) {
+        LocalMaps none;
+        memset(&none, 0, sizeof(none));
+        hipLaunchKernelGGL(k_map_match<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, s0, s1, ctl, *map, none, *mp);
+    }
     return hipGetLastError();
 }
 
@@ -4072,8 +4152,11 @@ __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const Dev
     for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
         const uint64_t i = (send[j].src >> 8) - gbase;
         const uint32_t X = st.sid[i];
+        const uint32_t* row = lm.slot + (uint64_t)X * lm.S;
+        const uint32_t toff = lm.S - 4u * lm.V;
         uint32_t c = 0;
-        for (uint32_t s = lane; s < lm.S; s += 64u) c += lm.slot[(uint64_t)X * lm.S + s] != DM_LM_NONE ? 1u : 0u;
+        for (uint32_t s = lane; s < toff; s += 64u) c += row[s] != DM_LM_NONE ? 1u : 0u;
+        for (uint32_t e = lane; e < lm.V; e += 64u) c += row[toff + 4u * e + 2u] != DM_LM_NONE ? 1u : 0u;
         c = wave_sum_u32(c);
         if (lane == 0) {
             MapPayHdr h;
@@ -4085,8 +4168,9 @@ __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const Dev
     }
 }
 
-// the records' pages in the records' order (off: exclusive prefix of the headers' npg), one
-// wave per record: its lanes copy each page's 64 cells
+// the records' pages in the records' order (off: exclusive prefix of the headers' npg), the
+// window's in slot order then the trail's in entry order; one wave per record: its lanes copy
+// each page's 64 cells
 __global__ void __launch_bounds__(kBlock) k_pay_pack(const DevState s0, const DevState s1, const Ctl* __restrict__ ctl,
                                                     const Rec* __restrict__ send, uint64_t nsend, uint64_t gbase, LocalMaps lm,
                                                     const uint32_t* __restrict__ off, MapPayPage* __restrict__ pay)
@@ -4097,11 +4181,19 @@ __global__ void __launch_bounds__(kBlock) k_pay_pack(const DevState s0, const De
     for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
         const uint64_t i = (send[j].src >> 8) - gbase;
         const uint32_t X = st.sid[i];
+        const uint32_t* row = lm.slot + (uint64_t)X * lm.S;
+        const uint32_t toff = lm.S - 4u * lm.V;
         uint64_t q = off[j];
-        for (uint32_t s = 0; s < lm.S; ++s) {
-            const uint32_t p = lm.slot[(uint64_t)X * lm.S + s];
+        for (uint32_t s = 0; s < toff + lm.V; ++s) {
+            const bool tr = s >= toff;
+            const uint32_t p = tr ? row[toff + 4u * (s - toff) + 2u] : row[s];
             if (p == DM_LM_NONE) continue;
-            if (lane == 0) { pay[q].slot = s; pay[q].pad = 0; }
+            if (lane == 0) {
+                pay[q].slot = tr ? (kPayTrail | (s - toff)) : s;
+                pay[q].a = tr ? (int32_t)row[toff + 4u * (s - toff)] : 0;
+                pay[q].b = tr ? (int32_t)row[toff + 4u * (s - toff) + 1u] : 0;
+                pay[q].pad = 0;
+            }
             pay[q].cell[lane] = lm.page[(uint64_t)p * DM_LM_PAGE_CELLS + lane];
             ++q;
         }
@@ -4132,41 +4224,25 @@ __global__ void __launch_bounds__(1024) k_pay_prefix(const MapPayHdr* __restrict
     if (threadIdx.x == 1023) out[m] = s_sum[1023];
 }
 
-// the received particles' page needs (their records' page counts), in dups order, and the
-// block sums (blocks of kLmBlock over the worst case n; past *ndup nothing)
-__global__ void __launch_bounds__(kLmBlock) k_recv_plan(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ ndup_dev,
-                                                        SidRef sr, const MapPayHdr* __restrict__ hdr, MergeParams mp)
-{
-    __shared__ uint32_t s_w[kLmBlock / 64];
-    const uint32_t* sid = cur_sid(sr);
-    const uint64_t j = (uint64_t)blockIdx.x * kLmBlock + threadIdx.x;
-    uint32_t need = 0;
-    if (j < *ndup_dev) need = hdr[sid[dups[j]] & ~kSidRecord].npg;
-    block_offsets(need, j < mp.n, mp.off + (j - threadIdx.x), mp.poff + blockIdx.x, s_w);
-}
-
-// received particle j takes free table frees[j] and pages from the free list, filled from its
-// record's payload; one wave per particle: its lanes copy each page's cells, then each lane
-// writes its slots of the table
-__global__ void __launch_bounds__(kLmBlock) k_recv_maps(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                        const uint32_t* __restrict__ ndup_dev, SidRef sr, Ctl* __restrict__ ctl,
+// the received records' maps: record r takes free table frees[r] and its pages at hoff[r] past
+// the free list's cursor (pages once per record: every output copied from it names the table,
+// which its next map update then finds shared -- copy on write, as the copies of a one-GPU
+// resample), filled from the payload.  One wave per record: its lanes copy each page's cells,
+// then write the table's row (window slots, then the trail's entries {a, b, page, -})
+__global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uint32_t* __restrict__ frees, Ctl* __restrict__ ctl,
                                                         const MapPayHdr* __restrict__ hdr, const uint32_t* __restrict__ hoff,
-                                                        const MapPayPage* __restrict__ pay, LocalMaps lm, MergeParams mp)
+                                                        const MapPayPage* __restrict__ pay, LocalMaps lm)
 {
     if (ctl->err & kFaultPages) return;
-    const uint32_t* sid = cur_sid(sr);
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint64_t ndup = *ndup_dev;
-    const uint64_t j0 = (uint64_t)blockIdx.x * kLmBlock;
-    for (uint32_t k = tid >> 6; k < (uint32_t)kLmBlock; k += kLmBlock / 64) {
-        const uint64_t j = j0 + k;
-        if (j >= ndup) break;
-        const uint64_t alloc = ctl->pg_cursor + mp.poff[blockIdx.x] + mp.off[j];
-        const uint32_t rec = sid[dups[j]] & ~kSidRecord;
-        const uint32_t T = frees[j];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * (kLmBlock / 64);
+    const uint32_t toff = lm.S - 4u * lm.V;
+    for (uint64_t r = (uint64_t)blockIdx.x * (kLmBlock / 64) + (threadIdx.x >> 6); r < nrec; r += nw) {
+        const uint64_t alloc = ctl->pg_cursor + hoff[r];
+        const uint32_t T = frees[r];
         const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
-        const uint32_t npg = hdr[rec].npg;
-        const uint64_t q0 = hoff[rec];
+        const uint32_t npg = hdr[r].npg;
+        const uint64_t q0 = hoff[r];
         for (uint32_t q = 0; q < npg; ++q) {
             const uint32_t np = lm.frees[alloc + q];
             lm.page[(uint64_t)np * DM_LM_PAGE_CELLS + lane] = pay[q0 + q].cell[lane];
@@ -4175,16 +4251,36 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(const uint32_t* __restri
         uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
         for (uint32_t s = lane; s < lm.S; s += 64u) {
             uint32_t v = DM_LM_NONE;
-            for (uint32_t q = 0; q < npg; ++q) v = pay[q0 + q].slot == s ? lm.frees[alloc + q] : v;
+            if (s < toff) {
+                for (uint32_t q = 0; q < npg; ++q) v = pay[q0 + q].slot == s ? lm.frees[alloc + q] : v;
+            } else {
+                const uint32_t e = (s - toff) >> 2, k = (s - toff) & 3u;
+                for (uint32_t q = 0; q < npg; ++q) {
+                    const MapPayPage& pp = pay[q0 + q];
+                    if (pp.slot != (kPayTrail | e)) continue;
+                    v = k == 0u ? (uint32_t)pp.a : k == 1u ? (uint32_t)pp.b : k == 2u ? lm.frees[alloc + q] : DM_LM_NONE;
+                }
+            }
             tsl[s] = v;
         }
-        if (lane == 0) lm.ctr[T] = hdr[rec].ctr;
+        if (lane == 0) lm.ctr[T] = hdr[r].ctr;
     }
 }
 
-// the particles a sharded resample received (cs.dups, *cs.ndup) take the first free tables and
-// pages from the page pool, filled from their records' payloads (needs eslam_launch_store_refs
-// first): hdr / pay the received headers and pages, hoff (nrecv + 1 words) scratch
+// the particles a sharded resample received from record r (sid = kSidRecord | r) name frees[r]
+__global__ void __launch_bounds__(kBlock) k_recv_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
+                                                        const uint32_t* __restrict__ ndup_dev, SidRef sr)
+{
+    uint32_t* sid = cur_sid(sr);
+    const uint64_t ndup = *ndup_dev;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < ndup; j += (uint64_t)gridDim.x * kBlock)
+        sid[dups[j]] = frees[sid[dups[j]] & ~kSidRecord];
+}
+
+// the particles a sharded resample received (cs.dups, *cs.ndup, from nrecv records) get their
+// records' maps: a free table and pages from the pool per record, filled from the payloads
+// (needs eslam_launch_store_refs first): hdr / pay the received headers and pages, hoff
+// (nrecv + 1 words) scratch
 extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint64_t n,
                                                  const CowScratch* cs, const void* hdr, uint64_t nrecv, uint32_t* hoff,
                                                  const void* pay, uint32_t* pgc, hipStream_t stream)
@@ -4193,19 +4289,26 @@ extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const Loc
     hipError_t e = compact(1, n, cs->ref, sid, cs->counts + cs->tiles + 1, cs->dups, cs->ndup, stream);
     if (e != hipSuccess) return e;
     const MapPayHdr* h = (const MapPayHdr*)hdr;
-    hipLaunchKernelGGL(k_pay_prefix, dim3(1), dim3(1024), 0, stream, h, nrecv, hoff);
-    const uint32_t nb = (uint32_t)((n + kLmBlock - 1) / kLmBlock);
-    e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
+    if (nrecv) {
+        hipLaunchKernelGGL(k_pay_prefix, dim3(1), dim3(1024), 0, stream, h, nrecv, hoff);
+    } else {
+        e = hipMemsetAsync(hoff, 0, 4, stream);
+        if (e != hipSuccess) return e;
+    }
+    // the plan is the records' page counts: one "block" whose sum is hoff[nrecv]
+    e = hipMemcpyAsync(mp->poff, hoff + nrecv, 4, hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(mp->poff + 1, 0, 4, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_recv_plan, dim3(nb), dim3(kLmBlock), 0, stream, cs->dups, cs->ndup, sid, h, *mp);
-    e = page_budget(ctl, lm, mp, nb, pgc, stream);
+    e = page_budget(ctl, lm, mp, 1u, pgc, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_recv_maps, dim3(nb), dim3(kLmBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid, ctl, h, hoff,
-                       (const MapPayPage*)pay, *lm, *mp);
+    const uint64_t gw = (nrecv + kLmBlock / 64 - 1) / (kLmBlock / 64);
+    if (nrecv)
+        hipLaunchKernelGGL(k_recv_maps, dim3((uint32_t)(gw < 8192 ? gw : 8192)), dim3(kLmBlock), 0, stream, nrecv, cs->frees, ctl, h,
+                           hoff, (const MapPayPage*)pay, *lm);
     hipLaunchKernelGGL(k_pg_advance, dim3(1), dim3(1), 0, stream, ctl);
     const uint64_t want_r = (n + kBlock - 1) / kBlock;
     const uint32_t gr = (uint32_t)(want_r < 2048 ? want_r : 2048);
-    hipLaunchKernelGGL(k_store_rename, dim3(gr), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid);
+    hipLaunchKernelGGL(k_recv_rename, dim3(gr), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid);
     return hipGetLastError();
 }
 

@@ -57,6 +57,8 @@ class Config(C.Structure):
         ("flags", C.c_uint32),
         ("local_map_pages", C.c_uint32),
         ("max_sensor_range", C.c_double),
+        ("local_map_trail", C.c_uint32),
+        ("pad_trail", C.c_uint32),
     ]
 
 
@@ -168,6 +170,7 @@ class UpdateInfo(C.Structure):
         ("map_cells_written", C.c_uint64),
         ("map_pages_taken", C.c_uint64),
         ("map_pages_free", C.c_uint64),
+        ("map_tiles_evicted", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -282,6 +285,7 @@ def default_config(lib=None):
     c.flags = 0
     c.local_map_pages = 0
     c.max_sensor_range = 3.0
+    c.local_map_trail = 16
     return c
 
 

@@ -232,6 +232,30 @@ int main()
                     std::memcmp(&a[i].mprob, &M[i], 8) || a[i].floating != (FL[i] != 0) || a[i].cpoints.size() != NC[i];
         EXPECT(diff == 0, "edits through getParticles() == download / edit / upload, bit for bit");
         EXPECT(&a == &ef.getParticles(), "getParticles() hands out the same vector");
+        // processMap(scanMap, true, false) on the shared map (the laser path's match-only call,
+        // src/EmbodiedSlamFilter.cpp:342-344): every particle against the shared grid
+        std::vector<eslam_ns::ScanPatch> scan;
+        std::vector<eslam_scan_patch> rs;
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 4; ++j) {
+                eslam_ns::ScanPatch sp;
+                sp.position = eslam_ns::Vector3d(0.35 + 0.1 * i, -0.6 + 0.2 * j, -0.13);
+                sp.stdev = 0.03;
+                scan.push_back(sp);
+                eslam_scan_patch r;
+                for (int k = 0; k < 3; ++k) r.position[k] = sp.position[k];
+                r.stdev = sp.stdev;
+                rs.push_back(r);
+            }
+        const double w0 = ef.getParticles()[0].weight;
+        ef.processMap(scan, true, false);
+        EXPECT(eslam_gpu_map_match(raw.handle(), rs.data(), (uint32_t)rs.size()) == ESLAM_OK, "raw shared-map match");
+        std::vector<eslam_ns::PoseParticle>& a2 = ef.getParticles();
+        EXPECT(eslam_gpu_download_particles(raw.handle(), &p) == ESLAM_OK, "match: raw download");
+        diff = a2.size() != n;
+        for (size_t i = 0; i < a2.size() && i < n; ++i) diff += std::memcmp(&a2[i].weight, &W[i], 8) != 0;
+        EXPECT(diff == 0, "processMap(match = true) on the shared map: façade == raw ABI, bit for bit");
+        EXPECT(a2[0].weight < w0, "a scan 5 cm above the grid lowers particle 0's weight");
     }
 
     // ---- UpdateThreshold::test(const Affine3d&) (src/Configuration.hpp:23-26, Q6 kept) -----

@@ -10,7 +10,7 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit", "records")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit", "records", "heirloom")
 EDIT_GLOBAL = (0, 37)                            # edit: the particles one rank edits
 CONFIG3_STEPS = 3
 MAP_SAMPLES = 64                                 # config4: particles whose maps are compared
@@ -26,12 +26,15 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0", "records"):
+    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0", "records", "heirloom"):
         S.bench_config(cfg, n_global)
         if name == "records":                    # logDebug: every update's contact points
             cfg.flags |= A.FLAG_RECORD_CONTACTS
-        if name in ("maps", "config4"):          # useSharedMap = false: per-particle maps
+        if name in ("maps", "config4", "heirloom"):   # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
+        if name == "heirloom":
+            # 4 pages per particle: the one map of ~50 pages fits the pool once, not once per copy
+            cfg.local_map_pages = 4
         if name == "config4":
             # 8 ranks x 8M and then one 64M context share one GPU's 288 GB: a 5 x 5-tile window
             # (1.5 m; the scan reaches 1.2 m) and 6 pages per particle (3 steps take ~5)
@@ -55,6 +58,8 @@ def scenario_grid(name):
         return S.unmapped_beyond(S.rough_map(cells=1000), 0.3)
     if name == "maps":                            # the front feet stand on cells only the scans map
         return S.unmapped_beyond(S.rough_map(cells=120), 0.3)
+    if name == "heirloom":                        # the empty prior: every cell is a particle's own
+        return S.unmapped_beyond(S.rough_map(cells=120), -1e9)
     return S.rough_map(cells=120) if name not in ("forced", "burst", "edit", "getter0", "records") else S.rough_map(cells=120, multi=False)
 
 
@@ -167,12 +172,58 @@ def _records(rec, key, f):
         rec[f"{key}/cp_{fld}"] = np.ascontiguousarray(cps[fld])
 
 
+def heirloom_arrays(n_global, lo, hi):
+    """every particle off the grid (x = 1000 m) with weight 0 but the last one: at the origin,
+    weight 1 -- its map is the only one, and a resample copies it to every output"""
+    pa = A.ParticleArrays(hi - lo)
+    pa.x[:] = 1000.0
+    pa.zpos[:] = 0.18
+    pa.zsigma[:] = 0.05
+    pa.mprob[:] = 1.0
+    pa.floating[:] = 1
+    if hi == n_global:
+        pa.x[-1] = 0.0
+        pa.weight[-1] = 1.0
+    return pa
+
+
+def _maps(rec, f, n):
+    """every particle's own patches, sorted by cell"""
+    count = np.zeros(n, np.uint32)
+    cells, mean, sd = [], [], []
+    for i in range(n):
+        c, m, s_ = f.particle_map(i)
+        o = np.argsort(c)
+        count[i] = len(c)
+        cells.append(c[o]); mean.append(m[o]); sd.append(s_[o])
+    rec["maps/count"] = count
+    rec["maps/cells"] = np.concatenate(cells) if cells else np.zeros(0, np.uint32)
+    rec["maps/mean"] = np.concatenate(mean) if mean else np.zeros(0, np.float32)
+    rec["maps/stdev"] = np.concatenate(sd) if sd else np.zeros(0, np.float32)
+
+
 def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
     """f: OracleFilter or GpuFilter-like (set_map/init_gaussian/upload/step/...).
     info_fn(f) returns the eslam_update_info of the last update."""
     rec = {}
     grid = scenario_grid(name)
     f.set_map(grid)
+    if name == "heirloom":
+        # one particle on the last rank maps a wide scan (~50 pages) and then holds all the weight:
+        # the resample copies it to every output, so every other rank receives one record for
+        # all its particles (one table and one set of pages for the record, not one per copy),
+        # and a map update then copies on write what each particle changes
+        f.upload(heirloom_arrays(n_global, lo, hi))
+        f.map_update(S.scan_patches(nx=16, ny=12, x0=-2.6, x1=4.6, y0=-2.5, y1=2.4))
+        f.resample()
+        _snap(rec, "res", f, True)
+        _maps(rec, f, hi - lo)
+        for k, st in enumerate(S.step_stream(2)):
+            f.step(st)
+            f.map_update(S.scan_patches())
+            _snap(rec, f"s{k}", f, True)
+        rec["maps2/count"] = np.array([len(f.particle_map(g - lo)[0]) for g in range(lo, hi) if g % 97 == 0], np.uint32)
+        return rec
     if name == "upload":
         f.upload(upload_arrays(n_global, lo, hi))
         rec["sum0"] = np.array([f.weights_sum()])
@@ -233,18 +284,7 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         if scan is not None:                     # processMap(scan, false, true)
             f.map_update(scan)
     if scan is not None:                         # every particle's own patches, sorted by cell
-        n = hi - lo
-        count = np.zeros(n, np.uint32)
-        cells, mean, sd = [], [], []
-        for i in range(n):
-            c, m, s_ = f.particle_map(i)
-            o = np.argsort(c)
-            count[i] = len(c)
-            cells.append(c[o]); mean.append(m[o]); sd.append(s_[o])
-        rec["maps/count"] = count
-        rec["maps/cells"] = np.concatenate(cells) if cells else np.zeros(0, np.uint32)
-        rec["maps/mean"] = np.concatenate(mean) if mean else np.zeros(0, np.float32)
-        rec["maps/stdev"] = np.concatenate(sd) if sd else np.zeros(0, np.float32)
+        _maps(rec, f, hi - lo)
     rec["best"] = np.array([f.best_index()])
     rec["rng"] = np.array([f.rng_state().minstd_x])
     pos, quat = f.centroid()                 # getCentroid (normalises in place, Q15)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
                                                  ("upload", 700, 3), ("hash", 3000, 2), ("hash", 1500, 3),
                                                  ("maps", 3000, 2), ("maps", 1500, 3),
                                                  ("burst", 5000, 2), ("burst", 7001, 3), ("edit", 3000, 2),
-                                                 ("edit", 1500, 3)])
+                                                 ("edit", 1500, 3), ("heirloom", 2000, 2), ("heirloom", 1500, 3)])
 def test_sharded_gpu_gloo_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, world, str(tmp_path), mem="host", timeout=400))

@@ -98,48 +98,102 @@ def test_fuse_and_window(oracle):
         assert np.max(m) >= 8 * pm + 24                  # it reaches 3 tiles ahead
 
 
-def test_window_forgets_what_it_leaves(oracle):
-    """The robot walks 6 m: the tiles its window leaves are forgotten, nothing within
-    maxSensorRange of the particle is dropped, and the map never holds more than the window."""
-    n = 32
+def loop_walk(trail, n=32, out=300, back=260):
+    """6 m out and (nearly) back on the empty prior with a map update after every step; returns
+    the filter, the first cells particle 0 mapped, the found-contact fraction per step of the
+    way back and the evictions"""
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS
+    cfg.local_map_trail = trail
     grid = S.unmapped_beyond(S.flat_map(cells=200), -1e9)          # the reference's empty start
     f = O.OracleFilter(cfg, O.SUM_CONTRACT)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
     scan = S.scan_patches()
-    first = None
-    for k, st in enumerate(S.step_stream(300, dx=0.02, dyaw=0.0)):
+    first, found_back, evicted = None, [], 0
+    stream = S.step_stream(out, dx=0.02, dyaw=0.0) + S.step_stream(back, dx=-0.02, dyaw=0.0)
+    for k, st in enumerate(stream):
         f.step(st)
         f.map_update(scan)
         assert f.info().map_patches_dropped == 0, k
+        evicted += f.info().map_tiles_evicted
         if k == 10:
             first = set(f.particle_map(0)[0].tolist())
+        if k >= out:
+            found_back.append(float(np.mean(f.download().n_contact_points == 4)))
+    return f, grid, first, found_back, evicted
+
+
+def test_trail_keeps_what_the_window_leaves(oracle):
+    """The robot walks 6 m and back (the reference keeps every grid its MLSMap made,
+    src/EmbodiedSlamFilter.cpp:195-207): the tiles the window leaves go to the trail, and on the
+    way back the feet find the cells mapped on the way out -- the scan looks ahead in +x, so
+    walking back it never maps the cells under the feet itself.  Without a trail they are
+    forgotten and the feet find nothing.  A trail larger than the walk needs changes no bit."""
+    f, grid, first, found, ev = loop_walk(16)
+    g, _, first0, found0, ev0 = loop_walk(0)
+    h, _, _, found_big, ev_big = loop_walk(64)
+    assert ev == 0 and ev_big == 0 and ev0 > 0
+    # the last 80 steps (1.6 m) of the way back: more than 3.2 m from where the walk turned
+    assert np.mean(found[-80:]) > 0.9 and min(found[-80:]) > 0.7, found   # the cells of the way out
+    assert max(found0[-80:]) < 0.05, found0             # forgotten without a trail
     last = set(f.particle_map(0)[0].tolist())
-    assert first and not (first & last)                 # 6 m later the first cells are gone
-    p = f.download()
-    c, _, _ = f.particle_map(0)
-    x = grid.offset[0] + (c % grid.width + 0.5) * grid.scale[0]
-    assert np.all(np.abs(x - p.x[0]) < 4.1)
-    assert np.mean(p.n_contact_points == 4) > 0.8       # the feet stand on merged cells only
+    assert first <= last                                # the first cells are still held
+    assert first0 and not (first0 & set(g.particle_map(0)[0].tolist()))
+    pf, ph = f.download(), h.download()
+    for fld in ("x", "y", "orientation", "zpos", "zsigma", "weight"):
+        assert np.array_equal(getattr(pf, fld), getattr(ph, fld)), fld
+    for i in (0, 7, 31):
+        c1, m1, s1 = f.particle_map(i)
+        c2, m2, s2 = h.particle_map(i)
+        assert sorted(zip(c1.tolist(), m1.tolist(), s1.tolist())) == sorted(zip(c2.tolist(), m2.tolist(), s2.tolist()))
 
 
 def _fma(a, b, c):
     return float(Fraction(a) * Fraction(b) + Fraction(c))
 
 
+def _model_recentre(ctr, tiles, trail, nc, h, w):
+    """the window moves from ctr to nc: the tiles leaving it go to the trail in slot order -- an
+    empty entry, else in place of the entry farthest from nc (Chebyshev, the first of them) if
+    that is farther than the tile -- then the trail's tiles inside the new window come back;
+    returns the new (tiles, trail) and the tiles forgotten"""
+    inside = lambda t: abs(t[0] - nc[0]) <= h and abs(t[1] - nc[1]) <= h
+    dist = lambda t: max(abs(t[0] - nc[0]), abs(t[1] - nc[1]))
+    keep = {t: v for t, v in tiles.items() if inside(t)}
+    leaving = sorted((t for t in tiles if not inside(t)), key=lambda t: (t[0] % w) + w * (t[1] % w))
+    trail = list(trail)
+    forgot = 0
+    for t in leaving:
+        if None in trail:
+            trail[trail.index(None)] = (t, tiles[t])
+            continue
+        forgot += 1
+        if trail:
+            far = max(range(len(trail)), key=lambda e: (dist(trail[e][0]), -e))
+            if dist(trail[far][0]) > dist(t):
+                trail[far] = (t, tiles[t])
+    for e, ent in enumerate(trail):
+        if ent is not None and inside(ent[0]):
+            keep[ent[0]] = ent[1]
+            trail[e] = None
+    return keep, trail, forgot
+
+
 def _model_update(maps, p, scan, grid, sincos):
-    """processMap on the window model: maps[i] = (centre, {tile: {cell_in_tile: (mean, sd)}})."""
+    """processMap on the window model: maps[i] = (centre, {tile: {cell_in_tile: (mean, sd)}},
+    trail [(tile, cells) or None] * V)."""
     h, w = 4, 9
     inv_x, inv_y = 1.0 / grid.scale[0], 1.0 / grid.scale[1]
-    drop = 0
+    drop = forgot = 0
     for i in range(len(maps)):
-        ctr, tiles = maps[i]
+        ctr, tiles, trail = maps[i]
         bx, by = p.x[i] - grid.offset[0], p.y[i] - grid.offset[1]
         nc = (math.floor(bx * inv_x) >> 3, math.floor(by * inv_y) >> 3)
         if nc != ctr:
-            tiles = {t: v for t, v in tiles.items() if abs(t[0] - nc[0]) <= h and abs(t[1] - nc[1]) <= h}
+            if ctr is not None:
+                tiles, trail, fg = _model_recentre(ctr, tiles, trail, nc, h, w)
+                forgot += fg
             ctr = nc
         tiles = {t: dict(v) for t, v in tiles.items()}
         sn, co = sincos(p.orientation[i])
@@ -165,44 +219,53 @@ def _model_update(maps, p, scan, grid, sincos):
                     cells[j] = (np.float32((m1 * var + wz * v1) / (v1 + var)), np.float32(math.sqrt((v1 * var) / (v1 + var))))
             else:
                 cells[j] = (np.float32(wz), np.float32(math.sqrt(var)))
-        maps[i] = (ctr, tiles)
-    return drop
+        maps[i] = (ctr, tiles, trail)
+    return drop, forgot
 
 
-@pytest.mark.parametrize("nx,ny,steps", [(10, 5, 40), (13, 10, 16)])
-def test_window_model(oracle, nx, ny, steps):
+@pytest.mark.parametrize("nx,ny,steps,dx,trail", [(10, 5, 40, 0.05, 16), (13, 10, 16, 0.05, 16), (10, 5, 40, 0.15, 16),
+                                                 (10, 5, 40, 0.15, 3), (10, 5, 30, 0.15, 0)])
+def test_window_model(oracle, nx, ny, steps, dx, trail):
     """The oracle's map update against the Python window model, cell for cell, over the bench
     stream (with its resample copies) on the empty prior and with a scan wide enough to reach
     past the window; the 130-patch scan is merged in parts of 64 (eslam_gpu_map_update), the
-    model takes it whole."""
+    model takes it whole.  dx 0.15: the windows move 6 m, tiles go to the trail (3 entries: it
+    overflows and forgets the farthest; 0: no trail)."""
     n = 12
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
-    grid = S.unmapped_beyond(S.flat_map(cells=160), -1e9)
+    cfg.local_map_trail = trail
+    grid = S.unmapped_beyond(S.flat_map(cells=240), -1e9)
     f = O.OracleFilter(cfg, O.SUM_CONTRACT)
     f.set_map(grid)
     f.init_gaussian(n, [0.0, 0.0, 0.0], [0.3, 0.3, 0.2], 0.18, 0.05)
     scan = S.scan_patches(nx=nx, ny=ny, x0=-0.5, x1=4.2, y0=-1.5, y1=1.0)
     sincos = lambda th: (O.dm(2, th), O.dm(3, th))
-    maps = [(None, {}) for _ in range(n)]
-    for k, st in enumerate(S.step_stream(steps, dx=0.05)):
+    maps = [(None, {}, [None] * trail) for _ in range(n)]
+    evicted = 0
+    for k, st in enumerate(S.step_stream(steps, dx=dx)):
         f.step(st)
         anc = f.ancestors().astype(np.int64) if f.info().resampled else np.arange(n)
         maps = [maps[a] for a in anc]
         p = f.download()
-        drop = _model_update(maps, p, scan, grid, sincos)
+        drop, forgot = _model_update(maps, p, scan, grid, sincos)
         f.map_update(scan)
         assert f.info().map_patches_dropped == drop, k
+        assert f.info().map_tiles_evicted == forgot, k
+        evicted += forgot
         for i in range(n):
             c, m, s_ = f.particle_map(i)
             want = {}
-            for (ta, tb), cells in maps[i][1].items():
+            held = list(maps[i][1].items()) + [e for e in maps[i][2] if e is not None]
+            for (ta, tb), cells in held:
                 for j, v in cells.items():
                     want[(8 * tb + j // 8) * grid.width + 8 * ta + j % 8] = v
             got = {int(cc): (mm, ss) for cc, mm, ss in zip(c, m, s_)}
             assert set(got) == set(want), (k, i)
             for cc, v in want.items():
                 assert got[cc][0].view(np.uint32) == v[0].view(np.uint32) and got[cc][1].view(np.uint32) == v[1].view(np.uint32), (k, i, cc)
+    if dx > 0.1:
+        assert (evicted > 0) == (trail < 16), evicted
 
 
 def test_covered_cells_are_counted(oracle):
@@ -232,6 +295,8 @@ def test_covered_cells_are_counted(oracle):
 
 
 def flat_scan(dz=0.0, **kw):
+    kw.setdefault("x0", 1.2)                # far enough ahead that no patch lands on the mapped
+    kw.setdefault("x1", 1.8)                # cells x < 0.3 (rotated grid included)
     scan = S.scan_patches(**kw)
     for k in range(len(scan)):
         scan[k].position[2] = -0.18 + dz
@@ -246,7 +311,8 @@ def test_match_weights_against_own_map(oracle, rotated):
     bit for bit), a scan dz higher multiplies each matched particle's weight by
     float(exp(-dz^2 / (2 * 0.2f^2)))^0.1f and leaves the unmatched ones as they are, and only
     every 10th patch counts (sampling 10).  rotated: a grid whose global2local is a rotation and
-    a shift (every cell placed through the transform)."""
+    a shift (every cell placed through the transform).  The scan lies on cells the shared grid
+    leaves empty (its own cells: test_match_against_the_shared_grid)."""
     if rotated:
         cfg = S.bench_config(A.default_config(), 600)
         cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
@@ -283,3 +349,52 @@ def test_match_weights_against_own_map(oracle, rotated):
     matched = np.abs(r - expect) < 1e-6
     assert np.all(matched | (r == 1.0))
     assert matched.mean() > 0.9
+
+
+def match_expect(p, dz, sd_scan=0.03, grid_sd=0.05):
+    """closed form of the shared-grid rule on the flat map (mean 0): every sampled patch of a
+    particle lands on a grid cell at local height -0.18 + dz + zPos, so its score is the same
+    for all of them: exp(-d^2 / (2 * 0.2f^2)) when the 3-sigma gate passes, else 0"""
+    sig = float(np.float32(0.2))
+    d = -0.18 + dz + p.zpos
+    qv = sd_scan * sd_scan + p.zsigma * p.zsigma
+    gs = float(np.float32(grid_sd))
+    score = np.where(d * d < 9.0 * (gs * gs + qv), np.exp(-(d * d) / (2.0 * sig * sig)), 0.0)
+    wf = score.astype(np.float32).astype(np.float64)
+    return wf ** float(np.float32(0.1))
+
+
+@pytest.mark.parametrize("pmaps", [False, True])
+def test_match_against_the_shared_grid(oracle, pmaps):
+    """processMap(scanMap, match = true) with the shared map (useSharedMap = true: the laser
+    path's match-only call, src/EmbodiedSlamFilter.cpp:214-221,342-344), and the grid's cells of
+    a per-particle map (the clone the reference merges into holds them): each sampled patch
+    scores against the patch getPatch's 3-sigma gate picks in its cell (0 when none passes);
+    patches off the grid do not count (weights unchanged)."""
+    n = 400
+    cfg = S.bench_config(A.default_config(), n)
+    if pmaps:
+        cfg.flags |= A.FLAG_PARTICLE_MAPS
+    grid = S.flat_map(cells=60)
+    f = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    f.set_map(grid)
+    f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    f.step(S.step_stream(1)[0])
+    for dz in (0.0, 0.07, 0.5):
+        p = f.download()
+        w0 = p.weight.copy()
+        f.map_match(flat_scan(dz, x0=0.35, x1=0.95))
+        r = f.download().weight / w0
+        want = match_expect(p, dz)
+        assert np.allclose(r, want, rtol=1e-12, atol=0.0), (dz, np.max(np.abs(r - want)))
+        if dz == 0.5:
+            assert np.all(r == 0.0)                      # no patch within 3 sigma: score 0
+        else:
+            f.upload(p)                                  # back to the weights before the match
+    f2 = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    f2.set_map(grid)
+    f2.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    f2.step(S.step_stream(1)[0])
+    w0 = f2.download().weight.copy()
+    f2.map_match(flat_scan(0.0, x0=40.0, x1=41.0))        # beyond the 6 m grid: nothing counts
+    assert np.array_equal(f2.download().weight, w0)
