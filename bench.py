@@ -70,6 +70,9 @@ def parse():
                     help="configs[4]'s per-particle local maps (useSharedMap = false): rough terrain, unmapped "
                          "beyond x = 0.3 m, one map update (processMap merge) per step; default 8M particles per "
                          "GPU (64M over 8 GPUs with --gpus 8)")
+    ap.add_argument("--scan-patches", type=int, default=0,
+                    help="with --local-maps: the scan's patch count (0: the 48-patch 0.6 x 0.9 m scan; e.g. 600: "
+                         "a 2.5 x 2.4 m MLS ahead at 0.1 m, synthetic.scan_area)")
     ap.add_argument("--match", action="store_true",
                     help="with --local-maps: processMap(scan, match = true, update = true), the match "
                          "weighting (eslam_gpu_map_match) before every merge")
@@ -202,79 +205,6 @@ def cpu_baseline(args, grid, flags=0, scan=None):
     return out
 
 
-def gpu_card(device):
-    """The sysfs node of the GPU this process runs on, matched by the PCI address the HIP
-    runtime (the one libeslam_gpu already loaded) reports for it; None if not found."""
-    import ctypes as C
-    import glob
-    try:
-        hip = C.CDLL("libamdhip64.so", mode=C.RTLD_GLOBAL)
-        buf = C.create_string_buffer(64)
-        rc = hip.hipDeviceGetPCIBusId(buf, 64, int(device))
-        if rc != 0:
-            raise RuntimeError(f"hipDeviceGetPCIBusId returned {rc}")
-        want = buf.value.decode().lower()
-    except Exception as e:                 # noqa: BLE001 -- a report field, never fatal
-        sys.stderr.write(f"bench.py: no PCI address for the clock report ({e})\n")
-        return None
-    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
-        if os.path.basename(os.path.realpath(dev)).lower() == want:
-            return dev
-    sys.stderr.write(f"bench.py: no sysfs card at PCI {want} for the clock report\n")
-    return None
-
-
-def _dpm_mhz(dev, name):
-    """the level marked '*' in sysfs pp_dpm_sclk / pp_dpm_mclk, in MHz (None if unreadable)"""
-    try:
-        with open(os.path.join(dev, name)) as fh:
-            for ln in fh:
-                if ln.rstrip().endswith("*"):
-                    return int("".join(c for c in ln.split(":", 1)[1] if c.isdigit()))
-    except (OSError, ValueError):
-        pass
-    return None
-
-
-class ClockSampler:
-    """The shader clock of this process's GPU sampled every 2 ms while the timed region runs
-    (sysfs, no HIP call): a box whose card ran below its peak clock shows it here."""
-
-    def __init__(self, device):
-        import threading
-        self.dev = gpu_card(device)
-        self.sclk = []
-        self._stop = threading.Event()
-        self._t = threading.Thread(target=self._run, daemon=True) if self.dev else None
-
-    def _run(self):
-        while not self._stop.is_set():
-            v = _dpm_mhz(self.dev, "pp_dpm_sclk")
-            if v is not None:
-                self.sclk.append(v)
-            self._stop.wait(0.002)
-
-    def __enter__(self):
-        if self._t:
-            self._t.start()
-        return self
-
-    def __exit__(self, *exc):
-        self._stop.set()
-        if self._t:
-            self._t.join()
-
-    def report(self):
-        if not self.dev:
-            return None
-        s = sorted(self.sclk)
-        return {"card": os.path.basename(os.path.dirname(self.dev)) if self.dev.endswith("/device") else self.dev,
-                "pci": os.path.basename(os.path.realpath(self.dev)),
-                "sclk_mhz_timed": {"samples": len(s), "min": s[0] if s else None, "median": s[len(s) // 2] if s else None,
-                                   "max": s[-1] if s else None},
-                "mclk_mhz": _dpm_mhz(self.dev, "pp_dpm_mclk")}
-
-
 def visible_gpus():
     """GPUs this process could open, counted without any HIP or torch.cuda call: the KFD
     topology's GPU nodes (simd_count > 0), narrowed by a *_VISIBLE_DEVICES list if one is set.
@@ -360,6 +290,8 @@ def main():
         args.rough = True
     if args.cpu_sample is None:
         args.cpu_sample = 262144 if args.local_maps else 1048576
+        if args.local_maps and args.scan_patches > 48:      # the same ~10-30 s of CPU work
+            args.cpu_sample = max(4096, (262144 * 48 // args.scan_patches) // 1024 * 1024)
     if args.cpu_steps is None:
         args.cpu_steps = 24 if args.local_maps else 48
     if args.particles is None:
@@ -401,7 +333,7 @@ def main():
     scan = None
     if args.local_maps:
         grid = S.unmapped_beyond(grid, 0.3)    # the front feet stand on cells only the scans map
-        scan = S.scan_patches()
+        scan = S.scan_area(args.scan_patches) if args.scan_patches > 0 else S.scan_patches()
     stream = S.step_stream(args.warmup + 2 * args.steps + 1, tilt=args.local_maps)
     cfg = S.bench_config(A.default_config(), n * world)
     if args.match and not args.local_maps:
@@ -455,15 +387,13 @@ def main():
     barrier()
     # timed region: K steps back to back, no per-kernel events (HIP event records between
     # the launches cost ~10 % of a step here)
-    clocks = ClockSampler(local_rank if dist is not None else 0)
-    with clocks:
-        t0 = time.perf_counter()
-        for st in stream[args.warmup:args.warmup + args.steps]:
-            f_step(st)
-        t_enq = time.perf_counter()         # the host has queued every launch (nothing waits on the GPU)
-        info = f.sync()
-        barrier()
-        dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for st in stream[args.warmup:args.warmup + args.steps]:
+        f_step(st)
+    t_enq = time.perf_counter()             # the host has queued every launch (nothing waits on the GPU)
+    info = f.sync()
+    barrier()
+    dt = time.perf_counter() - t0
     # kernel breakdown: the next K steps of the same stream with HIP events around every
     # launch, on the context's stream (eslam_gpu_enable_timing)
     f.enable_timing(True)
@@ -515,7 +445,6 @@ def main():
         "dtype_note": "all particle state, weights, sums and map values' arithmetic in fp64 (map cells stored as "
                       "fp32); the project step's Box-Muller radius and angle are IEEE fp32 (DESIGN.md 2), the "
                       "oracle computing the same fp32 operations",
-        "clocks": clocks.report(),
         "data": "synthetic (%s %gx%g m MLS map @0.1 m; odometry + 4 foot contacts per step%s)"
                 % ("rough multi-patch" if args.rough else "flat", args.map_cells / 10, args.map_cells / 10,
                    "; unmapped beyond x = 0.3 m, a %d-patch scan merged into every particle's map per step"
@@ -550,6 +479,7 @@ def main():
         **({"map_update": {"patches_dropped": info.map_patches_dropped, "tables_copied": info.map_stores_copied,
                            "maps_changed": info.map_stores_changed, "patches_covered": info.map_patches_covered,
                            "cells_written": info.map_cells_written, "pages_taken": info.map_pages_taken,
+                           "tiles_evicted": info.map_tiles_evicted, "scan_patches": len(scan),
                            "pages_free": info.map_pages_free, "patches_total": n * len(scan),
                            "data_particles": info.data_particles, "window_slots": window_slots(cfg.max_sensor_range, 0.1),
                            "note": "the last step's map update: scan patches beyond a particle's window (farther "

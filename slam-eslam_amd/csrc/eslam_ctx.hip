@@ -31,7 +31,7 @@ extern "C" hipError_t eslam_launch_store_refs(SidRef sid, uint64_t n, uint64_t p
                                               uint32_t* tgen, hipStream_t stream);
 extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint64_t n,
                                                  const CowScratch* cs, const void* hdr, uint64_t nrecv, uint32_t* hoff,
-                                                 const void* pay, uint32_t* pgc, hipStream_t stream);
+                                                 uint32_t* head, const void* pay, uint32_t* pgc, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
                                             const MergeParams* mp, uint32_t* pgc, hipStream_t stream);
 extern "C" hipError_t eslam_launch_map_match(DevState s0, DevState s1, const Ctl* ctl, const MapView* map, const LocalMaps* lm,
@@ -39,9 +39,11 @@ extern "C" hipError_t eslam_launch_map_match(DevState s0, DevState s1, const Ctl
 extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl, const MapView* map, const LocalMaps* lm,
                                              const MergeParams* mp, hipStream_t stream);
 extern "C" hipError_t eslam_launch_pay_hdr(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
-                                           uint64_t gbase, const LocalMaps* lm, void* hdr, uint32_t* off, hipStream_t stream);
+                                           uint64_t gbase, const LocalMaps* lm, const PaySeg* seg, void* hdr, uint32_t* off,
+                                           hipStream_t stream);
 extern "C" hipError_t eslam_launch_pay_pack(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
-                                            uint64_t gbase, const LocalMaps* lm, const uint32_t* off, void* pay, hipStream_t stream);
+                                            uint64_t gbase, const LocalMaps* lm, const void* hdr, const uint32_t* off, void* pay,
+                                            hipStream_t stream);
 extern "C" hipError_t eslam_launch_pack_records(DevState s0, DevState s1, const Ctl* ctl, uint64_t first, uint64_t stride,
                                                 uint64_t count, uint64_t gbase, const uint32_t* anc, const DebugRec* d,
                                                 eslam_particle_record* out, eslam_cpoint* cps, uint32_t max_cp,
@@ -341,6 +343,7 @@ struct eslam_ctx {
     void* sendhdr = nullptr; uint64_t sendhdr_cap = 0;
     void* recvhdr = nullptr; uint64_t recvhdr_cap = 0;
     uint32_t* payoff = nullptr; uint64_t payoff_cap = 0;   // header prefix (send side, then receive side)
+    uint32_t* rhead = nullptr; uint64_t rhead_cap = 0;     // received records: the record carrying each one's map
     uint64_t nrecv_maps = 0;                 // records whose maps wait in recvhdr / recvpay
     double* cent = nullptr; uint64_t cent_bytes = 0;   // sharded getCentroid's chunk records (set_comm)
     double* bspill = nullptr; uint64_t bspill_cap = 0;  // K1's parked per-bucket sums (k1_bspill_bytes)
@@ -716,7 +719,7 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     (void)hipFree(ctx->recs); (void)hipFree(ctx->mg); (void)hipHostFree(ctx->mg_host);
     (void)hipFree(ctx->sendbuf); (void)hipFree(ctx->recvbuf); (void)hipHostFree(ctx->stage);
     (void)hipFree(ctx->sendpay); (void)hipFree(ctx->recvpay); (void)hipFree(ctx->cent); (void)hipFree(ctx->bspill);
-    (void)hipFree(ctx->sendhdr); (void)hipFree(ctx->recvhdr); (void)hipFree(ctx->payoff);
+    (void)hipFree(ctx->sendhdr); (void)hipFree(ctx->recvhdr); (void)hipFree(ctx->payoff); (void)hipFree(ctx->rhead);
     (void)hipFree(ctx->d_hash); (void)hipFree(ctx->d_hash_blist); (void)hipFree(ctx->d_sort); (void)hipFree(ctx->sort_tmp); (void)hipFree(ctx->d_draws);
     (void)hipFree(ctx->hsend); (void)hipFree(ctx->hrecv); (void)hipFree(ctx->hsort);
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
@@ -1935,10 +1938,11 @@ static int store_receive(eslam_ctx* ctx)
     const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
     HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, nullptr, ctx->lm.tgen, ctx->stream));
     int rc = grow(ctx, (void**)&ctx->payoff, &ctx->payoff_cap, (ctx->nrecv_maps + 1) * 4, false);
+    if (!rc) rc = grow(ctx, (void**)&ctx->rhead, &ctx->rhead_cap, (ctx->nrecv_maps + 1) * 4, false);
     if (rc) return rc;
     const MergeParams mp = merge_params(ctx, cs);
     HIPCHK(ctx, eslam_launch_store_receive(sr, ctx->ctl, &ctx->lm, &mp, ctx->n, &cs, ctx->recvhdr, ctx->nrecv_maps, ctx->payoff,
-                                           ctx->recvpay, ctx->lm_pgc, ctx->stream));
+                                           ctx->rhead, ctx->recvpay, ctx->lm_pgc, ctx->stream));
     ctx->cow_pending = false;
     return ESLAM_OK;
 }
@@ -2108,8 +2112,12 @@ static int exchange_maps(eslam_ctx* ctx, uint64_t nsend, uint64_t nrecv, const u
     if (!rc) rc = grow(ctx, &ctx->recvhdr, &ctx->recvhdr_cap, (nrecv ? nrecv : 1) * H, false);
     if (!rc) rc = grow(ctx, (void**)&ctx->payoff, &ctx->payoff_cap, (nsend + nrecv + 2) * 4, false);
     if (rc) return rc;
-    HIPCHK(ctx, eslam_launch_pay_hdr(ctx->st[0], ctx->st[1], ctx->ctl, ctx->sendbuf, nsend, ctx->gbase, &ctx->lm, ctx->sendhdr,
-                                     ctx->payoff, xs));
+    PaySeg seg;
+    memset(&seg, 0, sizeof(seg));
+    for (int d = 0; d <= G; ++d) seg.off[d] = pp.send_off[d];
+    seg.n = G;
+    HIPCHK(ctx, eslam_launch_pay_hdr(ctx->st[0], ctx->st[1], ctx->ctl, ctx->sendbuf, nsend, ctx->gbase, &ctx->lm, &seg,
+                                     ctx->sendhdr, ctx->payoff, xs));
     // the page counts per destination (records [send_off[d], send_off[d + 1]) go to rank d)
     std::vector<uint32_t> bound(G + 1);
     for (int d = 0; d <= G; ++d)
@@ -2127,8 +2135,8 @@ static int exchange_maps(eslam_ctx* ctx, uint64_t nsend, uint64_t nrecv, const u
     rc = grow(ctx, &ctx->sendpay, &ctx->sendpay_cap, ((uint64_t)bound[G] + 1) * P, false);
     if (!rc) rc = grow(ctx, &ctx->recvpay, &ctx->recvpay_cap, (totr + 1) * P, false);
     if (rc) return rc;
-    HIPCHK(ctx, eslam_launch_pay_pack(ctx->st[0], ctx->st[1], ctx->ctl, ctx->sendbuf, nsend, ctx->gbase, &ctx->lm, ctx->payoff,
-                                      ctx->sendpay, xs));
+    HIPCHK(ctx, eslam_launch_pay_pack(ctx->st[0], ctx->st[1], ctx->ctl, ctx->sendbuf, nsend, ctx->gbase, &ctx->lm, ctx->sendhdr,
+                                      ctx->payoff, ctx->sendpay, xs));
     uint64_t hs[kMaxRanks], hr[kMaxRanks], ps[kMaxRanks], pr[kMaxRanks];
     for (int d = 0; d < G; ++d) {
         hs[d] = sb[d] / R * H; hr[d] = rb[d] / R * H;

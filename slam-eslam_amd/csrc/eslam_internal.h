@@ -140,6 +140,8 @@ struct LocalMaps {
     uint64_t npages, ntables;
 };
 static_assert(sizeof(int2) == 8, "centre");
+constexpr int kMaxRanks = 16;
+
 // sharded filters: a particle that a resample received from another rank names no local table
 // yet; its sid is kSidRecord | the record index, and the copy on write that follows the gather
 // gives it a free table (and pages) filled from the record's payload (the migrated map)
@@ -148,7 +150,16 @@ constexpr uint32_t kSidRecord = 0x80000000u;
 // of all records in the records' order, each with its slot
 struct alignas(8) MapPayHdr {
     int2 ctr;
-    uint32_t npg, pad;
+    uint32_t npg;
+    uint32_t share;                      // 1: the previous record (same source, same destination)
+                                         // carries this record's map (npg 0): they name one table
+};
+// the first record of each destination's range of a sharded send (PlanParams::send_off): a
+// record there always carries its map
+struct PaySeg {
+    uint64_t off[kMaxRanks + 1];
+    int32_t n;
+    int32_t pad;
 };
 struct alignas(8) MapPayPage {
     uint32_t slot;                       // a window slot, or kPayTrail | trail entry e of tile (a, b)
@@ -431,7 +442,6 @@ constexpr uint32_t kFaultTimeout = 4u;
 constexpr uint32_t kFaultPages = 8u;
 constexpr uint32_t kSpinLimit = 1u << 18;    // x s_sleep(8) (512 clocks): ~60 ms
 
-constexpr int kMaxRanks = 16;
 
 struct PlanParams {
     uint64_t n_global;

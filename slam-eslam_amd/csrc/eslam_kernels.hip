@@ -2049,11 +2049,13 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             lm_codes(map, lm, mp, q, codes, covered, dropped);
             const int2 oc = lm.ctr[q.X];
             const uint32_t T = q.shared ? mp.frees[i] : q.X;
-            // the window moves to the particle (and a shared table is copied to T): from here
-            // on every tile the scan reaches is in T's slots
+            // the window moves to the particle (into T: a shared table is copied): from here on
+            // every tile the scan reaches is in T's slots.  A shared table whose window stays is
+            // copied by the merge (a group of lanes per particle moves the row coalesced); its
+            // tiles are X's slots
             const bool moved = oc.x != q.na || oc.y != q.nb;
-            if (q.shared || moved) forgot = lm_rewrite(lm, q.X, T, oc, q.na, q.nb);
-            const uint32_t* trow = lm.slot + (uint64_t)T * lm.S;
+            if (moved) forgot = lm_rewrite(lm, q.X, T, oc, q.na, q.nb);
+            const uint32_t* trow = lm.slot + (uint64_t)(moved ? T : q.X) * lm.S;
             const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
             uint32_t L[kLmList];
             lm_collect(codes, mp.m, kLmNoList, L);
@@ -2165,6 +2167,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][kMaxScanPatches];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
     __shared__ uint8_t s_list[kLmPpb][kMaxScanPatches];                                // a stage's patches, in scan order
+    __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
@@ -2218,9 +2221,12 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
             const uint32_t k = l + kLmLanes * u;
             code[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
         }
-        // the plan has moved T's window (and copied a shared X to T): every tile of the scan is
-        // in T's slots, and the merge only adds the new pages
+        // the plan has moved T's window (a moved shared X copied to T): every tile of the scan is
+        // in T's slots, and the merge only adds the new pages -- but a shared X whose window
+        // stays is copied to T here, the pass's new pages folded in
+        const bool copy = shared && !(flags & kJobMoved);
         uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
+        const uint32_t* xsl = lm.slot + (uint64_t)X * lm.S;
         const uint32_t gshift = (tid & 63u) & ~(kLmLanes - 1u);
         const double zvar = zs * zs;
         uint8_t* stage = &s_stage[wv][0];
@@ -2285,6 +2291,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     if (code[u] != kCodeSkip && (int32_t)(code[u] >> 6) > lo) nx = min(nx, code[u] >> 6);
                 more = cnt == kLmList && grp_min(nx) != kLmNoList;
                 if (l < cnt) {
+                    __builtin_amdgcn_s_waitcnt(0);   // the group's stores of T's row (pass 0) have landed
                     P = tsl[Lr];
                     need = !(!shared && P != DM_LM_NONE && lm.owner[P] == gT);
                 }
@@ -2298,7 +2305,29 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
             alloc += __builtin_popcount(gmask);
             // ---- 2. the table: the new pages into T's slots (a later pass: T's slot may have
             // been written by this group above -- the same wave, in order)
-            if (need) {
+            if (pass == 0 && copy) {
+                // X's row to T, four words a lane (each group instruction moves 128 contiguous
+                // bytes), with this pass's new pages; the trail's words as they are
+                if (l < kLmList) {
+                    s_np[pl][2 * l] = Lr;
+                    s_np[pl][2 * l + 1] = NP;
+                }
+                const uint32_t lmin = cnt ? grp_get(Lr, 0) : 1u, lmax = cnt ? grp_get(Lr, cnt - 1) : 0u;
+                wave_sync();
+                for (uint32_t q = l; q < lm.S / 4; q += kLmLanes) {
+                    uint4 w4 = reinterpret_cast<const uint4*>(xsl)[q];
+                    if (4 * q + 3 >= lmin && 4 * q <= lmax) {
+                        uint32_t v[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                        for (uint32_t e = 0; e < 4; ++e)
+                            for (uint32_t r = 0; r < cnt; ++r)
+                                if (s_np[pl][2 * r] == 4 * q + e && s_np[pl][2 * r + 1] != DM_LM_NONE) v[e] = s_np[pl][2 * r + 1];
+                        w4 = make_uint4(v[0], v[1], v[2], v[3]);
+                    }
+                    reinterpret_cast<uint4*>(tsl)[q] = w4;
+                }
+                if (l == 0) lm.ctr[T] = lm.ctr[X];
+            } else if (need) {
                 if (pass != 0) __builtin_amdgcn_s_waitcnt(0);
                 tsl[Lr] = NP;
             }
@@ -4141,10 +4170,21 @@ extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl,
 }
 
 // ---- sharded filters: the maps travel with the migrating particles -----------------------
-// k_pack's companion: each record's map header (its source's table centre and page count)
+// k_pack's companion: each record's map header (its source's table centre and page count).
+// A record is one output; the copies of one source that go to one rank are consecutive
+// records, and only the first of them carries the map (the others share it: one table and one
+// set of pages on the receiver, as the copies share them here)
+__device__ __forceinline__ bool pay_shares(const Rec* send, uint64_t j, const PaySeg& seg)
+{
+    if (j == 0 || (send[j].src >> 8) != (send[j - 1].src >> 8)) return false;
+    for (int32_t d = 0; d <= seg.n; ++d)
+        if (seg.off[d] == j) return false;               // the first record for a destination
+    return true;
+}
+
 __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const DevState s1, const Ctl* __restrict__ ctl,
                                                    const Rec* __restrict__ send, uint64_t nsend, uint64_t gbase, LocalMaps lm,
-                                                   MapPayHdr* __restrict__ hdr)
+                                                   PaySeg seg, MapPayHdr* __restrict__ hdr)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nw = (uint64_t)gridDim.x * kWaves;
@@ -4152,17 +4192,20 @@ __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const Dev
     for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
         const uint64_t i = (send[j].src >> 8) - gbase;
         const uint32_t X = st.sid[i];
+        const bool share = pay_shares(send, j, seg);
         const uint32_t* row = lm.slot + (uint64_t)X * lm.S;
         const uint32_t toff = lm.S - 4u * lm.V;
         uint32_t c = 0;
-        for (uint32_t s = lane; s < toff; s += 64u) c += row[s] != DM_LM_NONE ? 1u : 0u;
-        for (uint32_t e = lane; e < lm.V; e += 64u) c += row[toff + 4u * e + 2u] != DM_LM_NONE ? 1u : 0u;
-        c = wave_sum_u32(c);
+        if (!share) {
+            for (uint32_t s = lane; s < toff; s += 64u) c += row[s] != DM_LM_NONE ? 1u : 0u;
+            for (uint32_t e = lane; e < lm.V; e += 64u) c += row[toff + 4u * e + 2u] != DM_LM_NONE ? 1u : 0u;
+            c = wave_sum_u32(c);
+        }
         if (lane == 0) {
             MapPayHdr h;
             h.ctr = lm.ctr[X];
             h.npg = c;
-            h.pad = 0;
+            h.share = share ? 1u : 0u;
             hdr[j] = h;
         }
     }
@@ -4173,12 +4216,14 @@ __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const Dev
 // each page's 64 cells
 __global__ void __launch_bounds__(kBlock) k_pay_pack(const DevState s0, const DevState s1, const Ctl* __restrict__ ctl,
                                                     const Rec* __restrict__ send, uint64_t nsend, uint64_t gbase, LocalMaps lm,
-                                                    const uint32_t* __restrict__ off, MapPayPage* __restrict__ pay)
+                                                    const MapPayHdr* __restrict__ hdr, const uint32_t* __restrict__ off,
+                                                    MapPayPage* __restrict__ pay)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nw = (uint64_t)gridDim.x * kWaves;
     const DevState st = ctl->base ? s1 : s0;
     for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
+        if (hdr[j].share) continue;                      // the previous record carries the map
         const uint64_t i = (send[j].src >> 8) - gbase;
         const uint32_t X = st.sid[i];
         const uint32_t* row = lm.slot + (uint64_t)X * lm.S;
@@ -4224,11 +4269,37 @@ __global__ void __launch_bounds__(1024) k_pay_prefix(const MapPayHdr* __restrict
     if (threadIdx.x == 1023) out[m] = s_sum[1023];
 }
 
-// the received records' maps: record r takes free table frees[r] and its pages at hoff[r] past
-// the free list's cursor (pages once per record: every output copied from it names the table,
-// which its next map update then finds shared -- copy on write, as the copies of a one-GPU
-// resample), filled from the payload.  One wave per record: its lanes copy each page's cells,
-// then write the table's row (window slots, then the trail's entries {a, b, page, -})
+// the received records' map owners: head[r] = the last record at or before r that carries a
+// map (the copies of one source that came together share it); one block, ranges per thread
+__global__ void __launch_bounds__(1024) k_recv_heads(const MapPayHdr* __restrict__ hdr, uint64_t m, uint32_t* __restrict__ head)
+{
+    __shared__ uint32_t s_h[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    uint32_t h = 0;                                      // 1 + the last head of the range (0: none)
+    for (uint64_t i = lo; i < hi; ++i)
+        if (!hdr[i].share) h = (uint32_t)i + 1u;
+    s_h[threadIdx.x] = h;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {                 // inclusive max-scan over the threads
+        const uint32_t v = threadIdx.x >= (uint32_t)o ? s_h[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_h[threadIdx.x] = max(s_h[threadIdx.x], v);
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? s_h[threadIdx.x - 1] : 0u;
+    for (uint64_t i = lo; i < hi; ++i) {
+        if (!hdr[i].share) run = (uint32_t)i + 1u;
+        head[i] = run ? run - 1u : 0u;                   // record 0 always carries its map
+    }
+}
+
+// the received records' maps: a record r that carries one takes free table frees[r] and its
+// pages at hoff[r] past the free list's cursor, filled from the payload; the records sharing it
+// (and every output of them) name that table, which their next map update then finds shared --
+// copy on write, as the copies of a one-GPU resample.  One wave per record: its lanes copy
+// each page's cells, then write the table's row (window slots, then the trail's entries
+// {a, b, page, -})
 __global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uint32_t* __restrict__ frees, Ctl* __restrict__ ctl,
                                                         const MapPayHdr* __restrict__ hdr, const uint32_t* __restrict__ hoff,
                                                         const MapPayPage* __restrict__ pay, LocalMaps lm)
@@ -4238,6 +4309,7 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uin
     const uint64_t nw = (uint64_t)gridDim.x * (kLmBlock / 64);
     const uint32_t toff = lm.S - 4u * lm.V;
     for (uint64_t r = (uint64_t)blockIdx.x * (kLmBlock / 64) + (threadIdx.x >> 6); r < nrec; r += nw) {
+        if (hdr[r].share) continue;
         const uint64_t alloc = ctl->pg_cursor + hoff[r];
         const uint32_t T = frees[r];
         const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
@@ -4267,14 +4339,16 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uin
     }
 }
 
-// the particles a sharded resample received from record r (sid = kSidRecord | r) name frees[r]
+// the particles a sharded resample received from record r (sid = kSidRecord | r) name the
+// table of the record carrying r's map, frees[head[r]]
 __global__ void __launch_bounds__(kBlock) k_recv_rename(const uint32_t* __restrict__ dups, const uint32_t* __restrict__ frees,
-                                                        const uint32_t* __restrict__ ndup_dev, SidRef sr)
+                                                        const uint32_t* __restrict__ head, const uint32_t* __restrict__ ndup_dev,
+                                                        SidRef sr)
 {
     uint32_t* sid = cur_sid(sr);
     const uint64_t ndup = *ndup_dev;
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < ndup; j += (uint64_t)gridDim.x * kBlock)
-        sid[dups[j]] = frees[sid[dups[j]] & ~kSidRecord];
+        sid[dups[j]] = frees[head[sid[dups[j]] & ~kSidRecord]];
 }
 
 // the particles a sharded resample received (cs.dups, *cs.ndup, from nrecv records) get their
@@ -4283,7 +4357,7 @@ __global__ void __launch_bounds__(kBlock) k_recv_rename(const uint32_t* __restri
 // (nrecv + 1 words) scratch
 extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const LocalMaps* lm, const MergeParams* mp, uint64_t n,
                                                  const CowScratch* cs, const void* hdr, uint64_t nrecv, uint32_t* hoff,
-                                                 const void* pay, uint32_t* pgc, hipStream_t stream)
+                                                 uint32_t* head, const void* pay, uint32_t* pgc, hipStream_t stream)
 {
     if (!n) return hipSuccess;
     hipError_t e = compact(1, n, cs->ref, sid, cs->counts + cs->tiles + 1, cs->dups, cs->ndup, stream);
@@ -4291,6 +4365,7 @@ extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const Loc
     const MapPayHdr* h = (const MapPayHdr*)hdr;
     if (nrecv) {
         hipLaunchKernelGGL(k_pay_prefix, dim3(1), dim3(1024), 0, stream, h, nrecv, hoff);
+        hipLaunchKernelGGL(k_recv_heads, dim3(1), dim3(1024), 0, stream, h, nrecv, head);
     } else {
         e = hipMemsetAsync(hoff, 0, 4, stream);
         if (e != hipSuccess) return e;
@@ -4308,30 +4383,32 @@ extern "C" hipError_t eslam_launch_store_receive(SidRef sid, Ctl* ctl, const Loc
     hipLaunchKernelGGL(k_pg_advance, dim3(1), dim3(1), 0, stream, ctl);
     const uint64_t want_r = (n + kBlock - 1) / kBlock;
     const uint32_t gr = (uint32_t)(want_r < 2048 ? want_r : 2048);
-    hipLaunchKernelGGL(k_recv_rename, dim3(gr), dim3(kBlock), 0, stream, cs->dups, cs->frees, cs->ndup, sid);
+    hipLaunchKernelGGL(k_recv_rename, dim3(gr), dim3(kBlock), 0, stream, cs->dups, cs->frees, head, cs->ndup, sid);
     return hipGetLastError();
 }
 
 // a sharded resample's map payloads (after k_pack): headers, their prefix (off: nsend + 1
 // words; the host reads the per-destination page counts from it), then the pages
 extern "C" hipError_t eslam_launch_pay_hdr(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
-                                           uint64_t gbase, const LocalMaps* lm, void* hdr, uint32_t* off, hipStream_t stream)
+                                           uint64_t gbase, const LocalMaps* lm, const PaySeg* seg, void* hdr, uint32_t* off,
+                                           hipStream_t stream)
 {
     if (!nsend) return hipMemsetAsync(off, 0, 4, stream);
     const uint64_t g = (nsend + kWaves - 1) / kWaves;
     hipLaunchKernelGGL(k_pay_hdr, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(kBlock), 0, stream, s0, s1, ctl, (const Rec*)send,
-                       nsend, gbase, *lm, (MapPayHdr*)hdr);
+                       nsend, gbase, *lm, *seg, (MapPayHdr*)hdr);
     hipLaunchKernelGGL(k_pay_prefix, dim3(1), dim3(1024), 0, stream, (const MapPayHdr*)hdr, nsend, off);
     return hipGetLastError();
 }
 
 extern "C" hipError_t eslam_launch_pay_pack(DevState s0, DevState s1, const Ctl* ctl, const void* send, uint64_t nsend,
-                                            uint64_t gbase, const LocalMaps* lm, const uint32_t* off, void* pay, hipStream_t stream)
+                                            uint64_t gbase, const LocalMaps* lm, const void* hdr, const uint32_t* off, void* pay,
+                                            hipStream_t stream)
 {
     if (!nsend) return hipSuccess;
     const uint64_t g = (nsend + kWaves - 1) / kWaves;
     hipLaunchKernelGGL(k_pay_pack, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(kBlock), 0, stream, s0, s1, ctl, (const Rec*)send,
-                       nsend, gbase, *lm, off, (MapPayPage*)pay);
+                       nsend, gbase, *lm, (const MapPayHdr*)hdr, off, (MapPayPage*)pay);
     return hipGetLastError();
 }
 

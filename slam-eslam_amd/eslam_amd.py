@@ -193,7 +193,8 @@ class GpuFilter:
         self._check(self.L.eslam_gpu_map_update(self.h, patches, len(patches)))
 
     def map_match(self, patches):
-        """eslam_gpu_map_match: processMap's visual weighting (match = true) against each own map"""
+        """eslam_gpu_map_match: processMap's visual weighting (match = true) against each
+        particle's map: the shared grid, or its own map (per-particle maps)"""
         self._check(self.L.eslam_gpu_map_match(self.h, patches, len(patches)))
 
     def particle_map(self, i, cap=1024):

@@ -144,3 +144,25 @@ def scan_patches(nx=8, ny=6, x0=0.35, x1=0.95, y0=-0.7, y1=0.2, z=-0.18, stdev=0
             out[k].stdev = stdev
             k += 1
     return out
+
+
+def scan_area(count, nx=25, spacing=0.1, x0=0.35, yc=-0.25, z=-0.18, stdev=0.03):
+    """A laser scan's MLS ahead of the robot at the map's resolution: `count` patches on a grid
+    of nx columns (x0 .. x0 + (nx - 1) spacing ahead) and ceil(count / nx) rows centred on yc,
+    in the yaw-free body frame (600 patches: 2.5 m x 2.4 m at 0.1 m, within maxSensorRange 3 m,
+    src/Configuration.hpp:107)."""
+    import eslam_abi as A
+    ny = -(-count // nx)
+    out = (A.ScanPatch * count)()
+    k = 0
+    for i in range(nx):
+        for j in range(ny):
+            if k == count:
+                break
+            x = x0 + spacing * i
+            y = yc + spacing * (j - (ny - 1) / 2.0)
+            out[k].position[:] = [x, y, z + 0.01 * math.sin(3.0 * x + 2.0 * y)]
+            out[k].stdev = stdev
+            k += 1
+    return out
+

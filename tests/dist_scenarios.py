@@ -33,8 +33,9 @@ def scenario_config(name, n_global):
         if name in ("maps", "config4", "heirloom"):   # useSharedMap = false: per-particle maps
             cfg.flags |= A.FLAG_PARTICLE_MAPS
         if name == "heirloom":
-            # 4 pages per particle: the one map of ~50 pages fits the pool once, not once per copy
-            cfg.local_map_pages = 4
+            # 8 pages per particle: the one map of ~50 pages fits the pool once, not once per copy
+            # (then a map update's copies on write take ~4 per particle)
+            cfg.local_map_pages = 8
         if name == "config4":
             # 8 ranks x 8M and then one 64M context share one GPU's 288 GB: a 5 x 5-tile window
             # (1.5 m; the scan reaches 1.2 m) and 6 pages per particle (3 steps take ~5)
@@ -212,16 +213,28 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         # one particle on the last rank maps a wide scan (~50 pages) and then holds all the weight:
         # the resample copies it to every output, so every other rank receives one record for
         # all its particles (one table and one set of pages for the record, not one per copy),
-        # and a map update then copies on write what each particle changes
+        # and map updates then copy on write what each particle changes.  (A resample that
+        # migrates many records deep-copies each record's pages: pages two records shared on
+        # the sending rank are two copies on the receiving one.)
+        import os
+        import sys
+        dbg = os.environ.get("ESLAM_DEBUG_HEIRLOOM") and hasattr(f, "sync")
+
+        def show(what):
+            if dbg:
+                i = f.sync()
+                sys.stderr.write(f"[{lo}] {what}: taken {i.map_pages_taken} free {i.map_pages_free} "
+                                 f"copied {i.map_stores_copied} changed {i.map_stores_changed}\n")
         f.upload(heirloom_arrays(n_global, lo, hi))
         f.map_update(S.scan_patches(nx=16, ny=12, x0=-2.6, x1=4.6, y0=-2.5, y1=2.4))
+        show("wide")
         f.resample()
         _snap(rec, "res", f, True)
+        show("received")
         _maps(rec, f, hi - lo)
-        for k, st in enumerate(S.step_stream(2)):
-            f.step(st)
-            f.map_update(S.scan_patches())
-            _snap(rec, f"s{k}", f, True)
+        for k in range(2):                       # the copies on write of the shared received table
+            f.map_update(S.scan_patches(x0=0.35 + 0.3 * k))
+            show(f"update {k}")
         rec["maps2/count"] = np.array([len(f.particle_map(g - lo)[0]) for g in range(lo, hi) if g % 97 == 0], np.uint32)
         return rec
     if name == "upload":

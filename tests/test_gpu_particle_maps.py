@@ -22,7 +22,7 @@ def u32(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
 
-MAP_INFO = ("map_patches_dropped", "map_stores_copied", "map_stores_changed", "map_patches_covered")
+MAP_INFO = ("map_patches_dropped", "map_stores_copied", "map_stores_changed", "map_patches_covered", "map_tiles_evicted")
 
 
 def map_info(i):
@@ -347,8 +347,8 @@ def test_particle_maps_match_bit_exact(gpu_mod, oracle, case):
 
 def test_particle_maps_match_edges(gpu_mod, oracle):
     """eslam_gpu_map_match's edges: an empty scan (weight 1: weights unchanged, bit for bit), a
-    scan of fewer than 10 patches (only patch 0 sampled), non-finite patches and a filter with
-    the shared map only (ESLAM_ERR_INVALID_ARG, nothing changed)."""
+    scan of fewer than 10 patches (only patch 0 sampled), non-finite patches (ESLAM_ERR_INVALID_ARG,
+    nothing changed) and a filter with the shared map only (the grid's cells: as the oracle)."""
     n = 700
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS
@@ -379,8 +379,90 @@ def test_particle_maps_match_edges(gpu_mod, oracle):
         gpu.map_match(bad)
     assert np.array_equal(gpu.download().weight, w1)
     shared = gpu_mod.GpuFilter(S.bench_config(A.default_config(), n))
-    shared.set_map(grid)
-    shared.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
-    with pytest.raises(gpu_mod.EslamError):
-        shared.map_match(scan)
+    so = O.OracleFilter(S.bench_config(A.default_config(), n), O.SUM_CONTRACT)
+    for f in (shared, so):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+        f.step(S.step_stream(1)[0])
+        f.map_match(S.scan_patches(x0=-0.3, x1=0.9))      # half on the grid's cells (x < 0.3)
+    assert_bit_identical(shared.download(), so.download(), "shared-map match")
     shared.close()
+
+
+@pytest.mark.parametrize("case", ["flat", "rough", "rough_heights", "rotated_grid"])
+def test_shared_map_match_bit_exact(gpu_mod, oracle, case):
+    """processMap(scanMap, match = true) with the shared map (useSharedMap = true: the laser
+    path's match-only call, src/EmbodiedSlamFilter.cpp:214-221,342-344): every 10th patch
+    scored against the patch getPatch's 3-sigma gate picks in the grid cell it lands on (0 when
+    none passes; the rule is the build's own), weights feeding the resample of the
+    next step.  Multi-patch cells (rough), vertical patches (heights) and a rotated grid; bit for
+    bit against the oracle after every call."""
+    n = 5003
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_RECORD_ANCESTORS
+    grid = S.flat_map(cells=120) if case == "flat" else S.rough_map(cells=120)
+    if case == "rough_heights":
+        rng = np.random.default_rng(3)
+        grid.patch_height = np.where(rng.random(grid.mean.shape[0]) < 0.3, rng.uniform(0.05, 0.5, grid.mean.shape[0]),
+                                     0.0).astype(np.float32)
+    if case == "rotated_grid":
+        grid = rotated(grid)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.05], 0.18, 0.05)
+    scans = [S.scan_patches(nx=12, ny=9, x0=-1.0, x1=2.5, y0=-1.5, y1=1.2, z=z) for z in (-0.18, -0.1, 0.4)]
+    changed = 0
+    for k, st in enumerate(S.step_stream(8, tilt=case != "flat")):
+        assert gpu.step(st) == orc.step(st)
+        w0 = gpu.download().weight.copy()
+        gpu.map_match(scans[k % 3])
+        orc.map_match(scans[k % 3])
+        assert_bit_identical(gpu.download(), orc.download(), f"{case} shared match step {k}")
+        changed += int(np.sum(gpu.download().weight != w0))
+    assert np.array_equal(gpu.ancestors(), orc.ancestors())
+    assert changed > n
+
+
+@pytest.mark.parametrize("trail,n", [(16, 4096), (3, 1024)])
+def test_particle_maps_loop_trail(gpu_mod, oracle, trail, n):
+    """A loop: 6 m out and (nearly) back on the empty prior, a map update after every step.  The
+    tiles each window leaves go to its trail and come back when the window returns (the
+    reference's MLSMap keeps every grid, src/EmbodiedSlamFilter.cpp:195-207): on the way back the
+    feet stand on the cells mapped on the way out (the scan looks ahead in +x, so it never maps
+    them itself).  Bit-exact against the oracle (every particle, the counters of every update,
+    the maps of sampled particles, trails included); a 3-entry trail overflows and forgets the
+    farthest tiles, counted alike."""
+    cfg = S.bench_config(A.default_config(), n)
+    cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
+    cfg.local_map_trail = trail
+    cfg.local_map_pages = 32
+    grid = S.unmapped_beyond(S.flat_map(cells=200), -1e9)
+    gpu = gpu_mod.GpuFilter(cfg)
+    orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
+    orc.set_threads(16)
+    for f in (gpu, orc):
+        f.set_map(grid)
+        f.init_gaussian(n, [0.0, 0.0, 0.0], [0.05, 0.05, 0.02], 0.18, 0.05)
+    scan = S.scan_patches()
+    stream = S.step_stream(300, dx=0.02, dyaw=0.0) + S.step_stream(260, dx=-0.02, dyaw=0.0)
+    evicted, found = 0, []
+    for k, st in enumerate(stream):
+        assert gpu.step(st) == orc.step(st)
+        gpu.map_update(scan)
+        orc.map_update(scan)
+        gi = gpu.sync()
+        assert map_info(gi) == map_info(orc.info()), (k, map_info(gi), map_info(orc.info()))
+        evicted += gi.map_tiles_evicted
+        if k >= 300:
+            found.append(gi.data_particles / n)
+        if k % 80 == 79 or k == len(stream) - 1:
+            assert_bit_identical(gpu.download(), orc.download(), f"loop trail={trail} step {k}")
+            assert_maps_equal(gpu, orc, [0, 1, n // 2, n - 1], f"loop step {k}")
+    assert np.array_equal(gpu.ancestors(), orc.ancestors())
+    if trail == 16:
+        assert evicted == 0
+        assert np.mean(found[-80:]) > 0.9, found[-80:]       # on the cells of the way out
+    else:
+        assert evicted > 0
