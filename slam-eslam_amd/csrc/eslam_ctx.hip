@@ -1887,7 +1887,8 @@ extern "C" int eslam_gpu_get_particle_map(eslam_ctx* ctx, uint64_t index, uint32
     uint32_t k = 0;
     float2 cell[DM_LM_PAGE_CELLS];
     const uint32_t W = lm.wx * lm.wy, toff = lm.S - 4u * lm.V;
-    for (uint32_t s = 0; s < W + lm.V; ++s) {
+    const uint32_t hw = sl[toff - 1u] == DM_LM_NONE ? 0u : sl[toff - 1u];   // the trail's used entries
+    for (uint32_t s = 0; s < W + hw; ++s) {
             const bool tr = s >= W;
             const uint32_t pg = tr ? sl[toff + 4u * (s - W) + 2u] : sl[s];
             if (pg == DM_LM_NONE) continue;

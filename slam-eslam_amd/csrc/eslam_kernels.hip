@@ -345,7 +345,8 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t m, uint32_t n
         pg = DM_LM_NONE;
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         const gmem<const u4>* t = reinterpret_cast<const gmem<const u4>*>(row + (S - 4u * V));
-        for (uint32_t e = 0; e < V; ++e) {
+        const uint32_t hwv = row[S - 4u * V - 1u], hw = hwv == DM_LM_NONE ? 0u : hwv;
+        for (uint32_t e = 0; e < hw; ++e) {
             const u4 v = t[e];
             if (v.z != DM_LM_NONE && v.x == a && v.y == b) pg = v.z;
         }
@@ -1658,8 +1659,12 @@ __device__ __forceinline__ bool lm_in(int32_t a, int32_t c, uint32_t h)
 }
 
 // ---- the trail (eslam_internal.h LocalMaps; the oracle's lm_trail_* and lm_recentre): a
-// table's tiles outside its window, V entries {a, b, page, -} closing its row
+// table's tiles outside its window, V entries {a, b, page, -} closing its row.  The last word
+// before them (window padding: (2h + 1)^2 is odd, so there always is one) holds the trail's
+// high-water mark hw (DM_LM_NONE: 0): entries from hw on are empty and are neither read nor
+// copied (their words may be stale)
 __device__ __forceinline__ uint32_t lm_trail_off(const LocalMaps& lm) { return lm.S - 4u * lm.V; }
+__device__ __forceinline__ uint32_t lm_hw_word(uint32_t w) { return w == DM_LM_NONE ? 0u : w; }
 __device__ __forceinline__ int32_t lm_cheb(int32_t a, int32_t b, int32_t na, int32_t nb)
 {
     const int32_t da = a > na ? a - na : na - a, db = b > nb ? b - nb : nb - b;
@@ -1671,9 +1676,10 @@ __device__ __forceinline__ uint32_t lm_trail_push(const LocalMaps& lm, uint32_t*
                                                   uint32_t pg)
 {
     uint4* t = reinterpret_cast<uint4*>(row + lm_trail_off(lm));
+    const uint32_t hw = lm_hw_word(row[lm_trail_off(lm) - 1u]);
     int32_t far = -1;
     uint32_t fe = 0;
-    for (uint32_t e = 0; e < lm.V; ++e) {
+    for (uint32_t e = 0; e < hw; ++e) {
         const uint4 v = t[e];
         if (v.z == DM_LM_NONE) {
             t[e] = make_uint4((uint32_t)a, (uint32_t)b, pg, DM_LM_NONE);
@@ -1681,6 +1687,11 @@ __device__ __forceinline__ uint32_t lm_trail_push(const LocalMaps& lm, uint32_t*
         }
         const int32_t d = lm_cheb((int32_t)v.x, (int32_t)v.y, na, nb);
         if (d > far) { far = d; fe = e; }
+    }
+    if (hw < lm.V) {                                     // the first entry never used
+        t[hw] = make_uint4((uint32_t)a, (uint32_t)b, pg, DM_LM_NONE);
+        row[lm_trail_off(lm) - 1u] = hw + 1u;
+        return 0u;
     }
     if (lm.V && far > lm_cheb(a, b, na, nb)) t[fe] = make_uint4((uint32_t)a, (uint32_t)b, pg, DM_LM_NONE);
     return 1u;
@@ -1794,27 +1805,36 @@ __device__ __forceinline__ uint32_t lm_find(const uint32_t (&L)[kLmList], uint32
 __device__ uint32_t lm_rewrite(const LocalMaps& lm, uint32_t X, uint32_t T, int2 oc, int32_t na, int32_t nb)
 {
     uint32_t* row = lm.slot + (uint64_t)T * lm.S;
-    if (X != T) {
+    const uint32_t toff = lm_trail_off(lm);
+    if (X != T) {                                        // the window's words and the trail's used entries
         const uint4* src = reinterpret_cast<const uint4*>(lm.slot + (uint64_t)X * lm.S);
         uint4* dst = reinterpret_cast<uint4*>(row);
-        for (uint32_t q = 0; q < lm.S / 4; ++q) dst[q] = src[q];
+        const uint32_t nq = toff / 4u + lm_hw_word(lm.slot[(uint64_t)X * lm.S + toff - 1u]);
+        for (uint32_t q = 0; q < nq; ++q) dst[q] = src[q];
     }
     uint32_t forgot = 0;
     if (oc.x != DM_LM_UNSET && (oc.x != na || oc.y != nb)) {
+        // the window's columns and rows whose tiles leave it (bit sa / sb), then their slots in
+        // slot order
+        uint32_t colx = 0, rowx = 0;
+        for (uint32_t sa = 0; sa < lm.wx; ++sa)
+            colx |= lm_in(lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx), na, lm.hx) ? 0u : 1u << sa;
+        for (uint32_t sb = 0; sb < lm.wy; ++sb)
+            rowx |= lm_in(lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by), nb, lm.hy) ? 0u : 1u << sb;
+        const uint32_t all = lm.wx >= 32u ? ~0u : (1u << lm.wx) - 1u;
         for (uint32_t sb = 0; sb < lm.wy; ++sb) {
             const int32_t b = lm_tile(sb, oc.y, lm.hy, lm.wy, lm.my, lm.by);
-            const bool row_leaves = !lm_in(b, nb, lm.hy);
-            for (uint32_t sa = 0; sa < lm.wx; ++sa) {
-                const int32_t a = lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx);
-                if (!row_leaves && lm_in(a, na, lm.hx)) continue;
+            for (uint32_t cols = ((rowx >> sb) & 1u) ? all : colx; cols; cols &= cols - 1u) {
+                const uint32_t sa = (uint32_t)__builtin_ctz(cols);
                 const uint32_t s = sa + lm.wx * sb, p = row[s];
                 if (p == DM_LM_NONE) continue;
-                forgot += lm_trail_push(lm, row, na, nb, a, b, p);
+                forgot += lm_trail_push(lm, row, na, nb, lm_tile(sa, oc.x, lm.hx, lm.wx, lm.mx, lm.bx), b, p);
                 row[s] = DM_LM_NONE;
             }
         }
-        uint4* t = reinterpret_cast<uint4*>(row + lm_trail_off(lm));
-        for (uint32_t e = 0; e < lm.V; ++e) {
+        uint4* t = reinterpret_cast<uint4*>(row + toff);
+        const uint32_t hw = lm_hw_word(row[toff - 1u]);
+        for (uint32_t e = 0; e < hw; ++e) {
             const uint4 v = t[e];
             if (v.z == DM_LM_NONE || !lm_in((int32_t)v.x, na, lm.hx) || !lm_in((int32_t)v.y, nb, lm.hy)) continue;
             row[lm_mod(v.x, lm.wx, lm.mx) + lm.wx * lm_mod(v.y, lm.wy, lm.my)] = v.z;
@@ -1905,7 +1925,8 @@ __global__ void __launch_bounds__(kBlock) k_pg_mark(LocalMaps lm, const uint32_t
             const uint32_t p = sl[s];
             if (p != DM_LM_NONE) lm.mark[p] = 1u;
         }
-        for (uint32_t e = lane; e < lm.V; e += 64u) {
+        const uint32_t hw = lm_hw_word(sl[toff - 1u]);
+        for (uint32_t e = lane; e < hw; e += 64u) {
             const uint32_t p = sl[toff + 4u * e + 2u];
             if (p != DM_LM_NONE) lm.mark[p] = 1u;
         }
@@ -2313,8 +2334,9 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     s_np[pl][2 * l + 1] = NP;
                 }
                 const uint32_t lmin = cnt ? grp_get(Lr, 0) : 1u, lmax = cnt ? grp_get(Lr, cnt - 1) : 0u;
+                const uint32_t toff = lm_trail_off(lm), nq = toff / 4u + lm_hw_word(xsl[toff - 1u]);
                 wave_sync();
-                for (uint32_t q = l; q < lm.S / 4; q += kLmLanes) {
+                for (uint32_t q = l; q < nq; q += kLmLanes) {
                     uint4 w4 = reinterpret_cast<const uint4*>(xsl)[q];
                     if (4 * q + 3 >= lmin && 4 * q <= lmax) {
                         uint32_t v[4] = {w4.x, w4.y, w4.z, w4.w};
@@ -2538,7 +2560,8 @@ __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, 
                     sl[q] = inw ? row[lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my)] : DM_LM_NONE;
                     if (!inw) {                  // a tile the window has left: the trail (rare)
                         const uint4* t = reinterpret_cast<const uint4*>(row + lm_trail_off(lm));
-                        for (uint32_t e = 0; e < lm.V; ++e) {
+                        const uint32_t hw = lm_hw_word(row[lm_trail_off(lm) - 1u]);
+                        for (uint32_t e = 0; e < hw; ++e) {
                             const uint4 v = t[e];
                             if (v.z != DM_LM_NONE && v.x == a && v.y == b) sl[q] = v.z;
                         }
@@ -4198,7 +4221,8 @@ __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const Dev
         uint32_t c = 0;
         if (!share) {
             for (uint32_t s = lane; s < toff; s += 64u) c += row[s] != DM_LM_NONE ? 1u : 0u;
-            for (uint32_t e = lane; e < lm.V; e += 64u) c += row[toff + 4u * e + 2u] != DM_LM_NONE ? 1u : 0u;
+            const uint32_t hw = lm_hw_word(row[toff - 1u]);
+            for (uint32_t e = lane; e < hw; e += 64u) c += row[toff + 4u * e + 2u] != DM_LM_NONE ? 1u : 0u;
             c = wave_sum_u32(c);
         }
         if (lane == 0) {
@@ -4229,7 +4253,8 @@ __global__ void __launch_bounds__(kBlock) k_pay_pack(const DevState s0, const De
         const uint32_t* row = lm.slot + (uint64_t)X * lm.S;
         const uint32_t toff = lm.S - 4u * lm.V;
         uint64_t q = off[j];
-        for (uint32_t s = 0; s < toff + lm.V; ++s) {
+        const uint32_t hw = lm_hw_word(row[toff - 1u]);
+        for (uint32_t s = 0; s < toff + hw; ++s) {
             const bool tr = s >= toff;
             const uint32_t p = tr ? row[toff + 4u * (s - toff) + 2u] : row[s];
             if (p == DM_LM_NONE) continue;
@@ -4323,7 +4348,12 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uin
         uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
         for (uint32_t s = lane; s < lm.S; s += 64u) {
             uint32_t v = DM_LM_NONE;
-            if (s < toff) {
+            if (s == toff - 1u) {                        // the trail's high-water mark
+                for (uint32_t q = 0; q < npg; ++q) {
+                    const uint32_t sl = pay[q0 + q].slot;
+                    if (sl & kPayTrail) v = (v == DM_LM_NONE || (sl & ~kPayTrail) + 1u > v) ? (sl & ~kPayTrail) + 1u : v;
+                }
+            } else if (s < toff) {
                 for (uint32_t q = 0; q < npg; ++q) v = pay[q0 + q].slot == s ? lm.frees[alloc + q] : v;
             } else {
                 const uint32_t e = (s - toff) >> 2, k = (s - toff) & 3u;
