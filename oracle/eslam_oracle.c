@@ -2308,9 +2308,11 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
     return 0;
 }
 
-/* processMap's merge of a whole scan: 64 patches at a time, in order (the GPU's parts,
- * eslam_gpu_map_update); every cell sees its patches in the scan's order, the counters add up */
-#define OR_SCAN_PART 64u
+/* processMap's merge of a whole scan in parts, in order (the GPU's parts, eslam_gpu_map_update:
+ * a scan of at most 64 patches in one part, a larger one 256 at a time); every cell sees its
+ * patches in the scan's order, the counters add up */
+#define OR_SCAN_PART_SMALL 64u
+#define OR_SCAN_PART_LARGE 256u
 #define OR_MATCH_SAMPLING 10u       /* src/EmbodiedSlamFilter.cpp:216 */
 #define OR_MATCH_SIGMA ((double)0.2f) /* :217, a float there */
 int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
@@ -2318,8 +2320,9 @@ int or_map_update(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
     f->info.map_patches_dropped = f->info.map_stores_changed = 0;
     f->info.map_stores_copied = f->info.map_patches_covered = 0;
     f->info.map_tiles_evicted = 0;
-    for (uint32_t c0 = 0; c0 == 0 || c0 < m; c0 += OR_SCAN_PART) {
-        const int rc = or_map_update_part(f, sp + c0, m - c0 < OR_SCAN_PART ? m - c0 : OR_SCAN_PART);
+    const uint32_t part = m <= OR_SCAN_PART_SMALL ? OR_SCAN_PART_SMALL : OR_SCAN_PART_LARGE;
+    for (uint32_t c0 = 0; c0 == 0 || c0 < m; c0 += part) {
+        const int rc = or_map_update_part(f, sp + c0, m - c0 < part ? m - c0 : part);
         if (rc) return rc;
     }
     return 0;

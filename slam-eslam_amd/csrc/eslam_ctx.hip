@@ -288,6 +288,14 @@ struct eslam_ctx {
     uint32_t* lm_off = nullptr;              // per particle: its first page in its plan block (MergeParams::off)
     void* lm_job = nullptr;                  // per particle: the plan's record (MergeParams::job)
     uint16_t* lm_codes = nullptr;            // per particle: the plan's cell codes (MergeParams::codes)
+    uint64_t lm_codes_cap = 0;               //   bytes (a small part's stride; grown for a large part's)
+    // the scan of a map update on the device (MergeParams::sp): two slots, each staged through
+    // pinned host memory; an update waits for the update before last to have read its slot
+    void* scan_host[2] = {nullptr, nullptr};
+    void* scan_dev[2] = {nullptr, nullptr};
+    uint64_t scan_host_cap[2] = {0, 0}, scan_dev_cap[2] = {0, 0};
+    hipEvent_t scan_ev[2] = {nullptr, nullptr};
+    uint32_t scan_slot = 0;
     uint32_t* lm_poff = nullptr;             // per merge block: page offsets (+ total)
     uint32_t* lm_pgc = nullptr;              // the page collection's compaction counts
     void* match_sp = nullptr;                // processMap match: the sampled scan patches (device)
@@ -664,7 +672,7 @@ static void free_local_maps(eslam_ctx* ctx)
 {
     (void)hipFree(ctx->lm.ctr); (void)hipFree(ctx->lm.slot); (void)hipFree(ctx->lm.page); (void)hipFree(ctx->lm.tgen);
     (void)hipFree(ctx->lm.owner); (void)hipFree(ctx->lm.frees); (void)hipFree(ctx->lm.mark);
-    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_job); (void)hipFree(ctx->lm_codes); (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc); (void)hipFree(ctx->match_sp);
+    (void)hipFree(ctx->lm_off); (void)hipFree(ctx->lm_job); (void)hipFree(ctx->lm_codes); ctx->lm_codes_cap = 0; (void)hipFree(ctx->lm_poff); (void)hipFree(ctx->lm_pgc); (void)hipFree(ctx->match_sp);
     ctx->lm = LocalMaps{};
     ctx->lm_off = nullptr; ctx->lm_job = nullptr; ctx->lm_codes = nullptr; ctx->lm_poff = nullptr; ctx->lm_pgc = nullptr; ctx->match_sp = nullptr; ctx->match_cap = 0;
     ctx->lm_ready = false;
@@ -726,6 +734,11 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->mring) if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->xring) if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < 2; ++k) {
+        if (ctx->scan_ev[k]) (void)hipEventDestroy(ctx->scan_ev[k]);
+        (void)hipHostFree(ctx->scan_host[k]);
+        (void)hipFree(ctx->scan_dev[k]);
+    }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -847,7 +860,8 @@ static int local_maps_reset(eslam_ctx* ctx)
     HIPCHK(ctx, hipMalloc(&lm.mark, ((lm.npages + 15) / 16) * 16));
     HIPCHK(ctx, hipMalloc(&ctx->lm_off, cap * 4));
     HIPCHK(ctx, hipMalloc(&ctx->lm_job, cap * sizeof(MergeJob)));
-    HIPCHK(ctx, hipMalloc(&ctx->lm_codes, cap * 2 * kMaxScanPatches));
+    ctx->lm_codes_cap = cap * 2 * kScanPartSmall;
+    HIPCHK(ctx, hipMalloc(&ctx->lm_codes, ctx->lm_codes_cap));
     HIPCHK(ctx, hipMalloc(&ctx->lm_poff, ((cap + kLmBlock - 1) / kLmBlock + 1) * 4));
     HIPCHK(ctx, hipMalloc(&ctx->lm_pgc, (ptiles + 1) * 4));
     HIPCHK(ctx, eslam_launch_store_init(ctx->sid_mem, &lm, cap, pool, ctx->stream));
@@ -1777,11 +1791,25 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
         if (rc) return rc;
     }
     mrec(ctx, 1);
-    // a scan of more than kMaxScanPatches patches merges kMaxScanPatches at a time, in order:
-    // every cell sees its patches in the scan's order; the parts' counters add up
-    // (map_stores_changed counts a map once per part that changed it)
-    for (uint32_t c0 = 0; c0 == 0 || c0 < count; c0 += (uint32_t)kMaxScanPatches) {
-        const uint32_t cm = count - c0 < (uint32_t)kMaxScanPatches ? count - c0 : (uint32_t)kMaxScanPatches;
+    // the scan on the device: this update's slot is free once the update before last is done
+    const uint32_t slot = ctx->scan_slot ^= 1u;
+    if (!ctx->scan_ev[slot]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->scan_ev[slot], hipEventDisableTiming));
+    else HIPCHK(ctx, hipEventSynchronize(ctx->scan_ev[slot]));
+    const uint64_t sbytes = (uint64_t)(count ? count : 1) * sizeof(ScanPatch);
+    int rc = grow(ctx, &ctx->scan_host[slot], &ctx->scan_host_cap[slot], sbytes, true);
+    if (!rc) rc = grow(ctx, &ctx->scan_dev[slot], &ctx->scan_dev_cap[slot], sbytes, false);
+    // a scan of more than kScanPartSmall patches merges in parts of kScanPartLarge
+    const uint32_t part = count <= kScanPartSmall ? kScanPartSmall : kScanPartLarge;
+    if (!rc && part == kScanPartLarge) rc = grow(ctx, (void**)&ctx->lm_codes, &ctx->lm_codes_cap, ctx->cap * 2 * kScanPartLarge, false);
+    if (rc) return rc;
+    ScanPatch* sh = (ScanPatch*)ctx->scan_host[slot];
+    for (uint32_t k = 0; k < count; ++k)
+        sh[k] = ScanPatch{patches[k].position[0], patches[k].position[1], patches[k].position[2], patches[k].stdev};
+    if (count) HIPCHK(ctx, hipMemcpyAsync(ctx->scan_dev[slot], sh, sbytes, hipMemcpyHostToDevice, ctx->stream));
+    // the parts in order: every cell sees its patches in the scan's order; the parts' counters
+    // add up (map_stores_changed counts a map once per part that changed it)
+    for (uint32_t c0 = 0; c0 == 0 || c0 < count; c0 += part) {
+        const uint32_t cm = count - c0 < part ? count - c0 : part;
         const SidRef sr{ctx->st[0].sid, ctx->st[1].sid, ctx->ctl};
         const CowScratch cs = cow_layout(ctx->cow, ctx->cap);
         HIPCHK(ctx, eslam_launch_store_refs(sr, ctx->n, store_pool(ctx->cap), &cs, fuse ? &gv : nullptr, ctx->lm.tgen,
@@ -1795,10 +1823,8 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
         mp.aux = (ctx->cfg.flags & ESLAM_FLAG_NO_AUX_GATHER) ? 0u : 1u;
         mp.acc = c0 ? 1u : 0u;
         mp.m = cm;
-        for (uint32_t k = 0; k < cm; ++k) {
-            const eslam_scan_patch& s = patches[c0 + k];
-            mp.sp[k] = ScanPatch{s.position[0], s.position[1], s.position[2], s.stdev};
-        }
+        mp.sp = (const ScanPatch*)ctx->scan_dev[slot] + c0;
+        mp.codes = ctx->lm_codes;
         HIPCHK(ctx, eslam_launch_map_plan(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->lm_pgc, ctx->stream));
         if (!c0) mrec(ctx, 3);
         HIPCHK(ctx, eslam_launch_map_merge(ctx->st[0], ctx->st[1], ctx->ctl, &ctx->map, &ctx->lm, &mp, ctx->stream));
@@ -1806,6 +1832,7 @@ extern "C" int eslam_gpu_map_update(eslam_ctx* ctx, const eslam_scan_patch* patc
             HIPCHK(ctx, eslam_launch_commit(ctx->ctl, ctx->stream));     // the gather's buffer flip, if one ran
         }
     }
+    HIPCHK(ctx, hipEventRecord(ctx->scan_ev[slot], ctx->stream));
     mrec(ctx, 4);
     return ESLAM_OK;
 }

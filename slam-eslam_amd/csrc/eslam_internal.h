@@ -284,6 +284,9 @@ struct ScanPatch {
     double x, y, z, stdev;
 };
 constexpr int kMaxScanPatches = 64;
+// a map update merges a scan in parts of kScanPartSmall patches (a scan of at most that many:
+// one part) or of kScanPartLarge (larger scans: fewer parts, so each tile is staged about once)
+constexpr uint32_t kScanPartSmall = 64, kScanPartLarge = 256;
 // processMap(scanMap, match = true) (k_map_match): every kMatchSampling-th scan patch
 constexpr uint32_t kMatchSampling = 10;          // src/EmbodiedSlamFilter.cpp:216
 constexpr double kMatchSigma = (double)0.2f;     // :217 (a float there)
@@ -366,13 +369,13 @@ struct MergeParams {
                                          // (k_map_plan / k_recv_plan: the exclusive prefix of the needs)
     uint32_t* poff;                      // per block of kLmBlock particles: first page offset (+ total)
     MergeJob* job;                       // per particle: k_map_plan's record for the merge
-    uint16_t* codes;                     // per particle: kMaxScanPatches scan-patch cell codes (plan)
+    uint16_t* codes;                     // per particle: a part's scan-patch cell codes (plan; the part's stride)
     uint32_t* fault;                     // host-mapped fault word (kFaultPages)
     GatherView gv;                       // fuse: a pending resample gather runs in the merge (one GPU)
     uint64_t gbase;
     uint32_t fuse, aux;                  // aux: carry mprob / flags (ESLAM_FLAG_NO_AUX_GATHER unset)
     uint32_t acc, pad2;                  // acc: add this merge's counters to the update's (a later 64-patch part)
-    ScanPatch sp[kMaxScanPatches];
+    const ScanPatch* sp;                 // the part's patches (device copy of the scan)
 };
 
 // logDebug records of the last update (k_contact_records), indexed by the particle's

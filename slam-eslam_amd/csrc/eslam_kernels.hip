@@ -1725,14 +1725,14 @@ __device__ __forceinline__ void lm_centre(const MapView& map, const MergeParams&
     }
 }
 
-// every scan patch's code for this particle: (slot << 6) | cell in the tile, or kCodeSkip
-// (off the grid, on a cell the shared grid covers, or outside the window); codes go to LDS
-// (patch-major, thread-minor).  Counts the covered and dropped patches.
-__device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
-                                         uint16_t* codes, uint32_t& covered, uint32_t& dropped)
+// scan patch k's code for this particle: (slot << 6) | cell in the tile, or kCodeSkip (off
+// the grid, on a cell the shared grid covers, or outside the window).  Counts the covered and
+// dropped patches.
+__device__ __forceinline__ uint16_t lm_code(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
+                                            uint32_t k, uint32_t& covered, uint32_t& dropped)
 {
     const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
-    for (uint32_t k = 0; k < mp.m; ++k) {
+    {
         const ScanPatch sp = mp.sp[k];
         uint32_t cell, cm, cn;
         if (mp.is_id) {
@@ -1766,7 +1766,67 @@ __device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm
                 }
             }
         }
-        codes[k * kLmBlock] = code;
+        return code;
+    }
+}
+
+// every scan patch's code into LDS (patch-major, thread-minor: a part of kScanPartSmall)
+__device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
+                                         uint16_t* codes, uint32_t& covered, uint32_t& dropped)
+{
+    for (uint32_t k = 0; k < mp.m; ++k) codes[k * kLmBlock] = lm_code(map, lm, mp, q, k, covered, dropped);
+}
+
+// slot s into the sorted list of the kLmList smallest distinct slots; more: a slot fell off
+__device__ __forceinline__ void lm_insert(uint32_t (&L)[kLmList], uint32_t s, bool& more)
+{
+    bool dup = false;
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) dup |= L[r] == s;
+    if (dup) return;
+    more |= L[kLmList - 1] != kLmNoList;
+#pragma unroll
+    for (uint32_t r = kLmList - 1; r >= 1; --r) L[r] = L[r - 1] > s ? L[r - 1] : (L[r] > s ? s : L[r]);
+    L[0] = L[0] > s ? s : L[0];
+}
+
+// a large part: every code straight to the particle's row of the codes buffer (eight per
+// 16-byte store), and the first pass's tiles collected on the way (L; more: further tiles)
+__device__ __forceinline__ void lm_codes_row(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
+                                             uint4* row, uint32_t (&L)[kLmList], bool& more, uint32_t& covered, uint32_t& dropped)
+{
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) L[r] = kLmNoList;
+    more = false;
+    for (uint32_t k0 = 0; k0 < mp.m; k0 += 8) {
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t k = k0 + j;
+            const uint32_t c = k < mp.m ? (uint32_t)lm_code(map, lm, mp, q, k, covered, dropped) : (uint32_t)kCodeSkip;
+            if (c != kCodeSkip) lm_insert(L, c >> 6, more);
+            w[j >> 1] = (j & 1) ? (w[j >> 1] | (c << 16)) : c;
+        }
+        row[k0 >> 3] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// the up to kLmList smallest distinct slots above t of a particle's codes row
+__device__ __forceinline__ void lm_collect_row(const uint4* row, uint32_t m, uint32_t t, uint32_t (&L)[kLmList])
+{
+#pragma unroll
+    for (uint32_t r = 0; r < kLmList; ++r) L[r] = kLmNoList;
+    bool more = false;
+    for (uint32_t k0 = 0; k0 < m; k0 += 8) {
+        const uint4 v = row[k0 >> 3];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t c = (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+            if (k0 + j >= m || c == kCodeSkip) continue;
+            const uint32_t s = c >> 6;
+            if (s > t) lm_insert(L, s, more);
+        }
     }
 }
 
@@ -1982,7 +2042,7 @@ constexpr uint32_t kLmLanes = ESLAM_LM_LANES;                       // lanes per
 constexpr uint32_t kLmMergeBlock = 128;
 constexpr uint32_t kLmPpb = kLmMergeBlock / kLmLanes;               // particles per block
 constexpr uint32_t kLmStage = ESLAM_LM_STAGE;                        // pages in LDS per particle
-constexpr uint32_t kLmPerLane = (uint32_t)kMaxScanPatches / kLmLanes;
+constexpr uint32_t kLmPerLane = kScanPartSmall / kLmLanes;              // codes a lane holds (small part)
 static_assert(kLmList <= kLmLanes && (kLmLanes == 8 || kLmLanes == 16) && kLmStage <= 4,
               "a lane per tile of a pass; 8 or 16 lanes; row masks of 8 bits per staged page in a word");
 constexpr uint32_t kLmChunk = kLmLanes * 16;                         // bytes of a page a group moves per instruction
@@ -2015,18 +2075,6 @@ __device__ __forceinline__ uint32_t grp_or(uint32_t v)
 }
 __device__ __forceinline__ uint32_t grp_get(uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)l, kLmLanes); }
 
-// the smallest slot of the lane's codes above lo (-1: any), over the group
-__device__ __forceinline__ uint32_t lm_next_slot(const uint16_t (&code)[kLmPerLane], int32_t lo)
-{
-    uint32_t mn = kLmNoList;
-#pragma unroll
-    for (uint32_t u = 0; u < kLmPerLane; ++u) {
-        const uint32_t s = (uint32_t)code[u] >> 6;
-        if (code[u] != kCodeSkip && (int32_t)s > lo) mn = min(mn, s);
-    }
-    return grp_min(mn);
-}
-
 // k_map_plan: per particle (a lane each: kLmBlock particles a block, so the latency of its
 // chain of lookups -- state, table, page, owner -- overlaps across many particles) the cell
 // codes of its scan (MergeParams::codes), the first pass's tiles with their pages and whether
@@ -2034,12 +2082,16 @@ __device__ __forceinline__ uint32_t lm_next_slot(const uint16_t (&code)[kLmPerLa
 // scan reaches that its table cannot write in place (a new tile, or a page it does not own).
 // The block sums give the allocation offsets (k_scan_excl).  A tile whose writes all turn out
 // no-ops leaves its page unused (free again at the next collection).
+template <uint32_t PART>
 __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1, const Ctl* __restrict__ ctl, MapView map,
                                                        LocalMaps lm, MergeParams mp)
 {
-    __shared__ __attribute__((aligned(16))) uint16_t s_code[kMaxScanPatches * kLmBlock];   // then the records
+    // a small part's codes leave through LDS (then the records); a large part's go straight to
+    // the rows (their LDS would cost the kernel its occupancy)
+    __shared__ __attribute__((aligned(16))) uint16_t s_code[kScanPartSmall * kLmBlock];
     __shared__ uint32_t s_w[kLmBlock / 64];
-    static_assert(sizeof(MergeJob) * kLmBlock <= sizeof(uint16_t) * kMaxScanPatches * kLmBlock, "records in s_code");
+    static_assert(sizeof(MergeJob) * kLmBlock <= sizeof(uint16_t) * kScanPartSmall * kLmBlock, "records in s_code");
+    constexpr bool kSmall = PART == kScanPartSmall;
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kLmBlock, i = base + tid;
     const uint32_t nb = (uint32_t)(mp.n - base < kLmBlock ? mp.n - base : kLmBlock);     // particles of the block
@@ -2067,7 +2119,15 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
         for (uint32_t r = 0; r < kLmList; ++r) { jb.L[r] = 0; jb.P[r] = DM_LM_NONE; }
         if (q.placed) {
             uint16_t* codes = s_code + tid;
-            lm_codes(map, lm, mp, q, codes, covered, dropped);
+            uint4* crow = reinterpret_cast<uint4*>(mp.codes + i * PART);
+            uint32_t L[kLmList];
+            bool more1 = false;
+            if constexpr (kSmall) {
+                lm_codes(map, lm, mp, q, codes, covered, dropped);
+                lm_collect(codes, mp.m, kLmNoList, L);
+            } else {
+                lm_codes_row(map, lm, mp, q, crow, L, more1, covered, dropped);
+            }
             const int2 oc = lm.ctr[q.X];
             const uint32_t T = q.shared ? mp.frees[i] : q.X;
             // the window moves to the particle (into T: a shared table is copied): from here on
@@ -2078,8 +2138,6 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             if (moved) forgot = lm_rewrite(lm, q.X, T, oc, q.na, q.nb);
             const uint32_t* trow = lm.slot + (uint64_t)(moved ? T : q.X) * lm.S;
             const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
-            uint32_t L[kLmList];
-            lm_collect(codes, mp.m, kLmNoList, L);
             uint32_t nt = 0, bits = 0;
 #pragma unroll
             for (uint32_t r = 0; r < kLmList; ++r) {
@@ -2094,8 +2152,9 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             need = __builtin_popcount(bits);
             // later passes (a scan reaching more than kLmList tiles): counted here, resolved by the merge
             bool more = false;
-            for (uint32_t t = L[kLmList - 1]; t != kLmNoList; t = L[kLmList - 1]) {
-                lm_collect(codes, mp.m, t, L);
+            for (uint32_t t = L[kLmList - 1]; t != kLmNoList && (kSmall || more1); t = L[kLmList - 1]) {
+                if constexpr (kSmall) lm_collect(codes, mp.m, t, L);
+                else lm_collect_row(crow, mp.m, t, L);
                 if (L[0] == kLmNoList) break;
                 more = true;
 #pragma unroll
@@ -2117,9 +2176,9 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
     // the codes rows and the records leave through LDS, so every store is a whole 1-KiB line of
     // the wave (a lane per particle storing its own 128-byte record wrote 64 lines partially)
     __syncthreads();
-    uint4* rows = reinterpret_cast<uint4*>(mp.codes + base * kMaxScanPatches);
-    for (uint32_t c = tid; c < nb * (kMaxScanPatches / 8); c += kLmBlock) {
-        const uint32_t p = c / (kMaxScanPatches / 8), k0 = (c % (kMaxScanPatches / 8)) * 8;
+    uint4* rows = reinterpret_cast<uint4*>(mp.codes + base * kScanPartSmall);
+    for (uint32_t c = tid; kSmall && c < nb * (kScanPartSmall / 8); c += kLmBlock) {
+        const uint32_t p = c / (kScanPartSmall / 8), k0 = (c % (kScanPartSmall / 8)) * 8;
         if (k0 >= mp.m) continue;
         uint32_t w[4];
 #pragma unroll
@@ -2179,15 +2238,17 @@ __device__ __forceinline__ uint32_t lm_stage_off(uint32_t rr, uint32_t ci, uint3
     constexpr uint32_t cpc = kLmChunk / 8;                           // cells per chunk
     return (rr * kLmNq + ci / cpc) * 1024 + g * kLmChunk + (ci % cpc) * 8;
 }
-using lm_codes_t = typename std::conditional<kLmLanes == 16, uint2, uint4>::type;   // a lane's codes
-
 #define LM_MERGE_ATTR __attribute__((amdgpu_waves_per_eu(ESLAM_LM_WPE)))
+template <uint32_t PART>
 __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
                                                              LocalMaps lm, MergeParams mp)
 {
-    __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][kMaxScanPatches];
+    constexpr uint32_t PER = PART / kLmLanes;                       // codes a lane holds
+    constexpr uint32_t NCH = PART / 8 / kLmLanes;                   // 16-byte chunks of codes a lane loads
+    static_assert(PART <= 256 && NCH >= 1, "patch indices fit s_list's bytes");
+    __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][PART];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
-    __shared__ uint8_t s_list[kLmPpb][kMaxScanPatches];                                // a stage's patches, in scan order
+    __shared__ uint8_t s_list[kLmPpb][PART];                                           // a stage's patches, in scan order
     __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
@@ -2203,14 +2264,19 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     uint32_t X = 0, T = 0, flags = 0, needb = 0, src = 0, Lr = kLmNoList, Pr = DM_LM_NONE;
     uint64_t gT = 0, alloc = 0;
     double z = 0.0, zs = 0.0;
-    lm_codes_t c4 = {};
+    uint4 c4[NCH];                            // chunks l, l + kLmLanes, ... of the row (8 codes each)
+#pragma unroll
+    for (uint32_t q = 0; q < NCH; ++q) c4[q] = make_uint4(0u, 0u, 0u, 0u);
     if (valid) {
         const MergeJob* J = mp.job + i;
         X = J->X; T = J->T; gT = J->gT;
         flags = J->flags; needb = J->need;
         z = J->z; zs = J->zs; src = J->src;
         if (l < kLmList) { Lr = J->L[l]; Pr = J->P[l]; }
-        c4 = reinterpret_cast<const lm_codes_t*>(mp.codes + i * kMaxScanPatches)[l];
+        const uint4* crow = reinterpret_cast<const uint4*>(mp.codes + i * PART);
+#pragma unroll
+        for (uint32_t q = 0; q < NCH; ++q)
+            if ((l + kLmLanes * q) * 8 < mp.m) c4[q] = crow[l + kLmLanes * q];
         alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
     }
     if (gath && valid) {                      // the gather's copies: a field a lane
@@ -2234,11 +2300,12 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
         // ---- 1. the codes: patch k = l + kLmLanes u in lane l (round u precedes round u + 1 in
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
-        reinterpret_cast<lm_codes_t*>(&s_code[pl][0])[l] = c4;
-        wave_sync();
-        uint32_t code[kLmPerLane];
 #pragma unroll
-        for (uint32_t u = 0; u < kLmPerLane; ++u) {
+        for (uint32_t q = 0; q < NCH; ++q) reinterpret_cast<uint4*>(&s_code[pl][0])[l + kLmLanes * q] = c4[q];
+        wave_sync();
+        uint32_t code[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; ++u) {
             const uint32_t k = l + kLmLanes * u;
             code[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
         }
@@ -2297,7 +2364,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 for (cnt = 0; cnt < kLmList; ++cnt) {
                     uint32_t mn = kLmNoList;
 #pragma unroll
-                    for (uint32_t u = 0; u < kLmPerLane; ++u) {
+                    for (uint32_t u = 0; u < PER; ++u) {
                         const uint32_t s = code[u] >> 6;
                         if (code[u] != kCodeSkip && (int32_t)s > lo) mn = min(mn, s);
                     }
@@ -2308,7 +2375,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 }
                 uint32_t nx = kLmNoList;
 #pragma unroll
-                for (uint32_t u = 0; u < kLmPerLane; ++u)
+                for (uint32_t u = 0; u < PER; ++u)
                     if (code[u] != kCodeSkip && (int32_t)(code[u] >> 6) > lo) nx = min(nx, code[u] >> 6);
                 more = cnt == kLmList && grp_min(nx) != kLmNoList;
                 if (l < cnt) {
@@ -2376,7 +2443,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 // compare), rounds in order -- every cell sees its patches in scan order
                 uint32_t nst = 0;
 #pragma unroll
-                for (uint32_t u = 0; u < kLmPerLane; ++u) {
+                for (uint32_t u = 0; u < PER; ++u) {
                     bool in = false;
 #pragma unroll
                     for (uint32_t w = 0; w < kLmStage; ++w) in |= code[u] != kCodeSkip && Ls[w] == (code[u] >> 6);
@@ -4166,7 +4233,10 @@ extern "C" hipError_t eslam_launch_map_plan(DevState s0, DevState s1, Ctl* ctl, 
     const uint32_t nb = (uint32_t)((mp->n + kLmBlock - 1) / kLmBlock);
     e = hipMemsetAsync(mp->poff + nb, 0, 4, stream);
     if (e != hipSuccess) return e;
-    if (nb) hipLaunchKernelGGL(k_map_plan, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    if (nb && mp->m > kScanPartSmall)
+        hipLaunchKernelGGL(k_map_plan<kScanPartLarge>, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    else if (nb)
+        hipLaunchKernelGGL(k_map_plan<kScanPartSmall>, dim3(nb), dim3(kLmBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     return page_budget(ctl, lm, mp, nb, pgc, stream);
 }
 
@@ -4187,7 +4257,10 @@ extern "C" hipError_t eslam_launch_map_merge(DevState s0, DevState s1, Ctl* ctl,
                                              const MergeParams* mp, hipStream_t stream)
 {
     const uint32_t nb = (uint32_t)((mp->n + kLmPpb - 1) / kLmPpb);
-    if (nb) hipLaunchKernelGGL(k_map_merge, dim3(nb), dim3(kLmMergeBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    if (nb && mp->m > kScanPartSmall)
+        hipLaunchKernelGGL(k_map_merge<kScanPartLarge>, dim3(nb), dim3(kLmMergeBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
+    else if (nb)
+        hipLaunchKernelGGL(k_map_merge<kScanPartSmall>, dim3(nb), dim3(kLmMergeBlock), 0, stream, s0, s1, ctl, *map, *lm, *mp);
     hipLaunchKernelGGL(k_merge_counts, dim3(1), dim3(kMergeCounterSlots), 0, stream, mp->cnt, ctl, mp->acc);
     return hipGetLastError();
 }

@@ -260,13 +260,15 @@ def rotated(grid, yaw=0.3, tx=0.4, ty=-0.25):
     return grid
 
 
-@pytest.mark.parametrize("case", ["wide_scan", "rotated_grid", "small_window", "large_window"])
+@pytest.mark.parametrize("case", ["wide_scan", "rotated_grid", "small_window", "large_window", "laser_scan"])
 def test_particle_maps_shapes(gpu_mod, oracle, case):
     """The window's other shapes against the oracle, bit for bit: a scan reaching more tiles than
     one merge pass holds (kLmList = 8: the plan's and the merge's later passes) and past the
     window (dropped patches); a grid whose global2local is not the identity (every cell placed
     through the transform, in the plan, the merge and K1's lookups); a 5 x 5-tile window
-    (maxSensorRange 1 m) and a 27 x 27-tile one (10 m, reaching past the grid's edges)."""
+    (maxSensorRange 1 m) and a 27 x 27-tile one (10 m, reaching past the grid's edges); a laser
+    scan's MLS of 600 patches at the map's resolution (parts of 256: the large plan and merge, and a
+    last part of 88)."""
     n = 1500
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
@@ -277,6 +279,9 @@ def test_particle_maps_shapes(gpu_mod, oracle, case):
         cfg.local_map_pages = 128            # ~50 tiles a particle and its copies' pages
     elif case == "rotated_grid":
         grid = rotated(grid)
+    elif case == "laser_scan":
+        scan = S.scan_area(600)
+        cfg.local_map_pages = 48             # ~16 tiles a particle and its copies' pages
     elif case == "small_window":
         cfg.max_sensor_range = 1.0
         scan = S.scan_patches(nx=10, ny=8, x0=-0.8, x1=1.9, y0=-1.2, y1=1.0)
