@@ -319,13 +319,13 @@ static uint32_t lm_tile_page(const uint32_t* row, const int32_t* ctr, uint32_t h
     return k >= 0 ? row[wx * wy + 3 * k + 2] : DM_LM_NONE;
 }
 
-/* per-particle maps: GridAccess::get on the particle's own map = the shared grid, and for a
- * cell the grid leaves empty the particle's patch there (same 3-sigma gate)               */
+/* per-particle maps: GridAccess::get on the particle's own map = its own patch of the cell
+ * when it holds one that passes the 3-sigma gate (its copy of a grid cell, or a cell the grid
+ * leaves empty), else the shared grid's                                                    */
 static int particle_map_fn(void* user, const double p[3], double q_mean, double q_var, double* mean, double* stdev)
 {
     const or_pmap* pm = (const or_pmap*)user;
     const eslam_mls_grid* g = pm->g;
-    if (or_mls_get_patch(g, p, q_mean, q_var, mean, stdev)) return 1;
     const double* A = g->global2local;
     static const double id[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     int is_id = 1;
@@ -339,18 +339,17 @@ static int particle_map_fn(void* user, const double p[3], double q_mean, double 
     const double fm = floor((lx - g->offset_x) * (1.0 / g->scale_x));
     const double fn = floor((ly - g->offset_y) * (1.0 / g->scale_y));
     if (!(fm >= 0.0 && fm < (double)g->width && fn >= 0.0 && fn < (double)g->height)) return 0;
-    const uint32_t m = (uint32_t)fm, n = (uint32_t)fn, cell = n * g->width + m;
-    if (g->cell_start[cell] != g->cell_start[cell + 1]) return 0;       /* the grid's cell: no patch passed */
+    const uint32_t m = (uint32_t)fm, n = (uint32_t)fn;
     const uint32_t a = m >> DM_LM_TILE_BITS, b = n >> DM_LM_TILE_BITS;
     const uint32_t pg = lm_tile_page(pm->slot, pm->ctr, pm->hx, pm->hy, pm->wx, pm->wy, pm->V, a, b);
-    if (pg == DM_LM_NONE) return 0;
     const uint32_t j = (m & 7u) + 8u * (n & 7u);
-    const float* v = lm_page(pm->blk, pg)->v;
-    if (!dm_lm_holds(v[2 * j + 1])) return 0;
-    const double mm = (double)v[2 * j], sd = (double)v[2 * j + 1];
-    const double diff = fabs(mm - lz);
-    if (diff * diff < 9.0 * (sd * sd + q_var)) { *mean = mm; *stdev = sd; return 1; }
-    return 0;
+    if (pg != DM_LM_NONE && dm_lm_holds(lm_page(pm->blk, pg)->v[2 * j + 1])) {
+        const float* v = lm_page(pm->blk, pg)->v;
+        const double mm = (double)v[2 * j], sd = (double)v[2 * j + 1];
+        const double diff = fabs(mm - lz);
+        if (diff * diff < 9.0 * (sd * sd + q_var)) { *mean = mm; *stdev = sd; return 1; }
+    }
+    return or_mls_get_patch(g, p, q_mean, q_var, mean, stdev);
 }
 
 /* ========================================================================================
@@ -2246,10 +2245,10 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
                 cn = (uint32_t)fn;
                 cell = cn * g->width + cm;
             }
-            if (g->cell_start[cell] != g->cell_start[cell + 1]) {
-                ++covered;          /* the shared grid covers the cell: not merged */
-                continue;
-            }
+            /* a cell the shared grid covers: the particle's copy of it (the reference's clone,
+             * src/PoseEstimator.cpp:31-47, merged at :222-227) starts from the grid's patch */
+            const int cov = g->cell_start[cell] != g->cell_start[cell + 1];
+            covered += (uint64_t)cov;
             const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
             if (!dm_lm_inside(a, ctr[0], hx, wx) || !dm_lm_inside(b, ctr[1], hy, wy)) {
                 ++dropped;          /* beyond maxSensorRange: outside the window */
@@ -2260,9 +2259,12 @@ static int or_map_update_part(or_filter* f, const eslam_scan_patch* sp, uint32_t
             const double var = sp[k].stdev * sp[k].stdev + zvar;
             uint32_t pg = sl[slot];
             float mo, so;
+            double gm, gs;
             if (pg != DM_LM_NONE && dm_lm_holds(lm_pg(f, pg)->v[2 * j + 1])) {
                 const float* v = lm_pg(f, pg)->v;
                 if (!dm_lm_fuse(v[2 * j], v[2 * j + 1], wz, var, &mo, &so)) continue;
+            } else if (cov && or_mls_cell_patch(g, cell, wz, var, &gm, &gs) && dm_lm_fuse((float)gm, (float)gs, wz, var, &mo, &so)) {
+                /* fused with the grid's patch that getPatch's 3-sigma gate picks for it */
             } else {
                 mo = (float)wz;
                 so = (float)dm_sqrt(var);
@@ -2396,6 +2398,19 @@ int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
                 cn = (uint32_t)fn;
             }
             const uint64_t cell = (uint64_t)cn * g->width + cm;
+            if (pmaps) {                      /* the particle's own cell first */
+                const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+                if (dm_lm_inside(a, na, hx, wx) && dm_lm_inside(b, nb, hy, wy)) {
+                    const uint32_t pg = lm_tile_page(f->pm_slot + (uint64_t)i * f->lm_R, f->pm_ctr + 2 * i, hx, hy, wx, wy, V, a, b);
+                    const uint32_t j = (cm & 7u) + 8u * (cn & 7u);
+                    if (pg != DM_LM_NONE && dm_lm_holds(lm_pg(f, pg)->v[2 * j + 1])) {
+                        const double d = wz - (double)lm_pg(f, pg)->v[2 * j];
+                        sum += dm_exp(-(d * d) / (2.0 * OR_MATCH_SIGMA * OR_MATCH_SIGMA));
+                        ++cnt;
+                        continue;
+                    }
+                }
+            }
             if (g->cell_start[cell] != g->cell_start[cell + 1]) {        /* a cell of the shared grid */
                 double mean, sd;
                 const double var = sp[k].stdev * sp[k].stdev + zvar;
@@ -2404,19 +2419,7 @@ int or_map_match(or_filter* f, const eslam_scan_patch* sp, uint32_t m)
                     sum += dm_exp(-(d * d) / (2.0 * OR_MATCH_SIGMA * OR_MATCH_SIGMA));
                 }
                 ++cnt;
-                continue;
             }
-            if (!pmaps) continue;
-            const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
-            if (!dm_lm_inside(a, na, hx, wx) || !dm_lm_inside(b, nb, hy, wy)) continue;
-            const uint32_t pg = lm_tile_page(f->pm_slot + (uint64_t)i * f->lm_R, f->pm_ctr + 2 * i, hx, hy, wx, wy, V, a, b);
-            if (pg == DM_LM_NONE) continue;
-            const float* v = lm_pg(f, pg)->v;
-            const uint32_t j = (cm & 7u) + 8u * (cn & 7u);
-            if (!dm_lm_holds(v[2 * j + 1])) continue;
-            const double d = wz - (double)v[2 * j];
-            sum += dm_exp(-(d * d) / (2.0 * OR_MATCH_SIGMA * OR_MATCH_SIGMA));
-            ++cnt;
         }
         const float wf = cnt ? (float)(sum / (double)cnt) : 1.0f;
         f->w[OD(i)] *= dm_pow((double)wf, (double)0.1f);

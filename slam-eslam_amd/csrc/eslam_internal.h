@@ -151,8 +151,9 @@ constexpr uint32_t kSidRecord = 0x80000000u;
 struct alignas(8) MapPayHdr {
     int2 ctr;
     uint32_t npg;
-    uint32_t share;                      // 1: the previous record (same source, same destination)
-                                         // carries this record's map (npg 0): they name one table
+    uint32_t share;                      // bit 0: the previous record (same source, same destination)
+                                         // carries this record's map (npg 0): they name one table;
+                                         // bit 1: the map holds copies of shared-grid cells (kLmShadow)
 };
 // the first record of each destination's range of a sharded send (PlanParams::send_off): a
 // record there always carries its map
@@ -169,6 +170,9 @@ struct alignas(8) MapPayPage {
 };
 static_assert(sizeof(MapPayPage) == 528, "payload page");
 constexpr uint32_t kPayTrail = 0x80000000u;
+// a table row's word lm_trail_off - 2 (window padding): kLmShadow when the map holds its own
+// copy of a cell the shared grid covers (lookups then ask the particle's cells first)
+constexpr uint32_t kLmShadow = 1u;
 // the tables' pool holds 2 x cap tables: at most n <= cap are named by a particle, so at least
 // cap are free whenever a map update starts, and particle i may take the i-th free one (copy
 // on write with a fixed, deterministic allocation of tables and no allocation counter)
@@ -342,6 +346,7 @@ inline CowScratch cow_layout(uint32_t* base, uint64_t cap)
 // k_map_plan -> k_map_merge, per particle (one 128-byte record): what the plan decided, so
 // the merge's first memory round trip brings everything its page moves need
 constexpr uint32_t kJobPlaced = 1u, kJobShared = 2u, kJobMore = 4u, kJobMoved = 8u;   // flags; tiles of pass 1 << 8
+constexpr uint32_t kJobCovered = 16u;    // a patch of this part lands on a cell the shared grid covers
 struct alignas(16) MergeJob {
     uint32_t X, T;                       // the table the particle names; the table its merge writes
     uint64_t gT;                         // tgen[T] << 32 | T: the owner word of T's pages

@@ -359,8 +359,20 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t m, uint32_t n
     return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), sd, lz, qv, mean, stdev);
 }
 
+// a particle's table name for get_patch<DELTA>, with bit 31 set when its map holds copies of
+// shared-grid cells (kLmShadow in its row): its lookups then ask its own cells first
+__device__ __forceinline__ uint32_t store_sid(uint32_t sid)
+{
+    const su16 h = kl16(KOFF(store));
+    const uint64_t w3 = kq(h, 3), w5 = kq(h, 5);
+    const uint32_t S = (uint32_t)w3, V = (uint32_t)(w5 >> 32);
+    const uint32_t f = kp<const uint32_t>(h, 1)[(uint64_t)sid * S + (S - 4u * V - 2u)];
+    return sid | (f == kLmShadow ? 0x80000000u : 0u);
+}
+
 // the map is K1Args::map, read by scalar loads (header: 64 bytes per lookup).  DELTA: the
-// particle's own map store answers for cells the shared grid leaves empty.
+// particle's own map answers for cells the shared grid leaves empty, and first for every cell
+// when it holds copies of shared-grid cells (sid bit 31, store_sid).
 template <bool DELTA = false>
 __device__ __forceinline__ bool get_patch(const Window& win, double px, double py, double pz, double qv, double& mean,
                                           double& stdev, uint32_t sid = 0)
@@ -377,6 +389,15 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     }
     const double ux = (lx - kd(h, 4)) * kd(h, 2);
     const double uy = (ly - kd(h, 5)) * kd(h, 3);
+    if constexpr (DELTA) {
+        if (sid >> 31) {                     // the particle's own cell first (the oracle's particle_map_fn)
+            sid &= 0x7fffffffu;
+            const double fm = floor(ux), fn = floor(uy);
+            if ((fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells) &&
+                store_patch(sid, (uint32_t)fm, (uint32_t)fn, lz, qv, mean, stdev))
+                return true;
+        }
+    }
     // fast path without branches: an in-window cell whose first patch passes the gate (the
     // window is only staged for maps without heights).  Everything else -- off the window,
     // heights, a failing first patch of a multi-patch cell -- takes the loop below.  The
@@ -1005,7 +1026,7 @@ __global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR __attribute__((amdgpu_wa
             if constexpr (DELTA) {
                 // per-particle maps: the host materialises every gather first, so particle i
                 // is at i; its store name sits next to the state (DevState::sid)
-                sid = kp<const uint32_t>(kl2(st_off + (uint32_t)offsetof(DevState, sid)), 0)[i];
+                sid = store_sid(kp<const uint32_t>(kl2(st_off + (uint32_t)offsetof(DevState, sid)), 0)[i]);
             }
             CMResult r = evaluate_pose<MAXP, BATCH, DELTA, UNG>(win, co, s, r22, x, y, z, meas_var, sid);
             if (meas_var == 0) {            // evaluatePose throws (src/ContactModel.cpp:122): no contact points
@@ -1343,7 +1364,7 @@ __global__ void __launch_bounds__(kBlock) k_contact_records(K1Args a, DebugRec d
             const double wz = ((c.zz + r22 * c.pz) + z) - a.p.radius;
             if (group_valid && c_eval) {
                 double mean = 0.0, stdev = 0.0;
-                if (get_patch<DELTA>(win, wx, wy, wz, meas_var, mean, stdev, DELTA ? st.sid[i] : 0u)) {
+                if (get_patch<DELTA>(win, wx, wy, wz, meas_var, mean, stdev, DELTA ? store_sid(st.sid[i]) : 0u)) {
                     const double zdiff = wz - mean;
                     const double zvar = stdev * stdev + meas_var;
                     if (!valid && c_end && ratio_surely_significant(zdiff, zvar, corr)) {
@@ -1754,16 +1775,15 @@ __device__ __forceinline__ uint16_t lm_code(const MapView& map, const LocalMaps&
         }
         uint16_t code = kCodeSkip;
         if (cell != 0xffffffffu) {
-            if ((map.occ[cell >> 5] >> (cell & 31u)) & 1u) {
-                ++covered;                   // the shared grid covers the cell: not merged
+            // a cell the shared grid covers: merged into the particle's own copy of it (the merge
+            // starts it from the grid's patch)
+            if ((map.occ[cell >> 5] >> (cell & 31u)) & 1u) ++covered;
+            const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
+            if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
+                const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
+                code = (uint16_t)((s << 6) | ((cm & 7u) + 8u * (cn & 7u)));
             } else {
-                const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
-                if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
-                    const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
-                    code = (uint16_t)((s << 6) | ((cm & 7u) + 8u * (cn & 7u)));
-                } else {
-                    ++dropped;               // beyond maxSensorRange: outside the window
-                }
+                ++dropped;                   // beyond maxSensorRange: outside the window
             }
         }
         return code;
@@ -2075,6 +2095,32 @@ __device__ __forceinline__ uint32_t grp_or(uint32_t v)
 }
 __device__ __forceinline__ uint32_t grp_get(uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)l, kLmLanes); }
 
+// the first patch of shared-grid cell ct (its MapView::cell_tab record) passing getPatch's
+// 3-sigma gate against the local height lz (the oracle's or_mls_cell_patch); its stdev in *sd
+__device__ __forceinline__ bool grid_cell_patch(const MapView& map, uint4 ct, double lz, double qv, double& mean,
+                                                double* sd = nullptr)
+{
+    for (uint32_t k = ct.z; k < ct.z + ct.w; ++k) {
+        const float2 pf = k == ct.z ? make_float2(__uint_as_float(ct.x), __uint_as_float(ct.y)) : map.patch[k];
+        const double pm = (double)pf.x, ps = (double)pf.y;
+        const double ph = map.height ? (double)map.height[k] : 0.0;
+        double diff;
+        if (ph > 0.0) {
+            if (lz > pm) diff = lz - pm;
+            else if (lz < pm - ph) diff = (pm - ph) - lz;
+            else diff = 0.0;
+        } else {
+            diff = dm_fabs(pm - lz);
+        }
+        if (diff * diff < 9.0 * (ps * ps + qv)) {
+            mean = pm;
+            if (sd) *sd = ps;
+            return true;
+        }
+    }
+    return false;
+}
+
 // k_map_plan: per particle (a lane each: kLmBlock particles a block, so the latency of its
 // chain of lookups -- state, table, page, owner -- overlaps across many particles) the cell
 // codes of its scan (MergeParams::codes), the first pass's tiles with their pages and whether
@@ -2122,6 +2168,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             uint4* crow = reinterpret_cast<uint4*>(mp.codes + i * PART);
             uint32_t L[kLmList];
             bool more1 = false;
+            const uint32_t cov0 = covered;
             if constexpr (kSmall) {
                 lm_codes(map, lm, mp, q, codes, covered, dropped);
                 lm_collect(codes, mp.m, kLmNoList, L);
@@ -2170,7 +2217,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
             jb.oy = oc.y;
             jb.need = bits;
             jb.flags = kJobPlaced | (q.shared ? kJobShared : 0u) | (more ? kJobMore : 0u) | (moved ? kJobMoved : 0u) |
-                       (nt << 8);
+                       (covered != cov0 ? kJobCovered : 0u) | (nt << 8);
         }
     }
     // the codes rows and the records leave through LDS, so every store is a whole 1-KiB line of
@@ -2263,6 +2310,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     // the plan's record, the codes and this particle's first page: one round trip
     uint32_t X = 0, T = 0, flags = 0, needb = 0, src = 0, Lr = kLmNoList, Pr = DM_LM_NONE;
     uint64_t gT = 0, alloc = 0;
+    int32_t na = 0, nb = 0;
     double z = 0.0, zs = 0.0;
     uint4 c4[NCH];                            // chunks l, l + kLmLanes, ... of the row (8 codes each)
 #pragma unroll
@@ -2271,6 +2319,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         const MergeJob* J = mp.job + i;
         X = J->X; T = J->T; gT = J->gT;
         flags = J->flags; needb = J->need;
+        na = J->na; nb = J->nb;
         z = J->z; zs = J->zs; src = J->src;
         if (l < kLmList) { Lr = J->L[l]; Pr = J->P[l]; }
         const uint4* crow = reinterpret_cast<const uint4*>(mp.codes + i * PART);
@@ -2294,7 +2343,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         default: break;
         }
     }
-    bool dirty = false, moved = false;
+    bool dirty = false, moved = false, covw = false;
     uint32_t written = 0, taken = 0;
     const bool shared = (flags & kJobShared) != 0;
     if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
@@ -2470,9 +2519,26 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                             const double wz = sp.z + z;
                             const double var = sp.stdev * sp.stdev + zvar;
                             float mo = cv.x, so = cv.y;
-                            bool w = true;
-                            if (dm_lm_holds(cv.y)) w = dm_lm_fuse(cv.x, cv.y, wz, var, &mo, &so);
-                            else { mo = (float)wz; so = (float)dm_sqrt(var); }
+                            bool w = true, ins = true;
+                            if (dm_lm_holds(cv.y)) {
+                                w = dm_lm_fuse(cv.x, cv.y, wz, var, &mo, &so);
+                                ins = false;
+                            } else if (flags & kJobCovered) {
+                                // a cell the shared grid covers: the particle's copy starts from
+                                // the grid's patch the 3-sigma gate picks (the oracle alike)
+                                const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
+                                const uint32_t cm = 8u * (uint32_t)lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx) + (ci & 7u);
+                                const uint32_t cn = 8u * (uint32_t)lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by) + (ci >> 3);
+                                const uint64_t cell = (uint64_t)cn * map.width + cm;
+                                double gm, gs;
+                                if (((map.occ[cell >> 5] >> (cell & 31u)) & 1u) &&
+                                    grid_cell_patch(map, map.cell_tab[cell], wz, var, gm, &gs) &&
+                                    dm_lm_fuse((float)gm, (float)gs, wz, var, &mo, &so)) {
+                                    ins = false;
+                                    covw = true;
+                                }
+                            }
+                            if (ins) { mo = (float)wz; so = (float)dm_sqrt(var); }
                             if (w) {
                                 *cp = make_float2(mo, so);
                                 wbits |= 1u << rr;
@@ -2498,6 +2564,12 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         }
         if (shared && dirty) moved = true;
         if ((gath || moved) && l == 0) st.sid[i] = moved ? T : X;
+        // the map now holds a copy of a shared-grid cell: its lookups ask its own cells first
+        // (after T's row words have landed: the copy above may have written this word)
+        if (grp_or(covw ? 1u : 0u) && l == 0) {
+            __builtin_amdgcn_s_waitcnt(0);
+            tsl[lm_trail_off(lm) - 2u] = kLmShadow;
+        }
     } else if (valid && gath && l == 0) {
         st.sid[i] = X;
     }
@@ -2514,27 +2586,6 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
         if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
     }
-}
-
-// the first patch of shared-grid cell ct (its MapView::cell_tab record) passing getPatch's
-// 3-sigma gate against the local height lz (the oracle's or_mls_cell_patch)
-__device__ __forceinline__ bool grid_cell_patch(const MapView& map, uint4 ct, double lz, double qv, double& mean)
-{
-    for (uint32_t k = ct.z; k < ct.z + ct.w; ++k) {
-        const float2 pf = k == ct.z ? make_float2(__uint_as_float(ct.x), __uint_as_float(ct.y)) : map.patch[k];
-        const double pm = (double)pf.x, ps = (double)pf.y;
-        const double ph = map.height ? (double)map.height[k] : 0.0;
-        double diff;
-        if (ph > 0.0) {
-            if (lz > pm) diff = lz - pm;
-            else if (lz < pm - ph) diff = (pm - ph) - lz;
-            else diff = 0.0;
-        } else {
-            diff = dm_fabs(pm - lz);
-        }
-        if (diff * diff < 9.0 * (ps * ps + qv)) { mean = pm; return true; }
-    }
-    return false;
 }
 
 // processMap(scanMap, match = true) per particle (the oracle's or_map_match; the rule is the
@@ -2639,25 +2690,24 @@ __global__ void __launch_bounds__(kBlock) k_map_match(DevState s0, DevState s1, 
         float2 cv[kMatchBatch];
 #pragma unroll
         for (uint32_t q = 0; q < kMatchBatch; ++q) {
-            pg[q] = (PMAPS && own[q] && ct[q].w == 0u) ? sl[q] : DM_LM_NONE;
+            pg[q] = (PMAPS && own[q]) ? sl[q] : DM_LM_NONE;
             cv[q] = pg[q] != DM_LM_NONE ? lm.page[(uint64_t)pg[q] * DM_LM_PAGE_CELLS + cj[q]] : make_float2(0.0f, -1.0f);
         }
 #pragma unroll
         for (uint32_t q = 0; q < kMatchBatch; ++q) {
             if (!on[q]) continue;
-            if (ct[q].w != 0u) {                 // a cell of the shared grid
+            if (pg[q] != DM_LM_NONE && dm_lm_holds(cv[q].y)) {     // the particle's own cell first
+                const double d = wzs[q] - (double)cv[q].x;
+                sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
+                ++cnt;
+            } else if (ct[q].w != 0u) {          // a cell of the shared grid
                 double mean;
                 if (grid_cell_patch(map, ct[q], lzs[q], var[q], mean)) {
                     const double d = lzs[q] - mean;
                     sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
                 }
                 ++cnt;
-                continue;
             }
-            if (pg[q] == DM_LM_NONE || !dm_lm_holds(cv[q].y)) continue;
-            const double d = wzs[q] - (double)cv[q].x;
-            sum += dm_exp(-(d * d) / (2.0 * kMatchSigma * kMatchSigma));
-            ++cnt;
         }
     }
     const float wf = cnt ? (float)(sum / (double)cnt) : 1.0f;
@@ -4302,7 +4352,7 @@ __global__ void __launch_bounds__(kBlock) k_pay_hdr(const DevState s0, const Dev
             MapPayHdr h;
             h.ctr = lm.ctr[X];
             h.npg = c;
-            h.share = share ? 1u : 0u;
+            h.share = (share ? 1u : 0u) | (row[toff - 2u] == kLmShadow ? 2u : 0u);
             hdr[j] = h;
         }
     }
@@ -4320,7 +4370,7 @@ __global__ void __launch_bounds__(kBlock) k_pay_pack(const DevState s0, const De
     const uint64_t nw = (uint64_t)gridDim.x * kWaves;
     const DevState st = ctl->base ? s1 : s0;
     for (uint64_t j = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); j < nsend; j += nw) {
-        if (hdr[j].share) continue;                      // the previous record carries the map
+        if (hdr[j].share & 1u) continue;                 // the previous record carries the map
         const uint64_t i = (send[j].src >> 8) - gbase;
         const uint32_t X = st.sid[i];
         const uint32_t* row = lm.slot + (uint64_t)X * lm.S;
@@ -4376,7 +4426,7 @@ __global__ void __launch_bounds__(1024) k_recv_heads(const MapPayHdr* __restrict
     const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
     uint32_t h = 0;                                      // 1 + the last head of the range (0: none)
     for (uint64_t i = lo; i < hi; ++i)
-        if (!hdr[i].share) h = (uint32_t)i + 1u;
+        if (!(hdr[i].share & 1u)) h = (uint32_t)i + 1u;
     s_h[threadIdx.x] = h;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {                 // inclusive max-scan over the threads
@@ -4387,7 +4437,7 @@ __global__ void __launch_bounds__(1024) k_recv_heads(const MapPayHdr* __restrict
     }
     uint32_t run = threadIdx.x ? s_h[threadIdx.x - 1] : 0u;
     for (uint64_t i = lo; i < hi; ++i) {
-        if (!hdr[i].share) run = (uint32_t)i + 1u;
+        if (!(hdr[i].share & 1u)) run = (uint32_t)i + 1u;
         head[i] = run ? run - 1u : 0u;                   // record 0 always carries its map
     }
 }
@@ -4407,7 +4457,7 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uin
     const uint64_t nw = (uint64_t)gridDim.x * (kLmBlock / 64);
     const uint32_t toff = lm.S - 4u * lm.V;
     for (uint64_t r = (uint64_t)blockIdx.x * (kLmBlock / 64) + (threadIdx.x >> 6); r < nrec; r += nw) {
-        if (hdr[r].share) continue;
+        if (hdr[r].share & 1u) continue;
         const uint64_t alloc = ctl->pg_cursor + hoff[r];
         const uint32_t T = frees[r];
         const uint64_t gT = ((uint64_t)lm.tgen[T] << 32) | T;
@@ -4421,7 +4471,9 @@ __global__ void __launch_bounds__(kLmBlock) k_recv_maps(uint64_t nrec, const uin
         uint32_t* tsl = lm.slot + (uint64_t)T * lm.S;
         for (uint32_t s = lane; s < lm.S; s += 64u) {
             uint32_t v = DM_LM_NONE;
-            if (s == toff - 1u) {                        // the trail's high-water mark
+            if (s == toff - 2u) {                        // the map's copies of shared-grid cells
+                v = (hdr[r].share & 2u) ? kLmShadow : DM_LM_NONE;
+            } else if (s == toff - 1u) {                 // the trail's high-water mark
                 for (uint32_t q = 0; q < npg; ++q) {
                     const uint32_t sl = pay[q0 + q].slot;
                     if (sl & kPayTrail) v = (v == DM_LM_NONE || (sl & ~kPayTrail) + 1u > v) ? (sl & ~kPayTrail) + 1u : v;

@@ -260,7 +260,7 @@ def rotated(grid, yaw=0.3, tx=0.4, ty=-0.25):
     return grid
 
 
-@pytest.mark.parametrize("case", ["wide_scan", "rotated_grid", "small_window", "large_window", "laser_scan"])
+@pytest.mark.parametrize("case", ["wide_scan", "rotated_grid", "small_window", "large_window", "laser_scan", "mapped_cells"])
 def test_particle_maps_shapes(gpu_mod, oracle, case):
     """The window's other shapes against the oracle, bit for bit: a scan reaching more tiles than
     one merge pass holds (kLmList = 8: the plan's and the merge's later passes) and past the
@@ -268,7 +268,8 @@ def test_particle_maps_shapes(gpu_mod, oracle, case):
     through the transform, in the plan, the merge and K1's lookups); a 5 x 5-tile window
     (maxSensorRange 1 m) and a 27 x 27-tile one (10 m, reaching past the grid's edges); a laser
     scan's MLS of 600 patches at the map's resolution (parts of 256: the large plan and merge, and a
-    last part of 88)."""
+    last part of 88); a scan reaching back over the mapped cells (each particle's copy of a
+    shared-grid cell starts from the grid's patch, and its lookups then ask its own cells first)."""
     n = 1500
     cfg = S.bench_config(A.default_config(), n)
     cfg.flags |= A.FLAG_PARTICLE_MAPS | A.FLAG_RECORD_ANCESTORS
@@ -279,6 +280,8 @@ def test_particle_maps_shapes(gpu_mod, oracle, case):
         cfg.local_map_pages = 128            # ~50 tiles a particle and its copies' pages
     elif case == "rotated_grid":
         grid = rotated(grid)
+    elif case == "mapped_cells":
+        scan = S.scan_patches(nx=10, ny=6, x0=-0.9, x1=0.95)
     elif case == "laser_scan":
         scan = S.scan_area(600)
         cfg.local_map_pages = 48             # ~16 tiles a particle and its copies' pages
@@ -310,9 +313,11 @@ def test_particle_maps_shapes(gpu_mod, oracle, case):
         assert dropped > 0                   # the scan reaches past the window
     else:
         assert dropped == 0
+    if case == "mapped_cells":
+        assert gi.map_patches_covered > 0
 
 
-@pytest.mark.parametrize("case", ["identity", "rotated_grid"])
+@pytest.mark.parametrize("case", ["identity", "rotated_grid", "mapped_cells"])
 def test_particle_maps_match_bit_exact(gpu_mod, oracle, case):
     """processMap(scanMap, match, update) (src/EmbodiedSlamFilter.cpp:179-232): the match
     weighting (eslam_gpu_map_match: every 10th patch scored against the particle's own map,
@@ -332,6 +337,9 @@ def test_particle_maps_match_bit_exact(gpu_mod, oracle, case):
         f.init_gaussian(n, [0.0, 0.0, 0.0], [0.1, 0.1, 0.05], 0.18, 0.05)
     scan = S.scan_patches(nx=12, ny=9)                # 108 patches: 11 sampled
     probe = S.scan_patches(nx=12, ny=9, z=-0.15)
+    if case == "mapped_cells":                        # reaching back over the shared grid's cells
+        scan = S.scan_patches(nx=12, ny=9, x0=-0.9, x1=0.95)
+        probe = S.scan_patches(nx=12, ny=9, x0=-0.9, x1=0.95, z=-0.15)
     lowered = 0
     for k, st in enumerate(S.step_stream(14, tilt=True)):
         assert gpu.step(st) == orc.step(st)

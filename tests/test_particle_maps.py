@@ -27,9 +27,9 @@ def setup(n=600, x0=0.3, cells=60):
     return f, grid
 
 
-def test_insert_into_empty_cells_only(oracle):
+def test_insert_into_empty_cells(oracle):
     f, grid = setup()
-    scan = S.scan_patches()
+    scan = S.scan_patches(x0=0.45)                       # clear of the mapped cells x < 0.3
     f.map_update(scan)
     p = f.download()
     cs = grid.cell_start
@@ -266,6 +266,33 @@ def test_window_model(oracle, nx, ny, steps, dx, trail):
                 assert got[cc][0].view(np.uint32) == v[0].view(np.uint32) and got[cc][1].view(np.uint32) == v[1].view(np.uint32), (k, i, cc)
     if dx > 0.1:
         assert (evicted > 0) == (trail < 16), evicted
+
+
+def test_scan_on_mapped_cells_fuses_with_the_grid(oracle):
+    """A scan patch on a cell the shared grid covers goes into the particle's own copy of the
+    cell (the reference merges into each particle's clone of the grid, src/EmbodiedSlamFilter.cpp:
+    222-227, clones at src/PoseEstimator.cpp:31-62): fused with the grid's patch (flat map: mean
+    0, stdev 0.05) when within 3 sigma; the contact update then reads the particle's patch."""
+    f, grid = setup(n=200)
+    back = S.scan_patches(nx=8, ny=6, x0=-0.6, x1=0.95)
+    f.map_update(back)
+    p = f.download()
+    cs = grid.cell_start.astype(np.int64)
+    g_sd = float(np.float32(0.05))
+    seen = 0
+    for i in range(0, p.n, 13):
+        cells, mean, sd = f.particle_map(i)
+        cov = cs[cells.astype(np.int64)] != cs[cells.astype(np.int64) + 1]
+        seen += int(cov.sum())
+        zs2 = p.zsigma[i] * p.zsigma[i]
+        var = 0.03 * 0.03 + zs2
+        v1 = g_sd * g_sd
+        want_sd = np.float32(math.sqrt((v1 * var) / (v1 + var)))
+        # fused with the grid's patch at least once: at most the fusion of one grid and one scan
+        # patch (a cell two scan patches reach fuses twice)
+        assert np.all(sd[cov] <= want_sd + 2e-7), (i, sd[cov], want_sd)
+        assert np.any(np.abs(sd[cov] - want_sd) < 2e-7) or not cov.any()
+    assert seen > 0
 
 
 def test_covered_cells_are_counted(oracle):
