@@ -2326,6 +2326,10 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 #pragma unroll
         for (uint32_t q = 0; q < NCH; ++q)
             if ((l + kLmLanes * q) * 8 < mp.m) c4[q] = crow[l + kLmLanes * q];
+        if constexpr (NCH > 1) {              // a large part's codes to LDS at once (no registers held)
+#pragma unroll
+            for (uint32_t q = 0; q < NCH; ++q) reinterpret_cast<uint4*>(&s_code[pl][0])[l + kLmLanes * q] = c4[q];
+        }
         alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
     }
     if (gath && valid) {                      // the gather's copies: a field a lane
@@ -2349,15 +2353,18 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
         // ---- 1. the codes: patch k = l + kLmLanes u in lane l (round u precedes round u + 1 in
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
-#pragma unroll
-        for (uint32_t q = 0; q < NCH; ++q) reinterpret_cast<uint4*>(&s_code[pl][0])[l + kLmLanes * q] = c4[q];
+        if constexpr (NCH == 1) reinterpret_cast<uint4*>(&s_code[pl][0])[l] = c4[0];
         wave_sync();
-        uint32_t code[PER];
+        // two 16-bit codes a register: code(u) is patch l + kLmLanes u
+        uint32_t cpk[(PER + 1) / 2];
 #pragma unroll
-        for (uint32_t u = 0; u < PER; ++u) {
-            const uint32_t k = l + kLmLanes * u;
-            code[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
+        for (uint32_t v = 0; v < (PER + 1) / 2; ++v) {
+            const uint32_t k0 = l + kLmLanes * (2 * v), k1 = k0 + kLmLanes;
+            const uint32_t c0 = k0 < mp.m ? (uint32_t)s_code[pl][k0] : (uint32_t)kCodeSkip;
+            const uint32_t c1 = (2 * v + 1 < PER && k1 < mp.m) ? (uint32_t)s_code[pl][k1] : (uint32_t)kCodeSkip;
+            cpk[v] = c0 | (c1 << 16);
         }
+        auto code = [&](uint32_t u) -> uint32_t { return (cpk[u >> 1] >> ((u & 1u) * 16u)) & 0xffffu; };
         // the plan has moved T's window (a moved shared X copied to T): every tile of the scan is
         // in T's slots, and the merge only adds the new pages -- but a shared X whose window
         // stays is copied to T here, the pass's new pages folded in
@@ -2414,8 +2421,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     uint32_t mn = kLmNoList;
 #pragma unroll
                     for (uint32_t u = 0; u < PER; ++u) {
-                        const uint32_t s = code[u] >> 6;
-                        if (code[u] != kCodeSkip && (int32_t)s > lo) mn = min(mn, s);
+                        const uint32_t s = code(u) >> 6;
+                        if (code(u) != kCodeSkip && (int32_t)s > lo) mn = min(mn, s);
                     }
                     mn = grp_min(mn);
                     if (mn == kLmNoList) break;
@@ -2425,7 +2432,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 uint32_t nx = kLmNoList;
 #pragma unroll
                 for (uint32_t u = 0; u < PER; ++u)
-                    if (code[u] != kCodeSkip && (int32_t)(code[u] >> 6) > lo) nx = min(nx, code[u] >> 6);
+                    if (code(u) != kCodeSkip && (int32_t)(code(u) >> 6) > lo) nx = min(nx, code(u) >> 6);
                 more = cnt == kLmList && grp_min(nx) != kLmNoList;
                 if (l < cnt) {
                     __builtin_amdgcn_s_waitcnt(0);   // the group's stores of T's row (pass 0) have landed
@@ -2495,7 +2502,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 for (uint32_t u = 0; u < PER; ++u) {
                     bool in = false;
 #pragma unroll
-                    for (uint32_t w = 0; w < kLmStage; ++w) in |= code[u] != kCodeSkip && Ls[w] == (code[u] >> 6);
+                    for (uint32_t w = 0; w < kLmStage; ++w) in |= code(u) != kCodeSkip && Ls[w] == (code(u) >> 6);
                     const uint32_t gm = (uint32_t)(__ballot(in) >> gshift) & ((1u << kLmLanes) - 1u);
                     if (in) s_list[pl][nst + __builtin_popcount(gm & ((1u << l) - 1u))] = (uint8_t)(l + kLmLanes * u);
                     nst += __builtin_popcount(gm);

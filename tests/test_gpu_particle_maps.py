@@ -282,12 +282,14 @@ def test_particle_maps_shapes(gpu_mod, oracle, case):
         grid = rotated(grid)
     elif case == "mapped_cells":
         scan = S.scan_patches(nx=10, ny=6, x0=-0.9, x1=0.95)
+        cfg.local_map_pages = 48
     elif case == "laser_scan":
         scan = S.scan_area(600)
         cfg.local_map_pages = 48             # ~16 tiles a particle and its copies' pages
     elif case == "small_window":
         cfg.max_sensor_range = 1.0
         scan = S.scan_patches(nx=10, ny=8, x0=-0.8, x1=1.9, y0=-1.2, y1=1.0)
+        cfg.local_map_pages = 48             # the scan reaches back over the mapped cells: their copies
     else:
         cfg.max_sensor_range = 10.0
         scan = S.scan_patches(nx=12, ny=10, x0=-5.0, x1=5.5, y0=-4.0, y1=4.0)
@@ -330,6 +332,8 @@ def test_particle_maps_match_bit_exact(gpu_mod, oracle, case):
     grid = S.unmapped_beyond(S.rough_map(cells=120), 0.3)
     if case == "rotated_grid":
         grid = rotated(grid)
+    if case == "mapped_cells":
+        cfg.local_map_pages = 48                      # copies of the mapped cells the scans reach
     gpu = gpu_mod.GpuFilter(cfg)
     orc = O.OracleFilter(cfg, O.SUM_CONTRACT)
     for f in (gpu, orc):
