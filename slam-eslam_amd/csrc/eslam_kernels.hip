@@ -2038,7 +2038,7 @@ __global__ void k_page_budget2(Ctl* __restrict__ ctl, const uint32_t* __restrict
 // maps is a whole table or page moved by the group together (a lane per particle touching
 // 8-byte cells scattered over 64 pages missed the caches on two of three accesses: r05h).
 // Per particle:
-//   1. the plan's record, the codes (kLmPerLane a lane) and the allocation offset arrive in one
+//   1. the plan's record, the codes (PART / kLmLanes a lane, two to a register) and the allocation offset arrive in one
 //      round trip; each patch is ranked among the earlier patches on its cell;
 //   2. lane r of the group takes tile r of the first pass: a new page when the plan says the
 //      table does not own it; a table copied on write or whose window moved is rewritten by
@@ -2062,7 +2062,6 @@ constexpr uint32_t kLmLanes = ESLAM_LM_LANES;                       // lanes per
 constexpr uint32_t kLmMergeBlock = 128;
 constexpr uint32_t kLmPpb = kLmMergeBlock / kLmLanes;               // particles per block
 constexpr uint32_t kLmStage = ESLAM_LM_STAGE;                        // pages in LDS per particle
-constexpr uint32_t kLmPerLane = kScanPartSmall / kLmLanes;              // codes a lane holds (small part)
 static_assert(kLmList <= kLmLanes && (kLmLanes == 8 || kLmLanes == 16) && kLmStage <= 4,
               "a lane per tile of a pass; 8 or 16 lanes; row masks of 8 bits per staged page in a word");
 constexpr uint32_t kLmChunk = kLmLanes * 16;                         // bytes of a page a group moves per instruction
@@ -2285,7 +2284,17 @@ __device__ __forceinline__ uint32_t lm_stage_off(uint32_t rr, uint32_t ci, uint3
     constexpr uint32_t cpc = kLmChunk / 8;                           // cells per chunk
     return (rr * kLmNq + ci / cpc) * 1024 + g * kLmChunk + (ci % cpc) * 8;
 }
-#define LM_MERGE_ATTR __attribute__((amdgpu_waves_per_eu(ESLAM_LM_WPE)))
+// a large part's 32 codes a lane: three waves a SIMD (168 VGPRs)
+#define LM_MERGE_ATTR __attribute__((amdgpu_waves_per_eu(PART == kScanPartSmall ? ESLAM_LM_WPE : ESLAM_LM_WPE_LARGE)))
+#ifndef ESLAM_LM_WPE_LARGE
+#define ESLAM_LM_WPE_LARGE 3
+#endif
+#ifndef ESLAM_LM_LDSCODES
+#define ESLAM_LM_LDSCODES 0
+#endif
+#ifndef ESLAM_LM_COV
+#define ESLAM_LM_COV 1                   // experiment builds may skip the covered-cell lookups (wrong bits)
+#endif
 template <uint32_t PART>
 __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
                                                              LocalMaps lm, MergeParams mp)
@@ -2355,6 +2364,12 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
         if constexpr (NCH == 1) reinterpret_cast<uint4*>(&s_code[pl][0])[l] = c4[0];
         wave_sync();
+#if ESLAM_LM_LDSCODES
+        auto code = [&](uint32_t u) -> uint32_t {
+            const uint32_t k = l + kLmLanes * u;
+            return k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
+        };
+#elif !defined(ESLAM_LM_NOPACK)
         // two 16-bit codes a register: code(u) is patch l + kLmLanes u
         uint32_t cpk[(PER + 1) / 2];
 #pragma unroll
@@ -2365,6 +2380,15 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
             cpk[v] = c0 | (c1 << 16);
         }
         auto code = [&](uint32_t u) -> uint32_t { return (cpk[u >> 1] >> ((u & 1u) * 16u)) & 0xffffu; };
+#else
+        uint32_t cun[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; ++u) {
+            const uint32_t k = l + kLmLanes * u;
+            cun[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
+        }
+        auto code = [&](uint32_t u) -> uint32_t { return cun[u]; };
+#endif
         // the plan has moved T's window (a moved shared X copied to T): every tile of the scan is
         // in T's slots, and the merge only adds the new pages -- but a shared X whose window
         // stays is copied to T here, the pass's new pages folded in
@@ -2518,11 +2542,27 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 #pragma unroll
                     for (uint32_t w = 0; w < kLmStage; ++w) rr = Ls[w] == (c >> 6) ? w : rr;
                     const uint32_t ci = c & 63u;
+                    // the patch, and for an empty cell the shared grid covers its occupancy word
+                    // and record, are loaded together ahead of the ranks (cells are never emptied)
+                    ScanPatch sp = {};
+                    uint4 gct = make_uint4(0u, 0u, 0u, 0u);
+                    uint32_t gocc = 0;
+                    if (act) {
+                        sp = mp.sp[k];
+                        const float2 cv0 = *reinterpret_cast<const float2*>(stage + lm_stage_off(rr, ci, g));
+                        if (ESLAM_LM_COV && (flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
+                            const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
+                            const uint32_t cm = 8u * (uint32_t)lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx) + (ci & 7u);
+                            const uint32_t cn = 8u * (uint32_t)lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by) + (ci >> 3);
+                            const uint64_t cell = (uint64_t)cn * map.width + cm;
+                            gocc = (map.occ[cell >> 5] >> (cell & 31u)) & 1u;
+                            gct = map.cell_tab[cell];
+                        }
+                    }
                     for (uint32_t rk = 0; rk <= maxr; ++rk) {
                         if (act && rank == rk) {
                             float2* cp = reinterpret_cast<float2*>(stage + lm_stage_off(rr, ci, g));
                             const float2 cv = *cp;
-                            const ScanPatch sp = mp.sp[k];
                             const double wz = sp.z + z;
                             const double var = sp.stdev * sp.stdev + zvar;
                             float mo = cv.x, so = cv.y;
@@ -2530,16 +2570,11 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                             if (dm_lm_holds(cv.y)) {
                                 w = dm_lm_fuse(cv.x, cv.y, wz, var, &mo, &so);
                                 ins = false;
-                            } else if (flags & kJobCovered) {
+                            } else if (gocc) {
                                 // a cell the shared grid covers: the particle's copy starts from
                                 // the grid's patch the 3-sigma gate picks (the oracle alike)
-                                const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
-                                const uint32_t cm = 8u * (uint32_t)lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx) + (ci & 7u);
-                                const uint32_t cn = 8u * (uint32_t)lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by) + (ci >> 3);
-                                const uint64_t cell = (uint64_t)cn * map.width + cm;
                                 double gm, gs;
-                                if (((map.occ[cell >> 5] >> (cell & 31u)) & 1u) &&
-                                    grid_cell_patch(map, map.cell_tab[cell], wz, var, gm, &gs) &&
+                                if (grid_cell_patch(map, gct, wz, var, gm, &gs) &&
                                     dm_lm_fuse((float)gm, (float)gs, wz, var, &mo, &so)) {
                                     ins = false;
                                     covw = true;

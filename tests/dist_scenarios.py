@@ -216,25 +216,13 @@ def run_scenario(f, name, n_global, lo, hi, steps=6, info_fn=None):
         # and map updates then copy on write what each particle changes.  (A resample that
         # migrates many records deep-copies each record's pages: pages two records shared on
         # the sending rank are two copies on the receiving one.)
-        import os
-        import sys
-        dbg = os.environ.get("ESLAM_DEBUG_HEIRLOOM") and hasattr(f, "sync")
-
-        def show(what):
-            if dbg:
-                i = f.sync()
-                sys.stderr.write(f"[{lo}] {what}: taken {i.map_pages_taken} free {i.map_pages_free} "
-                                 f"copied {i.map_stores_copied} changed {i.map_stores_changed}\n")
         f.upload(heirloom_arrays(n_global, lo, hi))
         f.map_update(S.scan_patches(nx=16, ny=12, x0=-2.6, x1=4.6, y0=-2.5, y1=2.4))
-        show("wide")
         f.resample()
         _snap(rec, "res", f, True)
-        show("received")
         _maps(rec, f, hi - lo)
         for k in range(2):                       # the copies on write of the shared received table
             f.map_update(S.scan_patches(x0=0.35 + 0.3 * k))
-            show(f"update {k}")
         rec["maps2/count"] = np.array([len(f.particle_map(g - lo)[0]) for g in range(lo, hi) if g % 97 == 0], np.uint32)
         return rec
     if name == "upload":
