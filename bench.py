@@ -484,8 +484,8 @@ def main():
                            "data_particles": info.data_particles, "window_slots": window_slots(cfg.max_sensor_range, 0.1),
                            "note": "the last step's map update: scan patches beyond a particle's window (farther "
                                    "than maxSensorRange), shared tables a change copied on write, maps the merge "
-                                   "changed, scan patches on cells the shared grid covers (not merged, DESIGN.md "
-                                   "5c), cell writes, pages taken from the pool and left free; data_particles: "
+                                   "changed, scan patches on cells the shared grid covers (merged into the particle's copy "
+                                   "of the grid's cell, DESIGN.md 5c), cell writes, pages taken from the pool and left free; data_particles: "
                                    "the last update's particles whose feet found patches; kernel_ms.map_* time "
                                    "the update's phases (map_cow_ms: the tables' sharing classes and free list, "
                                    "map_plan_ms: the page plan and any collection, map_merge_ms: the merge)"}}

@@ -174,17 +174,18 @@ __device__ __forceinline__ uint32_t jump_pow(const uint32_t* __restrict__ jt, ui
 constexpr uint32_t kStampBlocks = 32768, kStampSlots = 8;
 __device__ uint64_t g_stamps_k1[kStampBlocks][kStampSlots];
 __device__ uint64_t g_stamps_k3[kStampBlocks][kStampSlots];
+__device__ uint64_t g_stamps_mg[kStampBlocks][kStampSlots];   // the map merge (its first group)
 __device__ __forceinline__ uint64_t stamp_now()
 {
     uint64_t t;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
-__device__ uint32_t g_stamps_grid[2];    // gridDim.x of the last stamped K1 / K3 launch
+__device__ uint32_t g_stamps_grid[3];    // gridDim.x of the last stamped K1 / K3 launch
 #define ESLAM_STAMP(arr, k) \
     do { \
         if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) arr[blockIdx.x][(k)] = stamp_now(); \
-        if ((k) == 0 && threadIdx.x == 0 && blockIdx.x == 0) g_stamps_grid[&arr == &g_stamps_k1 ? 0 : 1] = gridDim.x; \
+        if ((k) == 0 && threadIdx.x == 0 && blockIdx.x == 0) g_stamps_grid[&arr == &g_stamps_k1 ? 0 : &arr == &g_stamps_k3 ? 1 : 2] = gridDim.x; \
     } while (0)
 #else
 #define ESLAM_STAMP(arr, k) do { } while (0)
@@ -2310,6 +2311,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
     const bool valid = i < mp.n;
+    ESLAM_STAMP(g_stamps_mg, 0);
     const DevState st = (ctl->base ^ ctl->flip) ? s1 : s0;      // by value: no private copy of the arguments
     // a pending resample gather (mp.fuse, one GPU) runs here instead of in its own launch:
     // output i reads its ancestor (the plan's src) in state[base] and the merge writes the
@@ -2364,6 +2366,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
         if constexpr (NCH == 1) reinterpret_cast<uint4*>(&s_code[pl][0])[l] = c4[0];
         wave_sync();
+        ESLAM_STAMP(g_stamps_mg, 1);
 #if ESLAM_LM_LDSCODES
         auto code = [&](uint32_t u) -> uint32_t {
             const uint32_t k = l + kLmLanes * u;
@@ -2517,7 +2520,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 }
                 __builtin_amdgcn_s_waitcnt(0);
                 wave_sync();
-                uint32_t wbits = 0;           // bit rr: this lane wrote page rr
+                if (pass == 0 && r0 == 0) ESLAM_STAMP(g_stamps_mg, 2);
+                uint32_t wbits = 0;           // bit 8 rr + row: this lane wrote that 64-byte row of page rr
                 // the stage's patches listed in scan order (k = l + kLmLanes u is u-major), then
                 // applied kLmLanes at a time: a round's lanes on one cell go by rank (DPP row
                 // compare), rounds in order -- every cell sees its patches in scan order
@@ -2583,7 +2587,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                             if (ins) { mo = (float)wz; so = (float)dm_sqrt(var); }
                             if (w) {
                                 *cp = make_float2(mo, so);
-                                wbits |= 1u << rr;
+                                wbits |= 1u << (8u * rr + (ci >> 3));
                                 ++written;
                             }
                         }
@@ -2591,19 +2595,25 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     }
                 }
                 wbits = grp_or(wbits);
-                // a page goes back whole when the patches changed it, or when it is new
+                if (pass == 0 && r0 == 0) ESLAM_STAMP(g_stamps_mg, 3);
+                static_assert(kLmStage <= 4 && kLmChunk == 128, "a lane's 16 bytes of a chunk lie in row 2 h + l / 4");
+                // a new page goes back whole; a page the table owns, only the rows the patches changed
 #pragma unroll
                 for (uint32_t rr = 0; rr < kLmStage; ++rr) {
-                    if (Ls[rr] == kLmNoList || (Ds[rr] == Ps[rr] && !((wbits >> rr) & 1u))) continue;
+                    const uint32_t rows = (wbits >> (8u * rr)) & 0xffu;
+                    const bool fresh = Ds[rr] != Ps[rr];
+                    if (Ls[rr] == kLmNoList || (!fresh && !rows)) continue;
                     uint4* dp = reinterpret_cast<uint4*>(lm.page + (uint64_t)Ds[rr] * DM_LM_PAGE_CELLS);
 #pragma unroll
                     for (uint32_t h = 0; h < kLmNq; ++h)
-                        dp[kLmLanes * h + l] = *reinterpret_cast<const uint4*>(stage + (rr * kLmNq + h) * 1024 + (tid & 63u) * 16);
+                        if (fresh || ((rows >> (2u * h + (l >> 2))) & 1u))
+                            dp[kLmLanes * h + l] = *reinterpret_cast<const uint4*>(stage + (rr * kLmNq + h) * 1024 + (tid & 63u) * 16);
                 }
                 dirty = dirty || wbits != 0;
             }
             if (!more) break;
         }
+        ESLAM_STAMP(g_stamps_mg, 4);
         if (shared && dirty) moved = true;
         if ((gath || moved) && l == 0) st.sid[i] = moved ? T : X;
         // the map now holds a copy of a shared-grid cell: its lookups ask its own cells first
@@ -2628,6 +2638,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         if (dmask) atomicAdd((unsigned long long*)&mp.cnt[kMergeCounterSlots + slot_c], (unsigned long long)__popcll(dmask));
         if (mmask) atomicAdd((unsigned long long*)&mp.cnt[2 * kMergeCounterSlots + slot_c], (unsigned long long)__popcll(mmask));
     }
+    ESLAM_STAMP(g_stamps_mg, 5);
 }
 
 // processMap(scanMap, match = true) per particle (the oracle's or_map_match; the rule is the
@@ -4824,24 +4835,27 @@ extern "C" int eslam_debug_k1_occupancy(int* blocks_per_cu, int lds)
 // early then leaves zeros, not an older launch's stamps)
 extern "C" int eslam_gpu_debug_stamps_clear(void)
 {
-    void *a = nullptr, *b = nullptr, *g = nullptr;
+    void *a = nullptr, *b = nullptr, *c = nullptr, *g = nullptr;
     if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_stamps_k1)) != hipSuccess || hipGetSymbolAddress(&b, HIP_SYMBOL(g_stamps_k3)) != hipSuccess ||
-        hipGetSymbolAddress(&g, HIP_SYMBOL(g_stamps_grid)) != hipSuccess)
+        hipGetSymbolAddress(&c, HIP_SYMBOL(g_stamps_mg)) != hipSuccess || hipGetSymbolAddress(&g, HIP_SYMBOL(g_stamps_grid)) != hipSuccess)
         return -1;
     const size_t bytes = sizeof(uint64_t) * kStampBlocks * kStampSlots;
-    if (hipMemset(a, 0, bytes) != hipSuccess || hipMemset(b, 0, bytes) != hipSuccess || hipMemset(g, 0, 8) != hipSuccess) return -1;
+    if (hipMemset(a, 0, bytes) != hipSuccess || hipMemset(b, 0, bytes) != hipSuccess || hipMemset(c, 0, bytes) != hipSuccess ||
+        hipMemset(g, 0, 12) != hipSuccess)
+        return -1;
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
-// copy the stamps of the last K1 (which = 1) or K3 (which = 3) launch; returns that launch's
+// copy the stamps of the last K1 (which = 1), K3 (which = 3) or map merge (which = 5) launch; returns that launch's
 // block count (its grid; blocks past kStampBlocks are not stamped), or -1
 extern "C" int64_t eslam_gpu_debug_stamps(int which, uint64_t* out, uint64_t blocks)
 {
     if (blocks > kStampBlocks) blocks = kStampBlocks;
-    uint32_t grid[2] = {0, 0};
+    uint32_t grid[3] = {0, 0, 0};
     const hipError_t e = which == 1 ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k1), blocks * kStampSlots * 8)
-                                    : hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k3), blocks * kStampSlots * 8);
+                         : which == 3 ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_k3), blocks * kStampSlots * 8)
+                                      : hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_mg), blocks * kStampSlots * 8);
     if (e != hipSuccess || hipMemcpyFromSymbol(grid, HIP_SYMBOL(g_stamps_grid), sizeof(grid)) != hipSuccess) return -1;
-    return (int64_t)grid[which == 1 ? 0 : 1];
+    return (int64_t)grid[which == 1 ? 0 : which == 3 ? 1 : 2];
 }
 #endif

@@ -296,8 +296,8 @@ def test_scan_on_mapped_cells_fuses_with_the_grid(oracle):
 
 
 def test_covered_cells_are_counted(oracle):
-    """Scan patches on cells the shared grid covers are not merged and are
-    counted (map_patches_covered): a scan reaching back over the mapped region x < 0.3."""
+    """Scan patches on cells the shared grid covers go into the particle's copy of the cell
+    (test_scan_on_mapped_cells_fuses_with_the_grid) and are counted (map_patches_covered): a scan reaching back over the mapped region x < 0.3."""
     f, grid = setup(n=200)
     back = S.scan_patches(nx=8, ny=6, x0=-0.6, x1=0.95)
     f.map_update(back)
