@@ -92,8 +92,8 @@ def parse():
     return ap.parse_args()
 
 
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r05", "summary.json")
-PROFILE_SUMMARIES = {"local-maps": os.path.join(ROOT, "profiles", "r05", "summary_local_maps.json")}
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r06", "summary.json")
+PROFILE_SUMMARIES = {"local-maps": os.path.join(ROOT, "profiles", "r06", "summary_local_maps.json")}
 
 
 def pmc_traffic(kernel, n, map_cells, workload):

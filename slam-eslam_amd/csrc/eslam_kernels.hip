@@ -2307,6 +2307,10 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
     __shared__ uint8_t s_list[kLmPpb][PART];                                           // a stage's patches, in scan order
     __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
+    // a small part's patches (z, stdev) in LDS; a large part's are read from memory (its LDS
+    // would cost the kernel a wave)
+    constexpr bool kSpLds = PART <= kScanPartSmall;
+    __shared__ double2 s_sp[kSpLds ? PART : 1];
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
@@ -2343,6 +2347,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         }
         alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
     }
+    // the part's patch heights and deviations, once per block, in the record's round trip
+    for (uint32_t k = tid; kSpLds && k < mp.m && k < PART; k += kLmMergeBlock) s_sp[k] = make_double2(mp.sp[k].z, mp.sp[k].stdev);
     if (gath && valid) {                      // the gather's copies: a field a lane
         for (uint32_t f = l; f < 10; f += kLmLanes) switch (f) {
         case 0: st.w[i] = in.w[src]; break;
@@ -2361,6 +2367,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     bool dirty = false, moved = false, covw = false;
     uint32_t written = 0, taken = 0;
     const bool shared = (flags & kJobShared) != 0;
+    if constexpr (kSpLds) __syncthreads();    // s_sp
     if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
         // ---- 1. the codes: patch k = l + kLmLanes u in lane l (round u precedes round u + 1 in
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
@@ -2548,11 +2555,12 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     const uint32_t ci = c & 63u;
                     // the patch, and for an empty cell the shared grid covers its occupancy word
                     // and record, are loaded together ahead of the ranks (cells are never emptied)
-                    ScanPatch sp = {};
+                    double2 sp = make_double2(0.0, 0.0);
                     uint4 gct = make_uint4(0u, 0u, 0u, 0u);
                     uint32_t gocc = 0;
                     if (act) {
-                        sp = mp.sp[k];
+                        if constexpr (kSpLds) sp = s_sp[k];
+                        else sp = make_double2(mp.sp[k].z, mp.sp[k].stdev);
                         const float2 cv0 = *reinterpret_cast<const float2*>(stage + lm_stage_off(rr, ci, g));
                         if (ESLAM_LM_COV && (flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
                             const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
@@ -2567,8 +2575,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                         if (act && rank == rk) {
                             float2* cp = reinterpret_cast<float2*>(stage + lm_stage_off(rr, ci, g));
                             const float2 cv = *cp;
-                            const double wz = sp.z + z;
-                            const double var = sp.stdev * sp.stdev + zvar;
+                            const double wz = sp.x + z;
+                            const double var = sp.y * sp.y + zvar;
                             float mo = cv.x, so = cv.y;
                             bool w = true, ins = true;
                             if (dm_lm_holds(cv.y)) {

@@ -20,5 +20,7 @@ step bench_16m 300 python bench.py --particles 16777216 --steps 20 --warmup 5 --
 step bench_rough 200 python bench.py --rough --steps 50 --warmup 10 --no-cpu-baseline
 step bench_local_maps 400 python bench.py --local-maps --steps 20 --warmup 5
 step bench_local_maps_steady 300 python bench.py --local-maps --steps 20 --warmup 30 --no-cpu-baseline
+step bench_local_maps_match 300 python bench.py --local-maps --match --steps 20 --warmup 10 --no-cpu-baseline
+step bench_local_maps_600 400 python bench.py --local-maps --scan-patches 600 --map-pages 40 --steps 5 --warmup 3
 step_smoke() { timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 && echo smoke ok || { echo "smoke rc=$?"; tail -5 $out/smoke.log; exit 1; }; }
 step_smoke
