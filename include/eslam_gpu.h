@@ -106,7 +106,10 @@ typedef struct eslam_config {
 #define ESLAM_FLAG_PROCESS_STATICS 0x20u  /* Q11: the hash-respawn counter (the function static
                                               of src/PoseEstimator.cpp:239) and rand() are the
                                               process's, shared by every context that sets this
-                                              flag (default: each context its own)           */
+                                              flag (default: each context its own); one
+                                              sharded (nranks > 1) context per process may
+                                              set it: eslam_gpu_set_comm refuses a second
+                                              (ranks in one process would share them)        */
 
 void eslam_config_default(eslam_config* cfg);
 
@@ -209,7 +212,10 @@ int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx** out);
 void eslam_gpu_destroy(eslam_ctx* ctx);
 /* Collective on a sharded filter (every rank, at the same point): completes the last
  * update's deferred exchange if this rank still owes it, then waits for the stream; on one
- * GPU it only waits for the stream.                                                       */
+ * GPU it only waits for the stream.  A rank whose filter a rank-local fault poisoned (e.g.
+ * ESLAM_ERR_OUT_OF_MEMORY from its page pool) cannot take part: finish returns at once
+ * there, and peers that still owe the exchange would wait for it.  Treat such an error as
+ * fatal for the whole group (abort the communicator), as for any failed collective.       */
 int eslam_gpu_finish(eslam_ctx* ctx);
 const char* eslam_gpu_last_error(const eslam_ctx* ctx);
 int eslam_gpu_abi_version(void);

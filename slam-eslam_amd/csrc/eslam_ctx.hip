@@ -18,6 +18,7 @@
 #include <string>
 #include <chrono>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "eslam_internal.h"
@@ -259,6 +260,10 @@ static ProcessStatics& process_statics()
     static ProcessStatics ps;
     return ps;
 }
+// sharded contexts of this process with the flag: at most one.  Ranks driven from one process
+// would advance the shared counter once each per step and draw each other's rand() values, so
+// their respawns and hash indices would disagree (eslam_gpu_set_comm refuses a second one)
+static std::atomic<int> g_statics_sharded{0};
 
 struct eslam_ctx {
     eslam_config cfg;
@@ -334,6 +339,7 @@ struct eslam_ctx {
     double zcomp[4] = {1, 0, 0, 0};
     // multi-GPU (eslam_gpu_set_comm): this context is shard [gbase, gbase + n) of n_global
     bool sharded = false;
+    bool statics_sharded = false;            // counted in g_statics_sharded
     eslam_comm comm = {};
     std::vector<uint64_t> gall;             // first global index of every rank (+ n_global)
     Shard* recs = nullptr;                  // gathered records of all ranks
@@ -715,6 +721,8 @@ extern "C" void eslam_gpu_destroy(eslam_ctx* ctx)
     // collective that completes it); destroy may run on an error path of one rank or after the
     // caller's communicator is gone, so it must not wait for the other ranks
     ctx->xpend = false;
+    if (ctx->statics_sharded) g_statics_sharded.fetch_sub(1);
+    ctx->statics_sharded = false;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->xstream) { (void)hipStreamSynchronize(ctx->xstream); (void)hipStreamDestroy(ctx->xstream); }
     if (ctx->ev_seg) (void)hipEventDestroy(ctx->ev_seg);
@@ -978,6 +986,8 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
     if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     free_particles(ctx);
+    if (ctx->statics_sharded) g_statics_sharded.fetch_sub(1);
+    ctx->statics_sharded = false;
     if (!comm) {
         ctx->sharded = false;
         ctx->gall.clear();
@@ -1017,6 +1027,15 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
             HIPCHK(ctx, hipMalloc(&ctx->cent, need));
             ctx->cent_bytes = need;
         }
+    }
+    if ((ctx->cfg.flags & ESLAM_FLAG_PROCESS_STATICS) && comm->nranks > 1) {
+        if (g_statics_sharded.fetch_add(1) != 0) {
+            g_statics_sharded.fetch_sub(1);
+            return fail(ctx, ESLAM_ERR_INVALID_ARG,
+                        "eslam_gpu_set_comm: ESLAM_FLAG_PROCESS_STATICS allows one sharded context per process "
+                        "(ranks in one process would share the respawn counter and rand())");
+        }
+        ctx->statics_sharded = true;
     }
     ctx->comm = *comm;
     ctx->sharded = true;

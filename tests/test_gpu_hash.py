@@ -120,3 +120,32 @@ def test_process_statics_shared_between_contexts(gpu_mod):
     assert sa.libc_rand_pos == sb.libc_rand_pos == ob.rng_state().libc_rand_pos
     ga.close()
     gb.close()
+
+
+def test_process_statics_one_sharded_context_per_process(gpu_mod):
+    """ESLAM_FLAG_PROCESS_STATICS with ranks in one process: two rank contexts would share the
+    respawn counter and rand() and their collectives would diverge, so eslam_gpu_set_comm
+    refuses the second one (ESLAM_ERR_INVALID_ARG); returning the first context to one GPU
+    (comm == NULL) frees the place.  set_comm itself runs no exchange, so the callbacks here
+    are never called."""
+    import ctypes as C
+    import eslam_abi as A
+    n = 4096
+    cfg = hash_config(n, steps=4, bins=20, period=3)
+    cfg.flags |= A.FLAG_PROCESS_STATICS
+
+    def never(*args):
+        raise AssertionError("set_comm ran a collective")
+    ag, a2a = A.ALLGATHER_FN(never), A.ALLTOALLV_FN(never)
+    bounds = A.shard_bounds(n, 2)
+    gb = (C.c_uint64 * len(bounds))(*bounds)
+    fa, fb = gpu_mod.GpuFilter(cfg), gpu_mod.GpuFilter(cfg)
+    ca, cb = A.Comm(None, 0, 2, 0, 0, ag, a2a), A.Comm(None, 1, 2, 0, 0, ag, a2a)
+    assert fa.L.eslam_gpu_set_comm(fa.h, C.byref(ca), n, gb) == 0
+    assert fb.L.eslam_gpu_set_comm(fb.h, C.byref(cb), n, gb) == A.ERR_INVALID_ARG
+    assert "PROCESS_STATICS" in fb.L.eslam_gpu_last_error(fb.h).decode()
+    assert fa.L.eslam_gpu_set_comm(fa.h, None, 0, None) == 0
+    assert fb.L.eslam_gpu_set_comm(fb.h, C.byref(cb), n, gb) == 0
+    assert fb.L.eslam_gpu_set_comm(fb.h, None, 0, None) == 0
+    fa.close()
+    fb.close()
