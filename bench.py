@@ -342,6 +342,11 @@ def main():
         cfg.flags |= A.FLAG_PARTICLE_MAPS
         cfg.local_map_pages = args.map_pages
     if sharded:
+        # the summation chunk sized by the rank's own particles (eslam_config.sum_chunk_rows):
+        # every rank's weighting kernel fills the chip whatever the rank count (4M a rank: 13
+        # rows, as on one GPU; configs[3]'s 2M a rank: 7 instead of the 16M's 13)
+        cfg.sum_chunk_rows = A.chunk_rows(n)
+    if sharded:
         # one global filter of n * world particles, sharded over the ranks: RCCL all_gathers
         # of the statistics / totals / counts and an all_to_all_v of the migrating particles
         import eslam_dist

@@ -1726,6 +1726,12 @@ DM_FN uint32_t dm_chunk_rows(uint64_t n_global)
     return j < 1 ? 1u : (uint32_t)j;
 }
 
+/* eslam_config::sum_chunk_rows when set, else dm_chunk_rows(n_global) */
+DM_FN uint32_t dm_chunk_rows_cfg(uint64_t n_global, uint32_t fixed)
+{
+    return fixed ? fixed : dm_chunk_rows(n_global);
+}
+
 /* exponent e >= 1 with max_w < 2^e (weight scale of the A_n / B_n accumulators) */
 DM_FN int dm_weight_exp(double max_w)
 {

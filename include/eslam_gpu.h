@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ESLAM_ABI_VERSION 7
+#define ESLAM_ABI_VERSION 8
 
 /* maximum number of contact points of one BodyContactState handled per step
  * (asguard: 4 wheels x 5 feet = 20, src/ContactModel.cpp grouping) */
@@ -92,7 +92,12 @@ typedef struct eslam_config {
      * to this many per map (default 16; 0: tiles leaving the window are forgotten).  Their
      * pages come from the same pool (local_map_pages).                                       */
     uint32_t local_map_trail;
-    uint32_t pad_trail;
+    /* rows of 64 particles per canonical summation chunk (ABI 8; 0: dm_chunk_rows(n_global),
+     * the default).  The chunk fixes the order of the fp64 partial sums, so two
+     * filters agree bit for bit only with the same value.  A sharded filter of G ranks may set
+     * dm_chunk_rows(n_global / G) so that every rank's weighting kernel fills the chip (16M
+     * over 8 ranks: 7 instead of 13); its one-GPU equal then sets the same.  At most 31.     */
+    uint32_t sum_chunk_rows;
 } eslam_config;
 
 #define ESLAM_FLAG_RECORD_ANCESTORS 0x1u   /* keep the last resample's ancestor indices     */

@@ -280,6 +280,7 @@ struct Configuration {
     uint32_t flags = 0;                   // build-specific ESLAM_FLAG_* (not in the reference)
     uint32_t localMapPages = 0;           // build-specific: per-particle map page pool per particle (0: 16)
     uint32_t localMapTrail = 16;          // build-specific: tiles a particle's map keeps behind its window
+    uint32_t sumChunkRows = 0;            // build-specific: eslam_config::sum_chunk_rows (0: by particle count)
 
     // the fields the MI355X path consumes, as the C ABI's POD (hash: the init() argument)
     eslam_config toC(const SurfaceHashConfig& hash = SurfaceHashConfig()) const
@@ -318,6 +319,7 @@ struct Configuration {
         c.max_sensor_range = maxSensorRange;       // the reach of a particle's own map
         c.local_map_pages = localMapPages;
         c.local_map_trail = localMapTrail;
+        c.sum_chunk_rows = sumChunkRows;
         return c;
     }
 };

@@ -1458,7 +1458,7 @@ static int or_update_weights(or_filter* f, const eslam_step_input* in, or_phase*
     /* reference mode: the sequential sum in particle order (non-data particles add +0.0) */
     for (uint64_t i = 0; i < f->n; ++i) sum_data_weights += sw_val[i];
 
-    const uint32_t J = dm_chunk_rows(NG(f));
+    const uint32_t J = dm_chunk_rows_cfg(NG(f), f->cfg.sum_chunk_rows);
     /* contract mode: every exact partial sum of the update; sharded filters combine them
      * across ranks in one exchange (the device's per-rank statistics record) */
     or_acc accs[2 * DM_NBUCKETS + 1];
@@ -1532,7 +1532,7 @@ static double normalize_with(or_filter* f, double S, double Q, int have_sums)
             S = 0;
             for (uint64_t i = 0; i < n; ++i) S += f->w[OD(i)];
         } else {
-            const uint32_t J = dm_chunk_rows(N);
+            const uint32_t J = dm_chunk_rows_cfg(N, f->cfg.sum_chunk_rows);
             int e = f->wexp;
             double* w2 = malloc(n * 8 + 8);
             for (uint64_t i = 0; i < n; ++i) w2[i] = f->w[OD(i)] * f->w[OD(i)];
@@ -1577,7 +1577,7 @@ double or_get_weights_sum(or_filter* f)
         return s;
     }
     or_acc A = {{0}};
-    chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
+    chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, f->n, dm_chunk_rows_cfg(NG(f), f->cfg.sum_chunk_rows), &A, DM_FX_SCALE - f->wexp);
     combine_accs(f, &A, 1);
     return acc_value(&A, DM_FX_SCALE - f->wexp);
 }
@@ -1874,7 +1874,7 @@ int or_set_comm(or_filter* f, const eslam_comm* comm, uint64_t n_global, const u
     or_free_particles(f);
     if (!comm) { f->sharded = 0; f->n_global = 0; f->gbase = 0; return 0; }
     if (comm->device_memory || comm->nranks < 1 || comm->nranks > ESLAM_ORACLE_MAX_RANKS) return ESLAM_ERR_INVALID_ARG;
-    const uint64_t csz = 64ull * dm_chunk_rows(n_global);
+    const uint64_t csz = 64ull * dm_chunk_rows_cfg(n_global, f->cfg.sum_chunk_rows);
     if (shard_gbase[0] != 0 || shard_gbase[comm->nranks] != n_global) return ESLAM_ERR_INVALID_ARG;
     for (int r = 0; r < comm->nranks; ++r)
         if (shard_gbase[r + 1] <= shard_gbase[r] || shard_gbase[r] % csz) return ESLAM_ERR_INVALID_ARG;
@@ -1893,7 +1893,7 @@ void or_resample(or_filter* f)
     int shift = 60;
     if (f->sum_mode == OR_SUM_CONTRACT) {
         or_acc A = {{0}};
-        chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, f->n, dm_chunk_rows(NG(f)), &A, DM_FX_SCALE - f->wexp);
+        chunk_reduce(f->w, OR_DSTRIDE, NULL, 0, f->n, dm_chunk_rows_cfg(NG(f), f->cfg.sum_chunk_rows), &A, DM_FX_SCALE - f->wexp);
         combine_accs(f, &A, 1);
         shift = 61 - (dm_weight_exp(acc_value(&A, DM_FX_SCALE - f->wexp)) + 1);
     }
@@ -1992,7 +1992,7 @@ uint64_t or_best_index(or_filter* f)
  * chunk records (the shards are chunk-aligned), so every rank gets the one-filter sums.    */
 static void centroid_contract(or_filter* f, double out[5])
 {
-    const uint32_t J = dm_chunk_rows(NG(f));
+    const uint32_t J = dm_chunk_rows_cfg(NG(f), f->cfg.sum_chunk_rows);
     const uint64_t csz = 64ull * J;
     const uint64_t nch = (f->n + csz - 1) / csz;
     int G = f->sharded ? f->comm.nranks : 1;

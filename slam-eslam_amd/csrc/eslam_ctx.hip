@@ -589,6 +589,8 @@ extern "C" int eslam_gpu_create(const eslam_config* cfg, int device, eslam_ctx**
     set_translation_pose(ctx->ud_pose, 1000, 0, 0);
     int rc = ESLAM_OK;
     do {
+        // nD <= 64 J and the contact points <= ESLAM_MAX_CONTACTS nD share one 32-bit word (K1)
+        if (cfg->sum_chunk_rows > 31) { rc = fail(ctx, ESLAM_ERR_INVALID_ARG, "sum_chunk_rows: at most 31"); break; }
         hipError_t e = hipSetDevice(device);
         if (e != hipSuccess) { ctx->err = std::string("hipSetDevice: ") + hipGetErrorString(e); rc = ESLAM_ERR_HIP; break; }
         if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { rc = fail(ctx, ESLAM_ERR_HIP, "stream"); break; }
@@ -962,7 +964,7 @@ static PlanParams plan_params(eslam_ctx* ctx)
     for (int r = 0; r <= ctx->comm.nranks; ++r) pp.gbase[r] = ctx->gall[r];
     pp.chunk_sel = ctx->mg + mg::kChunks;
     pp.n_local = ctx->n;
-    pp.J = dm_chunk_rows(ctx->n_global);
+    pp.J = dm_chunk_rows_cfg(ctx->n_global, ctx->cfg.sum_chunk_rows);
     return pp;
 }
 
@@ -1000,7 +1002,7 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: bad communicator (1 <= nranks <= 16)");
     if (n_global == 0 || n_global > (1ull << 30) - 64)     // resample mark encoding (kMarkOwn)
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: n_global must be in [1, 2^30 - 64]");
-    const uint64_t csz = 64ull * dm_chunk_rows(n_global);
+    const uint64_t csz = 64ull * dm_chunk_rows_cfg(n_global, ctx->cfg.sum_chunk_rows);
     if (shard_gbase[0] != 0 || shard_gbase[comm->nranks] != n_global)
         return fail(ctx, ESLAM_ERR_INVALID_ARG, "eslam_gpu_set_comm: shard_gbase must run from 0 to n_global");
     for (int r = 0; r < comm->nranks; ++r) {
@@ -1019,7 +1021,7 @@ extern "C" int eslam_gpu_set_comm(eslam_ctx* ctx, const eslam_comm* comm, uint64
     {
         // getCentroid's buffer (centroid_bytes): sized by the shard table, allocated here so
         // the per-step getCentroid of a Rock task allocates nothing
-        const uint64_t need = centroid_bytes(shard_gbase, comm->nranks, dm_chunk_rows(n_global));
+        const uint64_t need = centroid_bytes(shard_gbase, comm->nranks, dm_chunk_rows_cfg(n_global, ctx->cfg.sum_chunk_rows));
         if (need > ctx->cent_bytes) {
             (void)hipFree(ctx->cent);
             ctx->cent = nullptr;
@@ -2069,7 +2071,7 @@ static void fill_step_params(eslam_ctx* ctx, const eslam_step_input* in, StepPar
     p.n = ctx->n;
     p.gbase = ctx->gbase;
     p.n_global = ctx->n_global;
-    p.J = dm_chunk_rows(ctx->n_global);
+    p.J = dm_chunk_rows_cfg(ctx->n_global, ctx->cfg.sum_chunk_rows);
 }
 
 // particles per thread of the one-GPU K3: small filters take small tiles so the scan still
@@ -2765,7 +2767,7 @@ static int standalone(eslam_ctx* ctx, uint32_t mode)
     if (check_poisoned(ctx)) return ESLAM_ERR_HIP;
     const int rc = materialize(ctx);
     if (rc) return rc;
-    const uint32_t J = dm_chunk_rows(ctx->n_global);
+    const uint32_t J = dm_chunk_rows_cfg(ctx->n_global, ctx->cfg.sum_chunk_rows);
     HIPCHK(ctx, eslam_launch_weight_stats(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->shards, ctx->stream));
     if (mode == FIN_SUM && !ctx->sharded) {
         const FinParams fp = fin_params(ctx, mode);
@@ -2846,7 +2848,7 @@ extern "C" int eslam_gpu_get_centroid(eslam_ctx* ctx, double position[3], double
     if (const int rc_ = settle(ctx)) return rc_;    // a deferred sharded exchange first
     int rc = eslam_gpu_normalize_weights(ctx, nullptr);     // side effect, Q15
     if (rc) return rc;
-    const uint32_t J = dm_chunk_rows(ctx->n_global);
+    const uint32_t J = dm_chunk_rows_cfg(ctx->n_global, ctx->cfg.sum_chunk_rows);
     if (!ctx->sharded) {
         HIPCHK(ctx, eslam_launch_centroid(ctx->st[0], ctx->st[1], ctx->n, J, ctx->ctl, ctx->scratch, ctx->stream));
     } else {

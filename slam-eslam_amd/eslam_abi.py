@@ -58,7 +58,7 @@ class Config(C.Structure):
         ("local_map_pages", C.c_uint32),
         ("max_sensor_range", C.c_double),
         ("local_map_trail", C.c_uint32),
-        ("pad_trail", C.c_uint32),
+        ("sum_chunk_rows", C.c_uint32),
     ]
 
 
@@ -230,19 +230,23 @@ MAX_RANKS = 16
 CHUNK_WAVES, CHUNK_CAP = 5120, 13
 
 
-def chunk_rows(n_global):
-    """dm_chunk_rows (include/eslam_detmath.h): rows of 64 lanes per canonical summation chunk,
-    sized to whole generations of the weighting kernel's resident waves."""
+def chunk_rows(n_global, fixed=0):
+    """dm_chunk_rows_cfg (include/eslam_detmath.h): rows of 64 lanes per canonical summation
+    chunk -- eslam_config.sum_chunk_rows when set (`fixed`), else sized to whole generations of
+    the weighting kernel's resident waves."""
+    if fixed:
+        return int(fixed)
     rows = (n_global + 63) // 64
     per = CHUNK_WAVES * CHUNK_CAP
     slots = (1 if rows <= per else -(-rows // per)) * CHUNK_WAVES
     return max(1, -(-rows // slots))
 
 
-def shard_bounds(n_global, nranks):
+def shard_bounds(n_global, nranks, fixed=0):
     """First global index of every rank (+ n_global): near-equal shards whose starts are
-    multiples of the summation chunk (64 * chunk_rows), as eslam_gpu_set_comm requires."""
-    csz = 64 * chunk_rows(n_global)
+    multiples of the summation chunk (64 * chunk_rows; `fixed`: eslam_config.sum_chunk_rows),
+    as eslam_gpu_set_comm requires."""
+    csz = 64 * chunk_rows(n_global, fixed)
     chunks = -(-n_global // csz)
     if chunks < nranks:
         raise ValueError(f"{n_global} particles cannot be split into {nranks} chunk-aligned shards")
@@ -286,6 +290,7 @@ def default_config(lib=None):
     c.local_map_pages = 0
     c.max_sensor_range = 3.0
     c.local_map_trail = 16
+    c.sum_chunk_rows = 0
     return c
 
 

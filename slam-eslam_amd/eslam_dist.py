@@ -119,7 +119,7 @@ class ShardedGpuFilter:
     def __init__(self, cfg, n_global, comm, device=0):
         import eslam_amd
         self.comm = comm
-        self.bounds = A.shard_bounds(n_global, comm.nranks)
+        self.bounds = A.shard_bounds(n_global, comm.nranks, cfg.sum_chunk_rows)
         cfg.particle_count = n_global
         self.f = eslam_amd.GpuFilter(cfg, device=device)
         if comm.device_memory:
@@ -153,7 +153,7 @@ class RcclShardedGpuFilter:
         import torch.distributed as dist
         import eslam_amd
         L = eslam_amd.load_library()
-        self.bounds = A.shard_bounds(n_global, nranks)
+        self.bounds = A.shard_bounds(n_global, nranks, cfg.sum_chunk_rows)
         cfg.particle_count = n_global
         self.f = eslam_amd.GpuFilter(cfg, device=device)
         uid = (C.c_uint8 * 128)()

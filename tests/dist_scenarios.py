@@ -10,7 +10,7 @@ import eslam_abi as A
 import synthetic as S
 
 FIELDS = ("x", "y", "orientation", "zpos", "zsigma", "weight", "mprob", "floating", "n_contact_points")
-SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit", "records", "heirloom")
+SCENARIOS = ("forced", "natural", "upload", "hash", "config3", "config4", "maps", "edit", "records", "heirloom", "chunks")
 EDIT_GLOBAL = (0, 37)                            # edit: the particles one rank edits
 CONFIG3_STEPS = 3
 MAP_SAMPLES = 64                                 # config4: particles whose maps are compared
@@ -26,8 +26,15 @@ def scenario_config(name, n_global):
     cfg = A.default_config()
     cfg.seed = 1234
     cfg.flags |= A.FLAG_RECORD_ANCESTORS
-    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0", "records", "heirloom"):
+    if name in ("forced", "config3", "config4", "maps", "burst", "edit", "getter0", "records", "heirloom", "chunks"):
         S.bench_config(cfg, n_global)
+        if name == "chunks":                     # an explicit summation chunk (eslam_config.sum_chunk_rows)
+            cfg.sum_chunk_rows = 3
+        if name == "config3":
+            # the chunk a sharded configs[3] uses: sized by the 2M of one of its 8 ranks (7 rows),
+            # so that each rank's weighting kernel fills the chip (13 rows from the 16M would
+            # leave half of it idle: K1 +24 % per rank, profiles/r06/ab/ab_r06r_chunk_rows.log)
+            cfg.sum_chunk_rows = A.chunk_rows(-(-n_global // 8))
         if name == "records":                    # logDebug: every update's contact points
             cfg.flags |= A.FLAG_RECORD_CONTACTS
         if name in ("maps", "config4", "heirloom"):   # useSharedMap = false: per-particle maps

@@ -37,7 +37,7 @@ def main():
         dist.init_process_group("gloo", **init)
     comm = eslam_dist.TorchComm(device_memory=(mem in ("device", "rccl")))
     cfg = scenario_config(name, n_global)
-    bounds = A.shard_bounds(n_global, comm.nranks)
+    bounds = A.shard_bounds(n_global, comm.nranks, cfg.sum_chunk_rows)
     lo, hi = bounds[rank], bounds[rank + 1]
     if kind == "oracle":
         import oracle_ffi as O

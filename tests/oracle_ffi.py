@@ -163,7 +163,7 @@ class OracleFilter:
     def set_comm(self, comm, n_global):
         """Sharded mode over a host-memory eslam_comm (slam-eslam_amd/eslam_dist.TorchComm)."""
         self._comm = comm
-        self.bounds = A.shard_bounds(n_global, comm.nranks)
+        self.bounds = A.shard_bounds(n_global, comm.nranks, self.cfg.sum_chunk_rows)
         self._gb = (C.c_uint64 * len(self.bounds))(*self.bounds)
         rc = self.L.or_set_comm(self.h, C.byref(comm.struct), n_global, self._gb)
         assert rc == 0, rc

@@ -50,7 +50,7 @@ def test_library_built_from_these_sources(lib):
 
 def test_abi_version(lib):
     lib.eslam_gpu_abi_version.restype = C.c_int
-    assert lib.eslam_gpu_abi_version() == 7
+    assert lib.eslam_gpu_abi_version() == 8
 
 
 def test_config_default_matches_reference_defaults(lib):

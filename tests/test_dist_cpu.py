@@ -76,7 +76,8 @@ def single_oracle(name, n_global):
                                                  ("forced", 1000, 3), ("upload", 700, 3), ("hash", 2000, 2),
                                                  ("hash", 1500, 3), ("maps", 3000, 2), ("maps", 1500, 3),
                                                  ("burst", 3000, 2), ("edit", 3000, 2), ("edit", 1000, 3),
-                                                 ("heirloom", 2000, 2), ("heirloom", 1500, 3)])
+                                                 ("heirloom", 2000, 2), ("heirloom", 1500, 3),
+                                                 ("chunks", 3000, 2), ("chunks", 1500, 3)])
 def test_sharded_oracle_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("oracle", name, n_global, world, str(tmp_path)))

@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
                                                  ("upload", 700, 3), ("hash", 3000, 2), ("hash", 1500, 3),
                                                  ("maps", 3000, 2), ("maps", 1500, 3),
                                                  ("burst", 5000, 2), ("burst", 7001, 3), ("edit", 3000, 2),
-                                                 ("edit", 1500, 3), ("heirloom", 2000, 2), ("heirloom", 1500, 3)])
+                                                 ("edit", 1500, 3), ("heirloom", 2000, 2), ("heirloom", 1500, 3),
+                                                 ("chunks", 3000, 2), ("chunks", 1500, 3)])
 def test_sharded_gpu_gloo_equals_single(oracle, tmp_path, name, n_global, world):
     want = single_oracle(name, n_global)
     got = merge(launch("gpu", name, n_global, world, str(tmp_path), mem="host", timeout=400))
@@ -89,7 +90,7 @@ def test_sharded_gpu_two_row_chunks(oracle, tmp_path, mem, world):
 @pytest.mark.timeout(1200)
 def test_config3_eight_ranks_equal_single_context(oracle, tmp_path):
     """BASELINE configs[3]'s decomposition on one GPU: 16M particles as 8 ranks x 2M (gloo,
-    host staging; the ranks share the card), 3 steps of the bench workload with a forced
+    host staging; the ranks share the card; the summation chunk sized by a rank), 3 steps of the bench workload with a forced
     resample each.  Every rank's shard equals the same slice of ONE 16M-particle context bit
     for bit (all fields, the last resample's ancestors as global indices), every rank reports
     the single context's update info, best index and RNG state, and the single context's last
@@ -100,9 +101,11 @@ def test_config3_eight_ranks_equal_single_context(oracle, tmp_path):
     from parity_util import check_resample_properties
     n_global, world = 16 * 1024 * 1024, 8
     parts = launch("gpu", "config3", n_global, world, str(tmp_path), mem="host", timeout=900)
-    f = eslam_amd.GpuFilter(scenario_config("config3", n_global))
+    cfg = scenario_config("config3", n_global)
+    assert cfg.sum_chunk_rows == 7                 # sized by a rank's 2M (dm_chunk_rows(16M) = 13)
+    f = eslam_amd.GpuFilter(cfg)
     rec, fields, anc, best, rng = run_config3(f, n_global, 0, n_global, info_fn=lambda g: g.sync())
-    bounds = A.shard_bounds(n_global, world)
+    bounds = A.shard_bounds(n_global, world, cfg.sum_chunk_rows)
     for r, p in enumerate(parts):
         lo, hi = bounds[r], bounds[r + 1]
         assert tuple(p["range"]) == (lo, hi)
@@ -137,9 +140,10 @@ def test_config4_eight_ranks_equal_single_context(oracle, tmp_path):
     from parity_util import check_resample_properties
     n_global, world = 64 * 1024 * 1024, 8
     parts = launch("gpu", "config4", n_global, world, str(tmp_path), mem="host", timeout=1200)
-    f = eslam_amd.GpuFilter(scenario_config("config4", n_global))
+    cfg = scenario_config("config4", n_global)
+    f = eslam_amd.GpuFilter(cfg)
     rec, fields, anc, best, rng = run_config3(f, n_global, 0, n_global, info_fn=lambda g: g.sync(), name="config4")
-    bounds = A.shard_bounds(n_global, world)
+    bounds = A.shard_bounds(n_global, world, cfg.sum_chunk_rows)
     seen = 0
     for r, p in enumerate(parts):
         lo, hi = bounds[r], bounds[r + 1]
