@@ -2290,12 +2290,6 @@ __device__ __forceinline__ uint32_t lm_stage_off(uint32_t rr, uint32_t ci, uint3
 #ifndef ESLAM_LM_WPE_LARGE
 #define ESLAM_LM_WPE_LARGE 3
 #endif
-#ifndef ESLAM_LM_LDSCODES
-#define ESLAM_LM_LDSCODES 0
-#endif
-#ifndef ESLAM_LM_COV
-#define ESLAM_LM_COV 1                   // experiment builds may skip the covered-cell lookups (wrong bits)
-#endif
 template <uint32_t PART>
 __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevState s0, DevState s1, Ctl* __restrict__ ctl, MapView map,
                                                              LocalMaps lm, MergeParams mp)
@@ -2374,13 +2368,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         if constexpr (NCH == 1) reinterpret_cast<uint4*>(&s_code[pl][0])[l] = c4[0];
         wave_sync();
         ESLAM_STAMP(g_stamps_mg, 1);
-#if ESLAM_LM_LDSCODES
-        auto code = [&](uint32_t u) -> uint32_t {
-            const uint32_t k = l + kLmLanes * u;
-            return k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
-        };
-#elif !defined(ESLAM_LM_NOPACK)
-        // two 16-bit codes a register: code(u) is patch l + kLmLanes u
+        // two 16-bit codes a register: code(u) is patch l + kLmLanes u (round 6: against one
+        // code a register and against reading them from LDS, profiles/r06/ab/ab_r06k*, ab_r06l*)
         uint32_t cpk[(PER + 1) / 2];
 #pragma unroll
         for (uint32_t v = 0; v < (PER + 1) / 2; ++v) {
@@ -2390,15 +2379,6 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
             cpk[v] = c0 | (c1 << 16);
         }
         auto code = [&](uint32_t u) -> uint32_t { return (cpk[u >> 1] >> ((u & 1u) * 16u)) & 0xffffu; };
-#else
-        uint32_t cun[PER];
-#pragma unroll
-        for (uint32_t u = 0; u < PER; ++u) {
-            const uint32_t k = l + kLmLanes * u;
-            cun[u] = k < mp.m ? (uint32_t)s_code[pl][k] : (uint32_t)kCodeSkip;
-        }
-        auto code = [&](uint32_t u) -> uint32_t { return cun[u]; };
-#endif
         // the plan has moved T's window (a moved shared X copied to T): every tile of the scan is
         // in T's slots, and the merge only adds the new pages -- but a shared X whose window
         // stays is copied to T here, the pass's new pages folded in
@@ -2562,7 +2542,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                         if constexpr (kSpLds) sp = s_sp[k];
                         else sp = make_double2(mp.sp[k].z, mp.sp[k].stdev);
                         const float2 cv0 = *reinterpret_cast<const float2*>(stage + lm_stage_off(rr, ci, g));
-                        if (ESLAM_LM_COV && (flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
+                        if ((flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
                             const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
                             const uint32_t cm = 8u * (uint32_t)lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx) + (ci & 7u);
                             const uint32_t cn = 8u * (uint32_t)lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by) + (ci >> 3);
