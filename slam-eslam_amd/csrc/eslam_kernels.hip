@@ -2135,7 +2135,9 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
     // a small part's codes leave through LDS (then the records); a large part's go straight to
     // the rows (their LDS would cost the kernel its occupancy)
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kScanPartSmall * kLmBlock];
-    __shared__ uint32_t s_w[kLmBlock / 64];
+    // the block sums' words alias the codes: the block holds exactly 16 KiB of LDS (a 17th
+    // granule cost it a block per CU)
+    uint32_t* s_w = reinterpret_cast<uint32_t*>(s_code);
     static_assert(sizeof(MergeJob) * kLmBlock <= sizeof(uint16_t) * kScanPartSmall * kLmBlock, "records in s_code");
     constexpr bool kSmall = PART == kScanPartSmall;
     const uint32_t tid = threadIdx.x;
@@ -2255,6 +2257,7 @@ __global__ void __launch_bounds__(kLmBlock) k_map_plan(DevState s0, DevState s1,
         if (covered) atomicAdd((unsigned long long*)&mp.cnt[3 * kMergeCounterSlots + slot_c], (unsigned long long)covered);
         if (forgot) atomicAdd((unsigned long long*)&mp.cnt[6 * kMergeCounterSlots + slot_c], (unsigned long long)forgot);
     }
+    __syncthreads();                          // every record has left s_code (s_w aliases it)
     block_offsets(need, i < mp.n, mp.off + (i - tid), mp.poff + blockIdx.x, s_w);
 }
 
@@ -2301,10 +2304,6 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
     __shared__ uint8_t s_list[kLmPpb][PART];                                           // a stage's patches, in scan order
     __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
-    // a small part's patches (z, stdev) in LDS; a large part's are read from memory (its LDS
-    // would cost the kernel a wave)
-    constexpr bool kSpLds = PART <= kScanPartSmall;
-    __shared__ double2 s_sp[kSpLds ? PART : 1];
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
@@ -2341,8 +2340,6 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         }
         alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
     }
-    // the part's patch heights and deviations, once per block, in the record's round trip
-    for (uint32_t k = tid; kSpLds && k < mp.m && k < PART; k += kLmMergeBlock) s_sp[k] = make_double2(mp.sp[k].z, mp.sp[k].stdev);
     if (gath && valid) {                      // the gather's copies: a field a lane
         for (uint32_t f = l; f < 10; f += kLmLanes) switch (f) {
         case 0: st.w[i] = in.w[src]; break;
@@ -2361,7 +2358,6 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     bool dirty = false, moved = false, covw = false;
     uint32_t written = 0, taken = 0;
     const bool shared = (flags & kJobShared) != 0;
-    if constexpr (kSpLds) __syncthreads();    // s_sp
     if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
         // ---- 1. the codes: patch k = l + kLmLanes u in lane l (round u precedes round u + 1 in
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
@@ -2539,8 +2535,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     uint4 gct = make_uint4(0u, 0u, 0u, 0u);
                     uint32_t gocc = 0;
                     if (act) {
-                        if constexpr (kSpLds) sp = s_sp[k];
-                        else sp = make_double2(mp.sp[k].z, mp.sp[k].stdev);
+                        sp = make_double2(mp.sp[k].z, mp.sp[k].stdev);
                         const float2 cv0 = *reinterpret_cast<const float2*>(stage + lm_stage_off(rr, ci, g));
                         if ((flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
                             const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
