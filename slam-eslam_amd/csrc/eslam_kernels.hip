@@ -3300,6 +3300,15 @@ __device__ __forceinline__ void flush_marks(uint32_t* __restrict__ marks, uint32
     }
 }
 
+// one segment's start mark and row carries (flush_marks for a single item)
+__device__ __forceinline__ void flush_mark(uint32_t* __restrict__ marks, uint32_t* __restrict__ tile_first, uint64_t lo,
+                                           uint64_t hi, uint32_t val)
+{
+    if (hi <= lo) return;
+    marks[lo] = val;
+    for (uint64_t t = (lo + kRow - 1) / kRow; t * kRow < hi; ++t) tile_first[t] = val - 1u;
+}
+
 constexpr uint64_t kPubMask = (1ull << 61) - 1;
 
 // a tile's word into every replica (ScanParams::pub_stride), one lane each.  The sharded K3a
@@ -3722,25 +3731,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ITE
     wave_counts<ITEMS>(base, run, c, N, shift, xs, jt, s_u.T[wave], hi_r, lo);
     ESLAM_STAMP(g_stamps_k3, 6);
     if (i0 == 0) lo = 0;
-    uint64_t seg_lo[ITEMS], seg_hi[ITEMS];
-    uint32_t val[ITEMS];
+    // each item's segment [lo, hi) marked as it is found (no arrays of segments held)
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const uint64_t i = i0 + r;
-        seg_lo[r] = seg_hi[r] = 0;
-        val[r] = (uint32_t)(i + 1);
         if (i < sp.n) {
             uint64_t hi = hi_r[r];
             if (i == N - 1) {
                 if (hi < N) atomicAdd((unsigned long long*)&ctl->overruns, (unsigned long long)(N - hi));
                 hi = N;
             }
-            seg_lo[r] = lo;
-            seg_hi[r] = hi;
+            flush_mark(marks, tile_first, lo, hi, (uint32_t)(i + 1));
             lo = hi;
         }
     }
-    flush_marks(marks, tile_first, seg_lo, seg_hi, val);
     ESLAM_STAMP(g_stamps_k3, 7);
 }
 
