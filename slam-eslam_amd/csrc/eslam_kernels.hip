@@ -2302,9 +2302,16 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     static_assert(PART <= 256 && NCH >= 1, "patch indices fit s_list's bytes");
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][PART];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
-    __shared__ uint8_t s_list[kLmPpb][PART];                                           // a stage's patches, in scan order
-    __shared__ uint32_t s_np[kLmPpb][2 * kLmList];                                     // pass 1: slot, new page
+    __shared__ __attribute__((aligned(16))) uint8_t s_list[kLmPpb][PART];              // a stage's patches, in scan order
+    static_assert(PART >= 2 * kLmList * 4, "pass 0's slot / new page pairs fit a particle's s_list");
+    // a small part's patch heights and deviations, read by every round (a large part's come
+    // from memory: their 4 KiB would cost the kernel a block per CU)
+    constexpr bool kSpLds = PART <= kScanPartSmall;
+    __shared__ double2 s_sp[kSpLds ? PART : 1];
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
+    // pass 0's (slot, new page) pairs of a copied table live in the particle's s_list, which
+    // the stages fill only after the copy
+    uint32_t* const s_np = reinterpret_cast<uint32_t*>(&s_list[pl][0]);
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
     const bool valid = i < mp.n;
@@ -2340,6 +2347,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
         }
         alloc = ctl->pg_cursor + mp.poff[i / kLmBlock] + mp.off[i];
     }
+    for (uint32_t k = tid; kSpLds && k < mp.m && k < PART; k += kLmMergeBlock) s_sp[k] = make_double2(mp.sp[k].z, mp.sp[k].stdev);
     if (gath && valid) {                      // the gather's copies: a field a lane
         for (uint32_t f = l; f < 10; f += kLmLanes) switch (f) {
         case 0: st.w[i] = in.w[src]; break;
@@ -2358,6 +2366,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
     bool dirty = false, moved = false, covw = false;
     uint32_t written = 0, taken = 0;
     const bool shared = (flags & kJobShared) != 0;
+    if constexpr (kSpLds) __syncthreads();    // s_sp
     if (valid && (flags & kJobPlaced)) {      // group-uniform from here on
         // ---- 1. the codes: patch k = l + kLmLanes u in lane l (round u precedes round u + 1 in
         // the scan, so the rounds apply in order and only a round's own duplicates need ranks)
@@ -2463,8 +2472,8 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 // X's row to T, four words a lane (each group instruction moves 128 contiguous
                 // bytes), with this pass's new pages; the trail's words as they are
                 if (l < kLmList) {
-                    s_np[pl][2 * l] = Lr;
-                    s_np[pl][2 * l + 1] = NP;
+                    s_np[2 * l] = Lr;
+                    s_np[2 * l + 1] = NP;
                 }
                 const uint32_t lmin = cnt ? grp_get(Lr, 0) : 1u, lmax = cnt ? grp_get(Lr, cnt - 1) : 0u;
                 const uint32_t toff = lm_trail_off(lm), nq = toff / 4u + lm_hw_word(xsl[toff - 1u]);
@@ -2476,7 +2485,7 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 #pragma unroll
                         for (uint32_t e = 0; e < 4; ++e)
                             for (uint32_t r = 0; r < cnt; ++r)
-                                if (s_np[pl][2 * r] == 4 * q + e && s_np[pl][2 * r + 1] != DM_LM_NONE) v[e] = s_np[pl][2 * r + 1];
+                                if (s_np[2 * r] == 4 * q + e && s_np[2 * r + 1] != DM_LM_NONE) v[e] = s_np[2 * r + 1];
                         w4 = make_uint4(v[0], v[1], v[2], v[3]);
                     }
                     reinterpret_cast<uint4*>(tsl)[q] = w4;
@@ -2522,6 +2531,15 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 for (uint32_t j0 = 0; j0 < nst; j0 += kLmLanes) {
                     const bool act = j0 + l < nst;
                     const uint32_t k = act ? s_list[pl][j0 + l] : 0u;
+                    // the patch first (every lane: k = 0 is a patch of the part), so a large part's
+                    // load overlaps the ranking below
+                    double2 sp;
+                    if constexpr (kSpLds) {
+                        sp = s_sp[k];
+                    } else {
+                        const ScanPatch* spk = mp.sp + k;
+                        sp = make_double2(spk->z, spk->stdev);
+                    }
                     const uint32_t c = act ? (uint32_t)s_code[pl][k] : 0xfffffffeu - l;   // idle lanes never match
                     const uint32_t rank = row_rank(c, l);
                     const uint32_t maxr = grp_max(act ? rank : 0u);
@@ -2531,11 +2549,9 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     const uint32_t ci = c & 63u;
                     // the patch, and for an empty cell the shared grid covers its occupancy word
                     // and record, are loaded together ahead of the ranks (cells are never emptied)
-                    double2 sp = make_double2(0.0, 0.0);
                     uint4 gct = make_uint4(0u, 0u, 0u, 0u);
                     uint32_t gocc = 0;
                     if (act) {
-                        sp = make_double2(mp.sp[k].z, mp.sp[k].stdev);
                         const float2 cv0 = *reinterpret_cast<const float2*>(stage + lm_stage_off(rr, ci, g));
                         if ((flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
                             const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
