@@ -2299,19 +2299,19 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
 {
     constexpr uint32_t PER = PART / kLmLanes;                       // codes a lane holds
     constexpr uint32_t NCH = PART / 8 / kLmLanes;                   // 16-byte chunks of codes a lane loads
-    static_assert(PART <= 256 && NCH >= 1, "patch indices fit s_list's bytes");
+    static_assert(PART <= 256 && NCH >= 1 && kLmStage <= 4, "a list entry holds k (8 bits), the page (2) and the cell (6)");
     __shared__ __attribute__((aligned(16))) uint16_t s_code[kLmPpb][PART];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kLmMergeBlock / 64][kLmWaveStage];
-    __shared__ __attribute__((aligned(16))) uint8_t s_list[kLmPpb][PART];              // a stage's patches, in scan order
-    static_assert(PART >= 2 * kLmList * 4, "pass 0's slot / new page pairs fit a particle's s_list");
+    static_assert(PART * 2 >= 2 * kLmList * 4, "pass 0's slot / new page pairs fit a particle's s_code");
     // a small part's patch heights and deviations, read by every round (a large part's come
     // from memory: their 4 KiB would cost the kernel a block per CU)
     constexpr bool kSpLds = PART <= kScanPartSmall;
     __shared__ double2 s_sp[kSpLds ? PART : 1];
     const uint32_t tid = threadIdx.x, l = tid & (kLmLanes - 1), pl = tid / kLmLanes, g = pl % (64 / kLmLanes), wv = tid >> 6;
-    // pass 0's (slot, new page) pairs of a copied table live in the particle's s_list, which
-    // the stages fill only after the copy
-    uint32_t* const s_np = reinterpret_cast<uint32_t*>(&s_list[pl][0]);
+    // once the codes are in registers (cpk), the particle's s_code holds pass 0's (slot, new
+    // page) pairs of a copied table and then each stage's list of patches
+    uint32_t* const s_np = reinterpret_cast<uint32_t*>(&s_code[pl][0]);
+    uint16_t* const s_lst = &s_code[pl][0];
     const uint64_t i = (uint64_t)blockIdx.x * kLmPpb + pl;
     if (ctl->err & kFaultPages) return;       // the pool could not hold the plan: nothing is written
     const bool valid = i < mp.n;
@@ -2517,20 +2517,30 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                 // the stage's patches listed in scan order (k = l + kLmLanes u is u-major), then
                 // applied kLmLanes at a time: a round's lanes on one cell go by rank (DPP row
                 // compare), rounds in order -- every cell sees its patches in scan order
+                // an entry: patch k, its staged page rr and its cell ci (k | rr << 8 | ci << 10)
                 uint32_t nst = 0;
 #pragma unroll
                 for (uint32_t u = 0; u < PER; ++u) {
+                    const uint32_t cu = code(u);
                     bool in = false;
+                    uint32_t ru = 0;
 #pragma unroll
-                    for (uint32_t w = 0; w < kLmStage; ++w) in |= code(u) != kCodeSkip && Ls[w] == (code(u) >> 6);
+                    for (uint32_t w = 0; w < kLmStage; ++w) {
+                        const bool m = cu != kCodeSkip && Ls[w] == (cu >> 6);
+                        in |= m;
+                        ru = m ? w : ru;
+                    }
                     const uint32_t gm = (uint32_t)(__ballot(in) >> gshift) & ((1u << kLmLanes) - 1u);
-                    if (in) s_list[pl][nst + __builtin_popcount(gm & ((1u << l) - 1u))] = (uint8_t)(l + kLmLanes * u);
+                    if (in)
+                        s_lst[nst + __builtin_popcount(gm & ((1u << l) - 1u))] =
+                            (uint16_t)((l + kLmLanes * u) | (ru << 8) | ((cu & 63u) << 10));
                     nst += __builtin_popcount(gm);
                 }
                 wave_sync();
                 for (uint32_t j0 = 0; j0 < nst; j0 += kLmLanes) {
                     const bool act = j0 + l < nst;
-                    const uint32_t k = act ? s_list[pl][j0 + l] : 0u;
+                    const uint32_t e = act ? (uint32_t)s_lst[j0 + l] : 0u;
+                    const uint32_t k = e & 0xffu;
                     // the patch first (every lane: k = 0 is a patch of the part), so a large part's
                     // load overlaps the ranking below
                     double2 sp;
@@ -2540,13 +2550,10 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                         const ScanPatch* spk = mp.sp + k;
                         sp = make_double2(spk->z, spk->stdev);
                     }
-                    const uint32_t c = act ? (uint32_t)s_code[pl][k] : 0xfffffffeu - l;   // idle lanes never match
+                    const uint32_t c = act ? (e >> 8) : 0xfffffffeu - l;   // page and cell; idle lanes never match
                     const uint32_t rank = row_rank(c, l);
                     const uint32_t maxr = grp_max(act ? rank : 0u);
-                    uint32_t rr = 0;
-#pragma unroll
-                    for (uint32_t w = 0; w < kLmStage; ++w) rr = Ls[w] == (c >> 6) ? w : rr;
-                    const uint32_t ci = c & 63u;
+                    const uint32_t rr = (e >> 8) & 3u, ci = e >> 10;
                     // the patch, and for an empty cell the shared grid covers its occupancy word
                     // and record, are loaded together ahead of the ranks (cells are never emptied)
                     uint4 gct = make_uint4(0u, 0u, 0u, 0u);
@@ -2554,7 +2561,10 @@ __global__ void __launch_bounds__(kLmMergeBlock) LM_MERGE_ATTR k_map_merge(DevSt
                     if (act) {
                         const float2 cv0 = *reinterpret_cast<const float2*>(stage + lm_stage_off(rr, ci, g));
                         if ((flags & kJobCovered) && !dm_lm_holds(cv0.y)) {
-                            const uint32_t sl = c >> 6, sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
+                            uint32_t sl = Ls[0];
+#pragma unroll
+                            for (uint32_t w = 1; w < kLmStage; ++w) sl = rr == w ? Ls[w] : sl;
+                            const uint32_t sb = lm_div(sl, lm.mx), sa = sl - lm.wx * sb;
                             const uint32_t cm = 8u * (uint32_t)lm_tile(sa, na, lm.hx, lm.wx, lm.mx, lm.bx) + (ci & 7u);
                             const uint32_t cn = 8u * (uint32_t)lm_tile(sb, nb, lm.hy, lm.wy, lm.my, lm.by) + (ci >> 3);
                             const uint64_t cell = (uint64_t)cn * map.width + cm;
