@@ -1748,10 +1748,12 @@ __device__ __forceinline__ void lm_centre(const MapView& map, const MergeParams&
 }
 
 // scan patch k's code for this particle: (slot << 6) | cell in the tile, or kCodeSkip (off
-// the grid, on a cell the shared grid covers, or outside the window).  Counts the covered and
-// dropped patches.
+// the grid or outside the window).  Counts the dropped patches; cell_out: the grid cell
+// (0xffffffff off the grid), whose occupancy bit the callers test eight patches at a time
+// (a cell the shared grid covers: merged into the particle's own copy of it, which the
+// merge starts from the grid's patch)
 __device__ __forceinline__ uint16_t lm_code(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
-                                            uint32_t k, uint32_t& covered, uint32_t& dropped)
+                                            uint32_t k, uint32_t& cell_out, uint32_t& dropped)
 {
     const double bx = q.x - map.offset_x, by = q.y - map.offset_y;
     {
@@ -1775,10 +1777,8 @@ __device__ __forceinline__ uint16_t lm_code(const MapView& map, const LocalMaps&
             cell = in ? cn * map.width + cm : 0xffffffffu;
         }
         uint16_t code = kCodeSkip;
+        cell_out = cell;
         if (cell != 0xffffffffu) {
-            // a cell the shared grid covers: merged into the particle's own copy of it (the merge
-            // starts it from the grid's patch)
-            if ((map.occ[cell >> 5] >> (cell & 31u)) & 1u) ++covered;
             const uint32_t a = cm >> DM_LM_TILE_BITS, b = cn >> DM_LM_TILE_BITS;
             if (dm_lm_inside(a, q.na, lm.hx, lm.wx) && dm_lm_inside(b, q.nb, lm.hy, lm.wy)) {
                 const uint32_t s = lm_mod(a, lm.wx, lm.mx) + lm.wx * lm_mod(b, lm.wy, lm.my);
@@ -1791,11 +1791,31 @@ __device__ __forceinline__ uint16_t lm_code(const MapView& map, const LocalMaps&
     }
 }
 
+// how many of eight cells the shared grid covers: the eight occupancy words in one round trip
+__device__ __forceinline__ uint32_t lm_covered8(const MapView& map, const uint32_t (&cell)[8])
+{
+    uint32_t w[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) w[j] = cell[j] != 0xffffffffu ? map.occ[cell[j] >> 5] : 0u;
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) n += (w[j] >> (cell[j] & 31u)) & 1u;
+    return n;
+}
+
 // every scan patch's code into LDS (patch-major, thread-minor: a part of kScanPartSmall)
 __device__ __forceinline__ void lm_codes(const MapView& map, const LocalMaps& lm, const MergeParams& mp, const LmPart& q,
                                          uint16_t* codes, uint32_t& covered, uint32_t& dropped)
 {
-    for (uint32_t k = 0; k < mp.m; ++k) codes[k * kLmBlock] = lm_code(map, lm, mp, q, k, covered, dropped);
+    for (uint32_t k0 = 0; k0 < mp.m; k0 += 8) {
+        uint32_t cell[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            cell[j] = 0xffffffffu;
+            if (k0 + j < mp.m) codes[(k0 + j) * kLmBlock] = lm_code(map, lm, mp, q, k0 + j, cell[j], dropped);
+        }
+        covered += lm_covered8(map, cell);
+    }
 }
 
 // slot s into the sorted list of the kLmList smallest distinct slots; more: a slot fell off
@@ -1820,15 +1840,17 @@ __device__ __forceinline__ void lm_codes_row(const MapView& map, const LocalMaps
     for (uint32_t r = 0; r < kLmList; ++r) L[r] = kLmNoList;
     more = false;
     for (uint32_t k0 = 0; k0 < mp.m; k0 += 8) {
-        uint32_t w[4];
+        uint32_t w[4], cell[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) {
             const uint32_t k = k0 + j;
-            const uint32_t c = k < mp.m ? (uint32_t)lm_code(map, lm, mp, q, k, covered, dropped) : (uint32_t)kCodeSkip;
+            cell[j] = 0xffffffffu;
+            const uint32_t c = k < mp.m ? (uint32_t)lm_code(map, lm, mp, q, k, cell[j], dropped) : (uint32_t)kCodeSkip;
             if (c != kCodeSkip) lm_insert(L, c >> 6, more);
             w[j >> 1] = (j & 1) ? (w[j >> 1] | (c << 16)) : c;
         }
         row[k0 >> 3] = make_uint4(w[0], w[1], w[2], w[3]);
+        covered += lm_covered8(map, cell);
     }
 }
 
