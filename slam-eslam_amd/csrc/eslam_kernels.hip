@@ -360,6 +360,61 @@ __device__ __forceinline__ bool store_patch(uint32_t sid, uint32_t m, uint32_t n
     return patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf), sd, lz, qv, mean, stdev);
 }
 
+// store_patch for up to N feet of one particle at once (the cells get_patch<DELTA, true>
+// deferred: dm[i] = ~0 for the others): the table's centre and every foot's slot in one round
+// trip, then every page cell in one; the same results as store_patch foot by foot.  A tile
+// outside the window (rare) takes store_patch itself.
+constexpr uint32_t kStoreTrail = 0xfffffffeu;      // store_patches: a tile outside the window
+template <int N>
+__device__ __forceinline__ void store_patches(uint32_t sid, const uint32_t (&dm)[N], const uint32_t (&dn)[N],
+                                              const double (&lz)[N], double qv, bool (&fnd)[N], double (&mean)[N],
+                                              double (&stdev)[N])
+{
+    const su16 h = kl16(KOFF(store));
+    const uint64_t w3 = kq(h, 3), w4 = kq(h, 4), w5 = kq(h, 5);
+    const uint32_t S = (uint32_t)w3, wx = (uint32_t)(w3 >> 32), wy = (uint32_t)w4, hx = (uint32_t)(w4 >> 32);
+    const uint32_t hy = (uint32_t)w5;
+    const gmem<const uint32_t>* row = kp<const uint32_t>(h, 1) + (uint64_t)sid * S;
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) any |= dm[i] != 0xffffffffu;
+    if (!any) return;
+    const uint64_t c = kp<const uint64_t>(h, 0)[sid];   // int2 {x, y}
+    uint32_t pg[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        pg[i] = DM_LM_NONE;
+        if (dm[i] == 0xffffffffu) continue;
+        const uint32_t a = dm[i] >> DM_LM_TILE_BITS, b = dn[i] >> DM_LM_TILE_BITS;
+        const uint32_t qa = (uint32_t)(((uint64_t)a * kq(h, 6)) >> kLmMagicShift);
+        const uint32_t qb = (uint32_t)(((uint64_t)b * kq(h, 7)) >> kLmMagicShift);
+        pg[i] = row[(a - wx * qa) + wx * (b - wy * qb)];
+    }
+    uint64_t pf[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        pf[i] = 0;
+        if (dm[i] == 0xffffffffu) continue;
+        const uint32_t a = dm[i] >> DM_LM_TILE_BITS, b = dn[i] >> DM_LM_TILE_BITS;
+        if (!dm_lm_inside(a, (int32_t)(uint32_t)c, hx, wx) || !dm_lm_inside(b, (int32_t)(uint32_t)(c >> 32), hy, wy)) {
+            pg[i] = kStoreTrail;                         // the trail: store_patch below
+        } else if (pg[i] != DM_LM_NONE) {
+            pf[i] = reinterpret_cast<const gmem<const uint64_t>*>(kp<const float2>(h, 2))
+                [(uint64_t)pg[i] * DM_LM_PAGE_CELLS + (dm[i] & 7u) + 8u * (dn[i] & 7u)];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if (dm[i] == 0xffffffffu) continue;
+        if (pg[i] == kStoreTrail) {
+            fnd[i] = store_patch(sid, dm[i], dn[i], lz[i], qv, mean[i], stdev[i]);
+        } else if (pg[i] != DM_LM_NONE) {
+            const float sd = __uint_as_float((uint32_t)(pf[i] >> 32));
+            fnd[i] = dm_lm_holds(sd) && patch_gate(nullptr, 0, __uint_as_float((uint32_t)pf[i]), sd, lz[i], qv, mean[i], stdev[i]);
+        }
+    }
+}
+
 // a particle's table name for get_patch<DELTA>, with bit 31 set when its map holds copies of
 // shared-grid cells (kLmShadow in its row): its lookups then ask its own cells first
 __device__ __forceinline__ uint32_t store_sid(uint32_t sid)
@@ -374,10 +429,15 @@ __device__ __forceinline__ uint32_t store_sid(uint32_t sid)
 // the map is K1Args::map, read by scalar loads (header: 64 bytes per lookup).  DELTA: the
 // particle's own map answers for cells the shared grid leaves empty, and first for every cell
 // when it holds copies of shared-grid cells (sid bit 31, store_sid).
-template <bool DELTA = false>
+// DEFER (DELTA, a particle without copies of grid cells): a lookup that needs the particle's
+// own map does not make it but returns false with *dm, *dn = its cell (else *dm = ~0), so the
+// caller makes the lookups of all its feet together (store_patches)
+template <bool DELTA = false, bool DEFER = false>
 __device__ __forceinline__ bool get_patch(const Window& win, double px, double py, double pz, double qv, double& mean,
-                                          double& stdev, uint32_t sid = 0)
+                                          double& stdev, uint32_t sid = 0, uint32_t* dm = nullptr, uint32_t* dn = nullptr,
+                                          double* dlz = nullptr)
 {
+    if constexpr (DEFER) *dm = 0xffffffffu;
     const su16 h = kl16(KOFF(map));
     const uint32_t width = h[12], hcells = h[13], ident = h[14], has_height = h[15];
     double lx = px, ly = py, lz = pz;    // an identity global2local is applied as the identity
@@ -425,7 +485,15 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
     const bool in_grid = (fm >= 0.0) & (fm < (double)width) & (fn >= 0.0) & (fn < (double)hcells);
     if constexpr (DELTA) {
         if (!in_grid || (in_win && wc.count == 1)) return false;
-        if (in_win && wc.count == 0) return store_patch(sid, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
+        if (in_win && wc.count == 0) {
+            if constexpr (DEFER) {
+                *dm = (uint32_t)im;
+                *dn = (uint32_t)in;
+                *dlz = lz;
+                return false;
+            }
+            return store_patch(sid, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
+        }
     } else {
         if (!in_grid || (in_win && wc.count <= 1)) return false;
     }
@@ -444,7 +512,15 @@ __device__ __forceinline__ bool get_patch(const Window& win, double px, double p
         b = ct.z;
         e = ct.z + ct.w;
         if constexpr (DELTA) {
-            if (b == e) return store_patch(sid, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
+            if (b == e) {
+                if constexpr (DEFER) {
+                    *dm = (uint32_t)im;
+                    *dn = (uint32_t)in;
+                    *dlz = lz;
+                    return false;
+                }
+                return store_patch(sid, (uint32_t)im, (uint32_t)in, lz, qv, mean, stdev);
+            }
         }
         if (!has_height && b < e) {
             if (patch_gate(nullptr, 0, __uint_as_float(ct.x), __uint_as_float(ct.y), lz, qv, mean, stdev)) return true;
@@ -730,13 +806,42 @@ __device__ __forceinline__ CMResult evaluate_pose(const Window& win, double co, 
         // overlap (a lookup the group logic then skips is harmless: pure function)
         bool fnd[MAXP];
         double mn[MAXP], sd[MAXP], wzs[MAXP];
+        if constexpr (DELTA) {
+            if (!(sid >> 31)) {
+                // the feet the shared grid leaves to the particle's map: their lookups together
+                uint32_t dm[MAXP], dn[MAXP];
+                double dlz[MAXP];
 #pragma unroll
-        for (int i = 0; i < MAXP; ++i) {
-            fnd[i] = false; mn[i] = 0.0; sd[i] = 0.0; wzs[i] = 0.0;
-            if ((uint32_t)i < m) {
-                double wx, wy;
-                world((uint32_t)i, wx, wy, wzs[i]);
-                if ((eval_mask >> i) & 1u) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
+                for (int i = 0; i < MAXP; ++i) {
+                    fnd[i] = false; mn[i] = 0.0; sd[i] = 0.0; wzs[i] = 0.0; dm[i] = 0xffffffffu; dn[i] = 0u; dlz[i] = 0.0;
+                    if ((uint32_t)i < m) {
+                        double wx, wy;
+                        world((uint32_t)i, wx, wy, wzs[i]);
+                        if ((eval_mask >> i) & 1u)
+                            fnd[i] = get_patch<true, true>(win, wx, wy, wzs[i], qv, mn[i], sd[i], sid, &dm[i], &dn[i], &dlz[i]);
+                    }
+                }
+                store_patches<MAXP>(sid, dm, dn, dlz, qv, fnd, mn, sd);
+            } else {
+#pragma unroll
+                for (int i = 0; i < MAXP; ++i) {
+                    fnd[i] = false; mn[i] = 0.0; sd[i] = 0.0; wzs[i] = 0.0;
+                    if ((uint32_t)i < m) {
+                        double wx, wy;
+                        world((uint32_t)i, wx, wy, wzs[i]);
+                        if ((eval_mask >> i) & 1u) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < MAXP; ++i) {
+                fnd[i] = false; mn[i] = 0.0; sd[i] = 0.0; wzs[i] = 0.0;
+                if ((uint32_t)i < m) {
+                    double wx, wy;
+                    world((uint32_t)i, wx, wy, wzs[i]);
+                    if ((eval_mask >> i) & 1u) fnd[i] = lookup(wx, wy, wzs[i], mn[i], sd[i]);
+                }
             }
         }
         if constexpr (UNG) {
@@ -853,8 +958,11 @@ __device__ __forceinline__ uint32_t decode_source(uint32_t v, uint32_t multi, co
 // stores and agent-coherent sc1 stores measured beside them).  Same values, same bits.
 #define K1_ST(p, v) __builtin_nontemporal_store((v), (p))
 
+#ifndef ESLAM_K1D_WPE
+#define ESLAM_K1D_WPE 3                  // K1 DELTA: three waves a SIMD hold the batched own-map lookups unspilled
+#endif
 template <bool PROJECT, bool WEIGHT, int MAXP, bool BATCH, bool DELTA = false, bool UNG = false>
-__global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR __attribute__((amdgpu_waves_per_eu(DELTA ? 4 : 1))) k_project_weight(K1Args a)
+__global__ void __launch_bounds__(kBlock) ESLAM_K1_ATTR __attribute__((amdgpu_waves_per_eu(DELTA ? ESLAM_K1D_WPE : 1))) k_project_weight(K1Args a)
 {
     // Inside the particle loop every argument is read by a scalar load where it is used
     // (KOFF offsets into the K1Args kernel argument); "a." appears only outside the loop.
