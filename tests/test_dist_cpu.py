@@ -101,3 +101,15 @@ def test_shard_bounds_chunk_aligned():
             csz = 64 * A.chunk_rows(n)
             assert g[0] == 0 and g[-1] == n and all(g[r] % csz == 0 for r in range(w))
             assert all(g[r + 1] > g[r] for r in range(w))
+
+
+def test_shard_bounds_with_a_fixed_chunk():
+    """eslam_config.sum_chunk_rows (ABI 8): an explicit chunk overrides dm_chunk_rows, and the
+    shard starts follow it (configs[3]: 16M over 8 ranks in a rank's 7-row chunks)."""
+    import eslam_abi as A
+    assert A.chunk_rows(16 * 1024 * 1024) == 13 and A.chunk_rows(16 * 1024 * 1024, 7) == 7
+    assert A.chunk_rows(2 * 1024 * 1024) == 7
+    g = A.shard_bounds(16 * 1024 * 1024, 8, 7)
+    assert g[0] == 0 and g[-1] == 16 * 1024 * 1024
+    assert all(b % (64 * 7) == 0 for b in g[:-1]) and all(g[r + 1] > g[r] for r in range(8))
+    assert A.shard_bounds(3000, 2, 3) != A.shard_bounds(3000, 2) or A.chunk_rows(3000) == 3
